@@ -1,0 +1,356 @@
+#!/usr/bin/env python3
+"""Benchmark: GiB/s payload obfuscated, device-resident, 1M x 1350 B Salamander.
+
+One process per GPU (torchrun for N > 1).  Each rank owns an independent
+shard of 1,048,576 packets x 1350 B (BASELINE.json configs[1]) already
+resident in HBM; a step is one launch of the fused Salamander-obfuscate
+kernel over the shard (key derivation for every packet + XOR stream + salt
+prefix + out_len).  Packets are independent, so there is no data-path
+collective: per-GPU work is fixed as N grows ("weak").  The timed region is
+bracketed by a barrier + device sync on both sides, and the max over ranks is
+taken.
+
+Rank 0 prints ONE JSON line (bench contract) with two extra objects:
+  roofline      the dominant kernel's achieved algorithmic HBM bandwidth
+                (2L + 2S bytes per packet / avg kernel duration from HIP
+                events on the launch stream) vs 8 TB/s; `traffic` = HBM bytes
+                per launch from the rocprofv3 PMC pass committed under
+                profiles/ (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction), or
+                null when absent.
+  cpu_baseline  the CPU restatement (oracle/, "port": the Go reference cannot
+                be built here) on BASELINE configs[0]: 65,536 x 1200 B
+                Salamander obfuscate + deobfuscate round trips on the host
+                cores, rank 0 at N = 1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "sing-quic_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+METRIC = "GiB/s payload obfuscated, device-resident, 1M×1350B Salamander @1/2/4/8 GPU"
+PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+PSK = b"sing-quic-mi355x-bench-psk"  # SURVEY.md 8(d) default PSK (26 B)
+
+CONFIGS = {
+    # name: (kind, packets per rank, payload len (None = ragged), n_psk)
+    "salamander-1m": (0, 1 << 20, 1350, 1),         # configs[1]  (the metric)
+    "xplus-1m": (1, 1 << 20, 1200, 1),              # configs[2]
+    "salamander-ragged-4m": (0, 1 << 22, None, 1),  # configs[3]
+    "salamander-16m-256psk": (0, 1 << 24, 1350, 256),  # configs[4], sharded over ranks
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="salamander-1m", choices=sorted(CONFIGS))
+    ap.add_argument("--direction", default="obfuscate", choices=["obfuscate", "deobfuscate"])
+    ap.add_argument("--cpu-seconds", type=float, default=2.0,
+                    help="wall seconds of CPU-baseline sampling (x threads = CPU work)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e", action="store_true",
+                    help="also time the host-staged path (pinned H2D + kernel + D2H)")
+    return ap.parse_args()
+
+
+def slot(n: int, a: int = 16) -> int:
+    return (n + a - 1) // a * a
+
+
+def build_shard(torch, dev, kind, n, L, n_psk, rank, world, config):
+    """Synthetic shard in HBM: payload/salt bytes from torch's Philox RNG
+    seeded per rank; 16-byte-aligned slots for inputs and outputs."""
+    import numpy as np
+    S = 8 if kind == 0 else 16
+    g = torch.Generator(device=dev)
+    g.manual_seed(1 + 1000 * rank)
+    if L is None:  # configs[3]: U[64, 1452], seed 4
+        lens = torch.randint(64, 1453, (n,), generator=g, device=dev, dtype=torch.int64)
+    else:
+        lens = torch.full((n,), L, device=dev, dtype=torch.int64)
+    in_slot = (lens + 15) // 16 * 16
+    in_off = torch.cumsum(in_slot, 0) - in_slot
+    out_slot = (lens + S + 15) // 16 * 16
+    out_off = torch.cumsum(out_slot, 0) - out_slot
+    in_bytes = int(in_slot.sum().item())
+    out_bytes = int(out_slot.sum().item())
+    data = torch.randint(0, 256, (in_bytes,), generator=g, device=dev, dtype=torch.uint8)
+    salt = torch.randint(0, 256, (n * S,), generator=g, device=dev, dtype=torch.uint8)
+    out = torch.zeros(out_bytes, device=dev, dtype=torch.uint8)
+    # packet index shard: global ids rank*n .. for psk_id = i mod 256
+    psk_id = None
+    if n_psk > 1:
+        gid = torch.arange(rank * n, (rank + 1) * n, device=dev, dtype=torch.int64)
+        psk_id = (gid % n_psk).to(torch.int16)
+    rng = np.random.Generator(np.random.PCG64(3))
+    psks = [PSK] if n_psk == 1 else [
+        rng.integers(0, 256, int(k), dtype=np.uint8).tobytes() for k in rng.integers(8, 65, n_psk)]
+    return dict(lens=lens.to(torch.int32), in_off=in_off, out_off=out_off, data=data, salt=salt,
+                out=out, out_len=torch.zeros(n, device=dev, dtype=torch.int32), psk_id=psk_id,
+                psks=psks, S=S, payload_bytes=int(lens.sum().item()))
+
+
+def spot_check(torch, sh, kind, n, direction_out):
+    """Parity spot check vs the oracle on sampled packets (outside timing)."""
+    import numpy as np
+    import oracle_lib as ol
+    idx = sorted(set([0, n - 1] + list(range(0, n, 4099))))[:400]
+    S = sh["S"]
+    lens = sh["lens"].cpu().numpy()
+    in_off = sh["in_off"].cpu().numpy()
+    out_off = sh["out_off"].cpu().numpy()
+    data, salt, out = sh["data"], sh["salt"], direction_out
+    ids = sh["psk_id"].cpu().numpy() if sh["psk_id"] is not None else None
+    write = ol.salamander_write if kind == 0 else ol.xplus_write
+    for i in idx:
+        L = int(lens[i])
+        p = data[int(in_off[i]):int(in_off[i]) + L].cpu().numpy().tobytes()
+        s = salt[i * S:(i + 1) * S].cpu().numpy().tobytes()
+        psk = sh["psks"][int(ids[i]) if ids is not None else 0]
+        w, _ = write(psk, s, p)
+        got = out[int(out_off[i]):int(out_off[i]) + L + S].cpu().numpy().tobytes()
+        if got != w:
+            return False
+    return bool((sh["out_len"].cpu().numpy() == lens + S).all())
+
+
+def cpu_baseline(seconds: float):
+    """Oracle (CPU restatement, byte-at-a-time like salamander.go:51-53,62-64)
+    on configs[0]: 65,536 x 1200 B obfuscate -> deobfuscate round trips."""
+    import numpy as np
+    import sqobfs
+    import oracle_lib as ol
+    n, L, S = 65536, 1200, 8
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    rng = np.random.Generator(np.random.PCG64(1))
+    data = rng.integers(0, 256, n * L, dtype=np.uint8)
+    salt = np.random.Generator(np.random.PCG64(2)).integers(0, 256, n * S, dtype=np.uint8)
+    in_off = (np.arange(n, dtype=np.uint64) * L)
+    lens = np.full(n, L, np.uint32)
+    wire = np.zeros(n * (L + S), np.uint8)
+    w_off = np.arange(n, dtype=np.uint64) * (L + S)
+    w_len = np.zeros(n, np.uint32)
+    back = np.zeros(n * L, np.uint8)
+    b_len = np.zeros(n, np.uint32)
+    obf = sqobfs.HostBatch(data, in_off, lens, wire, w_off, w_len, salt)
+    deo = sqobfs.HostBatch(wire, w_off, np.full(n, L + S, np.uint32), back, in_off, b_len)
+    t_ob = t_de = 0.0
+    passes = 0
+    t_end = time.perf_counter() + seconds
+    while passes < 2 or time.perf_counter() < t_end:
+        t0 = time.perf_counter()
+        ol.batch_run(0, 0, [PSK], obf, nthreads=threads)
+        t1 = time.perf_counter()
+        ol.batch_run(0, 1, [PSK], deo, nthreads=threads)
+        t2 = time.perf_counter()
+        t_ob += t1 - t0
+        t_de += t2 - t1
+        passes += 1
+    ok = bool(np.array_equal(back, data))
+    gib = n * L * passes / 2**30
+    return {"value": gib / t_ob, "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"configs[0]: {passes} x (65,536 x 1200 B Salamander obfuscate + "
+                      f"deobfuscate), one PSK, C restatement (oracle/oracle.c, byte loops as "
+                      f"salamander.go:51-53,62-64) on {threads} threads; value = obfuscate "
+                      f"direction; deobfuscate {gib / t_de:.3f} GiB/s, round trip "
+                      f"{gib / (t_ob + t_de):.3f} GiB/s; round-trip identity {ok}; "
+                      f"Go reference unbuildable (no Go toolchain)",
+            "cpu_seconds": round((t_ob + t_de) * threads, 2)}
+
+
+def load_traffic(config: str, kernel_bytes: float):
+    """HBM bytes per launch from the committed PMC pass (profiles/)."""
+    path = os.path.join(REPO, "profiles", f"pmc_{config}.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch"), d
+
+
+def main():
+    args = parse()
+    import torch
+    import sqobfs
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    assert torch.cuda.is_available(), "bench.py needs a GPU"
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    kind, n_total, L, n_psk = CONFIGS[args.config]
+    # configs[4] is one 16M batch sharded over the ranks; the rest are per-GPU
+    n = n_total // world if args.config == "salamander-16m-256psk" else n_total
+    direction = sqobfs.OBFUSCATE if args.direction == "obfuscate" else sqobfs.DEOBFUSCATE
+    sh = build_shard(torch, dev, kind, n, L, n_psk, rank, world, args.config)
+    S = sh["S"]
+    ctx = sqobfs.Context(local)
+    kr = sqobfs.Keyring(ctx, kind, sh["psks"])
+    stream = torch.cuda.current_stream(dev)
+    s = stream.cuda_stream
+
+    if direction == sqobfs.OBFUSCATE:
+        b = sqobfs.make_batch(n, sh["data"], sh["in_off"], sh["lens"], sh["out"], sh["out_off"],
+                              sh["out_len"], sh["salt"], sh["psk_id"])
+        alg_bytes = 2 * sh["payload_bytes"] + 2 * S * n
+    else:
+        # decode the obfuscated shard (made once, untimed)
+        b0 = sqobfs.make_batch(n, sh["data"], sh["in_off"], sh["lens"], sh["out"],
+                               sh["out_off"], sh["out_len"], sh["salt"], sh["psk_id"])
+        sqobfs.launch(ctx, kr, sqobfs.OBFUSCATE, b0, s)
+        wire_len = (sh["lens"] + S).to(torch.int32)
+        back = torch.zeros_like(sh["data"])
+        b = sqobfs.make_batch(n, sh["out"], sh["out_off"], wire_len, back, sh["in_off"],
+                              sh["out_len"], None, sh["psk_id"])
+        alg_bytes = 2 * sh["payload_bytes"] + S * n
+
+    for _ in range(args.warmup):
+        sqobfs.launch(ctx, kr, direction, b, s)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for e0, e1 in ev:
+        e0.record(stream)
+        sqobfs.launch(ctx, kr, direction, b, s)
+        e1.record(stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kern_ms = sorted(e0.elapsed_time(e1) for e0, e1 in ev)
+    kern_avg_ms = sum(kern_ms) / len(kern_ms)
+
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        kt = torch.tensor([kern_avg_ms], device=dev, dtype=torch.float64)
+        dist.all_reduce(kt, op=dist.ReduceOp.MAX)
+        kern_avg_ms = float(kt.item())
+
+    parity = None
+    if direction == sqobfs.OBFUSCATE:
+        parity = spot_check(torch, sh, kind, n, sh["out"])
+    else:
+        lens = sh["lens"].cpu().numpy()
+        offs = sh["in_off"].cpu().numpy()
+        parity = all(torch.equal(back[int(offs[i]):int(offs[i]) + int(lens[i])],
+                                 sh["data"][int(offs[i]):int(offs[i]) + int(lens[i])])
+                     for i in sorted(set([0, n - 1] + list(range(0, n, 4099)))))
+    if dist:
+        pt = torch.tensor([1 if parity else 0], device=dev)
+        dist.all_reduce(pt, op=dist.ReduceOp.MIN)
+        parity = bool(pt.item())
+
+    total_payload = sh["payload_bytes"] * world * args.steps
+    value = total_payload / elapsed / 2**30
+    achieved = alg_bytes / (kern_avg_ms * 1e-3) / 1e9
+    traffic, pmc = load_traffic(args.config, alg_bytes)
+    out = {
+        "metric": METRIC if args.config == "salamander-1m" and direction == 0 else
+        f"GiB/s payload {'obfuscated' if direction == 0 else 'deobfuscated'}, device-resident, {args.config}",
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak" if args.config != "salamander-16m-256psk" else "strong",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (torch Philox random payloads/salts, seeded per rank)",
+        "config": {
+            "workload": {"salamander-1m": "configs[1]: Salamander obfuscate, 1,048,576 x 1350 B "
+                                          "per GPU, one 26-byte PSK",
+                         "xplus-1m": "configs[2]: XPlus, 1,048,576 x 1200 B per GPU, one PSK",
+                         "salamander-ragged-4m": "configs[3]: Salamander, 4,194,304 packets "
+                                                 "U[64,1452] per GPU, one PSK",
+                         "salamander-16m-256psk": "configs[4]: Salamander, 16,777,216 x 1350 B, "
+                                                  "256 PSKs round-robin, sharded over ranks"}[args.config],
+            "direction": args.direction,
+            "packets_per_gpu": n,
+            "payload_bytes_per_gpu": sh["payload_bytes"],
+            "layout": "inputs and outputs in 16-byte-aligned slots, offsets/lengths SoA in HBM",
+            "parallelism": f"shard{world} (independent packets, no collective)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": PEAK_HBM_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / PEAK_HBM_GBS, 4),
+            "traffic": traffic,
+            "kernel": f"obfs_kernel<{kind},{direction},{int(n_psk > 1)},4>",
+            "kernel_avg_us": round(kern_avg_ms * 1e3, 2),
+            "kernel_min_us": round(kern_ms[0] * 1e3, 2),
+            "algorithmic_bytes_per_launch": alg_bytes,
+            "bytes_rule": "obfuscate 2L+2S per packet, deobfuscate 2L+S (SURVEY.md 8(d))",
+        },
+        "parity_spot_check": parity,
+    }
+    if pmc:
+        out["roofline"]["traffic_source"] = pmc.get("source")
+    if args.e2e and rank == 0:
+        out["e2e"] = e2e_rate(torch, sqobfs, ctx, kr, kind, min(n, 1 << 18), L or 758)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    kr.close()
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+def e2e_rate(torch, sqobfs, ctx, kr, kind, n, L):
+    """Host-resident batch (pinned numpy) through sqobfs_run_host: memcpy into
+    pinned staging + H2D + kernel + D2H + memcpy out (DESIGN.md e2e rate)."""
+    import numpy as np
+    S = 8 if kind == 0 else 16
+    rng = np.random.Generator(np.random.PCG64(9))
+    data = rng.integers(0, 256, n * slot(L), dtype=np.uint8)
+    in_off = np.arange(n, dtype=np.uint64) * slot(L)
+    out = np.zeros(n * slot(L + S), np.uint8)
+    out_off = np.arange(n, dtype=np.uint64) * slot(L + S)
+    hb = sqobfs.HostBatch(data, in_off, np.full(n, L, np.uint32), out, out_off,
+                          np.zeros(n, np.uint32),
+                          rng.integers(0, 256, n * S, dtype=np.uint8))
+    sqobfs.run_host(ctx, kr, sqobfs.OBFUSCATE, hb.as_batch())
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        sqobfs.run_host(ctx, kr, sqobfs.OBFUSCATE, hb.as_batch())
+    dt = (time.perf_counter() - t0) / reps
+    return {"packets": n, "payload_bytes": L, "GiB_s_payload": round(n * L / dt / 2**30, 3),
+            "ms_per_batch": round(dt * 1e3, 3),
+            "path": "sqobfs_run_host: host memcpy -> pinned -> H2D -> kernel -> D2H -> memcpy"}
+
+
+if __name__ == "__main__":
+    main()

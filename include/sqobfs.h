@@ -1,0 +1,161 @@
+/*
+ * sqobfs.h -- C ABI of the MI355X-native Salamander / XPlus obfuscation path.
+ *
+ * Drop-in boundary for sing-quic's per-datagram obfuscation layer
+ * (reference: /root/reference, Go module github.com/sagernet/sing-quic).
+ * The reference exposes the layer only as net.PacketConn decorators; every
+ * entry point below replaces the per-packet body of one of those methods with
+ * a batched launch over a ragged batch of datagrams:
+ *
+ *   sqobfs_keyring_create        <- the `password []byte` / `key []byte` field
+ *                                   captured by NewSalamanderConn
+ *                                   (hysteria2/salamander.go:19-40) and
+ *                                   NewXPlusPacketConn (hysteria/xplus.go:19-44)
+ *   sqobfs_salamander_obfuscate  <- SalamanderPacketConn.WriteTo body
+ *                                   (hysteria2/salamander.go:57-70) and
+ *                                   VectorisedSalamanderPacketConn.WriteTo
+ *                                   (salamander.go:81-93)
+ *   sqobfs_salamander_deobfuscate<- SalamanderPacketConn.ReadFrom body
+ *                                   (hysteria2/salamander.go:42-55)
+ *   sqobfs_xplus_obfuscate       <- XPlusPacketConn.WriteTo body
+ *                                   (hysteria/xplus.go:62-75) and
+ *                                   VectorisedXPlusConn.WriteTo (xplus.go:86-98)
+ *   sqobfs_xplus_deobfuscate     <- XPlusPacketConn.ReadFrom body
+ *                                   (hysteria/xplus.go:46-60)
+ *   sqobfs_run_host              <- the same four, for batches that live in
+ *                                   host memory (socket buffers): stages
+ *                                   through pinned memory, H2D, launch, D2H.
+ *
+ * Plain C types only (no HIP/torch types): a cgo / ctypes / JNI binding needs
+ * nothing but this header (INTEGRATION.md shows the cgo stub).
+ *
+ * Semantics per packet i (S = 8 Salamander, 16 XPlus; key = BLAKE2b-256 or
+ * SHA-256 of psk || salt):
+ *   obfuscate:   out[out_off[i] .. +S)       = salt[i*S .. +S)
+ *                out[out_off[i]+S+j]         = in[in_off[i]+j] ^ key[j % 32],
+ *                                              j < in_len[i]
+ *                out_len[i] = S + in_len[i]
+ *   deobfuscate: n = in_len[i], wire = in[in_off[i] ..)
+ *     Salamander n <= 8: the n raw bytes are copied to out (the reference
+ *                returns n and leaves p untouched, salamander.go:47-49),
+ *                out_len[i] = n.
+ *     XPlus n < 16: nothing written, out_len[i] = 0 (xplus.go:50-52).
+ *     otherwise out[out_off[i]+j] = wire[S+j] ^ key[j % 32] for
+ *                j < m - S, where m = n for Salamander and
+ *                m = in_cap ? in_cap[i] : n for XPlus (xplus.go:55 XORs up
+ *                to len(p), the read buffer's length, not n);
+ *                out_len[i] = n - S.
+ * Memory rules: each packet's output bytes must not overlap any other
+ * packet's output, and must either not overlap its own input or be exactly
+ * in place (the payload's output address == its input address, e.g. a
+ * headroom layout with out_off = in_off - S for obfuscate).  Offsets and
+ * lengths are arbitrary (no alignment required); 16-byte-aligned outputs are
+ * the fast case.  `salt` must be 4-byte aligned.
+ */
+#ifndef SQOBFS_H
+#define SQOBFS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SQOBFS_ABI_VERSION 1
+
+#define SQOBFS_SALAMANDER_SALT_LEN 8 /* hysteria2/salamander.go:15 */
+#define SQOBFS_XPLUS_SALT_LEN 16     /* hysteria/xplus.go:17 */
+#define SQOBFS_OBFS_TYPE_SALAMANDER "salamander" /* salamander.go:17 */
+
+/* status codes (0 = OK, negative = error) */
+#define SQ_OK 0
+#define SQ_EINVAL (-1)   /* bad argument (NULL pointer, kind mismatch ...) */
+#define SQ_ENOMEM (-2)   /* host or device allocation failed */
+#define SQ_EDEVICE (-3)  /* HIP runtime / kernel launch error */
+#define SQ_ENODEV (-4)   /* no such GPU */
+#define SQ_EPSK (-5)     /* a psk_id was out of range (host-staged path) */
+
+/* out_len value written for a packet whose psk_id is out of range */
+#define SQOBFS_BAD_PSK 0xFFFFFFFFu
+
+enum sqobfs_kind { SQOBFS_SALAMANDER = 0, SQOBFS_XPLUS = 1 };
+enum sqobfs_dir { SQOBFS_OBFUSCATE = 0, SQOBFS_DEOBFUSCATE = 1 };
+
+typedef struct sqobfs_ctx sqobfs_ctx;
+typedef struct sqobfs_keyring sqobfs_keyring;
+
+/* A ragged batch of datagrams.  Structure-of-arrays, one entry per packet.
+ * For the device entry points every pointer is a device pointer on the
+ * context's GPU; for sqobfs_run_host every pointer is a host pointer. */
+typedef struct sqobfs_batch {
+  uint32_t n;               /* number of packets */
+  uint32_t flags;           /* reserved, must be 0 */
+  const uint8_t *in;        /* input base */
+  const uint64_t *in_off;   /* [n] byte offset of packet i in `in` */
+  const uint32_t *in_len;   /* [n] payload length (obfs) / datagram length n (deobfs) */
+  uint8_t *out;             /* output base */
+  const uint64_t *out_off;  /* [n] byte offset of packet i's output in `out` */
+  uint32_t *out_len;        /* [n] written: output length per the rules above */
+  const uint8_t *salt;      /* obfuscate: [n*S] salts (4-byte aligned); deobfs: unused */
+  const uint16_t *psk_id;   /* [n] keyring index per packet, NULL = all use 0 */
+  const uint32_t *in_cap;   /* XPlus deobfuscate only: [n] read-buffer length
+                               len(p) >= in_len (xplus.go:55); NULL = in_len */
+} sqobfs_batch;
+
+int sqobfs_abi_version(void);
+const char *sqobfs_strerror(int status);
+int sqobfs_device_count(int *count);
+
+/* One context per GPU.  Thread-safe: device launches only read immutable
+ * state; sqobfs_run_host serialises on an internal lock. */
+int sqobfs_open(int device, sqobfs_ctx **out);
+void sqobfs_close(sqobfs_ctx *ctx);
+/* the context's own non-blocking HIP stream (as void*), for callers that
+ * want a private stream; sqobfs_run_host uses it internally */
+void *sqobfs_stream(sqobfs_ctx *ctx);
+/* wait for all work on `stream` (NULL = the HIP null stream) */
+int sqobfs_sync(sqobfs_ctx *ctx, void *stream);
+
+/* Upload `count` pre-shared keys (host memory: psk k = blob[off[k] .. +len[k]])
+ * and derive each one's per-PSK hash state on the GPU.  kind selects the
+ * hash (BLAKE2b for Salamander, SHA-256 for XPlus).  Any PSK length works,
+ * including 0.  Synchronous. */
+int sqobfs_keyring_create(sqobfs_ctx *ctx, int kind, uint32_t count,
+                          const uint8_t *blob, const uint64_t *off,
+                          const uint32_t *len, sqobfs_keyring **out);
+void sqobfs_keyring_destroy(sqobfs_keyring *kr);
+int sqobfs_keyring_kind(const sqobfs_keyring *kr);
+uint32_t sqobfs_keyring_count(const sqobfs_keyring *kr);
+
+/* Device-resident batch launches: asynchronous on `stream` (a hipStream_t
+ * passed as void*; NULL = the HIP null stream, as in HIP itself).  All batch
+ * pointers are device pointers; the keyring's kind must match the entry
+ * point. */
+int sqobfs_salamander_obfuscate(sqobfs_ctx *ctx, const sqobfs_keyring *kr,
+                                const sqobfs_batch *b, void *stream);
+int sqobfs_salamander_deobfuscate(sqobfs_ctx *ctx, const sqobfs_keyring *kr,
+                                  const sqobfs_batch *b, void *stream);
+int sqobfs_xplus_obfuscate(sqobfs_ctx *ctx, const sqobfs_keyring *kr,
+                           const sqobfs_batch *b, void *stream);
+int sqobfs_xplus_deobfuscate(sqobfs_ctx *ctx, const sqobfs_keyring *kr,
+                             const sqobfs_batch *b, void *stream);
+/* the same, with kind/dir as arguments */
+int sqobfs_launch(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
+                  const sqobfs_batch *b, void *stream);
+
+/* Host-memory batch: copies the touched input range and the descriptors to
+ * the GPU through pinned staging, launches, copies the output range and
+ * out_len back.  Synchronous.  Output bytes outside the packets' output
+ * regions are preserved. */
+int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
+                    const sqobfs_batch *host_batch);
+
+/* Pinned host memory for zero-copy staging by callers (socket buffers). */
+int sqobfs_host_alloc(sqobfs_ctx *ctx, size_t bytes, void **out);
+void sqobfs_host_free(sqobfs_ctx *ctx, void *p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SQOBFS_H */

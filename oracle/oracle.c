@@ -1,0 +1,417 @@
+/*
+ * oracle.c -- CPU restatement of sing-quic's Salamander / XPlus obfuscation.
+ * TEST INFRASTRUCTURE ONLY (see oracle.h for scope, citations, and why parity
+ * with the Go reference is unpinned).  Plain C99 + pthreads, built by
+ * oracle/Makefile into oracle/liboracle.so.
+ */
+#include "oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ */
+/* BLAKE2b (RFC 7693 section 3)                                        */
+/* ------------------------------------------------------------------ */
+
+static const uint64_t b2_iv[8] = {
+    0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
+    0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+    0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+
+/* RFC 7693 section 2.7: message word schedule, rounds 10 and 11 repeat 0 and 1 */
+static const uint8_t b2_sigma[12][16] = {
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+    {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+    {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4},
+    {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+    {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13},
+    {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+    {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11},
+    {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+    {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5},
+    {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0},
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+    {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3}};
+
+static uint64_t rotr64(uint64_t x, unsigned n) {
+  return (x >> n) | (x << (64 - n));
+}
+
+static uint64_t load64le(const uint8_t *p) {
+  uint64_t v = 0;
+  for (int i = 7; i >= 0; i--) v = (v << 8) | p[i];
+  return v;
+}
+
+/* RFC 7693 section 3.1, the mixing function G */
+#define B2_G(a, b, c, d, x, y)          \
+  do {                                  \
+    v[a] = v[a] + v[b] + (x);           \
+    v[d] = rotr64(v[d] ^ v[a], 32);     \
+    v[c] = v[c] + v[d];                 \
+    v[b] = rotr64(v[b] ^ v[c], 24);     \
+    v[a] = v[a] + v[b] + (y);           \
+    v[d] = rotr64(v[d] ^ v[a], 16);     \
+    v[c] = v[c] + v[d];                 \
+    v[b] = rotr64(v[b] ^ v[c], 63);     \
+  } while (0)
+
+/* RFC 7693 section 3.2, compression function F */
+static void b2_compress(uint64_t h[8], const uint8_t block[128], uint64_t t,
+                        int last) {
+  uint64_t v[16], m[16];
+  for (int i = 0; i < 16; i++) m[i] = load64le(block + 8 * i);
+  for (int i = 0; i < 8; i++) {
+    v[i] = h[i];
+    v[i + 8] = b2_iv[i];
+  }
+  v[12] ^= t; /* low word of the 128-bit offset counter; high word stays 0 */
+  if (last) v[14] = ~v[14];
+  for (int r = 0; r < 12; r++) {
+    const uint8_t *s = b2_sigma[r];
+    B2_G(0, 4, 8, 12, m[s[0]], m[s[1]]);
+    B2_G(1, 5, 9, 13, m[s[2]], m[s[3]]);
+    B2_G(2, 6, 10, 14, m[s[4]], m[s[5]]);
+    B2_G(3, 7, 11, 15, m[s[6]], m[s[7]]);
+    B2_G(0, 5, 10, 15, m[s[8]], m[s[9]]);
+    B2_G(1, 6, 11, 12, m[s[10]], m[s[11]]);
+    B2_G(2, 7, 8, 13, m[s[12]], m[s[13]]);
+    B2_G(3, 4, 9, 14, m[s[14]], m[s[15]]);
+  }
+  for (int i = 0; i < 8; i++) h[i] ^= v[i] ^ v[i + 8];
+}
+
+void or_blake2b(const uint8_t *in, size_t len, uint8_t *out, size_t outlen) {
+  uint64_t h[8];
+  uint8_t block[128];
+  for (int i = 0; i < 8; i++) h[i] = b2_iv[i];
+  /* parameter block: digest length, key length 0, fanout 1, depth 1 */
+  h[0] ^= 0x01010000ULL ^ (uint64_t)outlen;
+  size_t off = 0;
+  /* every full block except the final one is compressed with last = 0 */
+  while (len - off > 128) {
+    b2_compress(h, in + off, (uint64_t)(off + 128), 0);
+    off += 128;
+  }
+  memset(block, 0, sizeof block);
+  memcpy(block, in + off, len - off);
+  b2_compress(h, block, (uint64_t)len, 1);
+  for (size_t i = 0; i < outlen; i++) out[i] = (uint8_t)(h[i / 8] >> (8 * (i % 8)));
+}
+
+void or_blake2b256(const uint8_t *in, size_t len, uint8_t out[32]) {
+  or_blake2b(in, len, out, 32);
+}
+
+/* ------------------------------------------------------------------ */
+/* SHA-256 (FIPS 180-4 section 6.2)                                    */
+/* ------------------------------------------------------------------ */
+
+static const uint32_t s2_k[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1,
+    0x923f82a4, 0xab1c5ed5, 0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3,
+    0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174, 0xe49b69c1, 0xefbe4786,
+    0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147,
+    0x06ca6351, 0x14292967, 0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13,
+    0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85, 0xa2bfe8a1, 0xa81a664b,
+    0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a,
+    0x5b9cca4f, 0x682e6ff3, 0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208,
+    0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+static uint32_t rotr32(uint32_t x, unsigned n) {
+  return (x >> n) | (x << (32 - n));
+}
+
+static void s2_compress(uint32_t st[8], const uint8_t blk[64]) {
+  uint32_t w[64];
+  for (int i = 0; i < 16; i++)
+    w[i] = ((uint32_t)blk[4 * i] << 24) | ((uint32_t)blk[4 * i + 1] << 16) |
+           ((uint32_t)blk[4 * i + 2] << 8) | blk[4 * i + 3];
+  for (int i = 16; i < 64; i++) {
+    uint32_t s0 = rotr32(w[i - 15], 7) ^ rotr32(w[i - 15], 18) ^ (w[i - 15] >> 3);
+    uint32_t s1 = rotr32(w[i - 2], 17) ^ rotr32(w[i - 2], 19) ^ (w[i - 2] >> 10);
+    w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+  }
+  uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5],
+           g = st[6], h = st[7];
+  for (int i = 0; i < 64; i++) {
+    uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
+    uint32_t ch = (e & f) ^ (~e & g);
+    uint32_t t1 = h + S1 + ch + s2_k[i] + w[i];
+    uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
+    uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    uint32_t t2 = S0 + mj;
+    h = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + t2;
+  }
+  st[0] += a;
+  st[1] += b;
+  st[2] += c;
+  st[3] += d;
+  st[4] += e;
+  st[5] += f;
+  st[6] += g;
+  st[7] += h;
+}
+
+void or_sha256(const uint8_t *in, size_t len, uint8_t out[32]) {
+  uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                    0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  uint8_t blk[128];
+  size_t off = 0;
+  while (len - off >= 64) {
+    s2_compress(st, in + off);
+    off += 64;
+  }
+  size_t rem = len - off;
+  memset(blk, 0, sizeof blk);
+  memcpy(blk, in + off, rem);
+  blk[rem] = 0x80;
+  size_t padlen = (rem + 1 + 8 <= 64) ? 64 : 128;
+  uint64_t bits = (uint64_t)len * 8;
+  for (int i = 0; i < 8; i++) blk[padlen - 1 - i] = (uint8_t)(bits >> (8 * i));
+  s2_compress(st, blk);
+  if (padlen == 128) s2_compress(st, blk + 64);
+  for (int i = 0; i < 8; i++) {
+    out[4 * i] = (uint8_t)(st[i] >> 24);
+    out[4 * i + 1] = (uint8_t)(st[i] >> 16);
+    out[4 * i + 2] = (uint8_t)(st[i] >> 8);
+    out[4 * i + 3] = (uint8_t)st[i];
+  }
+}
+
+/* ------------------------------------------------------------------ */
+/* Key derivation: hash(psk || salt).  The reference builds this input  */
+/* with append(password, salt...); here it is always a private copy     */
+/* (SURVEY.md section 5 explains the aliasing hazard in the Go code).   */
+/* ------------------------------------------------------------------ */
+
+static void hash_psk_salt(int kind, const uint8_t *psk, size_t psk_len,
+                          const uint8_t *salt, size_t salt_len,
+                          uint8_t key[32]) {
+  uint8_t small[256];
+  uint8_t *buf = (psk_len + salt_len <= sizeof small)
+                     ? small
+                     : (uint8_t *)malloc(psk_len + salt_len);
+  if (psk_len) memcpy(buf, psk, psk_len);
+  memcpy(buf + psk_len, salt, salt_len);
+  if (kind == OR_SALAMANDER)
+    or_blake2b256(buf, psk_len + salt_len, key);
+  else
+    or_sha256(buf, psk_len + salt_len, key);
+  if (buf != small) free(buf);
+}
+
+void or_salamander_key(const uint8_t *psk, size_t psk_len,
+                       const uint8_t salt[8], uint8_t key[32]) {
+  hash_psk_salt(OR_SALAMANDER, psk, psk_len, salt, OR_SALAMANDER_SALT, key);
+}
+
+void or_xplus_key(const uint8_t *psk, size_t psk_len, const uint8_t salt[16],
+                  uint8_t key[32]) {
+  hash_psk_salt(OR_XPLUS, psk, psk_len, salt, OR_XPLUS_SALT, key);
+}
+
+/* salamander.go:57-70 */
+long or_salamander_write(const uint8_t *psk, size_t psk_len,
+                         const uint8_t salt[8], const uint8_t *p, size_t len,
+                         uint8_t *wire) {
+  uint8_t key[32];
+  memcpy(wire, salt, OR_SALAMANDER_SALT);           /* :60 WriteRandom(8) */
+  or_salamander_key(psk, psk_len, salt, key);       /* :61 */
+  for (size_t index = 0; index < len; index++)      /* :62-64 */
+    wire[OR_SALAMANDER_SALT + index] = p[index] ^ key[index % 32];
+  return (long)len;                                 /* :69 */
+}
+
+/* salamander.go:42-55 */
+long or_salamander_read(const uint8_t *psk, size_t psk_len, uint8_t *p,
+                        size_t n) {
+  uint8_t key[32];
+  if (n <= OR_SALAMANDER_SALT) return (long)n;      /* :47-49 */
+  or_salamander_key(psk, psk_len, p, key);          /* :50 */
+  for (size_t index = 0; index < n - OR_SALAMANDER_SALT; index++) /* :51-53 */
+    p[index] = p[OR_SALAMANDER_SALT + index] ^ key[index % 32];
+  return (long)(n - OR_SALAMANDER_SALT);            /* :54 */
+}
+
+/* salamander.go:81-93 */
+long or_salamander_write_inplace(const uint8_t *psk, size_t psk_len,
+                                 const uint8_t salt[8], uint8_t *p,
+                                 size_t len) {
+  uint8_t key[32];
+  or_salamander_key(psk, psk_len, salt, key);       /* :84 */
+  for (size_t i = 0; i < len; i++) p[i] ^= key[i % 32]; /* :85-87 */
+  return (long)len;                                 /* :92 */
+}
+
+/* salamander.go:95-109, literally (line 104 included) */
+int or_salamander_write_vectorised(const uint8_t *psk, size_t psk_len,
+                                   const uint8_t salt[8], uint8_t **bufs,
+                                   const size_t *lens, size_t nbufs) {
+  uint8_t key[32];
+  or_salamander_key(psk, psk_len, salt, key);       /* :99 */
+  size_t bufferIndex = 0;                           /* :100 */
+  for (size_t b = 0; b < nbufs; b++) {
+    uint8_t *content = bufs[b];
+    for (size_t index = 0; index < lens[b]; index++) {
+      size_t ci = bufferIndex + index;              /* content[bufferIndex+index] */
+      size_t ki = bufferIndex + index % 32;         /* key[bufferIndex+index%32] */
+      if (ki >= 32) return OR_PANIC;                /* key is [32]byte */
+      if (ci >= lens[b]) return OR_PANIC;           /* content slice bound */
+      /* Go evaluates the range value c before the assignment */
+      content[ci] = content[index] ^ key[ki];
+    }
+    bufferIndex += lens[b];                         /* :106 */
+  }
+  return 0;
+}
+
+/* xplus.go:62-75 */
+long or_xplus_write(const uint8_t *psk, size_t psk_len,
+                    const uint8_t salt[16], const uint8_t *p, size_t len,
+                    uint8_t *wire) {
+  uint8_t key[32];
+  memcpy(wire, salt, OR_XPLUS_SALT);                /* :66-69 */
+  or_xplus_key(psk, psk_len, salt, key);            /* :70 */
+  for (size_t i = 0; i < len; i++)                  /* :71-73 */
+    wire[OR_XPLUS_SALT + i] = p[i] ^ key[i % 32];
+  return (long)(len + OR_XPLUS_SALT);               /* :74 returns inner n */
+}
+
+/* xplus.go:46-60 */
+long or_xplus_read(const uint8_t *psk, size_t psk_len, uint8_t *p, size_t n,
+                   size_t cap) {
+  uint8_t key[32];
+  if (n < OR_XPLUS_SALT) return 0;                  /* :50-52 */
+  or_xplus_key(psk, psk_len, p, key);               /* :54 */
+  for (size_t i = 0; i < cap - OR_XPLUS_SALT; i++)  /* :55-57 range p[16:] */
+    p[i] = p[OR_XPLUS_SALT + i] ^ key[i % 32];
+  return (long)(n - OR_XPLUS_SALT);                 /* :58 */
+}
+
+/* xplus.go:100-118 */
+void or_xplus_write_vectorised(const uint8_t *psk, size_t psk_len,
+                               const uint8_t salt[16], uint8_t **bufs,
+                               const size_t *lens, size_t nbufs) {
+  uint8_t key[32];
+  or_xplus_key(psk, psk_len, salt, key);            /* :107 */
+  size_t index = 0;
+  for (size_t b = 0; b < nbufs; b++)
+    for (size_t i = 0; i < lens[b]; i++) {          /* :110-114 */
+      bufs[b][i] ^= key[index % 32];
+      index++;
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* Batch restatement                                                    */
+/* ------------------------------------------------------------------ */
+
+typedef struct {
+  int kind, dir;
+  const or_psks *psks;
+  const or_batch *b;
+  uint32_t lo, hi;
+  int err;
+} or_job;
+
+static void run_one(int kind, int dir, const or_psks *psks, const or_batch *b,
+                    uint32_t i, uint8_t *scratch, size_t scratch_cap) {
+  uint32_t pid = b->psk_id ? b->psk_id[i] : 0;
+  const uint8_t *psk = psks->blob + psks->off[pid];
+  size_t psk_len = psks->len[pid];
+  const uint8_t *in = b->in + b->in_off[i];
+  uint8_t *out = b->out + b->out_off[i];
+  size_t n = b->in_len[i];
+  size_t S = kind == OR_SALAMANDER ? OR_SALAMANDER_SALT : OR_XPLUS_SALT;
+  (void)scratch_cap;
+  if (dir == OR_OBFUSCATE) {
+    const uint8_t *salt = b->salt + (size_t)i * S;
+    if (kind == OR_SALAMANDER)
+      or_salamander_write(psk, psk_len, salt, in, n, out);
+    else
+      or_xplus_write(psk, psk_len, salt, in, n, out);
+    b->out_len[i] = (uint32_t)(n + S);
+    return;
+  }
+  /* deobfuscate: the reference decodes in place in the read buffer; the
+   * batch form copies the datagram to scratch, runs the in-place routine and
+   * copies the valid result out. */
+  size_t cap = (kind == OR_XPLUS && b->in_cap) ? b->in_cap[i] : n;
+  memcpy(scratch, in, cap);
+  long r;
+  if (kind == OR_SALAMANDER) {
+    r = or_salamander_read(psk, psk_len, scratch, n);
+    memcpy(out, scratch, (size_t)r);
+  } else {
+    r = or_xplus_read(psk, psk_len, scratch, n, cap);
+    if (n >= OR_XPLUS_SALT) memcpy(out, scratch, cap - OR_XPLUS_SALT);
+  }
+  b->out_len[i] = (uint32_t)r;
+}
+
+static void *run_shard(void *arg) {
+  or_job *j = (or_job *)arg;
+  size_t cap = 0;
+  for (uint32_t i = j->lo; i < j->hi; i++) {
+    size_t c = (j->b->in_cap && j->kind == OR_XPLUS) ? j->b->in_cap[i]
+                                                      : j->b->in_len[i];
+    if (c > cap) cap = c;
+  }
+  uint8_t *scratch = (uint8_t *)malloc(cap + 1);
+  if (!scratch) {
+    j->err = -1;
+    return NULL;
+  }
+  for (uint32_t i = j->lo; i < j->hi; i++)
+    run_one(j->kind, j->dir, j->psks, j->b, i, scratch, cap);
+  free(scratch);
+  return NULL;
+}
+
+int or_batch_run(int kind, int dir, const or_psks *psks, const or_batch *b,
+                 int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if ((uint32_t)nthreads > b->n) nthreads = b->n ? (int)b->n : 1;
+  or_job *jobs = (or_job *)calloc((size_t)nthreads, sizeof(or_job));
+  pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+  int err = 0;
+  for (int t = 0; t < nthreads; t++) {
+    jobs[t].kind = kind;
+    jobs[t].dir = dir;
+    jobs[t].psks = psks;
+    jobs[t].b = b;
+    jobs[t].lo = (uint32_t)((uint64_t)b->n * t / nthreads);
+    jobs[t].hi = (uint32_t)((uint64_t)b->n * (t + 1) / nthreads);
+  }
+  if (nthreads == 1) {
+    run_shard(&jobs[0]);
+  } else {
+    for (int t = 0; t < nthreads; t++)
+      pthread_create(&th[t], NULL, run_shard, &jobs[t]);
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+  }
+  for (int t = 0; t < nthreads; t++) err |= jobs[t].err;
+  free(jobs);
+  free(th);
+  return err;
+}
+
+uint64_t or_fnv64(const uint8_t *p, size_t n, uint64_t h) {
+  if (!h) h = 0xcbf29ce484222325ULL;
+  for (size_t i = 0; i < n; i++) {
+    h ^= p[i];
+    h *= 0x100000001b3ULL;
+  }
+  return h;
+}

@@ -1,0 +1,143 @@
+/*
+ * oracle.h -- CPU restatement of sing-quic's per-datagram obfuscation layer.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This library is the parity checker for the HIP
+ * product path in sing-quic_amd/.  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it.  The product never links it.
+ *
+ * What it restates (reference = /root/reference, Go, module
+ * github.com/sagernet/sing-quic):
+ *   - hysteria2/salamander.go:42-109  (Salamander, BLAKE2b-256, 8-byte salt)
+ *   - hysteria/xplus.go:46-118         (XPlus, SHA-256, 16-byte salt)
+ *   - BLAKE2b-256: golang.org/x/crypto v0.37.0 blake2b.Sum256 (go.mod:9) --
+ *     not vendored; restated from RFC 7693 (unkeyed, digest 32 bytes).
+ *   - SHA-256: Go stdlib crypto/sha256.Sum256 -- restated from FIPS 180-4.
+ *
+ * Parity pinning: the reference has no tests, fixtures or golden vectors and
+ * no Go toolchain exists in the build container or on the GPU box, so the
+ * reference itself cannot be run.  The primitives are pinned by published
+ * known-answer tests (RFC 7693 Appendix A, FIPS 180-2 examples) and by an
+ * independent Python restatement (oracle/py_oracle.py, hashlib primitives)
+ * that generated tests/golden/.  With respect to the reference's own outputs
+ * parity is therefore UNPINNED ("parity unpinned" in DESIGN.md).
+ *
+ * The per-byte loops below are deliberately written byte-at-a-time, the way
+ * the reference writes them, so that the CPU baseline times the same
+ * algorithm the Go code runs.
+ */
+#ifndef SQ_ORACLE_H
+#define SQ_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OR_SALAMANDER_SALT 8  /* hysteria2/salamander.go:15 */
+#define OR_XPLUS_SALT 16      /* hysteria/xplus.go:17 */
+#define OR_PANIC (-1)         /* the reference would panic on this input */
+
+/* RFC 7693 BLAKE2b, unkeyed, 32-byte digest (== blake2b.Sum256). */
+void or_blake2b256(const uint8_t *in, size_t len, uint8_t out[32]);
+/* RFC 7693 BLAKE2b with arbitrary digest length 1..64 (for the KAT). */
+void or_blake2b(const uint8_t *in, size_t len, uint8_t *out, size_t outlen);
+/* FIPS 180-4 SHA-256 (== sha256.Sum256). */
+void or_sha256(const uint8_t *in, size_t len, uint8_t out[32]);
+
+/* Salamander key: BLAKE2b-256(psk || salt[0:8])  (salamander.go:50,61,84,99) */
+void or_salamander_key(const uint8_t *psk, size_t psk_len,
+                       const uint8_t salt[8], uint8_t key[32]);
+/* XPlus key: SHA-256(psk || salt[0:16])  (xplus.go:54,70,93,107) */
+void or_xplus_key(const uint8_t *psk, size_t psk_len,
+                  const uint8_t salt[16], uint8_t key[32]);
+
+/* SalamanderPacketConn.WriteTo (salamander.go:57-70): wire = salt || p^key.
+ * wire must hold len+8 bytes.  Returns the Go return value, len(p). */
+long or_salamander_write(const uint8_t *psk, size_t psk_len,
+                         const uint8_t salt[8], const uint8_t *p, size_t len,
+                         uint8_t *wire);
+
+/* SalamanderPacketConn.ReadFrom (salamander.go:42-55), after the socket read
+ * put n bytes into p: decodes in place (left shift by 8) and returns the Go
+ * return value: n when n <= 8 (p untouched), else n-8. */
+long or_salamander_read(const uint8_t *psk, size_t psk_len, uint8_t *p,
+                        size_t n);
+
+/* VectorisedSalamanderPacketConn.WriteTo (salamander.go:81-93): XORs p in
+ * place and returns len(p); the salt goes in a separate header. */
+long or_salamander_write_inplace(const uint8_t *psk, size_t psk_len,
+                                 const uint8_t salt[8], uint8_t *p,
+                                 size_t len);
+
+/* VectorisedSalamanderPacketConn.WriteVectorisedPacket (salamander.go:95-109)
+ * restated literally, including line 104's indexing
+ *   content[bufferIndex+index] = c ^ key[bufferIndex+index%32]
+ * Returns 0, or OR_PANIC where Go would raise an index-out-of-range panic
+ * (any non-empty buffer after a non-empty first one).  Buffers are XORed in
+ * place exactly as far as the Go loop gets before it would panic. */
+int or_salamander_write_vectorised(const uint8_t *psk, size_t psk_len,
+                                   const uint8_t salt[8], uint8_t **bufs,
+                                   const size_t *lens, size_t nbufs);
+
+/* XPlusPacketConn.WriteTo (xplus.go:62-75): wire = salt || p^key, wire
+ * holds len+16.  Returns the Go return value, the inner WriteTo's n = len+16. */
+long or_xplus_write(const uint8_t *psk, size_t psk_len,
+                    const uint8_t salt[16], const uint8_t *p, size_t len,
+                    uint8_t *wire);
+
+/* XPlusPacketConn.ReadFrom (xplus.go:46-60): p has capacity cap >= n bytes.
+ * n < 16 -> returns 0, p untouched.  Otherwise XORs in place for
+ * i in [0, cap-16) (NOT n-16: xplus.go:55 ranges over p[16:]) and returns
+ * n-16. */
+long or_xplus_read(const uint8_t *psk, size_t psk_len, uint8_t *p, size_t n,
+                   size_t cap);
+
+/* VectorisedXPlusConn.WriteVectorisedPacket (xplus.go:100-118): one running
+ * keystream index over all buffers, in place. */
+void or_xplus_write_vectorised(const uint8_t *psk, size_t psk_len,
+                               const uint8_t salt[16], uint8_t **bufs,
+                               const size_t *lens, size_t nbufs);
+
+/* ---- batch restatement over the sqobfs_batch layout (include/sqobfs.h) ----
+ * Host pointers.  psk table: psk_blob + psk_off[k] / psk_len[k].
+ * psk_id == NULL -> every packet uses psk 0.
+ * obfuscate: in = payloads, salt = n*S bytes, out = wire (S+L), out_len = S+L.
+ * deobfuscate: in = wire (n bytes), out = payload.  Salamander n<=8: the n raw
+ *   bytes are copied to out, out_len = n.  XPlus n<16: out_len = 0, nothing
+ *   written.  XPlus in_cap (may be NULL = in_len) reproduces xplus.go:55.
+ * nthreads > 1 splits the packets in contiguous shards over pthreads. */
+typedef struct {
+  uint32_t n;
+  const uint8_t *in;
+  const uint64_t *in_off;
+  const uint32_t *in_len;
+  uint8_t *out;
+  const uint64_t *out_off;
+  uint32_t *out_len;
+  const uint8_t *salt;
+  const uint16_t *psk_id;
+  const uint32_t *in_cap;
+} or_batch;
+
+typedef struct {
+  const uint8_t *blob;
+  const uint64_t *off;
+  const uint32_t *len;
+  uint32_t count;
+} or_psks;
+
+enum { OR_SALAMANDER = 0, OR_XPLUS = 1 };
+enum { OR_OBFUSCATE = 0, OR_DEOBFUSCATE = 1 };
+
+int or_batch_run(int kind, int dir, const or_psks *psks, const or_batch *b,
+                 int nthreads);
+
+/* FNV-1a-64 over n bytes; used for checksum-of-checksums properties. */
+uint64_t or_fnv64(const uint8_t *p, size_t n, uint64_t h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,66 @@
+// sq_internal.h -- layouts shared by the host C-ABI (sq_api.hip) and the
+// gfx950 kernels (sq_kernels.hip).  Not part of the public ABI.
+#pragma once
+
+#include <stdint.h>
+
+namespace sq {
+
+constexpr int kSalamanderSalt = 8;  // hysteria2/salamander.go:15
+constexpr int kXPlusSalt = 16;      // hysteria/xplus.go:17
+constexpr int kWave = 64;           // CDNA wavefront
+constexpr int kBlock = 256;         // 4 waves per workgroup
+constexpr int kWavesPerBlock = kBlock / kWave;
+
+// Per-PSK hash state, derived once per keyring on the GPU (psk_prepare).
+//
+// Both hashes are Merkle-Damgard-style over psk || salt, and the PSK is the
+// same for every packet of a connection (the `password` field captured by
+// NewSalamanderConn, hysteria2/salamander.go:19-40).  So every block made of
+// PSK bytes only is compressed once here, and the per-packet kernel starts
+// from the chaining value `h` with a message template `m` that already holds
+// the PSK tail (and, for SHA-256, the 0x80 pad byte and the bit length).  The
+// packet's salt is OR-ed into `m` at byte `salt_pos`, giving 1 compression
+// per packet for PSKs up to 120 B (BLAKE2b) / 39 B (SHA-256), at most 2 for
+// any PSK length.
+struct alignas(16) PskEntry {
+  uint64_t h[8];     // BLAKE2b chaining value | SHA-256: 8 u32 in h32()
+  uint64_t m[32];    // final block(s): BLAKE2b 2x16 LE u64 words |
+                     // SHA-256 2x16 BE u32 words packed in the first 128 B
+  uint64_t t_first;  // BLAKE2b byte counter for block 1 when nblocks == 2
+  uint64_t t_last;   // BLAKE2b byte counter for the final block
+  uint32_t nblocks;  // 1 or 2 compressions per packet
+  uint32_t salt_pos; // byte offset of the salt inside the final block(s)
+  uint32_t psk_len;
+  uint32_t kind;     // sqobfs_kind
+};
+static_assert(sizeof(PskEntry) == 352, "PskEntry layout");
+
+// Kernel arguments.  psk0 is the keyring's entry 0 passed by value, so the
+// single-PSK kernels read the hash state from the kernarg segment (scalar
+// loads, wave-uniform) instead of gathering it per lane.
+struct KParams {
+  const uint8_t *in;
+  const uint64_t *in_off;
+  const uint32_t *in_len;
+  uint8_t *out;
+  const uint64_t *out_off;
+  uint32_t *out_len;
+  const uint8_t *salt;
+  const uint16_t *psk_id;
+  const uint32_t *in_cap;
+  const PskEntry *psk_table;
+  uint32_t n;
+  uint32_t n_psk;
+  PskEntry psk0;
+};
+
+}  // namespace sq
+
+// launchers implemented in sq_kernels.hip
+extern "C" int sq_launch_obfs(int kind, int dir, const sq::KParams *kp,
+                              void *stream);
+extern "C" int sq_launch_psk_prepare(int kind, const uint8_t *blob,
+                                     const uint64_t *off, const uint32_t *len,
+                                     uint32_t count, sq::PskEntry *out,
+                                     void *stream);

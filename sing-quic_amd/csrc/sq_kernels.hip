@@ -1,0 +1,548 @@
+// sq_kernels.hip -- gfx950 kernels for the Salamander / XPlus obfuscation path.
+//
+// One fused kernel per (scheme, direction, psk-mode).  It replaces the
+// per-datagram bodies of
+//   SalamanderPacketConn.WriteTo / ReadFrom   hysteria2/salamander.go:42-70
+//   VectorisedSalamanderPacketConn.WriteTo    hysteria2/salamander.go:81-93
+//   XPlusPacketConn.WriteTo / ReadFrom        hysteria/xplus.go:46-75
+//   VectorisedXPlusConn.WriteTo               hysteria/xplus.go:86-98
+// for a whole ragged batch of datagrams per launch.
+//
+// Work decomposition (one wavefront = 64 packets, fully independent waves):
+//   1. descriptor  lane l owns packet 64*wave + l: reads its offsets/lengths
+//                  and salt (obfs: salt array; deobfs: first S wire bytes).
+//   2. key         lane l hashes its own packet's psk||salt (BLAKE2b-256 or
+//                  SHA-256) starting from the keyring's per-PSK midstate:
+//                  64 different packets hashed in parallel, no idle lanes.
+//   3. split       each packet's output is cut at 16-byte boundaries of the
+//                  DESTINATION address: "full" chunks (16 payload bytes) and
+//                  at most ~3 "edge" chunks (salt bytes, unaligned head,
+//                  tail).  A wave prefix-sum over full-chunk counts builds a
+//                  flat chunk space for the 64 packets; each packet's
+//                  addressing and its two 16-byte keystream phases go to LDS.
+//   4. edges       the owner lane writes its packet's edge chunks (byte-exact
+//                  masked stores; loads only 16-byte-aligned blocks that hold
+//                  valid bytes, so nothing outside a packet is ever touched).
+//   5. stream      the wave walks the flat chunk space, 64 lanes x U chunks
+//                  per step: one dwordx4 load, XOR with the LDS keystream,
+//                  one aligned dwordx4 store per chunk.  Chunk -> packet is a
+//                  ballot/popcount on the prefix sums held in registers.
+// HBM traffic is the algorithmic minimum: every payload byte is read once and
+// every output byte written once; the key never leaves LDS/registers.
+#include <hip/hip_runtime.h>
+
+#include "sq_hash.h"
+#include "sq_internal.h"
+
+namespace sq {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// dword-aligned 16-byte access: still one global_load_dwordx4 on gfx950
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+constexpr uint32_t kMaxPacket = 1u << 26;  // per-packet length bound (u32 chunk math)
+constexpr uint32_t kBadPsk = 0xFFFFFFFFu;
+constexpr uint32_t kBadLen = 0xFFFFFFFEu;
+
+// ------------------------------------------------------------ byte helpers
+
+// Bitwise select (v_bfi_b32).  Used instead of `c ? a[i] : b[i]`, which
+// clang folds into a select of POINTERS and then spills the arrays to scratch.
+__device__ __forceinline__ uint32_t bsel(bool c, uint32_t a, uint32_t b) {
+  const uint32_t m = 0u - (uint32_t)c;
+  return (a & m) | (b & ~m);
+}
+
+// 5 consecutive words w[q..q+4] out of N (q runtime, q+4 < N) by a 3-stage
+// barrel of bit selects (no scratch, no per-index compare chains).
+template <int N>
+__device__ __forceinline__ void take5(const uint32_t (&w)[N], uint32_t q,
+                                      uint32_t (&x)[5]) {
+  static_assert(N >= 12, "take5 needs 12 words");
+  uint32_t y[8], z[6];
+  const bool b2 = q & 4, b1 = q & 2, b0 = q & 1;
+#pragma unroll
+  for (int j = 0; j < 8; j++) y[j] = bsel(b2, w[j + 4], w[j]);
+#pragma unroll
+  for (int j = 0; j < 6; j++) z[j] = bsel(b1, y[j + 2], y[j]);
+#pragma unroll
+  for (int j = 0; j < 5; j++) x[j] = bsel(b0, z[j + 1], z[j]);
+}
+
+// 16 bytes starting at byte o (0..31) of a 48-byte register image w[12].
+__device__ __forceinline__ void win16(const uint32_t (&w)[12], uint32_t o,
+                                      uint32_t (&out)[4]) {
+  uint32_t x[5];
+  take5(w, o >> 2, x);
+  const uint32_t sh = o & 3;
+#pragma unroll
+  for (int j = 0; j < 4; j++) out[j] = __builtin_amdgcn_alignbyte(x[j + 1], x[j], sh);
+}
+
+// keystream bytes key[(r + k) % 32], k = 0..15, as 4 LE words
+__device__ __forceinline__ void keywin(const uint32_t (&key)[8], uint32_t r,
+                                       uint32_t (&out)[4]) {
+  uint32_t w[12];
+#pragma unroll
+  for (int j = 0; j < 12; j++) w[j] = key[j & 7];
+  win16(w, r & 31, out);
+}
+
+// mask of bytes [lo, hi) inside word j (bytes 4j .. 4j+3)
+__device__ __forceinline__ uint32_t bytes_below(int k) {
+  return k <= 0 ? 0u : (k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * k)) - 1u));
+}
+__device__ __forceinline__ uint32_t range_mask(int lo, int hi, int j) {
+  return bytes_below(hi - 4 * j) & ~bytes_below(lo - 4 * j);
+}
+
+__device__ __forceinline__ uint32_t pick4(const uint32_t (&v)[4], uint32_t i) {
+  const uint32_t a = bsel(i & 1, v[1], v[0]);
+  const uint32_t b = bsel(i & 1, v[3], v[2]);
+  return bsel(i & 2, b, a);
+}
+
+// Loads the 16-byte-aligned blocks that hold bytes [ps, pe) (1..16 bytes) and
+// returns the 16 bytes at address X (ps-15 <= X <= ps, pe <= X+16).  Only
+// blocks containing at least one valid byte are read, so a packet at the very
+// edge of an allocation never faults.
+__device__ __forceinline__ void load_window(uint64_t ps, uint64_t pe,
+                                            uint64_t X, uint32_t (&out)[4]) {
+  const uint64_t B0 = ps & ~15ull;
+  const u32x4 v0 = *reinterpret_cast<const u32x4 *>(B0);
+  u32x4 v1 = {0u, 0u, 0u, 0u};
+  if (pe > B0 + 16) v1 = *reinterpret_cast<const u32x4 *>(B0 + 16);
+  const uint32_t w[12] = {0u,   0u,   0u,   0u,   v0.x, v0.y,
+                          v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+  win16(w, (uint32_t)(X - B0 + 16), out);
+}
+
+// Store bytes [a, b) of the 16-byte value v to the 16-byte-aligned address A
+// with naturally aligned 1/2/4/8/16-byte stores (at most 9, usually 1-3).
+__device__ __forceinline__ void store_partial(uint64_t A, const uint32_t (&v)[4],
+                                              uint32_t a, uint32_t b) {
+  uint32_t pos = a;
+  if ((pos & 1) && pos + 1 <= b) {
+    *reinterpret_cast<uint8_t *>(A + pos) = (uint8_t)(pick4(v, pos >> 2) >> (8 * (pos & 3)));
+    pos += 1;
+  }
+  if ((pos & 2) && pos + 2 <= b) {
+    *reinterpret_cast<uint16_t *>(A + pos) = (uint16_t)(pick4(v, pos >> 2) >> (8 * (pos & 2)));
+    pos += 2;
+  }
+  if ((pos & 4) && pos + 4 <= b) {
+    *reinterpret_cast<uint32_t *>(A + pos) = pick4(v, pos >> 2);
+    pos += 4;
+  }
+  if ((pos & 8) && pos + 8 <= b) {
+    *reinterpret_cast<uint2 *>(A + 8) = make_uint2(v[2], v[3]);
+    pos += 8;
+  }
+  if (pos == 0 && b == 16) {
+    *reinterpret_cast<u32x4 *>(A) = u32x4{v[0], v[1], v[2], v[3]};
+    pos = 16;
+  }
+  if (pos + 8 <= b) {  // pos is 0 or 8 here
+    const bool hi = pos & 8;
+    *reinterpret_cast<uint2 *>(A + pos) = make_uint2(bsel(hi, v[2], v[0]), bsel(hi, v[3], v[1]));
+    pos += 8;
+  }
+  if (pos + 4 <= b) {
+    *reinterpret_cast<uint32_t *>(A + pos) = pick4(v, pos >> 2);
+    pos += 4;
+  }
+  if (pos + 2 <= b) {
+    *reinterpret_cast<uint16_t *>(A + pos) = (uint16_t)(pick4(v, pos >> 2) >> (8 * (pos & 2)));
+    pos += 2;
+  }
+  if (pos + 1 <= b) {
+    *reinterpret_cast<uint8_t *>(A + pos) = (uint8_t)(pick4(v, pos >> 2) >> (8 * (pos & 3)));
+  }
+}
+
+// ------------------------------------------------------------ key derivation
+
+// Salamander: key = BLAKE2b-256(psk || salt8) (hysteria2/salamander.go:50).
+__device__ __forceinline__ void salamander_key(const PskEntry *E,
+                                               const uint32_t (&salt)[4],
+                                               uint32_t (&key)[8]) {
+  uint64_t h[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) h[i] = E->h[i];
+  const uint32_t nb = E->nblocks, t = E->salt_pos;
+  const uint64_t sv = b2_pack(salt[0], salt[1]);
+  const uint32_t w = t >> 3, sh = (t & 7) * 8;
+  const uint64_t lo = sv << sh;
+  const uint64_t hi = sh ? (sv >> (64 - sh)) : 0ull;
+  for (uint32_t blk = 0; blk < nb; blk++) {
+    uint64_t m[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const uint32_t idx = 16 * blk + j;
+      uint64_t x = E->m[idx];
+      x |= (idx == w) ? lo : 0ull;
+      x |= (idx == w + 1) ? hi : 0ull;
+      m[j] = x;
+    }
+    const bool last = blk + 1 == nb;
+    b2_compress(h, m, last ? E->t_last : E->t_first, last);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    key[2 * i] = (uint32_t)h[i];
+    key[2 * i + 1] = (uint32_t)(h[i] >> 32);
+  }
+}
+
+// XPlus: key = SHA-256(psk || salt16) (hysteria/xplus.go:54).
+__device__ __forceinline__ void xplus_key(const PskEntry *E,
+                                          const uint32_t (&salt)[4],
+                                          uint32_t (&key)[8]) {
+  const uint32_t *h32 = reinterpret_cast<const uint32_t *>(E->h);
+  const uint32_t *m32 = reinterpret_cast<const uint32_t *>(E->m);
+  uint32_t st[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) st[i] = h32[i];
+  const uint32_t nb = E->nblocks, t = E->salt_pos;
+  const uint32_t w = t >> 2, sh = (t & 3) * 8;
+  uint32_t c[5];
+#pragma unroll
+  for (int k = 0; k < 5; k++) {
+    const uint32_t cur = k < 4 ? __builtin_bswap32(salt[k]) : 0u;
+    const uint32_t prev = k > 0 ? __builtin_bswap32(salt[k - 1]) : 0u;
+    c[k] = (cur >> sh) | (sh ? (prev << (32 - sh)) : 0u);
+  }
+  for (uint32_t blk = 0; blk < nb; blk++) {
+    uint32_t m[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const uint32_t idx = 16 * blk + j;
+      uint32_t x = m32[idx];
+#pragma unroll
+      for (int k = 0; k < 5; k++) x |= (idx == w + k) ? c[k] : 0u;
+      m[j] = x;
+    }
+    s2_compress(st, m);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) key[i] = __builtin_bswap32(st[i]);
+}
+
+// ------------------------------------------------------------ edge chunks
+
+struct PacketJob {
+  uint64_t src_pay;  // address of payload byte 0 in the input
+  uint64_t dst_pay;  // address of payload byte 0 in the output
+  uint64_t len;      // payload bytes to transform
+  uint32_t pre;      // salt bytes written in front of dst_pay (obfs) or 0
+};
+
+// One edge chunk: bytes [a, b) of the 16-byte output block at A.
+__device__ __forceinline__ void edge_chunk(const PacketJob &J, const uint32_t (&key)[8],
+                                           const uint32_t (&salt)[4], uint64_t A,
+                                           uint32_t a, uint32_t b) {
+  uint32_t val[4] = {0u, 0u, 0u, 0u};
+  const int64_t dp = (int64_t)(J.dst_pay - A);  // payload starts dp bytes into the block
+  const uint32_t pay_lo = dp > (int64_t)a ? (uint32_t)(dp < 16 ? dp : 16) : a;
+  if (pay_lo < b) {
+    const uint64_t X = J.src_pay - (uint64_t)dp;  // input address of output byte A
+    uint32_t win[4], ks[4];
+    load_window(X + pay_lo, X + b, X, win);
+    keywin(key, (uint32_t)(A - J.dst_pay) & 31u, ks);
+#pragma unroll
+    for (int j = 0; j < 4; j++) val[j] = (win[j] ^ ks[j]) & range_mask(pay_lo, b, j);
+  }
+  if (J.pre && dp > (int64_t)a) {
+    const uint32_t se = dp < (int64_t)b ? (uint32_t)dp : b;  // salt bytes [a, se)
+    const uint32_t w[12] = {0u, 0u, 0u, 0u, salt[0], salt[1], salt[2], salt[3], 0u, 0u, 0u, 0u};
+    uint32_t sw[4];
+    win16(w, (uint32_t)(16 + (int64_t)J.pre - dp), sw);
+#pragma unroll
+    for (int j = 0; j < 4; j++) val[j] |= sw[j] & range_mask(a, se, j);
+  }
+  store_partial(A, val, a, b);
+}
+
+__device__ __forceinline__ void edge_span(const PacketJob &J, const uint32_t (&key)[8],
+                                          const uint32_t (&salt)[4], uint64_t A0,
+                                          uint64_t A1) {
+  for (uint64_t A = A0 & ~15ull; A < A1; A += 16) {
+    const uint32_t a = (uint32_t)((A0 > A ? A0 : A) - A);
+    const uint32_t b = (uint32_t)((A1 < A + 16 ? A1 : A + 16) - A);
+    edge_chunk(J, key, salt, A, a, b);
+  }
+}
+
+// ------------------------------------------------------------ main kernel
+
+// LDS record per packet (48 B): input/output addressing for flat chunk c
+// (addr = base + 16*c) and the keystream for even / odd c.
+struct alignas(16) ChunkRec {
+  uint64_t ssub, dsub;
+  u32x4 ks[2];
+};
+
+template <int KIND, int DIR, bool MULTI, int U>
+__global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
+  constexpr uint32_t S = KIND == 0 ? kSalamanderSalt : kXPlusSalt;
+  __shared__ ChunkRec recs[kWavesPerBlock][kWave];
+
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint32_t wv = threadIdx.x / kWave;
+  const uint64_t p64 = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool valid = p64 < P.n;
+  const uint32_t p = (uint32_t)p64;
+
+  // ---- 1. descriptor
+  PacketJob J = {0, 0, 0, 0};
+  uint32_t salt[4] = {0u, 0u, 0u, 0u};
+  bool do_hash = false;
+  const PskEntry *E = &P.psk0;
+  if (valid) {
+    const uint64_t in_base = (uint64_t)P.in + P.in_off[p];
+    const uint64_t out_base = (uint64_t)P.out + P.out_off[p];
+    const uint32_t len = P.in_len[p];
+    uint32_t olen = 0;
+    bool bad = false;
+    if (MULTI) {
+      const uint32_t pid = P.psk_id[p];
+      if (pid >= P.n_psk) bad = true;
+      else E = P.psk_table + pid;
+    }
+    uint32_t cap = len;
+    if (KIND == 1 && DIR == 1 && P.in_cap) {
+      const uint32_t c = P.in_cap[p];
+      cap = c > len ? c : len;
+    }
+    if (len > kMaxPacket || cap > kMaxPacket) {
+      olen = kBadLen;
+    } else if (bad) {
+      olen = kBadPsk;
+    } else if (DIR == 0) {  // obfuscate: wire = salt || payload ^ key
+      const uint32_t *sp = reinterpret_cast<const uint32_t *>(P.salt + (uint64_t)p * S);
+#pragma unroll
+      for (uint32_t k = 0; k < S / 4; k++) salt[k] = sp[k];
+      J = {in_base, out_base + S, len, S};
+      olen = S + len;
+      do_hash = true;
+    } else if (KIND == 0 && len <= S) {
+      // salamander.go:47-49: short datagram returned as is -> copy (key 0)
+      J = {in_base, out_base, len, 0};
+      olen = len;
+    } else if (KIND == 1 && len < S) {
+      olen = 0;  // xplus.go:50-52: dropped as empty
+    } else {  // deobfuscate: salt = first S wire bytes
+      uint32_t w[4];
+      load_window(in_base, in_base + S, in_base, w);
+#pragma unroll
+      for (uint32_t k = 0; k < S / 4; k++) salt[k] = w[k];
+      J = {in_base + S, out_base, (uint64_t)cap - S, 0};
+      olen = len - S;
+      do_hash = true;
+    }
+    P.out_len[p] = olen;
+  }
+
+  // ---- 2. key (lane-parallel: one packet per lane)
+  uint32_t key[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+  if (do_hash) {
+    if (KIND == 0) salamander_key(E, salt, key);
+    else xplus_key(E, salt, key);
+  }
+
+  // ---- 3. split into full chunks (flat, streamed) and edges (owner lane)
+  const uint64_t rs = J.dst_pay - J.pre, re = J.dst_pay + J.len;
+  const uint64_t fa = (J.dst_pay + 15) & ~15ull, fb = re & ~15ull;
+  const uint32_t F = (J.len && fb > fa) ? (uint32_t)((fb - fa) >> 4) : 0u;
+  uint32_t incl = F;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d, kWave);
+    if (lane >= (uint32_t)d) incl += y;
+  }
+  const uint32_t start = incl - F;
+  const uint32_t T = __shfl(incl, kWave - 1, kWave);
+  {
+    uint32_t k0[4], k1[4];
+    const uint32_t r0 = (uint32_t)(fa - J.dst_pay);  // 0..15
+    keywin(key, r0, k0);
+    keywin(key, r0 + 16, k1);
+    const bool odd = start & 1;
+    ChunkRec R;
+    R.ssub = J.src_pay + (fa - J.dst_pay) - 16ull * start;
+    R.dsub = fa - 16ull * start;
+    R.ks[0] = u32x4{bsel(odd, k1[0], k0[0]), bsel(odd, k1[1], k0[1]),
+                    bsel(odd, k1[2], k0[2]), bsel(odd, k1[3], k0[3])};
+    R.ks[1] = u32x4{bsel(odd, k0[0], k1[0]), bsel(odd, k0[1], k1[1]),
+                    bsel(odd, k0[2], k1[2]), bsel(odd, k0[3], k1[3])};
+    recs[wv][lane] = R;
+  }
+
+  // ---- 4. edges: salt bytes, unaligned head, tail
+  if (re > rs) {
+    if (F) {
+      edge_span(J, key, salt, rs, fa);
+      edge_span(J, key, salt, fb, re);
+    } else {
+      edge_span(J, key, salt, rs, re);
+    }
+  }
+
+  // LDS records visible to the whole wave (same-wave LDS ops are ordered;
+  // this is a compiler barrier plus the LDS drain)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+  // ---- 5. stream the flat full-chunk space
+  for (uint32_t base = 0; base < T; base += kWave * U) {
+    uint64_t sa[U], da[U];
+    u32x4 ks[U], v[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t b0 = base + u * kWave;
+      const uint32_t c = b0 + lane;
+      ok[u] = c < T;
+      int pp = __popcll(__ballot(start <= b0)) - 1;
+      uint64_t M = __ballot(start > b0 && start < b0 + kWave);
+      while (M) {
+        const int l = __ffsll((unsigned long long)M) - 1;
+        M &= M - 1;
+        const uint32_t sl = __builtin_amdgcn_readlane(start, l);
+        pp += c >= sl ? 1 : 0;
+      }
+      const ChunkRec &R = recs[wv][pp];
+      sa[u] = R.ssub + 16ull * c;
+      da[u] = R.dsub + 16ull * c;
+      ks[u] = R.ks[c & 1];
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if (ok[u]) {
+        if ((sa[u] & 3) == 0) {
+          v[u] = *reinterpret_cast<const u32x4_a4 *>(sa[u]);
+        } else {
+          uint32_t w[4];
+          load_window(sa[u], sa[u] + 16, sa[u], w);
+          v[u] = u32x4{w[0], w[1], w[2], w[3]};
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if (ok[u]) *reinterpret_cast<u32x4 *>(da[u]) = v[u] ^ ks[u];
+    }
+  }
+}
+
+// ------------------------------------------------------------ PSK prepare
+
+__device__ __forceinline__ uint64_t ld64le(const uint8_t *p) {
+  uint64_t v = 0;
+  for (int i = 7; i >= 0; i--) v = (v << 8) | p[i];
+  return v;
+}
+__device__ __forceinline__ uint32_t ld32be(const uint8_t *p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+// One thread per PSK: compress the PSK-only leading blocks, lay out the final
+// block template.  Runs once per keyring (connection setup), not per packet.
+__global__ void psk_prepare_kernel(int kind, const uint8_t *blob, const uint64_t *off,
+                                   const uint32_t *len, uint32_t count, PskEntry *out) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= count) return;
+  const uint8_t *psk = blob + off[k];
+  const uint32_t L = len[k];
+  PskEntry E;
+  uint8_t tm[256];
+  for (int i = 0; i < 256; i++) tm[i] = 0;
+  E.psk_len = L;
+  E.kind = (uint32_t)kind;
+  if (kind == 0) {
+    // BLAKE2b: every PSK-only 128-byte block is followed by salt bytes, so it
+    // is never the final block (RFC 7693 section 3.3).
+    uint64_t h[8];
+    b2_init256(h);
+    const uint32_t nfull = L / 128;
+    for (uint32_t bk = 0; bk < nfull; bk++) {
+      uint64_t m[16];
+      for (int j = 0; j < 16; j++) m[j] = ld64le(psk + 128 * bk + 8 * j);
+      b2_compress(h, m, 128ull * (bk + 1), false);
+    }
+    const uint32_t tail = L - 128 * nfull;
+    const uint32_t tot = tail + kSalamanderSalt;
+    for (uint32_t i = 0; i < tail; i++) tm[i] = psk[128 * nfull + i];
+    for (int i = 0; i < 8; i++) E.h[i] = h[i];
+    for (int j = 0; j < 32; j++) E.m[j] = ld64le(tm + 8 * j);
+    E.nblocks = tot > 128 ? 2 : 1;
+    E.salt_pos = tail;
+    E.t_first = 128ull * nfull + 128;
+    E.t_last = 128ull * nfull + tot;
+  } else {
+    // SHA-256: Merkle-Damgard with 0x80 pad and 64-bit big-endian bit length
+    uint32_t st[8];
+    s2_init(st);
+    const uint32_t nfull = L / 64;
+    for (uint32_t bk = 0; bk < nfull; bk++) {
+      uint32_t m[16];
+      for (int j = 0; j < 16; j++) m[j] = ld32be(psk + 64 * bk + 4 * j);
+      s2_compress(st, m);
+    }
+    const uint32_t tail = L - 64 * nfull;
+    const uint32_t used = tail + kXPlusSalt + 1 + 8;
+    const uint32_t nb = used > 64 ? 2 : 1;
+    for (uint32_t i = 0; i < tail; i++) tm[i] = psk[64 * nfull + i];
+    tm[tail + kXPlusSalt] = 0x80;
+    const uint64_t bits = ((uint64_t)L + kXPlusSalt) * 8;
+    for (int i = 0; i < 8; i++) tm[64 * nb - 1 - i] = (uint8_t)(bits >> (8 * i));
+    uint32_t *h32 = reinterpret_cast<uint32_t *>(E.h);
+    for (int i = 0; i < 16; i++) h32[i] = i < 8 ? st[i] : 0u;
+    uint32_t *m32 = reinterpret_cast<uint32_t *>(E.m);
+    for (int j = 0; j < 64; j++) m32[j] = j < 32 ? ld32be(tm + 4 * j) : 0u;
+    E.nblocks = nb;
+    E.salt_pos = tail;
+    E.t_first = 0;
+    E.t_last = 0;
+  }
+  out[k] = E;
+}
+
+template <int KIND, int DIR, bool MULTI>
+static int launch_one(const KParams *kp, hipStream_t s) {
+  constexpr int U = 4;
+  const uint64_t blocks = ((uint64_t)kp->n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL((obfs_kernel<KIND, DIR, MULTI, U>), dim3((uint32_t)blocks),
+                     dim3(kBlock), 0, s, *kp);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+}  // namespace sq
+
+extern "C" int sq_launch_obfs(int kind, int dir, const sq::KParams *kp, void *stream) {
+  using namespace sq;
+  if (kp->n == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const bool multi = kp->psk_id != nullptr;
+  const int sel = (kind << 2) | (dir << 1) | (multi ? 1 : 0);
+  switch (sel) {
+    case 0: return launch_one<0, 0, false>(kp, s);
+    case 1: return launch_one<0, 0, true>(kp, s);
+    case 2: return launch_one<0, 1, false>(kp, s);
+    case 3: return launch_one<0, 1, true>(kp, s);
+    case 4: return launch_one<1, 0, false>(kp, s);
+    case 5: return launch_one<1, 0, true>(kp, s);
+    case 6: return launch_one<1, 1, false>(kp, s);
+    case 7: return launch_one<1, 1, true>(kp, s);
+  }
+  return -1;
+}
+
+extern "C" int sq_launch_psk_prepare(int kind, const uint8_t *blob, const uint64_t *off,
+                                     const uint32_t *len, uint32_t count, sq::PskEntry *out,
+                                     void *stream) {
+  if (count == 0) return 0;
+  const uint32_t threads = 64;
+  hipLaunchKernelGGL(sq::psk_prepare_kernel, dim3((count + threads - 1) / threads),
+                     dim3(threads), 0, (hipStream_t)stream, kind, blob, off, len, count, out);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}

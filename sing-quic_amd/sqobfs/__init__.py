@@ -1,0 +1,249 @@
+"""ctypes binding of libsqobfs.so (include/sqobfs.h) for tests and bench.py.
+
+The product is the C ABI + gfx950 kernels; this module is plumbing.  It
+loads the in-tree ``sing-quic_amd/libsqobfs.so`` and raises if it is missing
+-- there is no CPU fallback anywhere in the product path.
+
+Names mirror the reference's obfuscation layer:
+  hysteria2/salamander.go  -> SALAMANDER, salt 8, BLAKE2b-256
+  hysteria/xplus.go        -> XPLUS,      salt 16, SHA-256
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+from dataclasses import dataclass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+REPO = os.path.dirname(PKG)
+LIB_PATH = os.path.join(PKG, "libsqobfs.so")
+HEADER_PATH = os.path.join(REPO, "include", "sqobfs.h")
+
+SALAMANDER, XPLUS = 0, 1
+OBFUSCATE, DEOBFUSCATE = 0, 1
+SALT_LEN = {SALAMANDER: 8, XPLUS: 16}
+OBFS_TYPE_SALAMANDER = "salamander"  # hysteria2/salamander.go:17
+
+SQ_OK, SQ_EINVAL, SQ_ENOMEM, SQ_EDEVICE, SQ_ENODEV, SQ_EPSK = 0, -1, -2, -3, -4, -5
+BAD_PSK = 0xFFFFFFFF
+
+
+class SqError(RuntimeError):
+    def __init__(self, status: int, what: str):
+        self.status = status
+        super().__init__(f"{what}: {status} ({strerror(status)})")
+
+
+class Batch(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_uint32),
+        ("flags", ctypes.c_uint32),
+        ("in_", ctypes.c_void_p),
+        ("in_off", ctypes.c_void_p),
+        ("in_len", ctypes.c_void_p),
+        ("out", ctypes.c_void_p),
+        ("out_off", ctypes.c_void_p),
+        ("out_len", ctypes.c_void_p),
+        ("salt", ctypes.c_void_p),
+        ("psk_id", ctypes.c_void_p),
+        ("in_cap", ctypes.c_void_p),
+    ]
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libsqobfs.so (fails loudly: the product has no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} is missing: build it with `make -C sing-quic_amd` "
+            "(or __graft_entry__.build()); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u32, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
+    L.sqobfs_abi_version.restype = i32
+    L.sqobfs_strerror.restype = ctypes.c_char_p
+    L.sqobfs_strerror.argtypes = [i32]
+    L.sqobfs_device_count.argtypes = [ctypes.POINTER(i32)]
+    L.sqobfs_open.argtypes = [i32, ctypes.POINTER(vp)]
+    L.sqobfs_close.argtypes = [vp]
+    L.sqobfs_close.restype = None
+    L.sqobfs_stream.argtypes = [vp]
+    L.sqobfs_stream.restype = vp
+    L.sqobfs_sync.argtypes = [vp, vp]
+    L.sqobfs_keyring_create.argtypes = [vp, i32, u32, vp, vp, vp, ctypes.POINTER(vp)]
+    L.sqobfs_keyring_destroy.argtypes = [vp]
+    L.sqobfs_keyring_destroy.restype = None
+    L.sqobfs_keyring_kind.argtypes = [vp]
+    L.sqobfs_keyring_count.argtypes = [vp]
+    L.sqobfs_keyring_count.restype = u32
+    for name in ("sqobfs_salamander_obfuscate", "sqobfs_salamander_deobfuscate",
+                 "sqobfs_xplus_obfuscate", "sqobfs_xplus_deobfuscate"):
+        getattr(L, name).argtypes = [vp, vp, ctypes.POINTER(Batch), vp]
+    L.sqobfs_launch.argtypes = [vp, vp, i32, ctypes.POINTER(Batch), vp]
+    L.sqobfs_run_host.argtypes = [vp, vp, i32, ctypes.POINTER(Batch)]
+    L.sqobfs_host_alloc.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(vp)]
+    L.sqobfs_host_free.argtypes = [vp, vp]
+    L.sqobfs_host_free.restype = None
+    _lib = L
+    return L
+
+
+def strerror(status: int) -> str:
+    try:
+        return lib().sqobfs_strerror(status).decode()
+    except Exception:  # pragma: no cover - message only
+        return "?"
+
+
+def header_symbols() -> list[str]:
+    """Every function declared in include/sqobfs.h."""
+    src = open(HEADER_PATH).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(sqobfs_[a-z0-9_]+)\s*\(", src)))
+
+
+def _check(st: int, what: str) -> None:
+    if st != SQ_OK:
+        raise SqError(st, what)
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    st = lib().sqobfs_device_count(ctypes.byref(n))
+    if st == SQ_ENODEV:
+        return 0
+    _check(st, "sqobfs_device_count")
+    return n.value
+
+
+def _ptr(a) -> int | None:
+    """Address of a numpy array or torch tensor (None passes NULL)."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return a.data_ptr()  # torch.Tensor
+
+
+class Context:
+    """One GPU (sqobfs_open)."""
+
+    def __init__(self, device: int = 0):
+        h = ctypes.c_void_p()
+        _check(lib().sqobfs_open(device, ctypes.byref(h)), "sqobfs_open")
+        self.handle = h
+        self.device = device
+
+    def close(self) -> None:
+        if self.handle:
+            lib().sqobfs_close(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def stream(self) -> int:
+        return lib().sqobfs_stream(self.handle)
+
+    def sync(self, stream: int | None = None) -> None:
+        _check(lib().sqobfs_sync(self.handle, stream), "sqobfs_sync")
+
+
+class Keyring:
+    """Device copy of the PSK(s): the `password` field of
+    SalamanderPacketConn (salamander.go:19-22) / `key` of XPlusPacketConn
+    (xplus.go:39-44)."""
+
+    def __init__(self, ctx: Context, kind: int, psks: list[bytes]):
+        blob = np.frombuffer(b"".join(psks) + b"\0", dtype=np.uint8).copy()
+        lens = np.array([len(p) for p in psks], dtype=np.uint32)
+        offs = np.zeros(len(psks), dtype=np.uint64)
+        if len(psks) > 1:
+            offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        h = ctypes.c_void_p()
+        _check(lib().sqobfs_keyring_create(ctx.handle, kind, len(psks), _ptr(blob),
+                                           _ptr(offs), _ptr(lens), ctypes.byref(h)),
+               "sqobfs_keyring_create")
+        self.handle = h
+        self.ctx = ctx
+        self.kind = kind
+        self.count = len(psks)
+
+    def close(self) -> None:
+        if self.handle:
+            lib().sqobfs_keyring_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def make_batch(n, in_, in_off, in_len, out, out_off, out_len, salt=None,
+               psk_id=None, in_cap=None) -> Batch:
+    """Batch from numpy arrays (host) or torch tensors (device)."""
+    return Batch(n, 0, _ptr(in_), _ptr(in_off), _ptr(in_len), _ptr(out), _ptr(out_off),
+                 _ptr(out_len), _ptr(salt), _ptr(psk_id), _ptr(in_cap))
+
+
+def launch(ctx: Context, kr: Keyring, direction: int, batch: Batch,
+           stream: int | None = None) -> None:
+    """Device-resident launch (async on `stream`)."""
+    _check(lib().sqobfs_launch(ctx.handle, kr.handle, direction, ctypes.byref(batch), stream),
+           "sqobfs_launch")
+
+
+def run_host(ctx: Context, kr: Keyring, direction: int, batch: Batch) -> None:
+    """Host-memory batch (synchronous, staged through pinned memory)."""
+    _check(lib().sqobfs_run_host(ctx.handle, kr.handle, direction, ctypes.byref(batch)),
+           "sqobfs_run_host")
+
+
+@dataclass
+class HostBatch:
+    """A ragged batch in host numpy arrays plus its output buffers."""
+    data: np.ndarray
+    in_off: np.ndarray
+    in_len: np.ndarray
+    out: np.ndarray
+    out_off: np.ndarray
+    out_len: np.ndarray
+    salt: np.ndarray | None = None
+    psk_id: np.ndarray | None = None
+    in_cap: np.ndarray | None = None
+
+    @property
+    def n(self) -> int:
+        return int(self.in_len.shape[0])
+
+    def as_batch(self) -> Batch:
+        return make_batch(self.n, self.data, self.in_off, self.in_len, self.out,
+                          self.out_off, self.out_len, self.salt, self.psk_id, self.in_cap)
+
+
+def pack(packets: list[bytes], align: int = 16, lead: int = 0) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Pack byte strings into one buffer at `align`-aligned offsets (+lead)."""
+    offs, pos = [], lead
+    for p in packets:
+        offs.append(pos)
+        pos += len(p)
+        pos = (pos + align - 1) // align * align + lead if align > 1 else pos
+    buf = np.zeros(max(pos, 1) + 64, dtype=np.uint8)
+    for o, p in zip(offs, packets):
+        buf[o:o + len(p)] = np.frombuffer(p, dtype=np.uint8)
+    return (buf, np.array(offs, dtype=np.uint64),
+            np.array([len(p) for p in packets], dtype=np.uint32))

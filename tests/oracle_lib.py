@@ -1,0 +1,164 @@
+"""ctypes access to the CPU restatement oracle/liboracle.so (test checker only)."""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(REPO, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "liboracle.so")
+
+SALAMANDER, XPLUS = 0, 1
+OBFUSCATE, DEOBFUSCATE = 0, 1
+
+
+class OrBatch(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint32), ("in_", ctypes.c_void_p), ("in_off", ctypes.c_void_p),
+                ("in_len", ctypes.c_void_p), ("out", ctypes.c_void_p),
+                ("out_off", ctypes.c_void_p), ("out_len", ctypes.c_void_p),
+                ("salt", ctypes.c_void_p), ("psk_id", ctypes.c_void_p),
+                ("in_cap", ctypes.c_void_p)]
+
+
+class OrPsks(ctypes.Structure):
+    _fields_ = [("blob", ctypes.c_void_p), ("off", ctypes.c_void_p), ("len", ctypes.c_void_p),
+                ("count", ctypes.c_uint32)]
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+        L = ctypes.CDLL(ORACLE_SO)
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        L.or_blake2b.argtypes = [vp, sz, vp, sz]
+        L.or_blake2b256.argtypes = [vp, sz, vp]
+        L.or_sha256.argtypes = [vp, sz, vp]
+        L.or_salamander_key.argtypes = [vp, sz, vp, vp]
+        L.or_xplus_key.argtypes = [vp, sz, vp, vp]
+        L.or_salamander_write.argtypes = [vp, sz, vp, vp, sz, vp]
+        L.or_salamander_write.restype = ctypes.c_long
+        L.or_salamander_read.argtypes = [vp, sz, vp, sz]
+        L.or_salamander_read.restype = ctypes.c_long
+        L.or_salamander_write_inplace.argtypes = [vp, sz, vp, vp, sz]
+        L.or_salamander_write_inplace.restype = ctypes.c_long
+        L.or_salamander_write_vectorised.argtypes = [vp, sz, vp, vp, vp, sz]
+        L.or_xplus_write.argtypes = [vp, sz, vp, vp, sz, vp]
+        L.or_xplus_write.restype = ctypes.c_long
+        L.or_xplus_read.argtypes = [vp, sz, vp, sz, sz]
+        L.or_xplus_read.restype = ctypes.c_long
+        L.or_xplus_write_vectorised.argtypes = [vp, sz, vp, vp, vp, sz]
+        L.or_xplus_write_vectorised.restype = None
+        L.or_batch_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(OrPsks),
+                                   ctypes.POINTER(OrBatch), ctypes.c_int]
+        L.or_fnv64.argtypes = [vp, sz, ctypes.c_uint64]
+        L.or_fnv64.restype = ctypes.c_uint64
+        _lib = L
+    return _lib
+
+
+def _buf(b: bytes):
+    return ctypes.create_string_buffer(b, max(len(b), 1))
+
+
+def blake2b(msg: bytes, outlen: int = 32) -> bytes:
+    out = ctypes.create_string_buffer(outlen)
+    lib().or_blake2b(_buf(msg), len(msg), out, outlen)
+    return out.raw
+
+
+def sha256(msg: bytes) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    lib().or_sha256(_buf(msg), len(msg), out)
+    return out.raw
+
+
+def salamander_key(psk: bytes, salt: bytes) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    lib().or_salamander_key(_buf(psk), len(psk), _buf(salt), out)
+    return out.raw
+
+
+def xplus_key(psk: bytes, salt: bytes) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    lib().or_xplus_key(_buf(psk), len(psk), _buf(salt), out)
+    return out.raw
+
+
+def salamander_write(psk: bytes, salt: bytes, p: bytes) -> tuple[bytes, int]:
+    wire = ctypes.create_string_buffer(len(p) + 8)
+    r = lib().or_salamander_write(_buf(psk), len(psk), _buf(salt), _buf(p), len(p), wire)
+    return wire.raw, r
+
+
+def salamander_read(psk: bytes, dgram: bytes) -> tuple[bytes, int]:
+    b = _buf(dgram)
+    r = lib().or_salamander_read(_buf(psk), len(psk), b, len(dgram))
+    return b.raw[:len(dgram)], r
+
+
+def xplus_write(psk: bytes, salt: bytes, p: bytes) -> tuple[bytes, int]:
+    wire = ctypes.create_string_buffer(len(p) + 16)
+    r = lib().or_xplus_write(_buf(psk), len(psk), _buf(salt), _buf(p), len(p), wire)
+    return wire.raw, r
+
+
+def xplus_read(psk: bytes, full: bytes, n: int) -> tuple[bytes, int]:
+    b = _buf(full)
+    r = lib().or_xplus_read(_buf(psk), len(psk), b, n, len(full))
+    return b.raw[:len(full)], r
+
+
+def _vectorised(fn, psk: bytes, salt: bytes, bufs: list[bytes]):
+    cb = [_buf(x) for x in bufs]
+    arr = (ctypes.c_void_p * max(len(cb), 1))(*[ctypes.addressof(c) for c in cb])
+    lens = (ctypes.c_size_t * max(len(cb), 1))(*[len(x) for x in bufs])
+    r = fn(_buf(psk), len(psk), _buf(salt), arr, lens, len(bufs))
+    return [c.raw[:len(x)] for c, x in zip(cb, bufs)], r
+
+
+def salamander_write_vectorised(psk, salt, bufs):
+    out, r = _vectorised(lib().or_salamander_write_vectorised, psk, salt, bufs)
+    return out, r != 0
+
+
+def xplus_write_vectorised(psk, salt, bufs):
+    out, _ = _vectorised(lib().or_xplus_write_vectorised, psk, salt, bufs)
+    return out
+
+
+def psk_table(psks: list[bytes]):
+    blob = np.frombuffer(b"".join(psks) + b"\0", dtype=np.uint8).copy()
+    lens = np.array([len(p) for p in psks], dtype=np.uint32)
+    offs = np.zeros(len(psks), dtype=np.uint64)
+    if len(psks) > 1:
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    keep = (blob, offs, lens)
+    t = OrPsks(blob.ctypes.data, offs.ctypes.data, lens.ctypes.data, len(psks))
+    return t, keep
+
+
+def batch_run(kind: int, direction: int, psks: list[bytes], hb, nthreads: int = 1) -> None:
+    """Run the batch restatement over a sqobfs.HostBatch-shaped object."""
+    t, keep = psk_table(psks)
+
+    def p(a):
+        return None if a is None else a.ctypes.data
+
+    b = OrBatch(hb.n, p(hb.data), p(hb.in_off), p(hb.in_len), p(hb.out), p(hb.out_off),
+                p(hb.out_len), p(hb.salt), p(hb.psk_id), p(hb.in_cap))
+    st = lib().or_batch_run(kind, direction, ctypes.byref(t), ctypes.byref(b), nthreads)
+    del keep
+    if st != 0:
+        raise RuntimeError(f"or_batch_run failed: {st}")
+
+
+def fnv64(a: np.ndarray, h: int = 0) -> int:
+    return lib().or_fnv64(a.ctypes.data, a.nbytes, h)

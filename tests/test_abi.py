@@ -1,0 +1,80 @@
+"""CPU-side checks of the C-ABI boundary (no compute calls, no GPU needed)."""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+import sqobfs
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_header_symbol():
+    L = sqobfs.lib()
+    syms = sqobfs.header_symbols()
+    assert len(syms) >= 18
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+    # exported with C linkage (unmangled) in the dynamic symbol table
+    nm = subprocess.run(["nm", "-D", "--defined-only", sqobfs.LIB_PATH], capture_output=True,
+                        text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (sqobfs_\w+)", nm))
+    assert set(syms) <= exported, set(syms) - exported
+
+
+def test_header_is_plain_c():
+    """The boundary header compiles as C99 with no HIP/torch types."""
+    src = open(sqobfs.HEADER_PATH).read()
+    assert "hip" not in re.sub(r"/\*.*?\*/", "", src, flags=re.S).lower()
+    out = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-fsyntax-only", "-x", "c",
+                          sqobfs.HEADER_PATH], capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+
+
+def test_batch_struct_layout_matches_header():
+    """ctypes mirror of sqobfs_batch has the C layout (offsetof via gcc)."""
+    prog = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "sqobfs.h"
+int main(void){printf("%zu %zu %zu %zu %zu\n", sizeof(sqobfs_batch),
+ offsetof(sqobfs_batch,in), offsetof(sqobfs_batch,out_len), offsetof(sqobfs_batch,psk_id),
+ offsetof(sqobfs_batch,in_cap));return 0;}'''
+    exe = "/tmp/sq_layout_probe"
+    subprocess.run(["gcc", "-x", "c", "-", "-I", os.path.join(REPO, "include"), "-o", exe],
+                   input=prog, text=True, check=True)
+    got = [int(x) for x in subprocess.run([exe], capture_output=True, text=True).stdout.split()]
+    B = sqobfs.Batch
+    assert got == [ctypes.sizeof(B), B.in_.offset, B.out_len.offset, B.psk_id.offset,
+                   B.in_cap.offset]
+
+
+def test_abi_version_and_strerror():
+    L = sqobfs.lib()
+    assert L.sqobfs_abi_version() == 1
+    for st in (0, -1, -2, -3, -4, -5):
+        assert sqobfs.strerror(st) != "unknown status"
+
+
+def test_null_arguments_rejected_without_gpu():
+    L = sqobfs.lib()
+    assert L.sqobfs_open(0, None) == sqobfs.SQ_EINVAL
+    assert L.sqobfs_sync(None, None) == sqobfs.SQ_EINVAL
+    b = sqobfs.Batch()
+    assert L.sqobfs_launch(None, None, 0, ctypes.byref(b), None) == sqobfs.SQ_EINVAL
+    assert L.sqobfs_run_host(None, None, 0, ctypes.byref(b)) == sqobfs.SQ_EINVAL
+    assert L.sqobfs_keyring_create(None, 0, 1, None, None, None, None) == sqobfs.SQ_EINVAL
+
+
+@pytest.mark.skipif(os.environ.get("SQ_ASSUME_GPU") == "1", reason="GPU box")
+def test_no_gpu_reports_enodev_not_fallback():
+    """Without a GPU the product fails loudly (no CPU fallback)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(sqobfs.SqError) as e:
+        sqobfs.Context(0)
+    assert e.value.status == sqobfs.SQ_ENODEV

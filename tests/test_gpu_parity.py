@@ -1,0 +1,244 @@
+"""Parity of the gfx950 path (through the C ABI) with the CPU oracle.
+
+Bit-exact comparison of every output byte (including the bytes around each
+packet's output region, which must stay untouched) and every out_len, on
+seeded inputs: golden vectors, ragged batches, unaligned offsets, in-place
+layouts, multi-PSK keyrings, the reference's short-datagram and XPlus
+read-buffer quirks.  Full BASELINE sizes are covered in test_gpu_fullsize.py.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import sqobfs
+from sqobfs import DEOBFUSCATE, OBFUSCATE, SALAMANDER, XPLUS
+
+import gpu_harness as gh
+
+pytestmark = pytest.mark.gpu
+
+KINDS = [SALAMANDER, XPLUS]
+DIRS = [OBFUSCATE, DEOBFUSCATE]
+PSK = b"sing-quic-mi355x-bench-psk"
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    c = sqobfs.Context(0)
+    yield c
+    c.close()
+
+
+def check(ctx, kind, direction, psks, hb, what, path="device"):
+    ref = gh.run_oracle(kind, direction, psks, hb)
+    with sqobfs.Keyring(ctx, kind, psks) as kr:
+        if path == "device":
+            gh.run_device(ctx, kr, direction, hb)
+        else:
+            gh.run_host(ctx, kr, direction, hb)
+    gh.assert_same(hb, ref, what)
+
+
+# ---------------------------------------------------------------- golden
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_golden_write_vectors(ctx, golden, kind):
+    """All golden write vectors in ONE batch: one keyring entry per vector
+    (PSK lengths 0..300), psk_id per packet."""
+    vs = golden("salamander_write.json" if kind == SALAMANDER else "xplus_write.json")
+    psks = [bytes.fromhex(v["psk"]) for v in vs]
+    pays = [bytes.fromhex(v["payload"]) for v in vs]
+    S = sqobfs.SALT_LEN[kind]
+    data, off, ln = sqobfs.pack(pays)
+    oo, end = gh._place([S + len(p) for p in pays], 16, 0)
+    out = np.full(end + 64, gh.SENTINEL, np.uint8)
+    salt = np.frombuffer(b"".join(bytes.fromhex(v["salt"]) for v in vs), np.uint8).copy()
+    hb = sqobfs.HostBatch(data, off, ln, out, oo, np.zeros(len(vs), np.uint32), salt,
+                          np.arange(len(vs), dtype=np.uint16))
+    with sqobfs.Keyring(ctx, kind, psks) as kr:
+        gh.run_device(ctx, kr, OBFUSCATE, hb)
+    for i, v in enumerate(vs):
+        w = bytes.fromhex(v["wire"])
+        assert hb.out[int(oo[i]):int(oo[i]) + len(w)].tobytes() == w, f"vector {i}"
+        assert hb.out_len[i] == len(w)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_golden_read_vectors(ctx, golden, kind):
+    vs = golden("salamander_read.json" if kind == SALAMANDER else "xplus_read.json")
+    S = sqobfs.SALT_LEN[kind]
+    full = [bytes.fromhex(v.get("buffer_full", v["datagram"])) for v in vs]
+    dl = [len(bytes.fromhex(v["datagram"])) for v in vs]
+    data, off, _ = sqobfs.pack(full)
+    caps = np.array([len(f) for f in full], np.uint32)
+    osz = [gh.out_size(kind, DEOBFUSCATE, n, c) for n, c in zip(dl, caps)]
+    oo, end = gh._place(osz, 16, 0)
+    out = np.full(end + 64, gh.SENTINEL, np.uint8)
+    hb = sqobfs.HostBatch(data, off, np.array(dl, np.uint32), out, oo,
+                          np.zeros(len(vs), np.uint32), None, None,
+                          caps if kind == XPLUS else None)
+    with sqobfs.Keyring(ctx, kind, [bytes.fromhex(vs[0]["psk"])]) as kr:
+        gh.run_device(ctx, kr, DEOBFUSCATE, hb)
+    for i, v in enumerate(vs):
+        after = bytes.fromhex(v["buffer_after"])
+        ret = v["read_ret"]
+        assert hb.out_len[i] == ret, f"vector {i}"
+        # product output = what ReadFrom leaves in p[0 : out region)
+        got = hb.out[int(oo[i]):int(oo[i]) + osz[i]].tobytes()
+        assert got == after[:osz[i]], f"vector {i}"
+
+
+def test_survey_examples(ctx, golden):
+    for ex in golden("survey_examples.json"):
+        kind = SALAMANDER if ex["kind"] == "salamander" else XPLUS
+        pay = bytes.fromhex(ex["payload"])
+        data, off, ln = sqobfs.pack([pay])
+        S = sqobfs.SALT_LEN[kind]
+        out = np.zeros(S + len(pay) + 64, np.uint8)
+        hb = sqobfs.HostBatch(data, off, ln, out, np.zeros(1, np.uint64), np.zeros(1, np.uint32),
+                              np.frombuffer(bytes.fromhex(ex["salt"]), np.uint8).copy())
+        with sqobfs.Keyring(ctx, kind, [bytes.fromhex(ex["psk"])]) as kr:
+            gh.run_host(ctx, kr, OBFUSCATE, hb)
+        assert out[:S + len(pay)].tobytes().hex() == ex["wire"]
+
+
+# ---------------------------------------------------------------- ragged
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("direction", DIRS)
+@pytest.mark.parametrize("dist", ["tiny", "mixed", "mtu"])
+def test_ragged_single_psk(ctx, kind, direction, dist):
+    rng = np.random.Generator(np.random.PCG64(100 + 10 * kind + direction))
+    n = {"tiny": 3000, "mixed": 2500, "mtu": 700}[dist]
+    lo, hi = {"tiny": (0, 70), "mixed": (0, 1500), "mtu": (1200, 1500)}[dist]
+    lens = rng.integers(lo, hi + 1, n)
+    hb = gh.make_case(rng, kind, direction, lens, [PSK])
+    check(ctx, kind, direction, [PSK], hb, f"{kind}/{direction}/{dist}")
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("direction", DIRS)
+@pytest.mark.parametrize("in_align,in_lead,out_align,out_lead",
+                         [(1, 0, 1, 0), (1, 3, 16, 0), (16, 0, 1, 5), (16, 8, 16, 8),
+                          (16, 4, 16, 12), (4, 0, 8, 0)])
+def test_unaligned_layouts(ctx, kind, direction, in_align, in_lead, out_align, out_lead):
+    rng = np.random.Generator(np.random.PCG64(7 + in_align + in_lead * 3 + out_lead))
+    lens = np.concatenate([np.arange(0, 80), rng.integers(0, 1500, 400)])
+    hb = gh.make_case(rng, kind, direction, lens, [PSK], in_align=in_align, in_lead=in_lead,
+                      out_align=out_align, out_lead=out_lead, gaps=True)
+    check(ctx, kind, direction, [PSK], hb, "unaligned")
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("direction", DIRS)
+def test_in_place(ctx, kind, direction):
+    """Headroom layout (obfs) / decode at +S (deobfs): output over input."""
+    rng = np.random.Generator(np.random.PCG64(55 + kind + direction))
+    lens = np.concatenate([np.arange(0, 70), rng.integers(0, 1500, 600)])
+    hb = gh.make_case(rng, kind, direction, lens, [PSK], inplace=True)
+    check(ctx, kind, direction, [PSK], hb, "in place")
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("direction", DIRS)
+def test_multi_psk_256(ctx, kind, direction):
+    """Config-5 shape: 256 PSKs of length U[8,64] (some cross SHA-256's
+    39-byte two-block boundary), psk_id = i mod 256."""
+    rng = np.random.Generator(np.random.PCG64(3))
+    psks = [rng.integers(0, 256, int(k), dtype=np.uint8).tobytes()
+            for k in rng.integers(8, 65, 256)]
+    n = 3000
+    ids = (np.arange(n) % 256).astype(np.uint16)
+    lens = rng.integers(0, 1460, n)
+    hb = gh.make_case(rng, kind, direction, lens, psks, psk_ids=ids)
+    check(ctx, kind, direction, psks, hb, "multi psk")
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_long_and_empty_psks(ctx, kind):
+    psks = [b"", b"x", b"y" * 39, b"z" * 40, b"w" * 120, b"v" * 121, b"u" * 128,
+            b"t" * 255, b"s" * 1000]
+    rng = np.random.Generator(np.random.PCG64(11))
+    n = 900
+    ids = rng.integers(0, len(psks), n).astype(np.uint16)
+    for direction in DIRS:
+        hb = gh.make_case(rng, kind, direction, rng.integers(0, 400, n), psks, psk_ids=ids)
+        check(ctx, kind, direction, psks, hb, "long psk")
+
+
+def test_xplus_read_buffer_quirk(ctx):
+    """xplus.go:55 XORs up to len(p) - 16, not n - 16."""
+    rng = np.random.Generator(np.random.PCG64(12))
+    n = 800
+    lens = rng.integers(0, 1300, n)
+    extra = rng.integers(0, 700, n)
+    hb = gh.make_case(rng, XPLUS, DEOBFUSCATE, lens, [PSK], cap_extra=extra)
+    check(ctx, XPLUS, DEOBFUSCATE, [PSK], hb, "xplus cap")
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("direction", DIRS)
+def test_host_staged_path(ctx, kind, direction):
+    rng = np.random.Generator(np.random.PCG64(21 + kind + 2 * direction))
+    lens = rng.integers(0, 1500, 1500)
+    hb = gh.make_case(rng, kind, direction, lens, [PSK], in_align=1, out_align=1)
+    check(ctx, kind, direction, [PSK], hb, "host path", path="host")
+
+
+def test_empty_batch_and_zero_length(ctx):
+    with sqobfs.Keyring(ctx, SALAMANDER, [PSK]) as kr:
+        b = sqobfs.Batch()
+        sqobfs.launch(ctx, kr, OBFUSCATE, b)
+        ctx.sync()
+    rng = np.random.Generator(np.random.PCG64(1))
+    for kind in KINDS:
+        for direction in DIRS:
+            hb = gh.make_case(rng, kind, direction, [0] * 130, [PSK])
+            check(ctx, kind, direction, [PSK], hb, "zero length")
+
+
+def test_bad_psk_id_marked_and_untouched(ctx):
+    rng = np.random.Generator(np.random.PCG64(2))
+    hb = gh.make_case(rng, SALAMANDER, OBFUSCATE, [100] * 70, [PSK], psk_ids=[0] * 70)
+    hb.psk_id[5] = 9
+    before = hb.out.copy()
+    with sqobfs.Keyring(ctx, SALAMANDER, [PSK, b"second"]) as kr:
+        gh.run_device(ctx, kr, OBFUSCATE, hb)
+        assert hb.out_len[5] == sqobfs.BAD_PSK
+        o = int(hb.out_off[5])
+        assert np.array_equal(hb.out[o:o + 108], before[o:o + 108])
+        with pytest.raises(sqobfs.SqError) as e:
+            gh.run_host(ctx, kr, OBFUSCATE, hb)
+        assert e.value.status == sqobfs.SQ_EPSK
+
+
+def test_kind_mismatch_rejected(ctx):
+    import ctypes
+    with sqobfs.Keyring(ctx, XPLUS, [PSK]) as kr:
+        b = sqobfs.Batch()
+        b.n = 1
+        st = sqobfs.lib().sqobfs_salamander_obfuscate(ctx.handle, kr.handle, ctypes.byref(b),
+                                                      None)
+        assert st == sqobfs.SQ_EINVAL
+
+
+def test_round_trip_random(ctx):
+    """obfuscate -> deobfuscate is the identity on the payload (both kinds)."""
+    rng = np.random.Generator(np.random.PCG64(77))
+    for kind in KINDS:
+        S = sqobfs.SALT_LEN[kind]
+        lens = rng.integers(0, 1500, 2000)
+        hb = gh.make_case(rng, kind, OBFUSCATE, lens, [PSK], out_align=1)
+        with sqobfs.Keyring(ctx, kind, [PSK]) as kr:
+            gh.run_device(ctx, kr, OBFUSCATE, hb)
+            osz = [gh.out_size(kind, DEOBFUSCATE, S + int(L), S + int(L)) for L in lens]
+            oo, end = gh._place(osz, 1, 3)
+            back = sqobfs.HostBatch(hb.out, hb.out_off, hb.out_len.copy(),
+                                    np.zeros(end + 64, np.uint8), oo,
+                                    np.zeros(len(lens), np.uint32))
+            gh.run_device(ctx, kr, DEOBFUSCATE, back)
+        for i, L in enumerate(lens):
+            a, b = int(hb.in_off[i]), int(oo[i])
+            assert back.out[b:b + int(L)].tobytes() == hb.data[a:a + int(L)].tobytes()
