@@ -77,12 +77,13 @@ def build_shard(torch, dev, kind, n, L, n_psk, rank, world, config):
         lens = torch.randint(64, 1453, (n,), generator=g, device=dev, dtype=torch.int64)
     else:
         lens = torch.full((n,), L, device=dev, dtype=torch.int64)
+    lead = 64  # buffers start with 64 spare bytes (slack for timing probes)
     in_slot = (lens + 15) // 16 * 16
-    in_off = torch.cumsum(in_slot, 0) - in_slot
+    in_off = torch.cumsum(in_slot, 0) - in_slot + lead
     out_slot = (lens + S + 15) // 16 * 16
-    out_off = torch.cumsum(out_slot, 0) - out_slot
-    in_bytes = int(in_slot.sum().item())
-    out_bytes = int(out_slot.sum().item())
+    out_off = torch.cumsum(out_slot, 0) - out_slot + lead
+    in_bytes = int(in_slot.sum().item()) + 2 * lead
+    out_bytes = int(out_slot.sum().item()) + 2 * lead
     data = torch.randint(0, 256, (in_bytes,), generator=g, device=dev, dtype=torch.uint8)
     salt = torch.randint(0, 256, (n * S,), generator=g, device=dev, dtype=torch.uint8)
     out = torch.zeros(out_bytes, device=dev, dtype=torch.uint8)

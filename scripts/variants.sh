@@ -1,0 +1,12 @@
+#!/bin/bash
+# Build timing variants of libsqobfs.so: scripts/variants.sh name:"-DFLAGS" ...
+set -e
+cd "$(dirname "$0")/.."
+mkdir -p build/var
+for spec in "$@"; do
+  name=${spec%%:*}; flags=${spec#*:}
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $flags -Iinclude \
+    -Ising-quic_amd/csrc -shared -o build/var/lib_$name.so \
+    sing-quic_amd/csrc/sq_kernels.hip sing-quic_amd/csrc/sq_api.hip &
+done
+wait

@@ -37,8 +37,47 @@
 namespace sq {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 // dword-aligned 16-byte access: still one global_load_dwordx4 on gfx950
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+// Global-address-space accessors.  Packet addresses are computed as integers;
+// a plain cast would give FLAT pointers, whose loads/stores count in both
+// vmcnt and lgkmcnt and force the compiler to drain every outstanding store
+// before each LDS read (one full HBM round trip per loop iteration).
+#define SQ_GLOBAL __attribute__((address_space(1)))
+template <typename T>
+__device__ __forceinline__ T gld(uint64_t a) {
+  return *(const SQ_GLOBAL T *)a;
+}
+template <typename T>
+__device__ __forceinline__ void gst(uint64_t a, T v) {
+  *(SQ_GLOBAL T *)a = v;
+}
+
+// Streaming policy of the bulk chunk loads / stores (SQ_NT bit 0: loads,
+// bit 1: stores).  Payload bytes are touched exactly once, so nontemporal
+// (`nt`) accesses keep them from displacing useful L2 lines.
+#ifndef SQ_NT
+#define SQ_NT 3
+#endif
+#ifndef SQ_U
+#define SQ_U 8
+#endif
+
+
+// Timing-only ablation builds (scripts/ablate.sh; never the shipped .so):
+// 1 = skip edge chunks, 2 = skip key derivation, 3 = skip the chunk stream,
+// 4 = skip edges and key derivation.
+#ifndef SQ_ABLATE
+#define SQ_ABLATE 0
+#endif
+#ifndef SQ_ROLL
+#define SQ_ROLL 0
+#endif
+#ifndef SQ_EXP_FULL
+#define SQ_EXP_FULL 0
+#endif
 
 constexpr uint32_t kMaxPacket = 1u << 26;  // per-packet length bound (u32 chunk math)
 constexpr uint32_t kBadPsk = 0xFFFFFFFFu;
@@ -109,9 +148,9 @@ __device__ __forceinline__ uint32_t pick4(const uint32_t (&v)[4], uint32_t i) {
 __device__ __forceinline__ void load_window(uint64_t ps, uint64_t pe,
                                             uint64_t X, uint32_t (&out)[4]) {
   const uint64_t B0 = ps & ~15ull;
-  const u32x4 v0 = *reinterpret_cast<const u32x4 *>(B0);
+  const u32x4 v0 = gld<u32x4>(B0);
   u32x4 v1 = {0u, 0u, 0u, 0u};
-  if (pe > B0 + 16) v1 = *reinterpret_cast<const u32x4 *>(B0 + 16);
+  if (pe > B0 + 16) v1 = gld<u32x4>(B0 + 16);
   const uint32_t w[12] = {0u,   0u,   0u,   0u,   v0.x, v0.y,
                           v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
   win16(w, (uint32_t)(X - B0 + 16), out);
@@ -123,40 +162,40 @@ __device__ __forceinline__ void store_partial(uint64_t A, const uint32_t (&v)[4]
                                               uint32_t a, uint32_t b) {
   uint32_t pos = a;
   if ((pos & 1) && pos + 1 <= b) {
-    *reinterpret_cast<uint8_t *>(A + pos) = (uint8_t)(pick4(v, pos >> 2) >> (8 * (pos & 3)));
+    gst<uint8_t>(A + pos, (uint8_t)(pick4(v, pos >> 2) >> (8 * (pos & 3))));
     pos += 1;
   }
   if ((pos & 2) && pos + 2 <= b) {
-    *reinterpret_cast<uint16_t *>(A + pos) = (uint16_t)(pick4(v, pos >> 2) >> (8 * (pos & 2)));
+    gst<uint16_t>(A + pos, (uint16_t)(pick4(v, pos >> 2) >> (8 * (pos & 2))));
     pos += 2;
   }
   if ((pos & 4) && pos + 4 <= b) {
-    *reinterpret_cast<uint32_t *>(A + pos) = pick4(v, pos >> 2);
+    gst<uint32_t>(A + pos, pick4(v, pos >> 2));
     pos += 4;
   }
   if ((pos & 8) && pos + 8 <= b) {
-    *reinterpret_cast<uint2 *>(A + 8) = make_uint2(v[2], v[3]);
+    gst<u32x2>(A + 8, u32x2{v[2], v[3]});
     pos += 8;
   }
   if (pos == 0 && b == 16) {
-    *reinterpret_cast<u32x4 *>(A) = u32x4{v[0], v[1], v[2], v[3]};
+    gst<u32x4>(A, u32x4{v[0], v[1], v[2], v[3]});
     pos = 16;
   }
   if (pos + 8 <= b) {  // pos is 0 or 8 here
     const bool hi = pos & 8;
-    *reinterpret_cast<uint2 *>(A + pos) = make_uint2(bsel(hi, v[2], v[0]), bsel(hi, v[3], v[1]));
+    gst<u32x2>(A + pos, u32x2{bsel(hi, v[2], v[0]), bsel(hi, v[3], v[1])});
     pos += 8;
   }
   if (pos + 4 <= b) {
-    *reinterpret_cast<uint32_t *>(A + pos) = pick4(v, pos >> 2);
+    gst<uint32_t>(A + pos, pick4(v, pos >> 2));
     pos += 4;
   }
   if (pos + 2 <= b) {
-    *reinterpret_cast<uint16_t *>(A + pos) = (uint16_t)(pick4(v, pos >> 2) >> (8 * (pos & 2)));
+    gst<uint16_t>(A + pos, (uint16_t)(pick4(v, pos >> 2) >> (8 * (pos & 2))));
     pos += 2;
   }
   if (pos + 1 <= b) {
-    *reinterpret_cast<uint8_t *>(A + pos) = (uint8_t)(pick4(v, pos >> 2) >> (8 * (pos & 3)));
+    gst<uint8_t>(A + pos, (uint8_t)(pick4(v, pos >> 2) >> (8 * (pos & 3))));
   }
 }
 
@@ -273,7 +312,7 @@ __device__ __forceinline__ void edge_span(const PacketJob &J, const uint32_t (&k
   }
 }
 
-// ------------------------------------------------------------ main kernel
+// ------------------------------------------------------------ chunk stream
 
 // LDS record per packet (48 B): input/output addressing for flat chunk c
 // (addr = base + 16*c) and the keystream for even / odd c.
@@ -281,6 +320,154 @@ struct alignas(16) ChunkRec {
   uint64_t ssub, dsub;
   u32x4 ks[2];
 };
+
+// Packet owning flat chunk c = b0 + lane (c < T): the last lane l with
+// start[l] <= c.  b0 is wave-uniform, so this is two ballots, a popcount and
+// a scalar walk over the (few) packets that start inside the 64-chunk window.
+// Always returns a valid record index (0..63), also for c >= T.
+__device__ __forceinline__ uint32_t locate(uint32_t start, uint32_t b0, uint32_t c) {
+  int pp = __popcll(__ballot(start <= b0)) - 1;
+  uint64_t M = __ballot(start > b0 && start < b0 + kWave);
+  while (M) {
+    const int l = __ffsll((unsigned long long)M) - 1;
+    M &= M - 1;
+    const uint32_t sl = __builtin_amdgcn_readlane(start, l);
+    pp += c >= sl ? 1 : 0;
+  }
+  return (uint32_t)pp;
+}
+
+// Buffer-resource streaming.  The wave's input and output spans (all its
+// full chunks) each fit a 32-bit buffer range, described by one SGPR
+// resource per direction.  A chunk past the end gets an offset beyond
+// num_records: the hardware range check returns zeros for its load and
+// drops its store.  So every load/store in the loop is unconditional, with
+// no padding writes and no branches, and the compiler's waitcnt accounting
+// stays exact (a conditional store makes it fall back to draining).
+constexpr uint32_t kOffNone = 0xFFFFFFF0u;
+constexpr int kAuxLd = (SQ_NT & 1) ? 2 : 0;  // nt
+constexpr int kAuxSt = (SQ_NT & 2) ? 2 : 0;
+
+struct WaveBufs {
+  __amdgpu_buffer_rsrc_t src, dst;
+  uint32_t sbase, dbase;  // low 32 bits of the span bases
+};
+
+__device__ __forceinline__ uint32_t src_off(const ChunkRec *wrec, const WaveBufs &B,
+                                            uint32_t pp, uint32_t c, uint32_t T) {
+  return c < T ? (uint32_t)wrec[pp].ssub - B.sbase + 16u * c : kOffNone;
+}
+
+template <int U>
+__device__ __forceinline__ void stream_issue(const ChunkRec *wrec, const WaveBufs &B,
+                                             uint32_t start, uint32_t T, uint32_t lane,
+                                             uint32_t base, u32x4 (&v)[U], uint32_t (&pp)[U]) {
+  uint32_t off[U];
+  // all packet lookups (SALU + ballots) first, then all LDS reads, then all
+  // loads: one LDS round trip per step instead of one per chunk
+#pragma unroll
+  for (int u = 0; u < U; u++) pp[u] = locate(start, base + u * kWave, base + u * kWave + lane);
+#pragma unroll
+  for (int u = 0; u < U; u++) off[u] = src_off(wrec, B, pp[u], base + u * kWave + lane, T);
+#pragma unroll
+  for (int u = 0; u < U; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b128(B.src, off[u], 0, kAuxLd);
+}
+
+__device__ __forceinline__ void store_chunk(const ChunkRec *wrec, const WaveBufs &B,
+                                            uint32_t pp, uint32_t c, uint32_t T, u32x4 v) {
+  const ChunkRec &R = wrec[pp];
+  const uint32_t off = c < T ? (uint32_t)R.dsub - B.dbase + 16u * c : kOffNone;
+  __builtin_amdgcn_raw_buffer_store_b128(v ^ R.ks[c & 1], B.dst, off, 0, kAuxSt);
+}
+
+// Double-buffered: the U loads of step i+1 are issued before step i is
+// XORed and stored, so each wave keeps U..2U KiB of reads outstanding.
+template <int U>
+__device__ __forceinline__ void stream_dbuf(const ChunkRec *wrec, const WaveBufs &B,
+                                            uint32_t start, uint32_t T, uint32_t lane) {
+  constexpr uint32_t STEP = kWave * U;
+  u32x4 cur[U];
+  uint32_t cpp[U];
+  stream_issue<U>(wrec, B, start, T, lane, 0, cur, cpp);
+  for (uint32_t base = 0; base < T; base += STEP) {
+    u32x4 nxt[U];
+    uint32_t npp[U];
+    stream_issue<U>(wrec, B, start, T, lane, base + STEP, nxt, npp);
+#pragma unroll
+    for (int u = 0; u < U; u++) store_chunk(wrec, B, cpp[u], base + u * kWave + lane, T, cur[u]);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      cur[u] = nxt[u];
+      cpp[u] = npp[u];
+    }
+  }
+}
+
+// Rolling: slot u owns chunks c = u*64 + lane + k*64U and always has one
+// load in flight; visiting a slot stores its data and re-issues the slot's
+// next load.  U loads outstanding with only 4U data registers.
+template <int U>
+__device__ __forceinline__ void stream_roll(const ChunkRec *wrec, const WaveBufs &B,
+                                            uint32_t start, uint32_t T, uint32_t lane) {
+  constexpr uint32_t STEP = kWave * U;
+  u32x4 cur[U];
+  uint32_t cpp[U];
+  stream_issue<U>(wrec, B, start, T, lane, 0, cur, cpp);
+  for (uint32_t base = 0; base < T; base += STEP) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t c = base + u * kWave + lane;
+      store_chunk(wrec, B, cpp[u], c, T, cur[u]);
+      cpp[u] = locate(start, base + STEP + u * kWave, c + STEP);
+      cur[u] = __builtin_amdgcn_raw_buffer_load_b128(B.src, src_off(wrec, B, cpp[u], c + STEP, T),
+                                                     0, kAuxLd);
+    }
+  }
+}
+
+// Fallback for waves whose spans exceed a 32-bit buffer range or whose
+// input chunks are not 4-byte aligned: global accesses, any alignment
+// (two aligned 16-byte loads + byte funnel per chunk), one chunk per lane.
+__device__ __noinline__ void stream_generic(const ChunkRec *wrec, uint32_t start, uint32_t T,
+                                            uint32_t lane) {
+  for (uint32_t b0 = 0; b0 < T; b0 += kWave) {
+    const uint32_t c = min(b0 + lane, T - 1);
+    const ChunkRec &R = wrec[locate(start, b0, c)];
+    const uint64_t sa = R.ssub + 16ull * c;
+    uint32_t w[4];
+    if ((sa & 3) == 0) {
+      const u32x4 x = gld<u32x4_a4>(sa);
+      w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
+    } else {
+      load_window(sa, sa + 16, sa, w);
+    }
+    if (b0 + lane < T) gst<u32x4>(R.dsub + 16ull * c, u32x4{w[0], w[1], w[2], w[3]} ^ R.ks[c & 1]);
+  }
+}
+
+// 64-bit wave min / max (butterfly), result wave-uniform.
+__device__ __forceinline__ uint64_t wave_min64(uint64_t x) {
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const uint64_t y = __shfl_xor((unsigned long long)x, d, kWave);
+    x = y < x ? y : x;
+  }
+  return x;
+}
+__device__ __forceinline__ uint64_t wave_max64(uint64_t x) {
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const uint64_t y = __shfl_xor((unsigned long long)x, d, kWave);
+    x = y > x ? y : x;
+  }
+  return x;
+}
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+  return b2_pack(__builtin_amdgcn_readfirstlane((uint32_t)x),
+                 __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)));
+}
+
+// ------------------------------------------------------------ main kernel
 
 template <int KIND, int DIR, bool MULTI, int U>
 __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
@@ -345,6 +532,9 @@ __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
 
   // ---- 2. key (lane-parallel: one packet per lane)
   uint32_t key[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+#if SQ_ABLATE == 2 || SQ_ABLATE == 4  // timing-only build: no key derivation
+  if (do_hash) { key[0] = salt[0]; key[1] = salt[1]; do_hash = false; }
+#endif
   if (do_hash) {
     if (KIND == 0) salamander_key(E, salt, key);
     else xplus_key(E, salt, key);
@@ -352,7 +542,11 @@ __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
 
   // ---- 3. split into full chunks (flat, streamed) and edges (owner lane)
   const uint64_t rs = J.dst_pay - J.pre, re = J.dst_pay + J.len;
+#if SQ_EXP_FULL  // timing-only: stream every output chunk as a full 16-byte store
+  const uint64_t fa = rs & ~15ull, fb = (re + 15) & ~15ull;
+#else
   const uint64_t fa = (J.dst_pay + 15) & ~15ull, fb = re & ~15ull;
+#endif
   const uint32_t F = (J.len && fb > fa) ? (uint32_t)((fb - fa) >> 4) : 0u;
   uint32_t incl = F;
 #pragma unroll
@@ -362,6 +556,7 @@ __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
   }
   const uint32_t start = incl - F;
   const uint32_t T = __shfl(incl, kWave - 1, kWave);
+  const uint64_t s_first = J.src_pay + (fa - J.dst_pay);  // input of the first full chunk
   {
     uint32_t k0[4], k1[4];
     const uint32_t r0 = (uint32_t)(fa - J.dst_pay);  // 0..15
@@ -369,7 +564,7 @@ __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
     keywin(key, r0 + 16, k1);
     const bool odd = start & 1;
     ChunkRec R;
-    R.ssub = J.src_pay + (fa - J.dst_pay) - 16ull * start;
+    R.ssub = s_first - 16ull * start;
     R.dsub = fa - 16ull * start;
     R.ks[0] = u32x4{bsel(odd, k1[0], k0[0]), bsel(odd, k1[1], k0[1]),
                     bsel(odd, k1[2], k0[2]), bsel(odd, k1[3], k0[3])};
@@ -379,7 +574,7 @@ __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
   }
 
   // ---- 4. edges: salt bytes, unaligned head, tail
-  if (re > rs) {
+  if (!SQ_EXP_FULL && SQ_ABLATE != 1 && SQ_ABLATE != 4 && re > rs) {
     if (F) {
       edge_span(J, key, salt, rs, fa);
       edge_span(J, key, salt, fb, re);
@@ -393,44 +588,34 @@ __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
   // ---- 5. stream the flat full-chunk space
-  for (uint32_t base = 0; base < T; base += kWave * U) {
-    uint64_t sa[U], da[U];
-    u32x4 ks[U], v[U];
-    bool ok[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const uint32_t b0 = base + u * kWave;
-      const uint32_t c = b0 + lane;
-      ok[u] = c < T;
-      int pp = __popcll(__ballot(start <= b0)) - 1;
-      uint64_t M = __ballot(start > b0 && start < b0 + kWave);
-      while (M) {
-        const int l = __ffsll((unsigned long long)M) - 1;
-        M &= M - 1;
-        const uint32_t sl = __builtin_amdgcn_readlane(start, l);
-        pp += c >= sl ? 1 : 0;
-      }
-      const ChunkRec &R = recs[wv][pp];
-      sa[u] = R.ssub + 16ull * c;
-      da[u] = R.dsub + 16ull * c;
-      ks[u] = R.ks[c & 1];
-    }
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      if (ok[u]) {
-        if ((sa[u] & 3) == 0) {
-          v[u] = *reinterpret_cast<const u32x4_a4 *>(sa[u]);
-        } else {
-          uint32_t w[4];
-          load_window(sa[u], sa[u] + 16, sa[u], w);
-          v[u] = u32x4{w[0], w[1], w[2], w[3]};
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      if (ok[u]) *reinterpret_cast<u32x4 *>(da[u]) = v[u] ^ ks[u];
-    }
+  if (T == 0 || SQ_ABLATE == 3) return;
+  const ChunkRec *wrec = recs[wv];
+  // wave spans of the full chunks, for the two buffer resources
+  const bool has = F != 0;
+  const uint64_t s_lo = uniform64(wave_min64(has ? s_first : ~0ull));
+  const uint64_t s_hi = uniform64(wave_max64(has ? s_first + 16ull * F : 0ull));
+  const uint64_t d_lo = uniform64(wave_min64(has ? fa : ~0ull));
+  const uint64_t d_hi = uniform64(wave_max64(has ? fb : 0ull));
+  const bool mis = has && (s_first & 3);
+  constexpr uint64_t kMaxSpan = 0xFFFFFF00ull;
+  if (__ballot(mis) == 0 && s_hi - s_lo <= kMaxSpan && d_hi - d_lo <= kMaxSpan) {
+    WaveBufs B;
+    B.src = __builtin_amdgcn_make_buffer_rsrc((void *)s_lo, 0, (int)(uint32_t)(s_hi - s_lo),
+                                              0x00020000);
+    B.dst = __builtin_amdgcn_make_buffer_rsrc((void *)d_lo, 0, (int)(uint32_t)(d_hi - d_lo),
+                                              0x00020000);
+    B.sbase = (uint32_t)s_lo;
+    B.dbase = (uint32_t)d_lo;
+#ifdef SQ_PRIO
+    __builtin_amdgcn_s_setprio(SQ_PRIO);
+#endif
+#if SQ_ROLL
+    stream_roll<U>(wrec, B, start, T, lane);
+#else
+    stream_dbuf<U>(wrec, B, start, T, lane);
+#endif
+  } else {
+    stream_generic(wrec, start, T, lane);
   }
 }
 
@@ -509,7 +694,7 @@ __global__ void psk_prepare_kernel(int kind, const uint8_t *blob, const uint64_t
 
 template <int KIND, int DIR, bool MULTI>
 static int launch_one(const KParams *kp, hipStream_t s) {
-  constexpr int U = 4;
+  constexpr int U = SQ_U;
   const uint64_t blocks = ((uint64_t)kp->n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL((obfs_kernel<KIND, DIR, MULTI, U>), dim3((uint32_t)blocks),
                      dim3(kBlock), 0, s, *kp);

@@ -20,7 +20,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
 REPO = os.path.dirname(PKG)
-LIB_PATH = os.path.join(PKG, "libsqobfs.so")
+LIB_PATH = os.environ.get("SQOBFS_LIB") or os.path.join(PKG, "libsqobfs.so")
 HEADER_PATH = os.path.join(REPO, "include", "sqobfs.h")
 
 SALAMANDER, XPLUS = 0, 1
