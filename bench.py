@@ -57,6 +57,13 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=2.0,
                     help="wall seconds of CPU-baseline sampling (x threads = CPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--layout", default="dense", choices=["dense", "slot16", "inplace"],
+                    help="dense: wire-dense outputs, wire-sized input slots (default); "
+                         "slot16: 16-byte-aligned slots; inplace: obfuscate in the input "
+                         "buffer (headroom layout, vectorised WriteTo semantics)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL) for the timing barrier/max; gloo lets several "
+                         "ranks share one GPU in tests")
     ap.add_argument("--e2e", action="store_true",
                     help="also time the host-staged path (pinned H2D + kernel + D2H)")
     return ap.parse_args()
@@ -66,7 +73,18 @@ def slot(n: int, a: int = 16) -> int:
     return (n + a - 1) // a * a
 
 
-def build_shard(torch, dev, kind, n, L, n_psk, rank, world, config):
+def shard(config, n_total, world, rank):
+    """(packets on this rank, global index of its first packet).  configs[4]
+    is ONE 16M-packet batch split in contiguous shards over the ranks (strong
+    scaling); every other config gives each GPU its own full batch (weak)."""
+    if config == "salamander-16m-256psk":
+        lo = n_total * rank // world
+        hi = n_total * (rank + 1) // world
+        return hi - lo, lo
+    return n_total, rank * n_total
+
+
+def build_shard(torch, dev, kind, n, L, n_psk, rank, world, config, layout, first=0):
     """Synthetic shard in HBM: payload/salt bytes from torch's Philox RNG
     seeded per rank; 16-byte-aligned slots for inputs and outputs."""
     import numpy as np
@@ -77,34 +95,68 @@ def build_shard(torch, dev, kind, n, L, n_psk, rank, world, config):
         lens = torch.randint(64, 1453, (n,), generator=g, device=dev, dtype=torch.int64)
     else:
         lens = torch.full((n,), L, device=dev, dtype=torch.int64)
-    lead = 64  # buffers start with 64 spare bytes (slack for timing probes)
-    in_slot = (lens + 15) // 16 * 16
-    in_off = torch.cumsum(in_slot, 0) - in_slot + lead
-    out_slot = (lens + S + 15) // 16 * 16
-    out_off = torch.cumsum(out_slot, 0) - out_slot + lead
+    lead = 64  # buffers start with 64 spare bytes
+    if layout == "slot16":
+        # every packet in its own 16-byte-aligned slot (pad bytes untouched)
+        in_slot = (lens + 15) // 16 * 16
+        out_slot = (lens + S + 15) // 16 * 16
+        in_off = torch.cumsum(in_slot, 0) - in_slot + lead
+        out_off = torch.cumsum(out_slot, 0) - out_slot + lead
+    else:
+        # wire-dense: datagrams back to back (every output byte written);
+        # each payload sits behind S bytes of headroom in a wire-sized input
+        # slot, like a socket buffer reserved for the salt
+        out_slot = lens + S
+        out_off = torch.cumsum(out_slot, 0) - out_slot + lead
+        in_slot = out_slot
+        in_off = out_off + S
     in_bytes = int(in_slot.sum().item()) + 2 * lead
     out_bytes = int(out_slot.sum().item()) + 2 * lead
     data = torch.randint(0, 256, (in_bytes,), generator=g, device=dev, dtype=torch.uint8)
+    # non-payload input bytes (lead, headroom / slot padding) are zero, so a
+    # decoded batch can be compared with `data` as a whole buffer
+    gap = in_slot - lens
+    gstart = (in_off - S) if layout != "slot16" else (in_off + lens)
+    gidx = torch.repeat_interleave(gstart, gap) + (
+        torch.arange(int(gap.sum().item()), device=dev)
+        - torch.repeat_interleave(torch.cumsum(gap, 0) - gap, gap))
+    data[gidx] = 0
+    data[:lead] = 0
+    data[int((in_off[-1] + lens[-1]).item()):] = 0
     salt = torch.randint(0, 256, (n * S,), generator=g, device=dev, dtype=torch.uint8)
-    out = torch.zeros(out_bytes, device=dev, dtype=torch.uint8)
+    out = data if layout == "inplace" else torch.zeros(out_bytes, device=dev, dtype=torch.uint8)
     # packet index shard: global ids rank*n .. for psk_id = i mod 256
     psk_id = None
     if n_psk > 1:
-        gid = torch.arange(rank * n, (rank + 1) * n, device=dev, dtype=torch.int64)
+        gid = torch.arange(first, first + n, device=dev, dtype=torch.int64)
         psk_id = (gid % n_psk).to(torch.int16)
     rng = np.random.Generator(np.random.PCG64(3))
     psks = [PSK] if n_psk == 1 else [
         rng.integers(0, 256, int(k), dtype=np.uint8).tobytes() for k in rng.integers(8, 65, n_psk)]
     return dict(lens=lens.to(torch.int32), in_off=in_off, out_off=out_off, data=data, salt=salt,
                 out=out, out_len=torch.zeros(n, device=dev, dtype=torch.int32), psk_id=psk_id,
-                psks=psks, S=S, payload_bytes=int(lens.sum().item()))
+                psks=psks, S=S, payload_bytes=int(lens.sum().item()),
+                inplace=layout == "inplace")
 
 
-def spot_check(torch, sh, kind, n, direction_out):
-    """Parity spot check vs the oracle on sampled packets (outside timing)."""
+def sample_idx(n):
+    return sorted(set([0, n - 1] + list(range(0, n, 4099))))[:400]
+
+
+def save_samples(sh, n):
+    """Host copies of the sampled input payloads (before any launch)."""
+    lens = sh["lens"].cpu().numpy()
+    in_off = sh["in_off"].cpu().numpy()
+    return {i: sh["data"][int(in_off[i]):int(in_off[i]) + int(lens[i])].cpu().numpy().tobytes()
+            for i in sample_idx(n)}
+
+
+def spot_check(torch, sh, kind, n, direction_out, saved, launches):
+    """Parity spot check vs the oracle on sampled packets (outside timing).
+    In place, an even number of launches XORs the payload back to itself."""
     import numpy as np
     import oracle_lib as ol
-    idx = sorted(set([0, n - 1] + list(range(0, n, 4099))))[:400]
+    idx = sample_idx(n)
     S = sh["S"]
     lens = sh["lens"].cpu().numpy()
     in_off = sh["in_off"].cpu().numpy()
@@ -114,14 +166,28 @@ def spot_check(torch, sh, kind, n, direction_out):
     write = ol.salamander_write if kind == 0 else ol.xplus_write
     for i in idx:
         L = int(lens[i])
-        p = data[int(in_off[i]):int(in_off[i]) + L].cpu().numpy().tobytes()
+        p = saved[i]
         s = salt[i * S:(i + 1) * S].cpu().numpy().tobytes()
         psk = sh["psks"][int(ids[i]) if ids is not None else 0]
         w, _ = write(psk, s, p)
+        if sh["inplace"] and launches % 2 == 0:
+            w = s + p
         got = out[int(out_off[i]):int(out_off[i]) + L + S].cpu().numpy().tobytes()
         if got != w:
             return False
     return bool((sh["out_len"].cpu().numpy() == lens + S).all())
+
+
+def max_over_ranks(torch, dist, x: float, dev) -> float:
+    t = torch.tensor([x], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(torch, dist, x: float, dev) -> float:
+    t = torch.tensor([x], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
 
 
 def cpu_baseline(seconds: float):
@@ -190,25 +256,31 @@ def main():
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
     dist = None
+    ndev = torch.cuda.device_count()
+    assert ndev > 0, "bench.py needs a GPU"
+    gpu = local % ndev  # several gloo ranks may share a GPU (tests only)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    assert torch.cuda.is_available(), "bench.py needs a GPU"
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group("gloo")
+    dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
 
     kind, n_total, L, n_psk = CONFIGS[args.config]
-    # configs[4] is one 16M batch sharded over the ranks; the rest are per-GPU
-    n = n_total // world if args.config == "salamander-16m-256psk" else n_total
+    n, first = shard(args.config, n_total, world, rank)
     direction = sqobfs.OBFUSCATE if args.direction == "obfuscate" else sqobfs.DEOBFUSCATE
-    sh = build_shard(torch, dev, kind, n, L, n_psk, rank, world, args.config)
+    sh = build_shard(torch, dev, kind, n, L, n_psk, rank, world, args.config, args.layout, first)
     S = sh["S"]
-    ctx = sqobfs.Context(local)
+    ctx = sqobfs.Context(gpu)
     kr = sqobfs.Keyring(ctx, kind, sh["psks"])
     stream = torch.cuda.current_stream(dev)
     s = stream.cuda_stream
 
+    if direction == sqobfs.DEOBFUSCATE and sh["inplace"]:
+        raise SystemExit("--layout inplace is for obfuscate")
     if direction == sqobfs.OBFUSCATE:
         b = sqobfs.make_batch(n, sh["data"], sh["in_off"], sh["lens"], sh["out"], sh["out_off"],
                               sh["out_len"], sh["salt"], sh["psk_id"])
@@ -224,6 +296,7 @@ def main():
                               sh["out_len"], None, sh["psk_id"])
         alg_bytes = 2 * sh["payload_bytes"] + S * n
 
+    saved = save_samples(sh, n) if direction == sqobfs.OBFUSCATE else None
     for _ in range(args.warmup):
         sqobfs.launch(ctx, kr, direction, b, s)
     torch.cuda.synchronize(dev)
@@ -246,17 +319,14 @@ def main():
     kern_ms = sorted(e0.elapsed_time(e1) for e0, e1 in ev)
     kern_avg_ms = sum(kern_ms) / len(kern_ms)
 
+    tdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        kt = torch.tensor([kern_avg_ms], device=dev, dtype=torch.float64)
-        dist.all_reduce(kt, op=dist.ReduceOp.MAX)
-        kern_avg_ms = float(kt.item())
+        elapsed = max_over_ranks(torch, dist, elapsed, tdev)
+        kern_avg_ms = max_over_ranks(torch, dist, kern_avg_ms, tdev)
 
     parity = None
     if direction == sqobfs.OBFUSCATE:
-        parity = spot_check(torch, sh, kind, n, sh["out"])
+        parity = spot_check(torch, sh, kind, n, sh["out"], saved, args.warmup + args.steps)
     else:
         lens = sh["lens"].cpu().numpy()
         offs = sh["in_off"].cpu().numpy()
@@ -264,11 +334,11 @@ def main():
                                  sh["data"][int(offs[i]):int(offs[i]) + int(lens[i])])
                      for i in sorted(set([0, n - 1] + list(range(0, n, 4099)))))
     if dist:
-        pt = torch.tensor([1 if parity else 0], device=dev)
-        dist.all_reduce(pt, op=dist.ReduceOp.MIN)
-        parity = bool(pt.item())
+        parity = -max_over_ranks(torch, dist, -1.0 if parity else 0.0, tdev) > 0
 
-    total_payload = sh["payload_bytes"] * world * args.steps
+    total_payload = sh["payload_bytes"] * args.steps
+    if dist:
+        total_payload = sum_over_ranks(torch, dist, total_payload, tdev)
     value = total_payload / elapsed / 2**30
     achieved = alg_bytes / (kern_avg_ms * 1e-3) / 1e9
     traffic, pmc = load_traffic(args.config, alg_bytes)
@@ -297,7 +367,7 @@ def main():
             "direction": args.direction,
             "packets_per_gpu": n,
             "payload_bytes_per_gpu": sh["payload_bytes"],
-            "layout": "inputs and outputs in 16-byte-aligned slots, offsets/lengths SoA in HBM",
+            "layout": args.layout,
             "parallelism": f"shard{world} (independent packets, no collective)",
         },
         "roofline": {
