@@ -64,11 +64,13 @@ __global__ __launch_bounds__(256) void probe(const uint8_t *src, uint8_t *dst, u
   if (PAT == 2 && acc.x == 0x12345678u) st<0>(dst, acc);
 }
 
+static uint32_t g_lds = 0;  // dynamic LDS per block: caps blocks per CU
 template <int PAT, int U, int POL, int OFF>
 static void go(const void *s, void *d, uint64_t n, uint64_t rc, uint64_t g, hipStream_t st) {
-  hipLaunchKernelGGL((probe<PAT, U, POL, OFF>), dim3(g), dim3(256), 0, st, (const uint8_t *)s,
+  hipLaunchKernelGGL((probe<PAT, U, POL, OFF>), dim3(g), dim3(256), g_lds, st, (const uint8_t *)s,
                      (uint8_t *)d, n, rc);
 }
+extern "C" void probe_set_lds(uint32_t bytes) { g_lds = bytes; }
 
 #define CASE(P, U, POL, OFF)                                                      \
   if (pat == P && u == U && pol == POL && off == OFF) {                           \

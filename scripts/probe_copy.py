@@ -17,20 +17,30 @@ src = torch.randint(0, 256, (nbytes + 64,), dtype=torch.uint8, device="cuda")
 dst = torch.empty(nbytes + 64, dtype=torch.uint8, device="cuda")
 s = torch.cuda.current_stream().cuda_stream
 cases = []
-for pol in (0, 1, 2, 3):
-    for g in (1024, 2048, 8192):
-        cases.append((0, 4, pol, 0, 0, g))
-    cases.append((0, 8, pol, 0, 0, 2048))
-    cases.append((0, 16, pol, 0, 0, 1024))
-    cases.append((0, 4, pol, 8, 0, 2048))
-    for u in (4, 8, 16):
-        for reg in (87040, 21760):
-            cases.append((1, u, pol, 8, reg, 0))
-    cases.append((2, 4, pol, 0, 0, 2048))
-    cases.append((2, 8, pol, 0, 0, 2048))
-    cases.append((3, 4, pol, 0, 0, 2048))
-    cases.append((3, 8, pol, 0, 0, 2048))
-for pat, u, pol, off, reg, grid in cases:
+L.probe_set_lds.argtypes = [ctypes.c_uint32]
+import sys
+mode = sys.argv[1] if len(sys.argv) > 1 else "sweep"
+if mode == "occ":
+    for lds in (0, 20480, 27000, 40000, 53000, 80000):
+        for u in (8, 16):
+            cases.append((1, u, 3, 8, 87040, 0, lds))
+        cases.append((0, 4, 3, 0, 0, 8192, lds))
+else:
+    for pol in (0, 1, 2, 3):
+        for g in (1024, 2048, 8192):
+            cases.append((0, 4, pol, 0, 0, g, 0))
+        cases.append((0, 8, pol, 0, 0, 2048, 0))
+        cases.append((0, 16, pol, 0, 0, 1024, 0))
+        cases.append((0, 4, pol, 8, 0, 2048, 0))
+        for u in (4, 8, 16):
+            for reg in (87040, 21760):
+                cases.append((1, u, pol, 8, reg, 0, 0))
+        cases.append((2, 4, pol, 0, 0, 2048, 0))
+        cases.append((2, 8, pol, 0, 0, 2048, 0))
+        cases.append((3, 4, pol, 0, 0, 2048, 0))
+        cases.append((3, 8, pol, 0, 0, 2048, 0))
+for pat, u, pol, off, reg, grid, lds in cases:
+    L.probe_set_lds(lds)
     rc = L.probe_run(pat, u, pol, off, src.data_ptr(), dst.data_ptr(), nbytes, reg, grid, s)
     if rc != 0:
         print("skip", pat, u, pol, off, rc)
@@ -45,5 +55,5 @@ for pat, u, pol, off, reg, grid in cases:
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / 10 * 1e3
     moved = nbytes * (2 if pat in (0, 1) else 1)
-    print(json.dumps(dict(pat=pat, U=u, pol=pol, off=off, region=reg, grid=grid,
+    print(json.dumps(dict(pat=pat, U=u, pol=pol, off=off, region=reg, grid=grid, lds=lds,
                           us=round(us, 1), TBps=round(moved / us / 1e6, 3))), flush=True)

@@ -62,7 +62,7 @@ __device__ __forceinline__ void gst(uint64_t a, T v) {
 #define SQ_NT 3
 #endif
 #ifndef SQ_U
-#define SQ_U 8
+#define SQ_U 6
 #endif
 
 
@@ -75,6 +75,13 @@ __device__ __forceinline__ void gst(uint64_t a, T v) {
 #ifndef SQ_ROLL
 #define SQ_ROLL 0
 #endif
+// Packets per wavefront (<= 64).  Fewer packets per wave = shorter, more
+// numerous work units: a smaller address window in flight and a shorter
+// tail, at the price of idle lanes during the per-lane key derivation.
+#ifndef SQ_PPW
+#define SQ_PPW 32
+#endif
+constexpr int kPktPerWave = SQ_PPW;
 #ifndef SQ_EXP_FULL
 #define SQ_EXP_FULL 0
 #endif
@@ -476,8 +483,10 @@ __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
 
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wv = threadIdx.x / kWave;
-  const uint64_t p64 = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  const bool valid = p64 < P.n;
+  // each wave owns kPktPerWave consecutive packets (lanes >= kPktPerWave own
+  // none: they only help stream)
+  const uint64_t p64 = ((uint64_t)blockIdx.x * kWavesPerBlock + wv) * kPktPerWave + lane;
+  const bool valid = lane < (uint32_t)kPktPerWave && p64 < P.n;
   const uint32_t p = (uint32_t)p64;
 
   // ---- 1. descriptor
@@ -695,7 +704,8 @@ __global__ void psk_prepare_kernel(int kind, const uint8_t *blob, const uint64_t
 template <int KIND, int DIR, bool MULTI>
 static int launch_one(const KParams *kp, hipStream_t s) {
   constexpr int U = SQ_U;
-  const uint64_t blocks = ((uint64_t)kp->n + kBlock - 1) / kBlock;
+  constexpr uint64_t per_block = (uint64_t)kWavesPerBlock * kPktPerWave;
+  const uint64_t blocks = ((uint64_t)kp->n + per_block - 1) / per_block;
   hipLaunchKernelGGL((obfs_kernel<KIND, DIR, MULTI, U>), dim3((uint32_t)blocks),
                      dim3(kBlock), 0, s, *kp);
   return hipGetLastError() == hipSuccess ? 0 : -3;
