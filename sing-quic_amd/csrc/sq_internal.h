@@ -9,7 +9,10 @@ namespace sq {
 constexpr int kSalamanderSalt = 8;  // hysteria2/salamander.go:15
 constexpr int kXPlusSalt = 16;      // hysteria/xplus.go:17
 constexpr int kWave = 64;           // CDNA wavefront
-constexpr int kBlock = 256;         // 4 waves per workgroup
+#ifndef SQ_BLOCK
+#define SQ_BLOCK 256
+#endif
+constexpr int kBlock = SQ_BLOCK;    // 4 waves per workgroup
 constexpr int kWavesPerBlock = kBlock / kWave;
 
 // Per-PSK hash state, derived once per keyring on the GPU (psk_prepare).

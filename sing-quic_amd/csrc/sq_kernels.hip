@@ -82,6 +82,9 @@ __device__ __forceinline__ void gst(uint64_t a, T v) {
 #define SQ_PPW 32
 #endif
 constexpr int kPktPerWave = SQ_PPW;
+#ifndef SQ_XCD_SWZ
+#define SQ_XCD_SWZ 0
+#endif
 #ifndef SQ_EXP_FULL
 #define SQ_EXP_FULL 0
 #endif
@@ -474,6 +477,21 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
                  __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)));
 }
 
+// Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md,
+// "Workgroup dispatch").  With SQ_XCD_SWZ the logical block order is
+// remapped (a bijection, so placement only affects speed) so that each XCD
+// works on one contiguous range of packets: the boundary lines shared by
+// neighbouring blocks are then written through the same L2.
+__device__ __forceinline__ uint32_t logical_block() {
+#if SQ_XCD_SWZ
+  const uint32_t nb = gridDim.x, bid = blockIdx.x;
+  const uint32_t q = nb / 8, r = nb % 8, x = bid % 8, i = bid / 8;
+  return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
+#else
+  return blockIdx.x;
+#endif
+}
+
 // ------------------------------------------------------------ main kernel
 
 template <int KIND, int DIR, bool MULTI, int U>
@@ -485,7 +503,7 @@ __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
   const uint32_t wv = threadIdx.x / kWave;
   // each wave owns kPktPerWave consecutive packets (lanes >= kPktPerWave own
   // none: they only help stream)
-  const uint64_t p64 = ((uint64_t)blockIdx.x * kWavesPerBlock + wv) * kPktPerWave + lane;
+  const uint64_t p64 = ((uint64_t)logical_block() * kWavesPerBlock + wv) * kPktPerWave + lane;
   const bool valid = lane < (uint32_t)kPktPerWave && p64 < P.n;
   const uint32_t p = (uint32_t)p64;
 
