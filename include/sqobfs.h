@@ -76,6 +76,10 @@ extern "C" {
 #define SQ_ENODEV (-4)   /* no such GPU */
 #define SQ_EPSK (-5)     /* a psk_id was out of range (host-staged path) */
 
+/* batch flag (sqobfs_run_host): output bytes outside the packets' output
+ * regions need not be preserved (skips copying the output range in) */
+#define SQOBFS_FLAG_OUT_UNINIT 1u
+
 /* out_len value written for a packet whose psk_id is out of range */
 #define SQOBFS_BAD_PSK 0xFFFFFFFFu
 
@@ -90,7 +94,7 @@ typedef struct sqobfs_keyring sqobfs_keyring;
  * context's GPU; for sqobfs_run_host every pointer is a host pointer. */
 typedef struct sqobfs_batch {
   uint32_t n;               /* number of packets */
-  uint32_t flags;           /* reserved, must be 0 */
+  uint32_t flags;           /* 0 or SQOBFS_FLAG_* */
   const uint8_t *in;        /* input base */
   const uint64_t *in_off;   /* [n] byte offset of packet i in `in` */
   const uint32_t *in_len;   /* [n] payload length (obfs) / datagram length n (deobfs) */
@@ -144,10 +148,12 @@ int sqobfs_xplus_deobfuscate(sqobfs_ctx *ctx, const sqobfs_keyring *kr,
 int sqobfs_launch(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
                   const sqobfs_batch *b, void *stream);
 
-/* Host-memory batch: copies the touched input range and the descriptors to
- * the GPU through pinned staging, launches, copies the output range and
- * out_len back.  Synchronous.  Output bytes outside the packets' output
- * regions are preserved. */
+/* Host-memory batch, synchronous.  The batch is cut into up to 8 chunks of
+ * packets whose copy-in (H2D), kernel and copy-out (D2H) run on three
+ * streams and overlap.  Pinned caller buffers (sqobfs_host_alloc) are
+ * copied by DMA directly; pageable ones go through pinned staging.  Output
+ * bytes outside the packets' output regions are preserved unless
+ * flags has SQOBFS_FLAG_OUT_UNINIT. */
 int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
                     const sqobfs_batch *host_batch);
 

@@ -12,19 +12,29 @@
 #include <algorithm>
 #include <mutex>
 #include <new>
+#include <thread>
+#include <vector>
 
 #include "../../include/sqobfs.h"
 #include "sq_internal.h"
 
 struct sqobfs_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;  // compute (and sqobfs_stream)
+  hipStream_t h2d = nullptr;     // sqobfs_run_host copy-in
+  hipStream_t d2h = nullptr;     // sqobfs_run_host copy-out
   std::mutex mu;  // guards the staging buffers of sqobfs_run_host
   uint8_t *pinned = nullptr;
   size_t pinned_cap = 0;
   uint8_t *dev = nullptr;
   size_t dev_cap = 0;
+  hipEvent_t ev[16] = {};  // pipeline events of sqobfs_run_host
 };
+
+namespace {
+constexpr uint32_t kHostChunks = 8;  // sqobfs_run_host pipeline depth
+constexpr uint32_t kEvents = 16;
+}
 
 struct sqobfs_keyring {
   sqobfs_ctx *ctx = nullptr;
@@ -62,7 +72,7 @@ hipStream_t pick_stream(sqobfs_ctx *ctx, void *stream) {
 
 int check_batch_shape(const sqobfs_batch *b, int dir) {
   if (!b) return SQ_EINVAL;
-  if (b->flags != 0) return SQ_EINVAL;
+  if (b->flags & ~(uint32_t)SQOBFS_FLAG_OUT_UNINIT) return SQ_EINVAL;
   if (b->n == 0) return SQ_OK;
   if (!b->in || !b->in_off || !b->in_len || !b->out || !b->out_off || !b->out_len)
     return SQ_EINVAL;
@@ -92,6 +102,37 @@ sq::KParams make_params(const sqobfs_keyring *kr, const sqobfs_batch *b) {
 }
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+struct Range {
+  size_t lo, hi;     // byte range touched in the caller's buffer
+  uint32_t p0, p1;   // packets of the chunk
+};
+
+bool is_pinned(const void *p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory reports an error: clear it
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+// memcpy of large pageable ranges on several host threads
+void par_memcpy(void *dst, const void *src, size_t n) {
+  constexpr size_t kPer = 8u << 20;
+  const unsigned hw = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  const unsigned nt = (unsigned)std::min<size_t>(hw, (n + kPer - 1) / kPer);
+  if (nt <= 1) {
+    memcpy(dst, src, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; t++) {
+    const size_t lo = n * t / nt, hi = n * (t + 1) / nt;
+    th.emplace_back([=] { memcpy((uint8_t *)dst + lo, (const uint8_t *)src + lo, hi - lo); });
+  }
+  for (auto &x : th) x.join();
+}
 
 }  // namespace
 
@@ -131,8 +172,12 @@ int sqobfs_open(int device, sqobfs_ctx **out) {
   sqobfs_ctx *c = new (std::nothrow) sqobfs_ctx();
   if (!c) return SQ_ENOMEM;
   c->device = device;
-  const hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->h2d, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking);
   if (e != hipSuccess) {
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->h2d) (void)hipStreamDestroy(c->h2d);
     delete c;
     return hip_status(e);
   }
@@ -147,6 +192,10 @@ void sqobfs_close(sqobfs_ctx *ctx) {
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   if (ctx->dev) (void)hipFree(ctx->dev);
   (void)hipStreamDestroy(ctx->stream);
+  (void)hipStreamDestroy(ctx->h2d);
+  (void)hipStreamDestroy(ctx->d2h);
+  for (auto &e : ctx->ev)
+    if (e) (void)hipEventDestroy(e);
   delete ctx;
 }
 
@@ -268,22 +317,71 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
   const uint32_t n = hb->n;
   const int kind = kr->kind;
   const size_t S = salt_len(kind);
-  // extents of the touched input / output ranges, and psk_id validation
+  // ---- pass over the descriptors: psk ids, and per chunk of packets the
+  // input / output byte ranges it touches
+  const uint32_t nchunk = n < 4096 ? 1u : std::min<uint32_t>(kHostChunks, (n + 4095) / 4096);
+  std::vector<Range> rin(nchunk), rout(nchunk);
   size_t in_ext = 0, out_ext = 0;
-  for (uint32_t i = 0; i < n; i++) {
-    const size_t len = hb->in_len[i];
-    size_t cap = len;
-    if (kind == SQOBFS_XPLUS && dir == SQOBFS_DEOBFUSCATE && hb->in_cap)
-      cap = std::max<size_t>(len, hb->in_cap[i]);
-    in_ext = std::max(in_ext, (size_t)hb->in_off[i] + cap);
-    size_t osz;
-    if (dir == SQOBFS_OBFUSCATE) osz = S + len;
-    else if (kind == SQOBFS_SALAMANDER) osz = len <= S ? len : len - S;
-    else osz = len < S ? 0 : cap - S;
-    out_ext = std::max(out_ext, (size_t)hb->out_off[i] + osz);
-    if (hb->psk_id && hb->psk_id[i] >= kr->count) return SQ_EPSK;
+  for (uint32_t c = 0; c < nchunk; c++) {
+    const uint32_t p0 = (uint32_t)((uint64_t)n * c / nchunk);
+    const uint32_t p1 = (uint32_t)((uint64_t)n * (c + 1) / nchunk);
+    Range ri{SIZE_MAX, 0, p0, p1}, ro{SIZE_MAX, 0, p0, p1};
+    for (uint32_t i = p0; i < p1; i++) {
+      const size_t len = hb->in_len[i];
+      size_t cap = len;
+      if (kind == SQOBFS_XPLUS && dir == SQOBFS_DEOBFUSCATE && hb->in_cap)
+        cap = std::max<size_t>(len, hb->in_cap[i]);
+      size_t osz;
+      if (dir == SQOBFS_OBFUSCATE) osz = S + len;
+      else if (kind == SQOBFS_SALAMANDER) osz = len <= S ? len : len - S;
+      else osz = len < S ? 0 : cap - S;
+      if (cap) {
+        ri.lo = std::min<size_t>(ri.lo, hb->in_off[i]);
+        ri.hi = std::max<size_t>(ri.hi, hb->in_off[i] + cap);
+      }
+      if (osz) {
+        ro.lo = std::min<size_t>(ro.lo, hb->out_off[i]);
+        ro.hi = std::max<size_t>(ro.hi, hb->out_off[i] + osz);
+      }
+      if (hb->psk_id && hb->psk_id[i] >= kr->count) return SQ_EPSK;
+    }
+    if (ri.lo > ri.hi) ri.lo = ri.hi = 0;
+    if (ro.lo > ro.hi) ro.lo = ro.hi = 0;
+    in_ext = std::max(in_ext, ri.hi);
+    out_ext = std::max(out_ext, ro.hi);
+    rin[c] = ri;
+    rout[c] = ro;
   }
-  // one staging layout, mirrored in pinned host memory and on the device
+  // Chunks run concurrently: if one chunk's output bytes overlap another
+  // chunk's input or output bytes (in-place or interleaved layouts), run
+  // the batch as a single chunk instead.
+  auto meet = [](const uint8_t *a, const Range &ra, const uint8_t *b, const Range &rb) {
+    return ra.hi > ra.lo && rb.hi > rb.lo && a + ra.lo < b + rb.hi && b + rb.lo < a + ra.hi;
+  };
+  bool clash = false;
+  for (uint32_t x = 0; x < nchunk && !clash; x++)
+    for (uint32_t y = 0; y < nchunk && !clash; y++)
+      clash = x != y && (meet(hb->out, rout[x], hb->out, rout[y]) ||
+                         meet(hb->out, rout[x], hb->in, rin[y]));
+  if (clash) {
+    Range ri{SIZE_MAX, 0, 0, n}, ro{SIZE_MAX, 0, 0, n};
+    for (uint32_t c = 0; c < nchunk; c++) {
+      if (rin[c].hi > rin[c].lo) ri.lo = std::min(ri.lo, rin[c].lo), ri.hi = std::max(ri.hi, rin[c].hi);
+      if (rout[c].hi > rout[c].lo) ro.lo = std::min(ro.lo, rout[c].lo), ro.hi = std::max(ro.hi, rout[c].hi);
+    }
+    if (ri.lo > ri.hi) ri.lo = ri.hi = 0;
+    if (ro.lo > ro.hi) ro.lo = ro.hi = 0;
+    rin.assign(1, ri);
+    rout.assign(1, ro);
+  }
+  const uint32_t nrun = (uint32_t)rin.size();
+  // caller memory that is already pinned (sqobfs_host_alloc, hipHostMalloc)
+  // is copied by DMA directly; pageable memory goes through pinned staging
+  const bool in_pinned = is_pinned(hb->in), out_pinned = is_pinned(hb->out);
+  const bool preserve = !(hb->flags & SQOBFS_FLAG_OUT_UNINIT);
+
+  // staging layout (device mirror of the host ranges; pinned copies only
+  // for what is pageable)
   const size_t A = 256;
   size_t o = 0;
   const size_t o_in = o;       o = align_up(o + in_ext, A);
@@ -313,34 +411,80 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
     SQ_TRY(hipMalloc(&ctx->dev, total));
     ctx->dev_cap = total;
   }
+  for (auto &e : ctx->ev)
+    if (!e) SQ_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   uint8_t *H = ctx->pinned, *D = ctx->dev;
-  if (in_ext) memcpy(H + o_in, hb->in, in_ext);
-  if (out_ext) memcpy(H + o_out, hb->out, out_ext);  // preserve untouched bytes
+
+  // descriptors: small, copied once up front
   memcpy(H + o_inoff, hb->in_off, 8ull * n);
   memcpy(H + o_inlen, hb->in_len, 4ull * n);
   memcpy(H + o_outoff, hb->out_off, 8ull * n);
   if (dir == SQOBFS_OBFUSCATE) memcpy(H + o_salt, hb->salt, S * n);
   if (hb->psk_id) memcpy(H + o_pid, hb->psk_id, 2ull * n);
   if (hb->in_cap) memcpy(H + o_cap, hb->in_cap, 4ull * n);
-  SQ_TRY(hipMemcpyAsync(D, H, total, hipMemcpyHostToDevice, ctx->stream));
-  sqobfs_batch db = *hb;
-  db.in = D + o_in;
-  db.in_off = (const uint64_t *)(D + o_inoff);
-  db.in_len = (const uint32_t *)(D + o_inlen);
-  db.out = D + o_out;
-  db.out_off = (const uint64_t *)(D + o_outoff);
-  db.out_len = (uint32_t *)(D + o_outlen);
-  db.salt = dir == SQOBFS_OBFUSCATE ? D + o_salt : nullptr;
-  db.psk_id = hb->psk_id ? (const uint16_t *)(D + o_pid) : nullptr;
-  db.in_cap = hb->in_cap ? (const uint32_t *)(D + o_cap) : nullptr;
-  const sq::KParams kp = make_params(kr, &db);
-  st = sq_launch_obfs(kind, dir, &kp, ctx->stream);
-  if (st != SQ_OK) return st;
-  SQ_TRY(hipMemcpyAsync(H + o_out, D + o_out, out_ext, hipMemcpyDeviceToHost, ctx->stream));
-  SQ_TRY(hipMemcpyAsync(H + o_outlen, D + o_outlen, 4ull * n, hipMemcpyDeviceToHost,
-                        ctx->stream));
-  SQ_TRY(hipStreamSynchronize(ctx->stream));
-  if (out_ext) memcpy(hb->out, H + o_out, out_ext);
+  SQ_TRY(hipMemcpyAsync(D + o_inoff, H + o_inoff, o_outlen - o_inoff, hipMemcpyHostToDevice,
+                        ctx->h2d));
+  SQ_TRY(hipMemcpyAsync(D + o_salt, H + o_salt, total - o_salt, hipMemcpyHostToDevice,
+                        ctx->h2d));
+
+  // ---- pipeline: H2D(c) on h2d | kernel(c) on the compute stream | D2H(c)
+  // on d2h, chained by events; chunk c+1's copy-in overlaps chunk c's
+  // kernel and chunk c-1's copy-out.
+  for (uint32_t c = 0; c < nrun; c++) {
+    const Range &ri = rin[c], &ro = rout[c];
+    if (ri.hi > ri.lo) {
+      const uint8_t *src = hb->in + ri.lo;
+      if (!in_pinned) {
+        par_memcpy(H + o_in + ri.lo, src, ri.hi - ri.lo);
+        src = H + o_in + ri.lo;
+      }
+      SQ_TRY(hipMemcpyAsync(D + o_in + ri.lo, src, ri.hi - ri.lo, hipMemcpyHostToDevice,
+                            ctx->h2d));
+    }
+    if (preserve && ro.hi > ro.lo) {  // bytes between packets keep their value
+      const uint8_t *src = hb->out + ro.lo;
+      if (!out_pinned) {
+        par_memcpy(H + o_out + ro.lo, src, ro.hi - ro.lo);
+        src = H + o_out + ro.lo;
+      }
+      SQ_TRY(hipMemcpyAsync(D + o_out + ro.lo, src, ro.hi - ro.lo, hipMemcpyHostToDevice,
+                            ctx->h2d));
+    }
+    hipEvent_t ev_in = ctx->ev[(2 * c) % kEvents], ev_k = ctx->ev[(2 * c + 1) % kEvents];
+    SQ_TRY(hipEventRecord(ev_in, ctx->h2d));
+    SQ_TRY(hipStreamWaitEvent(ctx->stream, ev_in, 0));
+    sqobfs_batch db = *hb;
+    db.n = ri.p1 - ri.p0;
+    db.in = D + o_in;
+    db.in_off = (const uint64_t *)(D + o_inoff) + ri.p0;
+    db.in_len = (const uint32_t *)(D + o_inlen) + ri.p0;
+    db.out = D + o_out;
+    db.out_off = (const uint64_t *)(D + o_outoff) + ri.p0;
+    db.out_len = (uint32_t *)(D + o_outlen) + ri.p0;
+    db.salt = dir == SQOBFS_OBFUSCATE ? D + o_salt + S * ri.p0 : nullptr;
+    db.psk_id = hb->psk_id ? (const uint16_t *)(D + o_pid) + ri.p0 : nullptr;
+    db.in_cap = hb->in_cap ? (const uint32_t *)(D + o_cap) + ri.p0 : nullptr;
+    if (db.n) {
+      const sq::KParams kp = make_params(kr, &db);
+      st = sq_launch_obfs(kind, dir, &kp, ctx->stream);
+      if (st != SQ_OK) return st;
+    }
+    SQ_TRY(hipEventRecord(ev_k, ctx->stream));
+    SQ_TRY(hipStreamWaitEvent(ctx->d2h, ev_k, 0));
+    if (ro.hi > ro.lo) {
+      uint8_t *dst = out_pinned ? hb->out + ro.lo : H + o_out + ro.lo;
+      SQ_TRY(hipMemcpyAsync(dst, D + o_out + ro.lo, ro.hi - ro.lo, hipMemcpyDeviceToHost,
+                            ctx->d2h));
+    }
+  }
+  SQ_TRY(hipMemcpyAsync(H + o_outlen, D + o_outlen, 4ull * n, hipMemcpyDeviceToHost, ctx->d2h));
+  SQ_TRY(hipStreamSynchronize(ctx->d2h));
+  // pageable output: copy back in chunk order (later chunks win where
+  // ranges interleave, matching the device order)
+  if (!out_pinned)
+    for (uint32_t c = 0; c < nrun; c++)
+      if (rout[c].hi > rout[c].lo)
+        par_memcpy(hb->out + rout[c].lo, H + o_out + rout[c].lo, rout[c].hi - rout[c].lo);
   memcpy(hb->out_len, H + o_outlen, 4ull * n);
   return SQ_OK;
 }

@@ -30,6 +30,7 @@ OBFS_TYPE_SALAMANDER = "salamander"  # hysteria2/salamander.go:17
 
 SQ_OK, SQ_EINVAL, SQ_ENOMEM, SQ_EDEVICE, SQ_ENODEV, SQ_EPSK = 0, -1, -2, -3, -4, -5
 BAD_PSK = 0xFFFFFFFF
+FLAG_OUT_UNINIT = 1  # run_host: bytes between output regions need not be kept
 
 
 class SqError(RuntimeError):
@@ -225,14 +226,43 @@ class HostBatch:
     salt: np.ndarray | None = None
     psk_id: np.ndarray | None = None
     in_cap: np.ndarray | None = None
+    flags: int = 0
 
     @property
     def n(self) -> int:
         return int(self.in_len.shape[0])
 
     def as_batch(self) -> Batch:
-        return make_batch(self.n, self.data, self.in_off, self.in_len, self.out,
-                          self.out_off, self.out_len, self.salt, self.psk_id, self.in_cap)
+        b = make_batch(self.n, self.data, self.in_off, self.in_len, self.out,
+                       self.out_off, self.out_len, self.salt, self.psk_id, self.in_cap)
+        b.flags = self.flags
+        return b
+
+
+class PinnedArray:
+    """A uint8 numpy view of page-locked host memory (sqobfs_host_alloc);
+    run_host DMAs such buffers directly instead of staging them."""
+
+    def __init__(self, ctx: Context, nbytes: int):
+        self._ctx = ctx
+        p = ctypes.c_void_p()
+        _check(lib().sqobfs_host_alloc(ctx.handle, max(nbytes, 1), ctypes.byref(p)),
+               "sqobfs_host_alloc")
+        self._p = p
+        buf = (ctypes.c_uint8 * max(nbytes, 1)).from_address(p.value)
+        self.array = np.frombuffer(buf, dtype=np.uint8)[:nbytes]
+
+    def free(self) -> None:
+        if self._p is not None:
+            self.array = None
+            lib().sqobfs_host_free(self._ctx.handle, self._p)
+            self._p = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.free()
 
 
 def pack(packets: list[bytes], align: int = 16, lead: int = 0) -> tuple[np.ndarray, np.ndarray, np.ndarray]:

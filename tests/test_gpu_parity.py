@@ -187,6 +187,79 @@ def test_host_staged_path(ctx, kind, direction):
     check(ctx, kind, direction, [PSK], hb, "host path", path="host")
 
 
+def _pin(ctx, hb, keep):
+    """Move hb's data/out into page-locked memory (run_host's DMA path)."""
+    inplace = hb.out is hb.data
+    pd = sqobfs.PinnedArray(ctx, hb.data.size)
+    pd.array[:] = hb.data
+    keep.append(pd)
+    hb.data = pd.array
+    if inplace:
+        hb.out = hb.data
+    else:
+        po = sqobfs.PinnedArray(ctx, hb.out.size)
+        po.array[:] = hb.out
+        keep.append(po)
+        hb.out = po.array
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("direction", DIRS)
+@pytest.mark.parametrize("layout", ["dense", "gaps", "inplace", "shuffled"])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_pipeline(ctx, kind, direction, layout, pinned):
+    """Batches big enough for run_host's chunked H2D/kernel/D2H pipeline
+    (several chunks), with pageable and pinned caller buffers, 3 PSKs.
+    'shuffled' permutes the packet order so chunks' byte ranges interleave
+    (the single-chunk fallback)."""
+    rng = np.random.Generator(np.random.PCG64(300 + kind + 2 * direction + 4 * pinned))
+    n = 20000
+    lens = rng.integers(0, 1500, n)
+    psks = [PSK, b"", b"x" * 200]
+    ids = rng.integers(0, 3, n)
+    hb = gh.make_case(rng, kind, direction, lens, psks, psk_ids=ids,
+                      in_align=1 if layout == "gaps" else 16,
+                      out_align=1 if layout == "gaps" else 16,
+                      gaps=layout == "gaps", inplace=layout == "inplace")
+    if layout == "shuffled":
+        perm = rng.permutation(n)
+        S = sqobfs.SALT_LEN[kind]
+        hb.in_off, hb.in_len, hb.out_off = hb.in_off[perm], hb.in_len[perm], hb.out_off[perm]
+        if hb.salt is not None:
+            hb.salt = hb.salt.reshape(n, S)[perm].reshape(-1).copy()
+        if hb.psk_id is not None:
+            hb.psk_id = hb.psk_id[perm]
+        if hb.in_cap is not None:
+            hb.in_cap = hb.in_cap[perm]
+    keep = []
+    try:
+        if pinned:
+            _pin(ctx, hb, keep)
+        check(ctx, kind, direction, psks, hb, f"host pipeline {layout}", path="host")
+    finally:
+        for k in keep:
+            k.free()
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_host_out_uninit_flag(ctx, kind):
+    """SQOBFS_FLAG_OUT_UNINIT: every packet's output region and out_len are
+    exact; bytes between regions are not checked."""
+    rng = np.random.Generator(np.random.PCG64(77 + kind))
+    n = 12000
+    lens = rng.integers(0, 1500, n)
+    hb = gh.make_case(rng, kind, OBFUSCATE, lens, [PSK], gaps=True)
+    ref = gh.run_oracle(kind, OBFUSCATE, [PSK], hb)
+    hb.flags = sqobfs.FLAG_OUT_UNINIT
+    with sqobfs.Keyring(ctx, kind, [PSK]) as kr:
+        gh.run_host(ctx, kr, OBFUSCATE, hb)
+    assert np.array_equal(hb.out_len, ref.out_len)
+    mask = np.zeros(hb.out.size, bool)
+    for o, L in zip(hb.out_off.astype(np.int64), ref.out_len.astype(np.int64)):
+        mask[o:o + L] = True
+    assert np.array_equal(hb.out[mask], ref.out[mask])
+
+
 def test_empty_batch_and_zero_length(ctx):
     with sqobfs.Keyring(ctx, SALAMANDER, [PSK]) as kr:
         b = sqobfs.Batch()
