@@ -377,7 +377,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / PEAK_HBM_GBS, 4),
             "traffic": traffic,
-            "kernel": f"obfs_kernel<{kind},{direction},{int(n_psk > 1)},4>",
+            "kernel": f"obfs_kernel<{kind},{direction},{int(n_psk > 1)}> ({sqobfs.build_info()})",
             "kernel_avg_us": round(kern_avg_ms * 1e3, 2),
             "kernel_min_us": round(kern_ms[0] * 1e3, 2),
             "algorithmic_bytes_per_launch": alg_bytes,

@@ -108,6 +108,9 @@ typedef struct sqobfs_batch {
 } sqobfs_batch;
 
 int sqobfs_abi_version(void);
+/* Static string naming the compiled kernel configuration (target, unroll,
+ * packets per wavefront, nt policy), e.g. for bench records. */
+const char *sqobfs_build_info(void);
 const char *sqobfs_strerror(int status);
 int sqobfs_device_count(int *count);
 

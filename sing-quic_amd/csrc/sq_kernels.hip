@@ -89,6 +89,13 @@ constexpr int kPktPerWave = SQ_PPW;
 #define SQ_EXP_FULL 0
 #endif
 
+#define SQ_STR2(x) #x
+#define SQ_STR(x) SQ_STR2(x)
+extern "C" const char *sqobfs_build_info(void) {
+  return "gfx950 obfs_kernel U=" SQ_STR(SQ_U) " PPW=" SQ_STR(SQ_PPW) " NT=" SQ_STR(SQ_NT)
+         " block=" SQ_STR(SQ_BLOCK) " xcd_swz=" SQ_STR(SQ_XCD_SWZ) " ablate=" SQ_STR(SQ_ABLATE);
+}
+
 constexpr uint32_t kMaxPacket = 1u << 26;  // per-packet length bound (u32 chunk math)
 constexpr uint32_t kBadPsk = 0xFFFFFFFFu;
 constexpr uint32_t kBadLen = 0xFFFFFFFEu;

@@ -92,9 +92,15 @@ def lib() -> ctypes.CDLL:
     L.sqobfs_run_host.argtypes = [vp, vp, i32, ctypes.POINTER(Batch)]
     L.sqobfs_host_alloc.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(vp)]
     L.sqobfs_host_free.argtypes = [vp, vp]
+    L.sqobfs_build_info.restype = ctypes.c_char_p
+    L.sqobfs_build_info.argtypes = []
     L.sqobfs_host_free.restype = None
     _lib = L
     return L
+
+
+def build_info() -> str:
+    return lib().sqobfs_build_info().decode()
 
 
 def strerror(status: int) -> str:
