@@ -319,6 +319,18 @@ def main():
     kern_ms = sorted(e0.elapsed_time(e1) for e0, e1 in ev)
     kern_avg_ms = sum(kern_ms) / len(kern_ms)
 
+    tl_out = os.environ.get("SQ_TIMELINE_OUT")  # dev hook: timeline builds only
+    if tl_out and rank == 0:
+        import numpy as np
+        sqobfs.launch(ctx, kr, direction, b, s)
+        torch.cuda.synchronize(dev)
+        waves = (n + 15) // 16 * 4  # >= launched waves for PPW >= 16, block 256
+        tl = np.zeros(3 * waves, np.uint64)
+        fn = sqobfs.lib().sq_timeline_copy
+        fn.argtypes = [sqobfs.ctypes.c_void_p, sqobfs.ctypes.c_uint64]
+        assert fn(tl.ctypes.data, waves) == 0
+        np.save(tl_out, tl.reshape(-1, 3))
+
     tdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     if dist:
         elapsed = max_over_ranks(torch, dist, elapsed, tdev)

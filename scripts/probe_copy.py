@@ -24,6 +24,7 @@ if mode == "occ":
     for lds in (0, 20480, 27000, 40000, 53000, 80000):
         for u in (8, 16):
             cases.append((1, u, 3, 8, 87040, 0, lds))
+            cases.append((1, u, 3, 8, 21760, 0, lds))
         cases.append((0, 4, 3, 0, 0, 8192, lds))
 else:
     for pol in (0, 1, 2, 3):

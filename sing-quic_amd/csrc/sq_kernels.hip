@@ -8,17 +8,18 @@
 //   VectorisedXPlusConn.WriteTo               hysteria/xplus.go:86-98
 // for a whole ragged batch of datagrams per launch.
 //
-// Work decomposition (one wavefront = 64 packets, fully independent waves):
-//   1. descriptor  lane l owns packet 64*wave + l: reads its offsets/lengths
-//                  and salt (obfs: salt array; deobfs: first S wire bytes).
+// Work decomposition (one wavefront = PPW = 32 packets, independent waves):
+//   1. descriptor  lane l < PPW owns packet PPW*wave + l: reads its offsets,
+//                  lengths and salt (obfs: salt array; deobfs: first S wire
+//                  bytes).
 //   2. key         lane l hashes its own packet's psk||salt (BLAKE2b-256 or
 //                  SHA-256) starting from the keyring's per-PSK midstate:
-//                  64 different packets hashed in parallel, no idle lanes.
+//                  PPW different packets hashed in parallel.
 //   3. split       each packet's output is cut at 16-byte boundaries of the
 //                  DESTINATION address: "full" chunks (16 payload bytes) and
 //                  at most ~3 "edge" chunks (salt bytes, unaligned head,
 //                  tail).  A wave prefix-sum over full-chunk counts builds a
-//                  flat chunk space for the 64 packets; each packet's
+//                  flat chunk space for the wave's packets; each packet's
 //                  addressing and its two 16-byte keystream phases go to LDS.
 //   4. edges       the owner lane writes its packet's edge chunks (byte-exact
 //                  masked stores; loads only 16-byte-aligned blocks that hold
@@ -27,8 +28,9 @@
 //                  per step: one dwordx4 load, XOR with the LDS keystream,
 //                  one aligned dwordx4 store per chunk.  Chunk -> packet is a
 //                  ballot/popcount on the prefix sums held in registers.
-// HBM traffic is the algorithmic minimum: every payload byte is read once and
-// every output byte written once; the key never leaves LDS/registers.
+// Every payload byte is read once and every output byte written once; the
+// key never leaves LDS/registers.  Measured HBM traffic is 1.05x the
+// algorithmic bytes (boundary lines: DESIGN.md section 5).
 #include <hip/hip_runtime.h>
 
 #include "sq_hash.h"
@@ -72,9 +74,6 @@ __device__ __forceinline__ void gst(uint64_t a, T v) {
 #ifndef SQ_ABLATE
 #define SQ_ABLATE 0
 #endif
-#ifndef SQ_ROLL
-#define SQ_ROLL 0
-#endif
 // Packets per wavefront (<= 64).  Fewer packets per wave = shorter, more
 // numerous work units: a smaller address window in flight and a shorter
 // tail, at the price of idle lanes during the per-lane key derivation.
@@ -82,18 +81,20 @@ __device__ __forceinline__ void gst(uint64_t a, T v) {
 #define SQ_PPW 32
 #endif
 constexpr int kPktPerWave = SQ_PPW;
-#ifndef SQ_XCD_SWZ
-#define SQ_XCD_SWZ 0
+// Full chunks start and end on 64-byte line boundaries (1) or on 16-byte
+// chunk boundaries (0).
+#ifndef SQ_LINE_EDGES
+#define SQ_LINE_EDGES 0
 #endif
-#ifndef SQ_EXP_FULL
-#define SQ_EXP_FULL 0
+#ifndef SQ_TIMELINE
+#define SQ_TIMELINE 0
 #endif
 
 #define SQ_STR2(x) #x
 #define SQ_STR(x) SQ_STR2(x)
 extern "C" const char *sqobfs_build_info(void) {
   return "gfx950 obfs_kernel U=" SQ_STR(SQ_U) " PPW=" SQ_STR(SQ_PPW) " NT=" SQ_STR(SQ_NT)
-         " block=" SQ_STR(SQ_BLOCK) " xcd_swz=" SQ_STR(SQ_XCD_SWZ) " ablate=" SQ_STR(SQ_ABLATE);
+         " block=" SQ_STR(SQ_BLOCK) " ablate=" SQ_STR(SQ_ABLATE);
 }
 
 constexpr uint32_t kMaxPacket = 1u << 26;  // per-packet length bound (u32 chunk math)
@@ -293,11 +294,14 @@ struct PacketJob {
   uint32_t pre;      // salt bytes written in front of dst_pay (obfs) or 0
 };
 
-// One edge chunk: bytes [a, b) of the 16-byte output block at A.
-__device__ __forceinline__ void edge_chunk(const PacketJob &J, const uint32_t (&key)[8],
-                                           const uint32_t (&salt)[4], uint64_t A,
-                                           uint32_t a, uint32_t b) {
-  uint32_t val[4] = {0u, 0u, 0u, 0u};
+// Output bytes [a, b) of the 16-byte output block at A (other bytes zero):
+// salt bytes and/or payload bytes XOR keystream.  Reads only the 16-byte
+// input blocks that hold payload bytes of the range.
+__device__ __forceinline__ void block_val(const PacketJob &J, const uint32_t (&key)[8],
+                                          const uint32_t (&salt)[4], uint64_t A, uint32_t a,
+                                          uint32_t b, uint32_t (&val)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; j++) val[j] = 0u;
   const int64_t dp = (int64_t)(J.dst_pay - A);  // payload starts dp bytes into the block
   const uint32_t pay_lo = dp > (int64_t)a ? (uint32_t)(dp < 16 ? dp : 16) : a;
   if (pay_lo < b) {
@@ -316,16 +320,19 @@ __device__ __forceinline__ void edge_chunk(const PacketJob &J, const uint32_t (&
 #pragma unroll
     for (int j = 0; j < 4; j++) val[j] |= sw[j] & range_mask(a, se, j);
   }
-  store_partial(A, val, a, b);
 }
 
+// Byte-exact store of output bytes [A0, A1) (any alignment, edge chunks of
+// small packets and of packets without an adjacent neighbour).
 __device__ __forceinline__ void edge_span(const PacketJob &J, const uint32_t (&key)[8],
                                           const uint32_t (&salt)[4], uint64_t A0,
                                           uint64_t A1) {
   for (uint64_t A = A0 & ~15ull; A < A1; A += 16) {
     const uint32_t a = (uint32_t)((A0 > A ? A0 : A) - A);
     const uint32_t b = (uint32_t)((A1 < A + 16 ? A1 : A + 16) - A);
-    edge_chunk(J, key, salt, A, a, b);
+    uint32_t val[4];
+    block_val(J, key, salt, A, a, b, val);
+    store_partial(A, val, a, b);
   }
 }
 
@@ -397,15 +404,15 @@ __device__ __forceinline__ void store_chunk(const ChunkRec *wrec, const WaveBufs
   __builtin_amdgcn_raw_buffer_store_b128(v ^ R.ks[c & 1], B.dst, off, 0, kAuxSt);
 }
 
-// Double-buffered: the U loads of step i+1 are issued before step i is
-// XORed and stored, so each wave keeps U..2U KiB of reads outstanding.
+// Double-buffered stream loop.  The caller has issued step 0's loads into
+// cur/cpp (before the edge chunks, so the two overlap); each iteration issues
+// step i+1's U loads before step i is XORed and stored, so a wave keeps
+// U..2U KiB of reads outstanding.  Loads past T are range-checked away.
 template <int U>
-__device__ __forceinline__ void stream_dbuf(const ChunkRec *wrec, const WaveBufs &B,
-                                            uint32_t start, uint32_t T, uint32_t lane) {
+__device__ __forceinline__ void stream_loop(const ChunkRec *wrec, const WaveBufs &B,
+                                            uint32_t start, uint32_t T, uint32_t lane,
+                                            u32x4 (&cur)[U], uint32_t (&cpp)[U]) {
   constexpr uint32_t STEP = kWave * U;
-  u32x4 cur[U];
-  uint32_t cpp[U];
-  stream_issue<U>(wrec, B, start, T, lane, 0, cur, cpp);
   for (uint32_t base = 0; base < T; base += STEP) {
     u32x4 nxt[U];
     uint32_t npp[U];
@@ -416,28 +423,6 @@ __device__ __forceinline__ void stream_dbuf(const ChunkRec *wrec, const WaveBufs
     for (int u = 0; u < U; u++) {
       cur[u] = nxt[u];
       cpp[u] = npp[u];
-    }
-  }
-}
-
-// Rolling: slot u owns chunks c = u*64 + lane + k*64U and always has one
-// load in flight; visiting a slot stores its data and re-issues the slot's
-// next load.  U loads outstanding with only 4U data registers.
-template <int U>
-__device__ __forceinline__ void stream_roll(const ChunkRec *wrec, const WaveBufs &B,
-                                            uint32_t start, uint32_t T, uint32_t lane) {
-  constexpr uint32_t STEP = kWave * U;
-  u32x4 cur[U];
-  uint32_t cpp[U];
-  stream_issue<U>(wrec, B, start, T, lane, 0, cur, cpp);
-  for (uint32_t base = 0; base < T; base += STEP) {
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const uint32_t c = base + u * kWave + lane;
-      store_chunk(wrec, B, cpp[u], c, T, cur[u]);
-      cpp[u] = locate(start, base + STEP + u * kWave, c + STEP);
-      cur[u] = __builtin_amdgcn_raw_buffer_load_b128(B.src, src_off(wrec, B, cpp[u], c + STEP, T),
-                                                     0, kAuxLd);
     }
   }
 }
@@ -484,88 +469,101 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
                  __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)));
 }
 
-// Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md,
-// "Workgroup dispatch").  With SQ_XCD_SWZ the logical block order is
-// remapped (a bijection, so placement only affects speed) so that each XCD
-// works on one contiguous range of packets: the boundary lines shared by
-// neighbouring blocks are then written through the same L2.
-__device__ __forceinline__ uint32_t logical_block() {
-#if SQ_XCD_SWZ
-  const uint32_t nb = gridDim.x, bid = blockIdx.x;
-  const uint32_t q = nb / 8, r = nb % 8, x = bid % 8, i = bid / 8;
-  return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
+// Timing-only timeline builds (SQ_TIMELINE=1, never the shipped .so): every
+// stream wave records s_memrealtime (100 MHz) at start, at the start of its
+// stream and at exit; scripts/timeline.py reads them back after one launch.
+#if SQ_TIMELINE
+constexpr uint64_t kTimelineWaves = 1u << 20;
+__device__ uint64_t g_timeline[3 * kTimelineWaves];
+extern "C" int sq_timeline_copy(uint64_t *host, uint64_t waves) {
+  if (waves > kTimelineWaves) waves = kTimelineWaves;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_timeline), 3 * 8 * waves, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+struct TimelineRec {
+  uint64_t t0, t1;
+  __device__ ~TimelineRec() {
+    if ((threadIdx.x & (kWave - 1)) == 0) {
+      const uint64_t w = (uint64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+      if (w < kTimelineWaves) {
+        g_timeline[3 * w] = t0;
+        g_timeline[3 * w + 1] = t1;
+        g_timeline[3 * w + 2] = __builtin_amdgcn_s_memrealtime();
+      }
+    }
+  }
+};
+#define SQ_TL_START const uint64_t tl0_ = __builtin_amdgcn_s_memrealtime();
+#define SQ_TL_STREAM TimelineRec tl_rec_{tl0_, __builtin_amdgcn_s_memrealtime()};
 #else
-  return blockIdx.x;
+#define SQ_TL_START
+#define SQ_TL_STREAM
 #endif
+
+// ------------------------------------------------------------ per-packet steps
+
+// Step 1, descriptor: packet p's job (addresses and length of the XOR
+// stream, salt bytes to prepend), its salt (obfuscate: the salt array;
+// deobfuscate: the first S wire bytes), whether it needs a key, and its
+// out_len (the quirk table of include/sqobfs.h).
+template <int KIND, int DIR, bool MULTI>
+__device__ __forceinline__ void describe(const KParams &P, uint32_t p, bool valid, PacketJob &J,
+                                         uint32_t (&salt)[4], bool &do_hash,
+                                         const PskEntry *&E, uint32_t &olen) {
+  constexpr uint32_t S = KIND == 0 ? kSalamanderSalt : kXPlusSalt;
+  J = {0, 0, 0, 0};
+  do_hash = false;
+  E = &P.psk0;
+  olen = 0;
+  if (!valid) return;
+  const uint64_t in_base = (uint64_t)P.in + P.in_off[p];
+  const uint64_t out_base = (uint64_t)P.out + P.out_off[p];
+  const uint32_t len = P.in_len[p];
+  bool bad = false;
+  if (MULTI) {
+    const uint32_t pid = P.psk_id[p];
+    if (pid >= P.n_psk) bad = true;
+    else E = P.psk_table + pid;
+  }
+  uint32_t cap = len;
+  if (KIND == 1 && DIR == 1 && P.in_cap) {
+    const uint32_t c = P.in_cap[p];
+    cap = c > len ? c : len;
+  }
+  if (len > kMaxPacket || cap > kMaxPacket) {
+    olen = kBadLen;
+  } else if (bad) {
+    olen = kBadPsk;
+  } else if (DIR == 0) {  // obfuscate: wire = salt || payload ^ key
+    const uint32_t *sp = reinterpret_cast<const uint32_t *>(P.salt + (uint64_t)p * S);
+#pragma unroll
+    for (uint32_t k = 0; k < S / 4; k++) salt[k] = sp[k];
+    J = {in_base, out_base + S, len, S};
+    olen = S + len;
+    do_hash = true;
+  } else if (KIND == 0 && len <= S) {
+    // salamander.go:47-49: short datagram returned as is -> copy (key 0)
+    J = {in_base, out_base, len, 0};
+    olen = len;
+  } else if (KIND == 1 && len < S) {
+    olen = 0;  // xplus.go:50-52: dropped as empty
+  } else {  // deobfuscate: salt = first S wire bytes
+    uint32_t w[4];
+    load_window(in_base, in_base + S, in_base, w);
+#pragma unroll
+    for (uint32_t k = 0; k < S / 4; k++) salt[k] = w[k];
+    J = {in_base + S, out_base, (uint64_t)cap - S, 0};
+    olen = len - S;
+    do_hash = true;
+  }
 }
 
-// ------------------------------------------------------------ main kernel
-
-template <int KIND, int DIR, bool MULTI, int U>
-__global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
-  constexpr uint32_t S = KIND == 0 ? kSalamanderSalt : kXPlusSalt;
-  __shared__ ChunkRec recs[kWavesPerBlock][kWave];
-
-  const uint32_t lane = threadIdx.x & (kWave - 1);
-  const uint32_t wv = threadIdx.x / kWave;
-  // each wave owns kPktPerWave consecutive packets (lanes >= kPktPerWave own
-  // none: they only help stream)
-  const uint64_t p64 = ((uint64_t)logical_block() * kWavesPerBlock + wv) * kPktPerWave + lane;
-  const bool valid = lane < (uint32_t)kPktPerWave && p64 < P.n;
-  const uint32_t p = (uint32_t)p64;
-
-  // ---- 1. descriptor
-  PacketJob J = {0, 0, 0, 0};
-  uint32_t salt[4] = {0u, 0u, 0u, 0u};
-  bool do_hash = false;
-  const PskEntry *E = &P.psk0;
-  if (valid) {
-    const uint64_t in_base = (uint64_t)P.in + P.in_off[p];
-    const uint64_t out_base = (uint64_t)P.out + P.out_off[p];
-    const uint32_t len = P.in_len[p];
-    uint32_t olen = 0;
-    bool bad = false;
-    if (MULTI) {
-      const uint32_t pid = P.psk_id[p];
-      if (pid >= P.n_psk) bad = true;
-      else E = P.psk_table + pid;
-    }
-    uint32_t cap = len;
-    if (KIND == 1 && DIR == 1 && P.in_cap) {
-      const uint32_t c = P.in_cap[p];
-      cap = c > len ? c : len;
-    }
-    if (len > kMaxPacket || cap > kMaxPacket) {
-      olen = kBadLen;
-    } else if (bad) {
-      olen = kBadPsk;
-    } else if (DIR == 0) {  // obfuscate: wire = salt || payload ^ key
-      const uint32_t *sp = reinterpret_cast<const uint32_t *>(P.salt + (uint64_t)p * S);
+// Step 2, key: lane-parallel, one packet per lane.
+template <int KIND>
+__device__ __forceinline__ void derive_key(bool do_hash, const PskEntry *E,
+                                           const uint32_t (&salt)[4], uint32_t (&key)[8]) {
 #pragma unroll
-      for (uint32_t k = 0; k < S / 4; k++) salt[k] = sp[k];
-      J = {in_base, out_base + S, len, S};
-      olen = S + len;
-      do_hash = true;
-    } else if (KIND == 0 && len <= S) {
-      // salamander.go:47-49: short datagram returned as is -> copy (key 0)
-      J = {in_base, out_base, len, 0};
-      olen = len;
-    } else if (KIND == 1 && len < S) {
-      olen = 0;  // xplus.go:50-52: dropped as empty
-    } else {  // deobfuscate: salt = first S wire bytes
-      uint32_t w[4];
-      load_window(in_base, in_base + S, in_base, w);
-#pragma unroll
-      for (uint32_t k = 0; k < S / 4; k++) salt[k] = w[k];
-      J = {in_base + S, out_base, (uint64_t)cap - S, 0};
-      olen = len - S;
-      do_hash = true;
-    }
-    P.out_len[p] = olen;
-  }
-
-  // ---- 2. key (lane-parallel: one packet per lane)
-  uint32_t key[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+  for (int i = 0; i < 8; i++) key[i] = 0u;
 #if SQ_ABLATE == 2 || SQ_ABLATE == 4  // timing-only build: no key derivation
   if (do_hash) { key[0] = salt[0]; key[1] = salt[1]; do_hash = false; }
 #endif
@@ -573,14 +571,29 @@ __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
     if (KIND == 0) salamander_key(E, salt, key);
     else xplus_key(E, salt, key);
   }
+}
 
+// Steps 3-5 for the packets of one wave (one per lane, any subset of lanes
+// may be idle with J.len == 0):
+//   3. split every packet's output at 16-byte boundaries of the destination
+//      into full chunks (a flat chunk space over the wave, by prefix sum) and
+//      edges (salt bytes, unaligned head, tail);
+//   4. write the edges (owner lane, byte-exact, plain stores);
+//   5. stream the flat chunk space with nt loads and stores.
+// The edge bytes of a boundary line and the nt stream stores of the rest of
+// that line merge in L2: skipping the edges (SQ_ABLATE=1) leaves those lines
+// partial and costs ~10 %.  SQ_LINE_EDGES=1 (timing builds) instead streams
+// only whole 64-byte lines and writes the boundary lines as edges: no
+// partial nt stores at all, but the longer edge phase costs ~3 % more than
+// it saves.
+template <int U>
+__device__ __forceinline__ void transform(const PacketJob &J, const uint32_t (&key)[8],
+                                          const uint32_t (&salt)[4], uint32_t lane,
+                                          ChunkRec *wrec) {
   // ---- 3. split into full chunks (flat, streamed) and edges (owner lane)
+  constexpr uint64_t kAl = SQ_LINE_EDGES ? 64 : 16;
   const uint64_t rs = J.dst_pay - J.pre, re = J.dst_pay + J.len;
-#if SQ_EXP_FULL  // timing-only: stream every output chunk as a full 16-byte store
-  const uint64_t fa = rs & ~15ull, fb = (re + 15) & ~15ull;
-#else
-  const uint64_t fa = (J.dst_pay + 15) & ~15ull, fb = re & ~15ull;
-#endif
+  const uint64_t fa = (J.dst_pay + kAl - 1) & ~(kAl - 1), fb = re & ~(kAl - 1);
   const uint32_t F = (J.len && fb > fa) ? (uint32_t)((fb - fa) >> 4) : 0u;
   uint32_t incl = F;
 #pragma unroll
@@ -593,7 +606,7 @@ __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
   const uint64_t s_first = J.src_pay + (fa - J.dst_pay);  // input of the first full chunk
   {
     uint32_t k0[4], k1[4];
-    const uint32_t r0 = (uint32_t)(fa - J.dst_pay);  // 0..15
+    const uint32_t r0 = (uint32_t)(fa - J.dst_pay) & 31u;
     keywin(key, r0, k0);
     keywin(key, r0 + 16, k1);
     const bool odd = start & 1;
@@ -604,26 +617,8 @@ __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
                     bsel(odd, k1[2], k0[2]), bsel(odd, k1[3], k0[3])};
     R.ks[1] = u32x4{bsel(odd, k0[0], k1[0]), bsel(odd, k0[1], k1[1]),
                     bsel(odd, k0[2], k1[2]), bsel(odd, k0[3], k1[3])};
-    recs[wv][lane] = R;
+    wrec[lane] = R;
   }
-
-  // ---- 4. edges: salt bytes, unaligned head, tail
-  if (!SQ_EXP_FULL && SQ_ABLATE != 1 && SQ_ABLATE != 4 && re > rs) {
-    if (F) {
-      edge_span(J, key, salt, rs, fa);
-      edge_span(J, key, salt, fb, re);
-    } else {
-      edge_span(J, key, salt, rs, re);
-    }
-  }
-
-  // LDS records visible to the whole wave (same-wave LDS ops are ordered;
-  // this is a compiler barrier plus the LDS drain)
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-
-  // ---- 5. stream the flat full-chunk space
-  if (T == 0 || SQ_ABLATE == 3) return;
-  const ChunkRec *wrec = recs[wv];
   // wave spans of the full chunks, for the two buffer resources
   const bool has = F != 0;
   const uint64_t s_lo = uniform64(wave_min64(has ? s_first : ~0ull));
@@ -632,25 +627,68 @@ __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
   const uint64_t d_hi = uniform64(wave_max64(has ? fb : 0ull));
   const bool mis = has && (s_first & 3);
   constexpr uint64_t kMaxSpan = 0xFFFFFF00ull;
-  if (__ballot(mis) == 0 && s_hi - s_lo <= kMaxSpan && d_hi - d_lo <= kMaxSpan) {
-    WaveBufs B;
+  const bool fast = T != 0 && SQ_ABLATE != 3 && __ballot(mis) == 0 &&
+                    s_hi - s_lo <= kMaxSpan && d_hi - d_lo <= kMaxSpan;
+  // LDS records visible to the whole wave (same-wave LDS ops are ordered;
+  // this is a compiler barrier plus the LDS drain)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  SQ_TL_STREAM
+
+  // ---- 4. edges: salt bytes and the partial lines at both ends.  They never
+  // overlap the full chunks' input or output bytes.
+  if (SQ_ABLATE != 1 && SQ_ABLATE != 4 && re > rs) {
+    if (F) {
+      edge_span(J, key, salt, rs, fa);
+      edge_span(J, key, salt, fb, re);
+    } else {
+      edge_span(J, key, salt, rs, re);
+    }
+  }
+
+  WaveBufs B;
+  u32x4 cur[U];
+  uint32_t cpp[U];
+  if (fast) {
     B.src = __builtin_amdgcn_make_buffer_rsrc((void *)s_lo, 0, (int)(uint32_t)(s_hi - s_lo),
                                               0x00020000);
     B.dst = __builtin_amdgcn_make_buffer_rsrc((void *)d_lo, 0, (int)(uint32_t)(d_hi - d_lo),
                                               0x00020000);
     B.sbase = (uint32_t)s_lo;
     B.dbase = (uint32_t)d_lo;
-#ifdef SQ_PRIO
-    __builtin_amdgcn_s_setprio(SQ_PRIO);
-#endif
-#if SQ_ROLL
-    stream_roll<U>(wrec, B, start, T, lane);
-#else
-    stream_dbuf<U>(wrec, B, start, T, lane);
-#endif
-  } else {
-    stream_generic(wrec, start, T, lane);
+    stream_issue<U>(wrec, B, start, T, lane, 0, cur, cpp);
   }
+
+  // ---- 5. stream the flat full-chunk space
+  if (fast) stream_loop<U>(wrec, B, start, T, lane, cur, cpp);
+  else if (T != 0 && SQ_ABLATE != 3) stream_generic(wrec, start, T, lane);
+}
+
+// ------------------------------------------------------------ kernels
+
+// The kernel: each wave owns kPktPerWave consecutive packets (descriptor ->
+// key -> transform).  A two-pass variant (a key kernel with 64 hashes per
+// wave, then short stream-only tiles of 4-32 packets per wave) was measured
+// and dropped: its key pass alone took 74-85 us on configs[1] and the stream
+// pass was no faster than this kernel's stream.
+template <int KIND, int DIR, bool MULTI, int U>
+__global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
+  __shared__ ChunkRec recs[kWavesPerBlock][kWave];
+  SQ_TL_START
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint32_t wv = threadIdx.x / kWave;
+  const uint64_t p64 = ((uint64_t)blockIdx.x * kWavesPerBlock + wv) * kPktPerWave + lane;
+  const bool valid = lane < (uint32_t)kPktPerWave && p64 < P.n;
+  const uint32_t p = (uint32_t)p64;
+  PacketJob J;
+  uint32_t salt[4] = {0u, 0u, 0u, 0u};
+  bool do_hash;
+  const PskEntry *E;
+  uint32_t olen;
+  describe<KIND, DIR, MULTI>(P, p, valid, J, salt, do_hash, E, olen);
+  if (valid) P.out_len[p] = olen;
+  uint32_t key[8];
+  derive_key<KIND>(do_hash, E, salt, key);
+  transform<U>(J, key, salt, lane, recs[wv]);
 }
 
 // ------------------------------------------------------------ PSK prepare
@@ -731,8 +769,8 @@ static int launch_one(const KParams *kp, hipStream_t s) {
   constexpr int U = SQ_U;
   constexpr uint64_t per_block = (uint64_t)kWavesPerBlock * kPktPerWave;
   const uint64_t blocks = ((uint64_t)kp->n + per_block - 1) / per_block;
-  hipLaunchKernelGGL((obfs_kernel<KIND, DIR, MULTI, U>), dim3((uint32_t)blocks),
-                     dim3(kBlock), 0, s, *kp);
+  hipLaunchKernelGGL((obfs_kernel<KIND, DIR, MULTI, U>), dim3((uint32_t)blocks), dim3(kBlock), 0,
+                     s, *kp);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
