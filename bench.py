@@ -111,7 +111,10 @@ def build_shard(torch, dev, kind, n, L, n_psk, rank, world, config, layout, firs
         in_slot = out_slot
         in_off = out_off + S
     in_bytes = int(in_slot.sum().item()) + 2 * lead
-    out_bytes = int(out_slot.sum().item()) + 2 * lead
+    # dev probe of output placement (no effect measured)
+    shift = int(os.environ.get("SQ_BENCH_OUT_SHIFT", "0")) if layout != "inplace" else 0
+    out_off = out_off + shift
+    out_bytes = int(out_slot.sum().item()) + 2 * lead + shift
     data = torch.randint(0, 256, (in_bytes,), generator=g, device=dev, dtype=torch.uint8)
     # non-payload input bytes (lead, headroom / slot padding) are zero, so a
     # decoded batch can be compared with `data` as a whole buffer
