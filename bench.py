@@ -37,6 +37,7 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 METRIC = "GiB/s payload obfuscated, device-resident, 1M×1350B Salamander @1/2/4/8 GPU"
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 PSK = b"sing-quic-mi355x-bench-psk"  # SURVEY.md 8(d) default PSK (26 B)
+SALT_KEY = bytes(range(32))  # --device-salt: fixed ChaCha20 key so the run is checkable
 
 CONFIGS = {
     # name: (kind, packets per rank, payload len (None = ragged), n_psk)
@@ -64,6 +65,9 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL) for the timing barrier/max; gloo lets several "
                          "ranks share one GPU in tests")
+    ap.add_argument("--device-salt", action="store_true",
+                    help="obfuscate with SQOBFS_FLAG_DEVICE_SALT (salts from the GPU's "
+                         "ChaCha20 generator; 2L+S bytes per packet)")
     ap.add_argument("--e2e", action="store_true",
                     help="also time the host-staged path (pinned H2D + kernel + D2H)")
     return ap.parse_args()
@@ -284,7 +288,14 @@ def main():
 
     if direction == sqobfs.DEOBFUSCATE and sh["inplace"]:
         raise SystemExit("--layout inplace is for obfuscate")
-    if direction == sqobfs.OBFUSCATE:
+    if args.device_salt and (direction != sqobfs.OBFUSCATE or sh["inplace"]):
+        raise SystemExit("--device-salt is for obfuscate, not in place")
+    if direction == sqobfs.OBFUSCATE and args.device_salt:
+        ctx.salt_key(SALT_KEY, 0)
+        b = sqobfs.make_batch(n, sh["data"], sh["in_off"], sh["lens"], sh["out"], sh["out_off"],
+                              sh["out_len"], None, sh["psk_id"], flags=sqobfs.FLAG_DEVICE_SALT)
+        alg_bytes = 2 * sh["payload_bytes"] + S * n  # no salt array read
+    elif direction == sqobfs.OBFUSCATE:
         b = sqobfs.make_batch(n, sh["data"], sh["in_off"], sh["lens"], sh["out"], sh["out_off"],
                               sh["out_len"], sh["salt"], sh["psk_id"])
         alg_bytes = 2 * sh["payload_bytes"] + 2 * S * n
@@ -340,6 +351,13 @@ def main():
         kern_avg_ms = max_over_ranks(torch, dist, kern_avg_ms, tdev)
 
     parity = None
+    if args.device_salt:
+        # the last launch's salts, from the oracle's ChaCha20 (checker only)
+        import numpy as np
+        import oracle_lib as ol
+        last = ctx.salt_seq - 1
+        salts = np.frombuffer(ol.device_salts(SALT_KEY, last, n, S), np.uint8)
+        sh["salt"] = torch.from_numpy(salts.copy()).to(dev)
     if direction == sqobfs.OBFUSCATE:
         parity = spot_check(torch, sh, kind, n, sh["out"], saved, args.warmup + args.steps)
     else:
@@ -356,10 +374,15 @@ def main():
         total_payload = sum_over_ranks(torch, dist, total_payload, tdev)
     value = total_payload / elapsed / 2**30
     achieved = alg_bytes / (kern_avg_ms * 1e-3) / 1e9
-    traffic, pmc = load_traffic(args.config, alg_bytes)
+    # the committed PMC passes are for host-salt obfuscate on the dense layout
+    traffic, pmc = (None, None)
+    if not args.device_salt and direction == sqobfs.OBFUSCATE and args.layout == "dense":
+        traffic, pmc = load_traffic(args.config, alg_bytes)
     out = {
-        "metric": METRIC if args.config == "salamander-1m" and direction == 0 else
-        f"GiB/s payload {'obfuscated' if direction == 0 else 'deobfuscated'}, device-resident, {args.config}",
+        "metric": METRIC if args.config == "salamander-1m" and direction == 0
+        and not args.device_salt else
+        f"GiB/s payload {'obfuscated' if direction == 0 else 'deobfuscated'}"
+        f"{' (device salts)' if args.device_salt else ''}, device-resident, {args.config}",
         "value": round(value, 3),
         "unit": "GiB/s",
         "n_gpus": world,
@@ -380,6 +403,7 @@ def main():
                          "salamander-16m-256psk": "configs[4]: Salamander, 16,777,216 x 1350 B, "
                                                   "256 PSKs round-robin, sharded over ranks"}[args.config],
             "direction": args.direction,
+            "salts": "device ChaCha20 (SQOBFS_FLAG_DEVICE_SALT)" if args.device_salt else "host array",
             "packets_per_gpu": n,
             "payload_bytes_per_gpu": sh["payload_bytes"],
             "layout": args.layout,
@@ -396,7 +420,8 @@ def main():
             "kernel_avg_us": round(kern_avg_ms * 1e3, 2),
             "kernel_min_us": round(kern_ms[0] * 1e3, 2),
             "algorithmic_bytes_per_launch": alg_bytes,
-            "bytes_rule": "obfuscate 2L+2S per packet, deobfuscate 2L+S (SURVEY.md 8(d))",
+            "bytes_rule": "obfuscate 2L+2S per packet (2L+S with device salts), "
+                          "deobfuscate 2L+S (SURVEY.md 8(d))",
         },
         "parity_spot_check": parity,
     }

@@ -31,7 +31,9 @@
  *
  * Semantics per packet i (S = 8 Salamander, 16 XPlus; key = BLAKE2b-256 or
  * SHA-256 of psk || salt):
- *   obfuscate:   out[out_off[i] .. +S)       = salt[i*S .. +S)
+ *   obfuscate:   out[out_off[i] .. +S)       = salt[i*S .. +S) (or the
+ *                                              device salt, see
+ *                                              SQOBFS_FLAG_DEVICE_SALT)
  *                out[out_off[i]+S+j]         = in[in_off[i]+j] ^ key[j % 32],
  *                                              j < in_len[i]
  *                out_len[i] = S + in_len[i]
@@ -62,7 +64,7 @@
 extern "C" {
 #endif
 
-#define SQOBFS_ABI_VERSION 1
+#define SQOBFS_ABI_VERSION 2
 
 #define SQOBFS_SALAMANDER_SALT_LEN 8 /* hysteria2/salamander.go:15 */
 #define SQOBFS_XPLUS_SALT_LEN 16     /* hysteria/xplus.go:17 */
@@ -79,6 +81,23 @@ extern "C" {
 /* batch flag (sqobfs_run_host): output bytes outside the packets' output
  * regions need not be preserved (skips copying the output range in) */
 #define SQOBFS_FLAG_OUT_UNINIT 1u
+
+/* batch flag (obfuscate only): generate every packet's salt on the GPU
+ * instead of reading `salt` -- replaces the per-packet host RNG of
+ * SalamanderPacketConn.WriteTo (buf.WriteRandom, salamander.go:60,83,98)
+ * and XPlusPacketConn.WriteTo (math/rand under a mutex, xplus.go:67-69).
+ * The salts of one launch are the ChaCha20 keystream (RFC 8439 block
+ * function, 20 rounds):
+ *     salts[0 .. n*S) = ChaCha20(key, nonce, counter 0..)[0 .. n*S)
+ *     key   = the context's 32-byte salt key (random from getrandom(2) at
+ *             sqobfs_open, or set by sqobfs_salt_key)
+ *     nonce = "sqob" || le64(seq), seq = the context's launch sequence
+ *             number, incremented by every launch that uses this flag
+ * i.e. packet i's salt is bytes [(i % (64/S))*S, +S) of keystream block
+ * i / (64/S).  A (key, seq) pair is never reused by a context, so salts are
+ * unpredictable without the key and never repeat.  `salt` is ignored;
+ * `salt_out`, if not NULL, receives the n*S generated salts. */
+#define SQOBFS_FLAG_DEVICE_SALT 2u
 
 /* out_len value written for a packet whose psk_id is out of range */
 #define SQOBFS_BAD_PSK 0xFFFFFFFFu
@@ -105,6 +124,8 @@ typedef struct sqobfs_batch {
   const uint16_t *psk_id;   /* [n] keyring index per packet, NULL = all use 0 */
   const uint32_t *in_cap;   /* XPlus deobfuscate only: [n] read-buffer length
                                len(p) >= in_len (xplus.go:55); NULL = in_len */
+  uint8_t *salt_out;        /* SQOBFS_FLAG_DEVICE_SALT: [n*S] receives the
+                               generated salts (4-byte aligned), or NULL */
 } sqobfs_batch;
 
 int sqobfs_abi_version(void);
@@ -115,7 +136,8 @@ const char *sqobfs_strerror(int status);
 int sqobfs_device_count(int *count);
 
 /* One context per GPU.  Thread-safe: device launches only read immutable
- * state; sqobfs_run_host serialises on an internal lock. */
+ * state (and bump an atomic salt sequence number); sqobfs_run_host
+ * serialises on an internal lock. */
 int sqobfs_open(int device, sqobfs_ctx **out);
 void sqobfs_close(sqobfs_ctx *ctx);
 /* the context's own non-blocking HIP stream (as void*), for callers that
@@ -123,6 +145,13 @@ void sqobfs_close(sqobfs_ctx *ctx);
 void *sqobfs_stream(sqobfs_ctx *ctx);
 /* wait for all work on `stream` (NULL = the HIP null stream) */
 int sqobfs_sync(sqobfs_ctx *ctx, void *stream);
+
+/* Set the context's salt key and next launch sequence number for
+ * SQOBFS_FLAG_DEVICE_SALT (replay / tests; sqobfs_open draws a random key and
+ * starts at 0).  Not to be called concurrently with launches on the context. */
+int sqobfs_salt_key(sqobfs_ctx *ctx, const uint8_t key[32], uint64_t next_seq);
+/* The sequence number the next SQOBFS_FLAG_DEVICE_SALT launch will use. */
+uint64_t sqobfs_salt_seq(const sqobfs_ctx *ctx);
 
 /* Upload `count` pre-shared keys (host memory: psk k = blob[off[k] .. +len[k]])
  * and derive each one's per-PSK hash state on the GPU.  kind selects the
@@ -156,7 +185,9 @@ int sqobfs_launch(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
  * streams and overlap.  Pinned caller buffers (sqobfs_host_alloc) are
  * copied by DMA directly; pageable ones go through pinned staging.  Output
  * bytes outside the packets' output regions are preserved unless
- * flags has SQOBFS_FLAG_OUT_UNINIT. */
+ * flags has SQOBFS_FLAG_OUT_UNINIT.  With SQOBFS_FLAG_DEVICE_SALT every
+ * chunk is one launch with its own sequence number (salts of chunk c =
+ * keystream(seq_c) over the chunk's packets, in packet order). */
 int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
                     const sqobfs_batch *host_batch);
 

@@ -195,6 +195,67 @@ void or_sha256(const uint8_t *in, size_t len, uint8_t out[32]) {
 /* (SURVEY.md section 5 explains the aliasing hazard in the Go code).   */
 /* ------------------------------------------------------------------ */
 
+/* ---------------------------------------------------------------- ChaCha20
+ * RFC 8439 section 2.3, restated byte-exactly (little-endian words).  The
+ * device salt generator (SQOBFS_FLAG_DEVICE_SALT) replaces the host RNG of
+ * salamander.go:60,83,98 (sing buf.WriteRandom) and xplus.go:67-69
+ * (math/rand); this is its checker, pinned by RFC 8439 section 2.3.2 and by
+ * OpenSSL's chacha20 keystream (tests/golden/chacha20.json). */
+static uint32_t rotl32(uint32_t x, unsigned n) { return (x << n) | (x >> (32 - n)); }
+static uint32_t load32le(const uint8_t *p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) |
+         ((uint32_t)p[3] << 24);
+}
+#define OR_QR(a, b, c, d)                   \
+  do {                                      \
+    a += b; d ^= a; d = rotl32(d, 16);      \
+    c += d; b ^= c; b = rotl32(b, 12);      \
+    a += b; d ^= a; d = rotl32(d, 8);       \
+    c += d; b ^= c; b = rotl32(b, 7);       \
+  } while (0)
+
+void or_chacha20_block(const uint8_t key[32], uint32_t counter, const uint8_t nonce[12],
+                       uint8_t out[64]) {
+  uint32_t in[16], x[16];
+  in[0] = 0x61707865u; in[1] = 0x3320646eu; in[2] = 0x79622d32u; in[3] = 0x6b206574u;
+  for (int i = 0; i < 8; i++) in[4 + i] = load32le(key + 4 * i);
+  in[12] = counter;
+  for (int i = 0; i < 3; i++) in[13 + i] = load32le(nonce + 4 * i);
+  for (int i = 0; i < 16; i++) x[i] = in[i];
+  for (int r = 0; r < 10; r++) {
+    OR_QR(x[0], x[4], x[8], x[12]);
+    OR_QR(x[1], x[5], x[9], x[13]);
+    OR_QR(x[2], x[6], x[10], x[14]);
+    OR_QR(x[3], x[7], x[11], x[15]);
+    OR_QR(x[0], x[5], x[10], x[15]);
+    OR_QR(x[1], x[6], x[11], x[12]);
+    OR_QR(x[2], x[7], x[8], x[13]);
+    OR_QR(x[3], x[4], x[9], x[14]);
+  }
+  for (int i = 0; i < 16; i++) {
+    const uint32_t v = x[i] + in[i];
+    for (int k = 0; k < 4; k++) out[4 * i + k] = (uint8_t)(v >> (8 * k));
+  }
+}
+#undef OR_QR
+
+void or_chacha20_stream(const uint8_t key[32], const uint8_t nonce[12], uint32_t counter0,
+                        uint8_t *out, size_t len) {
+  uint8_t blk[64];
+  for (size_t pos = 0; pos < len; pos += 64) {
+    or_chacha20_block(key, counter0 + (uint32_t)(pos / 64), nonce, blk);
+    const size_t take = len - pos < 64 ? len - pos : 64;
+    memcpy(out + pos, blk, take);
+  }
+}
+
+void or_device_salts(const uint8_t key[32], uint64_t seq, uint32_t n, uint32_t S,
+                     uint8_t *out) {
+  uint8_t nonce[12] = {'s', 'q', 'o', 'b'};
+  for (int k = 0; k < 8; k++) nonce[4 + k] = (uint8_t)(seq >> (8 * k));
+  or_chacha20_stream(key, nonce, 0, out, (size_t)n * S);
+}
+
 static void hash_psk_salt(int kind, const uint8_t *psk, size_t psk_len,
                           const uint8_t *salt, size_t salt_len,
                           uint8_t key[32]) {

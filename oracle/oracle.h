@@ -46,6 +46,18 @@ void or_blake2b(const uint8_t *in, size_t len, uint8_t *out, size_t outlen);
 /* FIPS 180-4 SHA-256 (== sha256.Sum256). */
 void or_sha256(const uint8_t *in, size_t len, uint8_t out[32]);
 
+/* RFC 8439 section 2.3 ChaCha20 block function (20 rounds): 64 keystream
+ * bytes for (key, 32-bit block counter, 96-bit nonce). */
+void or_chacha20_block(const uint8_t key[32], uint32_t counter,
+                       const uint8_t nonce[12], uint8_t out[64]);
+/* len keystream bytes starting at block counter0 (RFC 8439 section 2.4). */
+void or_chacha20_stream(const uint8_t key[32], const uint8_t nonce[12],
+                        uint32_t counter0, uint8_t *out, size_t len);
+/* Device salts of one launch (include/sqobfs.h, SQOBFS_FLAG_DEVICE_SALT):
+ * out[0 .. n*S) = ChaCha20(key, "sqob" || le64(seq), counter 0..). */
+void or_device_salts(const uint8_t key[32], uint64_t seq, uint32_t n,
+                     uint32_t S, uint8_t *out);
+
 /* Salamander key: BLAKE2b-256(psk || salt[0:8])  (salamander.go:50,61,84,99) */
 void or_salamander_key(const uint8_t *psk, size_t psk_len,
                        const uint8_t salt[8], uint8_t key[32]);

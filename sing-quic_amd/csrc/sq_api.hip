@@ -9,7 +9,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <sys/random.h>
+
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <new>
 #include <thread>
@@ -29,6 +32,9 @@ struct sqobfs_ctx {
   uint8_t *dev = nullptr;
   size_t dev_cap = 0;
   hipEvent_t ev[16] = {};  // pipeline events of sqobfs_run_host
+  // SQOBFS_FLAG_DEVICE_SALT: ChaCha20 key and the next launch sequence number
+  uint32_t salt_key[8] = {};
+  std::atomic<uint64_t> salt_seq{0};
 };
 
 namespace {
@@ -72,17 +78,23 @@ hipStream_t pick_stream(sqobfs_ctx *ctx, void *stream) {
 
 int check_batch_shape(const sqobfs_batch *b, int dir) {
   if (!b) return SQ_EINVAL;
-  if (b->flags & ~(uint32_t)SQOBFS_FLAG_OUT_UNINIT) return SQ_EINVAL;
+  if (b->flags & ~(uint32_t)(SQOBFS_FLAG_OUT_UNINIT | SQOBFS_FLAG_DEVICE_SALT)) return SQ_EINVAL;
+  const bool dev_salt = b->flags & SQOBFS_FLAG_DEVICE_SALT;
+  if (dev_salt && dir != SQOBFS_OBFUSCATE) return SQ_EINVAL;
   if (b->n == 0) return SQ_OK;
   if (!b->in || !b->in_off || !b->in_len || !b->out || !b->out_off || !b->out_len)
     return SQ_EINVAL;
-  if (dir == SQOBFS_OBFUSCATE) {
+  if (dir == SQOBFS_OBFUSCATE && !dev_salt) {
     if (!b->salt || ((uintptr_t)b->salt & 3)) return SQ_EINVAL;
   }
+  if (dev_salt && ((uintptr_t)b->salt_out & 3)) return SQ_EINVAL;
   return SQ_OK;
 }
 
-sq::KParams make_params(const sqobfs_keyring *kr, const sqobfs_batch *b) {
+// "sqob" || le64(seq): the ChaCha20 nonce of one device-salt launch
+constexpr uint32_t kSaltDomain = 0x626f7173u;  // bytes 's' 'q' 'o' 'b'
+
+sq::KParams make_params(sqobfs_ctx *ctx, const sqobfs_keyring *kr, const sqobfs_batch *b) {
   sq::KParams kp;
   memset(&kp, 0, sizeof kp);
   kp.in = b->in;
@@ -98,6 +110,15 @@ sq::KParams make_params(const sqobfs_keyring *kr, const sqobfs_batch *b) {
   kp.n = b->n;
   kp.n_psk = kr->count;
   kp.psk0 = kr->host0;
+  if (b->flags & SQOBFS_FLAG_DEVICE_SALT) {
+    const uint64_t seq = ctx->salt_seq.fetch_add(1);
+    kp.device_salt = 1;
+    kp.salt_out = b->salt_out;
+    memcpy(kp.salt_key, ctx->salt_key, sizeof kp.salt_key);
+    kp.salt_nonce[0] = kSaltDomain;
+    kp.salt_nonce[1] = (uint32_t)seq;
+    kp.salt_nonce[2] = (uint32_t)(seq >> 32);
+  }
   return kp;
 }
 
@@ -172,6 +193,19 @@ int sqobfs_open(int device, sqobfs_ctx **out) {
   sqobfs_ctx *c = new (std::nothrow) sqobfs_ctx();
   if (!c) return SQ_ENOMEM;
   c->device = device;
+  {
+    uint8_t k[32];
+    size_t got = 0;
+    while (got < sizeof k) {
+      const ssize_t r = getrandom(k + got, sizeof k - got, 0);
+      if (r < 0) {
+        delete c;
+        return SQ_EDEVICE;
+      }
+      got += (size_t)r;
+    }
+    memcpy(c->salt_key, k, sizeof k);
+  }
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->h2d, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking);
@@ -198,6 +232,15 @@ void sqobfs_close(sqobfs_ctx *ctx) {
     if (e) (void)hipEventDestroy(e);
   delete ctx;
 }
+
+int sqobfs_salt_key(sqobfs_ctx *ctx, const uint8_t key[32], uint64_t next_seq) {
+  if (!ctx || !key) return SQ_EINVAL;
+  memcpy(ctx->salt_key, key, sizeof ctx->salt_key);  // little-endian words
+  ctx->salt_seq.store(next_seq);
+  return SQ_OK;
+}
+
+uint64_t sqobfs_salt_seq(const sqobfs_ctx *ctx) { return ctx ? ctx->salt_seq.load() : 0; }
 
 void *sqobfs_stream(sqobfs_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
 
@@ -271,7 +314,7 @@ int sqobfs_launch(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir, const sqob
   const int st = check_batch_shape(b, dir);
   if (st != SQ_OK || b->n == 0) return st;
   SQ_TRY(hipSetDevice(ctx->device));
-  const sq::KParams kp = make_params(kr, b);
+  const sq::KParams kp = make_params(ctx, kr, b);
   return sq_launch_obfs(kr->kind, dir, &kp, pick_stream(ctx, stream));
 }
 
@@ -390,7 +433,10 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
   const size_t o_inlen = o;    o = align_up(o + 4ull * n, A);
   const size_t o_outoff = o;   o = align_up(o + 8ull * n, A);
   const size_t o_outlen = o;   o = align_up(o + 4ull * n, A);
-  const size_t o_salt = o;     o = align_up(o + (dir == SQOBFS_OBFUSCATE ? S * n : 0), A);
+  const bool dev_salt = hb->flags & SQOBFS_FLAG_DEVICE_SALT;
+  const size_t o_saltout = o;  o = align_up(o + (dev_salt && hb->salt_out ? S * n : 0), A);
+  const size_t o_salt = o;
+  o = align_up(o + (dir == SQOBFS_OBFUSCATE && !dev_salt ? S * n : 0), A);
   const size_t o_pid = o;      o = align_up(o + (hb->psk_id ? 2ull * n : 0), A);
   const size_t o_cap = o;      o = align_up(o + (hb->in_cap ? 4ull * n : 0), A);
   const size_t total = o;
@@ -419,7 +465,7 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
   memcpy(H + o_inoff, hb->in_off, 8ull * n);
   memcpy(H + o_inlen, hb->in_len, 4ull * n);
   memcpy(H + o_outoff, hb->out_off, 8ull * n);
-  if (dir == SQOBFS_OBFUSCATE) memcpy(H + o_salt, hb->salt, S * n);
+  if (dir == SQOBFS_OBFUSCATE && !dev_salt) memcpy(H + o_salt, hb->salt, S * n);
   if (hb->psk_id) memcpy(H + o_pid, hb->psk_id, 2ull * n);
   if (hb->in_cap) memcpy(H + o_cap, hb->in_cap, 4ull * n);
   SQ_TRY(hipMemcpyAsync(D + o_inoff, H + o_inoff, o_outlen - o_inoff, hipMemcpyHostToDevice,
@@ -461,11 +507,12 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
     db.out = D + o_out;
     db.out_off = (const uint64_t *)(D + o_outoff) + ri.p0;
     db.out_len = (uint32_t *)(D + o_outlen) + ri.p0;
-    db.salt = dir == SQOBFS_OBFUSCATE ? D + o_salt + S * ri.p0 : nullptr;
+    db.salt = dir == SQOBFS_OBFUSCATE && !dev_salt ? D + o_salt + S * ri.p0 : nullptr;
+    db.salt_out = dev_salt && hb->salt_out ? D + o_saltout + S * ri.p0 : nullptr;
     db.psk_id = hb->psk_id ? (const uint16_t *)(D + o_pid) + ri.p0 : nullptr;
     db.in_cap = hb->in_cap ? (const uint32_t *)(D + o_cap) + ri.p0 : nullptr;
     if (db.n) {
-      const sq::KParams kp = make_params(kr, &db);
+      const sq::KParams kp = make_params(ctx, kr, &db);
       st = sq_launch_obfs(kind, dir, &kp, ctx->stream);
       if (st != SQ_OK) return st;
     }
@@ -478,6 +525,8 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
     }
   }
   SQ_TRY(hipMemcpyAsync(H + o_outlen, D + o_outlen, 4ull * n, hipMemcpyDeviceToHost, ctx->d2h));
+  if (dev_salt && hb->salt_out)
+    SQ_TRY(hipMemcpyAsync(H + o_saltout, D + o_saltout, S * n, hipMemcpyDeviceToHost, ctx->d2h));
   SQ_TRY(hipStreamSynchronize(ctx->d2h));
   // pageable output: copy back in chunk order (later chunks win where
   // ranges interleave, matching the device order)
@@ -486,6 +535,7 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
       if (rout[c].hi > rout[c].lo)
         par_memcpy(hb->out + rout[c].lo, H + o_out + rout[c].lo, rout[c].hi - rout[c].lo);
   memcpy(hb->out_len, H + o_outlen, 4ull * n);
+  if (dev_salt && hb->salt_out) memcpy(hb->salt_out, H + o_saltout, S * n);
   return SQ_OK;
 }
 

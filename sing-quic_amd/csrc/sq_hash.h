@@ -186,4 +186,44 @@ __device__ __host__ inline void s2_init(uint32_t st[8]) {
   st[7] = 0x5be0cd19;
 }
 
+// ---------------------------------------------------------------- ChaCha20
+
+// RFC 8439 section 2.3 block function (20 rounds), one block per lane.
+// Used as the device salt generator (SQOBFS_FLAG_DEVICE_SALT): it replaces
+// the host RNG reads of salamander.go:60,83,98 (buf.WriteRandom) and
+// xplus.go:67-69 (math/rand).  Rotations are v_alignbit_b32.
+__device__ __forceinline__ uint32_t cc_rotl(uint32_t x, int n) {
+  return __builtin_amdgcn_alignbit(x, x, 32 - n);
+}
+#define SQ_CC_QR(a, b, c, d)                  \
+  a += b; d ^= a; d = cc_rotl(d, 16);         \
+  c += d; b ^= c; b = cc_rotl(b, 12);         \
+  a += b; d ^= a; d = cc_rotl(d, 8);          \
+  c += d; b ^= c; b = cc_rotl(b, 7);
+
+__device__ __forceinline__ void chacha20_block(const uint32_t (&key)[8], uint32_t counter,
+                                               const uint32_t (&nonce)[3],
+                                               uint32_t (&out)[16]) {
+  uint32_t in[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
+                     key[0], key[1], key[2], key[3], key[4], key[5], key[6], key[7],
+                     counter, nonce[0], nonce[1], nonce[2]};
+  uint32_t x[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) x[i] = in[i];
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    SQ_CC_QR(x[0], x[4], x[8], x[12])
+    SQ_CC_QR(x[1], x[5], x[9], x[13])
+    SQ_CC_QR(x[2], x[6], x[10], x[14])
+    SQ_CC_QR(x[3], x[7], x[11], x[15])
+    SQ_CC_QR(x[0], x[5], x[10], x[15])
+    SQ_CC_QR(x[1], x[6], x[11], x[12])
+    SQ_CC_QR(x[2], x[7], x[8], x[13])
+    SQ_CC_QR(x[3], x[4], x[9], x[14])
+  }
+#pragma unroll
+  for (int i = 0; i < 16; i++) out[i] = x[i] + in[i];
+}
+#undef SQ_CC_QR
+
 }  // namespace sq

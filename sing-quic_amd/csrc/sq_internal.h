@@ -53,8 +53,12 @@ struct KParams {
   const uint16_t *psk_id;
   const uint32_t *in_cap;
   const PskEntry *psk_table;
+  uint8_t *salt_out;        // device salts: [n*S] copy of the generated salts, or NULL
   uint32_t n;
   uint32_t n_psk;
+  uint32_t device_salt;     // 1: obfuscate salts from ChaCha20(salt_key, salt_nonce)
+  uint32_t salt_key[8];
+  uint32_t salt_nonce[3];
   PskEntry psk0;
 };
 

@@ -502,6 +502,35 @@ struct TimelineRec {
 
 // ------------------------------------------------------------ per-packet steps
 
+// Device salt of packet p (SQOBFS_FLAG_DEVICE_SALT): bytes [(p % (64/S))*S,
+// +S) of ChaCha20 keystream block p / (64/S), so the batch's salts are the
+// keystream's first n*S bytes.  Each lane computes its own packet's block
+// (lanes sharing a block compute it redundantly: same instruction stream).
+template <uint32_t S>
+__device__ __forceinline__ void device_salt(const KParams &P, uint32_t p, uint32_t (&salt)[4]) {
+  constexpr uint32_t per_block = 64 / S;  // 8 Salamander, 4 XPlus
+  uint32_t blk[16];
+  chacha20_block(P.salt_key, p / per_block, P.salt_nonce, blk);
+  // word offset (p % per_block) * S/4: barrel-select S/4 words
+  const uint32_t q = (p % per_block) * (S / 4);
+  uint32_t y[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) y[j] = blk[j];
+#pragma unroll
+  for (int sh = 8; sh >= 1; sh >>= 1) {
+    const bool b = q & sh;
+#pragma unroll
+    for (int j = 0; j + sh < 16; j++) y[j] = bsel(b, y[j + sh], y[j]);
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < S / 4; k++) salt[k] = y[k];
+  if (P.salt_out) {
+    uint32_t *so = reinterpret_cast<uint32_t *>(P.salt_out + (uint64_t)p * S);
+#pragma unroll
+    for (uint32_t k = 0; k < S / 4; k++) so[k] = salt[k];
+  }
+}
+
 // Step 1, descriptor: packet p's job (addresses and length of the XOR
 // stream, salt bytes to prepend), its salt (obfuscate: the salt array;
 // deobfuscate: the first S wire bytes), whether it needs a key, and its
@@ -535,9 +564,13 @@ __device__ __forceinline__ void describe(const KParams &P, uint32_t p, bool vali
   } else if (bad) {
     olen = kBadPsk;
   } else if (DIR == 0) {  // obfuscate: wire = salt || payload ^ key
-    const uint32_t *sp = reinterpret_cast<const uint32_t *>(P.salt + (uint64_t)p * S);
+    if (P.device_salt) {
+      device_salt<S>(P, p, salt);
+    } else {
+      const uint32_t *sp = reinterpret_cast<const uint32_t *>(P.salt + (uint64_t)p * S);
 #pragma unroll
-    for (uint32_t k = 0; k < S / 4; k++) salt[k] = sp[k];
+      for (uint32_t k = 0; k < S / 4; k++) salt[k] = sp[k];
+    }
     J = {in_base, out_base + S, len, S};
     olen = S + len;
     do_hash = true;

@@ -31,6 +31,7 @@ OBFS_TYPE_SALAMANDER = "salamander"  # hysteria2/salamander.go:17
 SQ_OK, SQ_EINVAL, SQ_ENOMEM, SQ_EDEVICE, SQ_ENODEV, SQ_EPSK = 0, -1, -2, -3, -4, -5
 BAD_PSK = 0xFFFFFFFF
 FLAG_OUT_UNINIT = 1  # run_host: bytes between output regions need not be kept
+FLAG_DEVICE_SALT = 2  # obfuscate: salts from the GPU's ChaCha20 generator
 
 
 class SqError(RuntimeError):
@@ -52,6 +53,7 @@ class Batch(ctypes.Structure):
         ("salt", ctypes.c_void_p),
         ("psk_id", ctypes.c_void_p),
         ("in_cap", ctypes.c_void_p),
+        ("salt_out", ctypes.c_void_p),
     ]
 
 
@@ -95,6 +97,9 @@ def lib() -> ctypes.CDLL:
     L.sqobfs_build_info.restype = ctypes.c_char_p
     L.sqobfs_build_info.argtypes = []
     L.sqobfs_host_free.restype = None
+    L.sqobfs_salt_key.argtypes = [vp, vp, ctypes.c_uint64]
+    L.sqobfs_salt_seq.argtypes = [vp]
+    L.sqobfs_salt_seq.restype = ctypes.c_uint64
     _lib = L
     return L
 
@@ -167,6 +172,15 @@ class Context:
     def sync(self, stream: int | None = None) -> None:
         _check(lib().sqobfs_sync(self.handle, stream), "sqobfs_sync")
 
+    def salt_key(self, key: bytes, next_seq: int = 0) -> None:
+        """Deterministic device-salt key and sequence (tests / replay)."""
+        assert len(key) == 32
+        _check(lib().sqobfs_salt_key(self.handle, key, next_seq), "sqobfs_salt_key")
+
+    @property
+    def salt_seq(self) -> int:
+        return lib().sqobfs_salt_seq(self.handle)
+
 
 class Keyring:
     """Device copy of the PSK(s): the `password` field of
@@ -201,10 +215,10 @@ class Keyring:
 
 
 def make_batch(n, in_, in_off, in_len, out, out_off, out_len, salt=None,
-               psk_id=None, in_cap=None) -> Batch:
+               psk_id=None, in_cap=None, salt_out=None, flags=0) -> Batch:
     """Batch from numpy arrays (host) or torch tensors (device)."""
-    return Batch(n, 0, _ptr(in_), _ptr(in_off), _ptr(in_len), _ptr(out), _ptr(out_off),
-                 _ptr(out_len), _ptr(salt), _ptr(psk_id), _ptr(in_cap))
+    return Batch(n, flags, _ptr(in_), _ptr(in_off), _ptr(in_len), _ptr(out), _ptr(out_off),
+                 _ptr(out_len), _ptr(salt), _ptr(psk_id), _ptr(in_cap), _ptr(salt_out))
 
 
 def launch(ctx: Context, kr: Keyring, direction: int, batch: Batch,
@@ -233,16 +247,16 @@ class HostBatch:
     psk_id: np.ndarray | None = None
     in_cap: np.ndarray | None = None
     flags: int = 0
+    salt_out: np.ndarray | None = None
 
     @property
     def n(self) -> int:
         return int(self.in_len.shape[0])
 
     def as_batch(self) -> Batch:
-        b = make_batch(self.n, self.data, self.in_off, self.in_len, self.out,
-                       self.out_off, self.out_len, self.salt, self.psk_id, self.in_cap)
-        b.flags = self.flags
-        return b
+        return make_batch(self.n, self.data, self.in_off, self.in_len, self.out,
+                          self.out_off, self.out_len, self.salt, self.psk_id, self.in_cap,
+                          self.salt_out, self.flags)
 
 
 class PinnedArray:

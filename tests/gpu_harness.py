@@ -89,7 +89,8 @@ def clone(hb: HostBatch) -> HostBatch:
     out = data if inplace else hb.out.copy()
     c = lambda a: None if a is None else a.copy()  # noqa: E731
     return HostBatch(data, hb.in_off.copy(), hb.in_len.copy(), out, hb.out_off.copy(),
-                     hb.out_len.copy(), c(hb.salt), c(hb.psk_id), c(hb.in_cap))
+                     hb.out_len.copy(), c(hb.salt), c(hb.psk_id), c(hb.in_cap), hb.flags,
+                     c(hb.salt_out))
 
 
 def run_oracle(kind, direction, psks, hb: HostBatch, nthreads=4) -> HostBatch:
@@ -111,14 +112,18 @@ def run_device(ctx: sqobfs.Context, kr: sqobfs.Keyring, direction: int, hb: Host
     d_data = t(hb.data)
     d_out = d_data if inplace else t(hb.out)
     d = dict(in_off=t(hb.in_off), in_len=t(hb.in_len), out_off=t(hb.out_off),
-             out_len=t(hb.out_len), salt=t(hb.salt), psk_id=t(hb.psk_id), in_cap=t(hb.in_cap))
+             out_len=t(hb.out_len), salt=t(hb.salt), psk_id=t(hb.psk_id), in_cap=t(hb.in_cap),
+             salt_out=t(hb.salt_out))
     b = sqobfs.make_batch(hb.n, d_data, d["in_off"], d["in_len"], d_out, d["out_off"],
-                          d["out_len"], d["salt"], d["psk_id"], d["in_cap"])
+                          d["out_len"], d["salt"], d["psk_id"], d["in_cap"], d["salt_out"],
+                          hb.flags)
     s = torch.cuda.current_stream(dev).cuda_stream if stream is None else stream
     sqobfs.launch(ctx, kr, direction, b, s)
     torch.cuda.synchronize(dev)
     hb.out[:] = d_out.cpu().numpy()
     hb.out_len[:] = d["out_len"].cpu().numpy()
+    if hb.salt_out is not None:
+        hb.salt_out[:] = d["salt_out"].cpu().numpy()
 
 
 def run_host(ctx, kr, direction, hb: HostBatch) -> None:

@@ -56,6 +56,12 @@ def lib() -> ctypes.CDLL:
         L.or_xplus_read.restype = ctypes.c_long
         L.or_xplus_write_vectorised.argtypes = [vp, sz, vp, vp, vp, sz]
         L.or_xplus_write_vectorised.restype = None
+        L.or_chacha20_block.argtypes = [vp, ctypes.c_uint32, vp, vp]
+        L.or_chacha20_block.restype = None
+        L.or_chacha20_stream.argtypes = [vp, vp, ctypes.c_uint32, vp, sz]
+        L.or_chacha20_stream.restype = None
+        L.or_device_salts.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, vp]
+        L.or_device_salts.restype = None
         L.or_batch_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(OrPsks),
                                    ctypes.POINTER(OrBatch), ctypes.c_int]
         L.or_fnv64.argtypes = [vp, sz, ctypes.c_uint64]
@@ -162,3 +168,19 @@ def batch_run(kind: int, direction: int, psks: list[bytes], hb, nthreads: int = 
 
 def fnv64(a: np.ndarray, h: int = 0) -> int:
     return lib().or_fnv64(a.ctypes.data, a.nbytes, h)
+
+
+def chacha20_stream(key: bytes, nonce: bytes, counter0: int, n: int) -> bytes:
+    """RFC 8439 keystream (n bytes from block counter0), C restatement."""
+    assert len(key) == 32 and len(nonce) == 12
+    out = ctypes.create_string_buffer(max(n, 1))
+    lib().or_chacha20_stream(key, nonce, counter0, out, n)
+    return out.raw[:n]
+
+
+def device_salts(key: bytes, seq: int, n: int, S: int) -> bytes:
+    """Salts of one SQOBFS_FLAG_DEVICE_SALT launch (include/sqobfs.h)."""
+    assert len(key) == 32
+    out = ctypes.create_string_buffer(max(n * S, 1))
+    lib().or_device_salts(key, seq, n, S, out)
+    return out.raw[:n * S]

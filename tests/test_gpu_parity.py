@@ -315,3 +315,52 @@ def test_round_trip_random(ctx):
         for i, L in enumerate(lens):
             a, b = int(hb.in_off[i]), int(oo[i])
             assert back.out[b:b + int(L)].tobytes() == hb.data[a:a + int(L)].tobytes()
+
+
+# ---------------------------------------------------------------- device salts
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("path", ["device", "host"])
+@pytest.mark.parametrize("with_out", [True, False])
+def test_device_salt(ctx, kind, path, with_out):
+    """SQOBFS_FLAG_DEVICE_SALT: salts are the ChaCha20 keystream of
+    (context key, 'sqob' || le64(seq)); the wire is the oracle's obfuscation
+    with exactly those salts; `salt` is ignored; seq advances per launch."""
+    import oracle_lib as ol
+    S = sqobfs.SALT_LEN[kind]
+    rng = np.random.Generator(np.random.PCG64(900 + kind + 2 * (path == "host") + 4 * with_out))
+    n = 3000  # one run_host chunk
+    lens = rng.integers(0, 1500, n)
+    psks = [PSK, b"q" * 77]
+    ids = rng.integers(0, 2, n)
+    key = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+    seq0 = int(rng.integers(0, 2**40))
+    for launch in range(2):
+        hb = gh.make_case(rng, kind, OBFUSCATE, lens, psks, psk_ids=ids, in_align=1, out_align=1)
+        expect = np.frombuffer(ol.device_salts(key, seq0 + launch, n, S), np.uint8)
+        ref_in = gh.clone(hb)
+        ref_in.salt = expect.copy()
+        ref = gh.run_oracle(kind, OBFUSCATE, psks, ref_in)
+        hb.salt = rng.integers(0, 256, n * S, dtype=np.uint8)  # must be ignored
+        hb.flags = sqobfs.FLAG_DEVICE_SALT
+        hb.salt_out = np.zeros(n * S, np.uint8) if with_out else None
+        if launch == 0:
+            ctx.salt_key(key, seq0)
+        with sqobfs.Keyring(ctx, kind, psks) as kr:
+            if path == "device":
+                gh.run_device(ctx, kr, OBFUSCATE, hb)
+            else:
+                gh.run_host(ctx, kr, OBFUSCATE, hb)
+        assert ctx.salt_seq == seq0 + launch + 1
+        if with_out:
+            assert np.array_equal(hb.salt_out, expect), "salt_out differs from ChaCha20"
+        gh.assert_same(hb, ref, f"device salt {path} launch {launch}")
+
+
+def test_device_salt_rejected_for_deobfuscate(ctx):
+    rng = np.random.Generator(np.random.PCG64(5))
+    hb = gh.make_case(rng, SALAMANDER, DEOBFUSCATE, [40, 50], [PSK])
+    hb.flags = sqobfs.FLAG_DEVICE_SALT
+    with sqobfs.Keyring(ctx, SALAMANDER, [PSK]) as kr:
+        with pytest.raises(sqobfs.SqError):
+            gh.run_host(ctx, kr, DEOBFUSCATE, hb)

@@ -138,3 +138,25 @@ def test_batch_restatement_matches_per_packet():
             w, _ = write(psks[ids[i]], salt[i * S:(i + 1) * S].tobytes(), p)
             assert out[int(oo[i]):int(oo[i]) + len(w)].tobytes() == w
             assert olen[i] == len(p) + S
+
+
+def test_chacha20_keystreams(golden):
+    """ChaCha20 restatement (device-salt checker) vs RFC 8439 2.3.2 and
+    OpenSSL keystreams (tests/golden/make_chacha.py)."""
+    g = golden("chacha20.json")
+    assert g["streams"][0]["source"].startswith("RFC 8439")
+    for v in g["streams"]:
+        n = len(v["stream"]) // 2
+        assert ol.chacha20_stream(B(v["key"]), B(v["nonce"]), v["counter"], n).hex() == v["stream"]
+
+
+def test_device_salt_derivation(golden):
+    for v in golden("chacha20.json")["device_salts"]:
+        got = ol.device_salts(B(v["key"]), v["seq"], v["n"], v["S"])
+        assert got.hex() == v["salts"]
+        # packet i's salt is bytes [(i % (64/S))*S, +S) of block i // (64/S)
+        per = 64 // v["S"]
+        nonce = b"sqob" + v["seq"].to_bytes(8, "little")
+        for i in (0, v["n"] - 1):
+            blk = ol.chacha20_stream(B(v["key"]), nonce, i // per, 64)
+            assert got[i * v["S"]:(i + 1) * v["S"]] == blk[(i % per) * v["S"]:(i % per + 1) * v["S"]]
