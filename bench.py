@@ -68,6 +68,9 @@ def parse():
     ap.add_argument("--device-salt", action="store_true",
                     help="obfuscate with SQOBFS_FLAG_DEVICE_SALT (salts from the GPU's "
                          "ChaCha20 generator; 2L+S bytes per packet)")
+    ap.add_argument("--udp", action="store_true",
+                    help="also time loopback UDP end to end through the batched socket "
+                         "layer (sqobfs_udp_conn: sendmmsg/recvmmsg + GPU)")
     ap.add_argument("--e2e", action="store_true",
                     help="also time the host-staged path (pinned H2D + kernel + D2H)")
     return ap.parse_args()
@@ -429,6 +432,8 @@ def main():
         out["roofline"]["traffic_source"] = pmc.get("source")
     if args.e2e and rank == 0:
         out["e2e"] = e2e_rate(torch, sqobfs, ctx, kr, kind, min(n, 1 << 18), L or 758)
+    if args.udp and rank == 0:
+        out["udp_e2e"] = udp_rate(sqobfs, ctx, kr, kind, L or 758)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:
@@ -480,6 +485,93 @@ def e2e_rate(torch, sqobfs, ctx, kr, kind, n, L):
         p.free()
     res["path"] = "sqobfs_run_host: 8-chunk H2D | kernel | D2H pipeline on 3 HIP streams"
     return res
+
+
+def udp_rate(sqobfs, ctx, kr, kind, L, seconds=3.0, batch=256, nsock=4):
+    """Loopback UDP end to end through the batched socket layer
+    (sqobfs_udp_conn): a client endpoint obfuscates a batch on the GPU
+    (device salts) and sends it with sendmmsg to `nsock` server sockets; the
+    server endpoint receives the batch with recvmmsg fan-in and deobfuscates
+    it on the GPU.  One thread, batch after batch, so the rate is the sum of
+    both sides' costs (GPU round trips + syscalls + loopback stack)."""
+    import socket
+    import numpy as np
+    rng = np.random.Generator(np.random.PCG64(11))
+
+    def sock():
+        s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        s.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 8 << 20)
+        s.bind(("127.0.0.1", 0))
+        return s
+    srv_s = [sock() for _ in range(nsock)]
+    cli_s = sock()
+    to = [sqobfs.Addr.of("127.0.0.1", srv_s[i % nsock].getsockname()[1]) for i in range(batch)]
+    arr = (sqobfs.Addr * batch)(*to)
+    lens = np.full(batch, L, np.uint32)
+    srv = sqobfs.UdpConn(ctx, kr, [s.fileno() for s in srv_s], slots=batch)
+    cli = sqobfs.UdpConn(ctx, kr, [cli_s.fileno()], slots=batch)
+    for i in range(batch):
+        cli.tx_payload(i)[:L] = rng.integers(0, 256, L, dtype=np.uint8)
+    import ctypes
+    sent = ctypes.c_uint32(0)
+    lib = sqobfs.lib()
+    v = sqobfs.UdpView()
+    batches = moved = lost = 0
+    t_end = time.perf_counter() + seconds
+    t0 = time.perf_counter()
+    while time.perf_counter() < t_end:
+        st = lib.sqobfs_udp_conn_write(cli.handle, 0, batch, lens.ctypes.data, arr,
+                                       ctypes.byref(sent))
+        assert st == 0 and sent.value == batch
+        got = 0
+        while got < batch:
+            st = lib.sqobfs_udp_conn_read(srv.handle, 200, ctypes.byref(v))
+            assert st == 0
+            if v.count == 0:  # dropped by the loopback stack
+                lost += batch - got
+                break
+            got += v.count
+        moved += got
+        batches += 1
+    dt = time.perf_counter() - t0
+    srv.close()
+    cli.close()
+    # the same loop with the GPU step removed: raw sendmmsg / recvmmsg of
+    # already-obfuscated wire bytes (the socket layer's own ceiling here)
+    S = 8 if kind == 0 else 16
+    wire = rng.integers(0, 256, batch * (L + S), dtype=np.uint8)
+    off = np.arange(batch, dtype=np.uint64) * (L + S)
+    wlen = np.full(batch, L + S, np.uint32)
+    slots = np.zeros(batch * 2048, np.uint8)
+    fds = np.array([s.fileno() for s in srv_s], np.int32)
+    rlen = np.zeros(batch, np.uint32)
+    rfi = np.zeros(batch, np.uint16)
+    cnt = ctypes.c_uint32(0)
+    raw = 0
+    t_end = time.perf_counter() + seconds / 2
+    t1 = time.perf_counter()
+    while time.perf_counter() < t_end:
+        assert lib.sqobfs_udp_send(cli_s.fileno(), wire.ctypes.data, off.ctypes.data,
+                                   wlen.ctypes.data, arr, batch, ctypes.byref(sent)) == 0
+        got = 0
+        while got < batch:
+            assert lib.sqobfs_udp_recv(fds.ctypes.data, nsock, slots.ctypes.data, 2048, 0,
+                                       batch, 200, rlen.ctypes.data, rfi.ctypes.data, None,
+                                       ctypes.byref(cnt)) == 0
+            if cnt.value == 0:
+                break
+            got += cnt.value
+        raw += got
+    dt_raw = time.perf_counter() - t1
+    for s in srv_s + [cli_s]:
+        s.close()
+    return {"payload_bytes": L, "batch": batch, "server_sockets": nsock, "batches": batches,
+            "datagrams_per_s": round(moved / dt), "GiB_s_payload": round(moved * L / dt / 2**30, 4),
+            "lost": lost,
+            "sockets_only_datagrams_per_s": round(raw / dt_raw),
+            "path": "sqobfs_udp_conn_write (GPU obfuscate, device salts, sendmmsg) -> loopback "
+                    "-> sqobfs_udp_conn_read (recvmmsg fan-in over the server sockets, GPU "
+                    "deobfuscate), one thread"}
 
 
 if __name__ == "__main__":

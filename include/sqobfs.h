@@ -195,6 +195,82 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
 int sqobfs_host_alloc(sqobfs_ctx *ctx, size_t bytes, void **out);
 void sqobfs_host_free(sqobfs_ctx *ctx, void *p);
 
+/* ------------------------------------------------------------------------
+ * Batched UDP socket I/O (Linux) -- the host side of the path.
+ *
+ * The reference moves one datagram per syscall: every ReadFrom / WriteTo of
+ * the decorators wraps one recvfrom / sendto of the inner PacketConn
+ * (salamander.go:43,65,88; xplus.go:47,74,97), and port hopping runs one
+ * goroutine per socket feeding a 1024-deep channel of 2048-byte buffers
+ * (hysteria/hop.go:19,40-161, recvLoop).  These entry points move whole
+ * batches with recvmmsg / sendmmsg, fan several sockets into one batch, and
+ * hand the batch to the GPU in one launch.
+ */
+
+/* Socket address, plain C (no <sys/socket.h> needed by callers). */
+typedef struct sqobfs_addr {
+  uint16_t family;   /* AF_INET (2) or AF_INET6 (10) */
+  uint16_t port;     /* host byte order */
+  uint32_t scope_id; /* IPv6 scope id, 0 for IPv4 */
+  uint8_t addr[16];  /* IPv4: first 4 bytes; IPv6: all 16 */
+} sqobfs_addr;
+
+/* Receive up to `max` datagrams from the sockets fds[0..nfds) (fan-in).
+ * Waits up to timeout_ms (-1 = forever, 0 = no wait) for the first
+ * datagram, then drains every readable socket without blocking, round-robin,
+ * with recvmmsg.  Datagram k lands at slots + k*slot_bytes + headroom
+ * (at most slot_bytes - headroom bytes; longer ones are truncated, as a
+ * ReadFrom into a fixed buffer truncates).  Writes len[k], fd_index[k] (index
+ * into fds) and from[k] (may be NULL), and *count.  Returns SQ_OK with
+ * *count == 0 on timeout, SQ_EINVAL on bad arguments, or -errno. */
+int sqobfs_udp_recv(const int *fds, uint32_t nfds, uint8_t *slots, uint32_t slot_bytes,
+                    uint32_t headroom, uint32_t max, int timeout_ms, uint32_t *len,
+                    uint16_t *fd_index, sqobfs_addr *from, uint32_t *count);
+
+/* Send n datagrams on socket fd with sendmmsg: datagram k is
+ * base[off[k] .. +len[k]) to to[k].  Blocks while the socket buffer is
+ * full; *sent = datagrams handed to the kernel.  SQ_OK or -errno. */
+int sqobfs_udp_send(int fd, const uint8_t *base, const uint64_t *off, const uint32_t *len,
+                    const sqobfs_addr *to, uint32_t n, uint32_t *sent);
+
+/* An obfuscating batched UDP endpoint: the sockets of one hysteria /
+ * hysteria2 connection (several with port hopping), the keyring, and pinned
+ * receive / transmit slots of slot_bytes each (2048 as in hop.go:19). */
+typedef struct sqobfs_udp_conn sqobfs_udp_conn;
+
+/* One received and deobfuscated batch.  Message i: payload
+ * base[off[i] .. +len[i]) (len = what the reference's ReadFrom returns:
+ * n - S, the raw n bytes for a Salamander datagram of n <= 8, 0 for an XPlus
+ * datagram of n < 16 -- callers skip len 0), received on fds[fd_index[i]]
+ * from from[i].  Valid until the next sqobfs_udp_conn_read. */
+typedef struct sqobfs_udp_view {
+  uint32_t count;
+  const uint8_t *base;
+  const uint64_t *off;
+  const uint32_t *len;
+  const uint16_t *fd_index;
+  const sqobfs_addr *from;
+} sqobfs_udp_view;
+
+int sqobfs_udp_conn_open(sqobfs_ctx *ctx, const sqobfs_keyring *kr, const int *fds,
+                         uint32_t nfds, uint32_t slots, uint32_t slot_bytes,
+                         sqobfs_udp_conn **out);
+void sqobfs_udp_conn_close(sqobfs_udp_conn *c);
+/* ReadFrom for a whole batch: receive (sqobfs_udp_recv over the conn's
+ * sockets), deobfuscate on the GPU in one launch (sqobfs_run_host on the
+ * pinned slots, payload decoded in place behind the salt), return the view. */
+int sqobfs_udp_conn_read(sqobfs_udp_conn *c, int timeout_ms, sqobfs_udp_view *out);
+/* Transmit slot i's payload area: the caller writes payload i here (up to
+ * slot_bytes - S bytes) -- S bytes of headroom precede it for the salt, as
+ * the vectorised writers prepend it (salamander.go:81-93, xplus.go:86-98). */
+uint8_t *sqobfs_udp_conn_tx_payload(sqobfs_udp_conn *c, uint32_t i);
+/* WriteTo for a whole batch: obfuscate tx slots 0..n-1 (payload lengths
+ * len[i]) in place with device salts (SQOBFS_FLAG_DEVICE_SALT) in one GPU
+ * launch, then sendmmsg datagram i = salt || payload ^ key to to[i] on
+ * fds[fd_index].  *sent = datagrams sent. */
+int sqobfs_udp_conn_write(sqobfs_udp_conn *c, uint32_t fd_index, uint32_t n,
+                          const uint32_t *len, const sqobfs_addr *to, uint32_t *sent);
+
 #ifdef __cplusplus
 }
 #endif

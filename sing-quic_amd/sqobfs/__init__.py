@@ -57,6 +57,35 @@ class Batch(ctypes.Structure):
     ]
 
 
+class Addr(ctypes.Structure):
+    """sqobfs_addr: family, port (host order), scope id, 16 address bytes."""
+    _fields_ = [("family", ctypes.c_uint16), ("port", ctypes.c_uint16),
+                ("scope_id", ctypes.c_uint32), ("addr", ctypes.c_uint8 * 16)]
+
+    @classmethod
+    def of(cls, host: str, port: int) -> "Addr":
+        import ipaddress
+        ip = ipaddress.ip_address(host)
+        a = cls()
+        a.family = 2 if ip.version == 4 else 10
+        a.port = port
+        raw = ip.packed
+        ctypes.memmove(a.addr, raw, len(raw))
+        return a
+
+    def pair(self) -> tuple[str, int]:
+        import ipaddress
+        raw = bytes(self.addr)
+        ip = ipaddress.ip_address(raw[:4] if self.family == 2 else raw)
+        return str(ip), int(self.port)
+
+
+class UdpView(ctypes.Structure):
+    _fields_ = [("count", ctypes.c_uint32), ("base", ctypes.c_void_p), ("off", ctypes.c_void_p),
+                ("len", ctypes.c_void_p), ("fd_index", ctypes.c_void_p),
+                ("from_", ctypes.c_void_p)]
+
+
 _lib = None
 
 
@@ -97,6 +126,16 @@ def lib() -> ctypes.CDLL:
     L.sqobfs_build_info.restype = ctypes.c_char_p
     L.sqobfs_build_info.argtypes = []
     L.sqobfs_host_free.restype = None
+    u16p, u32p = ctypes.POINTER(ctypes.c_uint16), ctypes.POINTER(ctypes.c_uint32)
+    L.sqobfs_udp_recv.argtypes = [vp, u32, vp, u32, u32, u32, i32, vp, vp, vp, u32p]
+    L.sqobfs_udp_send.argtypes = [i32, vp, vp, vp, vp, u32, u32p]
+    L.sqobfs_udp_conn_open.argtypes = [vp, vp, vp, u32, u32, u32, ctypes.POINTER(vp)]
+    L.sqobfs_udp_conn_close.argtypes = [vp]
+    L.sqobfs_udp_conn_close.restype = None
+    L.sqobfs_udp_conn_read.argtypes = [vp, i32, ctypes.POINTER(UdpView)]
+    L.sqobfs_udp_conn_tx_payload.argtypes = [vp, u32]
+    L.sqobfs_udp_conn_tx_payload.restype = vp
+    L.sqobfs_udp_conn_write.argtypes = [vp, u32, u32, vp, vp, u32p]
     L.sqobfs_salt_key.argtypes = [vp, vp, ctypes.c_uint64]
     L.sqobfs_salt_seq.argtypes = [vp]
     L.sqobfs_salt_seq.restype = ctypes.c_uint64
@@ -297,3 +336,92 @@ def pack(packets: list[bytes], align: int = 16, lead: int = 0) -> tuple[np.ndarr
         buf[o:o + len(p)] = np.frombuffer(p, dtype=np.uint8)
     return (buf, np.array(offs, dtype=np.uint64),
             np.array([len(p) for p in packets], dtype=np.uint32))
+
+
+# ---------------------------------------------------------------- batched UDP
+
+def udp_recv(fds: list[int], slots: np.ndarray, slot_bytes: int, headroom: int, max_n: int,
+             timeout_ms: int):
+    """sqobfs_udp_recv: (count, len[count], fd_index[count], [Addr])."""
+    fa = np.asarray(fds, dtype=np.int32)
+    ln = np.zeros(max_n, np.uint32)
+    fi = np.zeros(max_n, np.uint16)
+    addrs = (Addr * max_n)()
+    cnt = ctypes.c_uint32(0)
+    _check(lib().sqobfs_udp_recv(_ptr(fa), len(fds), _ptr(slots), slot_bytes, headroom, max_n,
+                                 timeout_ms, _ptr(ln), _ptr(fi), addrs, ctypes.byref(cnt)),
+           "sqobfs_udp_recv")
+    n = cnt.value
+    return n, ln[:n].copy(), fi[:n].copy(), list(addrs)[:n]
+
+
+def udp_send(fd: int, base: np.ndarray, off, lens, to: list[Addr]) -> int:
+    off = np.asarray(off, dtype=np.uint64)
+    lens = np.asarray(lens, dtype=np.uint32)
+    arr = (Addr * max(len(to), 1))(*to)
+    sent = ctypes.c_uint32(0)
+    _check(lib().sqobfs_udp_send(fd, _ptr(base), _ptr(off), _ptr(lens), arr, len(to),
+                                 ctypes.byref(sent)), "sqobfs_udp_send")
+    return sent.value
+
+
+class UdpConn:
+    """sqobfs_udp_conn: an obfuscating batched UDP endpoint over one or more
+    sockets (hysteria port hopping fans several into one batch)."""
+
+    def __init__(self, ctx: Context, kr: Keyring, fds: list[int], slots: int = 1024,
+                 slot_bytes: int = 2048):
+        self._fds = np.asarray(fds, dtype=np.int32)
+        h = ctypes.c_void_p()
+        _check(lib().sqobfs_udp_conn_open(ctx.handle, kr.handle, _ptr(self._fds), len(fds),
+                                          slots, slot_bytes, ctypes.byref(h)),
+               "sqobfs_udp_conn_open")
+        self.handle = h
+        self.slots, self.slot_bytes = slots, slot_bytes
+        self.S = SALT_LEN[kr.kind]
+
+    def close(self) -> None:
+        if self.handle:
+            lib().sqobfs_udp_conn_close(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def read(self, timeout_ms: int = 1000):
+        """[(payload bytes, fd_index, Addr)] of one received, decoded batch."""
+        v = UdpView()
+        _check(lib().sqobfs_udp_conn_read(self.handle, timeout_ms, ctypes.byref(v)),
+               "sqobfs_udp_conn_read")
+        out = []
+        if v.count == 0:
+            return out
+        off = np.ctypeslib.as_array((ctypes.c_uint64 * v.count).from_address(v.off))
+        ln = np.ctypeslib.as_array((ctypes.c_uint32 * v.count).from_address(v.len))
+        fi = np.ctypeslib.as_array((ctypes.c_uint16 * v.count).from_address(v.fd_index))
+        addrs = (Addr * v.count).from_address(v.from_)
+        for i in range(v.count):
+            out.append((ctypes.string_at(v.base + int(off[i]), int(ln[i])), int(fi[i]),
+                        addrs[i]))
+        return out
+
+    def tx_payload(self, i: int) -> np.ndarray:
+        p = lib().sqobfs_udp_conn_tx_payload(self.handle, i)
+        if not p:
+            raise IndexError(i)
+        n = self.slot_bytes - self.S
+        return np.frombuffer((ctypes.c_uint8 * n).from_address(p), dtype=np.uint8)
+
+    def write(self, fd_index: int, payloads: list[bytes], to: list[Addr]) -> int:
+        """Copy payloads into the tx slots, obfuscate (device salts), send."""
+        lens = np.array([len(p) for p in payloads], dtype=np.uint32)
+        for i, p in enumerate(payloads):
+            self.tx_payload(i)[:len(p)] = np.frombuffer(p, np.uint8)
+        arr = (Addr * max(len(to), 1))(*to)
+        sent = ctypes.c_uint32(0)
+        _check(lib().sqobfs_udp_conn_write(self.handle, fd_index, len(payloads), _ptr(lens), arr,
+                                           ctypes.byref(sent)), "sqobfs_udp_conn_write")
+        return sent.value

@@ -1,0 +1,134 @@
+"""The obfuscating batched UDP endpoint (sqobfs_udp_conn) on loopback, with
+the GPU doing every byte transform.  Checks against the CPU oracle that
+
+  * what the endpoint SENDS is reference wire format: each datagram, decoded
+    by the restated SalamanderPacketConn / XPlusPacketConn ReadFrom
+    (salamander.go:42-55, xplus.go:46-60), gives back the payload;
+  * what it RECEIVES from reference-format senders decodes to exactly what
+    the reference's ReadFrom returns, including the short-datagram quirks
+    (salamander.go:47-49; xplus.go:50-52);
+  * several sockets fan into one batch (hysteria/hop.go:40-161) with each
+    datagram tagged by socket and source address.
+"""
+from __future__ import annotations
+
+import socket
+
+import numpy as np
+import pytest
+import sqobfs
+from sqobfs import SALAMANDER, XPLUS, Addr
+
+import oracle_lib as ol
+
+pytestmark = pytest.mark.gpu
+
+PSK = b"sing-quic-mi355x-bench-psk"
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    c = sqobfs.Context(0)
+    yield c
+    c.close()
+
+
+def _sock():
+    s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    s.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 8 << 20)
+    s.bind(("127.0.0.1", 0))
+    return s
+
+
+def _ref_read(kind, psk, d):
+    """The reference ReadFrom on datagram d: (payload, n returned)."""
+    if kind == SALAMANDER:
+        buf, n = ol.salamander_read(psk, d)
+    else:
+        buf, n = ol.xplus_read(psk, d + bytes(64), len(d))
+    return buf[:n], n
+
+
+def _read_n(conn, n):
+    got = []
+    while len(got) < n:
+        batch = conn.read(3000)
+        assert batch, f"timed out after {len(got)} of {n}"
+        got += batch
+    return got
+
+
+@pytest.mark.parametrize("kind", [SALAMANDER, XPLUS])
+def test_conn_round_trip_with_fan_in(ctx, kind):
+    S = sqobfs.SALT_LEN[kind]
+    rng = np.random.Generator(np.random.PCG64(60 + kind))
+    srv_socks = [_sock() for _ in range(3)]
+    cli_sock = _sock()
+    spy = _sock()  # sees raw wire datagrams
+    with sqobfs.Keyring(ctx, kind, [PSK]) as kr, \
+            sqobfs.UdpConn(ctx, kr, [s.fileno() for s in srv_socks], slots=256) as srv, \
+            sqobfs.UdpConn(ctx, kr, [cli_sock.fileno()], slots=256) as cli:
+        for burst in range(6):
+            pay = [rng.integers(0, 256, int(rng.integers(1, 1400)), dtype=np.uint8).tobytes()
+                   for _ in range(40)]
+            dst = [int(rng.integers(0, 3)) for _ in pay]
+            to = [Addr.of("127.0.0.1", srv_socks[j].getsockname()[1]) for j in dst]
+            assert cli.write(0, pay, to) == len(pay)
+            got = _read_n(srv, len(pay))
+            # per server socket, order is preserved
+            for j in range(3):
+                want = [p for p, jj in zip(pay, dst) if jj == j]
+                have = [q for q, fi, a in got if fi == j]
+                assert have == want, f"burst {burst} socket {j}"
+            assert all(a.pair() == cli_sock.getsockname() for _, _, a in got)
+        # the wire is reference format: decode raw datagrams with the oracle
+        pay = [rng.integers(0, 256, int(L), dtype=np.uint8).tobytes()
+               for L in (0, 1, 7, 8, 9, 31, 32, 33, 1200, 1350, 2048 - S)]
+        assert cli.write(0, pay, [Addr.of("127.0.0.1", spy.getsockname()[1])] * len(pay)) == len(pay)
+        spy.settimeout(3)
+        salts = set()
+        for p in pay:
+            d, _ = spy.recvfrom(4096)
+            assert len(d) == len(p) + S
+            q, n = _ref_read(kind, PSK, d)
+            if kind == SALAMANDER and len(p) == 0:
+                assert (q, n) == (d, 8)  # salamander.go:47-49: an 8-byte datagram reads raw
+            else:
+                assert n == len(p) and q == p
+            salts.add(d[:S])
+        assert len(salts) == len(pay)  # device salts differ per packet
+    for s in srv_socks + [cli_sock, spy]:
+        s.close()
+
+
+@pytest.mark.parametrize("kind", [SALAMANDER, XPLUS])
+def test_conn_reads_reference_senders(ctx, kind):
+    """Datagrams made by the restated reference WriteTo (host salts), plus
+    short and junk datagrams, decode to what the reference ReadFrom returns."""
+    S = sqobfs.SALT_LEN[kind]
+    rng = np.random.Generator(np.random.PCG64(70 + kind))
+    srv = _sock()
+    tx = _sock()
+    write = ol.salamander_write if kind == SALAMANDER else ol.xplus_write
+    dgrams = []
+    for L in list(range(0, 20)) + [int(x) for x in rng.integers(0, 1450, 100)]:
+        if L < 20 and L % 3 == 0:  # raw short / junk datagrams
+            dgrams.append(rng.integers(0, 256, L, dtype=np.uint8).tobytes())
+        else:
+            salt = rng.integers(0, 256, S, dtype=np.uint8).tobytes()
+            pay = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+            dgrams.append(write(PSK, salt, pay)[0])
+    with sqobfs.Keyring(ctx, kind, [PSK]) as kr, \
+            sqobfs.UdpConn(ctx, kr, [srv.fileno()], slots=64) as conn:
+        got = []
+        for k0 in range(0, len(dgrams), 40):
+            chunk = [d for d in dgrams[k0:k0 + 40] if len(d) > 0]  # empty datagrams: skip
+            for d in chunk:
+                tx.sendto(d, srv.getsockname())
+            got += [(q, len(q)) for q, _, _ in _read_n(conn, len(chunk))]
+    want = [_ref_read(kind, PSK, d) for d in dgrams if len(d) > 0]
+    assert got == want
+    srv.close()
+    tx.close()
