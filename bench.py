@@ -433,7 +433,8 @@ def main():
     if args.e2e and rank == 0:
         out["e2e"] = e2e_rate(torch, sqobfs, ctx, kr, kind, min(n, 1 << 18), L or 758)
     if args.udp and rank == 0:
-        out["udp_e2e"] = udp_rate(sqobfs, ctx, kr, kind, L or 758)
+        out["udp_e2e"] = [udp_rate(sqobfs, ctx, kr, kind, L or 758, batch=bt)
+                          for bt in (64, 256, 1024)]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:
@@ -503,7 +504,7 @@ def udp_rate(sqobfs, ctx, kr, kind, L, seconds=3.0, batch=256, nsock=4):
         s.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 8 << 20)
         s.bind(("127.0.0.1", 0))
         return s
-    srv_s = [sock() for _ in range(nsock)]
+    srv_s = [sock() for _ in range(nsock)]  # fan-in, as hysteria port hopping
     cli_s = sock()
     to = [sqobfs.Addr.of("127.0.0.1", srv_s[i % nsock].getsockname()[1]) for i in range(batch)]
     arr = (sqobfs.Addr * batch)(*to)
@@ -569,9 +570,9 @@ def udp_rate(sqobfs, ctx, kr, kind, L, seconds=3.0, batch=256, nsock=4):
             "datagrams_per_s": round(moved / dt), "GiB_s_payload": round(moved * L / dt / 2**30, 4),
             "lost": lost,
             "sockets_only_datagrams_per_s": round(raw / dt_raw),
-            "path": "sqobfs_udp_conn_write (GPU obfuscate, device salts, sendmmsg) -> loopback "
-                    "-> sqobfs_udp_conn_read (recvmmsg fan-in over the server sockets, GPU "
-                    "deobfuscate), one thread"}
+            "path": "sqobfs_udp_conn_write (GPU obfuscate in the mapped slots, device salts, "
+                    "sendmmsg) -> loopback -> sqobfs_udp_conn_read (recvmmsg fan-in over the "
+                    "server sockets, GPU deobfuscate in the mapped slots), one thread"}
 
 
 if __name__ == "__main__":

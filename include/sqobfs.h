@@ -257,8 +257,9 @@ int sqobfs_udp_conn_open(sqobfs_ctx *ctx, const sqobfs_keyring *kr, const int *f
                          sqobfs_udp_conn **out);
 void sqobfs_udp_conn_close(sqobfs_udp_conn *c);
 /* ReadFrom for a whole batch: receive (sqobfs_udp_recv over the conn's
- * sockets), deobfuscate on the GPU in one launch (sqobfs_run_host on the
- * pinned slots, payload decoded in place behind the salt), return the view. */
+ * sockets), deobfuscate on the GPU in one launch that reads and writes the
+ * conn's page-locked, GPU-mapped slots directly (zero copy; payload decoded
+ * in place behind the salt), return the view.  slot_bytes: multiple of 16. */
 int sqobfs_udp_conn_read(sqobfs_udp_conn *c, int timeout_ms, sqobfs_udp_view *out);
 /* Transmit slot i's payload area: the caller writes payload i here (up to
  * slot_bytes - S bytes) -- S bytes of headroom precede it for the salt, as

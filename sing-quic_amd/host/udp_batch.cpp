@@ -11,7 +11,14 @@
 // dropped: the kernel socket buffers queue), deobfuscated by one GPU launch
 // on the pinned slots, and transmitted batches are obfuscated in place by
 // one launch and sent with sendmmsg.
+//
+// Zero copy: the slots AND the batch arrays live in one page-locked block
+// mapped into the GPU's address space, and the kernel reads and writes them
+// over PCIe directly (sqobfs_launch on the mapped pointers, then a stream
+// sync).  A socket batch is a few hundred KiB, so one launch + sync costs far
+// less than the staged H2D | kernel | D2H of sqobfs_run_host.
 #include <errno.h>
+#include <hip/hip_runtime.h>
 #include <netinet/in.h>
 #include <poll.h>
 #include <string.h>
@@ -70,17 +77,30 @@ struct sqobfs_udp_conn {
   const sqobfs_keyring *kr = nullptr;
   std::vector<int> fds;
   uint32_t slots = 0, slot_bytes = 0, S = 0;
-  uint8_t *rx = nullptr, *tx = nullptr;  // pinned (sqobfs_host_alloc)
+  void *block = nullptr;  // page-locked, GPU-mapped: slots + batch arrays
+  uint8_t *rx = nullptr, *tx = nullptr;
   std::mutex rx_mu, tx_mu;
-  // receive batch
-  std::vector<uint64_t> rx_in_off, rx_out_off;
-  std::vector<uint32_t> rx_len, rx_out_len;
+  // receive batch (in the mapped block)
+  uint64_t *rx_in_off = nullptr, *rx_out_off = nullptr;
+  uint32_t *rx_len = nullptr, *rx_out_len = nullptr;
   std::vector<uint16_t> rx_fd;
   std::vector<sqobfs_addr> rx_from;
-  // transmit batch
-  std::vector<uint64_t> tx_in_off, tx_out_off;
-  std::vector<uint32_t> tx_out_len, tx_wire_len;
+  // transmit batch (in the mapped block)
+  uint64_t *tx_in_off = nullptr, *tx_out_off = nullptr;
+  uint32_t *tx_len = nullptr, *tx_out_len = nullptr;
+  std::vector<uint32_t> tx_wire_len;
 };
+
+namespace {
+
+// one launch on the mapped block + wait (the conn's batches are small)
+int launch_sync(sqobfs_udp_conn *c, int dir, const sqobfs_batch &b) {
+  void *s = sqobfs_stream(c->ctx);
+  const int st = sqobfs_launch(c->ctx, c->kr, dir, &b, s);
+  return st != SQ_OK ? st : sqobfs_sync(c->ctx, s);
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -197,7 +217,7 @@ int sqobfs_udp_conn_open(sqobfs_ctx *ctx, const sqobfs_keyring *kr, const int *f
   const int kind = sqobfs_keyring_kind(kr);
   const uint32_t S = kind == SQOBFS_SALAMANDER ? SQOBFS_SALAMANDER_SALT_LEN
                                                : SQOBFS_XPLUS_SALT_LEN;
-  if (slot_bytes <= S || slot_bytes % 4) return SQ_EINVAL;
+  if (slot_bytes <= S || slot_bytes % 16) return SQ_EINVAL;
   sqobfs_udp_conn *c = new (std::nothrow) sqobfs_udp_conn();
   if (!c) return SQ_ENOMEM;
   c->ctx = ctx;
@@ -206,26 +226,33 @@ int sqobfs_udp_conn_open(sqobfs_ctx *ctx, const sqobfs_keyring *kr, const int *f
   c->slots = slots;
   c->slot_bytes = slot_bytes;
   c->S = S;
-  const size_t bytes = (size_t)slots * slot_bytes;
-  void *rx = nullptr, *tx = nullptr;
-  int st = sqobfs_host_alloc(ctx, bytes, &rx);
-  if (st == SQ_OK) st = sqobfs_host_alloc(ctx, bytes, &tx);
-  if (st != SQ_OK) {
-    if (rx) sqobfs_host_free(ctx, rx);
+  // one mapped block: rx slots | tx slots | 4 u64 arrays | 4 u32 arrays
+  const size_t sb = (size_t)slots * slot_bytes, a64 = 8ull * slots, a32 = 4ull * slots;
+  const size_t bytes = 2 * sb + 4 * a64 + 4 * a32;
+  if (sqobfs_host_alloc(ctx, bytes, &c->block) != SQ_OK) {
     delete c;
-    return st;
+    return SQ_ENOMEM;
   }
-  c->rx = (uint8_t *)rx;
-  c->tx = (uint8_t *)tx;
-  c->rx_in_off.resize(slots);
-  c->rx_out_off.resize(slots);
-  c->rx_len.resize(slots);
-  c->rx_out_len.resize(slots);
+  void *dev = nullptr;  // the GPU's view of the block (the same address on ROCm)
+  if (hipHostGetDevicePointer(&dev, c->block, 0) != hipSuccess || dev != c->block) {
+    (void)hipGetLastError();
+    sqobfs_host_free(ctx, c->block);
+    delete c;
+    return SQ_EDEVICE;
+  }
+  uint8_t *p = (uint8_t *)c->block;
+  c->rx = p;                                 p += sb;
+  c->tx = p;                                 p += sb;
+  c->rx_in_off = (uint64_t *)p;              p += a64;
+  c->rx_out_off = (uint64_t *)p;             p += a64;
+  c->tx_in_off = (uint64_t *)p;              p += a64;
+  c->tx_out_off = (uint64_t *)p;             p += a64;
+  c->rx_len = (uint32_t *)p;                 p += a32;
+  c->rx_out_len = (uint32_t *)p;             p += a32;
+  c->tx_len = (uint32_t *)p;                 p += a32;
+  c->tx_out_len = (uint32_t *)p;
   c->rx_fd.resize(slots);
   c->rx_from.resize(slots);
-  c->tx_in_off.resize(slots);
-  c->tx_out_off.resize(slots);
-  c->tx_out_len.resize(slots);
   c->tx_wire_len.resize(slots);
   for (uint32_t i = 0; i < slots; i++) {
     c->rx_in_off[i] = (uint64_t)i * slot_bytes;       // wire at the slot start
@@ -239,8 +266,7 @@ int sqobfs_udp_conn_open(sqobfs_ctx *ctx, const sqobfs_keyring *kr, const int *f
 
 void sqobfs_udp_conn_close(sqobfs_udp_conn *c) {
   if (!c) return;
-  sqobfs_host_free(c->ctx, c->rx);
-  sqobfs_host_free(c->ctx, c->tx);
+  sqobfs_host_free(c->ctx, c->block);
   delete c;
 }
 
@@ -250,25 +276,24 @@ int sqobfs_udp_conn_read(sqobfs_udp_conn *c, int timeout_ms, sqobfs_udp_view *ou
   memset(out, 0, sizeof *out);
   uint32_t n = 0;
   int st = sqobfs_udp_recv(c->fds.data(), (uint32_t)c->fds.size(), c->rx, c->slot_bytes, 0,
-                           c->slots, timeout_ms, c->rx_len.data(), c->rx_fd.data(),
+                           c->slots, timeout_ms, c->rx_len, c->rx_fd.data(),
                            c->rx_from.data(), &n);
   if (st != SQ_OK || n == 0) return st;
   sqobfs_batch b;
   memset(&b, 0, sizeof b);
   b.n = n;
-  b.flags = SQOBFS_FLAG_OUT_UNINIT;
   b.in = c->rx;
-  b.in_off = c->rx_in_off.data();
-  b.in_len = c->rx_len.data();
+  b.in_off = c->rx_in_off;
+  b.in_len = c->rx_len;
   b.out = c->rx;
-  b.out_off = c->rx_out_off.data();
-  b.out_len = c->rx_out_len.data();
-  st = sqobfs_run_host(c->ctx, c->kr, SQOBFS_DEOBFUSCATE, &b);
+  b.out_off = c->rx_out_off;
+  b.out_len = c->rx_out_len;
+  st = launch_sync(c, SQOBFS_DEOBFUSCATE, b);
   if (st != SQ_OK) return st;
   out->count = n;
   out->base = c->rx;
-  out->off = c->rx_out_off.data();
-  out->len = c->rx_out_len.data();
+  out->off = c->rx_out_off;
+  out->len = c->rx_out_len;
   out->fd_index = c->rx_fd.data();
   out->from = c->rx_from.data();
   return SQ_OK;
@@ -288,22 +313,23 @@ int sqobfs_udp_conn_write(sqobfs_udp_conn *c, uint32_t fd_index, uint32_t n,
   std::lock_guard<std::mutex> lk(c->tx_mu);
   for (uint32_t i = 0; i < n; i++) {
     if (len[i] > c->slot_bytes - c->S) return SQ_EINVAL;
+    c->tx_len[i] = len[i];
     c->tx_wire_len[i] = len[i] + c->S;
   }
   sqobfs_batch b;
   memset(&b, 0, sizeof b);
   b.n = n;
-  b.flags = SQOBFS_FLAG_OUT_UNINIT | SQOBFS_FLAG_DEVICE_SALT;
+  b.flags = SQOBFS_FLAG_DEVICE_SALT;
   b.in = c->tx;
-  b.in_off = c->tx_in_off.data();
-  b.in_len = len;
+  b.in_off = c->tx_in_off;
+  b.in_len = c->tx_len;
   b.out = c->tx;
-  b.out_off = c->tx_out_off.data();
-  b.out_len = c->tx_out_len.data();
-  const int st = sqobfs_run_host(c->ctx, c->kr, SQOBFS_OBFUSCATE, &b);
+  b.out_off = c->tx_out_off;
+  b.out_len = c->tx_out_len;
+  const int st = launch_sync(c, SQOBFS_OBFUSCATE, b);
   if (st != SQ_OK) return st;
-  return sqobfs_udp_send(c->fds[fd_index], c->tx, c->tx_out_off.data(), c->tx_wire_len.data(),
-                         to, n, sent);
+  return sqobfs_udp_send(c->fds[fd_index], c->tx, c->tx_out_off, c->tx_wire_len.data(), to, n,
+                         sent);
 }
 
 }  // extern "C"
