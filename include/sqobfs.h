@@ -196,6 +196,74 @@ int sqobfs_host_alloc(sqobfs_ctx *ctx, size_t bytes, void **out);
 void sqobfs_host_free(sqobfs_ctx *ctx, void *p);
 
 /* ------------------------------------------------------------------------
+ * QUIC packet protection, AEAD_CHACHA20_POLY1305.
+ *
+ * The next per-datagram byte transform under the obfuscation layer: quic-go
+ * (v0.52.0-beta.1, go.mod:7; not in the reference tree) seals every 1-RTT
+ * packet (internal/handshake/aead.go) and applies header protection
+ * (internal/handshake/header_protector.go) one packet at a time.  Here a
+ * ragged batch of packets is protected / unprotected in one launch:
+ *   seal:  nonce = iv XOR be96(pn)                         (RFC 9001 5.3)
+ *          payload -> ChaCha20-Poly1305(key, nonce, aad = header)
+ *                                                          (RFC 8439 2.8)
+ *          sample = 16 bytes at pn_offset + 4 of the sealed packet;
+ *          mask = ChaCha20(hp, counter = sample[0:4], nonce = sample[4:16]);
+ *          first byte ^= mask[0] & (long header ? 0x0f : 0x1f),
+ *          packet number bytes ^= mask[1 .. pn_len]        (RFC 9001 5.4)
+ *   open:  the reverse; the packet number is decoded from its truncated
+ *          form against the largest received one (RFC 9000 Appendix A.3)
+ *          and the tag is verified.
+ * The packet-number length is (first byte & 3) + 1 of the unprotected
+ * header, as QUIC encodes it. */
+
+/* One connection's 1-RTT keys (from the TLS key schedule: "quic key",
+ * "quic iv", "quic hp", RFC 9001 5.1). */
+typedef struct sqobfs_quic_key {
+  uint8_t key[32];
+  uint8_t iv[12];
+  uint8_t hp[32];
+} sqobfs_quic_key;
+
+typedef struct sqobfs_quic_keyring sqobfs_quic_keyring;
+
+/* out_len values of packets that were not processed */
+#define SQOBFS_QUIC_EKEY 0xFFFFFFFFu   /* key_id out of range */
+#define SQOBFS_QUIC_ESHORT 0xFFFFFFFEu /* too short to sample / bad pn_offset */
+#define SQOBFS_QUIC_EAUTH 0xFFFFFFFDu  /* open: tag mismatch (output undefined) */
+
+/* A ragged batch of QUIC packets (device pointers).
+ *   seal: in  = header || payload (in_len[i] bytes); out = protected
+ *         header || ciphertext || 16-byte tag, out_len[i] = in_len[i] + 16.
+ *   open: in  = protected packet incl. tag; out = unprotected header ||
+ *         plaintext, out_len[i] = in_len[i] - 16; pn_out[i] (optional) =
+ *         the decoded packet number.
+ * out may be exactly in place (out_off == in_off; seal needs 16 bytes of
+ * room after each packet) or disjoint from every input. */
+typedef struct sqobfs_quic_batch {
+  uint32_t n;
+  uint32_t flags;              /* 0 */
+  const uint8_t *in;
+  const uint64_t *in_off;
+  const uint32_t *in_len;
+  uint8_t *out;
+  const uint64_t *out_off;
+  uint32_t *out_len;
+  const uint16_t *pn_offset;   /* [n] offset of the packet number field */
+  const uint64_t *pn;          /* [n] seal: the packet number; open: the
+                                  largest packet number received so far */
+  const uint16_t *key_id;      /* [n] keyring index, NULL = all use 0 */
+  uint64_t *pn_out;            /* open: [n] decoded packet numbers, or NULL */
+} sqobfs_quic_batch;
+
+int sqobfs_quic_keyring_create(sqobfs_ctx *ctx, uint32_t count, const sqobfs_quic_key *keys,
+                               sqobfs_quic_keyring **out);
+void sqobfs_quic_keyring_destroy(sqobfs_quic_keyring *kr);
+int sqobfs_quic_seal(sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr,
+                     const sqobfs_quic_batch *b, void *stream);
+int sqobfs_quic_open(sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr,
+                     const sqobfs_quic_batch *b, void *stream);
+
+/* ------------------------------------------------------------------------
  * Batched UDP socket I/O (Linux) -- the host side of the path.
  *
  * The reference moves one datagram per syscall: every ReadFrom / WriteTo of

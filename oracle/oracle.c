@@ -256,6 +256,191 @@ void or_device_salts(const uint8_t key[32], uint64_t seq, uint32_t n, uint32_t S
   or_chacha20_stream(key, nonce, 0, out, (size_t)n * S);
 }
 
+/* ---------------------------------------------------------------- Poly1305
+ * RFC 8439 section 2.5, restated with 130-bit arithmetic in 26-bit limbs
+ * (the accumulator h, the clamped r; reduction modulo 2^130 - 5). */
+void or_poly1305(const uint8_t key[32], const uint8_t *msg, size_t len, uint8_t tag[16]) {
+  const uint32_t r0 = load32le(key + 0) & 0x3ffffff;
+  const uint32_t r1 = (load32le(key + 3) >> 2) & 0x3ffff03;
+  const uint32_t r2 = (load32le(key + 6) >> 4) & 0x3ffc0ff;
+  const uint32_t r3 = (load32le(key + 9) >> 6) & 0x3f03fff;
+  const uint32_t r4 = (load32le(key + 12) >> 8) & 0x00fffff;
+  const uint32_t s1 = r1 * 5, s2 = r2 * 5, s3 = r3 * 5, s4 = r4 * 5;
+  uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0, h4 = 0;
+  while (len > 0) {
+    uint8_t blk[17] = {0};
+    const size_t take = len < 16 ? len : 16;
+    memcpy(blk, msg, take);
+    blk[take] = 1;  /* the 2^(8*take) bit */
+    h0 += load32le(blk + 0) & 0x3ffffff;
+    h1 += (load32le(blk + 3) >> 2) & 0x3ffffff;
+    h2 += (load32le(blk + 6) >> 4) & 0x3ffffff;
+    h3 += (load32le(blk + 9) >> 6) & 0x3ffffff;
+    h4 += (load32le(blk + 12) >> 8) | ((uint32_t)blk[16] << 24);
+    const uint64_t d0 = (uint64_t)h0 * r0 + (uint64_t)h1 * s4 + (uint64_t)h2 * s3 +
+                        (uint64_t)h3 * s2 + (uint64_t)h4 * s1;
+    uint64_t d1 = (uint64_t)h0 * r1 + (uint64_t)h1 * r0 + (uint64_t)h2 * s4 +
+                  (uint64_t)h3 * s3 + (uint64_t)h4 * s2;
+    uint64_t d2 = (uint64_t)h0 * r2 + (uint64_t)h1 * r1 + (uint64_t)h2 * r0 +
+                  (uint64_t)h3 * s4 + (uint64_t)h4 * s3;
+    uint64_t d3 = (uint64_t)h0 * r3 + (uint64_t)h1 * r2 + (uint64_t)h2 * r1 +
+                  (uint64_t)h3 * r0 + (uint64_t)h4 * s4;
+    uint64_t d4 = (uint64_t)h0 * r4 + (uint64_t)h1 * r3 + (uint64_t)h2 * r2 +
+                  (uint64_t)h3 * r1 + (uint64_t)h4 * r0;
+    uint32_t c = (uint32_t)(d0 >> 26); h0 = (uint32_t)d0 & 0x3ffffff;
+    d1 += c; c = (uint32_t)(d1 >> 26); h1 = (uint32_t)d1 & 0x3ffffff;
+    d2 += c; c = (uint32_t)(d2 >> 26); h2 = (uint32_t)d2 & 0x3ffffff;
+    d3 += c; c = (uint32_t)(d3 >> 26); h3 = (uint32_t)d3 & 0x3ffffff;
+    d4 += c; c = (uint32_t)(d4 >> 26); h4 = (uint32_t)d4 & 0x3ffffff;
+    h0 += c * 5; c = h0 >> 26; h0 &= 0x3ffffff;
+    h1 += c;
+    msg += take;
+    len -= take;
+  }
+  /* full carry, then h mod 2^130-5 (subtract p if h >= p) */
+  uint32_t c = h1 >> 26; h1 &= 0x3ffffff;
+  h2 += c; c = h2 >> 26; h2 &= 0x3ffffff;
+  h3 += c; c = h3 >> 26; h3 &= 0x3ffffff;
+  h4 += c; c = h4 >> 26; h4 &= 0x3ffffff;
+  h0 += c * 5; c = h0 >> 26; h0 &= 0x3ffffff;
+  h1 += c;
+  uint32_t g0 = h0 + 5; c = g0 >> 26; g0 &= 0x3ffffff;
+  uint32_t g1 = h1 + c; c = g1 >> 26; g1 &= 0x3ffffff;
+  uint32_t g2 = h2 + c; c = g2 >> 26; g2 &= 0x3ffffff;
+  uint32_t g3 = h3 + c; c = g3 >> 26; g3 &= 0x3ffffff;
+  uint32_t g4 = h4 + c - (1u << 26);
+  uint32_t mask = (g4 >> 31) - 1;  /* all ones if h >= p */
+  h0 = (h0 & ~mask) | (g0 & mask);
+  h1 = (h1 & ~mask) | (g1 & mask);
+  h2 = (h2 & ~mask) | (g2 & mask);
+  h3 = (h3 & ~mask) | (g3 & mask);
+  h4 = (h4 & ~mask) | (g4 & mask);
+  /* h + s mod 2^128 */
+  uint64_t f0 = ((h0) | (h1 << 26)) + (uint64_t)load32le(key + 16);
+  uint64_t f1 = ((h1 >> 6) | (h2 << 20)) + (uint64_t)load32le(key + 20) + (f0 >> 32);
+  uint64_t f2 = ((h2 >> 12) | (h3 << 14)) + (uint64_t)load32le(key + 24) + (f1 >> 32);
+  uint64_t f3 = ((h3 >> 18) | (h4 << 8)) + (uint64_t)load32le(key + 28) + (f2 >> 32);
+  const uint32_t w[4] = {(uint32_t)f0, (uint32_t)f1, (uint32_t)f2, (uint32_t)f3};
+  for (int i = 0; i < 4; i++)
+    for (int k = 0; k < 4; k++) tag[4 * i + k] = (uint8_t)(w[i] >> (8 * k));
+}
+
+/* RFC 8439 section 2.8: otk = block 0; ct = pt ^ keystream from counter 1;
+ * mac_data = aad || pad16 || ct || pad16 || le64(aad_len) || le64(ct_len). */
+void or_aead_seal(const uint8_t key[32], const uint8_t nonce[12], const uint8_t *aad,
+                  size_t aad_len, const uint8_t *pt, size_t len, uint8_t *ct, uint8_t tag[16]) {
+  uint8_t blk[64];
+  or_chacha20_block(key, 0, nonce, blk);
+  for (size_t pos = 0; pos < len; pos += 64) {
+    uint8_t ks[64];
+    or_chacha20_block(key, 1 + (uint32_t)(pos / 64), nonce, ks);
+    for (size_t i = pos; i < len && i < pos + 64; i++) ct[i] = pt[i] ^ ks[i - pos];
+  }
+  const size_t pa = (aad_len + 15) / 16 * 16, pc = (len + 15) / 16 * 16;
+  uint8_t *mac = (uint8_t *)calloc(pa + pc + 16, 1);
+  memcpy(mac, aad, aad_len);
+  memcpy(mac + pa, ct, len);
+  for (int k = 0; k < 8; k++) {
+    mac[pa + pc + k] = (uint8_t)((uint64_t)aad_len >> (8 * k));
+    mac[pa + pc + 8 + k] = (uint8_t)((uint64_t)len >> (8 * k));
+  }
+  or_poly1305(blk, mac, pa + pc + 16, tag);
+  free(mac);
+}
+
+static void quic_nonce(const uint8_t iv[12], uint64_t pn, uint8_t nonce[12]) {
+  memcpy(nonce, iv, 12);  /* RFC 9001 5.3: iv XOR left-padded big-endian pn */
+  for (int k = 0; k < 8; k++) nonce[11 - k] ^= (uint8_t)(pn >> (8 * k));
+}
+
+/* RFC 9001 5.4.4: mask = ChaCha20(hp, counter = sample[0..4), nonce =
+ * sample[4..16)) applied to 5 zero bytes. */
+static void quic_mask(const uint8_t hp[32], const uint8_t sample[16], uint8_t mask[5]) {
+  uint8_t blk[64];
+  or_chacha20_block(hp, load32le(sample), sample + 4, blk);
+  memcpy(mask, blk, 5);
+}
+
+long or_quic_seal(const uint8_t key[32], const uint8_t iv[12], const uint8_t hp[32],
+                  uint64_t pn, const uint8_t *pkt, size_t len, size_t pn_offset, uint8_t *out) {
+  const size_t pn_len = (size_t)(pkt[0] & 3) + 1, hdr = pn_offset + pn_len;
+  if (hdr > len || pn_offset + 4 + 16 > len + 16) return -1;
+  uint8_t nonce[12];
+  quic_nonce(iv, pn, nonce);
+  uint8_t *tmp = (uint8_t *)malloc(len + 16);
+  memcpy(tmp, pkt, hdr);
+  or_aead_seal(key, nonce, pkt, hdr, pkt + hdr, len - hdr, tmp + hdr, tmp + len);
+  uint8_t mask[5];
+  quic_mask(hp, tmp + pn_offset + 4, mask);
+  tmp[0] ^= mask[0] & ((tmp[0] & 0x80) ? 0x0f : 0x1f);
+  for (size_t i = 0; i < pn_len; i++) tmp[pn_offset + i] ^= mask[1 + i];
+  memcpy(out, tmp, len + 16);
+  free(tmp);
+  return (long)(len + 16);
+}
+
+/* RFC 9000 Appendix A.3 */
+static uint64_t decode_pn(uint64_t largest, uint64_t truncated, unsigned nbits) {
+  const uint64_t expected = largest + 1, win = 1ull << nbits, hwin = win / 2;
+  const uint64_t mask = win - 1;
+  const uint64_t cand = (expected & ~mask) | truncated;
+  if (cand + hwin <= expected && cand < (1ull << 62) - win) return cand + win;
+  if (cand > expected + hwin && cand >= win) return cand - win;
+  return cand;
+}
+
+long or_quic_open(const uint8_t key[32], const uint8_t iv[12], const uint8_t hp[32],
+                  uint64_t largest_pn, const uint8_t *pkt, size_t len, size_t pn_offset,
+                  uint8_t *out, uint64_t *pn_out) {
+  if (len < 16 || pn_offset + 4 + 16 > len) return -1;
+  uint8_t mask[5];
+  quic_mask(hp, pkt + pn_offset + 4, mask);
+  uint8_t *tmp = (uint8_t *)malloc(len);
+  memcpy(tmp, pkt, len);
+  tmp[0] ^= mask[0] & ((tmp[0] & 0x80) ? 0x0f : 0x1f);
+  const size_t pn_len = (size_t)(tmp[0] & 3) + 1, hdr = pn_offset + pn_len;
+  uint64_t trunc = 0;
+  for (size_t i = 0; i < pn_len; i++) {
+    tmp[pn_offset + i] ^= mask[1 + i];
+    trunc = (trunc << 8) | tmp[pn_offset + i];
+  }
+  if (hdr > len - 16) {
+    free(tmp);
+    return -1;
+  }
+  const uint64_t pn = decode_pn(largest_pn, trunc, (unsigned)(8 * pn_len));
+  uint8_t nonce[12], tag[16];
+  quic_nonce(iv, pn, nonce);
+  /* decrypt = encrypt with the same keystream; the MAC covers the ciphertext */
+  const size_t clen = len - 16 - hdr;
+  uint8_t *pt = (uint8_t *)malloc(clen ? clen : 1);
+  uint8_t otk[64];
+  or_chacha20_block(key, 0, nonce, otk);
+  const size_t pa = (hdr + 15) / 16 * 16, pc = (clen + 15) / 16 * 16;
+  uint8_t *mac = (uint8_t *)calloc(pa + pc + 16, 1);
+  memcpy(mac, tmp, hdr);
+  memcpy(mac + pa, tmp + hdr, clen);
+  for (int k = 0; k < 8; k++) {
+    mac[pa + pc + k] = (uint8_t)((uint64_t)hdr >> (8 * k));
+    mac[pa + pc + 8 + k] = (uint8_t)((uint64_t)clen >> (8 * k));
+  }
+  or_poly1305(otk, mac, pa + pc + 16, tag);
+  free(mac);
+  uint8_t diff = 0;
+  for (int i = 0; i < 16; i++) diff |= tag[i] ^ tmp[len - 16 + i];
+  for (size_t pos = 0; pos < clen; pos += 64) {
+    uint8_t ks[64];
+    or_chacha20_block(key, 1 + (uint32_t)(pos / 64), nonce, ks);
+    for (size_t i = pos; i < clen && i < pos + 64; i++) pt[i] = tmp[hdr + i] ^ ks[i - pos];
+  }
+  memcpy(out, tmp, hdr);
+  memcpy(out + hdr, pt, clen);
+  free(pt);
+  free(tmp);
+  if (pn_out) *pn_out = pn;
+  return diff ? -2 : (long)(len - 16);
+}
+
 static void hash_psk_salt(int kind, const uint8_t *psk, size_t psk_len,
                           const uint8_t *salt, size_t salt_len,
                           uint8_t key[32]) {

@@ -58,6 +58,31 @@ void or_chacha20_stream(const uint8_t key[32], const uint8_t nonce[12],
 void or_device_salts(const uint8_t key[32], uint64_t seq, uint32_t n,
                      uint32_t S, uint8_t *out);
 
+/* ---- QUIC packet protection (quic-go v0.52.0-beta.1
+ * handshake/aead.go + header_protector.go, not in the reference tree):
+ * AEAD_CHACHA20_POLY1305 (RFC 8439 section 2.8) with QUIC's nonce and
+ * ChaCha20 header protection (RFC 9001 sections 5.3, 5.4.1, 5.4.4). */
+/* RFC 8439 section 2.5 Poly1305 one-time authenticator. */
+void or_poly1305(const uint8_t key[32], const uint8_t *msg, size_t len, uint8_t tag[16]);
+/* RFC 8439 section 2.8 AEAD seal: ct[0..len) and tag[16]. */
+void or_aead_seal(const uint8_t key[32], const uint8_t nonce[12], const uint8_t *aad,
+                  size_t aad_len, const uint8_t *pt, size_t len, uint8_t *ct, uint8_t tag[16]);
+/* Protect one QUIC packet: pkt[0..len) = header (packet number of
+ * (pkt[0] & 3) + 1 bytes at pn_offset) || payload.  out[0..len+16) =
+ * protected header || ciphertext || tag.  Returns len + 16, or -1 if the
+ * packet is too short to sample (RFC 9001 5.4.2: pn_offset + 4 + 16 >
+ * len + 16). */
+long or_quic_seal(const uint8_t key[32], const uint8_t iv[12], const uint8_t hp[32],
+                  uint64_t pn, const uint8_t *pkt, size_t len, size_t pn_offset, uint8_t *out);
+/* Unprotect + open one packet of `len` bytes (tag included).  largest_pn:
+ * the largest packet number received so far in this space (RFC 9000
+ * Appendix A.3).  out[0..len-16) = unprotected header || plaintext;
+ * *pn_out = the decoded packet number.  Returns len - 16, -1 if too short,
+ * -2 if the tag does not verify. */
+long or_quic_open(const uint8_t key[32], const uint8_t iv[12], const uint8_t hp[32],
+                  uint64_t largest_pn, const uint8_t *pkt, size_t len, size_t pn_offset,
+                  uint8_t *out, uint64_t *pn_out);
+
 /* Salamander key: BLAKE2b-256(psk || salt[0:8])  (salamander.go:50,61,84,99) */
 void or_salamander_key(const uint8_t *psk, size_t psk_len,
                        const uint8_t salt[8], uint8_t key[32]);

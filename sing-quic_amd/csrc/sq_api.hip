@@ -42,6 +42,13 @@ constexpr uint32_t kHostChunks = 8;  // sqobfs_run_host pipeline depth
 constexpr uint32_t kEvents = 16;
 }
 
+struct sqobfs_quic_keyring {
+  sqobfs_ctx *ctx = nullptr;
+  uint32_t count = 0;
+  sq::QuicKeyDev *table = nullptr;  // device
+  sq::QuicKeyDev host0;             // entry 0, passed by value
+};
+
 struct sqobfs_keyring {
   sqobfs_ctx *ctx = nullptr;
   int kind = 0;
@@ -299,7 +306,7 @@ int sqobfs_keyring_create(sqobfs_ctx *ctx, int kind, uint32_t count, const uint8
 void sqobfs_keyring_destroy(sqobfs_keyring *kr) {
   if (!kr) return;
   (void)hipSetDevice(kr->ctx->device);
-  (void)hipStreamSynchronize(kr->ctx->stream);
+  (void)hipDeviceSynchronize();  // launches on any stream may still read the table
   if (kr->table) (void)hipFree(kr->table);
   delete kr;
 }
@@ -337,6 +344,86 @@ int sqobfs_xplus_deobfuscate(sqobfs_ctx *ctx, const sqobfs_keyring *kr, const sq
                              void *stream) {
   if (!kr || kr->kind != SQOBFS_XPLUS) return SQ_EINVAL;
   return sqobfs_launch(ctx, kr, SQOBFS_DEOBFUSCATE, b, stream);
+}
+
+// ---------------------------------------------------------------- QUIC
+
+int sqobfs_quic_keyring_create(sqobfs_ctx *ctx, uint32_t count, const sqobfs_quic_key *keys,
+                               sqobfs_quic_keyring **out) {
+  if (out) *out = nullptr;
+  if (!ctx || !out || count == 0 || !keys) return SQ_EINVAL;
+  SQ_TRY(hipSetDevice(ctx->device));
+  std::vector<sq::QuicKeyDev> h(count);
+  auto le = [](const uint8_t *b) {
+    return (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) |
+           ((uint32_t)b[3] << 24);
+  };
+  for (uint32_t k = 0; k < count; k++) {
+    memset(&h[k], 0, sizeof h[k]);
+    for (int i = 0; i < 8; i++) h[k].key[i] = le(keys[k].key + 4 * i);
+    for (int i = 0; i < 3; i++) h[k].iv[i] = le(keys[k].iv + 4 * i);
+    for (int i = 0; i < 8; i++) h[k].hp[i] = le(keys[k].hp + 4 * i);
+  }
+  sqobfs_quic_keyring *kr = new (std::nothrow) sqobfs_quic_keyring();
+  if (!kr) return SQ_ENOMEM;
+  kr->ctx = ctx;
+  kr->count = count;
+  kr->host0 = h[0];
+  hipError_t e = hipMalloc(&kr->table, sizeof(sq::QuicKeyDev) * count);
+  if (e == hipSuccess)
+    e = hipMemcpy(kr->table, h.data(), sizeof(sq::QuicKeyDev) * count, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    if (kr->table) (void)hipFree(kr->table);
+    delete kr;
+    return hip_status(e);
+  }
+  *out = kr;
+  return SQ_OK;
+}
+
+void sqobfs_quic_keyring_destroy(sqobfs_quic_keyring *kr) {
+  if (!kr) return;
+  (void)hipSetDevice(kr->ctx->device);
+  (void)hipDeviceSynchronize();
+  if (kr->table) (void)hipFree(kr->table);
+  delete kr;
+}
+
+static int quic_launch(int open, sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr,
+                       const sqobfs_quic_batch *b, void *stream) {
+  if (!ctx || !kr || kr->ctx != ctx || !b || b->flags) return SQ_EINVAL;
+  if (b->n == 0) return SQ_OK;
+  if (!b->in || !b->in_off || !b->in_len || !b->out || !b->out_off || !b->out_len ||
+      !b->pn_offset || !b->pn)
+    return SQ_EINVAL;
+  SQ_TRY(hipSetDevice(ctx->device));
+  sq::QParams q;
+  memset(&q, 0, sizeof q);
+  q.in = b->in;
+  q.in_off = b->in_off;
+  q.in_len = b->in_len;
+  q.out = b->out;
+  q.out_off = b->out_off;
+  q.out_len = b->out_len;
+  q.pn_offset = b->pn_offset;
+  q.pn = b->pn;
+  q.key_id = b->key_id;
+  q.pn_out = open ? b->pn_out : nullptr;
+  q.keys = kr->table;
+  q.n = b->n;
+  q.n_keys = kr->count;
+  q.key0 = kr->host0;
+  return sq_launch_quic(open, &q, pick_stream(ctx, stream));
+}
+
+int sqobfs_quic_seal(sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr, const sqobfs_quic_batch *b,
+                     void *stream) {
+  return quic_launch(0, ctx, kr, b, stream);
+}
+
+int sqobfs_quic_open(sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr, const sqobfs_quic_batch *b,
+                     void *stream) {
+  return quic_launch(1, ctx, kr, b, stream);
 }
 
 int sqobfs_host_alloc(sqobfs_ctx *ctx, size_t bytes, void **out) {

@@ -62,7 +62,39 @@ struct KParams {
   PskEntry psk0;
 };
 
+// QUIC 1-RTT keys of one connection as little-endian words (ChaCha20 state
+// order): key, iv (nonce base), hp (header protection key).
+struct QuicKeyDev {
+  uint32_t key[8];
+  uint32_t iv[3];
+  uint32_t hp[8];
+  uint32_t pad;
+};
+static_assert(sizeof(QuicKeyDev) == 80, "QuicKeyDev layout");
+
+// QUIC packet protection launch (sq_quic.hip); key0 = keyring entry 0 by
+// value (single-connection batches read it from the kernarg segment).
+struct QParams {
+  const uint8_t *in;
+  const uint64_t *in_off;
+  const uint32_t *in_len;
+  uint8_t *out;
+  const uint64_t *out_off;
+  uint32_t *out_len;
+  const uint16_t *pn_offset;
+  const uint64_t *pn;
+  const uint16_t *key_id;
+  uint64_t *pn_out;
+  const QuicKeyDev *keys;
+  uint32_t n;
+  uint32_t n_keys;
+  QuicKeyDev key0;
+};
+
 }  // namespace sq
+
+// launchers implemented in sq_quic.hip
+extern "C" int sq_launch_quic(int open, const sq::QParams *qp, void *stream);
 
 // launchers implemented in sq_kernels.hip
 extern "C" int sq_launch_obfs(int kind, int dir, const sq::KParams *kp,

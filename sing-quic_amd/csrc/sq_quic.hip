@@ -1,0 +1,360 @@
+// sq_quic.hip -- gfx950 QUIC packet protection, AEAD_CHACHA20_POLY1305
+// (SURVEY.md 8(f) rank 4).
+//
+// Replaces, for a whole ragged batch per launch, quic-go's per-packet
+//   internal/handshake/aead.go           Seal / Open of 1-RTT packets
+//   internal/handshake/header_protector.go  chacha header protection
+// (quic-go v0.52.0-beta.1, go.mod:7; reached from the reference through
+// quic.go:47-102; not in the reference tree).  The algorithms are RFC 8439
+// sections 2.5 / 2.8 (Poly1305, the AEAD) and RFC 9001 sections 5.3 / 5.4.4
+// (nonce, ChaCha20 header protection); the packet-number decode is RFC 9000
+// Appendix A.3.  The CPU checker is oracle/oracle.c (or_quic_seal / open),
+// pinned by RFC 9001 Appendix A.5 and OpenSSL (tests/golden/quic.json).
+//
+// Decomposition: one lane per packet, 64 packets per wave.  Each lane walks
+// its packet once: ChaCha20 keystream blocks (counter 1..) XOR the payload
+// 16 bytes at a time, every ciphertext chunk goes straight into the Poly1305
+// accumulator (26-bit limbs, v_mad_u64_u32 products), the tag is appended,
+// and the header-protection mask is taken from the sample of the ciphertext
+// still held in registers.  VALU-heavy (~28K instructions per 1350-byte
+// packet), so 64 independent packets per wave keep every lane busy.
+#include <hip/hip_runtime.h>
+
+#include "sq_bytes.h"
+#include "sq_hash.h"
+#include "sq_internal.h"
+
+namespace sq {
+
+constexpr uint32_t kQBlock = 256;
+constexpr uint32_t kQMaxPacket = 1u << 20;
+constexpr uint32_t kQEKey = 0xFFFFFFFFu, kQEShort = 0xFFFFFFFEu, kQEAuth = 0xFFFFFFFDu;
+
+// ---------------------------------------------------------------- Poly1305
+
+struct Poly {
+  uint32_t r0, r1, r2, r3, r4, s1, s2, s3, s4;
+  uint32_t h0, h1, h2, h3, h4;
+};
+
+// r = clamp(otk[0..16)), h = 0 (RFC 8439 2.5.1)
+__device__ __forceinline__ void poly_init(Poly &P, const uint32_t (&otk)[16]) {
+  P.r0 = otk[0] & 0x3ffffffu;
+  P.r1 = __builtin_amdgcn_alignbit(otk[1], otk[0], 26) & 0x3ffff03u;
+  P.r2 = __builtin_amdgcn_alignbit(otk[2], otk[1], 20) & 0x3ffc0ffu;
+  P.r3 = __builtin_amdgcn_alignbit(otk[3], otk[2], 14) & 0x3f03fffu;
+  P.r4 = (otk[3] >> 8) & 0x00fffffu;
+  P.s1 = P.r1 * 5;
+  P.s2 = P.r2 * 5;
+  P.s3 = P.r3 * 5;
+  P.s4 = P.r4 * 5;
+  P.h0 = P.h1 = P.h2 = P.h3 = P.h4 = 0;
+}
+
+__device__ __forceinline__ uint64_t mul(uint32_t a, uint32_t b) { return (uint64_t)a * b; }
+
+// h = (h + m + 2^128) * r mod 2^130 - 5, one full 16-byte block
+__device__ __forceinline__ void poly_block(Poly &P, const uint32_t (&m)[4]) {
+  const uint32_t h0 = P.h0 + (m[0] & 0x3ffffffu);
+  const uint32_t h1 = P.h1 + (__builtin_amdgcn_alignbit(m[1], m[0], 26) & 0x3ffffffu);
+  const uint32_t h2 = P.h2 + (__builtin_amdgcn_alignbit(m[2], m[1], 20) & 0x3ffffffu);
+  const uint32_t h3 = P.h3 + (__builtin_amdgcn_alignbit(m[3], m[2], 14) & 0x3ffffffu);
+  const uint32_t h4 = P.h4 + ((m[3] >> 8) | (1u << 24));
+  const uint64_t d0 = mul(h0, P.r0) + mul(h1, P.s4) + mul(h2, P.s3) + mul(h3, P.s2) + mul(h4, P.s1);
+  uint64_t d1 = mul(h0, P.r1) + mul(h1, P.r0) + mul(h2, P.s4) + mul(h3, P.s3) + mul(h4, P.s2);
+  uint64_t d2 = mul(h0, P.r2) + mul(h1, P.r1) + mul(h2, P.r0) + mul(h3, P.s4) + mul(h4, P.s3);
+  uint64_t d3 = mul(h0, P.r3) + mul(h1, P.r2) + mul(h2, P.r1) + mul(h3, P.r0) + mul(h4, P.s4);
+  uint64_t d4 = mul(h0, P.r4) + mul(h1, P.r3) + mul(h2, P.r2) + mul(h3, P.r1) + mul(h4, P.r0);
+  uint32_t c = (uint32_t)(d0 >> 26);
+  P.h0 = (uint32_t)d0 & 0x3ffffffu;
+  d1 += c; c = (uint32_t)(d1 >> 26); P.h1 = (uint32_t)d1 & 0x3ffffffu;
+  d2 += c; c = (uint32_t)(d2 >> 26); P.h2 = (uint32_t)d2 & 0x3ffffffu;
+  d3 += c; c = (uint32_t)(d3 >> 26); P.h3 = (uint32_t)d3 & 0x3ffffffu;
+  d4 += c; c = (uint32_t)(d4 >> 26); P.h4 = (uint32_t)d4 & 0x3ffffffu;
+  P.h0 += c * 5;
+  c = P.h0 >> 26;
+  P.h0 &= 0x3ffffffu;
+  P.h1 += c;
+}
+
+// tag = (h mod p) + s mod 2^128, s = otk[16..32)
+__device__ __forceinline__ void poly_finish(Poly &P, const uint32_t (&otk)[16],
+                                            uint32_t (&tag)[4]) {
+  uint32_t h0 = P.h0, h1 = P.h1, h2 = P.h2, h3 = P.h3, h4 = P.h4;
+  uint32_t c = h1 >> 26; h1 &= 0x3ffffffu;
+  h2 += c; c = h2 >> 26; h2 &= 0x3ffffffu;
+  h3 += c; c = h3 >> 26; h3 &= 0x3ffffffu;
+  h4 += c; c = h4 >> 26; h4 &= 0x3ffffffu;
+  h0 += c * 5; c = h0 >> 26; h0 &= 0x3ffffffu;
+  h1 += c;
+  uint32_t g0 = h0 + 5; c = g0 >> 26; g0 &= 0x3ffffffu;
+  uint32_t g1 = h1 + c; c = g1 >> 26; g1 &= 0x3ffffffu;
+  uint32_t g2 = h2 + c; c = g2 >> 26; g2 &= 0x3ffffffu;
+  uint32_t g3 = h3 + c; c = g3 >> 26; g3 &= 0x3ffffffu;
+  const uint32_t g4 = h4 + c - (1u << 26);
+  const uint32_t sel = (g4 >> 31) - 1u;  // all ones if h >= p
+  h0 = bsel(sel, g0, h0);
+  h1 = bsel(sel, g1, h1);
+  h2 = bsel(sel, g2, h2);
+  h3 = bsel(sel, g3, h3);
+  h4 = bsel(sel, g4, h4);
+  uint64_t f = (uint64_t)(h0 | (h1 << 26)) + otk[4];
+  tag[0] = (uint32_t)f;
+  f = (uint64_t)((h1 >> 6) | (h2 << 20)) + otk[5] + (f >> 32);
+  tag[1] = (uint32_t)f;
+  f = (uint64_t)((h2 >> 12) | (h3 << 14)) + otk[6] + (f >> 32);
+  tag[2] = (uint32_t)f;
+  f = (uint64_t)((h3 >> 18) | (h4 << 8)) + otk[7] + (f >> 32);
+  tag[3] = (uint32_t)f;
+}
+
+// ---------------------------------------------------------------- helpers
+
+// nonce = iv XOR be96(pn) as little-endian words (RFC 9001 5.3)
+__device__ __forceinline__ void quic_nonce(const QuicKeyDev &K, uint64_t pn, uint32_t (&n)[3]) {
+  n[0] = K.iv[0];
+  n[1] = K.iv[1] ^ __builtin_bswap32((uint32_t)(pn >> 32));
+  n[2] = K.iv[2] ^ __builtin_bswap32((uint32_t)pn);
+}
+
+// 5 mask bytes (RFC 9001 5.4.4): ChaCha20(hp, counter = sample[0..4),
+// nonce = sample[4..16)) of zeros; returned as words (bytes 0..3, byte 4)
+__device__ __forceinline__ void hp_mask(const QuicKeyDev &K, const uint32_t (&sample)[4],
+                                        uint32_t &m0, uint32_t &m1) {
+  const uint32_t nonce[3] = {sample[1], sample[2], sample[3]};
+  uint32_t blk[16];
+  chacha20_block(K.hp, sample[0], nonce, blk);
+  m0 = blk[0];
+  m1 = blk[1] & 0xFFu;
+}
+
+// mask byte k (0..4) of (m0, m1)
+__device__ __forceinline__ uint32_t mask_byte(uint32_t m0, uint32_t m1, uint32_t k) {
+  return k < 4 ? (m0 >> (8 * k)) & 0xFFu : m1;
+}
+
+// Set byte `pos` (0..15, runtime) of a 16-byte register value to b.
+__device__ __forceinline__ void set_byte(uint32_t (&v)[4], uint32_t pos, uint32_t b) {
+  const uint32_t sh = 8 * (pos & 3), w = pos >> 2;
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) {
+    const uint32_t nv = (v[j] & ~(0xFFu << sh)) | (b << sh);
+    v[j] = bsel(j == w, nv, v[j]);
+  }
+}
+
+// byte k (0..31, runtime) of an 8-word register image
+__device__ __forceinline__ uint32_t byte32(const uint32_t (&v)[8], uint32_t k) {
+  const uint32_t w = k >> 2;
+  uint32_t a = bsel(w & 1, v[1], v[0]), b = bsel(w & 1, v[3], v[2]);
+  uint32_t c = bsel(w & 1, v[5], v[4]), d = bsel(w & 1, v[7], v[6]);
+  a = bsel(w & 2, b, a);
+  c = bsel(w & 2, d, c);
+  return (bsel(w & 4, c, a) >> (8 * (k & 3))) & 0xFFu;
+}
+
+// RFC 9000 Appendix A.3
+__device__ __forceinline__ uint64_t decode_pn(uint64_t largest, uint64_t truncated, uint32_t nbits) {
+  const uint64_t expected = largest + 1, win = 1ull << nbits, hwin = win / 2, mask = win - 1;
+  const uint64_t cand = (expected & ~mask) | truncated;
+  if (cand + hwin <= expected && cand < (1ull << 62) - win) return cand + win;
+  if (cand > expected + hwin && cand >= win) return cand - win;
+  return cand;
+}
+
+// Payload pass shared by seal (MAC over the output) and open (MAC over the
+// input): XOR `len` bytes from src with the keystream from counter 1, MAC
+// the ciphertext side, store to dst.  first32 receives ciphertext bytes
+// 0..31 (zero past len) for the header-protection sample.
+template <bool SEAL>
+__device__ __forceinline__ void payload_pass(const QuicKeyDev &K, const uint32_t (&nonce)[3],
+                                             uint64_t src, uint64_t dst, uint32_t len, Poly &P,
+                                             uint32_t (&first32)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; j++) first32[j] = 0u;
+  for (uint32_t b = 0; b * 64 < len; b++) {
+    uint32_t ks[16];
+    chacha20_block(K.key, 1 + b, nonce, ks);
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) {
+      const uint32_t off = b * 64 + q * 16;
+      if (off < len) {
+        const uint32_t nb = len - off < 16 ? len - off : 16;
+        uint32_t in[4], out[4];
+        load16(src + off, src + len, in);
+#pragma unroll
+        for (int j = 0; j < 4; j++) out[j] = (in[j] ^ ks[4 * q + j]) & range_mask(0, nb, j);
+        if (SEAL) poly_block(P, out);
+        else poly_block(P, in);
+        store16(dst + off, out, nb);
+        if (b == 0 && q < 2) {
+#pragma unroll
+          for (int j = 0; j < 4; j++) first32[4 * q + j] = SEAL ? out[j] : in[j];
+        }
+      }
+    }
+  }
+}
+
+// lengths block of the AEAD MAC: le64(aad_len) || le64(ct_len)
+__device__ __forceinline__ void poly_lengths(Poly &P, uint32_t aad, uint32_t ct) {
+  const uint32_t m[4] = {aad, 0u, ct, 0u};
+  poly_block(P, m);
+}
+
+// ---------------------------------------------------------------- kernels
+
+template <bool MULTI>
+__device__ __forceinline__ bool pick_key(const QParams &Q, uint32_t p, const QuicKeyDev *&K) {
+  K = &Q.key0;
+  if (!MULTI) return true;
+  const uint32_t kid = Q.key_id[p];
+  if (kid >= Q.n_keys) return false;
+  K = Q.keys + kid;
+  return true;
+}
+
+template <bool MULTI>
+__global__ __launch_bounds__(kQBlock) void quic_seal_kernel(const QParams Q) {
+  const uint64_t p64 = (uint64_t)blockIdx.x * kQBlock + threadIdx.x;
+  if (p64 >= Q.n) return;
+  const uint32_t p = (uint32_t)p64;
+  const QuicKeyDev *K;
+  if (!pick_key<MULTI>(Q, p, K)) {
+    Q.out_len[p] = kQEKey;
+    return;
+  }
+  const uint64_t src = (uint64_t)Q.in + Q.in_off[p], dst = (uint64_t)Q.out + Q.out_off[p];
+  const uint32_t len = Q.in_len[p], pno = Q.pn_offset[p];
+  const uint32_t first = len ? gld<uint8_t>(src) : 0u;
+  const uint32_t pn_len = (first & 3) + 1, hdr = pno + pn_len;
+  if (len == 0 || len > kQMaxPacket || hdr > len || pno + 4 > len) {
+    Q.out_len[p] = kQEShort;
+    return;
+  }
+  const uint32_t pl = len - hdr;
+  uint32_t nonce[3], otk[16];
+  quic_nonce(*K, Q.pn[p], nonce);
+  chacha20_block(K->key, 0, nonce, otk);
+  Poly P;
+  poly_init(P, otk);
+  // AAD = the unprotected header (copied to the output unchanged for now)
+  for (uint32_t q = 0; q < hdr; q += 16) {
+    uint32_t w[4];
+    load16(src + q, src + hdr, w);
+    poly_block(P, w);
+    if (dst != src) store16(dst + q, w, hdr - q < 16 ? hdr - q : 16);
+  }
+  uint32_t ct32[8];
+  payload_pass<true>(*K, nonce, src + hdr, dst + hdr, pl, P, ct32);
+  poly_lengths(P, hdr, pl);
+  uint32_t tag[4];
+  poly_finish(P, otk, tag);
+  store16(dst + len, tag, 16);
+  // header protection: sample = (ciphertext || tag)[4 - pn_len ..][0..16)
+  const uint32_t so = 4 - pn_len;
+  uint32_t sample[4];
+  if (pl >= so + 16) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) sample[j] = __builtin_amdgcn_alignbyte(ct32[j + 1], ct32[j], so);
+  } else {  // short payload: the sample reaches into the tag
+    const uint32_t t8[8] = {tag[0], tag[1], tag[2], tag[3], 0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int j = 0; j < 4; j++) sample[j] = 0u;
+    for (uint32_t i = 0; i < 16; i++) {
+      const uint32_t k = so + i;
+      const uint32_t b = k < pl ? byte32(ct32, k) : byte32(t8, k - pl);
+      sample[i >> 2] |= b << (8 * (i & 3));
+    }
+  }
+  uint32_t m0, m1;
+  hp_mask(*K, sample, m0, m1);
+  gst<uint8_t>(dst, (uint8_t)(first ^ (m0 & ((first & 0x80) ? 0x0Fu : 0x1Fu))));
+  for (uint32_t i = 0; i < pn_len; i++) {
+    const uint32_t b = gld<uint8_t>(src + pno + i);
+    gst<uint8_t>(dst + pno + i, (uint8_t)(b ^ mask_byte(m0, m1, 1 + i)));
+  }
+  Q.out_len[p] = len + 16;
+}
+
+template <bool MULTI>
+__global__ __launch_bounds__(kQBlock) void quic_open_kernel(const QParams Q) {
+  const uint64_t p64 = (uint64_t)blockIdx.x * kQBlock + threadIdx.x;
+  if (p64 >= Q.n) return;
+  const uint32_t p = (uint32_t)p64;
+  const QuicKeyDev *K;
+  if (!pick_key<MULTI>(Q, p, K)) {
+    Q.out_len[p] = kQEKey;
+    return;
+  }
+  const uint64_t src = (uint64_t)Q.in + Q.in_off[p], dst = (uint64_t)Q.out + Q.out_off[p];
+  const uint32_t len = Q.in_len[p], pno = Q.pn_offset[p];
+  if (len < 16 || len > kQMaxPacket || pno + 4 + 16 > len) {
+    Q.out_len[p] = kQEShort;
+    return;
+  }
+  uint32_t sample[4], rtag[4];
+  load16(src + pno + 4, src + len, sample);
+  load16(src + len - 16, src + len, rtag);  // before any in-place write
+  uint32_t m0, m1;
+  hp_mask(*K, sample, m0, m1);
+  const uint32_t pfirst = gld<uint8_t>(src);
+  const uint32_t first = pfirst ^ (m0 & ((pfirst & 0x80) ? 0x0Fu : 0x1Fu));
+  const uint32_t pn_len = (first & 3) + 1, hdr = pno + pn_len;
+  if (hdr > len - 16) {
+    Q.out_len[p] = kQEShort;
+    return;
+  }
+  uint64_t trunc = 0;
+  uint32_t pnb[4] = {0u, 0u, 0u, 0u};
+  for (uint32_t i = 0; i < pn_len; i++) {
+    pnb[i] = gld<uint8_t>(src + pno + i) ^ mask_byte(m0, m1, 1 + i);
+    trunc = (trunc << 8) | pnb[i];
+  }
+  const uint64_t pn = decode_pn(Q.pn[p], trunc, 8 * pn_len);
+  if (Q.pn_out) Q.pn_out[p] = pn;
+  uint32_t nonce[3], otk[16];
+  quic_nonce(*K, pn, nonce);
+  chacha20_block(K->key, 0, nonce, otk);
+  Poly P;
+  poly_init(P, otk);
+  // AAD = the unprotected header: protected bytes patched, then written out
+  for (uint32_t q = 0; q < hdr; q += 16) {
+    uint32_t w[4];
+    load16(src + q, src + hdr, w);
+    if (q == 0) set_byte(w, 0, first);
+    for (uint32_t i = 0; i < pn_len; i++) {
+      const uint32_t pos = pno + i;
+      if (pos >= q && pos < q + 16) set_byte(w, pos - q, pnb[i]);
+    }
+    poly_block(P, w);
+    store16(dst + q, w, hdr - q < 16 ? hdr - q : 16);
+  }
+  const uint32_t cl = len - 16 - hdr;
+  uint32_t ct32[8];
+  payload_pass<false>(*K, nonce, src + hdr, dst + hdr, cl, P, ct32);
+  poly_lengths(P, hdr, cl);
+  uint32_t tag[4];
+  poly_finish(P, otk, tag);
+  const bool ok = ((tag[0] ^ rtag[0]) | (tag[1] ^ rtag[1]) | (tag[2] ^ rtag[2]) |
+                   (tag[3] ^ rtag[3])) == 0;
+  Q.out_len[p] = ok ? len - 16 : kQEAuth;
+}
+
+}  // namespace sq
+
+extern "C" int sq_launch_quic(int open, const sq::QParams *qp, void *stream) {
+  using namespace sq;
+  if (qp->n == 0) return 0;
+  const dim3 grid((qp->n + kQBlock - 1) / kQBlock);
+  hipStream_t s = (hipStream_t)stream;
+  const bool multi = qp->key_id != nullptr;
+  if (open) {
+    if (multi) hipLaunchKernelGGL(quic_open_kernel<true>, grid, dim3(kQBlock), 0, s, *qp);
+    else hipLaunchKernelGGL(quic_open_kernel<false>, grid, dim3(kQBlock), 0, s, *qp);
+  } else {
+    if (multi) hipLaunchKernelGGL(quic_seal_kernel<true>, grid, dim3(kQBlock), 0, s, *qp);
+    else hipLaunchKernelGGL(quic_seal_kernel<false>, grid, dim3(kQBlock), 0, s, *qp);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}

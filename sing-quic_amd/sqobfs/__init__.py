@@ -80,6 +80,31 @@ class Addr(ctypes.Structure):
         return str(ip), int(self.port)
 
 
+class QuicKey(ctypes.Structure):
+    """sqobfs_quic_key: one connection's 1-RTT key, iv, hp."""
+    _fields_ = [("key", ctypes.c_uint8 * 32), ("iv", ctypes.c_uint8 * 12),
+                ("hp", ctypes.c_uint8 * 32)]
+
+    @classmethod
+    def of(cls, key: bytes, iv: bytes, hp: bytes) -> "QuicKey":
+        k = cls()
+        ctypes.memmove(k.key, key, 32)
+        ctypes.memmove(k.iv, iv, 12)
+        ctypes.memmove(k.hp, hp, 32)
+        return k
+
+
+class QuicBatch(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint32), ("flags", ctypes.c_uint32), ("in_", ctypes.c_void_p),
+                ("in_off", ctypes.c_void_p), ("in_len", ctypes.c_void_p),
+                ("out", ctypes.c_void_p), ("out_off", ctypes.c_void_p),
+                ("out_len", ctypes.c_void_p), ("pn_offset", ctypes.c_void_p),
+                ("pn", ctypes.c_void_p), ("key_id", ctypes.c_void_p), ("pn_out", ctypes.c_void_p)]
+
+
+QUIC_EKEY, QUIC_ESHORT, QUIC_EAUTH = 0xFFFFFFFF, 0xFFFFFFFE, 0xFFFFFFFD
+
+
 class UdpView(ctypes.Structure):
     _fields_ = [("count", ctypes.c_uint32), ("base", ctypes.c_void_p), ("off", ctypes.c_void_p),
                 ("len", ctypes.c_void_p), ("fd_index", ctypes.c_void_p),
@@ -136,6 +161,11 @@ def lib() -> ctypes.CDLL:
     L.sqobfs_udp_conn_tx_payload.argtypes = [vp, u32]
     L.sqobfs_udp_conn_tx_payload.restype = vp
     L.sqobfs_udp_conn_write.argtypes = [vp, u32, u32, vp, vp, u32p]
+    L.sqobfs_quic_keyring_create.argtypes = [vp, u32, vp, ctypes.POINTER(vp)]
+    L.sqobfs_quic_keyring_destroy.argtypes = [vp]
+    L.sqobfs_quic_keyring_destroy.restype = None
+    L.sqobfs_quic_seal.argtypes = [vp, vp, ctypes.POINTER(QuicBatch), vp]
+    L.sqobfs_quic_open.argtypes = [vp, vp, ctypes.POINTER(QuicBatch), vp]
     L.sqobfs_salt_key.argtypes = [vp, vp, ctypes.c_uint64]
     L.sqobfs_salt_seq.argtypes = [vp]
     L.sqobfs_salt_seq.restype = ctypes.c_uint64
@@ -425,3 +455,45 @@ class UdpConn:
         _check(lib().sqobfs_udp_conn_write(self.handle, fd_index, len(payloads), _ptr(lens), arr,
                                            ctypes.byref(sent)), "sqobfs_udp_conn_write")
         return sent.value
+
+
+# ---------------------------------------------------------------- QUIC
+
+class QuicKeyring:
+    """Device copy of per-connection QUIC 1-RTT keys (sqobfs_quic_keyring)."""
+
+    def __init__(self, ctx: Context, keys: list[QuicKey]):
+        arr = (QuicKey * len(keys))(*keys)
+        h = ctypes.c_void_p()
+        _check(lib().sqobfs_quic_keyring_create(ctx.handle, len(keys), arr, ctypes.byref(h)),
+               "sqobfs_quic_keyring_create")
+        self.handle = h
+        self.ctx = ctx
+        self.count = len(keys)
+
+    def close(self) -> None:
+        if self.handle:
+            lib().sqobfs_quic_keyring_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def quic_batch(n, in_, in_off, in_len, out, out_off, out_len, pn_offset, pn, key_id=None,
+               pn_out=None) -> QuicBatch:
+    return QuicBatch(n, 0, _ptr(in_), _ptr(in_off), _ptr(in_len), _ptr(out), _ptr(out_off),
+                     _ptr(out_len), _ptr(pn_offset), _ptr(pn), _ptr(key_id), _ptr(pn_out))
+
+
+def quic_seal(ctx: Context, kr: QuicKeyring, batch: QuicBatch, stream=None) -> None:
+    _check(lib().sqobfs_quic_seal(ctx.handle, kr.handle, ctypes.byref(batch), stream),
+           "sqobfs_quic_seal")
+
+
+def quic_open(ctx: Context, kr: QuicKeyring, batch: QuicBatch, stream=None) -> None:
+    _check(lib().sqobfs_quic_open(ctx.handle, kr.handle, ctypes.byref(batch), stream),
+           "sqobfs_quic_open")

@@ -62,6 +62,15 @@ def lib() -> ctypes.CDLL:
         L.or_chacha20_stream.restype = None
         L.or_device_salts.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, vp]
         L.or_device_salts.restype = None
+        L.or_poly1305.argtypes = [vp, vp, sz, vp]
+        L.or_poly1305.restype = None
+        L.or_aead_seal.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp]
+        L.or_aead_seal.restype = None
+        L.or_quic_seal.argtypes = [vp, vp, vp, ctypes.c_uint64, vp, sz, sz, vp]
+        L.or_quic_seal.restype = ctypes.c_long
+        L.or_quic_open.argtypes = [vp, vp, vp, ctypes.c_uint64, vp, sz, sz, vp,
+                                   ctypes.POINTER(ctypes.c_uint64)]
+        L.or_quic_open.restype = ctypes.c_long
         L.or_batch_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(OrPsks),
                                    ctypes.POINTER(OrBatch), ctypes.c_int]
         L.or_fnv64.argtypes = [vp, sz, ctypes.c_uint64]
@@ -184,3 +193,33 @@ def device_salts(key: bytes, seq: int, n: int, S: int) -> bytes:
     out = ctypes.create_string_buffer(max(n * S, 1))
     lib().or_device_salts(key, seq, n, S, out)
     return out.raw[:n * S]
+
+
+def poly1305(key: bytes, msg: bytes) -> bytes:
+    tag = ctypes.create_string_buffer(16)
+    lib().or_poly1305(key, msg, len(msg), tag)
+    return tag.raw
+
+
+def aead_seal(key: bytes, nonce: bytes, aad: bytes, pt: bytes) -> bytes:
+    """ct || tag (RFC 8439 2.8)."""
+    ct = ctypes.create_string_buffer(max(len(pt), 1))
+    tag = ctypes.create_string_buffer(16)
+    lib().or_aead_seal(key, nonce, aad, len(aad), pt, len(pt), ct, tag)
+    return ct.raw[:len(pt)] + tag.raw
+
+
+def quic_seal(key: bytes, iv: bytes, hp: bytes, pn: int, pkt: bytes, pn_offset: int):
+    """(protected packet, return code) -- RFC 9001 5.3/5.4, ChaCha20-Poly1305."""
+    out = ctypes.create_string_buffer(len(pkt) + 16)
+    r = lib().or_quic_seal(key, iv, hp, pn, pkt, len(pkt), pn_offset, out)
+    return (out.raw[:r] if r > 0 else b""), r
+
+
+def quic_open(key: bytes, iv: bytes, hp: bytes, largest_pn: int, pkt: bytes, pn_offset: int):
+    """(unprotected header || plaintext, return code, decoded pn)."""
+    out = ctypes.create_string_buffer(max(len(pkt), 1))
+    pn = ctypes.c_uint64(0)
+    r = lib().or_quic_open(key, iv, hp, largest_pn, pkt, len(pkt), pn_offset, out,
+                           ctypes.byref(pn))
+    return (out.raw[:len(pkt) - 16] if len(pkt) >= 16 else b""), r, pn.value

@@ -160,3 +160,35 @@ def test_device_salt_derivation(golden):
         for i in (0, v["n"] - 1):
             blk = ol.chacha20_stream(B(v["key"]), nonce, i // per, 64)
             assert got[i * v["S"]:(i + 1) * v["S"]] == blk[(i % per) * v["S"]:(i % per + 1) * v["S"]]
+
+
+def test_poly1305_and_aead(golden):
+    """Poly1305 / AEAD restatement vs RFC 8439 2.5.2 and OpenSSL."""
+    g = golden("quic.json")
+    for v in g["poly1305"]:
+        assert ol.poly1305(B(v["key"]), B(v["msg"])).hex() == v["tag"]
+    for v in g["aead"]:
+        assert ol.aead_seal(B(v["key"]), B(v["nonce"]), B(v["aad"]), B(v["pt"])).hex() == \
+            v["ct_tag"]
+
+
+def test_quic_packet_protection(golden):
+    """QUIC seal / open restatement vs RFC 9001 A.5 and OpenSSL-built
+    packets (short and long headers, pn lengths 1-4, minimum-size payloads)."""
+    g = golden("quic.json")
+    a5 = g["rfc9001_a5"]
+    prot, r = ol.quic_seal(B(a5["key"]), B(a5["iv"]), B(a5["hp"]), a5["pn"],
+                           B(a5["header"] + a5["payload"]), a5["pn_offset"])
+    assert prot.hex() == a5["protected"]
+    plain, r, pn = ol.quic_open(B(a5["key"]), B(a5["iv"]), B(a5["hp"]), a5["pn"] - 1,
+                                B(a5["protected"]), a5["pn_offset"])
+    assert r > 0 and pn == a5["pn"] and plain.hex() == a5["header"] + a5["payload"]
+    for v in g["packets"]:
+        k, iv, hp = B(v["key"]), B(v["iv"]), B(v["hp"])
+        prot, r = ol.quic_seal(k, iv, hp, v["pn"], B(v["packet"]), v["pn_offset"])
+        assert prot.hex() == v["protected"]
+        plain, r, pn = ol.quic_open(k, iv, hp, v["largest_pn"], prot, v["pn_offset"])
+        assert r == len(prot) - 16 and pn == v["pn"] and plain.hex() == v["packet"]
+        bad = bytearray(prot)
+        bad[-1] ^= 1  # tag bit flip
+        assert ol.quic_open(k, iv, hp, v["largest_pn"], bytes(bad), v["pn_offset"])[1] == -2
