@@ -68,6 +68,9 @@ def parse():
     ap.add_argument("--device-salt", action="store_true",
                     help="obfuscate with SQOBFS_FLAG_DEVICE_SALT (salts from the GPU's "
                          "ChaCha20 generator; 2L+S bytes per packet)")
+    ap.add_argument("--quic", action="store_true",
+                    help="also time QUIC ChaCha20-Poly1305 packet protection (seal/open of "
+                         "1M short-header packets, SURVEY.md 8(f) rank 4)")
     ap.add_argument("--udp", action="store_true",
                     help="also time loopback UDP end to end through the batched socket "
                          "layer (sqobfs_udp_conn: sendmmsg/recvmmsg + GPU)")
@@ -432,6 +435,8 @@ def main():
         out["roofline"]["traffic_source"] = pmc.get("source")
     if args.e2e and rank == 0:
         out["e2e"] = e2e_rate(torch, sqobfs, ctx, kr, kind, min(n, 1 << 18), L or 758)
+    if args.quic and rank == 0:
+        out["quic"] = quic_rate(torch, sqobfs, ctx, dev, max(5, args.steps))
     if args.udp and rank == 0:
         out["udp_e2e"] = [udp_rate(sqobfs, ctx, kr, kind, L or 758, batch=bt)
                           for bt in (64, 256, 1024)]
@@ -485,6 +490,97 @@ def e2e_rate(torch, sqobfs, ctx, kr, kind, n, L):
     for p in pins:
         p.free()
     res["path"] = "sqobfs_run_host: 8-chunk H2D | kernel | D2H pipeline on 3 HIP streams"
+    return res
+
+
+def quic_rate(torch, sqobfs, ctx, dev, steps, n=1 << 20, payload=1350, cpu_seconds=2.0):
+    """QUIC 1-RTT packet protection: seal and open
+    of n short-header packets (1 + 8-byte DCID + 2-byte packet number +
+    `payload` bytes), dense in HBM, one key.  Algorithmic bytes per packet:
+    seal reads len, writes len + 16; open reads len + 16, writes len.
+    Parity: sampled packets against the oracle.  CPU leg: the oracle's
+    threaded or_quic_seal_batch on a bounded sample."""
+    import numpy as np
+    import oracle_lib as ol
+    hdr = 11
+    ln = hdr + payload
+    rng = np.random.Generator(np.random.PCG64(12))
+    key, iv, hp = (rng.integers(0, 256, m, dtype=np.uint8).tobytes() for m in (32, 12, 32))
+    in_off = torch.arange(n, device=dev, dtype=torch.int64) * ln
+    out_off = torch.arange(n, device=dev, dtype=torch.int64) * (ln + 16)
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    data = torch.randint(0, 256, (n * ln,), generator=g, device=dev, dtype=torch.uint8)
+    data.view(n, ln)[:, 0] = 0x41  # short header, pn_len 2
+    pn = torch.arange(n, device=dev, dtype=torch.int64) + 1000
+    data.view(n, ln)[:, 9] = ((pn >> 8) & 0xFF).to(torch.uint8)
+    data.view(n, ln)[:, 10] = (pn & 0xFF).to(torch.uint8)
+    sealed = torch.zeros(n * (ln + 16), device=dev, dtype=torch.uint8)
+    opened = torch.zeros(n * ln, device=dev, dtype=torch.uint8)
+    lens = torch.full((n,), ln, device=dev, dtype=torch.int32)
+    slens = torch.full((n,), ln + 16, device=dev, dtype=torch.int32)
+    pno = torch.full((n,), 9, device=dev, dtype=torch.int16)
+    largest = pn - 1
+    olen = torch.zeros(n, device=dev, dtype=torch.int32)
+    olen2 = torch.zeros(n, device=dev, dtype=torch.int32)
+    pn_out = torch.zeros(n, device=dev, dtype=torch.int64)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    res = {"packets": n, "packet_bytes": ln, "payload_bytes": payload,
+           "cipher": "AEAD_CHACHA20_POLY1305 + ChaCha20 header protection (RFC 9001)"}
+    with sqobfs.QuicKeyring(ctx, [sqobfs.QuicKey.of(key, iv, hp)]) as kr:
+        bs = sqobfs.quic_batch(n, data, in_off, lens, sealed, out_off, olen, pno, pn)
+        bo = sqobfs.quic_batch(n, sealed, out_off, slens, opened, in_off, olen2, pno, largest,
+                               pn_out=pn_out)
+        for name, fn, b, alg in (("seal", sqobfs.quic_seal, bs, n * (2 * ln + 16)),
+                                 ("open", sqobfs.quic_open, bo, n * (2 * ln + 16))):
+            for _ in range(2):
+                fn(ctx, kr, b, s)
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(steps)]
+            for e0, e1 in ev:
+                e0.record()
+                fn(ctx, kr, b, s)
+                e1.record()
+            torch.cuda.synchronize(dev)
+            ms = sum(e0.elapsed_time(e1) for e0, e1 in ev) / steps
+            res[name] = {"kernel_avg_us": round(ms * 1e3, 2),
+                         "GiB_s_payload": round(n * payload / (ms * 1e-3) / 2**30, 2),
+                         "achieved_GBs": round(alg / (ms * 1e-3) / 1e9, 1),
+                         "frac_of_8TBs": round(alg / (ms * 1e-3) / 8e12, 4)}
+    # parity on sampled packets
+    idx = sorted(set([0, n - 1] + list(range(0, n, 4099))))[:300]
+    d = data.view(n, ln)[idx].cpu().numpy()
+    sl = sealed.view(n, ln + 16)[idx].cpu().numpy()
+    op = opened.view(n, ln)[idx].cpu().numpy()
+    ok = bool((olen.cpu().numpy() == ln + 16).all() and (olen2.cpu().numpy() == ln).all()
+              and (pn_out.cpu().numpy() == pn.cpu().numpy()).all())
+    for k, i in enumerate(idx):
+        want, _ = ol.quic_seal(key, iv, hp, 1000 + i, d[k].tobytes(), 9)
+        ok = ok and sl[k].tobytes() == want and op[k].tobytes() == d[k].tobytes()
+    res["parity_spot_check"] = ok
+    # CPU leg: oracle (scalar C restatement), threaded
+    m = 65536
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    cin = np.tile(d[0], m)
+    ci_off = np.arange(m, dtype=np.uint64) * ln
+    co_off = np.arange(m, dtype=np.uint64) * (ln + 16)
+    cout = np.zeros(m * (ln + 16), np.uint8)
+    c_len = np.full(m, ln, np.uint32)
+    c_pno = np.full(m, 9, np.uint16)
+    c_pn = np.arange(m, dtype=np.uint64)
+    L_ = ol.lib()
+    reps = 0
+    t0 = time.perf_counter()
+    while reps < 1 or time.perf_counter() - t0 < cpu_seconds:
+        L_.or_quic_seal_batch(key, iv, hp, cin.ctypes.data, ci_off.ctypes.data, c_len.ctypes.data,
+                              c_pno.ctypes.data, c_pn.ctypes.data, m, cout.ctypes.data,
+                              co_off.ctypes.data, threads)
+        reps += 1
+    dt = time.perf_counter() - t0
+    res["cpu_baseline"] = {"value": round(reps * m * payload / dt / 2**30, 3), "unit": "GiB/s",
+                           "cores": threads, "kind": "port",
+                           "sample": f"{reps} x {m} packets seal, oracle/oracle.c "
+                                     "or_quic_seal_batch (scalar C, not OpenSSL)"}
     return res
 
 

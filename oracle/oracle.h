@@ -83,6 +83,12 @@ long or_quic_open(const uint8_t key[32], const uint8_t iv[12], const uint8_t hp[
                   uint64_t largest_pn, const uint8_t *pkt, size_t len, size_t pn_offset,
                   uint8_t *out, uint64_t *pn_out);
 
+/* or_quic_seal over a batch (one key) on nthreads threads; 0 or -1. */
+int or_quic_seal_batch(const uint8_t key[32], const uint8_t iv[12], const uint8_t hp[32],
+                       const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
+                       const uint16_t *pn_offset, const uint64_t *pn, uint32_t n, uint8_t *out,
+                       const uint64_t *out_off, int nthreads);
+
 /* Salamander key: BLAKE2b-256(psk || salt[0:8])  (salamander.go:50,61,84,99) */
 void or_salamander_key(const uint8_t *psk, size_t psk_len,
                        const uint8_t salt[8], uint8_t key[32]);

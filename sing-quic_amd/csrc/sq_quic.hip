@@ -12,12 +12,16 @@
 // pinned by RFC 9001 Appendix A.5 and OpenSSL (tests/golden/quic.json).
 //
 // Decomposition: one lane per packet, 64 packets per wave.  Each lane walks
-// its packet once: ChaCha20 keystream blocks (counter 1..) XOR the payload
-// 16 bytes at a time, every ciphertext chunk goes straight into the Poly1305
-// accumulator (26-bit limbs, v_mad_u64_u32 products), the tag is appended,
-// and the header-protection mask is taken from the sample of the ciphertext
-// still held in registers.  VALU-heavy (~28K instructions per 1350-byte
-// packet), so 64 independent packets per wave keep every lane busy.
+// its packet once in 64-byte steps: one ChaCha20 keystream block (counter
+// 1..) XORs four 16-byte chunks, every ciphertext chunk goes straight into
+// the Poly1305 accumulator (26-bit limbs, v_mad_u64_u32 products), the tag
+// is appended, and the header-protection mask is taken from the sample of
+// the ciphertext still held in registers.  The input is read as aligned
+// 16-byte blocks one step ahead and realigned in registers, the output is
+// written as aligned 16-byte blocks (streaming realigner), so any packet
+// alignment costs one load and one store per 16 bytes.  VALU-heavy (~25K
+// instructions per 1350-byte packet): 64 independent packets per wave keep
+// every lane busy.
 #include <hip/hip_runtime.h>
 
 #include "sq_bytes.h"
@@ -26,6 +30,9 @@
 
 namespace sq {
 
+#ifndef SQ_QABLATE
+#define SQ_QABLATE 0  // timing builds only (never the shipped .so)
+#endif
 constexpr uint32_t kQBlock = 256;
 constexpr uint32_t kQMaxPacket = 1u << 20;
 constexpr uint32_t kQEKey = 0xFFFFFFFFu, kQEShort = 0xFFFFFFFEu, kQEAuth = 0xFFFFFFFDu;
@@ -162,37 +169,103 @@ __device__ __forceinline__ uint64_t decode_pn(uint64_t largest, uint64_t truncat
   return cand;
 }
 
+// 16 bytes starting at byte o (0..16) of the 32-byte concatenation lo || hi
+__device__ __forceinline__ void funnel(const uint32_t (&lo)[4], const uint32_t (&hi)[4],
+                                       uint32_t o, uint32_t (&out)[4]) {
+  const uint32_t w[12] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3], 0u, 0u, 0u, 0u};
+  win16(w, o, out);
+}
+
 // Payload pass shared by seal (MAC over the output) and open (MAC over the
 // input): XOR `len` bytes from src with the keystream from counter 1, MAC
-// the ciphertext side, store to dst.  first32 receives ciphertext bytes
-// 0..31 (zero past len) for the header-protection sample.
+// the ciphertext side, store to dst.  A streaming realigner: one aligned
+// 16-byte load of the input and one aligned 16-byte store of the output per
+// chunk, whatever the alignments of src and dst (only the first and last
+// output blocks are partial stores; only aligned blocks holding valid input
+// bytes are read).  In place (src == dst) works: every input block is loaded
+// before the output block at the same address is stored.  first32 receives
+// ciphertext bytes 0..31 (zero past len) for the header-protection sample.
 template <bool SEAL>
 __device__ __forceinline__ void payload_pass(const QuicKeyDev &K, const uint32_t (&nonce)[3],
                                              uint64_t src, uint64_t dst, uint32_t len, Poly &P,
                                              uint32_t (&first32)[8]) {
 #pragma unroll
   for (int j = 0; j < 8; j++) first32[j] = 0u;
-  for (uint32_t b = 0; b * 64 < len; b++) {
+  if (len == 0) return;
+  const uint32_t ib = (uint32_t)(src & 15), oa = (uint32_t)(dst & 15);
+  const uint64_t S0 = src - ib, D0 = dst - oa;
+  const uint64_t last = (src + len - 1) & ~15ull;  // last aligned block with valid bytes
+  // aligned input block i (0 = the one holding src), zero past the end; the
+  // address is clamped so the load is unconditional (no branch, exact waits)
+  auto load_blk = [&](uint32_t i, uint32_t (&v)[4]) {
+    const uint64_t A = S0 + 16ull * i;
+#if SQ_QABLATE  // timing-only: no payload loads
+    const u32x4 x = {(uint32_t)A, 1u, 2u, 3u};
+#else
+    const u32x4 x = gld<u32x4>(A < last ? A : last);
+#endif
+    const bool ok = A <= last;
+    v[0] = ok ? x.x : 0u; v[1] = ok ? x.y : 0u; v[2] = ok ? x.z : 0u; v[3] = ok ? x.w : 0u;
+  };
+  uint32_t in_prev[4], prev_c[4] = {0u, 0u, 0u, 0u};
+  uint32_t cur[4][4], nxt[4][4];
+  load_blk(0, in_prev);
+#pragma unroll
+  for (int q = 0; q < 4; q++) load_blk(1 + q, cur[q]);
+  const uint32_t nchunk = (len + 15) / 16, nstep = (nchunk + 3) / 4;
+  for (uint32_t st = 0; st < nstep; st++) {
+    // the next step's 64 input bytes are in flight during this step's
+    // ChaCha20 block and MAC
+#pragma unroll
+    for (int q = 0; q < 4; q++) load_blk(4 * st + 5 + q, nxt[q]);
     uint32_t ks[16];
-    chacha20_block(K.key, 1 + b, nonce, ks);
+    chacha20_block(K.key, 1 + st, nonce, ks);
 #pragma unroll
     for (uint32_t q = 0; q < 4; q++) {
-      const uint32_t off = b * 64 + q * 16;
-      if (off < len) {
-        const uint32_t nb = len - off < 16 ? len - off : 16;
-        uint32_t in[4], out[4];
-        load16(src + off, src + len, in);
+      const uint32_t j = 4 * st + q;
+      if (j < nchunk) {
+        const uint32_t nb = len - 16 * j < 16 ? len - 16 * j : 16;
+        uint32_t in[4], c[4];
+        funnel(in_prev, cur[q], ib, in);
 #pragma unroll
-        for (int j = 0; j < 4; j++) out[j] = (in[j] ^ ks[4 * q + j]) & range_mask(0, nb, j);
-        if (SEAL) poly_block(P, out);
-        else poly_block(P, in);
-        store16(dst + off, out, nb);
-        if (b == 0 && q < 2) {
-#pragma unroll
-          for (int j = 0; j < 4; j++) first32[4 * q + j] = SEAL ? out[j] : in[j];
+        for (int w = 0; w < 4; w++) {
+          in_prev[w] = cur[q][w];
+          in[w] &= range_mask(0, (int)nb, w);
+          c[w] = (in[w] ^ ks[4 * q + w]) & range_mask(0, (int)nb, w);
         }
+        if (SEAL) poly_block(P, c);
+        else poly_block(P, in);
+        if (j < 2) {
+#pragma unroll
+          for (int w = 0; w < 4; w++) first32[4 * j + w] = SEAL ? c[w] : in[w];
+        }
+        // output block D0 + 16j: bytes [0, oa) from the previous chunk's
+        // tail, [oa, 16) from this chunk's head
+        uint32_t blk[4];
+        funnel(prev_c, c, 16 - oa, blk);
+        const uint32_t lo = j == 0 ? oa : 0u;
+        const uint32_t hi = oa + len - 16 * j < 16 ? oa + len - 16 * j : 16u;
+#if SQ_QABLATE  // timing-only: keep the values, store only the last
+        if (j + 1 == nchunk) store_partial(D0 + 16ull * j, blk, lo, hi);
+#else
+        if (lo == 0 && hi == 16) gst<u32x4>(D0 + 16ull * j, u32x4{blk[0], blk[1], blk[2], blk[3]});
+        else store_partial(D0 + 16ull * j, blk, lo, hi);
+#endif
+#pragma unroll
+        for (int w = 0; w < 4; w++) prev_c[w] = c[w];
       }
     }
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+#pragma unroll
+      for (int w = 0; w < 4; w++) cur[q][w] = nxt[q][w];
+  }
+  // the last chunk's tail spills into one more output block
+  if (oa + len > 16 * nchunk) {
+    const uint32_t zero[4] = {0u, 0u, 0u, 0u};
+    uint32_t blk[4];
+    funnel(prev_c, zero, 16 - oa, blk);
+    store_partial(D0 + 16ull * nchunk, blk, 0, oa + len - 16 * nchunk);
   }
 }
 

@@ -71,6 +71,8 @@ def lib() -> ctypes.CDLL:
         L.or_quic_open.argtypes = [vp, vp, vp, ctypes.c_uint64, vp, sz, sz, vp,
                                    ctypes.POINTER(ctypes.c_uint64)]
         L.or_quic_open.restype = ctypes.c_long
+        L.or_quic_seal_batch.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, ctypes.c_uint32, vp, vp,
+                                         ctypes.c_int]
         L.or_batch_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(OrPsks),
                                    ctypes.POINTER(OrBatch), ctypes.c_int]
         L.or_fnv64.argtypes = [vp, sz, ctypes.c_uint64]
