@@ -104,6 +104,54 @@ extern "C" int probe_pers_run(int mode, int u, int dummy, int nb, const void *sr
   return -2;
 }
 
+// MODE 5: as MODE 0 (one region per wave, U KiB per step), but the loads are
+// LDS-DMA (global_load_lds_dwordx4: no VGPR destination) into a per-wave
+// LDS buffer, then ds_read_b128 + XOR + nt store.  AUX: load cache policy.
+template <int U, int AUX>
+__global__ __launch_bounds__(256) void probe_glds(const uint8_t *src, uint8_t *dst, uint64_t n,
+                                                  uint64_t R) {
+  __shared__ u32x4 buf[4][U][64];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x / 64;
+  const u32x4 k = {0x11111111u, 0x22222222u, 0x33333333u, 0x44444444u};
+  const uint64_t b = ((uint64_t)blockIdx.x * 4 + w) * R;
+  uint64_t e = b + R;
+  e = e < n ? e : n;
+  if (b >= e) return;
+  for (uint64_t c0 = b; c0 < e; c0 += 64 * U) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      uint64_t c = c0 + 64 * u + lane;
+      c = c < e ? c : e - 1;
+      __builtin_amdgcn_global_load_lds((const void *)(src + 16 * c + 8),
+                                       (__attribute__((address_space(3))) void *)&buf[w][u][0],
+                                       16, 0, AUX);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t c = c0 + 64 * u + lane;
+      const u32x4 v = buf[w][u][lane];
+      if (c < e) __builtin_nontemporal_store(v ^ k, (G u32x4 *)(dst + 16 * c));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
+extern "C" int probe_glds_run(int u, int aux, const void *src, void *dst, uint64_t bytes,
+                              uint64_t region_bytes, void *stream) {
+  const uint64_t n = bytes / 16, R = region_bytes / 16;
+  const uint64_t g = ((n + R - 1) / R + 3) / 4;
+  hipStream_t s = (hipStream_t)stream;
+#define GC(UU, AA)                                                                          \
+  if (u == UU && aux == AA) {                                                              \
+    hipLaunchKernelGGL((probe_glds<UU, AA>), dim3(g), dim3(256), 0, s, (const uint8_t *)src, \
+                       (uint8_t *)dst, n, R);                                              \
+    return hipGetLastError() == hipSuccess ? 0 : -1;                                       \
+  }
+  GC(4, 0) GC(4, 2) GC(8, 0) GC(8, 2) GC(6, 2)
+  return -2;
+}
+
 template <int MODE, int U, int BS>
 static int go(const void *s, void *d, uint64_t n, uint64_t R, hipStream_t st) {
   constexpr int W = BS / 64;
