@@ -34,6 +34,10 @@ namespace sq {
 #define SQ_QABLATE 0  // timing builds only (never the shipped .so)
 #endif
 constexpr uint32_t kQBlock = 256;
+constexpr uint32_t kQWaves = kQBlock / kWave;
+constexpr uint32_t kQPpw = 16;          // packets per wave
+constexpr uint32_t kQCoopMax = 2048;    // payloads up to this size take the cooperative pass
+constexpr uint32_t kQMaxBlk = kQPpw * (kQCoopMax / 64);
 constexpr uint32_t kQMaxPacket = 1u << 20;
 constexpr uint32_t kQEKey = 0xFFFFFFFFu, kQEShort = 0xFFFFFFFEu, kQEAuth = 0xFFFFFFFDu;
 
@@ -60,13 +64,9 @@ __device__ __forceinline__ void poly_init(Poly &P, const uint32_t (&otk)[16]) {
 
 __device__ __forceinline__ uint64_t mul(uint32_t a, uint32_t b) { return (uint64_t)a * b; }
 
-// h = (h + m + 2^128) * r mod 2^130 - 5, one full 16-byte block
-__device__ __forceinline__ void poly_block(Poly &P, const uint32_t (&m)[4]) {
-  const uint32_t h0 = P.h0 + (m[0] & 0x3ffffffu);
-  const uint32_t h1 = P.h1 + (__builtin_amdgcn_alignbit(m[1], m[0], 26) & 0x3ffffffu);
-  const uint32_t h2 = P.h2 + (__builtin_amdgcn_alignbit(m[2], m[1], 20) & 0x3ffffffu);
-  const uint32_t h3 = P.h3 + (__builtin_amdgcn_alignbit(m[3], m[2], 14) & 0x3ffffffu);
-  const uint32_t h4 = P.h4 + ((m[3] >> 8) | (1u << 24));
+// h = h * r mod 2^130 - 5 (partially reduced limbs)
+__device__ __forceinline__ void poly_mul(Poly &P) {
+  const uint32_t h0 = P.h0, h1 = P.h1, h2 = P.h2, h3 = P.h3, h4 = P.h4;
   const uint64_t d0 = mul(h0, P.r0) + mul(h1, P.s4) + mul(h2, P.s3) + mul(h3, P.s2) + mul(h4, P.s1);
   uint64_t d1 = mul(h0, P.r1) + mul(h1, P.r0) + mul(h2, P.s4) + mul(h3, P.s3) + mul(h4, P.s2);
   uint64_t d2 = mul(h0, P.r2) + mul(h1, P.r1) + mul(h2, P.r0) + mul(h3, P.s4) + mul(h4, P.s3);
@@ -82,6 +82,22 @@ __device__ __forceinline__ void poly_block(Poly &P, const uint32_t (&m)[4]) {
   c = P.h0 >> 26;
   P.h0 &= 0x3ffffffu;
   P.h1 += c;
+}
+
+// h = (h + m + 2^128) * r mod 2^130 - 5, one full 16-byte block
+__device__ __forceinline__ void poly_block(Poly &P, const uint32_t (&m)[4]) {
+  P.h0 += m[0] & 0x3ffffffu;
+  P.h1 += __builtin_amdgcn_alignbit(m[1], m[0], 26) & 0x3ffffffu;
+  P.h2 += __builtin_amdgcn_alignbit(m[2], m[1], 20) & 0x3ffffffu;
+  P.h3 += __builtin_amdgcn_alignbit(m[3], m[2], 14) & 0x3ffffffu;
+  P.h4 += (m[3] >> 8) | (1u << 24);
+  poly_mul(P);
+}
+
+// multiplier := h of X (a power of r), with its 5x terms
+__device__ __forceinline__ void poly_set_r(Poly &P, const Poly &X) {
+  P.r0 = X.h0; P.r1 = X.h1; P.r2 = X.h2; P.r3 = X.h3; P.r4 = X.h4;
+  P.s1 = P.r1 * 5; P.s2 = P.r2 * 5; P.s3 = P.r3 * 5; P.s4 = P.r4 * 5;
 }
 
 // tag = (h mod p) + s mod 2^128, s = otk[16..32)
@@ -287,42 +303,284 @@ __device__ __forceinline__ bool pick_key(const QParams &Q, uint32_t p, const Qui
   return true;
 }
 
-template <bool MULTI>
-__global__ __launch_bounds__(kQBlock) void quic_seal_kernel(const QParams Q) {
-  const uint64_t p64 = (uint64_t)blockIdx.x * kQBlock + threadIdx.x;
-  if (p64 >= Q.n) return;
+// Per-packet record in LDS for the cooperative payload pass.
+struct alignas(16) QRec {
+  uint64_t src, dst;      // payload start in the input / output
+  uint32_t pl, start;     // payload bytes; first flat keystream block
+  uint32_t kid, pad0;
+  uint32_t nonce[3], pad1;
+  uint32_t r[5], s[4], pad2[3];
+  uint32_t ct32[8];       // ciphertext bytes 0..31 (the header-protection sample)
+};
+
+// Packet owning flat block c (>= b0) of the window [b0, b0 + 64): the last
+// lane l with start[l] <= c (starts are sorted over the lanes).
+__device__ __forceinline__ uint32_t q_locate(uint32_t start, uint32_t b0, uint32_t c) {
+  int pp = __popcll(__ballot(start <= b0)) - 1;
+  uint64_t M = __ballot(start > b0 && start < b0 + kWave);
+  while (M) {
+    const int l = __ffsll((unsigned long long)M) - 1;
+    M &= M - 1;
+    pp += c >= (uint32_t)__builtin_amdgcn_readlane(start, l) ? 1 : 0;
+  }
+  return pp < 0 ? 0u : (uint32_t)pp;
+}
+
+// One 64-byte keystream block of one packet (cooperative pass, any lane):
+// XOR up to 64 payload bytes, Horner their <= 4 MAC blocks from h = 0 with
+// the packet's r, realign into aligned 16-byte output stores.
+template <bool OPEN>
+__device__ __forceinline__ void coop_block(const QuicKeyDev &K, QRec &R, uint32_t b,
+                                           uint32_t (&contrib)[5]) {
+  uint32_t ks[16];
+  chacha20_block(K.key, 1 + b, R.nonce, ks);
+  const uint32_t off0 = 64 * b, nv = R.pl - off0 < 64 ? R.pl - off0 : 64;
+  // input: the aligned blocks covering [S, S + 64), clamped to valid ones
+  const uint64_t S = R.src + off0, last = (R.src + R.pl - 1) & ~15ull;
+  const uint32_t ib = (uint32_t)(S & 15);
+  uint32_t blk[5][4];
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    const uint64_t A = S - ib + 16ull * i;
+    const u32x4 x = gld<u32x4>(A < last ? A : last);
+    const bool ok = A <= last;
+    blk[i][0] = ok ? x.x : 0u; blk[i][1] = ok ? x.y : 0u;
+    blk[i][2] = ok ? x.z : 0u; blk[i][3] = ok ? x.w : 0u;
+  }
+  Poly L;
+  L.r0 = R.r[0]; L.r1 = R.r[1]; L.r2 = R.r[2]; L.r3 = R.r[3]; L.r4 = R.r[4];
+  L.s1 = R.s[0]; L.s2 = R.s[1]; L.s3 = R.s[2]; L.s4 = R.s[3];
+  L.h0 = L.h1 = L.h2 = L.h3 = L.h4 = 0;
+  uint32_t o[4][4];
+#pragma unroll
+  for (uint32_t q = 0; q < 4; q++) {
+    const int nb = (int)nv - 16 * (int)q;  // valid bytes of this chunk (may be <= 0)
+    uint32_t in[4];
+    funnel(blk[q], blk[q + 1], ib, in);
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+      in[w] &= range_mask(0, nb, w);
+      o[q][w] = (in[w] ^ ks[4 * q + w]) & range_mask(0, nb, w);
+    }
+    if (nb > 0) {
+      if (OPEN) poly_block(L, in);
+      else poly_block(L, o[q]);
+    }
+    if (!OPEN && b == 0 && q < 2) {
+#pragma unroll
+      for (int w = 0; w < 4; w++) R.ct32[4 * q + w] = o[q][w];
+    }
+  }
+  contrib[0] = L.h0; contrib[1] = L.h1; contrib[2] = L.h2; contrib[3] = L.h3; contrib[4] = L.h4;
+  // output: realign the 64 bytes at D into aligned 16-byte blocks; the first
+  // and last are shared with the neighbouring blocks' lanes (partial stores)
+  const uint64_t D = R.dst + off0;
+  const uint32_t oa = (uint32_t)(D & 15);
+  const uint32_t zero[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (uint32_t j = 0; j < 5; j++) {
+    uint32_t ob[4];
+    funnel(j == 0 ? zero : o[j - 1], j == 4 ? zero : o[j], 16 - oa, ob);
+    const uint32_t lo = j == 0 ? oa : 0u;
+    const int hi_i = (int)(oa + nv) - 16 * (int)j;
+    const uint32_t hi = hi_i < 16 ? (uint32_t)(hi_i > 0 ? hi_i : 0) : 16u;
+    if (hi > lo) {
+      if (lo == 0 && hi == 16) gst<u32x4>(D - oa + 16ull * j, u32x4{ob[0], ob[1], ob[2], ob[3]});
+      else store_partial(D - oa + 16ull * j, ob, lo, hi);
+    }
+  }
+}
+
+// Seal (OPEN = false) or open (OPEN = true) a ragged batch: PPW = 16 packets
+// per wave.
+//   1. owner lane (one per packet): descriptor, header protection removal
+//      and packet number (open), nonce, Poly1305 key, MAC over the header;
+//   2. all 64 lanes: the packets' 64-byte keystream blocks as one flat
+//      space (prefix sum), one block per lane per step -- consecutive lanes
+//      read and write consecutive 64 bytes of a packet (coalesced); each
+//      lane leaves its block's partial MAC P_b in LDS;
+//   3. owner lane: h = h * r^k_b + P_b over the blocks (Horner in 4-block
+//      strides: 1 multiply per 64 bytes), the lengths block, the tag, and
+//      (seal) header protection from the sample kept in LDS.
+// Payloads above kQCoopMax bytes are walked by their owner lane in phase 3
+// (the sequential payload_pass), so any length works.
+template <bool OPEN, bool MULTI>
+__global__ __launch_bounds__(kQBlock) void quic_kernel(const QParams Q) {
+  __shared__ QRec recs[kQWaves][kQPpw];
+  __shared__ uint32_t parts[kQWaves][kQMaxBlk][5];
+  const uint32_t lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+  const uint64_t p64 = ((uint64_t)blockIdx.x * kQWaves + wv) * kQPpw + lane;
+  const bool owner = lane < kQPpw && p64 < Q.n;
   const uint32_t p = (uint32_t)p64;
-  const QuicKeyDev *K;
-  if (!pick_key<MULTI>(Q, p, K)) {
-    Q.out_len[p] = kQEKey;
-    return;
-  }
-  const uint64_t src = (uint64_t)Q.in + Q.in_off[p], dst = (uint64_t)Q.out + Q.out_off[p];
-  const uint32_t len = Q.in_len[p], pno = Q.pn_offset[p];
-  const uint32_t first = len ? gld<uint8_t>(src) : 0u;
-  const uint32_t pn_len = (first & 3) + 1, hdr = pno + pn_len;
-  if (len == 0 || len > kQMaxPacket || hdr > len || pno + 4 > len) {
-    Q.out_len[p] = kQEShort;
-    return;
-  }
-  const uint32_t pl = len - hdr;
-  uint32_t nonce[3], otk[16];
-  quic_nonce(*K, Q.pn[p], nonce);
-  chacha20_block(K->key, 0, nonce, otk);
+
+  // ---- 1. owner lanes
+  bool live = owner;
+  uint32_t status = 0, len = 0, pno = 0, first = 0, pn_len = 0, hdr = 0, pl = 0;
+  uint64_t src = 0, dst = 0;
+  const QuicKeyDev *K = &Q.key0;
+  uint32_t nonce[3] = {0u, 0u, 0u}, otk[16], rtag[4] = {0u, 0u, 0u, 0u};
   Poly P;
-  poly_init(P, otk);
-  // AAD = the unprotected header (copied to the output unchanged for now)
-  for (uint32_t q = 0; q < hdr; q += 16) {
-    uint32_t w[4];
-    load16(src + q, src + hdr, w);
-    poly_block(P, w);
-    if (dst != src) store16(dst + q, w, hdr - q < 16 ? hdr - q : 16);
+  P.h0 = P.h1 = P.h2 = P.h3 = P.h4 = 0;
+  P.r0 = P.r1 = P.r2 = P.r3 = P.r4 = P.s1 = P.s2 = P.s3 = P.s4 = 0;
+#pragma unroll
+  for (int i = 0; i < 16; i++) otk[i] = 0u;
+  if (live && !pick_key<MULTI>(Q, p, K)) {
+    status = kQEKey;
+    live = false;
+  }
+  if (live) {
+    src = (uint64_t)Q.in + Q.in_off[p];
+    dst = (uint64_t)Q.out + Q.out_off[p];
+    len = Q.in_len[p];
+    pno = Q.pn_offset[p];
+    uint64_t pn = Q.pn[p];
+    uint32_t pnb[4] = {0u, 0u, 0u, 0u};
+    if (!OPEN) {
+      first = len ? gld<uint8_t>(src) : 0u;
+      pn_len = (first & 3) + 1;
+      hdr = pno + pn_len;
+      if (len == 0 || len > kQMaxPacket || hdr > len || pno + 4 > len) live = false;
+      else pl = len - hdr;
+    } else if (len < 16 || len > kQMaxPacket || pno + 4 + 16 > len) {
+      live = false;
+    } else {
+      uint32_t sample[4], m0, m1;
+      load16(src + pno + 4, src + len, sample);
+      load16(src + len - 16, src + len, rtag);  // before any in-place write
+      hp_mask(*K, sample, m0, m1);
+      const uint32_t pfirst = gld<uint8_t>(src);
+      first = pfirst ^ (m0 & ((pfirst & 0x80) ? 0x0Fu : 0x1Fu));
+      pn_len = (first & 3) + 1;
+      hdr = pno + pn_len;
+      if (hdr > len - 16) {
+        live = false;
+      } else {
+        uint64_t trunc = 0;
+        for (uint32_t i = 0; i < pn_len; i++) {
+          pnb[i] = gld<uint8_t>(src + pno + i) ^ mask_byte(m0, m1, 1 + i);
+          trunc = (trunc << 8) | pnb[i];
+        }
+        pn = decode_pn(pn, trunc, 8 * pn_len);
+        if (Q.pn_out) Q.pn_out[p] = pn;
+        pl = len - 16 - hdr;
+      }
+    }
+    if (!live) status = kQEShort;
+    if (live) {
+      quic_nonce(*K, pn, nonce);
+      chacha20_block(K->key, 0, nonce, otk);
+      poly_init(P, otk);
+      // AAD = the unprotected header; seal copies it unchanged (protection
+      // is applied in phase 3), open writes the unprotected header
+      for (uint32_t q = 0; q < hdr; q += 16) {
+        uint32_t w[4];
+        load16(src + q, src + hdr, w);
+        if (OPEN) {
+          if (q == 0) set_byte(w, 0, first);
+          for (uint32_t i = 0; i < pn_len; i++) {
+            const uint32_t pos = pno + i;
+            if (pos >= q && pos < q + 16) set_byte(w, pos - q, pnb[i]);
+          }
+        }
+        poly_block(P, w);
+        if (OPEN || dst != src) store16(dst + q, w, hdr - q < 16 ? hdr - q : 16);
+      }
+    }
+  }
+  const bool coop = live && pl <= kQCoopMax;
+  const uint32_t nblk = coop ? (pl + 63) / 64 : 0u;
+  uint32_t incl = nblk;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d, kWave);
+    if (lane >= (uint32_t)d) incl += y;
+  }
+  const uint32_t start = incl - nblk, T = __shfl(incl, kWave - 1, kWave);
+  if (lane < kQPpw) {
+    QRec &R = recs[wv][lane];
+    R.src = src + hdr;
+    R.dst = dst + hdr;
+    R.pl = pl;
+    R.start = start;
+    R.kid = MULTI && live ? (uint32_t)(K - Q.keys) : 0u;
+#pragma unroll
+    for (int i = 0; i < 3; i++) R.nonce[i] = nonce[i];
+    R.r[0] = P.r0; R.r[1] = P.r1; R.r[2] = P.r2; R.r[3] = P.r3; R.r[4] = P.r4;
+    R.s[0] = P.s1; R.s[1] = P.s2; R.s[2] = P.s3; R.s[3] = P.s4;
+#pragma unroll
+    for (int i = 0; i < 8; i++) R.ct32[i] = 0u;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+  // ---- 2. cooperative payload pass over the flat block space
+  for (uint32_t base = 0; base < T; base += kWave) {
+    const uint32_t f = base + lane;
+    const uint32_t pp = q_locate(start, base, f < T ? f : T - 1);
+    if (f < T) {
+      QRec &R = recs[wv][pp];
+      const QuicKeyDev &KB = MULTI ? Q.keys[R.kid] : Q.key0;
+      uint32_t c5[5];
+      coop_block<OPEN>(KB, R, f - R.start, c5);
+#pragma unroll
+      for (int i = 0; i < 5; i++) parts[wv][f][i] = c5[i];
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+  // ---- 3. owner lanes: combine, tag, header protection
+  if (!owner) return;
+  if (!live) {
+    Q.out_len[p] = status;
+    return;
   }
   uint32_t ct32[8];
-  payload_pass<true>(*K, nonce, src + hdr, dst + hdr, pl, P, ct32);
+  if (coop) {
+    // r^1..r^4 as multipliers
+    Poly X = P, R1, R2, R3, R4;
+    X.h0 = P.r0; X.h1 = P.r1; X.h2 = P.r2; X.h3 = P.r3; X.h4 = P.r4;
+    poly_set_r(R1, X);
+    poly_mul(X);
+    poly_set_r(R2, X);
+    poly_mul(X);
+    poly_set_r(R3, X);
+    poly_mul(X);
+    poly_set_r(R4, X);
+    const uint32_t klast = ((pl - 64 * (nblk ? nblk - 1 : 0)) + 15) / 16;  // 1..4 chunks
+    // the last block's multiplier r^klast, selected limb by limb
+    const uint32_t L0 = klast == 4 ? R4.r0 : klast == 3 ? R3.r0 : klast == 2 ? R2.r0 : R1.r0;
+    const uint32_t L1 = klast == 4 ? R4.r1 : klast == 3 ? R3.r1 : klast == 2 ? R2.r1 : R1.r1;
+    const uint32_t L2 = klast == 4 ? R4.r2 : klast == 3 ? R3.r2 : klast == 2 ? R2.r2 : R1.r2;
+    const uint32_t L3 = klast == 4 ? R4.r3 : klast == 3 ? R3.r3 : klast == 2 ? R2.r3 : R1.r3;
+    const uint32_t L4 = klast == 4 ? R4.r4 : klast == 3 ? R3.r4 : klast == 2 ? R2.r4 : R1.r4;
+    for (uint32_t b = 0; b < nblk; b++) {
+      const bool lastb = b + 1 == nblk;
+      P.r0 = lastb ? L0 : R4.r0;
+      P.r1 = lastb ? L1 : R4.r1;
+      P.r2 = lastb ? L2 : R4.r2;
+      P.r3 = lastb ? L3 : R4.r3;
+      P.r4 = lastb ? L4 : R4.r4;
+      P.s1 = P.r1 * 5; P.s2 = P.r2 * 5; P.s3 = P.r3 * 5; P.s4 = P.r4 * 5;
+      poly_mul(P);
+      const uint32_t *c5 = parts[wv][start + b];
+      P.h0 += c5[0]; P.h1 += c5[1]; P.h2 += c5[2]; P.h3 += c5[3]; P.h4 += c5[4];
+    }
+    // restore r for the lengths block
+    P.r0 = R1.r0; P.r1 = R1.r1; P.r2 = R1.r2; P.r3 = R1.r3; P.r4 = R1.r4;
+    P.s1 = R1.s1; P.s2 = R1.s2; P.s3 = R1.s3; P.s4 = R1.s4;
+#pragma unroll
+    for (int i = 0; i < 8; i++) ct32[i] = recs[wv][lane].ct32[i];
+  } else {
+    payload_pass<!OPEN>(*K, nonce, src + hdr, dst + hdr, pl, P, ct32);
+  }
   poly_lengths(P, hdr, pl);
   uint32_t tag[4];
   poly_finish(P, otk, tag);
+  if (OPEN) {
+    const bool ok = ((tag[0] ^ rtag[0]) | (tag[1] ^ rtag[1]) | (tag[2] ^ rtag[2]) |
+                     (tag[3] ^ rtag[3])) == 0;
+    Q.out_len[p] = ok ? len - 16 : kQEAuth;
+    return;
+  }
   store16(dst + len, tag, 16);
   // header protection: sample = (ciphertext || tag)[4 - pn_len ..][0..16)
   const uint32_t so = 4 - pn_len;
@@ -336,82 +594,18 @@ __global__ __launch_bounds__(kQBlock) void quic_seal_kernel(const QParams Q) {
     for (int j = 0; j < 4; j++) sample[j] = 0u;
     for (uint32_t i = 0; i < 16; i++) {
       const uint32_t k = so + i;
-      const uint32_t b = k < pl ? byte32(ct32, k) : byte32(t8, k - pl);
-      sample[i >> 2] |= b << (8 * (i & 3));
+      const uint32_t bb = k < pl ? byte32(ct32, k) : byte32(t8, k - pl);
+      sample[i >> 2] |= bb << (8 * (i & 3));
     }
   }
   uint32_t m0, m1;
   hp_mask(*K, sample, m0, m1);
   gst<uint8_t>(dst, (uint8_t)(first ^ (m0 & ((first & 0x80) ? 0x0Fu : 0x1Fu))));
   for (uint32_t i = 0; i < pn_len; i++) {
-    const uint32_t b = gld<uint8_t>(src + pno + i);
-    gst<uint8_t>(dst + pno + i, (uint8_t)(b ^ mask_byte(m0, m1, 1 + i)));
+    const uint32_t bb = gld<uint8_t>(src + pno + i);
+    gst<uint8_t>(dst + pno + i, (uint8_t)(bb ^ mask_byte(m0, m1, 1 + i)));
   }
   Q.out_len[p] = len + 16;
-}
-
-template <bool MULTI>
-__global__ __launch_bounds__(kQBlock) void quic_open_kernel(const QParams Q) {
-  const uint64_t p64 = (uint64_t)blockIdx.x * kQBlock + threadIdx.x;
-  if (p64 >= Q.n) return;
-  const uint32_t p = (uint32_t)p64;
-  const QuicKeyDev *K;
-  if (!pick_key<MULTI>(Q, p, K)) {
-    Q.out_len[p] = kQEKey;
-    return;
-  }
-  const uint64_t src = (uint64_t)Q.in + Q.in_off[p], dst = (uint64_t)Q.out + Q.out_off[p];
-  const uint32_t len = Q.in_len[p], pno = Q.pn_offset[p];
-  if (len < 16 || len > kQMaxPacket || pno + 4 + 16 > len) {
-    Q.out_len[p] = kQEShort;
-    return;
-  }
-  uint32_t sample[4], rtag[4];
-  load16(src + pno + 4, src + len, sample);
-  load16(src + len - 16, src + len, rtag);  // before any in-place write
-  uint32_t m0, m1;
-  hp_mask(*K, sample, m0, m1);
-  const uint32_t pfirst = gld<uint8_t>(src);
-  const uint32_t first = pfirst ^ (m0 & ((pfirst & 0x80) ? 0x0Fu : 0x1Fu));
-  const uint32_t pn_len = (first & 3) + 1, hdr = pno + pn_len;
-  if (hdr > len - 16) {
-    Q.out_len[p] = kQEShort;
-    return;
-  }
-  uint64_t trunc = 0;
-  uint32_t pnb[4] = {0u, 0u, 0u, 0u};
-  for (uint32_t i = 0; i < pn_len; i++) {
-    pnb[i] = gld<uint8_t>(src + pno + i) ^ mask_byte(m0, m1, 1 + i);
-    trunc = (trunc << 8) | pnb[i];
-  }
-  const uint64_t pn = decode_pn(Q.pn[p], trunc, 8 * pn_len);
-  if (Q.pn_out) Q.pn_out[p] = pn;
-  uint32_t nonce[3], otk[16];
-  quic_nonce(*K, pn, nonce);
-  chacha20_block(K->key, 0, nonce, otk);
-  Poly P;
-  poly_init(P, otk);
-  // AAD = the unprotected header: protected bytes patched, then written out
-  for (uint32_t q = 0; q < hdr; q += 16) {
-    uint32_t w[4];
-    load16(src + q, src + hdr, w);
-    if (q == 0) set_byte(w, 0, first);
-    for (uint32_t i = 0; i < pn_len; i++) {
-      const uint32_t pos = pno + i;
-      if (pos >= q && pos < q + 16) set_byte(w, pos - q, pnb[i]);
-    }
-    poly_block(P, w);
-    store16(dst + q, w, hdr - q < 16 ? hdr - q : 16);
-  }
-  const uint32_t cl = len - 16 - hdr;
-  uint32_t ct32[8];
-  payload_pass<false>(*K, nonce, src + hdr, dst + hdr, cl, P, ct32);
-  poly_lengths(P, hdr, cl);
-  uint32_t tag[4];
-  poly_finish(P, otk, tag);
-  const bool ok = ((tag[0] ^ rtag[0]) | (tag[1] ^ rtag[1]) | (tag[2] ^ rtag[2]) |
-                   (tag[3] ^ rtag[3])) == 0;
-  Q.out_len[p] = ok ? len - 16 : kQEAuth;
 }
 
 }  // namespace sq
@@ -419,15 +613,16 @@ __global__ __launch_bounds__(kQBlock) void quic_open_kernel(const QParams Q) {
 extern "C" int sq_launch_quic(int open, const sq::QParams *qp, void *stream) {
   using namespace sq;
   if (qp->n == 0) return 0;
-  const dim3 grid((qp->n + kQBlock - 1) / kQBlock);
+  const uint64_t waves = ((uint64_t)qp->n + kQPpw - 1) / kQPpw;
+  const dim3 grid((uint32_t)((waves + kQWaves - 1) / kQWaves));
   hipStream_t s = (hipStream_t)stream;
   const bool multi = qp->key_id != nullptr;
   if (open) {
-    if (multi) hipLaunchKernelGGL(quic_open_kernel<true>, grid, dim3(kQBlock), 0, s, *qp);
-    else hipLaunchKernelGGL(quic_open_kernel<false>, grid, dim3(kQBlock), 0, s, *qp);
+    if (multi) hipLaunchKernelGGL((quic_kernel<true, true>), grid, dim3(kQBlock), 0, s, *qp);
+    else hipLaunchKernelGGL((quic_kernel<true, false>), grid, dim3(kQBlock), 0, s, *qp);
   } else {
-    if (multi) hipLaunchKernelGGL(quic_seal_kernel<true>, grid, dim3(kQBlock), 0, s, *qp);
-    else hipLaunchKernelGGL(quic_seal_kernel<false>, grid, dim3(kQBlock), 0, s, *qp);
+    if (multi) hipLaunchKernelGGL((quic_kernel<false, true>), grid, dim3(kQBlock), 0, s, *qp);
+    else hipLaunchKernelGGL((quic_kernel<false, false>), grid, dim3(kQBlock), 0, s, *qp);
   }
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
