@@ -170,3 +170,30 @@ def test_open_rejects_tampering_and_bad_input(ctx):
     _, _, ol_, _, _ = run(ctx, [QuicKey.of(*kb)], True, [b"\x40\x01\x02", b"\x43" + bytes(40)],
                           [1, 1], [1, 2], key_ids=[0, 5])
     assert ol_[0] == sqobfs.QUIC_ESHORT and ol_[1] == sqobfs.QUIC_EKEY
+
+
+def test_long_payloads_owner_path(ctx):
+    """Payloads either side of the cooperative limit (2,048 B), walked by the
+    owner lane above it, mixed in one batch with short packets."""
+    rng = np.random.Generator(np.random.PCG64(991))
+    kb = tuple(rng.integers(0, 256, m, dtype=np.uint8).tobytes() for m in (32, 12, 32))
+    pkts, pnos, pns = [], [], []
+    for plen in [2030, 2047, 2048, 2049, 2050, 2064, 3000, 9000, 65, 2, 4000, 1350]:
+        pn_len = 2
+        pkt = bytes([0x41]) + bytes(8) + (7).to_bytes(pn_len, "big") + \
+            rng.integers(0, 256, plen, dtype=np.uint8).tobytes()
+        pkts.append(pkt)
+        pnos.append(9)
+        pns.append(7)
+    out, oo, ol_, _, _ = run(ctx, [QuicKey.of(*kb)], True, pkts, pnos, pns)
+    prot = []
+    for i, p in enumerate(pkts):
+        want, r = ol.quic_seal(*kb, pns[i], p, pnos[i])
+        assert ol_[i] == r == len(p) + 16
+        got = out[int(oo[i]):int(oo[i]) + r].tobytes()
+        assert got == want, (i, len(p))
+        prot.append(got)
+    out2, oo2, ol2, pno2, _ = run(ctx, [QuicKey.of(*kb)], False, prot, pnos, [6] * len(prot))
+    for i, p in enumerate(pkts):
+        assert ol2[i] == len(p) and pno2[i] == 7
+        assert out2[int(oo2[i]):int(oo2[i]) + ol2[i]].tobytes() == p
