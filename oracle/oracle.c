@@ -348,35 +348,224 @@ void or_aead_seal(const uint8_t key[32], const uint8_t nonce[12], const uint8_t 
   free(mac);
 }
 
+/* ---- AES-128 (FIPS-197) and GCM (NIST SP 800-38D), for the
+ * TLS_AES_128_GCM_SHA256 QUIC suite (RFC 9001 5.3, 5.4.3).  Byte-oriented
+ * restatement: the S-box is computed from its definition (multiplicative
+ * inverse in GF(2^8) mod x^8+x^4+x^3+x+1, then the affine map), GHASH
+ * multiplies bit by bit (SP 800-38D Algorithm 1). */
+static uint8_t aes_sbox[256];
+static int aes_sbox_ready;
+
+static uint8_t gf8_mul(uint8_t a, uint8_t b) {
+  uint8_t r = 0;
+  while (b) {
+    if (b & 1) r ^= a;
+    a = (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0));
+    b >>= 1;
+  }
+  return r;
+}
+
+static void aes_init_sbox(void) {
+  if (aes_sbox_ready) return;
+  for (int x = 0; x < 256; x++) {
+    uint8_t inv = 0;  /* x^254 = x^-1, and 0 -> 0 */
+    if (x) {
+      uint8_t acc = 1, base = (uint8_t)x;
+      for (int e = 254; e; e >>= 1) {
+        if (e & 1) acc = gf8_mul(acc, base);
+        base = gf8_mul(base, base);
+      }
+      inv = acc;
+    }
+    uint8_t b = inv, y = 0x63;
+    for (int k = 0; k < 5; k++) y ^= (uint8_t)((b << k) | (b >> ((8 - k) & 7)));
+    aes_sbox[x] = y;
+  }
+  aes_sbox_ready = 1;
+}
+
+uint8_t or_aes_sbox(uint8_t x) {
+  aes_init_sbox();
+  return aes_sbox[x];
+}
+
+/* FIPS-197 5.2: 11 round keys of 16 bytes */
+void or_aes128_expand(const uint8_t key[16], uint8_t rk[176]) {
+  aes_init_sbox();
+  memcpy(rk, key, 16);
+  uint8_t rcon = 1;
+  for (int i = 4; i < 44; i++) {
+    uint8_t t[4];
+    memcpy(t, rk + 4 * (i - 1), 4);
+    if (i % 4 == 0) {
+      const uint8_t t0 = t[0];
+      t[0] = (uint8_t)(aes_sbox[t[1]] ^ rcon);
+      t[1] = aes_sbox[t[2]];
+      t[2] = aes_sbox[t[3]];
+      t[3] = aes_sbox[t0];
+      rcon = gf8_mul(rcon, 2);
+    }
+    for (int k = 0; k < 4; k++) rk[4 * i + k] = rk[4 * (i - 4) + k] ^ t[k];
+  }
+}
+
+/* FIPS-197 5.1: state byte r + 4c = input byte r + 4c */
+void or_aes128_encrypt(const uint8_t rk[176], const uint8_t in[16], uint8_t out[16]) {
+  aes_init_sbox();
+  uint8_t s[16];
+  for (int i = 0; i < 16; i++) s[i] = in[i] ^ rk[i];
+  for (int round = 1; round <= 10; round++) {
+    uint8_t t[16];
+    for (int c = 0; c < 4; c++)      /* SubBytes + ShiftRows */
+      for (int r = 0; r < 4; r++) t[r + 4 * c] = aes_sbox[s[r + 4 * ((c + r) & 3)]];
+    if (round < 10) {                /* MixColumns */
+      for (int c = 0; c < 4; c++) {
+        const uint8_t a0 = t[4 * c], a1 = t[4 * c + 1], a2 = t[4 * c + 2], a3 = t[4 * c + 3];
+        s[4 * c] = gf8_mul(a0, 2) ^ gf8_mul(a1, 3) ^ a2 ^ a3;
+        s[4 * c + 1] = a0 ^ gf8_mul(a1, 2) ^ gf8_mul(a2, 3) ^ a3;
+        s[4 * c + 2] = a0 ^ a1 ^ gf8_mul(a2, 2) ^ gf8_mul(a3, 3);
+        s[4 * c + 3] = gf8_mul(a0, 3) ^ a1 ^ a2 ^ gf8_mul(a3, 2);
+      }
+    } else {
+      memcpy(s, t, 16);
+    }
+    for (int i = 0; i < 16; i++) s[i] ^= rk[16 * round + i];
+  }
+  memcpy(out, s, 16);
+}
+
+/* SP 800-38D 6.3, Algorithm 1: X * Y in GF(2^128), bit 0 = MSB of byte 0 */
+void or_gf128_mul(const uint8_t x[16], const uint8_t y[16], uint8_t out[16]) {
+  uint8_t z[16] = {0}, v[16];
+  memcpy(v, y, 16);
+  for (int i = 0; i < 128; i++) {
+    if ((x[i / 8] >> (7 - (i % 8))) & 1)
+      for (int k = 0; k < 16; k++) z[k] ^= v[k];
+    const int lsb = v[15] & 1;
+    for (int k = 15; k > 0; k--) v[k] = (uint8_t)((v[k] >> 1) | (v[k - 1] << 7));
+    v[0] >>= 1;
+    if (lsb) v[0] ^= 0xe1;
+  }
+  memcpy(out, z, 16);
+}
+
+/* GHASH_H over aad (zero-padded) || ct (zero-padded) || be64(bits(aad)) ||
+ * be64(bits(ct)) (SP 800-38D 7.1 step 5) */
+static void gcm_ghash(const uint8_t h[16], const uint8_t *aad, size_t aad_len,
+                      const uint8_t *ct, size_t len, uint8_t x[16]) {
+  memset(x, 0, 16);
+  const uint8_t *parts[2] = {aad, ct};
+  const size_t lens[2] = {aad_len, len};
+  for (int p = 0; p < 2; p++)
+    for (size_t pos = 0; pos < lens[p]; pos += 16) {
+      for (size_t k = 0; k < 16 && pos + k < lens[p]; k++) x[k] ^= parts[p][pos + k];
+      or_gf128_mul(x, h, x);
+    }
+  uint8_t l[16];
+  for (int k = 0; k < 8; k++) {
+    l[7 - k] = (uint8_t)(((uint64_t)aad_len * 8) >> (8 * k));
+    l[15 - k] = (uint8_t)(((uint64_t)len * 8) >> (8 * k));
+  }
+  for (int k = 0; k < 16; k++) x[k] ^= l[k];
+  or_gf128_mul(x, h, x);
+}
+
+/* AES-128-GCM with a 96-bit nonce: J0 = nonce || be32(1), payload counter
+ * blocks from be32(2), tag = E(K, J0) ^ GHASH (SP 800-38D 7.1).  ct may be
+ * pt (in place).  Open: pass the ciphertext as pt with decrypt = 1; the tag
+ * is then computed over the input. */
+void or_gcm_crypt(const uint8_t key[16], const uint8_t nonce[12], const uint8_t *aad,
+                  size_t aad_len, const uint8_t *in, size_t len, uint8_t *out, uint8_t tag[16],
+                  int decrypt) {
+  uint8_t rk[176], h[16] = {0}, j[16], ks[16], x[16];
+  or_aes128_expand(key, rk);
+  or_aes128_encrypt(rk, h, h);
+  memcpy(j, nonce, 12);
+  if (decrypt) gcm_ghash(h, aad, aad_len, in, len, x);
+  for (size_t pos = 0; pos < len; pos += 16) {
+    const uint32_t ctr = 2 + (uint32_t)(pos / 16);
+    j[12] = (uint8_t)(ctr >> 24); j[13] = (uint8_t)(ctr >> 16);
+    j[14] = (uint8_t)(ctr >> 8); j[15] = (uint8_t)ctr;
+    or_aes128_encrypt(rk, j, ks);
+    for (size_t k = 0; k < 16 && pos + k < len; k++) out[pos + k] = in[pos + k] ^ ks[k];
+  }
+  if (!decrypt) gcm_ghash(h, aad, aad_len, out, len, x);
+  j[12] = j[13] = j[14] = 0;
+  j[15] = 1;
+  or_aes128_encrypt(rk, j, ks);
+  for (int k = 0; k < 16; k++) tag[k] = x[k] ^ ks[k];
+}
+
 static void quic_nonce(const uint8_t iv[12], uint64_t pn, uint8_t nonce[12]) {
   memcpy(nonce, iv, 12);  /* RFC 9001 5.3: iv XOR left-padded big-endian pn */
   for (int k = 0; k < 8; k++) nonce[11 - k] ^= (uint8_t)(pn >> (8 * k));
 }
 
 /* RFC 9001 5.4.4: mask = ChaCha20(hp, counter = sample[0..4), nonce =
- * sample[4..16)) applied to 5 zero bytes. */
-static void quic_mask(const uint8_t hp[32], const uint8_t sample[16], uint8_t mask[5]) {
+ * sample[4..16)) applied to 5 zero bytes; 5.4.3: mask = AES-ECB(hp, sample). */
+static void quic_mask(int suite, const uint8_t *hp, const uint8_t sample[16], uint8_t mask[5]) {
   uint8_t blk[64];
-  or_chacha20_block(hp, load32le(sample), sample + 4, blk);
+  if (suite == OR_QUIC_AES128GCM) {
+    uint8_t rk[176];
+    or_aes128_expand(hp, rk);
+    or_aes128_encrypt(rk, sample, blk);
+  } else {
+    or_chacha20_block(hp, load32le(sample), sample + 4, blk);
+  }
   memcpy(mask, blk, 5);
 }
 
-long or_quic_seal(const uint8_t key[32], const uint8_t iv[12], const uint8_t hp[32],
-                  uint64_t pn, const uint8_t *pkt, size_t len, size_t pn_offset, uint8_t *out) {
+/* The payload AEAD of either suite; open (decrypt = 1) MACs the input. */
+static void quic_aead(int suite, const uint8_t *key, const uint8_t nonce[12], const uint8_t *aad,
+                      size_t aad_len, const uint8_t *in, size_t len, uint8_t *out,
+                      uint8_t tag[16], int decrypt) {
+  if (suite == OR_QUIC_AES128GCM) {
+    or_gcm_crypt(key, nonce, aad, aad_len, in, len, out, tag, decrypt);
+    return;
+  }
+  uint8_t otk[64];
+  or_chacha20_block(key, 0, nonce, otk);
+  const size_t pa = (aad_len + 15) / 16 * 16, pc = (len + 15) / 16 * 16;
+  uint8_t *mac = (uint8_t *)calloc(pa + pc + 16, 1);
+  memcpy(mac, aad, aad_len);
+  if (decrypt) memcpy(mac + pa, in, len);
+  for (size_t pos = 0; pos < len; pos += 64) {
+    uint8_t ks[64];
+    or_chacha20_block(key, 1 + (uint32_t)(pos / 64), nonce, ks);
+    for (size_t i = pos; i < len && i < pos + 64; i++) out[i] = in[i] ^ ks[i - pos];
+  }
+  if (!decrypt) memcpy(mac + pa, out, len);
+  for (int k = 0; k < 8; k++) {
+    mac[pa + pc + k] = (uint8_t)((uint64_t)aad_len >> (8 * k));
+    mac[pa + pc + 8 + k] = (uint8_t)((uint64_t)len >> (8 * k));
+  }
+  or_poly1305(otk, mac, pa + pc + 16, tag);
+  free(mac);
+}
+
+long or_quic_seal2(int suite, const uint8_t *key, const uint8_t iv[12], const uint8_t *hp,
+                   uint64_t pn, const uint8_t *pkt, size_t len, size_t pn_offset, uint8_t *out) {
+  if (len == 0) return -1;
   const size_t pn_len = (size_t)(pkt[0] & 3) + 1, hdr = pn_offset + pn_len;
   if (hdr > len || pn_offset + 4 + 16 > len + 16) return -1;
   uint8_t nonce[12];
   quic_nonce(iv, pn, nonce);
   uint8_t *tmp = (uint8_t *)malloc(len + 16);
   memcpy(tmp, pkt, hdr);
-  or_aead_seal(key, nonce, pkt, hdr, pkt + hdr, len - hdr, tmp + hdr, tmp + len);
+  quic_aead(suite, key, nonce, pkt, hdr, pkt + hdr, len - hdr, tmp + hdr, tmp + len, 0);
   uint8_t mask[5];
-  quic_mask(hp, tmp + pn_offset + 4, mask);
+  quic_mask(suite, hp, tmp + pn_offset + 4, mask);
   tmp[0] ^= mask[0] & ((tmp[0] & 0x80) ? 0x0f : 0x1f);
   for (size_t i = 0; i < pn_len; i++) tmp[pn_offset + i] ^= mask[1 + i];
   memcpy(out, tmp, len + 16);
   free(tmp);
   return (long)(len + 16);
+}
+
+long or_quic_seal(const uint8_t key[32], const uint8_t iv[12], const uint8_t hp[32],
+                  uint64_t pn, const uint8_t *pkt, size_t len, size_t pn_offset, uint8_t *out) {
+  return or_quic_seal2(OR_QUIC_CHACHA20, key, iv, hp, pn, pkt, len, pn_offset, out);
 }
 
 /* RFC 9000 Appendix A.3 */
@@ -389,12 +578,12 @@ static uint64_t decode_pn(uint64_t largest, uint64_t truncated, unsigned nbits) 
   return cand;
 }
 
-long or_quic_open(const uint8_t key[32], const uint8_t iv[12], const uint8_t hp[32],
-                  uint64_t largest_pn, const uint8_t *pkt, size_t len, size_t pn_offset,
-                  uint8_t *out, uint64_t *pn_out) {
+long or_quic_open2(int suite, const uint8_t *key, const uint8_t iv[12], const uint8_t *hp,
+                   uint64_t largest_pn, const uint8_t *pkt, size_t len, size_t pn_offset,
+                   uint8_t *out, uint64_t *pn_out) {
   if (len < 16 || pn_offset + 4 + 16 > len) return -1;
   uint8_t mask[5];
-  quic_mask(hp, pkt + pn_offset + 4, mask);
+  quic_mask(suite, hp, pkt + pn_offset + 4, mask);
   uint8_t *tmp = (uint8_t *)malloc(len);
   memcpy(tmp, pkt, len);
   tmp[0] ^= mask[0] & ((tmp[0] & 0x80) ? 0x0f : 0x1f);
@@ -411,34 +600,24 @@ long or_quic_open(const uint8_t key[32], const uint8_t iv[12], const uint8_t hp[
   const uint64_t pn = decode_pn(largest_pn, trunc, (unsigned)(8 * pn_len));
   uint8_t nonce[12], tag[16];
   quic_nonce(iv, pn, nonce);
-  /* decrypt = encrypt with the same keystream; the MAC covers the ciphertext */
   const size_t clen = len - 16 - hdr;
   uint8_t *pt = (uint8_t *)malloc(clen ? clen : 1);
-  uint8_t otk[64];
-  or_chacha20_block(key, 0, nonce, otk);
-  const size_t pa = (hdr + 15) / 16 * 16, pc = (clen + 15) / 16 * 16;
-  uint8_t *mac = (uint8_t *)calloc(pa + pc + 16, 1);
-  memcpy(mac, tmp, hdr);
-  memcpy(mac + pa, tmp + hdr, clen);
-  for (int k = 0; k < 8; k++) {
-    mac[pa + pc + k] = (uint8_t)((uint64_t)hdr >> (8 * k));
-    mac[pa + pc + 8 + k] = (uint8_t)((uint64_t)clen >> (8 * k));
-  }
-  or_poly1305(otk, mac, pa + pc + 16, tag);
-  free(mac);
+  quic_aead(suite, key, nonce, tmp, hdr, tmp + hdr, clen, pt, tag, 1);
   uint8_t diff = 0;
   for (int i = 0; i < 16; i++) diff |= tag[i] ^ tmp[len - 16 + i];
-  for (size_t pos = 0; pos < clen; pos += 64) {
-    uint8_t ks[64];
-    or_chacha20_block(key, 1 + (uint32_t)(pos / 64), nonce, ks);
-    for (size_t i = pos; i < clen && i < pos + 64; i++) pt[i] = tmp[hdr + i] ^ ks[i - pos];
-  }
   memcpy(out, tmp, hdr);
   memcpy(out + hdr, pt, clen);
   free(pt);
   free(tmp);
   if (pn_out) *pn_out = pn;
   return diff ? -2 : (long)(len - 16);
+}
+
+long or_quic_open(const uint8_t key[32], const uint8_t iv[12], const uint8_t hp[32],
+                  uint64_t largest_pn, const uint8_t *pkt, size_t len, size_t pn_offset,
+                  uint8_t *out, uint64_t *pn_out) {
+  return or_quic_open2(OR_QUIC_CHACHA20, key, iv, hp, largest_pn, pkt, len, pn_offset, out,
+                       pn_out);
 }
 
 static void hash_psk_salt(int kind, const uint8_t *psk, size_t psk_len,
@@ -656,6 +835,7 @@ int or_batch_run(int kind, int dir, const or_psks *psks, const or_batch *b,
 /* QUIC seal of a whole batch on nthreads host threads (single key): the
  * CPU timing leg of bench.py --quic. */
 typedef struct {
+  int suite;
   const uint8_t *key, *iv, *hp, *in;
   const uint64_t *in_off, *out_off, *pn;
   const uint32_t *in_len;
@@ -668,23 +848,24 @@ typedef struct {
 static void *quic_shard(void *arg) {
   or_qjob *j = (or_qjob *)arg;
   for (uint32_t i = j->lo; i < j->hi; i++) {
-    const long r = or_quic_seal(j->key, j->iv, j->hp, j->pn[i], j->in + j->in_off[i],
-                                j->in_len[i], j->pn_offset[i], j->out + j->out_off[i]);
+    const long r = or_quic_seal2(j->suite, j->key, j->iv, j->hp, j->pn[i],
+                                 j->in + j->in_off[i], j->in_len[i], j->pn_offset[i],
+                                 j->out + j->out_off[i]);
     if (r < 0) j->err = r;
   }
   return NULL;
 }
 
-int or_quic_seal_batch(const uint8_t key[32], const uint8_t iv[12], const uint8_t hp[32],
-                       const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
-                       const uint16_t *pn_offset, const uint64_t *pn, uint32_t n, uint8_t *out,
-                       const uint64_t *out_off, int nthreads) {
+int or_quic_seal_batch2(int suite, const uint8_t *key, const uint8_t iv[12], const uint8_t *hp,
+                        const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
+                        const uint16_t *pn_offset, const uint64_t *pn, uint32_t n, uint8_t *out,
+                        const uint64_t *out_off, int nthreads) {
   if (nthreads < 1) nthreads = 1;
   if ((uint32_t)nthreads > n) nthreads = n ? (int)n : 1;
   or_qjob *jobs = (or_qjob *)calloc((size_t)nthreads, sizeof(or_qjob));
   pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
   for (int t = 0; t < nthreads; t++) {
-    or_qjob j = {key, iv, hp, in, in_off, out_off, pn, in_len, pn_offset, out,
+    or_qjob j = {suite, key, iv, hp, in, in_off, out_off, pn, in_len, pn_offset, out,
                  (uint32_t)((uint64_t)n * t / nthreads),
                  (uint32_t)((uint64_t)n * (t + 1) / nthreads), 0};
     jobs[t] = j;
@@ -696,6 +877,14 @@ int or_quic_seal_batch(const uint8_t key[32], const uint8_t iv[12], const uint8_
   free(jobs);
   free(th);
   return err ? -1 : 0;
+}
+
+int or_quic_seal_batch(const uint8_t key[32], const uint8_t iv[12], const uint8_t hp[32],
+                       const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
+                       const uint16_t *pn_offset, const uint64_t *pn, uint32_t n, uint8_t *out,
+                       const uint64_t *out_off, int nthreads) {
+  return or_quic_seal_batch2(OR_QUIC_CHACHA20, key, iv, hp, in, in_off, in_len, pn_offset, pn,
+                             n, out, out_off, nthreads);
 }
 
 uint64_t or_fnv64(const uint8_t *p, size_t n, uint64_t h) {

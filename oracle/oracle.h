@@ -83,11 +83,37 @@ long or_quic_open(const uint8_t key[32], const uint8_t iv[12], const uint8_t hp[
                   uint64_t largest_pn, const uint8_t *pkt, size_t len, size_t pn_offset,
                   uint8_t *out, uint64_t *pn_out);
 
+/* ---- TLS_AES_128_GCM_SHA256 (RFC 9001 5.3, 5.4.3): AES-128 (FIPS-197),
+ * GCM with a 96-bit nonce (NIST SP 800-38D 7.1). */
+uint8_t or_aes_sbox(uint8_t x);
+void or_aes128_expand(const uint8_t key[16], uint8_t rk[176]);
+void or_aes128_encrypt(const uint8_t rk[176], const uint8_t in[16], uint8_t out[16]);
+/* X * Y in GF(2^128) (SP 800-38D Algorithm 1) */
+void or_gf128_mul(const uint8_t x[16], const uint8_t y[16], uint8_t out[16]);
+/* decrypt = 0: seal, tag over the output; 1: open, tag over the input */
+void or_gcm_crypt(const uint8_t key[16], const uint8_t nonce[12], const uint8_t *aad,
+                  size_t aad_len, const uint8_t *in, size_t len, uint8_t *out, uint8_t tag[16],
+                  int decrypt);
+
+/* Suite-generic forms of or_quic_seal / or_quic_open: key and hp are 32
+ * bytes for OR_QUIC_CHACHA20, 16 for OR_QUIC_AES128GCM. */
+#define OR_QUIC_CHACHA20 0
+#define OR_QUIC_AES128GCM 1
+long or_quic_seal2(int suite, const uint8_t *key, const uint8_t iv[12], const uint8_t *hp,
+                   uint64_t pn, const uint8_t *pkt, size_t len, size_t pn_offset, uint8_t *out);
+long or_quic_open2(int suite, const uint8_t *key, const uint8_t iv[12], const uint8_t *hp,
+                   uint64_t largest_pn, const uint8_t *pkt, size_t len, size_t pn_offset,
+                   uint8_t *out, uint64_t *pn_out);
+
 /* or_quic_seal over a batch (one key) on nthreads threads; 0 or -1. */
 int or_quic_seal_batch(const uint8_t key[32], const uint8_t iv[12], const uint8_t hp[32],
                        const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
                        const uint16_t *pn_offset, const uint64_t *pn, uint32_t n, uint8_t *out,
                        const uint64_t *out_off, int nthreads);
+int or_quic_seal_batch2(int suite, const uint8_t *key, const uint8_t iv[12], const uint8_t *hp,
+                        const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
+                        const uint16_t *pn_offset, const uint64_t *pn, uint32_t n, uint8_t *out,
+                        const uint64_t *out_off, int nthreads);
 
 /* Salamander key: BLAKE2b-256(psk || salt[0:8])  (salamander.go:50,61,84,99) */
 void or_salamander_key(const uint8_t *psk, size_t psk_len,

@@ -73,6 +73,21 @@ def lib() -> ctypes.CDLL:
         L.or_quic_open.restype = ctypes.c_long
         L.or_quic_seal_batch.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, ctypes.c_uint32, vp, vp,
                                          ctypes.c_int]
+        L.or_quic_seal_batch2.argtypes = [ctypes.c_int] + L.or_quic_seal_batch.argtypes
+        L.or_quic_seal2.argtypes = [ctypes.c_int] + L.or_quic_seal.argtypes
+        L.or_quic_seal2.restype = ctypes.c_long
+        L.or_quic_open2.argtypes = [ctypes.c_int] + L.or_quic_open.argtypes
+        L.or_quic_open2.restype = ctypes.c_long
+        L.or_aes_sbox.argtypes = [ctypes.c_uint8]
+        L.or_aes_sbox.restype = ctypes.c_uint8
+        L.or_aes128_expand.argtypes = [vp, vp]
+        L.or_aes128_expand.restype = None
+        L.or_aes128_encrypt.argtypes = [vp, vp, vp]
+        L.or_aes128_encrypt.restype = None
+        L.or_gf128_mul.argtypes = [vp, vp, vp]
+        L.or_gf128_mul.restype = None
+        L.or_gcm_crypt.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, ctypes.c_int]
+        L.or_gcm_crypt.restype = None
         L.or_batch_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(OrPsks),
                                    ctypes.POINTER(OrBatch), ctypes.c_int]
         L.or_fnv64.argtypes = [vp, sz, ctypes.c_uint64]
@@ -211,17 +226,46 @@ def aead_seal(key: bytes, nonce: bytes, aad: bytes, pt: bytes) -> bytes:
     return ct.raw[:len(pt)] + tag.raw
 
 
-def quic_seal(key: bytes, iv: bytes, hp: bytes, pn: int, pkt: bytes, pn_offset: int):
-    """(protected packet, return code) -- RFC 9001 5.3/5.4, ChaCha20-Poly1305."""
+CHACHA20, AES128GCM = 0, 1  # QUIC suites (oracle.h OR_QUIC_*)
+
+
+def quic_seal(key: bytes, iv: bytes, hp: bytes, pn: int, pkt: bytes, pn_offset: int,
+              suite: int = CHACHA20):
+    """(protected packet, return code) -- RFC 9001 5.3/5.4; suite CHACHA20
+    (32-byte key/hp) or AES128GCM (16-byte key/hp)."""
     out = ctypes.create_string_buffer(len(pkt) + 16)
-    r = lib().or_quic_seal(key, iv, hp, pn, pkt, len(pkt), pn_offset, out)
+    r = lib().or_quic_seal2(suite, key, iv, hp, pn, pkt, len(pkt), pn_offset, out)
     return (out.raw[:r] if r > 0 else b""), r
 
 
-def quic_open(key: bytes, iv: bytes, hp: bytes, largest_pn: int, pkt: bytes, pn_offset: int):
+def quic_open(key: bytes, iv: bytes, hp: bytes, largest_pn: int, pkt: bytes, pn_offset: int,
+              suite: int = CHACHA20):
     """(unprotected header || plaintext, return code, decoded pn)."""
     out = ctypes.create_string_buffer(max(len(pkt), 1))
     pn = ctypes.c_uint64(0)
-    r = lib().or_quic_open(key, iv, hp, largest_pn, pkt, len(pkt), pn_offset, out,
-                           ctypes.byref(pn))
+    r = lib().or_quic_open2(suite, key, iv, hp, largest_pn, pkt, len(pkt), pn_offset, out,
+                            ctypes.byref(pn))
     return (out.raw[:len(pkt) - 16] if len(pkt) >= 16 else b""), r, pn.value
+
+
+def aes128_encrypt(key: bytes, block: bytes) -> bytes:
+    """FIPS-197 AES-128 of one block."""
+    rk = ctypes.create_string_buffer(176)
+    out = ctypes.create_string_buffer(16)
+    lib().or_aes128_expand(key, rk)
+    lib().or_aes128_encrypt(rk, block, out)
+    return out.raw
+
+
+def gf128_mul(x: bytes, y: bytes) -> bytes:
+    out = ctypes.create_string_buffer(16)
+    lib().or_gf128_mul(x, y, out)
+    return out.raw
+
+
+def gcm_seal(key: bytes, nonce: bytes, aad: bytes, pt: bytes) -> bytes:
+    """ct || tag (SP 800-38D, 96-bit nonce)."""
+    ct = ctypes.create_string_buffer(max(len(pt), 1))
+    tag = ctypes.create_string_buffer(16)
+    lib().or_gcm_crypt(key, nonce, aad, len(aad), pt, len(pt), ct, tag, 0)
+    return ct.raw[:len(pt)] + tag.raw

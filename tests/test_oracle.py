@@ -192,3 +192,44 @@ def test_quic_packet_protection(golden):
         bad = bytearray(prot)
         bad[-1] ^= 1  # tag bit flip
         assert ol.quic_open(k, iv, hp, v["largest_pn"], bytes(bad), v["pn_offset"])[1] == -2
+
+
+def test_aes128_and_gcm(golden):
+    """AES-128 (FIPS-197) and AES-128-GCM restatements against FIPS-197, the
+    GCM specification's test cases and OpenSSL (tests/golden/make_quic_gcm.py)."""
+    g = golden("quic_gcm.json")
+    for v in g["aes"]:
+        assert ol.aes128_encrypt(B(v["key"]), B(v["pt"])).hex() == v["ct"], v["source"]
+    for v in g["gcm"]:
+        assert ol.gcm_seal(B(v["key"]), B(v["nonce"]), B(v["aad"]), B(v["pt"])).hex() == \
+            v["ct_tag"], v["source"]
+    # GF(2^128): x * 1 = x (1 is the bit-reflected 0x80..00), commutative
+    one = bytes([0x80]) + bytes(15)
+    x, y = bytes(range(16)), bytes(range(100, 116))
+    assert ol.gf128_mul(x, one) == x
+    assert ol.gf128_mul(x, y) == ol.gf128_mul(y, x)
+
+
+def test_quic_aes_gcm_packet_protection(golden):
+    """RFC 9001 A.3 (server Initial, AES-128-GCM) and 40 OpenSSL-built packets:
+    seal bit-exact, open round trip with the packet number decoded."""
+    g = golden("quic_gcm.json")
+    a3, sk = g["rfc9001_a3"], g["rfc9001_a1"]["server"]
+    k, iv, hp = B(sk["key"]), B(sk["iv"]), B(sk["hp"])
+    pkt = B(a3["header"] + a3["payload"])
+    prot, r = ol.quic_seal(k, iv, hp, a3["pn"], pkt, a3["pn_offset"], suite=ol.AES128GCM)
+    assert r == len(pkt) + 16 and prot.hex() == a3["protected"]
+    back, r, pn = ol.quic_open(k, iv, hp, 0, prot, a3["pn_offset"], suite=ol.AES128GCM)
+    assert r == len(pkt) and back == pkt and pn == a3["pn"]
+    for v in g["packets"]:
+        k, iv, hp = B(v["key"]), B(v["iv"]), B(v["hp"])
+        pkt = B(v["packet"])
+        prot, r = ol.quic_seal(k, iv, hp, v["pn"], pkt, v["pn_offset"], suite=ol.AES128GCM)
+        assert prot.hex() == v["protected"]
+        back, r, pn = ol.quic_open(k, iv, hp, v["largest_pn"], prot, v["pn_offset"],
+                                   suite=ol.AES128GCM)
+        assert r == len(pkt) and back == pkt and pn == v["pn"]
+        bad = bytearray(prot)
+        bad[-1] ^= 1
+        assert ol.quic_open(k, iv, hp, v["largest_pn"], bytes(bad), v["pn_offset"],
+                            suite=ol.AES128GCM)[1] == -2
