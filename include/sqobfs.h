@@ -64,7 +64,7 @@
 extern "C" {
 #endif
 
-#define SQOBFS_ABI_VERSION 2
+#define SQOBFS_ABI_VERSION 3
 
 #define SQOBFS_SALAMANDER_SALT_LEN 8 /* hysteria2/salamander.go:15 */
 #define SQOBFS_XPLUS_SALT_LEN 16     /* hysteria/xplus.go:17 */
@@ -196,7 +196,8 @@ int sqobfs_host_alloc(sqobfs_ctx *ctx, size_t bytes, void **out);
 void sqobfs_host_free(sqobfs_ctx *ctx, void *p);
 
 /* ------------------------------------------------------------------------
- * QUIC packet protection, AEAD_CHACHA20_POLY1305.
+ * QUIC packet protection: AEAD_CHACHA20_POLY1305
+ * and AEAD_AES_128_GCM, each with its header protection.
  *
  * The next per-datagram byte transform under the obfuscation layer: quic-go
  * (v0.52.0-beta.1, go.mod:7; not in the reference tree) seals every 1-RTT
@@ -213,16 +214,24 @@ void sqobfs_host_free(sqobfs_ctx *ctx, void *p);
  *   open:  the reverse; the packet number is decoded from its truncated
  *          form against the largest received one (RFC 9000 Appendix A.3)
  *          and the tag is verified.
+ * AES-128-GCM (TLS_AES_128_GCM_SHA256) is the same with
+ *          payload -> AES-128-GCM(key, nonce, aad = header)   (SP 800-38D)
+ *          mask = AES-128-ECB(hp, sample)                  (RFC 9001 5.4.3)
  * The packet-number length is (first byte & 3) + 1 of the unprotected
  * header, as QUIC encodes it. */
 
 /* One connection's 1-RTT keys (from the TLS key schedule: "quic key",
- * "quic iv", "quic hp", RFC 9001 5.1). */
+ * "quic iv", "quic hp", RFC 9001 5.1).  AES-128-GCM uses key[0..16) and
+ * hp[0..16). */
 typedef struct sqobfs_quic_key {
   uint8_t key[32];
   uint8_t iv[12];
   uint8_t hp[32];
 } sqobfs_quic_key;
+
+/* Cipher suites (the AEAD of the negotiated TLS 1.3 suite, RFC 9001 5.3) */
+#define SQOBFS_QUIC_CHACHA20_POLY1305 0u /* TLS_CHACHA20_POLY1305_SHA256 */
+#define SQOBFS_QUIC_AES_128_GCM 1u       /* TLS_AES_128_GCM_SHA256 */
 
 typedef struct sqobfs_quic_keyring sqobfs_quic_keyring;
 
@@ -255,6 +264,12 @@ typedef struct sqobfs_quic_batch {
   uint64_t *pn_out;            /* open: [n] decoded packet numbers, or NULL */
 } sqobfs_quic_batch;
 
+/* A keyring holds connections of ONE suite (a batch is sealed / opened
+ * with the keyring's suite).  sqobfs_quic_keyring_create is the
+ * ChaCha20-Poly1305 form.  For AES-128-GCM the key schedules and the GHASH
+ * tables (about 33 KiB per connection) are prepared here, once. */
+int sqobfs_quic_keyring_create_suite(sqobfs_ctx *ctx, uint32_t suite, uint32_t count,
+                                     const sqobfs_quic_key *keys, sqobfs_quic_keyring **out);
 int sqobfs_quic_keyring_create(sqobfs_ctx *ctx, uint32_t count, const sqobfs_quic_key *keys,
                                sqobfs_quic_keyring **out);
 void sqobfs_quic_keyring_destroy(sqobfs_quic_keyring *kr);

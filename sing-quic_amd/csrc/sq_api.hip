@@ -44,9 +44,13 @@ constexpr uint32_t kEvents = 16;
 
 struct sqobfs_quic_keyring {
   sqobfs_ctx *ctx = nullptr;
+  uint32_t suite = SQOBFS_QUIC_CHACHA20_POLY1305;
   uint32_t count = 0;
-  sq::QuicKeyDev *table = nullptr;  // device
+  sq::QuicKeyDev *table = nullptr;  // device (ChaCha20-Poly1305)
   sq::QuicKeyDev host0;             // entry 0, passed by value
+  sq::QuicGcmKeyDev *gtable = nullptr;  // device (AES-128-GCM)
+  uint32_t *t0 = nullptr;               // device AES T-table (256 words)
+  uint32_t grk0[44], ghrk0[44], giv0[3];
 };
 
 struct sqobfs_keyring {
@@ -348,32 +352,204 @@ int sqobfs_xplus_deobfuscate(sqobfs_ctx *ctx, const sqobfs_keyring *kr, const sq
 
 // ---------------------------------------------------------------- QUIC
 
-int sqobfs_quic_keyring_create(sqobfs_ctx *ctx, uint32_t count, const sqobfs_quic_key *keys,
-                               sqobfs_quic_keyring **out) {
+// ---- AES-128-GCM key preparation (host, once per keyring): FIPS-197 key
+// expansion, H = AES_K(0^128), and the 4-bit GHASH tables of H^1..H^128
+// that sq_quic_gcm.hip reads.  Connection setup work, not per packet.
+extern "C++" {
+namespace {
+uint8_t gf8_mul(uint8_t a, uint8_t b) {
+  uint8_t r = 0;
+  for (; b; b >>= 1) {
+    if (b & 1) r ^= a;
+    a = (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0));
+  }
+  return r;
+}
+
+struct AesTables {
+  uint8_t sbox[256];
+  uint32_t t0[256];  // little-endian column (2s, s, s, 3s)
+  AesTables() {
+    for (int x = 0; x < 256; x++) {
+      uint8_t inv = 0, base = (uint8_t)x, acc = 1;
+      if (x) {
+        for (int e = 254; e; e >>= 1) {
+          if (e & 1) acc = gf8_mul(acc, base);
+          base = gf8_mul(base, base);
+        }
+        inv = acc;
+      }
+      uint8_t y = 0x63;
+      for (int k = 0; k < 5; k++) y ^= (uint8_t)((inv << k) | (inv >> ((8 - k) & 7)));
+      sbox[x] = y;
+      const uint32_t s1 = y, s2 = gf8_mul(y, 2), s3 = s2 ^ s1;
+      t0[x] = s2 | (s1 << 8) | (s1 << 16) | (s3 << 24);
+    }
+  }
+};
+const AesTables &aes_tables() {
+  static const AesTables t;
+  return t;
+}
+
+uint32_t le32(const uint8_t *b) {
+  return (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24);
+}
+
+void aes128_expand(const uint8_t key[16], uint32_t rk[44]) {
+  const uint8_t *sb = aes_tables().sbox;
+  uint8_t w[176];
+  memcpy(w, key, 16);
+  uint8_t rcon = 1;
+  for (int i = 4; i < 44; i++) {
+    uint8_t t[4] = {w[4 * i - 4], w[4 * i - 3], w[4 * i - 2], w[4 * i - 1]};
+    if (i % 4 == 0) {
+      const uint8_t t0 = t[0];
+      t[0] = (uint8_t)(sb[t[1]] ^ rcon);
+      t[1] = sb[t[2]];
+      t[2] = sb[t[3]];
+      t[3] = sb[t0];
+      rcon = gf8_mul(rcon, 2);
+    }
+    for (int k = 0; k < 4; k++) w[4 * i + k] = w[4 * i - 16 + k] ^ t[k];
+  }
+  for (int i = 0; i < 44; i++) rk[i] = le32(w + 4 * i);
+}
+
+// one block, same column-word form as the device
+void aes128_block(const uint32_t rk[44], const uint8_t in[16], uint8_t out[16]) {
+  const uint32_t *T = aes_tables().t0;
+  auto rot = [](uint32_t x, int n) { return (x << n) | (x >> (32 - n)); };
+  uint32_t s[4];
+  for (int c = 0; c < 4; c++) s[c] = le32(in + 4 * c) ^ rk[c];
+  for (int r = 1; r <= 10; r++) {
+    uint32_t t[4];
+    for (int c = 0; c < 4; c++) {
+      const uint32_t a0 = T[s[c] & 0xFF], a1 = T[(s[(c + 1) & 3] >> 8) & 0xFF];
+      const uint32_t a2 = T[(s[(c + 2) & 3] >> 16) & 0xFF], a3 = T[s[(c + 3) & 3] >> 24];
+      t[c] = r < 10 ? a0 ^ rot(a1, 8) ^ rot(a2, 16) ^ rot(a3, 24)
+                    : ((a0 >> 8) & 0xFF) | (a1 & 0xFF00) | ((a2 << 8) & 0xFF0000) |
+                          ((a3 << 16) & 0xFF000000u);
+      t[c] ^= rk[4 * r + c];
+    }
+    memcpy(s, t, sizeof s);
+  }
+  for (int c = 0; c < 4; c++)
+    for (int k = 0; k < 4; k++) out[4 * c + k] = (uint8_t)(s[c] >> (8 * k));
+}
+
+// GF(2^128) element as a big-endian 128-bit integer (hi, lo); bit 127 of the
+// integer is the coefficient of x^0 (SP 800-38D bit order)
+struct G128 {
+  uint64_t hi, lo;
+};
+G128 g_load(const uint8_t b[16]) {
+  G128 g{0, 0};
+  for (int k = 0; k < 8; k++) g.hi = (g.hi << 8) | b[k];
+  for (int k = 8; k < 16; k++) g.lo = (g.lo << 8) | b[k];
+  return g;
+}
+G128 g_mulx(G128 v) {  // v * x
+  const bool lsb = v.lo & 1;
+  v.lo = (v.lo >> 1) | (v.hi << 63);
+  v.hi >>= 1;
+  if (lsb) v.hi ^= 0xE100000000000000ull;
+  return v;
+}
+G128 g_mul(G128 x, G128 y) {  // SP 800-38D Algorithm 1
+  G128 z{0, 0}, v = y;
+  for (int i = 0; i < 128; i++) {
+    const bool bit = i < 64 ? (x.hi >> (63 - i)) & 1 : (x.lo >> (127 - i)) & 1;
+    if (bit) {
+      z.hi ^= v.hi;
+      z.lo ^= v.lo;
+    }
+    v = g_mulx(v);
+  }
+  return z;
+}
+
+void gcm_key(const sqobfs_quic_key &k, sq::QuicGcmKeyDev &d) {
+  memset(&d, 0, sizeof d);
+  aes128_expand(k.key, d.rk);
+  aes128_expand(k.hp, d.hrk);
+  for (int i = 0; i < 3; i++) d.iv[i] = le32(k.iv + 4 * i);
+  const uint8_t zero[16] = {0};
+  uint8_t hb[16];
+  aes128_block(d.rk, zero, hb);
+  const G128 h = g_load(hb);
+  G128 p = h;
+  for (uint32_t pw = 0; pw < sq::kGcmPow; pw++) {
+    if (pw) p = g_mul(p, h);
+    G128 e[16] = {};
+    e[8] = p;  // Shoup: entry 8 = H^k, 4 = H^k x, 2 = H^k x^2, 1 = H^k x^3
+    e[4] = g_mulx(e[8]);
+    e[2] = g_mulx(e[4]);
+    e[1] = g_mulx(e[2]);
+    for (int n = 1; n < 16; n++) {
+      if (n == 1 || n == 2 || n == 4 || n == 8) continue;
+      G128 v{0, 0};
+      for (int b = 1; b < 16; b <<= 1)
+        if (n & b) {
+          v.hi ^= e[b].hi;
+          v.lo ^= e[b].lo;
+        }
+      e[n] = v;
+    }
+    for (int n = 0; n < 16; n++) {
+      d.htab[pw][n][0] = (uint32_t)(e[n].hi >> 32);
+      d.htab[pw][n][1] = (uint32_t)e[n].hi;
+      d.htab[pw][n][2] = (uint32_t)(e[n].lo >> 32);
+      d.htab[pw][n][3] = (uint32_t)e[n].lo;
+    }
+  }
+}
+}  // namespace
+}  // extern "C++"
+
+int sqobfs_quic_keyring_create_suite(sqobfs_ctx *ctx, uint32_t suite, uint32_t count,
+                                     const sqobfs_quic_key *keys, sqobfs_quic_keyring **out) {
   if (out) *out = nullptr;
   if (!ctx || !out || count == 0 || !keys) return SQ_EINVAL;
+  if (suite != SQOBFS_QUIC_CHACHA20_POLY1305 && suite != SQOBFS_QUIC_AES_128_GCM)
+    return SQ_EINVAL;
   SQ_TRY(hipSetDevice(ctx->device));
-  std::vector<sq::QuicKeyDev> h(count);
-  auto le = [](const uint8_t *b) {
-    return (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) |
-           ((uint32_t)b[3] << 24);
-  };
-  for (uint32_t k = 0; k < count; k++) {
-    memset(&h[k], 0, sizeof h[k]);
-    for (int i = 0; i < 8; i++) h[k].key[i] = le(keys[k].key + 4 * i);
-    for (int i = 0; i < 3; i++) h[k].iv[i] = le(keys[k].iv + 4 * i);
-    for (int i = 0; i < 8; i++) h[k].hp[i] = le(keys[k].hp + 4 * i);
-  }
   sqobfs_quic_keyring *kr = new (std::nothrow) sqobfs_quic_keyring();
   if (!kr) return SQ_ENOMEM;
   kr->ctx = ctx;
+  kr->suite = suite;
   kr->count = count;
-  kr->host0 = h[0];
-  hipError_t e = hipMalloc(&kr->table, sizeof(sq::QuicKeyDev) * count);
-  if (e == hipSuccess)
-    e = hipMemcpy(kr->table, h.data(), sizeof(sq::QuicKeyDev) * count, hipMemcpyHostToDevice);
+  hipError_t e = hipSuccess;
+  if (suite == SQOBFS_QUIC_CHACHA20_POLY1305) {
+    std::vector<sq::QuicKeyDev> h(count);
+    for (uint32_t k = 0; k < count; k++) {
+      memset(&h[k], 0, sizeof h[k]);
+      for (int i = 0; i < 8; i++) h[k].key[i] = le32(keys[k].key + 4 * i);
+      for (int i = 0; i < 3; i++) h[k].iv[i] = le32(keys[k].iv + 4 * i);
+      for (int i = 0; i < 8; i++) h[k].hp[i] = le32(keys[k].hp + 4 * i);
+    }
+    kr->host0 = h[0];
+    e = hipMalloc(&kr->table, sizeof(sq::QuicKeyDev) * count);
+    if (e == hipSuccess)
+      e = hipMemcpy(kr->table, h.data(), sizeof(sq::QuicKeyDev) * count, hipMemcpyHostToDevice);
+  } else {
+    std::vector<sq::QuicGcmKeyDev> h(count);
+    for (uint32_t k = 0; k < count; k++) gcm_key(keys[k], h[k]);
+    memcpy(kr->grk0, h[0].rk, sizeof kr->grk0);
+    memcpy(kr->ghrk0, h[0].hrk, sizeof kr->ghrk0);
+    memcpy(kr->giv0, h[0].iv, sizeof kr->giv0);
+    e = hipMalloc(&kr->gtable, sizeof(sq::QuicGcmKeyDev) * count);
+    if (e == hipSuccess)
+      e = hipMemcpy(kr->gtable, h.data(), sizeof(sq::QuicGcmKeyDev) * count,
+                    hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&kr->t0, sizeof(uint32_t) * 256);
+    if (e == hipSuccess)
+      e = hipMemcpy(kr->t0, aes_tables().t0, sizeof(uint32_t) * 256, hipMemcpyHostToDevice);
+  }
   if (e != hipSuccess) {
     if (kr->table) (void)hipFree(kr->table);
+    if (kr->gtable) (void)hipFree(kr->gtable);
+    if (kr->t0) (void)hipFree(kr->t0);
     delete kr;
     return hip_status(e);
   }
@@ -381,11 +557,18 @@ int sqobfs_quic_keyring_create(sqobfs_ctx *ctx, uint32_t count, const sqobfs_qui
   return SQ_OK;
 }
 
+int sqobfs_quic_keyring_create(sqobfs_ctx *ctx, uint32_t count, const sqobfs_quic_key *keys,
+                               sqobfs_quic_keyring **out) {
+  return sqobfs_quic_keyring_create_suite(ctx, SQOBFS_QUIC_CHACHA20_POLY1305, count, keys, out);
+}
+
 void sqobfs_quic_keyring_destroy(sqobfs_quic_keyring *kr) {
   if (!kr) return;
   (void)hipSetDevice(kr->ctx->device);
   (void)hipDeviceSynchronize();
   if (kr->table) (void)hipFree(kr->table);
+  if (kr->gtable) (void)hipFree(kr->gtable);
+  if (kr->t0) (void)hipFree(kr->t0);
   delete kr;
 }
 
@@ -397,6 +580,28 @@ static int quic_launch(int open, sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr,
       !b->pn_offset || !b->pn)
     return SQ_EINVAL;
   SQ_TRY(hipSetDevice(ctx->device));
+  if (kr->suite == SQOBFS_QUIC_AES_128_GCM) {
+    sq::QGParams g;
+    memset(&g, 0, sizeof g);
+    g.in = b->in;
+    g.in_off = b->in_off;
+    g.in_len = b->in_len;
+    g.out = b->out;
+    g.out_off = b->out_off;
+    g.out_len = b->out_len;
+    g.pn_offset = b->pn_offset;
+    g.pn = b->pn;
+    g.key_id = b->key_id;
+    g.pn_out = open ? b->pn_out : nullptr;
+    g.keys = kr->gtable;
+    g.t0 = kr->t0;
+    g.n = b->n;
+    g.n_keys = kr->count;
+    memcpy(g.rk0, kr->grk0, sizeof g.rk0);
+    memcpy(g.hrk0, kr->ghrk0, sizeof g.hrk0);
+    memcpy(g.iv0, kr->giv0, sizeof g.iv0);
+    return sq_launch_quic_gcm(open, &g, pick_stream(ctx, stream));
+  }
   sq::QParams q;
   memset(&q, 0, sizeof q);
   q.in = b->in;

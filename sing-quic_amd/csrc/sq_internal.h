@@ -91,7 +91,46 @@ struct QParams {
   QuicKeyDev key0;
 };
 
+// AES-128-GCM (TLS_AES_128_GCM_SHA256) connection keys on the device:
+// AES-128 key schedules of the payload key and the header-protection key as
+// little-endian column words (word 4r + c = bytes 4c..4c+3 of round key r),
+// the IV, and 4-bit GHASH tables of H^1 .. H^kGcmPow (Shoup's method; entry
+// n of table k-1 = the nibble polynomial n times H^k, as big-endian words).
+constexpr uint32_t kGcmPow = 128;
+struct QuicGcmKeyDev {
+  uint32_t rk[44];
+  uint32_t hrk[44];
+  uint32_t iv[3];
+  uint32_t pad;
+  uint32_t htab[kGcmPow][16][4];
+};
+
+// AES-128-GCM launch; rk0 / hrk0 / iv0 = keyring entry 0 (kernarg); t0 = the
+// 256-word AES T-table (device, 1 KiB), staged into LDS by every block.
+struct QGParams {
+  const uint8_t *in;
+  const uint64_t *in_off;
+  const uint32_t *in_len;
+  uint8_t *out;
+  const uint64_t *out_off;
+  uint32_t *out_len;
+  const uint16_t *pn_offset;
+  const uint64_t *pn;
+  const uint16_t *key_id;
+  uint64_t *pn_out;
+  const QuicGcmKeyDev *keys;
+  const uint32_t *t0;
+  uint32_t n;
+  uint32_t n_keys;
+  uint32_t rk0[44];
+  uint32_t hrk0[44];
+  uint32_t iv0[3];
+};
+
 }  // namespace sq
+
+// launchers implemented in sq_quic_gcm.hip
+extern "C" int sq_launch_quic_gcm(int open, const sq::QGParams *qp, void *stream);
 
 // launchers implemented in sq_quic.hip
 extern "C" int sq_launch_quic(int open, const sq::QParams *qp, void *stream);

@@ -1,0 +1,509 @@
+// sq_quic_gcm.hip -- gfx950 QUIC packet protection, TLS_AES_128_GCM_SHA256
+// (the suite every QUIC stack must implement).
+//
+// Replaces, for a whole ragged batch per launch, quic-go's per-packet
+//   internal/handshake/aead.go              Seal / Open (AES-128-GCM)
+//   internal/handshake/header_protector.go  aesHeaderProtector
+// (quic-go v0.52.0-beta.1, go.mod:7; reached from the reference through
+// quic.go:47-102; not in the reference tree).  The algorithms are FIPS-197
+// (AES-128), NIST SP 800-38D (GCM with a 96-bit nonce: J0 = nonce || 1,
+// payload counters from 2) and RFC 9001 sections 5.3 / 5.4.3 (nonce, AES
+// header protection: mask = AES-ECB(hp, sample)).  The CPU checker is
+// oracle/oracle.c (or_quic_seal2 / or_quic_open2), pinned by FIPS-197, the GCM
+// specification's test cases, RFC 9001 A.3 and OpenSSL
+// (tests/golden/quic_gcm.json).
+//
+// gfx950 has no carry-less multiply and no AES instructions, so both run as
+// LDS table lookups, laid out for the LDS banking rules:
+//   * AES rounds: one 1 KiB T-table (T1..T3 are byte rotations of T0),
+//     replicated 32 times with entry x of copy c at word 32x + c.  Lane l
+//     reads copy l & 31, so a ds_read_b32 (two 32-lane halves, bank =
+//     word mod 32) is conflict-free whatever the state bytes are.
+//   * GHASH: Shoup's 4-bit tables (16 entries x 16 B = one 256-byte bank
+//     row), so every ds_read_b128 is conflict-free for lanes multiplying by
+//     the same power.  Tables of H^1 .. H^128 (32 KiB) let each chunk of the
+//     cooperative pass multiply its partial GHASH by the power that places it
+//     in the packet: GHASH is linear, so the packet's value is the XOR of
+//     the chunk partials times H^m (ds_xor_b32 into the packet's record) --
+//     no serial combine.
+// Work decomposition, per wave of 16 packets (as the ChaCha20 kernel):
+//   1. owner lane per packet: descriptor; for open, header protection and
+//      the packet number; nonce; GHASH over the header (the AAD), times
+//      H^(payload blocks);
+//   2. all 64 lanes: the packets' 64-byte payload chunks as one flat space;
+//      a lane runs 4 AES-CTR blocks, XORs, Horners its <= 4 ciphertext blocks
+//      with H from 0, multiplies by H^m (m = payload blocks after the chunk),
+//      XORs the result into the packet's accumulator, and stores realigned
+//      output;
+//   3. owner lane: the lengths block, E(K, J0), the tag; for seal, header
+//      protection.
+// Payloads above 2,048 B (chunk multipliers past H^128) are walked by their
+// owner lane in phase 3 (plain Horner), so any length works.
+// Single-key launches keep the round keys in the kernarg segment (scalar
+// operands) and the GHASH tables in LDS; multi-key launches read both from
+// the packet's keyring entry in global memory.
+#include <hip/hip_runtime.h>
+
+#include "sq_bytes.h"
+#include "sq_internal.h"
+#include "sq_quic.h"
+
+namespace sq {
+
+constexpr uint32_t kGBlock = 512;
+constexpr uint32_t kGWaves = kGBlock / kWave;
+constexpr uint32_t kGPpw = 16;                 // packets per wave
+constexpr uint32_t kGCoopMax = 16 * kGcmPow;   // 2048 B
+
+// ---------------------------------------------------------------- AES-128
+
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int n) {
+  return __builtin_amdgcn_alignbit(x, x, 32 - n);
+}
+
+// round key r (4 column words): kernarg (single key) or the lane's entry
+template <bool MULTI>
+__device__ __forceinline__ void round_key(const uint32_t *rk, int r, uint32_t (&k)[4]) {
+  if (MULTI) {
+    const u32x4 v = gld<u32x4>((uint64_t)(rk + 4 * r));
+    k[0] = v.x; k[1] = v.y; k[2] = v.z; k[3] = v.w;
+  } else {
+    k[0] = rk[4 * r]; k[1] = rk[4 * r + 1]; k[2] = rk[4 * r + 2]; k[3] = rk[4 * r + 3];
+  }
+}
+
+// T0[x] from this lane's copy of the replicated table
+__device__ __forceinline__ uint32_t tlook(const uint32_t *tT, uint32_t x, uint32_t l31) {
+  return tT[(x << 5) | l31];
+}
+
+// FIPS-197 cipher on one block held as 4 little-endian column words.
+// Round: column c = T0[s_c.b0] ^ rotl8 T0[s_c+1.b1] ^ rotl16 T0[s_c+2.b2] ^
+// rotl24 T0[s_c+3.b3] ^ rk (ShiftRows folded into the byte picks); the last
+// round takes the S-box byte (byte 1 of T0) instead.
+template <bool MULTI>
+__device__ __forceinline__ void aes_encrypt(const uint32_t *rk, const uint32_t *tT, uint32_t l31,
+                                            uint32_t (&s)[4]) {
+  uint32_t k[4];
+  round_key<MULTI>(rk, 0, k);
+#pragma unroll
+  for (int c = 0; c < 4; c++) s[c] ^= k[c];
+#pragma unroll
+  for (int r = 1; r < 10; r++) {
+    round_key<MULTI>(rk, r, k);
+    uint32_t t[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const uint32_t a0 = tlook(tT, s[c] & 0xFFu, l31);
+      const uint32_t a1 = tlook(tT, (s[(c + 1) & 3] >> 8) & 0xFFu, l31);
+      const uint32_t a2 = tlook(tT, (s[(c + 2) & 3] >> 16) & 0xFFu, l31);
+      const uint32_t a3 = tlook(tT, s[(c + 3) & 3] >> 24, l31);
+      t[c] = a0 ^ rotl(a1, 8) ^ rotl(a2, 16) ^ rotl(a3, 24) ^ k[c];
+    }
+#pragma unroll
+    for (int c = 0; c < 4; c++) s[c] = t[c];
+  }
+  round_key<MULTI>(rk, 10, k);
+  uint32_t t[4];
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const uint32_t a0 = tlook(tT, s[c] & 0xFFu, l31);
+    const uint32_t a1 = tlook(tT, (s[(c + 1) & 3] >> 8) & 0xFFu, l31);
+    const uint32_t a2 = tlook(tT, (s[(c + 2) & 3] >> 16) & 0xFFu, l31);
+    const uint32_t a3 = tlook(tT, s[(c + 3) & 3] >> 24, l31);
+    t[c] = (((a0 >> 8) & 0xFFu) | (a1 & 0xFF00u) | ((a2 << 8) & 0xFF0000u) |
+            ((a3 << 16) & 0xFF000000u)) ^ k[c];
+  }
+#pragma unroll
+  for (int c = 0; c < 4; c++) s[c] = t[c];
+}
+
+// ---------------------------------------------------------------- GHASH
+
+// x <- x * H^k in GF(2^128) (SP 800-38D bit order), x as big-endian words
+// (x[0] = bytes 0..3).  tab = the 16-entry 4-bit table of H^k; nibbles are
+// consumed from the low end of the 128-bit integer, each step multiplying
+// the accumulator by x^4 (shift right 4, fold the 4 bits shifted out back
+// with the reduction polynomial: rem * 0x1C20 carry-less, at bits 112..127).
+template <bool GLOBAL>
+__device__ __forceinline__ void gmul(uint32_t (&x)[4], const uint32_t *tab) {
+  uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
+  uint32_t w = x[3], w2 = x[2], w1 = x[1], w0 = x[0];
+  // one word (8 nibbles) per iteration, kept rolled: unrolled, the compiler
+  // hoists all 32 table reads and holds 128 VGPRs of entries
+#pragma unroll 1
+  for (int i = 0; i < 4; i++) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint32_t nib = (w >> (4 * j)) & 0xFu;
+      if (i | j) {
+        const uint32_t rem = z3 & 0xFu;
+        z3 = __builtin_amdgcn_alignbit(z2, z3, 4);
+        z2 = __builtin_amdgcn_alignbit(z1, z2, 4);
+        z1 = __builtin_amdgcn_alignbit(z0, z1, 4);
+        z0 = (z0 >> 4) ^ (rem << 28) ^ (rem << 27) ^ (rem << 26) ^ (rem << 21);
+      }
+      u32x4 e;
+      if (GLOBAL) e = gld<u32x4>((uint64_t)(tab + 4 * nib));
+      else e = *(const u32x4 *)(tab + 4 * nib);
+      z0 ^= e.x; z1 ^= e.y; z2 ^= e.z; z3 ^= e.w;
+    }
+    w = w2;
+    w2 = w1;
+    w1 = w0;
+  }
+  x[0] = z0; x[1] = z1; x[2] = z2; x[3] = z3;
+}
+
+// y ^= 16 bytes held as little-endian words
+__device__ __forceinline__ void ghash_absorb(uint32_t (&y)[4], const uint32_t (&m)[4]) {
+#pragma unroll
+  for (int w = 0; w < 4; w++) y[w] ^= __builtin_bswap32(m[w]);
+}
+
+// Key material of one packet: round keys, header-protection round keys,
+// IV, and the GHASH tables (table k-1 = H^k).
+template <bool MULTI>
+struct GKey {
+  const uint32_t *rk, *hrk, *iv, *htab;
+  __device__ __forceinline__ const uint32_t *pow(uint32_t k) const { return htab + 64 * (k - 1); }
+};
+
+// ---------------------------------------------------------------- payload
+
+// Payload bytes [0, nv) at src -> dst: CTR blocks ctr0, ctr0 + 1, ...; y
+// absorbs every ciphertext block (y = (y ^ C) * H).  Streaming realigner
+// (one aligned 16-byte load and store per block whatever the alignments,
+// one block of read-ahead), as payload_pass in sq_quic.hip.  In place
+// (src == dst) works.  first32 = ciphertext bytes 0..31 (zero past nv).
+template <bool OPEN, bool MULTI>
+__device__ __forceinline__ void gcm_run(const GKey<MULTI> &K, const uint32_t *tT, uint32_t l31,
+                                        const uint32_t (&nonce)[3], uint32_t ctr0, uint64_t src,
+                                        uint64_t dst, uint32_t nv, uint32_t (&y)[4],
+                                        uint32_t (&first32)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; j++) first32[j] = 0u;
+  if (nv == 0) return;
+  const uint32_t ib = (uint32_t)(src & 15), oa = (uint32_t)(dst & 15);
+  const uint64_t S0 = src - ib, D0 = dst - oa;
+  const uint64_t last = (src + nv - 1) & ~15ull;
+  auto load_blk = [&](uint32_t i, uint32_t (&v)[4]) {
+    const uint64_t A = S0 + 16ull * i;
+    const u32x4 x = gld<u32x4>(A < last ? A : last);
+    const bool ok = A <= last;
+    v[0] = ok ? x.x : 0u; v[1] = ok ? x.y : 0u; v[2] = ok ? x.z : 0u; v[3] = ok ? x.w : 0u;
+  };
+  uint32_t in_prev[4], cur[4], prev_c[4] = {0u, 0u, 0u, 0u};
+  load_blk(0, in_prev);
+  load_blk(1, cur);
+  const uint32_t nchunk = (nv + 15) / 16;
+  const uint32_t *h1 = K.pow(1);
+  for (uint32_t j = 0; j < nchunk; j++) {
+    uint32_t nxt[4];
+    load_blk(j + 2, nxt);  // in flight during this block's AES and GHASH
+    const int nb = (int)(nv - 16 * j < 16 ? nv - 16 * j : 16);
+    uint32_t in[4], c[4], s[4] = {nonce[0], nonce[1], nonce[2], __builtin_bswap32(ctr0 + j)};
+    funnel(in_prev, cur, ib, in);
+    aes_encrypt<MULTI>(K.rk, tT, l31, s);
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+      in_prev[w] = cur[w];
+      cur[w] = nxt[w];
+      in[w] &= range_mask(0, nb, w);
+      c[w] = (in[w] ^ s[w]) & range_mask(0, nb, w);
+    }
+    const uint32_t(&g)[4] = OPEN ? in : c;
+    ghash_absorb(y, g);
+    gmul<MULTI>(y, h1);
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+      first32[w] = bsel(j == 0, g[w], first32[w]);
+      first32[4 + w] = bsel(j == 1, g[w], first32[4 + w]);
+    }
+    uint32_t blk[4];
+    funnel(prev_c, c, 16 - oa, blk);
+    const uint32_t lo = j == 0 ? oa : 0u;
+    const uint32_t hi = oa + nv - 16 * j < 16 ? oa + nv - 16 * j : 16u;
+    if (lo == 0 && hi == 16) gst<u32x4>(D0 + 16ull * j, u32x4{blk[0], blk[1], blk[2], blk[3]});
+    else store_partial(D0 + 16ull * j, blk, lo, hi);
+#pragma unroll
+    for (int w = 0; w < 4; w++) prev_c[w] = c[w];
+  }
+  if (oa + nv > 16 * nchunk) {  // the last block's tail spills into one more output block
+    const uint32_t zero[4] = {0u, 0u, 0u, 0u};
+    uint32_t blk[4];
+    funnel(prev_c, zero, 16 - oa, blk);
+    store_partial(D0 + 16ull * nchunk, blk, 0, oa + nv - 16 * nchunk);
+  }
+}
+
+// 5 header-protection mask bytes (RFC 9001 5.4.3): AES-ECB(hp, sample)
+template <bool MULTI>
+__device__ __forceinline__ void gcm_hp_mask(const GKey<MULTI> &K, const uint32_t *tT, uint32_t l31,
+                                            const uint32_t (&sample)[4], uint32_t &m0,
+                                            uint32_t &m1) {
+  uint32_t s[4] = {sample[0], sample[1], sample[2], sample[3]};
+  aes_encrypt<MULTI>(K.hrk, tT, l31, s);
+  m0 = s[0];
+  m1 = s[1] & 0xFFu;
+}
+
+// ---------------------------------------------------------------- kernel
+
+struct alignas(16) GRec {
+  uint64_t src, dst;   // payload start in the input / output
+  uint32_t pl, start;  // payload bytes; first flat chunk
+  uint32_t np, kid;    // payload blocks (16 B); keyring index
+  uint32_t nonce[3], pad;
+  uint32_t x[4];       // GHASH accumulator (big-endian words), ds_xor target
+  uint32_t ct32[8];    // ciphertext bytes 0..31 (the header-protection sample)
+};
+
+template <bool MULTI>
+__device__ __forceinline__ GKey<MULTI> key_of(const QGParams &Q, uint32_t kid, const uint32_t *tH) {
+  GKey<MULTI> K;
+  if (MULTI) {
+    const QuicGcmKeyDev *E = Q.keys + kid;
+    K.rk = E->rk; K.hrk = E->hrk; K.iv = E->iv; K.htab = &E->htab[0][0][0];
+  } else {
+    K.rk = Q.rk0; K.hrk = Q.hrk0; K.iv = Q.iv0; K.htab = tH;
+  }
+  return K;
+}
+
+template <bool OPEN, bool MULTI>
+__global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
+  __shared__ uint32_t tT[256 * 32];
+  __shared__ __attribute__((aligned(16))) uint32_t tH[MULTI ? 4 : kGcmPow * 64];
+  __shared__ GRec recs[kGWaves][kGPpw];
+  // stage the replicated T-table and (single key) the GHASH tables
+  for (uint32_t i = threadIdx.x; i < 256 * 32; i += kGBlock) tT[i] = Q.t0[i >> 5];
+  if (!MULTI) {
+    const uint32_t *src = &Q.keys[0].htab[0][0][0];
+    for (uint32_t i = threadIdx.x; i < kGcmPow * 16; i += kGBlock) {
+      const u32x4 v = gld<u32x4>((uint64_t)(src + 4 * i));
+      *(u32x4 *)(tH + 4 * i) = v;
+    }
+  }
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave, l31 = lane & 31;
+  const uint64_t units = ((uint64_t)Q.n + kGPpw - 1) / kGPpw;
+  const uint64_t stride = (uint64_t)gridDim.x * kGWaves;
+  for (uint64_t u = (uint64_t)blockIdx.x * kGWaves + wv; u < units; u += stride) {
+    const uint64_t p64 = u * kGPpw + lane;
+    const bool owner = lane < kGPpw && p64 < Q.n;
+    const uint32_t p = (uint32_t)p64;
+
+    // ---- 1. owner lanes
+    bool live = owner;
+    uint32_t status = 0, len = 0, pno = 0, first = 0, pn_len = 0, hdr = 0, pl = 0, kid = 0;
+    uint64_t src = 0, dst = 0;
+    uint32_t nonce[3] = {0u, 0u, 0u}, rtag[4] = {0u, 0u, 0u, 0u}, y[4] = {0u, 0u, 0u, 0u};
+    if (live && MULTI) {
+      kid = Q.key_id[p];
+      if (kid >= Q.n_keys) {
+        status = kQEKey;
+        live = false;
+        kid = 0;
+      }
+    }
+    const GKey<MULTI> K = key_of<MULTI>(Q, kid, tH);
+    if (live) {
+      src = (uint64_t)Q.in + Q.in_off[p];
+      dst = (uint64_t)Q.out + Q.out_off[p];
+      len = Q.in_len[p];
+      pno = Q.pn_offset[p];
+      uint64_t pn = Q.pn[p];
+      uint32_t pnb[4] = {0u, 0u, 0u, 0u};
+      if (!OPEN) {
+        first = len ? gld<uint8_t>(src) : 0u;
+        pn_len = (first & 3) + 1;
+        hdr = pno + pn_len;
+        if (len == 0 || len > kQMaxPacket || hdr > len || pno + 4 > len) live = false;
+        else pl = len - hdr;
+      } else if (len < 16 || len > kQMaxPacket || pno + 4 + 16 > len) {
+        live = false;
+      } else {
+        uint32_t sample[4], m0, m1;
+        load16(src + pno + 4, src + len, sample);
+        load16(src + len - 16, src + len, rtag);  // before any in-place write
+        gcm_hp_mask<MULTI>(K, tT, l31, sample, m0, m1);
+        const uint32_t pfirst = gld<uint8_t>(src);
+        first = pfirst ^ (m0 & ((pfirst & 0x80) ? 0x0Fu : 0x1Fu));
+        pn_len = (first & 3) + 1;
+        hdr = pno + pn_len;
+        if (hdr > len - 16) {
+          live = false;
+        } else {
+          uint64_t trunc = 0;
+          for (uint32_t i = 0; i < pn_len; i++) {
+            pnb[i] = gld<uint8_t>(src + pno + i) ^ mask_byte(m0, m1, 1 + i);
+            trunc = (trunc << 8) | pnb[i];
+          }
+          pn = decode_pn(pn, trunc, 8 * pn_len);
+          if (Q.pn_out) Q.pn_out[p] = pn;
+          pl = len - 16 - hdr;
+        }
+      }
+      if (!live) status = kQEShort;
+      if (live) {
+        const uint32_t iv[3] = {K.iv[0], K.iv[1], K.iv[2]};
+        quic_nonce_iv(iv, pn, nonce);
+        // AAD = the unprotected header; seal copies it unchanged (protection
+        // is applied in phase 3), open writes the unprotected header
+        for (uint32_t q = 0; q < hdr; q += 16) {
+          uint32_t w[4];
+          load16(src + q, src + hdr, w);
+          if (OPEN) {
+            if (q == 0) set_byte(w, 0, first);
+            for (uint32_t i = 0; i < pn_len; i++) {
+              const uint32_t pos = pno + i;
+              if (pos >= q && pos < q + 16) set_byte(w, pos - q, pnb[i]);
+            }
+          }
+          ghash_absorb(y, w);
+          gmul<MULTI>(y, K.pow(1));
+          if (OPEN || dst != src) store16(dst + q, w, hdr - q < 16 ? hdr - q : 16);
+        }
+      }
+    }
+    const bool coop = live && pl <= kGCoopMax;
+    const uint32_t np = (pl + 15) / 16;
+    // the header's GHASH, placed ahead of the payload blocks
+    if (coop && np) gmul<MULTI>(y, K.pow(np));
+    const uint32_t nblk = coop ? (pl + 63) / 64 : 0u;
+    uint32_t incl = nblk;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const uint32_t t = __shfl_up(incl, d, kWave);
+      if (lane >= (uint32_t)d) incl += t;
+    }
+    const uint32_t start = incl - nblk, T = __shfl(incl, kWave - 1, kWave);
+    if (lane < kGPpw) {
+      GRec &R = recs[wv][lane];
+      R.src = src + hdr;
+      R.dst = dst + hdr;
+      R.pl = pl;
+      R.start = start;
+      R.np = np;
+      R.kid = kid;
+#pragma unroll
+      for (int i = 0; i < 3; i++) R.nonce[i] = nonce[i];
+#pragma unroll
+      for (int i = 0; i < 4; i++) R.x[i] = coop ? y[i] : 0u;
+#pragma unroll
+      for (int i = 0; i < 8; i++) R.ct32[i] = 0u;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+    // ---- 2. cooperative payload pass over the flat chunk space
+    for (uint32_t base = 0; base < T; base += kWave) {
+      const uint32_t f = base + lane;
+      const uint32_t pp = q_locate(start, base, f < T ? f : T - 1);
+      if (f < T) {
+        GRec &R = recs[wv][pp];
+        const GKey<MULTI> KB = key_of<MULTI>(Q, R.kid, tH);
+        const uint32_t b = f - R.start, off0 = 64 * b;
+        const uint32_t nv = R.pl - off0 < 64 ? R.pl - off0 : 64u;
+        const uint32_t rn[3] = {R.nonce[0], R.nonce[1], R.nonce[2]};
+        uint32_t yb[4] = {0u, 0u, 0u, 0u}, f32[8];
+        gcm_run<OPEN, MULTI>(KB, tT, l31, rn, 2 + 4 * b, R.src + off0, R.dst + off0, nv, yb, f32);
+        const uint32_t m = R.np - 4 * b - (nv + 15) / 16;  // payload blocks after this chunk
+        if (m) gmul<MULTI>(yb, KB.pow(m));
+#pragma unroll
+        for (int i = 0; i < 4; i++) atomicXor(&R.x[i], yb[i]);
+        if (!OPEN && b == 0) {
+#pragma unroll
+          for (int i = 0; i < 8; i++) R.ct32[i] = f32[i];
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+    // ---- 3. owner lanes: lengths block, tag, header protection
+    if (!owner) continue;
+    if (!live) {
+      Q.out_len[p] = status;
+      continue;
+    }
+    uint32_t ct32[8];
+    if (coop) {
+#pragma unroll
+      for (int i = 0; i < 4; i++) y[i] = recs[wv][lane].x[i];
+#pragma unroll
+      for (int i = 0; i < 8; i++) ct32[i] = recs[wv][lane].ct32[i];
+    } else {
+      gcm_run<OPEN, MULTI>(K, tT, l31, nonce, 2, src + hdr, dst + hdr, pl, y, ct32);
+    }
+    // lengths block: be64(8 * hdr) || be64(8 * pl)
+    y[1] ^= 8 * hdr;
+    y[2] ^= pl >> 29;
+    y[3] ^= 8 * pl;
+    gmul<MULTI>(y, K.pow(1));
+    uint32_t tag[4] = {nonce[0], nonce[1], nonce[2], __builtin_bswap32(1u)};
+    aes_encrypt<MULTI>(K.rk, tT, l31, tag);  // E(K, J0)
+#pragma unroll
+    for (int w = 0; w < 4; w++) tag[w] ^= __builtin_bswap32(y[w]);
+    if (OPEN) {
+      const bool ok = ((tag[0] ^ rtag[0]) | (tag[1] ^ rtag[1]) | (tag[2] ^ rtag[2]) |
+                       (tag[3] ^ rtag[3])) == 0;
+      Q.out_len[p] = ok ? len - 16 : kQEAuth;
+      continue;
+    }
+    store16(dst + len, tag, 16);
+    // header protection: sample = (ciphertext || tag)[4 - pn_len ..][0..16)
+    const uint32_t so = 4 - pn_len;
+    uint32_t sample[4];
+    if (pl >= so + 16) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) sample[j] = __builtin_amdgcn_alignbyte(ct32[j + 1], ct32[j], so);
+    } else {  // short payload: the sample reaches into the tag
+      const uint32_t t8[8] = {tag[0], tag[1], tag[2], tag[3], 0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int j = 0; j < 4; j++) sample[j] = 0u;
+      for (uint32_t i = 0; i < 16; i++) {
+        const uint32_t k = so + i;
+        const uint32_t bb = k < pl ? byte32(ct32, k) : byte32(t8, k - pl);
+        sample[i >> 2] |= bb << (8 * (i & 3));
+      }
+    }
+    uint32_t m0, m1;
+    gcm_hp_mask<MULTI>(K, tT, l31, sample, m0, m1);
+    gst<uint8_t>(dst, (uint8_t)(first ^ (m0 & ((first & 0x80) ? 0x0Fu : 0x1Fu))));
+    for (uint32_t i = 0; i < pn_len; i++) {
+      const uint32_t bb = gld<uint8_t>(src + pno + i);
+      gst<uint8_t>(dst + pno + i, (uint8_t)(bb ^ mask_byte(m0, m1, 1 + i)));
+    }
+    Q.out_len[p] = len + 16;
+  }
+}
+
+template <bool OPEN, bool MULTI>
+static int launch_gcm(const QGParams *qp, hipStream_t s) {
+  static int per_cu = 0, cus = 0;
+  if (!per_cu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, quic_gcm_kernel<OPEN, MULTI>,
+                                                       kGBlock, 0);
+    if (per_cu < 1) per_cu = 1;
+    if (cus < 1) cus = 1;
+  }
+  const uint64_t waves = ((uint64_t)qp->n + kGPpw - 1) / kGPpw;
+  const uint64_t want = (waves + kGWaves - 1) / kGWaves, cap = (uint64_t)per_cu * cus;
+  const dim3 grid((uint32_t)(want < cap ? want : cap));
+  hipLaunchKernelGGL((quic_gcm_kernel<OPEN, MULTI>), grid, dim3(kGBlock), 0, s, *qp);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+}  // namespace sq
+
+extern "C" int sq_launch_quic_gcm(int open, const sq::QGParams *qp, void *stream) {
+  using namespace sq;
+  if (qp->n == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const bool multi = qp->key_id != nullptr;
+  if (open) return multi ? launch_gcm<true, true>(qp, s) : launch_gcm<true, false>(qp, s);
+  return multi ? launch_gcm<false, true>(qp, s) : launch_gcm<false, false>(qp, s);
+}

@@ -87,10 +87,12 @@ class QuicKey(ctypes.Structure):
 
     @classmethod
     def of(cls, key: bytes, iv: bytes, hp: bytes) -> "QuicKey":
+        """key / hp: 32 bytes (ChaCha20-Poly1305) or 16 (AES-128-GCM)."""
+        assert len(key) in (16, 32) and len(hp) == len(key) and len(iv) == 12
         k = cls()
-        ctypes.memmove(k.key, key, 32)
+        ctypes.memmove(k.key, key, len(key))
         ctypes.memmove(k.iv, iv, 12)
-        ctypes.memmove(k.hp, hp, 32)
+        ctypes.memmove(k.hp, hp, len(hp))
         return k
 
 
@@ -103,6 +105,7 @@ class QuicBatch(ctypes.Structure):
 
 
 QUIC_EKEY, QUIC_ESHORT, QUIC_EAUTH = 0xFFFFFFFF, 0xFFFFFFFE, 0xFFFFFFFD
+QUIC_CHACHA20_POLY1305, QUIC_AES_128_GCM = 0, 1  # SQOBFS_QUIC_* suites
 
 
 class UdpView(ctypes.Structure):
@@ -162,6 +165,7 @@ def lib() -> ctypes.CDLL:
     L.sqobfs_udp_conn_tx_payload.restype = vp
     L.sqobfs_udp_conn_write.argtypes = [vp, u32, u32, vp, vp, u32p]
     L.sqobfs_quic_keyring_create.argtypes = [vp, u32, vp, ctypes.POINTER(vp)]
+    L.sqobfs_quic_keyring_create_suite.argtypes = [vp, u32, u32, vp, ctypes.POINTER(vp)]
     L.sqobfs_quic_keyring_destroy.argtypes = [vp]
     L.sqobfs_quic_keyring_destroy.restype = None
     L.sqobfs_quic_seal.argtypes = [vp, vp, ctypes.POINTER(QuicBatch), vp]
@@ -460,13 +464,16 @@ class UdpConn:
 # ---------------------------------------------------------------- QUIC
 
 class QuicKeyring:
-    """Device copy of per-connection QUIC 1-RTT keys (sqobfs_quic_keyring)."""
+    """Device copy of per-connection QUIC 1-RTT keys (sqobfs_quic_keyring) of
+    one suite: QUIC_CHACHA20_POLY1305 (default) or QUIC_AES_128_GCM."""
 
-    def __init__(self, ctx: Context, keys: list[QuicKey]):
+    def __init__(self, ctx: Context, keys: list[QuicKey], suite: int = QUIC_CHACHA20_POLY1305):
         arr = (QuicKey * len(keys))(*keys)
         h = ctypes.c_void_p()
-        _check(lib().sqobfs_quic_keyring_create(ctx.handle, len(keys), arr, ctypes.byref(h)),
-               "sqobfs_quic_keyring_create")
+        _check(lib().sqobfs_quic_keyring_create_suite(ctx.handle, suite, len(keys), arr,
+                                                      ctypes.byref(h)),
+               "sqobfs_quic_keyring_create_suite")
+        self.suite = suite
         self.handle = h
         self.ctx = ctx
         self.count = len(keys)

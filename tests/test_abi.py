@@ -54,7 +54,7 @@ int main(void){printf("%zu %zu %zu %zu %zu\n", sizeof(sqobfs_batch),
 
 def test_abi_version_and_strerror():
     L = sqobfs.lib()
-    assert L.sqobfs_abi_version() == 2
+    assert L.sqobfs_abi_version() == 3
     for st in (0, -1, -2, -3, -4, -5):
         assert sqobfs.strerror(st) != "unknown status"
 

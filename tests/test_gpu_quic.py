@@ -34,7 +34,8 @@ def _place(sizes, align, gap):
     return np.array(offs, np.uint64), pos + 64
 
 
-def run(ctx, keys, seal, pkts, pn_offsets, pns, key_ids=None, align=1, inplace=False):
+def run(ctx, keys, seal, pkts, pn_offsets, pns, key_ids=None, align=1, inplace=False,
+        suite=0):
     """One device batch; returns (out buffer, out offsets, out_len, pn_out)."""
     import torch
     dev = torch.device("cuda", 0)
@@ -60,7 +61,7 @@ def run(ctx, keys, seal, pkts, pn_offsets, pns, key_ids=None, align=1, inplace=F
              pn_out=t(np.zeros(n, np.uint64)))
     b = sqobfs.quic_batch(n, d_data, d["in_off"], d["in_len"], d_out, d["out_off"], d["out_len"],
                           d["pno"], d["pn"], d["kid"], d["pn_out"])
-    with sqobfs.QuicKeyring(ctx, keys) as kr:
+    with sqobfs.QuicKeyring(ctx, keys, suite) as kr:
         s = torch.cuda.current_stream(dev).cuda_stream
         (sqobfs.quic_seal if seal else sqobfs.quic_open)(ctx, kr, b, s)
         torch.cuda.synchronize(dev)
