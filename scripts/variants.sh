@@ -7,7 +7,6 @@ for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $flags -Iinclude \
     -Ising-quic_amd/csrc -Ising-quic_amd/host -shared -o build/var/lib_$name.so \
-    sing-quic_amd/csrc/sq_kernels.hip sing-quic_amd/csrc/sq_quic.hip sing-quic_amd/csrc/sq_api.hip \
-    sing-quic_amd/host/udp_batch.cpp sing-quic_amd/host/packet_conn.cpp &
+    sing-quic_amd/csrc/*.hip sing-quic_amd/host/*.cpp &
 done
 wait

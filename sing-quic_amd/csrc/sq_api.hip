@@ -496,11 +496,25 @@ void gcm_key(const sqobfs_quic_key &k, sq::QuicGcmKeyDev &d) {
         }
       e[n] = v;
     }
-    for (int n = 0; n < 16; n++) {
-      d.htab[pw][n][0] = (uint32_t)(e[n].hi >> 32);
-      d.htab[pw][n][1] = (uint32_t)e[n].hi;
-      d.htab[pw][n][2] = (uint32_t)(e[n].lo >> 32);
-      d.htab[pw][n][3] = (uint32_t)e[n].lo;
+    for (int n = 0; n < 16; n++) {  // slot n ^ (pw & 15): see gmul in sq_quic_gcm.hip
+      const int sl = n ^ (int)(pw & 15);
+      d.htab[pw][sl][0] = (uint32_t)(e[n].hi >> 32);
+      d.htab[pw][sl][1] = (uint32_t)e[n].hi;
+      d.htab[pw][sl][2] = (uint32_t)(e[n].lo >> 32);
+      d.htab[pw][sl][3] = (uint32_t)e[n].lo;
+    }
+    if (pw == 0) {  // position tables of H: nibble j enters Shoup's Horner
+                    // loop j-th and is multiplied by x^4 (31 - j) more times
+      for (int n = 0; n < 16; n++) {
+        G128 v = e[n];
+        for (int j = 31; j >= 0; j--) {
+          d.hpos[j][n][0] = (uint32_t)(v.hi >> 32);
+          d.hpos[j][n][1] = (uint32_t)v.hi;
+          d.hpos[j][n][2] = (uint32_t)(v.lo >> 32);
+          d.hpos[j][n][3] = (uint32_t)v.lo;
+          for (int k = 0; k < 4; k++) v = g_mulx(v);
+        }
+      }
     }
   }
 }

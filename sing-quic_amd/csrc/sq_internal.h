@@ -94,14 +94,18 @@ struct QParams {
 // AES-128-GCM (TLS_AES_128_GCM_SHA256) connection keys on the device:
 // AES-128 key schedules of the payload key and the header-protection key as
 // little-endian column words (word 4r + c = bytes 4c..4c+3 of round key r),
-// the IV, and 4-bit GHASH tables of H^1 .. H^kGcmPow (Shoup's method; entry
-// n of table k-1 = the nibble polynomial n times H^k, as big-endian words).
+// the IV, per-position tables of H (hpos[j][n] = htab[0][n] x^(4 (31 - j)):
+// X * H is the XOR of hpos[j][nibble j of X], 32 independent lookups, no
+// shifts), and 4-bit GHASH tables of H^1 .. H^kGcmPow (Shoup's method; slot
+// n ^ ((k-1) & 15) of table k-1 = the nibble polynomial n times H^k, as
+// big-endian words).
 constexpr uint32_t kGcmPow = 128;
 struct QuicGcmKeyDev {
   uint32_t rk[44];
   uint32_t hrk[44];
   uint32_t iv[3];
   uint32_t pad;
+  uint32_t hpos[32][16][4];
   uint32_t htab[kGcmPow][16][4];
 };
 

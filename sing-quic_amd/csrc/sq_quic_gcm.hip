@@ -15,13 +15,15 @@
 //
 // gfx950 has no carry-less multiply and no AES instructions, so both run as
 // LDS table lookups, laid out for the LDS banking rules:
-//   * AES rounds: one 1 KiB T-table (T1..T3 are byte rotations of T0),
-//     replicated 32 times with entry x of copy c at word 32x + c.  Lane l
-//     reads copy l & 31, so a ds_read_b32 (two 32-lane halves, bank =
-//     word mod 32) is conflict-free whatever the state bytes are.
-//   * GHASH: Shoup's 4-bit tables (16 entries x 16 B = one 256-byte bank
-//     row), so every ds_read_b128 is conflict-free for lanes multiplying by
-//     the same power.  Tables of H^1 .. H^128 (32 KiB) let each chunk of the
+//   * AES rounds: T0 and T1 = rotl8 T0 (T2, T3 are 16-bit rotations of
+//     them), 32 copies each, as 256 rows of 256 bytes (64 KiB).  Lane l
+//     reads copy l & 31, so a ds_read_b32 (two 32-lane halves, bank = word
+//     mod 32) is conflict-free whatever the state bytes are, and a lookup's
+//     address is one v_perm of the state word.
+//   * GHASH: multiplication by H uses per-position tables (32 nibble
+//     positions x 16 entries x 16 B = 8 KiB): X * H is the XOR of 32
+//     independent ds_read_b128, each in a 256-byte bank row (conflict-free).
+//     Shoup's 4-bit tables of H^1 .. H^128 (32 KiB) let each chunk of the
 //     cooperative pass multiply its partial GHASH by the power that places it
 //     in the packet: GHASH is linear, so the packet's value is the XOR of
 //     the chunk partials times H^m (ds_xor_b32 into the packet's record) --
@@ -50,7 +52,13 @@
 
 namespace sq {
 
-constexpr uint32_t kGBlock = 512;
+#ifndef SQ_GBLOCK
+#define SQ_GBLOCK 1024
+#endif
+#ifndef SQ_GNB
+#define SQ_GNB 2
+#endif
+constexpr uint32_t kGBlock = SQ_GBLOCK;  // 16 waves: one block per CU (128 KiB of LDS)
 constexpr uint32_t kGWaves = kGBlock / kWave;
 constexpr uint32_t kGPpw = 16;                 // packets per wave
 constexpr uint32_t kGCoopMax = 16 * kGcmPow;   // 2048 B
@@ -72,50 +80,80 @@ __device__ __forceinline__ void round_key(const uint32_t *rk, int r, uint32_t (&
   }
 }
 
-// T0[x] from this lane's copy of the replicated table
-__device__ __forceinline__ uint32_t tlook(const uint32_t *tT, uint32_t x, uint32_t l31) {
-  return tT[(x << 5) | l31];
+// The T-table image in LDS: 256 rows of 256 bytes; row x = 32 copies of
+// T0[x] then 32 copies of T1[x] = rotl8 T0[x].  Lane l reads column l & 31,
+// so a ds_read_b32 (bank = word mod 32 per 32-lane half) is conflict-free.
+// The byte offset of (row = byte r of s, this lane's column) is one v_perm:
+// byte 0 = the lane's column offset lo = 4 (l & 31), byte 1 = s.byte r.
+__device__ __forceinline__ uint32_t trow(uint32_t s, uint32_t lo, int r) {
+  return __builtin_amdgcn_perm(lo, s, 0x0C0C0004u | ((uint32_t)r << 8));
+}
+__device__ __forceinline__ uint32_t t0at(const uint32_t *tT, uint32_t a) {
+  return *(const uint32_t *)((const char *)tT + a);
+}
+__device__ __forceinline__ uint32_t t1at(const uint32_t *tT, uint32_t a) {
+  return *(const uint32_t *)((const char *)tT + a + 128);
 }
 
 // FIPS-197 cipher on one block held as 4 little-endian column words.
-// Round: column c = T0[s_c.b0] ^ rotl8 T0[s_c+1.b1] ^ rotl16 T0[s_c+2.b2] ^
-// rotl24 T0[s_c+3.b3] ^ rk (ShiftRows folded into the byte picks); the last
-// round takes the S-box byte (byte 1 of T0) instead.
-template <bool MULTI>
-__device__ __forceinline__ void aes_encrypt(const uint32_t *rk, const uint32_t *tT, uint32_t l31,
-                                            uint32_t (&s)[4]) {
+// Round: column c = T0[s_c.b0] ^ T1[s_c+1.b1] ^ rotl16(T0[s_c+2.b2] ^
+// T1[s_c+3.b3]) ^ rk (T2 = rotl16 T0, T3 = rotl16 T1; ShiftRows folded into
+// the byte picks); the last round takes the S-box byte (T0 byte 1, T1 bytes
+// 2 and 3) instead.
+template <bool MULTI, int NB>
+__device__ __forceinline__ void aes_encrypt_n(const uint32_t *rk, const uint32_t *tT, uint32_t lo,
+                                              uint32_t (&s)[NB][4]) {
   uint32_t k[4];
   round_key<MULTI>(rk, 0, k);
 #pragma unroll
-  for (int c = 0; c < 4; c++) s[c] ^= k[c];
+  for (int q = 0; q < NB; q++)
+#pragma unroll
+    for (int c = 0; c < 4; c++) s[q][c] ^= k[c];
 #pragma unroll
   for (int r = 1; r < 10; r++) {
     round_key<MULTI>(rk, r, k);
-    uint32_t t[4];
+    uint32_t t[NB][4];
 #pragma unroll
-    for (int c = 0; c < 4; c++) {
-      const uint32_t a0 = tlook(tT, s[c] & 0xFFu, l31);
-      const uint32_t a1 = tlook(tT, (s[(c + 1) & 3] >> 8) & 0xFFu, l31);
-      const uint32_t a2 = tlook(tT, (s[(c + 2) & 3] >> 16) & 0xFFu, l31);
-      const uint32_t a3 = tlook(tT, s[(c + 3) & 3] >> 24, l31);
-      t[c] = a0 ^ rotl(a1, 8) ^ rotl(a2, 16) ^ rotl(a3, 24) ^ k[c];
-    }
+    for (int q = 0; q < NB; q++)
 #pragma unroll
-    for (int c = 0; c < 4; c++) s[c] = t[c];
+      for (int c = 0; c < 4; c++) {
+        const uint32_t a0 = t0at(tT, trow(s[q][c], lo, 0));
+        const uint32_t a1 = t1at(tT, trow(s[q][(c + 1) & 3], lo, 1));
+        const uint32_t a2 = t0at(tT, trow(s[q][(c + 2) & 3], lo, 2));
+        const uint32_t a3 = t1at(tT, trow(s[q][(c + 3) & 3], lo, 3));
+        t[q][c] = a0 ^ a1 ^ rotl(a2 ^ a3, 16) ^ k[c];
+      }
+#pragma unroll
+    for (int q = 0; q < NB; q++)
+#pragma unroll
+      for (int c = 0; c < 4; c++) s[q][c] = t[q][c];
   }
   round_key<MULTI>(rk, 10, k);
-  uint32_t t[4];
+  uint32_t t[NB][4];
 #pragma unroll
-  for (int c = 0; c < 4; c++) {
-    const uint32_t a0 = tlook(tT, s[c] & 0xFFu, l31);
-    const uint32_t a1 = tlook(tT, (s[(c + 1) & 3] >> 8) & 0xFFu, l31);
-    const uint32_t a2 = tlook(tT, (s[(c + 2) & 3] >> 16) & 0xFFu, l31);
-    const uint32_t a3 = tlook(tT, s[(c + 3) & 3] >> 24, l31);
-    t[c] = (((a0 >> 8) & 0xFFu) | (a1 & 0xFF00u) | ((a2 << 8) & 0xFF0000u) |
-            ((a3 << 16) & 0xFF000000u)) ^ k[c];
-  }
+  for (int q = 0; q < NB; q++)
 #pragma unroll
-  for (int c = 0; c < 4; c++) s[c] = t[c];
+    for (int c = 0; c < 4; c++) {
+      const uint32_t a0 = t0at(tT, trow(s[q][c], lo, 0));
+      const uint32_t a1 = t0at(tT, trow(s[q][(c + 1) & 3], lo, 1));
+      const uint32_t a2 = t1at(tT, trow(s[q][(c + 2) & 3], lo, 2));
+      const uint32_t a3 = t1at(tT, trow(s[q][(c + 3) & 3], lo, 3));
+      t[q][c] = (((a0 >> 8) & 0xFFu) | (a1 & 0xFF00u) | (a2 & 0xFF0000u) | (a3 & 0xFF000000u)) ^
+                k[c];
+    }
+#pragma unroll
+  for (int q = 0; q < NB; q++)
+#pragma unroll
+    for (int c = 0; c < 4; c++) s[q][c] = t[q][c];
+}
+
+template <bool MULTI>
+__device__ __forceinline__ void aes_encrypt(const uint32_t *rk, const uint32_t *tT, uint32_t lo,
+                                            uint32_t (&s)[4]) {
+  uint32_t b[1][4] = {{s[0], s[1], s[2], s[3]}};
+  aes_encrypt_n<MULTI, 1>(rk, tT, lo, b);
+#pragma unroll
+  for (int c = 0; c < 4; c++) s[c] = b[0][c];
 }
 
 // ---------------------------------------------------------------- GHASH
@@ -125,8 +163,11 @@ __device__ __forceinline__ void aes_encrypt(const uint32_t *rk, const uint32_t *
 // consumed from the low end of the 128-bit integer, each step multiplying
 // the accumulator by x^4 (shift right 4, fold the 4 bits shifted out back
 // with the reduction polynomial: rem * 0x1C20 carry-less, at bits 112..127).
+// Entry n of table k-1 is stored in slot n ^ sw, sw = (k-1) & 15: lanes
+// multiplying by different powers then read different 16-byte slots of the
+// bank row for the same nibble (no ds_read_b128 bank conflicts).
 template <bool GLOBAL>
-__device__ __forceinline__ void gmul(uint32_t (&x)[4], const uint32_t *tab) {
+__device__ __forceinline__ void gmul(uint32_t (&x)[4], const uint32_t *tab, uint32_t sw) {
   uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
   uint32_t w = x[3], w2 = x[2], w1 = x[1], w0 = x[0];
   // one word (8 nibbles) per iteration, kept rolled: unrolled, the compiler
@@ -144,10 +185,40 @@ __device__ __forceinline__ void gmul(uint32_t (&x)[4], const uint32_t *tab) {
         z0 = (z0 >> 4) ^ (rem << 28) ^ (rem << 27) ^ (rem << 26) ^ (rem << 21);
       }
       u32x4 e;
-      if (GLOBAL) e = gld<u32x4>((uint64_t)(tab + 4 * nib));
-      else e = *(const u32x4 *)(tab + 4 * nib);
+      if (GLOBAL) e = gld<u32x4>((uint64_t)(tab + 4 * (nib ^ sw)));
+      else e = *(const u32x4 *)(tab + 4 * (nib ^ sw));
       z0 ^= e.x; z1 ^= e.y; z2 ^= e.z; z3 ^= e.w;
     }
+    w = w2;
+    w2 = w1;
+    w1 = w0;
+  }
+  x[0] = z0; x[1] = z1; x[2] = z2; x[3] = z3;
+}
+
+// x <- x * H with the position tables of H: XOR of pos[j][nibble j of x]
+// over the 32 nibbles (from the low end of the 128-bit integer).  No
+// dependency between the lookups; one word's 8 lookups at a time (the
+// scheduling barrier keeps the compiler from hoisting all 32 entries into
+// 128 VGPRs).
+template <bool GLOBAL>
+__device__ __forceinline__ void gmul_pos(uint32_t (&x)[4], const uint32_t *pos) {
+  uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
+  uint32_t w = x[3], w2 = x[2], w1 = x[1], w0 = x[0];
+  const char *base = (const char *)pos;
+  // one word (8 lookups) per iteration, kept rolled: unrolled, the compiler
+  // hoists all 32 entries into 128 VGPRs
+#pragma unroll 1
+  for (int i = 0; i < 4; i++) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint32_t off = (((w >> (4 * j)) & 0xFu) << 4) + 256u * j;
+      u32x4 e;
+      if (GLOBAL) e = gld<u32x4>((uint64_t)(base + off));
+      else e = *(const u32x4 *)(base + off);
+      z0 ^= e.x; z1 ^= e.y; z2 ^= e.z; z3 ^= e.w;
+    }
+    base += 8 * 256;
     w = w2;
     w2 = w1;
     w1 = w0;
@@ -165,8 +236,12 @@ __device__ __forceinline__ void ghash_absorb(uint32_t (&y)[4], const uint32_t (&
 // IV, and the GHASH tables (table k-1 = H^k).
 template <bool MULTI>
 struct GKey {
-  const uint32_t *rk, *hrk, *iv, *htab;
+  const uint32_t *rk, *hrk, *iv, *hpos, *htab;
   __device__ __forceinline__ const uint32_t *pow(uint32_t k) const { return htab + 64 * (k - 1); }
+  // x <- x * H^k (k = 1 .. kGcmPow)
+  __device__ __forceinline__ void mul_pow(uint32_t (&x)[4], uint32_t k) const {
+    gmul<MULTI>(x, pow(k), (k - 1) & 15u);
+  }
 };
 
 // ---------------------------------------------------------------- payload
@@ -177,7 +252,7 @@ struct GKey {
 // one block of read-ahead), as payload_pass in sq_quic.hip.  In place
 // (src == dst) works.  first32 = ciphertext bytes 0..31 (zero past nv).
 template <bool OPEN, bool MULTI>
-__device__ __forceinline__ void gcm_run(const GKey<MULTI> &K, const uint32_t *tT, uint32_t l31,
+__device__ __forceinline__ void gcm_run(const GKey<MULTI> &K, const uint32_t *tT, uint32_t tcol,
                                         const uint32_t (&nonce)[3], uint32_t ctr0, uint64_t src,
                                         uint64_t dst, uint32_t nv, uint32_t (&y)[4],
                                         uint32_t (&first32)[8]) {
@@ -193,28 +268,18 @@ __device__ __forceinline__ void gcm_run(const GKey<MULTI> &K, const uint32_t *tT
     const bool ok = A <= last;
     v[0] = ok ? x.x : 0u; v[1] = ok ? x.y : 0u; v[2] = ok ? x.z : 0u; v[3] = ok ? x.w : 0u;
   };
-  uint32_t in_prev[4], cur[4], prev_c[4] = {0u, 0u, 0u, 0u};
-  load_blk(0, in_prev);
-  load_blk(1, cur);
+  // two counter blocks per iteration: their AES rounds interleave, so each
+  // round has 32 independent T-table reads in flight instead of 16
+  uint32_t A[4], Bq[4], C[4], prev_c[4] = {0u, 0u, 0u, 0u};
+  load_blk(0, A);
+  load_blk(1, Bq);
+  load_blk(2, C);
   const uint32_t nchunk = (nv + 15) / 16;
-  const uint32_t *h1 = K.pow(1);
-  for (uint32_t j = 0; j < nchunk; j++) {
-    uint32_t nxt[4];
-    load_blk(j + 2, nxt);  // in flight during this block's AES and GHASH
-    const int nb = (int)(nv - 16 * j < 16 ? nv - 16 * j : 16);
-    uint32_t in[4], c[4], s[4] = {nonce[0], nonce[1], nonce[2], __builtin_bswap32(ctr0 + j)};
-    funnel(in_prev, cur, ib, in);
-    aes_encrypt<MULTI>(K.rk, tT, l31, s);
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-      in_prev[w] = cur[w];
-      cur[w] = nxt[w];
-      in[w] &= range_mask(0, nb, w);
-      c[w] = (in[w] ^ s[w]) & range_mask(0, nb, w);
-    }
+  // one output block: GHASH, header-protection sample, realigned store
+  auto finish = [&](uint32_t j, const uint32_t (&in)[4], const uint32_t (&c)[4]) {
     const uint32_t(&g)[4] = OPEN ? in : c;
     ghash_absorb(y, g);
-    gmul<MULTI>(y, h1);
+    gmul_pos<MULTI>(y, K.hpos);
 #pragma unroll
     for (int w = 0; w < 4; w++) {
       first32[w] = bsel(j == 0, g[w], first32[w]);
@@ -228,7 +293,56 @@ __device__ __forceinline__ void gcm_run(const GKey<MULTI> &K, const uint32_t *tT
     else store_partial(D0 + 16ull * j, blk, lo, hi);
 #pragma unroll
     for (int w = 0; w < 4; w++) prev_c[w] = c[w];
+  };
+#if SQ_GNB == 1
+  for (uint32_t j = 0; j < nchunk; j++) {
+    uint32_t D[4];
+    load_blk(j + 3, D);
+    uint32_t in[4], c[4];
+    uint32_t s1[4] = {nonce[0], nonce[1], nonce[2], __builtin_bswap32(ctr0 + j)};
+    funnel(A, Bq, ib, in);
+    aes_encrypt<MULTI>(K.rk, tT, tcol, s1);
+    const int nb = (int)nv - 16 * (int)j;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+      in[w] &= range_mask(0, nb, w);
+      c[w] = (in[w] ^ s1[w]) & range_mask(0, nb, w);
+      A[w] = Bq[w];
+      Bq[w] = C[w];
+      C[w] = D[w];
+    }
+    finish(j, in, c);
   }
+#else
+  for (uint32_t j = 0; j < nchunk; j += 2) {
+    uint32_t D[4], E[4];
+    load_blk(j + 3, D);  // in flight during this pair's AES and GHASH
+    load_blk(j + 4, E);
+    uint32_t in[2][4], c[2][4];
+    uint32_t s2[2][4] = {{nonce[0], nonce[1], nonce[2], __builtin_bswap32(ctr0 + j)},
+                         {nonce[0], nonce[1], nonce[2], __builtin_bswap32(ctr0 + j + 1)}};
+    funnel(A, Bq, ib, in[0]);
+    funnel(Bq, C, ib, in[1]);
+    aes_encrypt_n<MULTI, 2>(K.rk, tT, tcol, s2);
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      const int nb = (int)nv - 16 * (int)(j + q);  // valid bytes (may be <= 0)
+#pragma unroll
+      for (int w = 0; w < 4; w++) {
+        in[q][w] &= range_mask(0, nb, w);
+        c[q][w] = (in[q][w] ^ s2[q][w]) & range_mask(0, nb, w);
+      }
+    }
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+      A[w] = C[w];
+      Bq[w] = D[w];
+      C[w] = E[w];
+    }
+    finish(j, in[0], c[0]);
+    if (j + 1 < nchunk) finish(j + 1, in[1], c[1]);
+  }
+#endif
   if (oa + nv > 16 * nchunk) {  // the last block's tail spills into one more output block
     const uint32_t zero[4] = {0u, 0u, 0u, 0u};
     uint32_t blk[4];
@@ -239,11 +353,11 @@ __device__ __forceinline__ void gcm_run(const GKey<MULTI> &K, const uint32_t *tT
 
 // 5 header-protection mask bytes (RFC 9001 5.4.3): AES-ECB(hp, sample)
 template <bool MULTI>
-__device__ __forceinline__ void gcm_hp_mask(const GKey<MULTI> &K, const uint32_t *tT, uint32_t l31,
+__device__ __forceinline__ void gcm_hp_mask(const GKey<MULTI> &K, const uint32_t *tT, uint32_t tcol,
                                             const uint32_t (&sample)[4], uint32_t &m0,
                                             uint32_t &m1) {
   uint32_t s[4] = {sample[0], sample[1], sample[2], sample[3]};
-  aes_encrypt<MULTI>(K.hrk, tT, l31, s);
+  aes_encrypt<MULTI>(K.hrk, tT, tcol, s);
   m0 = s[0];
   m1 = s[1] & 0xFFu;
 }
@@ -260,33 +374,41 @@ struct alignas(16) GRec {
 };
 
 template <bool MULTI>
-__device__ __forceinline__ GKey<MULTI> key_of(const QGParams &Q, uint32_t kid, const uint32_t *tH) {
+__device__ __forceinline__ GKey<MULTI> key_of(const QGParams &Q, uint32_t kid, const uint32_t *tP,
+                                              const uint32_t *tH) {
   GKey<MULTI> K;
   if (MULTI) {
     const QuicGcmKeyDev *E = Q.keys + kid;
-    K.rk = E->rk; K.hrk = E->hrk; K.iv = E->iv; K.htab = &E->htab[0][0][0];
+    K.rk = E->rk; K.hrk = E->hrk; K.iv = E->iv;
+    K.hpos = &E->hpos[0][0][0]; K.htab = &E->htab[0][0][0];
   } else {
-    K.rk = Q.rk0; K.hrk = Q.hrk0; K.iv = Q.iv0; K.htab = tH;
+    K.rk = Q.rk0; K.hrk = Q.hrk0; K.iv = Q.iv0; K.hpos = tP; K.htab = tH;
   }
   return K;
 }
 
 template <bool OPEN, bool MULTI>
 __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
-  __shared__ uint32_t tT[256 * 32];
+  __shared__ uint32_t tT[256 * 64];
+  __shared__ __attribute__((aligned(16))) uint32_t tP[MULTI ? 4 : 32 * 64];
   __shared__ __attribute__((aligned(16))) uint32_t tH[MULTI ? 4 : kGcmPow * 64];
   __shared__ GRec recs[kGWaves][kGPpw];
-  // stage the replicated T-table and (single key) the GHASH tables
-  for (uint32_t i = threadIdx.x; i < 256 * 32; i += kGBlock) tT[i] = Q.t0[i >> 5];
+  // stage the T-table image and (single key) the GHASH tables
+  for (uint32_t i = threadIdx.x; i < 256 * 64; i += kGBlock) {
+    const uint32_t v = Q.t0[i >> 6];
+    tT[i] = (i & 32) ? rotl(v, 8) : v;
+  }
   if (!MULTI) {
-    const uint32_t *src = &Q.keys[0].htab[0][0][0];
-    for (uint32_t i = threadIdx.x; i < kGcmPow * 16; i += kGBlock) {
+    const uint32_t *src = &Q.keys[0].hpos[0][0][0];  // hpos then htab, contiguous
+    for (uint32_t i = threadIdx.x; i < (32 + kGcmPow) * 16; i += kGBlock) {
       const u32x4 v = gld<u32x4>((uint64_t)(src + 4 * i));
-      *(u32x4 *)(tH + 4 * i) = v;
+      if (i < 32 * 16) *(u32x4 *)(tP + 4 * i) = v;
+      else *(u32x4 *)(tH + 4 * (i - 32 * 16)) = v;
     }
   }
   __syncthreads();
-  const uint32_t lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave, l31 = lane & 31;
+  const uint32_t lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+  const uint32_t tcol = 4 * (lane & 31);  // this lane's T-table column (byte offset)
   const uint64_t units = ((uint64_t)Q.n + kGPpw - 1) / kGPpw;
   const uint64_t stride = (uint64_t)gridDim.x * kGWaves;
   for (uint64_t u = (uint64_t)blockIdx.x * kGWaves + wv; u < units; u += stride) {
@@ -307,7 +429,7 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
         kid = 0;
       }
     }
-    const GKey<MULTI> K = key_of<MULTI>(Q, kid, tH);
+    const GKey<MULTI> K = key_of<MULTI>(Q, kid, tP, tH);
     if (live) {
       src = (uint64_t)Q.in + Q.in_off[p];
       dst = (uint64_t)Q.out + Q.out_off[p];
@@ -327,7 +449,7 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
         uint32_t sample[4], m0, m1;
         load16(src + pno + 4, src + len, sample);
         load16(src + len - 16, src + len, rtag);  // before any in-place write
-        gcm_hp_mask<MULTI>(K, tT, l31, sample, m0, m1);
+        gcm_hp_mask<MULTI>(K, tT, tcol, sample, m0, m1);
         const uint32_t pfirst = gld<uint8_t>(src);
         first = pfirst ^ (m0 & ((pfirst & 0x80) ? 0x0Fu : 0x1Fu));
         pn_len = (first & 3) + 1;
@@ -362,7 +484,7 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
             }
           }
           ghash_absorb(y, w);
-          gmul<MULTI>(y, K.pow(1));
+          gmul_pos<MULTI>(y, K.hpos);
           if (OPEN || dst != src) store16(dst + q, w, hdr - q < 16 ? hdr - q : 16);
         }
       }
@@ -370,7 +492,7 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
     const bool coop = live && pl <= kGCoopMax;
     const uint32_t np = (pl + 15) / 16;
     // the header's GHASH, placed ahead of the payload blocks
-    if (coop && np) gmul<MULTI>(y, K.pow(np));
+    if (coop && np) K.mul_pow(y, np);
     const uint32_t nblk = coop ? (pl + 63) / 64 : 0u;
     uint32_t incl = nblk;
 #pragma unroll
@@ -402,14 +524,14 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
       const uint32_t pp = q_locate(start, base, f < T ? f : T - 1);
       if (f < T) {
         GRec &R = recs[wv][pp];
-        const GKey<MULTI> KB = key_of<MULTI>(Q, R.kid, tH);
+        const GKey<MULTI> KB = key_of<MULTI>(Q, R.kid, tP, tH);
         const uint32_t b = f - R.start, off0 = 64 * b;
         const uint32_t nv = R.pl - off0 < 64 ? R.pl - off0 : 64u;
         const uint32_t rn[3] = {R.nonce[0], R.nonce[1], R.nonce[2]};
         uint32_t yb[4] = {0u, 0u, 0u, 0u}, f32[8];
-        gcm_run<OPEN, MULTI>(KB, tT, l31, rn, 2 + 4 * b, R.src + off0, R.dst + off0, nv, yb, f32);
+        gcm_run<OPEN, MULTI>(KB, tT, tcol, rn, 2 + 4 * b, R.src + off0, R.dst + off0, nv, yb, f32);
         const uint32_t m = R.np - 4 * b - (nv + 15) / 16;  // payload blocks after this chunk
-        if (m) gmul<MULTI>(yb, KB.pow(m));
+        if (m) KB.mul_pow(yb, m);
 #pragma unroll
         for (int i = 0; i < 4; i++) atomicXor(&R.x[i], yb[i]);
         if (!OPEN && b == 0) {
@@ -433,15 +555,15 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
 #pragma unroll
       for (int i = 0; i < 8; i++) ct32[i] = recs[wv][lane].ct32[i];
     } else {
-      gcm_run<OPEN, MULTI>(K, tT, l31, nonce, 2, src + hdr, dst + hdr, pl, y, ct32);
+      gcm_run<OPEN, MULTI>(K, tT, tcol, nonce, 2, src + hdr, dst + hdr, pl, y, ct32);
     }
     // lengths block: be64(8 * hdr) || be64(8 * pl)
     y[1] ^= 8 * hdr;
     y[2] ^= pl >> 29;
     y[3] ^= 8 * pl;
-    gmul<MULTI>(y, K.pow(1));
+    gmul_pos<MULTI>(y, K.hpos);
     uint32_t tag[4] = {nonce[0], nonce[1], nonce[2], __builtin_bswap32(1u)};
-    aes_encrypt<MULTI>(K.rk, tT, l31, tag);  // E(K, J0)
+    aes_encrypt<MULTI>(K.rk, tT, tcol, tag);  // E(K, J0)
 #pragma unroll
     for (int w = 0; w < 4; w++) tag[w] ^= __builtin_bswap32(y[w]);
     if (OPEN) {
@@ -468,7 +590,7 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
       }
     }
     uint32_t m0, m1;
-    gcm_hp_mask<MULTI>(K, tT, l31, sample, m0, m1);
+    gcm_hp_mask<MULTI>(K, tT, tcol, sample, m0, m1);
     gst<uint8_t>(dst, (uint8_t)(first ^ (m0 & ((first & 0x80) ? 0x0Fu : 0x1Fu))));
     for (uint32_t i = 0; i < pn_len; i++) {
       const uint32_t bb = gld<uint8_t>(src + pno + i);
