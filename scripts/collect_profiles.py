@@ -32,8 +32,8 @@ if os.path.exists(b):
 q = os.path.join(src, "quic")
 if os.path.isdir(q):
     os.makedirs(f"{dst}/quic", exist_ok=True)
-    for root, _, files in os.walk(q):
-        for f in files:
-            if f.endswith("kernel_stats.csv"):
-                shutil.copy(os.path.join(root, f), f"{dst}/quic/kernel_stats_quic.csv")
+    for sub, name in (("kt", "aes_128_gcm"), ("kt2", "chacha20_poly1305")):
+        f = os.path.join(q, sub, "kt_kernel_stats.csv")
+        if os.path.exists(f):
+            shutil.copy(f, f"{dst}/quic/kernel_stats_{name}.csv")
     shutil.copy(os.path.join(q, "bench_quic.json"), f"{dst}/quic/bench_quic.json")
