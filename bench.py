@@ -436,10 +436,15 @@ def main():
     if args.e2e and rank == 0:
         out["e2e"] = e2e_rate(torch, sqobfs, ctx, kr, kind, min(n, 1 << 18), L or 758)
     if args.quic and rank == 0:
-        out["quic"] = quic_rate(torch, sqobfs, ctx, dev, max(5, args.steps))
+        out["quic"] = {
+            "chacha20_poly1305": quic_rate(torch, sqobfs, ctx, dev, max(5, args.steps), suite=0),
+            "aes_128_gcm": quic_rate(torch, sqobfs, ctx, dev, max(5, args.steps), suite=1)}
     if args.udp and rank == 0:
         out["udp_e2e"] = [udp_rate(sqobfs, ctx, kr, kind, L or 758, batch=bt)
-                          for bt in (64, 256, 1024)]
+                          for bt in (64, 256, 1024)] + \
+                         [udp_rate(sqobfs, ctx, kr, kind, L or 758, batch=bt,
+                                   offload=sqobfs.UDP_TX_GSO | sqobfs.UDP_RX_GRO)
+                          for bt in (256, 1024)]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:
@@ -493,19 +498,25 @@ def e2e_rate(torch, sqobfs, ctx, kr, kind, n, L):
     return res
 
 
-def quic_rate(torch, sqobfs, ctx, dev, steps, n=1 << 20, payload=1350, cpu_seconds=2.0):
+def quic_rate(torch, sqobfs, ctx, dev, steps, n=1 << 20, payload=1350, cpu_seconds=2.0,
+              suite=0):
     """QUIC 1-RTT packet protection: seal and open
     of n short-header packets (1 + 8-byte DCID + 2-byte packet number +
-    `payload` bytes), dense in HBM, one key.  Algorithmic bytes per packet:
-    seal reads len, writes len + 16; open reads len + 16, writes len.
-    Parity: sampled packets against the oracle.  CPU leg: the oracle's
-    threaded or_quic_seal_batch on a bounded sample."""
+    `payload` bytes), dense in HBM, one key; suite 0 = ChaCha20-Poly1305,
+    1 = AES-128-GCM.  Algorithmic bytes per packet: seal reads len, writes
+    len + 16; open reads len + 16, writes len.  Parity: sampled packets
+    against the oracle.  CPU legs on bounded samples: the oracle's threaded
+    or_quic_seal_batch2 (scalar C port), and OpenSSL libcrypto
+    (oracle/ossl_quic.c: AES-NI / vector code, the class of code quic-go
+    runs)."""
+    import ctypes
     import numpy as np
     import oracle_lib as ol
     hdr = 11
     ln = hdr + payload
+    kl = 16 if suite else 32
     rng = np.random.Generator(np.random.PCG64(12))
-    key, iv, hp = (rng.integers(0, 256, m, dtype=np.uint8).tobytes() for m in (32, 12, 32))
+    key, iv, hp = (rng.integers(0, 256, m, dtype=np.uint8).tobytes() for m in (kl, 12, kl))
     in_off = torch.arange(n, device=dev, dtype=torch.int64) * ln
     out_off = torch.arange(n, device=dev, dtype=torch.int64) * (ln + 16)
     g = torch.Generator(device=dev)
@@ -526,8 +537,9 @@ def quic_rate(torch, sqobfs, ctx, dev, steps, n=1 << 20, payload=1350, cpu_secon
     pn_out = torch.zeros(n, device=dev, dtype=torch.int64)
     s = torch.cuda.current_stream(dev).cuda_stream
     res = {"packets": n, "packet_bytes": ln, "payload_bytes": payload,
-           "cipher": "AEAD_CHACHA20_POLY1305 + ChaCha20 header protection (RFC 9001)"}
-    with sqobfs.QuicKeyring(ctx, [sqobfs.QuicKey.of(key, iv, hp)]) as kr:
+           "cipher": ("AEAD_AES_128_GCM + AES header protection (RFC 9001)" if suite else
+                      "AEAD_CHACHA20_POLY1305 + ChaCha20 header protection (RFC 9001)")}
+    with sqobfs.QuicKeyring(ctx, [sqobfs.QuicKey.of(key, iv, hp)], suite) as kr:
         bs = sqobfs.quic_batch(n, data, in_off, lens, sealed, out_off, olen, pno, pn)
         bo = sqobfs.quic_batch(n, sealed, out_off, slens, opened, in_off, olen2, pno, largest,
                                pn_out=pn_out)
@@ -555,11 +567,11 @@ def quic_rate(torch, sqobfs, ctx, dev, steps, n=1 << 20, payload=1350, cpu_secon
     ok = bool((olen.cpu().numpy() == ln + 16).all() and (olen2.cpu().numpy() == ln).all()
               and (pn_out.cpu().numpy() == pn.cpu().numpy()).all())
     for k, i in enumerate(idx):
-        want, _ = ol.quic_seal(key, iv, hp, 1000 + i, d[k].tobytes(), 9)
+        want, _ = ol.quic_seal(key, iv, hp, 1000 + i, d[k].tobytes(), 9, suite=suite)
         ok = ok and sl[k].tobytes() == want and op[k].tobytes() == d[k].tobytes()
     res["parity_spot_check"] = ok
-    # CPU leg: oracle (scalar C restatement), threaded
-    m = 65536
+    # CPU legs, threaded: the oracle (scalar C restatement) and OpenSSL
+    m = 65536 if suite == 0 else 8192
     threads = max(1, min(16, len(os.sched_getaffinity(0))))
     cin = np.tile(d[0], m)
     ci_off = np.arange(m, dtype=np.uint64) * ln
@@ -568,29 +580,45 @@ def quic_rate(torch, sqobfs, ctx, dev, steps, n=1 << 20, payload=1350, cpu_secon
     c_len = np.full(m, ln, np.uint32)
     c_pno = np.full(m, 9, np.uint16)
     c_pn = np.arange(m, dtype=np.uint64)
-    L_ = ol.lib()
-    reps = 0
-    t0 = time.perf_counter()
-    while reps < 1 or time.perf_counter() - t0 < cpu_seconds:
-        L_.or_quic_seal_batch(key, iv, hp, cin.ctypes.data, ci_off.ctypes.data, c_len.ctypes.data,
-                              c_pno.ctypes.data, c_pn.ctypes.data, m, cout.ctypes.data,
-                              co_off.ctypes.data, threads)
-        reps += 1
-    dt = time.perf_counter() - t0
+    args_ = (key, iv, hp, cin.ctypes.data, ci_off.ctypes.data, c_len.ctypes.data,
+             c_pno.ctypes.data, c_pn.ctypes.data, m, cout.ctypes.data, co_off.ctypes.data, threads)
+
+    def timed(fn):
+        reps, t0 = 0, time.perf_counter()
+        while reps < 1 or time.perf_counter() - t0 < cpu_seconds:
+            assert fn(suite, *args_) == 0
+            reps += 1
+        return reps, time.perf_counter() - t0
+    reps, dt = timed(ol.lib().or_quic_seal_batch2)
     res["cpu_baseline"] = {"value": round(reps * m * payload / dt / 2**30, 3), "unit": "GiB/s",
                            "cores": threads, "kind": "port",
                            "sample": f"{reps} x {m} packets seal, oracle/oracle.c "
-                                     "or_quic_seal_batch (scalar C, not OpenSSL)"}
+                                     "or_quic_seal_batch2 (scalar C restatement)"}
+    so = os.path.join(REPO, "oracle", "libossl_quic.so")
+    if os.path.exists(so):
+        L2 = ctypes.CDLL(so)
+        L2.ossl_quic_seal_batch.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 8 + \
+            [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        m_before = m
+        reps, dt = timed(L2.ossl_quic_seal_batch)
+        chk = ol.quic_seal(key, iv, hp, 0, d[0].tobytes(), 9, suite=suite)[0]
+        res["cpu_openssl"] = {"value": round(reps * m_before * payload / dt / 2**30, 3),
+                              "unit": "GiB/s", "cores": threads,
+                              "matches_oracle": cout[:ln + 16].tobytes() == chk,
+                              "sample": f"{reps} x {m_before} packets seal, OpenSSL libcrypto "
+                                        "EVP (oracle/ossl_quic.c), one context per thread"}
     return res
 
 
-def udp_rate(sqobfs, ctx, kr, kind, L, seconds=3.0, batch=256, nsock=4):
+def udp_rate(sqobfs, ctx, kr, kind, L, seconds=3.0, batch=256, nsock=4, offload=0):
     """Loopback UDP end to end through the batched socket layer
     (sqobfs_udp_conn): a client endpoint obfuscates a batch on the GPU
     (device salts) and sends it with sendmmsg to `nsock` server sockets; the
     server endpoint receives the batch with recvmmsg fan-in and deobfuscates
     it on the GPU.  One thread, batch after batch, so the rate is the sum of
-    both sides' costs (GPU round trips + syscalls + loopback stack)."""
+    both sides' costs (GPU round trips + syscalls + loopback stack).
+    offload: UDP_TX_GSO on the client and / or UDP_RX_GRO on the server
+    (runs of batch / nsock datagrams go to each server socket)."""
     import socket
     import numpy as np
     rng = np.random.Generator(np.random.PCG64(11))
@@ -602,11 +630,13 @@ def udp_rate(sqobfs, ctx, kr, kind, L, seconds=3.0, batch=256, nsock=4):
         return s
     srv_s = [sock() for _ in range(nsock)]  # fan-in, as hysteria port hopping
     cli_s = sock()
-    to = [sqobfs.Addr.of("127.0.0.1", srv_s[i % nsock].getsockname()[1]) for i in range(batch)]
+    to = [sqobfs.Addr.of("127.0.0.1", srv_s[i * nsock // batch].getsockname()[1])
+          for i in range(batch)]
     arr = (sqobfs.Addr * batch)(*to)
     lens = np.full(batch, L, np.uint32)
     srv = sqobfs.UdpConn(ctx, kr, [s.fileno() for s in srv_s], slots=batch)
     cli = sqobfs.UdpConn(ctx, kr, [cli_s.fileno()], slots=batch)
+    on = cli.set_offload(offload & sqobfs.UDP_TX_GSO) | srv.set_offload(offload & sqobfs.UDP_RX_GRO)
     for i in range(batch):
         cli.tx_payload(i)[:L] = rng.integers(0, 256, L, dtype=np.uint8)
     import ctypes
@@ -663,6 +693,7 @@ def udp_rate(sqobfs, ctx, kr, kind, L, seconds=3.0, batch=256, nsock=4):
     for s in srv_s + [cli_s]:
         s.close()
     return {"payload_bytes": L, "batch": batch, "server_sockets": nsock, "batches": batches,
+            "offload": {"asked": offload, "in_effect": on},
             "datagrams_per_s": round(moved / dt), "GiB_s_payload": round(moved * L / dt / 2**30, 4),
             "lost": lost,
             "sockets_only_datagrams_per_s": round(raw / dt_raw),

@@ -355,6 +355,26 @@ uint8_t *sqobfs_udp_conn_tx_payload(sqobfs_udp_conn *c, uint32_t i);
 int sqobfs_udp_conn_write(sqobfs_udp_conn *c, uint32_t fd_index, uint32_t n,
                           const uint32_t *len, const sqobfs_addr *to, uint32_t *sent);
 
+/* UDP segmentation offloads (Linux UDP_SEGMENT / UDP_GRO).
+ * sqobfs_udp_send_gso: as sqobfs_udp_send, but consecutive datagrams to the
+ * same address whose lengths are equal (the last of a run may be shorter)
+ * go out as ONE message with a UDP_SEGMENT control message (at most 64
+ * datagrams / 65,000 bytes per message); the kernel (or the NIC) cuts it
+ * into the original datagrams.  -EIO / -EINVAL when the socket or route
+ * cannot segment. */
+int sqobfs_udp_send_gso(int fd, const uint8_t *base, const uint64_t *off, const uint32_t *len,
+                        const sqobfs_addr *to, uint32_t n, uint32_t *sent);
+
+#define SQOBFS_UDP_TX_GSO 1u /* conn_write sends runs with UDP_SEGMENT */
+#define SQOBFS_UDP_RX_GRO 2u /* conn_read receives coalesced datagrams (UDP_GRO) */
+/* Enable offloads on an endpoint.  With RX_GRO the receive region is used
+ * as 64 KiB buffers that each hold up to 64 coalesced datagrams, so the
+ * view's off[] are no longer slot-aligned (needs slots >= 64 and
+ * slots * slot_bytes >= 64 KiB).  TX_GSO falls back to one datagram per
+ * message if the first GSO send is refused.  Returns the flags in effect
+ * (>= 0) or SQ_EINVAL. */
+int sqobfs_udp_conn_set_offload(sqobfs_udp_conn *c, uint32_t flags);
+
 #ifdef __cplusplus
 }
 #endif

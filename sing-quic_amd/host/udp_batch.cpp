@@ -20,6 +20,7 @@
 #include <errno.h>
 #include <hip/hip_runtime.h>
 #include <netinet/in.h>
+#include <netinet/udp.h>
 #include <poll.h>
 #include <string.h>
 #include <sys/socket.h>
@@ -35,6 +36,9 @@ namespace {
 
 constexpr uint32_t kMmsgChunk = 256;     // messages per recvmmsg / sendmmsg call
 constexpr uint32_t kFairPerRound = 64;   // per socket per fan-in round
+constexpr uint32_t kGsoMaxSegs = 64;     // UDP_MAX_SEGMENTS of older kernels
+constexpr uint32_t kGsoMaxBytes = 65000; // one GSO send stays below 64 KiB of IP payload
+constexpr uint32_t kGroBuf = 65536;      // one coalesced receive
 
 void to_sockaddr(const sqobfs_addr &a, sockaddr_storage *ss, socklen_t *sl) {
   memset(ss, 0, sizeof *ss);
@@ -89,6 +93,7 @@ struct sqobfs_udp_conn {
   uint64_t *tx_in_off = nullptr, *tx_out_off = nullptr;
   uint32_t *tx_len = nullptr, *tx_out_len = nullptr;
   std::vector<uint32_t> tx_wire_len;
+  uint32_t offload = 0;  // SQOBFS_UDP_TX_GSO | SQOBFS_UDP_RX_GRO in effect
 };
 
 namespace {
@@ -98,6 +103,122 @@ int launch_sync(sqobfs_udp_conn *c, int dir, const sqobfs_batch &b) {
   void *s = sqobfs_stream(c->ctx);
   const int st = sqobfs_launch(c->ctx, c->kr, dir, &b, s);
   return st != SQ_OK ? st : sqobfs_sync(c->ctx, s);
+}
+
+// sendmmsg of msg[0..n), waiting while the socket buffer is full.  Returns
+// the number of messages handed to the kernel, or -errno if none was.
+int send_all(int fd, mmsghdr *msg, uint32_t n, uint32_t *done_msgs) {
+  uint32_t done = 0;
+  while (done < n) {
+    const int m = sendmmsg(fd, msg + done, n - done, 0);
+    if (m < 0) {
+      if (errno == EINTR) continue;
+      if (errno == EAGAIN || errno == EWOULDBLOCK) {
+        pollfd p = {fd, POLLOUT, 0};
+        if (poll(&p, 1, -1) < 0 && errno != EINTR) break;
+        continue;
+      }
+      *done_msgs = done;
+      return -errno;
+    }
+    done += (uint32_t)m;
+  }
+  *done_msgs = done;
+  return SQ_OK;
+}
+
+// (Re)set the receive batch offsets to the fixed slot layout.
+void rx_fixed_offsets(sqobfs_udp_conn *c) {
+  for (uint32_t i = 0; i < c->slots; i++) {
+    c->rx_in_off[i] = (uint64_t)i * c->slot_bytes;
+    c->rx_out_off[i] = (uint64_t)i * c->slot_bytes + c->S;
+  }
+}
+
+// Fan-in receive with UDP GRO: recvmmsg into 64 KiB buffers laid over the
+// rx region; a coalesced message holds several datagrams of gso_size bytes
+// (the last may be shorter, cmsg UDP_GRO).  Writes the batch offsets.
+int recv_gro(sqobfs_udp_conn *c, int timeout_ms, uint32_t *count) {
+  *count = 0;
+  const uint32_t nfds = (uint32_t)c->fds.size();
+  std::vector<pollfd> pfd(nfds);
+  for (uint32_t i = 0; i < nfds; i++) pfd[i] = {c->fds[i], POLLIN, 0};
+  int r;
+  do {
+    r = poll(pfd.data(), nfds, timeout_ms);
+  } while (r < 0 && errno == EINTR);
+  if (r < 0) return -errno;
+  if (r == 0) return SQ_OK;
+  const uint64_t region = (uint64_t)c->slots * c->slot_bytes;
+  // at most kGsoMaxSegs datagrams per buffer, so the batch arrays (slots
+  // entries) always have room for a whole buffer
+  const uint32_t nbuf = std::max<uint32_t>(
+      1, std::min<uint64_t>(region / kGroBuf, c->slots / kGsoMaxSegs));
+  std::vector<mmsghdr> msg(nbuf);
+  std::vector<iovec> iov(nbuf);
+  std::vector<sockaddr_storage> ss(nbuf);
+  std::vector<uint64_t> ctl(nbuf * 8);
+  std::vector<bool> live(nfds, true);
+  uint32_t got = 0, used = 0, nlive = nfds;
+  int first_err = 0;
+  while (used < nbuf && nlive > 0) {
+    for (uint32_t f = 0; f < nfds && used < nbuf; f++) {
+      if (!live[f]) continue;
+      const uint32_t want = nbuf - used;
+      for (uint32_t k = 0; k < want; k++) {
+        iov[k].iov_base = c->rx + (size_t)(used + k) * kGroBuf;
+        iov[k].iov_len = kGroBuf;
+        memset(&msg[k], 0, sizeof msg[k]);
+        msg[k].msg_hdr.msg_iov = &iov[k];
+        msg[k].msg_hdr.msg_iovlen = 1;
+        msg[k].msg_hdr.msg_name = &ss[k];
+        msg[k].msg_hdr.msg_namelen = sizeof ss[k];
+        msg[k].msg_hdr.msg_control = &ctl[8 * k];
+        msg[k].msg_hdr.msg_controllen = 8 * sizeof(uint64_t);
+      }
+      const int m = recvmmsg(c->fds[f], msg.data(), want, MSG_DONTWAIT, nullptr);
+      if (m < 0) {
+        if (errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR && !first_err)
+          first_err = -errno;
+        if (errno != EINTR) {
+          live[f] = false;
+          nlive--;
+        }
+        continue;
+      }
+      for (int k = 0; k < m; k++) {
+        const uint32_t total = msg[k].msg_len;
+        uint32_t seg = total;
+        for (cmsghdr *cm = CMSG_FIRSTHDR(&msg[k].msg_hdr); cm;
+             cm = CMSG_NXTHDR(&msg[k].msg_hdr, cm))
+          if (cm->cmsg_level == SOL_UDP && cm->cmsg_type == UDP_GRO) {
+            int v;
+            memcpy(&v, CMSG_DATA(cm), sizeof v);
+            if (v > 0) seg = (uint32_t)v;
+          }
+        const uint64_t base = (uint64_t)(used + k) * kGroBuf;
+        sqobfs_addr from;
+        from_sockaddr(ss[k], &from);
+        for (uint32_t o = 0; o < total || (total == 0 && o == 0); o += seg ? seg : 1) {
+          const uint32_t l = std::min(seg, total - o);
+          c->rx_in_off[got] = base + o;
+          c->rx_out_off[got] = base + o + c->S;
+          c->rx_len[got] = l;
+          c->rx_fd[got] = (uint16_t)f;
+          c->rx_from[got] = from;
+          got++;
+          if (total == 0) break;
+        }
+      }
+      used += (uint32_t)m;
+      if ((uint32_t)m < want) {
+        live[f] = false;
+        nlive--;
+      }
+    }
+  }
+  *count = got;
+  return got == 0 && first_err ? first_err : SQ_OK;
 }
 
 }  // namespace
@@ -209,6 +330,93 @@ int sqobfs_udp_send(int fd, const uint8_t *base, const uint64_t *off, const uint
   return SQ_OK;
 }
 
+int sqobfs_udp_send_gso(int fd, const uint8_t *base, const uint64_t *off, const uint32_t *len,
+                        const sqobfs_addr *to, uint32_t n, uint32_t *sent) {
+  if (sent) *sent = 0;
+  if (n == 0) return SQ_OK;
+  if (!base || !off || !len || !to || !sent) return SQ_EINVAL;
+  std::vector<mmsghdr> msg;
+  std::vector<iovec> iov(n);
+  std::vector<sockaddr_storage> ss;
+  std::vector<uint64_t> ctl;
+  std::vector<uint32_t> first;  // first datagram of each message
+  msg.reserve(n);
+  ss.reserve(n);
+  first.reserve(n + 1);
+  constexpr size_t kCtlWords = (CMSG_SPACE(sizeof(uint16_t)) + 7) / 8;  // 24 bytes
+  ctl.reserve(kCtlWords * n);
+  for (uint32_t i = 0; i < n;) {
+    // a run to one destination: every datagram gso bytes, the last <= gso
+    const uint32_t gso = len[i];
+    uint32_t j = i + 1, bytes = gso;
+    while (j < n && j - i < kGsoMaxSegs && gso > 0 && len[j] <= gso && len[j] > 0 &&
+           bytes + len[j] <= kGsoMaxBytes && memcmp(&to[j], &to[i], sizeof to[i]) == 0) {
+      bytes += len[j];
+      j++;
+      if (len[j - 1] < gso) break;
+    }
+    for (uint32_t k = i; k < j; k++) {
+      iov[k].iov_base = const_cast<uint8_t *>(base + off[k]);
+      iov[k].iov_len = len[k];
+    }
+    mmsghdr h;
+    memset(&h, 0, sizeof h);
+    ss.emplace_back();
+    socklen_t sl;
+    to_sockaddr(to[i], &ss.back(), &sl);
+    h.msg_hdr.msg_name = &ss.back();
+    h.msg_hdr.msg_namelen = sl;
+    h.msg_hdr.msg_iov = &iov[i];
+    h.msg_hdr.msg_iovlen = j - i;
+    if (j - i > 1) {  // UDP_SEGMENT: the kernel cuts the message into gso-byte datagrams
+      ctl.resize(ctl.size() + kCtlWords, 0);  // within the reservation: no reallocation
+      h.msg_hdr.msg_control = &ctl[ctl.size() - kCtlWords];
+      h.msg_hdr.msg_controllen = CMSG_SPACE(sizeof(uint16_t));
+      cmsghdr *cm = CMSG_FIRSTHDR(&h.msg_hdr);
+      cm->cmsg_level = SOL_UDP;
+      cm->cmsg_type = UDP_SEGMENT;
+      cm->cmsg_len = CMSG_LEN(sizeof(uint16_t));
+      const uint16_t g = (uint16_t)gso;
+      memcpy(CMSG_DATA(cm), &g, sizeof g);
+    }
+    msg.push_back(h);
+    first.push_back(i);
+    i = j;
+  }
+  first.push_back(n);
+  uint32_t done_msgs = 0;
+  int st = SQ_OK;
+  for (uint32_t m0 = 0; m0 < msg.size() && st == SQ_OK;) {
+    const uint32_t k_n = std::min<uint32_t>((uint32_t)msg.size() - m0, kMmsgChunk);
+    uint32_t d = 0;
+    st = send_all(fd, msg.data() + m0, k_n, &d);
+    done_msgs = m0 + d;
+    m0 += k_n;
+  }
+  *sent = first[done_msgs];
+  return st;
+}
+
+int sqobfs_udp_conn_set_offload(sqobfs_udp_conn *c, uint32_t flags) {
+  if (!c || (flags & ~(SQOBFS_UDP_TX_GSO | SQOBFS_UDP_RX_GRO))) return SQ_EINVAL;
+  std::lock_guard<std::mutex> lr(c->rx_mu);
+  std::lock_guard<std::mutex> lt(c->tx_mu);
+  uint32_t on = flags & SQOBFS_UDP_TX_GSO;  // probed on the first send
+  const bool gro_fits = c->slots >= kGsoMaxSegs && (uint64_t)c->slots * c->slot_bytes >= kGroBuf;
+  const int want_gro = (flags & SQOBFS_UDP_RX_GRO) && gro_fits ? 1 : 0;
+  bool gro_ok = true;
+  for (int fd : c->fds)
+    if (setsockopt(fd, SOL_UDP, UDP_GRO, &want_gro, sizeof want_gro) != 0) gro_ok = false;
+  if (want_gro && gro_ok) on |= SQOBFS_UDP_RX_GRO;
+  if (!(on & SQOBFS_UDP_RX_GRO)) {
+    const int zero = 0;
+    for (int fd : c->fds) (void)setsockopt(fd, SOL_UDP, UDP_GRO, &zero, sizeof zero);
+    rx_fixed_offsets(c);
+  }
+  c->offload = on;
+  return (int)on;
+}
+
 int sqobfs_udp_conn_open(sqobfs_ctx *ctx, const sqobfs_keyring *kr, const int *fds,
                          uint32_t nfds, uint32_t slots, uint32_t slot_bytes,
                          sqobfs_udp_conn **out) {
@@ -254,9 +462,8 @@ int sqobfs_udp_conn_open(sqobfs_ctx *ctx, const sqobfs_keyring *kr, const int *f
   c->rx_fd.resize(slots);
   c->rx_from.resize(slots);
   c->tx_wire_len.resize(slots);
+  rx_fixed_offsets(c);  // wire at the slot start, payload decoded in place behind it
   for (uint32_t i = 0; i < slots; i++) {
-    c->rx_in_off[i] = (uint64_t)i * slot_bytes;       // wire at the slot start
-    c->rx_out_off[i] = (uint64_t)i * slot_bytes + S;  // payload decoded in place
     c->tx_in_off[i] = (uint64_t)i * slot_bytes + S;   // payload behind S of headroom
     c->tx_out_off[i] = (uint64_t)i * slot_bytes;      // wire = salt || payload, in place
   }
@@ -275,9 +482,11 @@ int sqobfs_udp_conn_read(sqobfs_udp_conn *c, int timeout_ms, sqobfs_udp_view *ou
   std::lock_guard<std::mutex> lk(c->rx_mu);
   memset(out, 0, sizeof *out);
   uint32_t n = 0;
-  int st = sqobfs_udp_recv(c->fds.data(), (uint32_t)c->fds.size(), c->rx, c->slot_bytes, 0,
-                           c->slots, timeout_ms, c->rx_len, c->rx_fd.data(),
-                           c->rx_from.data(), &n);
+  int st = (c->offload & SQOBFS_UDP_RX_GRO)
+               ? recv_gro(c, timeout_ms, &n)
+               : sqobfs_udp_recv(c->fds.data(), (uint32_t)c->fds.size(), c->rx, c->slot_bytes,
+                                 0, c->slots, timeout_ms, c->rx_len, c->rx_fd.data(),
+                                 c->rx_from.data(), &n);
   if (st != SQ_OK || n == 0) return st;
   sqobfs_batch b;
   memset(&b, 0, sizeof b);
@@ -328,6 +537,15 @@ int sqobfs_udp_conn_write(sqobfs_udp_conn *c, uint32_t fd_index, uint32_t n,
   b.out_len = c->tx_out_len;
   const int st = launch_sync(c, SQOBFS_OBFUSCATE, b);
   if (st != SQ_OK) return st;
+  if (c->offload & SQOBFS_UDP_TX_GSO) {
+    const int g = sqobfs_udp_send_gso(c->fds[fd_index], c->tx, c->tx_out_off,
+                                      c->tx_wire_len.data(), to, n, sent);
+    // no UDP GSO on this socket / route: fall back to one datagram per message
+    if (g == SQ_OK || *sent > 0 || (g != -EIO && g != -EINVAL && g != -ENOPROTOOPT &&
+                                    g != -EOPNOTSUPP))
+      return g;
+    c->offload &= ~SQOBFS_UDP_TX_GSO;
+  }
   return sqobfs_udp_send(c->fds[fd_index], c->tx, c->tx_out_off, c->tx_wire_len.data(), to, n,
                          sent);
 }

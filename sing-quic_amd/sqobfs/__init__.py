@@ -157,6 +157,9 @@ def lib() -> ctypes.CDLL:
     u16p, u32p = ctypes.POINTER(ctypes.c_uint16), ctypes.POINTER(ctypes.c_uint32)
     L.sqobfs_udp_recv.argtypes = [vp, u32, vp, u32, u32, u32, i32, vp, vp, vp, u32p]
     L.sqobfs_udp_send.argtypes = [i32, vp, vp, vp, vp, u32, u32p]
+    L.sqobfs_udp_send_gso.argtypes = [i32, vp, vp, vp, vp, u32, u32p]
+    L.sqobfs_udp_conn_set_offload.argtypes = [vp, u32]
+    L.sqobfs_udp_conn_set_offload.restype = i32
     L.sqobfs_udp_conn_open.argtypes = [vp, vp, vp, u32, u32, u32, ctypes.POINTER(vp)]
     L.sqobfs_udp_conn_close.argtypes = [vp]
     L.sqobfs_udp_conn_close.restype = None
@@ -389,13 +392,18 @@ def udp_recv(fds: list[int], slots: np.ndarray, slot_bytes: int, headroom: int, 
     return n, ln[:n].copy(), fi[:n].copy(), list(addrs)[:n]
 
 
-def udp_send(fd: int, base: np.ndarray, off, lens, to: list[Addr]) -> int:
+UDP_TX_GSO, UDP_RX_GRO = 1, 2  # sqobfs_udp_conn_set_offload flags
+
+
+def udp_send(fd: int, base: np.ndarray, off, lens, to: list[Addr], gso: bool = False) -> int:
+    """sqobfs_udp_send (sendmmsg), or sqobfs_udp_send_gso (UDP_SEGMENT runs)."""
     off = np.asarray(off, dtype=np.uint64)
     lens = np.asarray(lens, dtype=np.uint32)
     arr = (Addr * max(len(to), 1))(*to)
     sent = ctypes.c_uint32(0)
-    _check(lib().sqobfs_udp_send(fd, _ptr(base), _ptr(off), _ptr(lens), arr, len(to),
-                                 ctypes.byref(sent)), "sqobfs_udp_send")
+    fn = lib().sqobfs_udp_send_gso if gso else lib().sqobfs_udp_send
+    _check(fn(fd, _ptr(base), _ptr(off), _ptr(lens), arr, len(to), ctypes.byref(sent)),
+           "sqobfs_udp_send_gso" if gso else "sqobfs_udp_send")
     return sent.value
 
 
@@ -424,6 +432,13 @@ class UdpConn:
 
     def __exit__(self, *exc):
         self.close()
+
+    def set_offload(self, flags: int) -> int:
+        """sqobfs_udp_conn_set_offload: UDP_TX_GSO | UDP_RX_GRO; returns the
+        flags in effect."""
+        r = lib().sqobfs_udp_conn_set_offload(self.handle, flags)
+        _check(min(r, 0), "sqobfs_udp_conn_set_offload")
+        return r
 
     def read(self, timeout_ms: int = 1000):
         """[(payload bytes, fd_index, Addr)] of one received, decoded batch."""
