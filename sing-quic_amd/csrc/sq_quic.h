@@ -77,4 +77,38 @@ __device__ __forceinline__ uint32_t q_locate(uint32_t start, uint32_t b0, uint32
   return pp < 0 ? 0u : (uint32_t)pp;
 }
 
+// The first 32 bytes of a packet of len >= 1 bytes at src (zero past the
+// end), as 8 little-endian words.  One round of loads (at most four aligned
+// blocks, all independent) yields the first byte, the packet number and any
+// header of up to 32 bytes, instead of a chain of dependent byte loads.
+__device__ __forceinline__ void load_head32(uint64_t src, uint32_t len, uint32_t (&hd)[8]) {
+  const uint64_t end = src + len;
+  uint32_t a[4], b[4] = {0u, 0u, 0u, 0u};
+  load16(src, end, a);
+  if (len > 16) load16(src + 16, end, b);
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    hd[j] = a[j];
+    hd[4 + j] = b[j];
+  }
+}
+
+// byte k of the packet: from hd when k < 32, else loaded
+__device__ __forceinline__ uint32_t head_byte(const uint32_t (&hd)[8], uint64_t src, uint32_t k) {
+  return k < 32 ? byte32(hd, k) : (uint32_t)gld<uint8_t>(src + k);
+}
+
+// header block at q (a multiple of 16) with the bytes past hdr zeroed (the
+// AAD's zero padding): from hd when q < 32, else loaded
+__device__ __forceinline__ void head_block(const uint32_t (&hd)[8], uint64_t src, uint32_t q,
+                                           uint32_t hdr, uint32_t (&w)[4]) {
+  if (q < 32) {
+    const int nb = (int)(hdr - q < 16 ? hdr - q : 16);
+#pragma unroll
+    for (int j = 0; j < 4; j++) w[j] = bsel(q == 0, hd[j], hd[4 + j]) & range_mask(0, nb, j);
+  } else {
+    load16(src + q, src + hdr, w);
+  }
+}
+
 }  // namespace sq

@@ -421,6 +421,7 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
     uint32_t status = 0, len = 0, pno = 0, first = 0, pn_len = 0, hdr = 0, pl = 0, kid = 0;
     uint64_t src = 0, dst = 0;
     uint32_t nonce[3] = {0u, 0u, 0u}, rtag[4] = {0u, 0u, 0u, 0u}, y[4] = {0u, 0u, 0u, 0u};
+    uint32_t hd[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, pnw = 0;  // packet bytes 0..31; seal: pn bytes
     if (live && MULTI) {
       kid = Q.key_id[p];
       if (kid >= Q.n_keys) {
@@ -438,19 +439,25 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
       uint64_t pn = Q.pn[p];
       uint32_t pnb[4] = {0u, 0u, 0u, 0u};
       if (!OPEN) {
-        first = len ? gld<uint8_t>(src) : 0u;
+        if (len) load_head32(src, len, hd);
+        first = hd[0] & 0xFFu;
         pn_len = (first & 3) + 1;
         hdr = pno + pn_len;
-        if (len == 0 || len > kQMaxPacket || hdr > len || pno + 4 > len) live = false;
-        else pl = len - hdr;
+        if (len == 0 || len > kQMaxPacket || hdr > len || pno + 4 > len) {
+          live = false;
+        } else {
+          pl = len - hdr;
+          for (uint32_t i = 0; i < pn_len; i++) pnw |= head_byte(hd, src, pno + i) << (8 * i);
+        }
       } else if (len < 16 || len > kQMaxPacket || pno + 4 + 16 > len) {
         live = false;
       } else {
         uint32_t sample[4], m0, m1;
         load16(src + pno + 4, src + len, sample);
         load16(src + len - 16, src + len, rtag);  // before any in-place write
+        load_head32(src, len, hd);
         gcm_hp_mask<MULTI>(K, tT, tcol, sample, m0, m1);
-        const uint32_t pfirst = gld<uint8_t>(src);
+        const uint32_t pfirst = hd[0] & 0xFFu;
         first = pfirst ^ (m0 & ((pfirst & 0x80) ? 0x0Fu : 0x1Fu));
         pn_len = (first & 3) + 1;
         hdr = pno + pn_len;
@@ -459,7 +466,7 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
         } else {
           uint64_t trunc = 0;
           for (uint32_t i = 0; i < pn_len; i++) {
-            pnb[i] = gld<uint8_t>(src + pno + i) ^ mask_byte(m0, m1, 1 + i);
+            pnb[i] = head_byte(hd, src, pno + i) ^ mask_byte(m0, m1, 1 + i);
             trunc = (trunc << 8) | pnb[i];
           }
           pn = decode_pn(pn, trunc, 8 * pn_len);
@@ -475,7 +482,7 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
         // is applied in phase 3), open writes the unprotected header
         for (uint32_t q = 0; q < hdr; q += 16) {
           uint32_t w[4];
-          load16(src + q, src + hdr, w);
+          head_block(hd, src, q, hdr, w);
           if (OPEN) {
             if (q == 0) set_byte(w, 0, first);
             for (uint32_t i = 0; i < pn_len; i++) {
@@ -593,7 +600,7 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
     gcm_hp_mask<MULTI>(K, tT, tcol, sample, m0, m1);
     gst<uint8_t>(dst, (uint8_t)(first ^ (m0 & ((first & 0x80) ? 0x0Fu : 0x1Fu))));
     for (uint32_t i = 0; i < pn_len; i++) {
-      const uint32_t bb = gld<uint8_t>(src + pno + i);
+      const uint32_t bb = (pnw >> (8 * i)) & 0xFFu;
       gst<uint8_t>(dst + pno + i, (uint8_t)(bb ^ mask_byte(m0, m1, 1 + i)));
     }
     Q.out_len[p] = len + 16;
