@@ -247,6 +247,27 @@ def cpu_baseline(seconds: float):
             "cpu_seconds": round((t_ob + t_de) * threads, 2)}
 
 
+def host_info(torch, dev) -> dict:
+    """Where the line was measured (nproc, CPU model, ROCm)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    rocm = None
+    for path in ("/opt/rocm/.info/version", "/opt/rocm/.info/version-dev"):
+        if os.path.exists(path):
+            rocm = open(path).read().strip()
+            break
+    return {"gpu": torch.cuda.get_device_name(dev), "cpu_model": model,
+            "nproc": os.cpu_count(), "cpu_affinity": len(os.sched_getaffinity(0)),
+            "rocm": rocm, "torch": torch.__version__}
+
+
 def load_traffic(config: str, kernel_bytes: float):
     """HBM bytes per launch from the committed PMC pass (profiles/)."""
     path = os.path.join(REPO, "profiles", f"pmc_{config}.json")
@@ -425,6 +446,7 @@ def main():
             "kernel": f"obfs_kernel<{kind},{direction},{int(n_psk > 1)}> ({sqobfs.build_info()})",
             "kernel_avg_us": round(kern_avg_ms * 1e3, 2),
             "kernel_min_us": round(kern_ms[0] * 1e3, 2),
+            "kernel_median_us": round(kern_ms[len(kern_ms) // 2] * 1e3, 2),
             "algorithmic_bytes_per_launch": alg_bytes,
             "bytes_rule": "obfuscate 2L+2S per packet (2L+S with device salts), "
                           "deobfuscate 2L+S (SURVEY.md 8(d))",
@@ -447,6 +469,8 @@ def main():
                           for bt in (256, 1024)]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        out["host"] = host_info(torch, dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
     kr.close()
