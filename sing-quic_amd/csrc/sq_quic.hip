@@ -40,7 +40,13 @@ namespace sq {
 constexpr uint32_t kQBlock = 256;
 constexpr uint32_t kQWaves = kQBlock / kWave;
 constexpr uint32_t kQPpw = 16;          // packets per wave
-constexpr uint32_t kQCoopMax = 2048;    // payloads up to this size take the cooperative pass
+#ifndef SQ_QCOOPMAX
+#define SQ_QCOOPMAX 2048
+#endif
+#ifndef SQ_QMINW
+#define SQ_QMINW 0  // >0: ask for this many waves per SIMD (register cap)
+#endif
+constexpr uint32_t kQCoopMax = SQ_QCOOPMAX;  // payloads up to this size take the cooperative pass
 constexpr uint32_t kQMaxBlk = kQPpw * (kQCoopMax / 64);
 
 // ---------------------------------------------------------------- Poly1305
@@ -357,7 +363,12 @@ __device__ __forceinline__ void coop_block(const QuicKeyDev &K, QRec &R, uint32_
 // Payloads above kQCoopMax bytes are walked by their owner lane in phase 3
 // (the sequential payload_pass), so any length works.
 template <bool OPEN, bool MULTI>
-__global__ __launch_bounds__(kQBlock) void quic_kernel(const QParams Q) {
+#if SQ_QMINW
+__global__ __launch_bounds__(kQBlock, SQ_QMINW) void quic_kernel
+#else
+__global__ __launch_bounds__(kQBlock) void quic_kernel
+#endif
+(const QParams Q) {
   __shared__ QRec recs[kQWaves][kQPpw];
   __shared__ uint32_t parts[kQWaves][kQMaxBlk][5];
   const uint32_t lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
