@@ -452,9 +452,9 @@ class UdpConn:
         ln = np.ctypeslib.as_array((ctypes.c_uint32 * v.count).from_address(v.len))
         fi = np.ctypeslib.as_array((ctypes.c_uint16 * v.count).from_address(v.fd_index))
         addrs = (Addr * v.count).from_address(v.from_)
-        for i in range(v.count):
+        for i in range(v.count):  # copies: the next read reuses the endpoint's arrays
             out.append((ctypes.string_at(v.base + int(off[i]), int(ln[i])), int(fi[i]),
-                        addrs[i]))
+                        Addr.from_buffer_copy(addrs[i])))
         return out
 
     def tx_payload(self, i: int) -> np.ndarray:

@@ -172,3 +172,37 @@ def test_conn_offloads_gso_gro(ctx, kind):
         assert [g[0] for g in _read_n(srv, 2)] == pay
     for s in (srv_sock, cli_sock, spy):
         s.close()
+
+
+def test_conn_gro_fan_in_mixed_sources(ctx):
+    """GRO receive over two server sockets, from a GSO endpoint and from a
+    plain reference-format sender at once: every datagram is tagged with its
+    socket and source, per-source order holds, and payloads decode exactly."""
+    kind = SALAMANDER
+    rng = np.random.Generator(np.random.PCG64(123))
+    srv = [_sock(), _sock()]
+    cli_sock, plain = _sock(), _sock()
+    with sqobfs.Keyring(ctx, kind, [PSK]) as kr, \
+            sqobfs.UdpConn(ctx, kr, [s.fileno() for s in srv], slots=512) as conn, \
+            sqobfs.UdpConn(ctx, kr, [cli_sock.fileno()], slots=256) as cli:
+        assert conn.set_offload(sqobfs.UDP_RX_GRO) in (0, sqobfs.UDP_RX_GRO)
+        cli.set_offload(sqobfs.UDP_TX_GSO)
+        for burst in range(4):
+            pay_g = [rng.integers(0, 256, 900, dtype=np.uint8).tobytes() for _ in range(120)]
+            to = [Addr.of(*srv[0 if i < 60 else 1].getsockname()) for i in range(120)]
+            pay_p = [rng.integers(0, 256, int(rng.integers(1, 1300)), dtype=np.uint8).tobytes()
+                     for _ in range(30)]
+            assert cli.write(0, pay_g, to) == 120
+            for p in pay_p:  # reference WriteTo: salt || payload ^ key
+                salt = rng.integers(0, 256, 8, dtype=np.uint8).tobytes()
+                plain.sendto(ol.salamander_write(PSK, salt, p)[0], srv[1].getsockname())
+            got = _read_n(conn, 150)
+            by_src = {}
+            for payload, fi, addr in got:
+                by_src.setdefault((fi, addr.pair()), []).append(payload)
+            c = cli_sock.getsockname()
+            assert by_src[(0, c)] == pay_g[:60]
+            assert by_src[(1, c)] == pay_g[60:]
+            assert by_src[(1, plain.getsockname())] == pay_p
+    for s in srv + [cli_sock, plain]:
+        s.close()
