@@ -71,6 +71,11 @@ constexpr int kPktPerWave = SQ_PPW;
 #ifndef SQ_TIMELINE
 #define SQ_TIMELINE 0
 #endif
+// Wave priority experiment (timing builds): 1 = raise the priority of waves
+// once they stream, 2 = raise it while they prepare (descriptor, hash, edges).
+#ifndef SQ_PRIO
+#define SQ_PRIO 0
+#endif
 
 #define SQ_STR2(x) #x
 #define SQ_STR(x) SQ_STR2(x)
@@ -532,6 +537,11 @@ __device__ __forceinline__ void transform(const PacketJob &J, const uint32_t (&k
   // this is a compiler barrier plus the LDS drain)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   SQ_TL_STREAM
+#if SQ_PRIO == 1
+  __builtin_amdgcn_s_setprio(3);
+#elif SQ_PRIO == 2
+  __builtin_amdgcn_s_setprio(0);
+#endif
 
   // ---- 4. edges: salt bytes and the partial lines at both ends.  They never
   // overlap the full chunks' input or output bytes.
@@ -573,6 +583,9 @@ template <int KIND, int DIR, bool MULTI, int U>
 __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
   __shared__ ChunkRec recs[kWavesPerBlock][kWave];
   SQ_TL_START
+#if SQ_PRIO == 2
+  __builtin_amdgcn_s_setprio(3);
+#endif
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wv = threadIdx.x / kWave;
   const uint64_t p64 = ((uint64_t)blockIdx.x * kWavesPerBlock + wv) * kPktPerWave + lane;
