@@ -240,8 +240,18 @@ __device__ __forceinline__ uint32_t locate(uint32_t start, uint32_t b0, uint32_t
 // no padding writes and no branches, and the compiler's waitcnt accounting
 // stays exact (a conditional store makes it fall back to draining).
 constexpr uint32_t kOffNone = 0xFFFFFFF0u;
+// cache-policy bits of the stream's buffer ops (gfx950: sc0 = 1, nt = 2,
+// sc1 = 16); SQ_AUXLD / SQ_AUXST override them in timing builds
+#ifdef SQ_AUXLD
+constexpr int kAuxLd = SQ_AUXLD;
+#else
 constexpr int kAuxLd = (SQ_NT & 1) ? 2 : 0;  // nt
+#endif
+#ifdef SQ_AUXST
+constexpr int kAuxSt = SQ_AUXST;
+#else
 constexpr int kAuxSt = (SQ_NT & 2) ? 2 : 0;
+#endif
 
 struct WaveBufs {
   __amdgpu_buffer_rsrc_t src, dst;
