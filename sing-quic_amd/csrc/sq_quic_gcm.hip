@@ -609,18 +609,17 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
 
 template <bool OPEN, bool MULTI>
 static int launch_gcm(const QGParams *qp, hipStream_t s) {
-  static int per_cu = 0, cus = 0;
-  if (!per_cu) {
-    int dev = 0;
+  // resident blocks on the device, queried once (thread-safe static init)
+  static const uint64_t cap = [] {
+    int dev = 0, per_cu = 0, cus = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, quic_gcm_kernel<OPEN, MULTI>,
                                                        kGBlock, 0);
-    if (per_cu < 1) per_cu = 1;
-    if (cus < 1) cus = 1;
-  }
+    return (uint64_t)(per_cu < 1 ? 1 : per_cu) * (uint64_t)(cus < 1 ? 1 : cus);
+  }();
   const uint64_t waves = ((uint64_t)qp->n + kGPpw - 1) / kGPpw;
-  const uint64_t want = (waves + kGWaves - 1) / kGWaves, cap = (uint64_t)per_cu * cus;
+  const uint64_t want = (waves + kGWaves - 1) / kGWaves;
   const dim3 grid((uint32_t)(want < cap ? want : cap));
   hipLaunchKernelGGL((quic_gcm_kernel<OPEN, MULTI>), grid, dim3(kGBlock), 0, s, *qp);
   return hipGetLastError() == hipSuccess ? 0 : -3;
