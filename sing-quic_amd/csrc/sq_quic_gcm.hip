@@ -58,6 +58,12 @@ namespace sq {
 #ifndef SQ_GNB
 #define SQ_GNB 2
 #endif
+// 1: single-key round keys staged in LDS (broadcast reads) instead of the
+// kernarg segment (SGPRs, which spill to VGPR lanes at 88 words); measured
+// 17 % slower at 16-wave blocks (the keys then occupy VGPRs), so off
+#ifndef SQ_GRK_LDS
+#define SQ_GRK_LDS 0
+#endif
 constexpr uint32_t kGBlock = SQ_GBLOCK;  // 16 waves: one block per CU (128 KiB of LDS)
 constexpr uint32_t kGWaves = kGBlock / kWave;
 constexpr uint32_t kGPpw = 16;                 // packets per wave
@@ -375,14 +381,19 @@ struct alignas(16) GRec {
 
 template <bool MULTI>
 __device__ __forceinline__ GKey<MULTI> key_of(const QGParams &Q, uint32_t kid, const uint32_t *tP,
-                                              const uint32_t *tH) {
+                                              const uint32_t *tH, const uint32_t *tK) {
   GKey<MULTI> K;
   if (MULTI) {
     const QuicGcmKeyDev *E = Q.keys + kid;
     K.rk = E->rk; K.hrk = E->hrk; K.iv = E->iv;
     K.hpos = &E->hpos[0][0][0]; K.htab = &E->htab[0][0][0];
   } else {
-    K.rk = Q.rk0; K.hrk = Q.hrk0; K.iv = Q.iv0; K.hpos = tP; K.htab = tH;
+#if SQ_GRK_LDS
+    K.rk = tK; K.hrk = tK + 44;
+#else
+    K.rk = Q.rk0; K.hrk = Q.hrk0;
+#endif
+    K.iv = Q.iv0; K.hpos = tP; K.htab = tH;
   }
   return K;
 }
@@ -393,11 +404,14 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
   __shared__ __attribute__((aligned(16))) uint32_t tP[MULTI ? 4 : 32 * 64];
   __shared__ __attribute__((aligned(16))) uint32_t tH[MULTI ? 4 : kGcmPow * 64];
   __shared__ GRec recs[kGWaves][kGPpw];
-  // stage the T-table image and (single key) the GHASH tables
+  __shared__ __attribute__((aligned(16))) uint32_t tK[88];  // single key: rk0 || hrk0
+  // stage the T-table image and (single key) the round keys and GHASH tables
   for (uint32_t i = threadIdx.x; i < 256 * 64; i += kGBlock) {
     const uint32_t v = Q.t0[i >> 6];
     tT[i] = (i & 32) ? rotl(v, 8) : v;
   }
+  if (!MULTI && threadIdx.x < 88) tK[threadIdx.x] = threadIdx.x < 44 ? Q.rk0[threadIdx.x]
+                                                                     : Q.hrk0[threadIdx.x - 44];
   if (!MULTI) {
     const uint32_t *src = &Q.keys[0].hpos[0][0][0];  // hpos then htab, contiguous
     for (uint32_t i = threadIdx.x; i < (32 + kGcmPow) * 16; i += kGBlock) {
@@ -430,7 +444,7 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
         kid = 0;
       }
     }
-    const GKey<MULTI> K = key_of<MULTI>(Q, kid, tP, tH);
+    const GKey<MULTI> K = key_of<MULTI>(Q, kid, tP, tH, tK);
     if (live) {
       src = (uint64_t)Q.in + Q.in_off[p];
       dst = (uint64_t)Q.out + Q.out_off[p];
@@ -531,7 +545,7 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
       const uint32_t pp = q_locate(start, base, f < T ? f : T - 1);
       if (f < T) {
         GRec &R = recs[wv][pp];
-        const GKey<MULTI> KB = key_of<MULTI>(Q, R.kid, tP, tH);
+        const GKey<MULTI> KB = key_of<MULTI>(Q, R.kid, tP, tH, tK);
         const uint32_t b = f - R.start, off0 = 64 * b;
         const uint32_t nv = R.pl - off0 < 64 ? R.pl - off0 : 64u;
         const uint32_t rn[3] = {R.nonce[0], R.nonce[1], R.nonce[2]};
