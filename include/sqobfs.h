@@ -278,6 +278,31 @@ int sqobfs_quic_seal(sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr,
 int sqobfs_quic_open(sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr,
                      const sqobfs_quic_batch *b, void *stream);
 
+/* QUIC protection and the Salamander layer in ONE pass (Hysteria2's send and
+ * receive path: quic-go seals a packet, then SalamanderPacketConn.WriteTo
+ * obfuscates the datagram, salamander.go:57-70; ReadFrom then Open on the
+ * way in).  One read of the plaintext and one write of the wire datagram
+ * instead of two kernels and an intermediate buffer.
+ *   seal: in = header || payload (as sqobfs_quic_seal); out = the wire
+ *         datagram salt[i] || (protected packet || tag) ^ K_i, K_i =
+ *         BLAKE2b-256(psk || salt[i]) repeated, out_len[i] = in_len[i] + 24.
+ *         salt: [n*8] device bytes.  out must not overlap in, except the
+ *         in-place form out_off[i] == in_off[i] - 8 (8 bytes of headroom in
+ *         front of each packet, as the vectorised Salamander writer).
+ *   open: in = wire datagram (in_len[i] bytes, salt first); out = unprotected
+ *         header || plaintext, out_len[i] = in_len[i] - 24 (or a
+ *         SQOBFS_QUIC_E* code; datagrams shorter than the salt give
+ *         SQOBFS_QUIC_ESHORT).  In place (out_off == in_off) works.
+ * okr: a Salamander keyring (entry 0 is the connection's PSK); kr: a
+ * ChaCha20-Poly1305 keyring (the AES-128-GCM form is not fused yet:
+ * SQ_EINVAL). */
+int sqobfs_quic_seal_salamander(sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr,
+                                const sqobfs_keyring *okr, const sqobfs_quic_batch *b,
+                                const uint8_t *salt, void *stream);
+int sqobfs_quic_open_salamander(sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr,
+                                const sqobfs_keyring *okr, const sqobfs_quic_batch *b,
+                                void *stream);
+
 /* ------------------------------------------------------------------------
  * Batched UDP socket I/O (Linux) -- the host side of the path.
  *

@@ -587,8 +587,12 @@ void sqobfs_quic_keyring_destroy(sqobfs_quic_keyring *kr) {
 }
 
 static int quic_launch(int open, sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr,
-                       const sqobfs_quic_batch *b, void *stream) {
+                       const sqobfs_quic_batch *b, void *stream,
+                       const sqobfs_keyring *okr = nullptr, const uint8_t *salt = nullptr) {
   if (!ctx || !kr || kr->ctx != ctx || !b || b->flags) return SQ_EINVAL;
+  if (okr && (okr->ctx != ctx || okr->kind != SQOBFS_SALAMANDER ||
+              kr->suite != SQOBFS_QUIC_CHACHA20_POLY1305 || (!open && !salt)))
+    return SQ_EINVAL;
   if (b->n == 0) return SQ_OK;
   if (!b->in || !b->in_off || !b->in_len || !b->out || !b->out_off || !b->out_len ||
       !b->pn_offset || !b->pn)
@@ -632,7 +636,26 @@ static int quic_launch(int open, sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr,
   q.n = b->n;
   q.n_keys = kr->count;
   q.key0 = kr->host0;
+  if (okr) {
+    q.obfs = 1;
+    q.osalt = salt;
+    q.opsk = okr->host0;
+  }
   return sq_launch_quic(open, &q, pick_stream(ctx, stream));
+}
+
+int sqobfs_quic_seal_salamander(sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr,
+                                const sqobfs_keyring *okr, const sqobfs_quic_batch *b,
+                                const uint8_t *salt, void *stream) {
+  if (!okr) return SQ_EINVAL;
+  return quic_launch(0, ctx, kr, b, stream, okr, salt);
+}
+
+int sqobfs_quic_open_salamander(sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr,
+                                const sqobfs_keyring *okr, const sqobfs_quic_batch *b,
+                                void *stream) {
+  if (!okr) return SQ_EINVAL;
+  return quic_launch(1, ctx, kr, b, stream, okr, nullptr);
 }
 
 int sqobfs_quic_seal(sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr, const sqobfs_quic_batch *b,

@@ -89,6 +89,12 @@ struct QParams {
   uint32_t n;
   uint32_t n_keys;
   QuicKeyDev key0;
+  // fused Salamander layer (sqobfs_quic_seal_salamander / _open_salamander):
+  // the QUIC packet travels as salt8 || packet ^ BLAKE2b-256(psk || salt8)
+  const uint8_t *osalt;  // seal: [n*8] salts (device)
+  uint32_t obfs;         // 1: fused path
+  uint32_t pad_;
+  PskEntry opsk;         // the Salamander keyring's entry 0
 };
 
 // AES-128-GCM (TLS_AES_128_GCM_SHA256) connection keys on the device:

@@ -27,6 +27,7 @@
 #include "sq_bytes.h"
 #include "sq_hash.h"
 #include "sq_internal.h"
+#include "sq_obfs_key.h"
 #include "sq_quic.h"
 
 namespace sq {
@@ -166,10 +167,13 @@ __device__ __forceinline__ void hp_mask(const QuicKeyDev &K, const uint32_t (&sa
 // bytes are read).  In place (src == dst) works: every input block is loaded
 // before the output block at the same address is stored.  first32 receives
 // ciphertext bytes 0..31 (zero past len) for the header-protection sample.
-template <bool SEAL>
+// OB (fused Salamander layer): the output (seal) or input (open) bytes are
+// also XORed with the packet's Salamander key, okr = that key rotated to the
+// payload's first byte (chunk j uses its half j & 1).
+template <bool SEAL, bool OB>
 __device__ __forceinline__ void payload_pass(const QuicKeyDev &K, const uint32_t (&nonce)[3],
                                              uint64_t src, uint64_t dst, uint32_t len, Poly &P,
-                                             uint32_t (&first32)[8]) {
+                                             uint32_t (&first32)[8], const uint32_t (&okr)[8]) {
 #pragma unroll
   for (int j = 0; j < 8; j++) first32[j] = 0u;
   if (len == 0) return;
@@ -212,6 +216,7 @@ __device__ __forceinline__ void payload_pass(const QuicKeyDev &K, const uint32_t
         for (int w = 0; w < 4; w++) {
           in_prev[w] = cur[q][w];
           in[w] &= range_mask(0, (int)nb, w);
+          if (OB && !SEAL) in[w] ^= okr[4 * (q & 1) + w] & range_mask(0, (int)nb, w);
           c[w] = (in[w] ^ ks[4 * q + w]) & range_mask(0, (int)nb, w);
         }
         if (SEAL) poly_block(P, c);
@@ -219,6 +224,10 @@ __device__ __forceinline__ void payload_pass(const QuicKeyDev &K, const uint32_t
         if (j < 2) {
 #pragma unroll
           for (int w = 0; w < 4; w++) first32[4 * j + w] = SEAL ? c[w] : in[w];
+        }
+        if (OB && SEAL) {
+#pragma unroll
+          for (int w = 0; w < 4; w++) c[w] ^= okr[4 * (q & 1) + w] & range_mask(0, (int)nb, w);
         }
         // output block D0 + 16j: bytes [0, oa) from the previous chunk's
         // tail, [oa, 16) from this chunk's head
@@ -276,6 +285,7 @@ struct alignas(16) QRec {
   uint32_t nonce[3], pad1;
   uint32_t r[5], s[4], pad2[3];
   uint32_t ct32[8];       // ciphertext bytes 0..31 (the header-protection sample)
+  uint32_t okr[8];        // fused Salamander layer: key rotated to the payload start
 };
 
 // One 64-byte keystream block of one packet (cooperative pass, any lane):
@@ -298,7 +308,7 @@ __device__ __forceinline__ void coop_load(const QRec &R, uint32_t b, uint32_t (&
   }
 }
 
-template <bool OPEN>
+template <bool OPEN, bool OB>
 __device__ __forceinline__ void coop_block(const QuicKeyDev &K, QRec &R, uint32_t b,
                                            const uint32_t (&blk)[5][4], uint32_t (&contrib)[5]) {
   uint32_t ks[16];
@@ -318,6 +328,7 @@ __device__ __forceinline__ void coop_block(const QuicKeyDev &K, QRec &R, uint32_
 #pragma unroll
     for (int w = 0; w < 4; w++) {
       in[w] &= range_mask(0, nb, w);
+      if (OB && OPEN) in[w] ^= R.okr[(4 * q + w) & 7] & range_mask(0, nb, w);
       o[q][w] = (in[w] ^ ks[4 * q + w]) & range_mask(0, nb, w);
     }
     if (nb > 0) {
@@ -327,6 +338,10 @@ __device__ __forceinline__ void coop_block(const QuicKeyDev &K, QRec &R, uint32_
     if (!OPEN && b == 0 && q < 2) {
 #pragma unroll
       for (int w = 0; w < 4; w++) R.ct32[4 * q + w] = o[q][w];
+    }
+    if (OB && !OPEN) {
+#pragma unroll
+      for (int w = 0; w < 4; w++) o[q][w] ^= R.okr[(4 * q + w) & 7] & range_mask(0, nb, w);
     }
   }
   contrib[0] = L.h0; contrib[1] = L.h1; contrib[2] = L.h2; contrib[3] = L.h3; contrib[4] = L.h4;
@@ -362,7 +377,7 @@ __device__ __forceinline__ void coop_block(const QuicKeyDev &K, QRec &R, uint32_
 //      (seal) header protection from the sample kept in LDS.
 // Payloads above kQCoopMax bytes are walked by their owner lane in phase 3
 // (the sequential payload_pass), so any length works.
-template <bool OPEN, bool MULTI>
+template <bool OPEN, bool MULTI, bool OB>
 #if SQ_QMINW
 __global__ __launch_bounds__(kQBlock, SQ_QMINW) void quic_kernel
 #else
@@ -383,6 +398,9 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
   const QuicKeyDev *K = &Q.key0;
   uint32_t nonce[3] = {0u, 0u, 0u}, otk[16], rtag[4] = {0u, 0u, 0u, 0u};
   uint32_t hd[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, pnw = 0;  // packet bytes 0..31; seal: pn bytes
+  // fused Salamander layer (OB): wire = salt8 || QUIC packet ^ okey
+  uint64_t wire = 0;
+  uint32_t okey[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, osalt[4] = {0u, 0u, 0u, 0u};
   Poly P;
   P.h0 = P.h1 = P.h2 = P.h3 = P.h4 = 0;
   P.r0 = P.r1 = P.r2 = P.r3 = P.r4 = P.s1 = P.s2 = P.s3 = P.s4 = 0;
@@ -399,6 +417,28 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
     pno = Q.pn_offset[p];
     uint64_t pn = Q.pn[p];
     uint32_t pnb[4] = {0u, 0u, 0u, 0u};
+    if (OB) {
+      if (!OPEN) {  // wire = salt || protected packet ^ key
+        wire = dst;
+        dst = wire + kSalamanderSalt;
+        const uint32_t *sp = reinterpret_cast<const uint32_t *>(Q.osalt + 8ull * p);
+        osalt[0] = sp[0];
+        osalt[1] = sp[1];
+      } else if (len >= (uint32_t)kSalamanderSalt && len <= kQMaxPacket) {
+        wire = src;  // salt = the first 8 wire bytes (salamander.go:50)
+        load16(src, src + kSalamanderSalt, osalt);
+        src += kSalamanderSalt;
+        len -= kSalamanderSalt;
+      } else {
+        len = 0;  // too short for a salt: rejected below
+      }
+      salamander_key(&Q.opsk, osalt, okey);
+    }
+    // packet byte k (de-obfuscated when the fused layer is on)
+    auto hb = [&](uint32_t k) -> uint32_t {
+      const uint32_t b = head_byte(hd, src, k);
+      return (OB && OPEN && k >= 32) ? b ^ byte32(okey, k & 31) : b;
+    };
     if (!OPEN) {
       if (len) load_head32(src, len, hd);
       first = hd[0] & 0xFFu;
@@ -408,7 +448,7 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
         live = false;
       } else {
         pl = len - hdr;
-        for (uint32_t i = 0; i < pn_len; i++) pnw |= head_byte(hd, src, pno + i) << (8 * i);
+        for (uint32_t i = 0; i < pn_len; i++) pnw |= hb(pno + i) << (8 * i);
       }
     } else if (len < 16 || len > kQMaxPacket || pno + 4 + 16 > len) {
       live = false;
@@ -417,6 +457,21 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
       load16(src + pno + 4, src + len, sample);
       load16(src + len - 16, src + len, rtag);  // before any in-place write
       load_head32(src, len, hd);
+      if (OB) {  // de-obfuscate what was read: key byte of QUIC offset k is okey[k % 32]
+        uint32_t k4[4];
+        keywin(okey, (pno + 4) & 31, k4);
+#pragma unroll
+        for (int w = 0; w < 4; w++) sample[w] ^= k4[w];
+        keywin(okey, (len - 16) & 31, k4);
+#pragma unroll
+        for (int w = 0; w < 4; w++) rtag[w] ^= k4[w];
+        keywin(okey, 0, k4);
+#pragma unroll
+        for (int w = 0; w < 4; w++) hd[w] ^= k4[w];
+        keywin(okey, 16, k4);
+#pragma unroll
+        for (int w = 0; w < 4; w++) hd[4 + w] ^= k4[w];
+      }
       hp_mask(*K, sample, m0, m1);
       const uint32_t pfirst = hd[0] & 0xFFu;
       first = pfirst ^ (m0 & ((pfirst & 0x80) ? 0x0Fu : 0x1Fu));
@@ -427,7 +482,7 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
       } else {
         uint64_t trunc = 0;
         for (uint32_t i = 0; i < pn_len; i++) {
-          pnb[i] = head_byte(hd, src, pno + i) ^ mask_byte(m0, m1, 1 + i);
+          pnb[i] = hb(pno + i) ^ mask_byte(m0, m1, 1 + i);
           trunc = (trunc << 8) | pnb[i];
         }
         pn = decode_pn(pn, trunc, 8 * pn_len);
@@ -445,6 +500,12 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
       for (uint32_t q = 0; q < hdr; q += 16) {
         uint32_t w[4];
         head_block(hd, src, q, hdr, w);
+        if (OB && OPEN && q >= 32) {
+          uint32_t k4[4];
+          keywin(okey, q & 31, k4);
+#pragma unroll
+          for (int j = 0; j < 4; j++) w[j] ^= k4[j] & range_mask(0, (int)(hdr - q), j);
+        }
         if (OPEN) {
           if (q == 0) set_byte(w, 0, first);
           for (uint32_t i = 0; i < pn_len; i++) {
@@ -453,7 +514,13 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
           }
         }
         poly_block(P, w);
-        if (OPEN || dst != src) store16(dst + q, w, hdr - q < 16 ? hdr - q : 16);
+        if (OB && !OPEN) {  // the wire carries the (still unprotected) header ^ key
+          uint32_t k4[4];
+          keywin(okey, q & 31, k4);
+#pragma unroll
+          for (int j = 0; j < 4; j++) w[j] ^= k4[j];
+        }
+        if (OPEN || OB || dst != src) store16(dst + q, w, hdr - q < 16 ? hdr - q : 16);
       }
     }
   }
@@ -479,6 +546,15 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
     R.s[0] = P.s1; R.s[1] = P.s2; R.s[2] = P.s3; R.s[3] = P.s4;
 #pragma unroll
     for (int i = 0; i < 8; i++) R.ct32[i] = 0u;
+    if (OB) {
+      uint32_t k4[4];
+      keywin(okey, hdr & 31, k4);
+#pragma unroll
+      for (int i = 0; i < 4; i++) R.okr[i] = k4[i];
+      keywin(okey, (hdr + 16) & 31, k4);
+#pragma unroll
+      for (int i = 0; i < 4; i++) R.okr[4 + i] = k4[i];
+    }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
@@ -498,7 +574,7 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
       QRec &R = recs[wv][pp];
       const QuicKeyDev &KB = MULTI ? Q.keys[R.kid] : Q.key0;
       uint32_t c5[5];
-      coop_block<OPEN>(KB, R, f - R.start, blk, c5);
+      coop_block<OPEN, OB>(KB, R, f - R.start, blk, c5);
 #pragma unroll
       for (int i = 0; i < 5; i++) parts[wv][f][i] = c5[i];
     }
@@ -518,7 +594,7 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
       const QuicKeyDev &KB = MULTI ? Q.keys[R.kid] : Q.key0;
       uint32_t c5[5], blk[5][4];
       coop_load(R, f - R.start, blk);
-      coop_block<OPEN>(KB, R, f - R.start, blk, c5);
+      coop_block<OPEN, OB>(KB, R, f - R.start, blk, c5);
 #pragma unroll
       for (int i = 0; i < 5; i++) parts[wv][f][i] = c5[i];
     }
@@ -569,7 +645,10 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
 #pragma unroll
     for (int i = 0; i < 8; i++) ct32[i] = recs[wv][lane].ct32[i];
   } else {
-    payload_pass<!OPEN>(*K, nonce, src + hdr, dst + hdr, pl, P, ct32);
+    uint32_t okr[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) okr[i] = OB ? recs[wv][lane].okr[i] : 0u;
+    payload_pass<!OPEN, OB>(*K, nonce, src + hdr, dst + hdr, pl, P, ct32, okr);
   }
   poly_lengths(P, hdr, pl);
   uint32_t tag[4];
@@ -580,7 +659,16 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
     Q.out_len[p] = ok ? len - 16 : kQEAuth;
     return;
   }
-  store16(dst + len, tag, 16);
+  if (OB) {
+    uint32_t k4[4], t4[4];
+    keywin(okey, len & 31, k4);
+#pragma unroll
+    for (int w = 0; w < 4; w++) t4[w] = tag[w] ^ k4[w];
+    store16(dst + len, t4, 16);
+    store16(wire, osalt, kSalamanderSalt);
+  } else {
+    store16(dst + len, tag, 16);
+  }
   // header protection: sample = (ciphertext || tag)[4 - pn_len ..][0..16)
   const uint32_t so = 4 - pn_len;
   uint32_t sample[4];
@@ -599,12 +687,16 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
   }
   uint32_t m0, m1;
   hp_mask(*K, sample, m0, m1);
-  gst<uint8_t>(dst, (uint8_t)(first ^ (m0 & ((first & 0x80) ? 0x0Fu : 0x1Fu))));
+  // protected header bytes; with the fused layer also ^ the key byte of
+  // their position
+  const uint32_t kb0 = OB ? okey[0] & 0xFFu : 0u;
+  gst<uint8_t>(dst, (uint8_t)(first ^ kb0 ^ (m0 & ((first & 0x80) ? 0x0Fu : 0x1Fu))));
   for (uint32_t i = 0; i < pn_len; i++) {
     const uint32_t bb = (pnw >> (8 * i)) & 0xFFu;
-    gst<uint8_t>(dst + pno + i, (uint8_t)(bb ^ mask_byte(m0, m1, 1 + i)));
+    const uint32_t kb = OB ? byte32(okey, (pno + i) & 31) : 0u;
+    gst<uint8_t>(dst + pno + i, (uint8_t)(bb ^ kb ^ mask_byte(m0, m1, 1 + i)));
   }
-  Q.out_len[p] = len + 16;
+  Q.out_len[p] = len + 16 + (OB ? kSalamanderSalt : 0u);
 }
 
 }  // namespace sq
@@ -616,12 +708,14 @@ extern "C" int sq_launch_quic(int open, const sq::QParams *qp, void *stream) {
   const dim3 grid((uint32_t)((waves + kQWaves - 1) / kQWaves));
   hipStream_t s = (hipStream_t)stream;
   const bool multi = qp->key_id != nullptr;
-  if (open) {
-    if (multi) hipLaunchKernelGGL((quic_kernel<true, true>), grid, dim3(kQBlock), 0, s, *qp);
-    else hipLaunchKernelGGL((quic_kernel<true, false>), grid, dim3(kQBlock), 0, s, *qp);
+#define SQ_QL(O, M, B) hipLaunchKernelGGL((quic_kernel<O, M, B>), grid, dim3(kQBlock), 0, s, *qp)
+  if (qp->obfs) {
+    if (open) { if (multi) SQ_QL(true, true, true); else SQ_QL(true, false, true); }
+    else { if (multi) SQ_QL(false, true, true); else SQ_QL(false, false, true); }
   } else {
-    if (multi) hipLaunchKernelGGL((quic_kernel<false, true>), grid, dim3(kQBlock), 0, s, *qp);
-    else hipLaunchKernelGGL((quic_kernel<false, false>), grid, dim3(kQBlock), 0, s, *qp);
+    if (open) { if (multi) SQ_QL(true, true, false); else SQ_QL(true, false, false); }
+    else { if (multi) SQ_QL(false, true, false); else SQ_QL(false, false, false); }
   }
+#undef SQ_QL
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -173,6 +173,8 @@ def lib() -> ctypes.CDLL:
     L.sqobfs_quic_keyring_destroy.restype = None
     L.sqobfs_quic_seal.argtypes = [vp, vp, ctypes.POINTER(QuicBatch), vp]
     L.sqobfs_quic_open.argtypes = [vp, vp, ctypes.POINTER(QuicBatch), vp]
+    L.sqobfs_quic_seal_salamander.argtypes = [vp, vp, vp, ctypes.POINTER(QuicBatch), vp, vp]
+    L.sqobfs_quic_open_salamander.argtypes = [vp, vp, vp, ctypes.POINTER(QuicBatch), vp]
     L.sqobfs_salt_key.argtypes = [vp, vp, ctypes.c_uint64]
     L.sqobfs_salt_seq.argtypes = [vp]
     L.sqobfs_salt_seq.restype = ctypes.c_uint64
@@ -519,3 +521,19 @@ def quic_seal(ctx: Context, kr: QuicKeyring, batch: QuicBatch, stream=None) -> N
 def quic_open(ctx: Context, kr: QuicKeyring, batch: QuicBatch, stream=None) -> None:
     _check(lib().sqobfs_quic_open(ctx.handle, kr.handle, ctypes.byref(batch), stream),
            "sqobfs_quic_open")
+
+
+def quic_seal_salamander(ctx: Context, kr: QuicKeyring, okr: Keyring, batch: QuicBatch, salt,
+                         stream=None) -> None:
+    """Seal + Salamander obfuscation in one pass (wire = salt || obfs(packet))."""
+    _check(lib().sqobfs_quic_seal_salamander(ctx.handle, kr.handle, okr.handle,
+                                             ctypes.byref(batch), _ptr(salt), stream),
+           "sqobfs_quic_seal_salamander")
+
+
+def quic_open_salamander(ctx: Context, kr: QuicKeyring, okr: Keyring, batch: QuicBatch,
+                         stream=None) -> None:
+    """Salamander de-obfuscation + open in one pass."""
+    _check(lib().sqobfs_quic_open_salamander(ctx.handle, kr.handle, okr.handle,
+                                             ctypes.byref(batch), stream),
+           "sqobfs_quic_open_salamander")
