@@ -583,6 +583,9 @@ def quic_rate(torch, sqobfs, ctx, dev, steps, n=1 << 20, payload=1350, cpu_secon
                          "GiB_s_payload": round(n * payload / (ms * 1e-3) / 2**30, 2),
                          "achieved_GBs": round(alg / (ms * 1e-3) / 1e9, 1),
                          "frac_of_8TBs": round(alg / (ms * 1e-3) / 8e12, 4)}
+    if suite == 0:
+        res["fused_salamander"] = quic_fused_rate(torch, sqobfs, ctx, dev, steps, n, ln, data,
+                                                  in_off, lens, pno, pn, key, iv, hp)
     # parity on sampled packets
     idx = sorted(set([0, n - 1] + list(range(0, n, 4099))))[:300]
     d = data.view(n, ln)[idx].cpu().numpy()
@@ -631,6 +634,73 @@ def quic_rate(torch, sqobfs, ctx, dev, steps, n=1 << 20, payload=1350, cpu_secon
                               "matches_oracle": cout[:ln + 16].tobytes() == chk,
                               "sample": f"{reps} x {m_before} packets seal, OpenSSL libcrypto "
                                         "EVP (oracle/ossl_quic.c), one context per thread"}
+    return res
+
+
+def quic_fused_rate(torch, sqobfs, ctx, dev, steps, n, ln, data, in_off, lens, pno, pn, key, iv,
+                    hp):
+    """Hysteria2's datagram path: QUIC seal then Salamander obfuscation, as
+    two launches (sqobfs_quic_seal into an intermediate buffer, then
+    sqobfs_launch) and fused (sqobfs_quic_seal_salamander); and the way in
+    (deobfuscate + open vs sqobfs_quic_open_salamander).  Parity of the fused
+    wire against the two-launch wire on every byte."""
+    import numpy as np
+    PSK_ = PSK
+    wl = ln + 24
+    s = torch.cuda.current_stream(dev).cuda_stream
+    g = torch.Generator(device=dev)
+    g.manual_seed(9)
+    salts = torch.randint(0, 256, (n * 8,), generator=g, device=dev, dtype=torch.uint8)
+    sealed = torch.zeros(n * (ln + 16), device=dev, dtype=torch.uint8)
+    wire2 = torch.zeros(n * wl, device=dev, dtype=torch.uint8)
+    wire1 = torch.zeros(n * wl, device=dev, dtype=torch.uint8)
+    opened = torch.zeros(n * ln, device=dev, dtype=torch.uint8)
+    s_off = torch.arange(n, device=dev, dtype=torch.int64) * (ln + 16)
+    w_off = torch.arange(n, device=dev, dtype=torch.int64) * wl
+    slens = torch.full((n,), ln + 16, device=dev, dtype=torch.int32)
+    wlens = torch.full((n,), wl, device=dev, dtype=torch.int32)
+    z = lambda: torch.zeros(n, device=dev, dtype=torch.int32)  # noqa: E731
+    o1, o2, o3, o4, o5 = z(), z(), z(), z(), z()
+    largest = pn - 1
+    res = {}
+    with sqobfs.QuicKeyring(ctx, [sqobfs.QuicKey.of(key, iv, hp)]) as kr, \
+            sqobfs.Keyring(ctx, sqobfs.SALAMANDER, [PSK_]) as okr:
+        b_seal = sqobfs.quic_batch(n, data, in_off, lens, sealed, s_off, o1, pno, pn)
+        b_obfs = sqobfs.make_batch(n, sealed, s_off, slens, wire2, w_off, o2, salt=salts)
+        b_fused = sqobfs.quic_batch(n, data, in_off, lens, wire1, w_off, o3, pno, pn)
+        b_deo = sqobfs.make_batch(n, wire1, w_off, wlens, sealed, s_off, o4)
+        b_open = sqobfs.quic_batch(n, sealed, s_off, slens, opened, in_off, o5, pno, largest)
+        b_fopen = sqobfs.quic_batch(n, wire1, w_off, wlens, opened, in_off, o5, pno, largest)
+
+        def timed(fn):
+            for _ in range(2):
+                fn()
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(steps)]
+            for e0, e1 in ev:
+                e0.record()
+                fn()
+                e1.record()
+            torch.cuda.synchronize(dev)
+            return sum(e0.elapsed_time(e1) for e0, e1 in ev) / steps * 1e3
+        two_out = timed(lambda: (sqobfs.quic_seal(ctx, kr, b_seal, s),
+                                 sqobfs.launch(ctx, okr, sqobfs.OBFUSCATE, b_obfs, s)))
+        fused_out = timed(lambda: sqobfs.quic_seal_salamander(ctx, kr, okr, b_fused, salts, s))
+        same = bool(torch.equal(wire1, wire2))
+        two_in = timed(lambda: (sqobfs.launch(ctx, okr, sqobfs.DEOBFUSCATE, b_deo, s),
+                                sqobfs.quic_open(ctx, kr, b_open, s)))
+        fused_in = timed(lambda: sqobfs.quic_open_salamander(ctx, kr, okr, b_fopen, s))
+        ok_in = bool((o5 == ln).all()) and bool(torch.equal(opened, data))
+    payload = n * (ln - 11)
+    for name, us in (("seal_then_obfuscate_us", two_out), ("fused_seal_us", fused_out),
+                     ("deobfuscate_then_open_us", two_in), ("fused_open_us", fused_in)):
+        res[name] = round(us, 2)
+    res["fused_seal_GiB_s_payload"] = round(payload / (fused_out * 1e-6) / 2**30, 2)
+    res["fused_open_GiB_s_payload"] = round(payload / (fused_in * 1e-6) / 2**30, 2)
+    res["fused_wire_equals_two_launch_wire"] = same
+    res["fused_open_round_trip"] = ok_in
+    res["traffic_note"] = ("two launches move read L + write L+16 + read L+16 + write L+24 "
+                           "per packet; fused: read L + write L+24")
     return res
 
 
