@@ -583,9 +583,8 @@ def quic_rate(torch, sqobfs, ctx, dev, steps, n=1 << 20, payload=1350, cpu_secon
                          "GiB_s_payload": round(n * payload / (ms * 1e-3) / 2**30, 2),
                          "achieved_GBs": round(alg / (ms * 1e-3) / 1e9, 1),
                          "frac_of_8TBs": round(alg / (ms * 1e-3) / 8e12, 4)}
-    if suite == 0:
-        res["fused_salamander"] = quic_fused_rate(torch, sqobfs, ctx, dev, steps, n, ln, data,
-                                                  in_off, lens, pno, pn, key, iv, hp)
+    res["fused_salamander"] = quic_fused_rate(torch, sqobfs, ctx, dev, steps, n, ln, data,
+                                              in_off, lens, pno, pn, key, iv, hp, suite)
     # parity on sampled packets
     idx = sorted(set([0, n - 1] + list(range(0, n, 4099))))[:300]
     d = data.view(n, ln)[idx].cpu().numpy()
@@ -638,7 +637,7 @@ def quic_rate(torch, sqobfs, ctx, dev, steps, n=1 << 20, payload=1350, cpu_secon
 
 
 def quic_fused_rate(torch, sqobfs, ctx, dev, steps, n, ln, data, in_off, lens, pno, pn, key, iv,
-                    hp):
+                    hp, suite=0):
     """Hysteria2's datagram path: QUIC seal then Salamander obfuscation, as
     two launches (sqobfs_quic_seal into an intermediate buffer, then
     sqobfs_launch) and fused (sqobfs_quic_seal_salamander); and the way in
@@ -663,7 +662,7 @@ def quic_fused_rate(torch, sqobfs, ctx, dev, steps, n, ln, data, in_off, lens, p
     o1, o2, o3, o4, o5 = z(), z(), z(), z(), z()
     largest = pn - 1
     res = {}
-    with sqobfs.QuicKeyring(ctx, [sqobfs.QuicKey.of(key, iv, hp)]) as kr, \
+    with sqobfs.QuicKeyring(ctx, [sqobfs.QuicKey.of(key, iv, hp)], suite) as kr, \
             sqobfs.Keyring(ctx, sqobfs.SALAMANDER, [PSK_]) as okr:
         b_seal = sqobfs.quic_batch(n, data, in_off, lens, sealed, s_off, o1, pno, pn)
         b_obfs = sqobfs.make_batch(n, sealed, s_off, slens, wire2, w_off, o2, salt=salts)

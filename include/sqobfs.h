@@ -293,9 +293,8 @@ int sqobfs_quic_open(sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr,
  *         header || plaintext, out_len[i] = in_len[i] - 24 (or a
  *         SQOBFS_QUIC_E* code; datagrams shorter than the salt give
  *         SQOBFS_QUIC_ESHORT).  In place (out_off == in_off) works.
- * okr: a Salamander keyring (entry 0 is the connection's PSK); kr: a
- * ChaCha20-Poly1305 keyring (the AES-128-GCM form is not fused yet:
- * SQ_EINVAL). */
+ * okr: a Salamander keyring (entry 0 is the connection's PSK); kr: a QUIC
+ * keyring of either suite. */
 int sqobfs_quic_seal_salamander(sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr,
                                 const sqobfs_keyring *okr, const sqobfs_quic_batch *b,
                                 const uint8_t *salt, void *stream);

@@ -590,8 +590,7 @@ static int quic_launch(int open, sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr,
                        const sqobfs_quic_batch *b, void *stream,
                        const sqobfs_keyring *okr = nullptr, const uint8_t *salt = nullptr) {
   if (!ctx || !kr || kr->ctx != ctx || !b || b->flags) return SQ_EINVAL;
-  if (okr && (okr->ctx != ctx || okr->kind != SQOBFS_SALAMANDER ||
-              kr->suite != SQOBFS_QUIC_CHACHA20_POLY1305 || (!open && !salt)))
+  if (okr && (okr->ctx != ctx || okr->kind != SQOBFS_SALAMANDER || (!open && !salt)))
     return SQ_EINVAL;
   if (b->n == 0) return SQ_OK;
   if (!b->in || !b->in_off || !b->in_len || !b->out || !b->out_off || !b->out_len ||
@@ -618,6 +617,11 @@ static int quic_launch(int open, sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr,
     memcpy(g.rk0, kr->grk0, sizeof g.rk0);
     memcpy(g.hrk0, kr->ghrk0, sizeof g.hrk0);
     memcpy(g.iv0, kr->giv0, sizeof g.iv0);
+    if (okr) {
+      g.obfs = 1;
+      g.osalt = salt;
+      g.opsk = okr->host0;
+    }
     return sq_launch_quic_gcm(open, &g, pick_stream(ctx, stream));
   }
   sq::QParams q;

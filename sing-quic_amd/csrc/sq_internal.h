@@ -135,6 +135,9 @@ struct QGParams {
   uint32_t rk0[44];
   uint32_t hrk0[44];
   uint32_t iv0[3];
+  uint32_t obfs;         // 1: fused Salamander layer (as QParams)
+  const uint8_t *osalt;  // seal: [n*8] salts (device)
+  PskEntry opsk;         // the Salamander keyring's entry 0
 };
 
 }  // namespace sq

@@ -48,6 +48,7 @@
 
 #include "sq_bytes.h"
 #include "sq_internal.h"
+#include "sq_obfs_key.h"
 #include "sq_quic.h"
 
 namespace sq {
@@ -257,11 +258,14 @@ struct GKey {
 // (one aligned 16-byte load and store per block whatever the alignments,
 // one block of read-ahead), as payload_pass in sq_quic.hip.  In place
 // (src == dst) works.  first32 = ciphertext bytes 0..31 (zero past nv).
-template <bool OPEN, bool MULTI>
+// OB (fused Salamander layer): output (seal) or input (open) bytes are also
+// XORed with the packet's Salamander key; okr = the key rotated to the first
+// byte at src / dst (16-byte block j uses half j & 1).
+template <bool OPEN, bool MULTI, bool OB>
 __device__ __forceinline__ void gcm_run(const GKey<MULTI> &K, const uint32_t *tT, uint32_t tcol,
                                         const uint32_t (&nonce)[3], uint32_t ctr0, uint64_t src,
                                         uint64_t dst, uint32_t nv, uint32_t (&y)[4],
-                                        uint32_t (&first32)[8]) {
+                                        uint32_t (&first32)[8], const uint32_t (&okr)[8]) {
 #pragma unroll
   for (int j = 0; j < 8; j++) first32[j] = 0u;
   if (nv == 0) return;
@@ -282,8 +286,8 @@ __device__ __forceinline__ void gcm_run(const GKey<MULTI> &K, const uint32_t *tT
   load_blk(2, C);
   const uint32_t nchunk = (nv + 15) / 16;
   // one output block: GHASH, header-protection sample, realigned store
-  auto finish = [&](uint32_t j, const uint32_t (&in)[4], const uint32_t (&c)[4]) {
-    const uint32_t(&g)[4] = OPEN ? in : c;
+  auto finish = [&](uint32_t j, const uint32_t (&in)[4], const uint32_t (&c0)[4]) {
+    const uint32_t(&g)[4] = OPEN ? in : c0;
     ghash_absorb(y, g);
     gmul_pos<MULTI>(y, K.hpos);
 #pragma unroll
@@ -291,6 +295,12 @@ __device__ __forceinline__ void gcm_run(const GKey<MULTI> &K, const uint32_t *tT
       first32[w] = bsel(j == 0, g[w], first32[w]);
       first32[4 + w] = bsel(j == 1, g[w], first32[4 + w]);
     }
+    uint32_t c[4];  // what goes on the wire
+    const int nbj = (int)nv - 16 * (int)j;
+#pragma unroll
+    for (int w = 0; w < 4; w++)
+      c[w] = (OB && !OPEN) ? c0[w] ^ (bsel(j & 1, okr[4 + w], okr[w]) & range_mask(0, nbj, w))
+                           : c0[w];
     uint32_t blk[4];
     funnel(prev_c, c, 16 - oa, blk);
     const uint32_t lo = j == 0 ? oa : 0u;
@@ -312,6 +322,7 @@ __device__ __forceinline__ void gcm_run(const GKey<MULTI> &K, const uint32_t *tT
 #pragma unroll
     for (int w = 0; w < 4; w++) {
       in[w] &= range_mask(0, nb, w);
+      if (OB && OPEN) in[w] ^= bsel(j & 1, okr[4 + w], okr[w]) & range_mask(0, nb, w);
       c[w] = (in[w] ^ s1[w]) & range_mask(0, nb, w);
       A[w] = Bq[w];
       Bq[w] = C[w];
@@ -336,6 +347,7 @@ __device__ __forceinline__ void gcm_run(const GKey<MULTI> &K, const uint32_t *tT
 #pragma unroll
       for (int w = 0; w < 4; w++) {
         in[q][w] &= range_mask(0, nb, w);
+        if (OB && OPEN) in[q][w] ^= okr[4 * q + w] & range_mask(0, nb, w);  // j is even
         c[q][w] = (in[q][w] ^ s2[q][w]) & range_mask(0, nb, w);
       }
     }
@@ -377,6 +389,7 @@ struct alignas(16) GRec {
   uint32_t nonce[3], pad;
   uint32_t x[4];       // GHASH accumulator (big-endian words), ds_xor target
   uint32_t ct32[8];    // ciphertext bytes 0..31 (the header-protection sample)
+  uint32_t okr[8];     // fused Salamander layer: key rotated to the payload start
 };
 
 template <bool MULTI>
@@ -398,7 +411,7 @@ __device__ __forceinline__ GKey<MULTI> key_of(const QGParams &Q, uint32_t kid, c
   return K;
 }
 
-template <bool OPEN, bool MULTI>
+template <bool OPEN, bool MULTI, bool OB>
 __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
   __shared__ uint32_t tT[256 * 64];
   __shared__ __attribute__((aligned(16))) uint32_t tP[MULTI ? 4 : 32 * 64];
@@ -436,6 +449,9 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
     uint64_t src = 0, dst = 0;
     uint32_t nonce[3] = {0u, 0u, 0u}, rtag[4] = {0u, 0u, 0u, 0u}, y[4] = {0u, 0u, 0u, 0u};
     uint32_t hd[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, pnw = 0;  // packet bytes 0..31; seal: pn bytes
+    // fused Salamander layer (OB): wire = salt8 || QUIC packet ^ okey
+    uint64_t wire = 0;
+    uint32_t okey[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, osalt[4] = {0u, 0u, 0u, 0u};
     if (live && MULTI) {
       kid = Q.key_id[p];
       if (kid >= Q.n_keys) {
@@ -452,6 +468,28 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
       pno = Q.pn_offset[p];
       uint64_t pn = Q.pn[p];
       uint32_t pnb[4] = {0u, 0u, 0u, 0u};
+      if (OB) {
+        if (!OPEN) {  // wire = salt || protected packet ^ key
+          wire = dst;
+          dst = wire + kSalamanderSalt;
+          const uint32_t *sp = reinterpret_cast<const uint32_t *>(Q.osalt + 8ull * p);
+          osalt[0] = sp[0];
+          osalt[1] = sp[1];
+        } else if (len >= (uint32_t)kSalamanderSalt && len <= kQMaxPacket) {
+          wire = src;  // salt = the first 8 wire bytes (salamander.go:50)
+          load16(src, src + kSalamanderSalt, osalt);
+          src += kSalamanderSalt;
+          len -= kSalamanderSalt;
+        } else {
+          len = 0;  // too short for a salt: rejected below
+        }
+        salamander_key(&Q.opsk, osalt, okey);
+      }
+      // packet byte k (de-obfuscated when the fused layer is on)
+      auto hb = [&](uint32_t k) -> uint32_t {
+        const uint32_t b = head_byte(hd, src, k);
+        return (OB && OPEN && k >= 32) ? b ^ byte32(okey, k & 31) : b;
+      };
       if (!OPEN) {
         if (len) load_head32(src, len, hd);
         first = hd[0] & 0xFFu;
@@ -461,7 +499,7 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
           live = false;
         } else {
           pl = len - hdr;
-          for (uint32_t i = 0; i < pn_len; i++) pnw |= head_byte(hd, src, pno + i) << (8 * i);
+          for (uint32_t i = 0; i < pn_len; i++) pnw |= hb(pno + i) << (8 * i);
         }
       } else if (len < 16 || len > kQMaxPacket || pno + 4 + 16 > len) {
         live = false;
@@ -470,6 +508,21 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
         load16(src + pno + 4, src + len, sample);
         load16(src + len - 16, src + len, rtag);  // before any in-place write
         load_head32(src, len, hd);
+        if (OB) {  // de-obfuscate what was read: key byte of QUIC offset k is okey[k % 32]
+          uint32_t k4[4];
+          keywin(okey, (pno + 4) & 31, k4);
+#pragma unroll
+          for (int w = 0; w < 4; w++) sample[w] ^= k4[w];
+          keywin(okey, (len - 16) & 31, k4);
+#pragma unroll
+          for (int w = 0; w < 4; w++) rtag[w] ^= k4[w];
+          keywin(okey, 0, k4);
+#pragma unroll
+          for (int w = 0; w < 4; w++) hd[w] ^= k4[w];
+          keywin(okey, 16, k4);
+#pragma unroll
+          for (int w = 0; w < 4; w++) hd[4 + w] ^= k4[w];
+        }
         gcm_hp_mask<MULTI>(K, tT, tcol, sample, m0, m1);
         const uint32_t pfirst = hd[0] & 0xFFu;
         first = pfirst ^ (m0 & ((pfirst & 0x80) ? 0x0Fu : 0x1Fu));
@@ -480,7 +533,7 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
         } else {
           uint64_t trunc = 0;
           for (uint32_t i = 0; i < pn_len; i++) {
-            pnb[i] = head_byte(hd, src, pno + i) ^ mask_byte(m0, m1, 1 + i);
+            pnb[i] = hb(pno + i) ^ mask_byte(m0, m1, 1 + i);
             trunc = (trunc << 8) | pnb[i];
           }
           pn = decode_pn(pn, trunc, 8 * pn_len);
@@ -497,6 +550,12 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
         for (uint32_t q = 0; q < hdr; q += 16) {
           uint32_t w[4];
           head_block(hd, src, q, hdr, w);
+          if (OB && OPEN && q >= 32) {
+            uint32_t k4[4];
+            keywin(okey, q & 31, k4);
+#pragma unroll
+            for (int j = 0; j < 4; j++) w[j] ^= k4[j] & range_mask(0, (int)(hdr - q), j);
+          }
           if (OPEN) {
             if (q == 0) set_byte(w, 0, first);
             for (uint32_t i = 0; i < pn_len; i++) {
@@ -506,7 +565,13 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
           }
           ghash_absorb(y, w);
           gmul_pos<MULTI>(y, K.hpos);
-          if (OPEN || dst != src) store16(dst + q, w, hdr - q < 16 ? hdr - q : 16);
+          if (OB && !OPEN) {  // the wire carries the (still unprotected) header ^ key
+            uint32_t k4[4];
+            keywin(okey, q & 31, k4);
+#pragma unroll
+            for (int j = 0; j < 4; j++) w[j] ^= k4[j];
+          }
+          if (OPEN || OB || dst != src) store16(dst + q, w, hdr - q < 16 ? hdr - q : 16);
         }
       }
     }
@@ -536,6 +601,15 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
       for (int i = 0; i < 4; i++) R.x[i] = coop ? y[i] : 0u;
 #pragma unroll
       for (int i = 0; i < 8; i++) R.ct32[i] = 0u;
+      if (OB) {
+        uint32_t k4[4];
+        keywin(okey, hdr & 31, k4);
+#pragma unroll
+        for (int i = 0; i < 4; i++) R.okr[i] = k4[i];
+        keywin(okey, (hdr + 16) & 31, k4);
+#pragma unroll
+        for (int i = 0; i < 4; i++) R.okr[4 + i] = k4[i];
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
@@ -550,7 +624,11 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
         const uint32_t nv = R.pl - off0 < 64 ? R.pl - off0 : 64u;
         const uint32_t rn[3] = {R.nonce[0], R.nonce[1], R.nonce[2]};
         uint32_t yb[4] = {0u, 0u, 0u, 0u}, f32[8];
-        gcm_run<OPEN, MULTI>(KB, tT, tcol, rn, 2 + 4 * b, R.src + off0, R.dst + off0, nv, yb, f32);
+        uint32_t rokr[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) rokr[i] = OB ? R.okr[i] : 0u;
+        gcm_run<OPEN, MULTI, OB>(KB, tT, tcol, rn, 2 + 4 * b, R.src + off0, R.dst + off0, nv, yb,
+                                 f32, rokr);
         const uint32_t m = R.np - 4 * b - (nv + 15) / 16;  // payload blocks after this chunk
         if (m) KB.mul_pow(yb, m);
 #pragma unroll
@@ -576,7 +654,10 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
 #pragma unroll
       for (int i = 0; i < 8; i++) ct32[i] = recs[wv][lane].ct32[i];
     } else {
-      gcm_run<OPEN, MULTI>(K, tT, tcol, nonce, 2, src + hdr, dst + hdr, pl, y, ct32);
+      uint32_t rokr[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) rokr[i] = OB ? recs[wv][lane].okr[i] : 0u;
+      gcm_run<OPEN, MULTI, OB>(K, tT, tcol, nonce, 2, src + hdr, dst + hdr, pl, y, ct32, rokr);
     }
     // lengths block: be64(8 * hdr) || be64(8 * pl)
     y[1] ^= 8 * hdr;
@@ -593,7 +674,16 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
       Q.out_len[p] = ok ? len - 16 : kQEAuth;
       continue;
     }
-    store16(dst + len, tag, 16);
+    if (OB) {
+      uint32_t k4[4], t4[4];
+      keywin(okey, len & 31, k4);
+#pragma unroll
+      for (int w = 0; w < 4; w++) t4[w] = tag[w] ^ k4[w];
+      store16(dst + len, t4, 16);
+      store16(wire, osalt, kSalamanderSalt);
+    } else {
+      store16(dst + len, tag, 16);
+    }
     // header protection: sample = (ciphertext || tag)[4 - pn_len ..][0..16)
     const uint32_t so = 4 - pn_len;
     uint32_t sample[4];
@@ -612,30 +702,32 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
     }
     uint32_t m0, m1;
     gcm_hp_mask<MULTI>(K, tT, tcol, sample, m0, m1);
-    gst<uint8_t>(dst, (uint8_t)(first ^ (m0 & ((first & 0x80) ? 0x0Fu : 0x1Fu))));
+    const uint32_t kb0 = OB ? okey[0] & 0xFFu : 0u;
+    gst<uint8_t>(dst, (uint8_t)(first ^ kb0 ^ (m0 & ((first & 0x80) ? 0x0Fu : 0x1Fu))));
     for (uint32_t i = 0; i < pn_len; i++) {
       const uint32_t bb = (pnw >> (8 * i)) & 0xFFu;
-      gst<uint8_t>(dst + pno + i, (uint8_t)(bb ^ mask_byte(m0, m1, 1 + i)));
+      const uint32_t kb = OB ? byte32(okey, (pno + i) & 31) : 0u;
+      gst<uint8_t>(dst + pno + i, (uint8_t)(bb ^ kb ^ mask_byte(m0, m1, 1 + i)));
     }
-    Q.out_len[p] = len + 16;
+    Q.out_len[p] = len + 16 + (OB ? kSalamanderSalt : 0u);
   }
 }
 
-template <bool OPEN, bool MULTI>
+template <bool OPEN, bool MULTI, bool OB>
 static int launch_gcm(const QGParams *qp, hipStream_t s) {
   // resident blocks on the device, queried once (thread-safe static init)
   static const uint64_t cap = [] {
     int dev = 0, per_cu = 0, cus = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, quic_gcm_kernel<OPEN, MULTI>,
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, quic_gcm_kernel<OPEN, MULTI, OB>,
                                                        kGBlock, 0);
     return (uint64_t)(per_cu < 1 ? 1 : per_cu) * (uint64_t)(cus < 1 ? 1 : cus);
   }();
   const uint64_t waves = ((uint64_t)qp->n + kGPpw - 1) / kGPpw;
   const uint64_t want = (waves + kGWaves - 1) / kGWaves;
   const dim3 grid((uint32_t)(want < cap ? want : cap));
-  hipLaunchKernelGGL((quic_gcm_kernel<OPEN, MULTI>), grid, dim3(kGBlock), 0, s, *qp);
+  hipLaunchKernelGGL((quic_gcm_kernel<OPEN, MULTI, OB>), grid, dim3(kGBlock), 0, s, *qp);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -646,6 +738,10 @@ extern "C" int sq_launch_quic_gcm(int open, const sq::QGParams *qp, void *stream
   if (qp->n == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const bool multi = qp->key_id != nullptr;
-  if (open) return multi ? launch_gcm<true, true>(qp, s) : launch_gcm<true, false>(qp, s);
-  return multi ? launch_gcm<false, true>(qp, s) : launch_gcm<false, false>(qp, s);
+  if (qp->obfs) {
+    if (open) return multi ? launch_gcm<true, true, true>(qp, s) : launch_gcm<true, false, true>(qp, s);
+    return multi ? launch_gcm<false, true, true>(qp, s) : launch_gcm<false, false, true>(qp, s);
+  }
+  if (open) return multi ? launch_gcm<true, true, false>(qp, s) : launch_gcm<true, false, false>(qp, s);
+  return multi ? launch_gcm<false, true, false>(qp, s) : launch_gcm<false, false, false>(qp, s);
 }

@@ -1,4 +1,4 @@
-"""QUIC protection fused with the Salamander layer on the GPU
+"""QUIC protection (both suites) fused with the Salamander layer on the GPU
 (sqobfs_quic_seal_salamander / _open_salamander): Hysteria2's datagram is
 salt8 || (protected QUIC packet) ^ BLAKE2b-256(psk || salt8).  Checked byte
 for byte against the oracle composition: or_quic_seal (RFC 9001, ChaCha20-
@@ -28,7 +28,8 @@ def _place(sizes, lead, gap, align=1):
     return np.array(offs, np.uint64), pos + 64
 
 
-def _seal(ctx, keys, kr_o, pkts, pnos, pns, salts, key_ids=None, inplace=False, align=1):  # noqa: F811
+def _seal(ctx, keys, kr_o, pkts, pnos, pns, salts, key_ids=None, inplace=False, align=1,  # noqa: F811
+          suite=0):
     import torch
     dev = torch.device("cuda", 0)
     n = len(pkts)
@@ -52,14 +53,15 @@ def _seal(ctx, keys, kr_o, pkts, pnos, pns, salts, key_ids=None, inplace=False, 
              salt=t(np.frombuffer(b"".join(salts), np.uint8).copy()))
     b = sqobfs.quic_batch(n, d_data, d["in_off"], d["in_len"], d_out, d["out_off"], d["out_len"],
                           d["pno"], d["pn"], d["kid"])
-    with sqobfs.QuicKeyring(ctx, keys) as kr:
+    with sqobfs.QuicKeyring(ctx, keys, suite) as kr:
         s = torch.cuda.current_stream(dev).cuda_stream
         sqobfs.quic_seal_salamander(ctx, kr, kr_o, b, d["salt"], s)
         torch.cuda.synchronize(dev)
     return d_out.cpu().numpy(), out_off, d["out_len"].cpu().numpy(), out
 
 
-def _open(ctx, keys, kr_o, wires, pnos, largest, key_ids=None, inplace=False):  # noqa: F811
+def _open(ctx, keys, kr_o, wires, pnos, largest, key_ids=None, inplace=False,  # noqa: F811
+          suite=0):
     import torch
     dev = torch.device("cuda", 0)
     n = len(wires)
@@ -82,39 +84,42 @@ def _open(ctx, keys, kr_o, wires, pnos, largest, key_ids=None, inplace=False):  
              pn_out=t(np.zeros(n, np.uint64)))
     b = sqobfs.quic_batch(n, d_data, d["in_off"], d["in_len"], d_out, d["out_off"], d["out_len"],
                           d["pno"], d["pn"], d["kid"], d["pn_out"])
-    with sqobfs.QuicKeyring(ctx, keys) as kr:
+    with sqobfs.QuicKeyring(ctx, keys, suite) as kr:
         s = torch.cuda.current_stream(dev).cuda_stream
         sqobfs.quic_open_salamander(ctx, kr, kr_o, b, s)
         torch.cuda.synchronize(dev)
     return d_out.cpu().numpy(), out_off, d["out_len"].cpu().numpy(), d["pn_out"].cpu().numpy()
 
 
-def _keys(rng, n):
-    kb = [tuple(rng.integers(0, 256, m, dtype=np.uint8).tobytes() for m in (32, 12, 32))
+def _keys(rng, n, suite=0):
+    kl = 16 if suite else 32
+    kb = [tuple(rng.integers(0, 256, m, dtype=np.uint8).tobytes() for m in (kl, 12, kl))
           for _ in range(n)]
     return kb, [QuicKey.of(*k) for k in kb]
 
 
-def _want_wire(kb, pkt, pno, pn, salt):
-    prot, r = ol.quic_seal(*kb, pn, pkt, pno)
+def _want_wire(kb, pkt, pno, pn, salt, suite=0):
+    prot, r = ol.quic_seal(*kb, pn, pkt, pno, suite=suite)
     assert r == len(pkt) + 16
     return ol.salamander_write(PSK, salt, prot)[0]
 
 
+@pytest.mark.parametrize("suite", [0, 1])
 @pytest.mark.parametrize("nkeys,inplace", [(1, False), (1, True), (3, False)])
-def test_seal_open_ragged_vs_oracle(ctx, nkeys, inplace):  # noqa: F811
-    rng = np.random.Generator(np.random.PCG64(500 + nkeys + inplace))
-    kb, keys = _keys(rng, nkeys)
+def test_seal_open_ragged_vs_oracle(ctx, nkeys, inplace, suite):  # noqa: F811
+    rng = np.random.Generator(np.random.PCG64(500 + nkeys + inplace + 10 * suite))
+    kb, keys = _keys(rng, nkeys, suite)
     pkts, pnos, pns = _random_packets(rng, 2000)
     salts = [rng.integers(0, 256, 8, dtype=np.uint8).tobytes() for _ in pkts]
     kid = rng.integers(0, nkeys, len(pkts)) if nkeys > 1 else np.zeros(len(pkts), np.int64)
     kid_arg = kid if nkeys > 1 else None
     with sqobfs.Keyring(ctx, sqobfs.SALAMANDER, [PSK]) as kr_o:
-        out, oo, olen, buf = _seal(ctx, keys, kr_o, pkts, pnos, pns, salts, kid_arg, inplace)
+        out, oo, olen, buf = _seal(ctx, keys, kr_o, pkts, pnos, pns, salts, kid_arg, inplace,
+                                   suite=suite)
         ref = buf.copy()
         wires = []
         for i, p in enumerate(pkts):
-            w = _want_wire(kb[kid[i]], p, pnos[i], pns[i], salts[i])
+            w = _want_wire(kb[kid[i]], p, pnos[i], pns[i], salts[i], suite)
             assert olen[i] == len(p) + 24, i
             ref[int(oo[i]):int(oo[i]) + len(w)] = np.frombuffer(w, np.uint8)
             got = out[int(oo[i]):int(oo[i]) + len(w)].tobytes()
@@ -123,28 +128,30 @@ def test_seal_open_ragged_vs_oracle(ctx, nkeys, inplace):  # noqa: F811
         if not inplace:
             assert np.array_equal(out, ref), "bytes outside the datagrams were touched"
         largest = [max(0, pn - int(rng.integers(1, 100))) for pn in pns]
-        out2, oo2, ol2, pno2 = _open(ctx, keys, kr_o, wires, pnos, largest, kid_arg, inplace)
+        out2, oo2, ol2, pno2 = _open(ctx, keys, kr_o, wires, pnos, largest, kid_arg, inplace,
+                                     suite=suite)
         for i, p in enumerate(pkts):
             assert ol2[i] == len(p) and pno2[i] == pns[i], i
             assert out2[int(oo2[i]):int(oo2[i]) + len(p)].tobytes() == p, i
 
 
-def test_long_payloads_and_rejects(ctx):  # noqa: F811
-    rng = np.random.Generator(np.random.PCG64(77))
-    kb, keys = _keys(rng, 1)
+@pytest.mark.parametrize("suite", [0, 1])
+def test_long_payloads_and_rejects(ctx, suite):  # noqa: F811
+    rng = np.random.Generator(np.random.PCG64(77 + suite))
+    kb, keys = _keys(rng, 1, suite)
     pkts = [bytes([0x41]) + bytes(8) + (7).to_bytes(2, "big") +
             rng.integers(0, 256, plen, dtype=np.uint8).tobytes()
             for plen in [2047, 2048, 2049, 3000, 9000, 65, 2, 1350]]
     pnos, pns = [9] * len(pkts), [7] * len(pkts)
     salts = [rng.integers(0, 256, 8, dtype=np.uint8).tobytes() for _ in pkts]
     with sqobfs.Keyring(ctx, sqobfs.SALAMANDER, [PSK]) as kr_o:
-        out, oo, olen, _ = _seal(ctx, keys, kr_o, pkts, pnos, pns, salts)
+        out, oo, olen, _ = _seal(ctx, keys, kr_o, pkts, pnos, pns, salts, suite=suite)
         wires = []
         for i, p in enumerate(pkts):
-            w = _want_wire(kb[0], p, pnos[i], pns[i], salts[i])
+            w = _want_wire(kb[0], p, pnos[i], pns[i], salts[i], suite)
             assert out[int(oo[i]):int(oo[i]) + len(w)].tobytes() == w, len(p)
             wires.append(w)
-        out2, oo2, ol2, pno2 = _open(ctx, keys, kr_o, wires, pnos, [6] * len(wires))
+        out2, oo2, ol2, pno2 = _open(ctx, keys, kr_o, wires, pnos, [6] * len(wires), suite=suite)
         for i, p in enumerate(pkts):
             assert ol2[i] == len(p) and out2[int(oo2[i]):int(oo2[i]) + len(p)].tobytes() == p
         # tampering anywhere (salt, header, payload, tag) and too-short datagrams
@@ -154,10 +161,10 @@ def test_long_payloads_and_rejects(ctx):  # noqa: F811
             w[[0, 9, len(w) // 2, len(w) - 1][i % 4]] ^= 0x10
             bad.append(bytes(w))
         bad += [b"\x01\x02\x03", bytes(8), bytes(20)]
-        _, _, ol3, _ = _open(ctx, keys, kr_o, bad, [9] * len(bad), [6] * len(bad))
+        _, _, ol3, _ = _open(ctx, keys, kr_o, bad, [9] * len(bad), [6] * len(bad), suite=suite)
         for i, w in enumerate(bad):
             plain, n = ol.salamander_read(PSK, w)
-            want = ol.quic_open(*kb[0], 6, plain[:n], 9)[1] if len(w) > 8 else -1
+            want = ol.quic_open(*kb[0], 6, plain[:n], 9, suite=suite)[1] if len(w) > 8 else -1
             assert want < 0
             if len(w) <= 8:
                 assert ol3[i] == sqobfs.QUIC_ESHORT
