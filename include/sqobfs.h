@@ -379,6 +379,27 @@ uint8_t *sqobfs_udp_conn_tx_payload(sqobfs_udp_conn *c, uint32_t i);
 int sqobfs_udp_conn_write(sqobfs_udp_conn *c, uint32_t fd_index, uint32_t n,
                           const uint32_t *len, const sqobfs_addr *to, uint32_t *sent);
 
+/* QUIC through the endpoint (Hysteria2's data path; the conn's keyring must
+ * be Salamander): one launch per batch seals AND obfuscates
+ * (sqobfs_quic_seal_salamander) or de-obfuscates AND opens
+ * (sqobfs_quic_open_salamander), in the mapped slots.
+ * write_quic: QUIC packet i (header || payload, len[i] bytes, at most
+ *   slot_bytes - 24) is written by the caller at sqobfs_udp_conn_tx_payload(i);
+ *   packet numbers pn[i], pn field at pn_offset (the connection's short
+ *   header: 1 + DCID length); salts from getrandom.  Packets the kernel
+ *   rejects are not sent; *sent = datagrams sent.
+ * read_quic: receive a batch, open it with packet numbers decoded against
+ *   largest_pn; view.len[i] = the packet's length (header || plaintext, at
+ *   view.base + view.off[i]) or a SQOBFS_QUIC_E* code; *pn_out (optional) =
+ *   the decoded packet numbers.  Valid until the next read. */
+int sqobfs_udp_conn_write_quic(sqobfs_udp_conn *c, const sqobfs_quic_keyring *qkr,
+                               uint32_t fd_index, uint32_t n, const uint32_t *len,
+                               uint16_t pn_offset, const uint64_t *pn, const sqobfs_addr *to,
+                               uint32_t *sent);
+int sqobfs_udp_conn_read_quic(sqobfs_udp_conn *c, const sqobfs_quic_keyring *qkr,
+                              uint16_t pn_offset, uint64_t largest_pn, int timeout_ms,
+                              sqobfs_udp_view *out, const uint64_t **pn_out);
+
 /* UDP segmentation offloads (Linux UDP_SEGMENT / UDP_GRO).
  * sqobfs_udp_send_gso: as sqobfs_udp_send, but consecutive datagrams to the
  * same address whose lengths are equal (the last of a run may be shorter)

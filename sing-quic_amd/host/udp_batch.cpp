@@ -23,6 +23,7 @@
 #include <netinet/udp.h>
 #include <poll.h>
 #include <string.h>
+#include <sys/random.h>
 #include <sys/socket.h>
 
 #include <algorithm>
@@ -94,6 +95,11 @@ struct sqobfs_udp_conn {
   uint32_t *tx_len = nullptr, *tx_out_len = nullptr;
   std::vector<uint32_t> tx_wire_len;
   uint32_t offload = 0;  // SQOBFS_UDP_TX_GSO | SQOBFS_UDP_RX_GRO in effect
+  // QUIC batch arrays (in the mapped block): packet numbers, decoded packet
+  // numbers, packet-number offsets, Salamander salts
+  uint64_t *qpn = nullptr, *qpn_out = nullptr;
+  uint16_t *qpno = nullptr;
+  uint8_t *qsalt = nullptr;
 };
 
 namespace {
@@ -434,9 +440,10 @@ int sqobfs_udp_conn_open(sqobfs_ctx *ctx, const sqobfs_keyring *kr, const int *f
   c->slots = slots;
   c->slot_bytes = slot_bytes;
   c->S = S;
-  // one mapped block: rx slots | tx slots | 4 u64 arrays | 4 u32 arrays
+  // one mapped block: rx slots | tx slots | 6 u64 arrays | 4 u32 arrays |
+  // salts (8 B each) | u16 packet-number offsets
   const size_t sb = (size_t)slots * slot_bytes, a64 = 8ull * slots, a32 = 4ull * slots;
-  const size_t bytes = 2 * sb + 4 * a64 + 4 * a32;
+  const size_t bytes = 2 * sb + 6 * a64 + 4 * a32 + 8ull * slots + 2ull * slots;
   if (sqobfs_host_alloc(ctx, bytes, &c->block) != SQ_OK) {
     delete c;
     return SQ_ENOMEM;
@@ -455,10 +462,14 @@ int sqobfs_udp_conn_open(sqobfs_ctx *ctx, const sqobfs_keyring *kr, const int *f
   c->rx_out_off = (uint64_t *)p;             p += a64;
   c->tx_in_off = (uint64_t *)p;              p += a64;
   c->tx_out_off = (uint64_t *)p;             p += a64;
+  c->qpn = (uint64_t *)p;                    p += a64;
+  c->qpn_out = (uint64_t *)p;                p += a64;
   c->rx_len = (uint32_t *)p;                 p += a32;
   c->rx_out_len = (uint32_t *)p;             p += a32;
   c->tx_len = (uint32_t *)p;                 p += a32;
-  c->tx_out_len = (uint32_t *)p;
+  c->tx_out_len = (uint32_t *)p;             p += a32;
+  c->qsalt = p;                              p += 8ull * slots;
+  c->qpno = (uint16_t *)p;
   c->rx_fd.resize(slots);
   c->rx_from.resize(slots);
   c->tx_wire_len.resize(slots);
@@ -548,6 +559,120 @@ int sqobfs_udp_conn_write(sqobfs_udp_conn *c, uint32_t fd_index, uint32_t n,
   }
   return sqobfs_udp_send(c->fds[fd_index], c->tx, c->tx_out_off, c->tx_wire_len.data(), to, n,
                          sent);
+}
+
+// ---- QUIC over the endpoint: the fused seal / open + Salamander kernels
+// (sqobfs_quic_seal_salamander, sqobfs_quic_open_salamander) on the mapped
+// slots, so one launch per batch does QUIC protection and obfuscation.
+
+int sqobfs_udp_conn_write_quic(sqobfs_udp_conn *c, const sqobfs_quic_keyring *qkr,
+                               uint32_t fd_index, uint32_t n, const uint32_t *len,
+                               uint16_t pn_offset, const uint64_t *pn, const sqobfs_addr *to,
+                               uint32_t *sent) {
+  if (sent) *sent = 0;
+  if (!c || !qkr || !sent || fd_index >= c->fds.size() || n > c->slots ||
+      sqobfs_keyring_kind(c->kr) != SQOBFS_SALAMANDER)
+    return SQ_EINVAL;
+  if (n == 0) return SQ_OK;
+  if (!len || !pn || !to) return SQ_EINVAL;
+  std::lock_guard<std::mutex> lk(c->tx_mu);
+  for (uint32_t i = 0; i < n; i++) {
+    if (len[i] + 16 + c->S > c->slot_bytes) return SQ_EINVAL;
+    c->tx_len[i] = len[i];
+    c->qpn[i] = pn[i];
+    c->qpno[i] = pn_offset;
+  }
+  // salts: 8 random bytes per datagram (salamander.go:60 buf.WriteRandom)
+  for (size_t got = 0, want = 8ull * n; got < want;) {
+    const ssize_t r = getrandom(c->qsalt + got, want - got, 0);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return -errno;
+    }
+    got += (size_t)r;
+  }
+  sqobfs_quic_batch b;
+  memset(&b, 0, sizeof b);
+  b.n = n;
+  b.in = c->tx;
+  b.in_off = c->tx_in_off;    // packet at slot + 8 ...
+  b.in_len = c->tx_len;
+  b.out = c->tx;
+  b.out_off = c->tx_out_off;  // ... wire from the slot start (the in-place form)
+  b.out_len = c->tx_out_len;
+  b.pn_offset = c->qpno;
+  b.pn = c->qpn;
+  void *s = sqobfs_stream(c->ctx);
+  int st = sqobfs_quic_seal_salamander(c->ctx, qkr, c->kr, &b, c->qsalt, s);
+  if (st == SQ_OK) st = sqobfs_sync(c->ctx, s);
+  if (st != SQ_OK) return st;
+  // packets the kernel rejected (SQOBFS_QUIC_E*) are not sent
+  std::vector<uint64_t> off;
+  std::vector<uint32_t> wl;
+  std::vector<sqobfs_addr> dst;
+  off.reserve(n);
+  wl.reserve(n);
+  dst.reserve(n);
+  for (uint32_t i = 0; i < n; i++) {
+    if (c->tx_out_len[i] != len[i] + 16 + c->S) continue;
+    off.push_back(c->tx_out_off[i]);
+    wl.push_back(c->tx_out_len[i]);
+    dst.push_back(to[i]);
+  }
+  const uint32_t m = (uint32_t)off.size();
+  if (c->offload & SQOBFS_UDP_TX_GSO) {
+    const int g = sqobfs_udp_send_gso(c->fds[fd_index], c->tx, off.data(), wl.data(), dst.data(),
+                                      m, sent);
+    if (g == SQ_OK || *sent > 0 || (g != -EIO && g != -EINVAL && g != -ENOPROTOOPT &&
+                                    g != -EOPNOTSUPP))
+      return g;
+    c->offload &= ~SQOBFS_UDP_TX_GSO;
+  }
+  return sqobfs_udp_send(c->fds[fd_index], c->tx, off.data(), wl.data(), dst.data(), m, sent);
+}
+
+int sqobfs_udp_conn_read_quic(sqobfs_udp_conn *c, const sqobfs_quic_keyring *qkr,
+                              uint16_t pn_offset, uint64_t largest_pn, int timeout_ms,
+                              sqobfs_udp_view *out, const uint64_t **pn_out) {
+  if (!c || !qkr || !out || sqobfs_keyring_kind(c->kr) != SQOBFS_SALAMANDER) return SQ_EINVAL;
+  std::lock_guard<std::mutex> lk(c->rx_mu);
+  memset(out, 0, sizeof *out);
+  if (pn_out) *pn_out = nullptr;
+  uint32_t n = 0;
+  int st = (c->offload & SQOBFS_UDP_RX_GRO)
+               ? recv_gro(c, timeout_ms, &n)
+               : sqobfs_udp_recv(c->fds.data(), (uint32_t)c->fds.size(), c->rx, c->slot_bytes,
+                                 0, c->slots, timeout_ms, c->rx_len, c->rx_fd.data(),
+                                 c->rx_from.data(), &n);
+  if (st != SQ_OK || n == 0) return st;
+  for (uint32_t i = 0; i < n; i++) {
+    c->qpno[i] = pn_offset;
+    c->qpn[i] = largest_pn;
+  }
+  sqobfs_quic_batch b;
+  memset(&b, 0, sizeof b);
+  b.n = n;
+  b.in = c->rx;
+  b.in_off = c->rx_in_off;
+  b.in_len = c->rx_len;
+  b.out = c->rx;
+  b.out_off = c->rx_in_off;  // in place: the plaintext packet from the datagram start
+  b.out_len = c->rx_out_len;
+  b.pn_offset = c->qpno;
+  b.pn = c->qpn;
+  b.pn_out = c->qpn_out;
+  void *s = sqobfs_stream(c->ctx);
+  st = sqobfs_quic_open_salamander(c->ctx, qkr, c->kr, &b, s);
+  if (st == SQ_OK) st = sqobfs_sync(c->ctx, s);
+  if (st != SQ_OK) return st;
+  out->count = n;
+  out->base = c->rx;
+  out->off = c->rx_in_off;
+  out->len = c->rx_out_len;
+  out->fd_index = c->rx_fd.data();
+  out->from = c->rx_from.data();
+  if (pn_out) *pn_out = c->qpn_out;
+  return SQ_OK;
 }
 
 }  // extern "C"

@@ -159,6 +159,9 @@ def lib() -> ctypes.CDLL:
     L.sqobfs_udp_send.argtypes = [i32, vp, vp, vp, vp, u32, u32p]
     L.sqobfs_udp_send_gso.argtypes = [i32, vp, vp, vp, vp, u32, u32p]
     L.sqobfs_udp_conn_set_offload.argtypes = [vp, u32]
+    L.sqobfs_udp_conn_write_quic.argtypes = [vp, vp, u32, u32, vp, ctypes.c_uint16, vp, vp, u32p]
+    L.sqobfs_udp_conn_read_quic.argtypes = [vp, vp, ctypes.c_uint16, ctypes.c_uint64, i32, vp,
+                                            ctypes.POINTER(ctypes.c_void_p)]
     L.sqobfs_udp_conn_set_offload.restype = i32
     L.sqobfs_udp_conn_open.argtypes = [vp, vp, vp, u32, u32, u32, ctypes.POINTER(vp)]
     L.sqobfs_udp_conn_close.argtypes = [vp]
@@ -457,6 +460,44 @@ class UdpConn:
         for i in range(v.count):  # copies: the next read reuses the endpoint's arrays
             out.append((ctypes.string_at(v.base + int(off[i]), int(ln[i])), int(fi[i]),
                         Addr.from_buffer_copy(addrs[i])))
+        return out
+
+    def write_quic(self, qkr: "QuicKeyring", fd_index: int, packets: list[bytes],
+                   pn_offset: int, pns: list[int], to: list[Addr]) -> int:
+        """QUIC packets (header || payload) -> one fused seal + Salamander
+        launch -> send.  Returns datagrams sent."""
+        lens = np.array([len(p) for p in packets], dtype=np.uint32)
+        for i, p in enumerate(packets):
+            self.tx_payload(i)[:len(p)] = np.frombuffer(p, np.uint8)
+        pn = np.asarray(pns, dtype=np.uint64)
+        arr = (Addr * max(len(to), 1))(*to)
+        sent = ctypes.c_uint32(0)
+        _check(lib().sqobfs_udp_conn_write_quic(self.handle, qkr.handle, fd_index, len(packets),
+                                                _ptr(lens), pn_offset, _ptr(pn), arr,
+                                                ctypes.byref(sent)), "sqobfs_udp_conn_write_quic")
+        return sent.value
+
+    def read_quic(self, qkr: "QuicKeyring", pn_offset: int, largest_pn: int,
+                  timeout_ms: int = 1000):
+        """[(packet bytes or None, out_len code, fd_index, Addr, pn)] of one
+        received batch, de-obfuscated and opened in one launch."""
+        v = UdpView()
+        pp = ctypes.c_void_p()
+        _check(lib().sqobfs_udp_conn_read_quic(self.handle, qkr.handle, pn_offset, largest_pn,
+                                               timeout_ms, ctypes.byref(v), ctypes.byref(pp)),
+               "sqobfs_udp_conn_read_quic")
+        out = []
+        if v.count == 0:
+            return out
+        off = np.ctypeslib.as_array((ctypes.c_uint64 * v.count).from_address(v.off))
+        ln = np.ctypeslib.as_array((ctypes.c_uint32 * v.count).from_address(v.len))
+        fi = np.ctypeslib.as_array((ctypes.c_uint16 * v.count).from_address(v.fd_index))
+        pn = np.ctypeslib.as_array((ctypes.c_uint64 * v.count).from_address(pp.value))
+        addrs = (Addr * v.count).from_address(v.from_)
+        for i in range(v.count):
+            n = int(ln[i])
+            data = ctypes.string_at(v.base + int(off[i]), n) if n < 0xFFFFFFF0 else None
+            out.append((data, n, int(fi[i]), Addr.from_buffer_copy(addrs[i]), int(pn[i])))
         return out
 
     def tx_payload(self, i: int) -> np.ndarray:

@@ -206,3 +206,52 @@ def test_conn_gro_fan_in_mixed_sources(ctx):
             assert by_src[(1, plain.getsockname())] == pay_p
     for s in srv + [cli_sock, plain]:
         s.close()
+
+
+@pytest.mark.parametrize("suite,offload", [(0, 0), (0, 3), (1, 3)])
+def test_conn_quic_fused(ctx, suite, offload):
+    """Hysteria2's data path through the endpoint: QUIC packets sealed and
+    Salamander-obfuscated in one launch, sent (GSO), received (GRO),
+    de-obfuscated and opened in one launch.  The wire is checked against the
+    oracle composition (or_quic_seal then the restated WriteTo), the
+    received packets and packet numbers against the originals."""
+    rng = np.random.Generator(np.random.PCG64(300 + 10 * suite + offload))
+    kl = 16 if suite else 32
+    kb = tuple(rng.integers(0, 256, m, dtype=np.uint8).tobytes() for m in (kl, 12, kl))
+    srv_sock, cli_sock, spy = _sock(), _sock(), _sock()
+    dcid = rng.integers(0, 256, 8, dtype=np.uint8).tobytes()
+    pno = 1 + len(dcid)
+    with sqobfs.Keyring(ctx, SALAMANDER, [PSK]) as kr, \
+            sqobfs.QuicKeyring(ctx, [sqobfs.QuicKey.of(*kb)], suite) as qkr, \
+            sqobfs.UdpConn(ctx, kr, [srv_sock.fileno()], slots=256) as srv, \
+            sqobfs.UdpConn(ctx, kr, [cli_sock.fileno()], slots=256) as cli:
+        cli.set_offload(offload & sqobfs.UDP_TX_GSO)
+        srv.set_offload(offload & sqobfs.UDP_RX_GRO)
+        to = Addr.of(*srv_sock.getsockname())
+        pn0 = 1000
+        for burst in range(4):
+            L = int(rng.integers(40, 1300))
+            pkts = [bytes([0x41]) + dcid + ((pn0 + i) & 0xFFFF).to_bytes(2, "big") +
+                    rng.integers(0, 256, L if i % 9 else int(rng.integers(3, L + 1)),
+                                 dtype=np.uint8).tobytes() for i in range(100)]
+            pns = [pn0 + i for i in range(100)]
+            assert cli.write_quic(qkr, 0, pkts, pno, pns, [to] * 100) == 100
+            got = []
+            while len(got) < 100:
+                b = srv.read_quic(qkr, pno, pn0 - 1, 3000)
+                assert b, f"timed out after {len(got)}"
+                got += b
+            assert [g[0] for g in got] == pkts
+            assert [g[4] for g in got] == pns
+            pn0 += 100
+        # the wire: salt || (RFC 9001 protected packet) ^ BLAKE2b(psk || salt)
+        pkts = [bytes([0x41]) + dcid + (7).to_bytes(2, "big") + b"\x33" * 200]
+        assert cli.write_quic(qkr, 0, pkts, pno, [pn0 + 7], [Addr.of(*spy.getsockname())]) == 1
+        spy.settimeout(2.0)
+        w = spy.recv(65536)
+        assert len(w) == len(pkts[0]) + 24
+        plain, n = ol.salamander_read(PSK, w)
+        want, r = ol.quic_seal(*kb, pn0 + 7, pkts[0], pno, suite=suite)
+        assert plain[:n] == want
+    for s in (srv_sock, cli_sock, spy):
+        s.close()
