@@ -467,6 +467,10 @@ def main():
                          [udp_rate(sqobfs, ctx, kr, kind, L or 758, batch=bt,
                                    offload=sqobfs.UDP_TX_GSO | sqobfs.UDP_RX_GRO)
                           for bt in (256, 1024)]
+        if kind == 0:
+            out["udp_quic_e2e"] = [udp_quic_rate(sqobfs, ctx, kr, (L or 758) + 11, batch=bt,
+                                                 suite=su)
+                                   for su in (0, 1) for bt in (256, 1024)]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:
@@ -701,6 +705,83 @@ def quic_fused_rate(torch, sqobfs, ctx, dev, steps, n, ln, data, in_off, lens, p
     res["traffic_note"] = ("two launches move read L + write L+16 + read L+16 + write L+24 "
                            "per packet; fused: read L + write L+24")
     return res
+
+
+def udp_quic_rate(sqobfs, ctx, kr, plen, seconds=3.0, batch=256, suite=0):
+    """Hysteria2's data path over loopback, one thread: QUIC packets of plen
+    bytes (11-byte short header) -> sqobfs_udp_conn_write_quic (seal +
+    Salamander in one launch, GSO send) -> sqobfs_udp_conn_read_quic (GRO
+    receive, de-obfuscate + open in one launch)."""
+    import ctypes
+    import socket
+    import numpy as np
+    rng = np.random.Generator(np.random.PCG64(13))
+
+    def sock():
+        s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        s.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 8 << 20)
+        s.bind(("127.0.0.1", 0))
+        return s
+    srv_s, cli_s = sock(), sock()
+    kl = 16 if suite else 32
+    key, iv, hp = (rng.integers(0, 256, m, dtype=np.uint8).tobytes() for m in (kl, 12, kl))
+    qkr = sqobfs.QuicKeyring(ctx, [sqobfs.QuicKey.of(key, iv, hp)], suite)
+    srv = sqobfs.UdpConn(ctx, kr, [srv_s.fileno()], slots=batch)
+    cli = sqobfs.UdpConn(ctx, kr, [cli_s.fileno()], slots=batch)
+    on = cli.set_offload(sqobfs.UDP_TX_GSO) | srv.set_offload(sqobfs.UDP_RX_GRO)
+    lib = sqobfs.lib()
+    lens = np.full(batch, plen, np.uint32)
+    to = (sqobfs.Addr * batch)(*[sqobfs.Addr.of(*srv_s.getsockname())] * batch)
+    pn = np.arange(batch, dtype=np.uint64)
+    for i in range(batch):
+        p = cli.tx_payload(i)
+        p[:plen] = rng.integers(0, 256, plen, dtype=np.uint8)
+        p[0] = 0x41
+    slot0 = lib.sqobfs_udp_conn_tx_payload(cli.handle, 0) - 8  # Salamander: S = 8
+    tx = np.ctypeslib.as_array((ctypes.c_uint8 * (batch * 2048)).from_address(slot0))
+    tx = tx.reshape(batch, 2048)
+    sent = ctypes.c_uint32(0)
+    v = sqobfs.UdpView()
+    pp = ctypes.c_void_p()
+    moved = lost = bad = 0
+    base = 0
+    t_end = time.perf_counter() + seconds
+    t0 = time.perf_counter()
+    while time.perf_counter() < t_end:
+        # headers (the in-place seal left wire bytes in the slots): first byte
+        # and the 2-byte packet number, for the whole batch at once
+        seq = np.arange(base, base + batch, dtype=np.int64)
+        tx[:, 8] = 0x41
+        tx[:, 8 + 9] = (seq >> 8) & 0xFF
+        tx[:, 8 + 10] = seq & 0xFF
+        pn[:] = np.arange(base, base + batch, dtype=np.uint64)
+        assert lib.sqobfs_udp_conn_write_quic(cli.handle, qkr.handle, 0, batch, lens.ctypes.data,
+                                              9, pn.ctypes.data, to, ctypes.byref(sent)) == 0
+        got = 0
+        while got < batch:
+            assert lib.sqobfs_udp_conn_read_quic(srv.handle, qkr.handle, 9, max(base, 1) - 1,
+                                                 200, ctypes.byref(v), ctypes.byref(pp)) == 0
+            if v.count == 0:
+                lost += batch - got
+                break
+            ln = np.ctypeslib.as_array((ctypes.c_uint32 * v.count).from_address(v.len))
+            bad += int((ln != plen).sum())
+            got += v.count
+        moved += got
+        base += batch
+    dt = time.perf_counter() - t0
+    srv.close()
+    cli.close()
+    qkr.close()
+    srv_s.close()
+    cli_s.close()
+    return {"suite": ["chacha20_poly1305", "aes_128_gcm"][suite], "quic_packet_bytes": plen,
+            "batch": batch, "offload": on, "datagrams_per_s": round(moved / dt),
+            "GiB_s_quic_payload": round(moved * (plen - 11) / dt / 2**30, 4),
+            "lost": lost, "failed_open": bad,
+            "path": "sqobfs_udp_conn_write_quic (QUIC seal + Salamander obfuscate, one launch, "
+                    "GSO sendmmsg) -> loopback -> sqobfs_udp_conn_read_quic (GRO recvmmsg, "
+                    "deobfuscate + open, one launch), one thread"}
 
 
 def udp_rate(sqobfs, ctx, kr, kind, L, seconds=3.0, batch=256, nsock=4, offload=0):
