@@ -20,7 +20,20 @@ cases = []
 L.probe_set_lds.argtypes = [ctypes.c_uint32]
 import sys
 mode = sys.argv[1] if len(sys.argv) > 1 else "sweep"
-if mode == "occ":
+if mode == "groups":
+    for lds in (0, 53000, 80000):
+        cases.append((1, 8, 3, 8, 21760, 0, lds))
+        cases.append((1, 16, 3, 8, 21760, 0, lds))
+        cases.append((6, 6, 3, 8, 21760, 0, lds))
+        cases.append((6, 6, 3, 8, 87040, 0, lds))
+elif mode == "holes":
+    for lds in (0, 80000):
+        for u in (8, 16):
+            for pat in (1, 4, 5):
+                cases.append((pat, u, 3, 8, 21760, 0, lds))
+            cases.append((4, u, 1, 8, 21760, 0, lds))
+            cases.append((5, u, 1, 8, 21760, 0, lds))
+elif mode == "occ":
     for lds in (0, 20480, 27000, 40000, 53000, 80000):
         for u in (8, 16):
             cases.append((1, u, 3, 8, 87040, 0, lds))
@@ -55,6 +68,6 @@ for pat, u, pol, off, reg, grid, lds in cases:
     e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / 10 * 1e3
-    moved = nbytes * (2 if pat in (0, 1) else 1)
+    moved = nbytes * (2 if pat in (0, 1, 4, 5, 6) else 1)
     print(json.dumps(dict(pat=pat, U=u, pol=pol, off=off, region=reg, grid=grid, lds=lds,
                           us=round(us, 1), TBps=round(moved / us / 1e6, 3))), flush=True)

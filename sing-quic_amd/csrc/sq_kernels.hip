@@ -8,29 +8,34 @@
 //   VectorisedXPlusConn.WriteTo               hysteria/xplus.go:86-98
 // for a whole ragged batch of datagrams per launch.
 //
-// Work decomposition (one wavefront = PPW = 32 packets, independent waves):
-//   1. descriptor  lane l < PPW owns packet PPW*wave + l: reads its offsets,
-//                  lengths and salt (obfs: salt array; deobfs: first S wire
-//                  bytes).
-//   2. key         lane l hashes its own packet's psk||salt (BLAKE2b-256 or
-//                  SHA-256) starting from the keyring's per-PSK midstate:
-//                  PPW different packets hashed in parallel.
-//   3. split       each packet's output is cut at 16-byte boundaries of the
-//                  DESTINATION address: "full" chunks (16 payload bytes) and
-//                  at most ~3 "edge" chunks (salt bytes, unaligned head,
-//                  tail).  A wave prefix-sum over full-chunk counts builds a
-//                  flat chunk space for the wave's packets; each packet's
-//                  addressing and its two 16-byte keystream phases go to LDS.
-//   4. edges       the owner lane writes its packet's edge chunks (byte-exact
-//                  masked stores; loads only 16-byte-aligned blocks that hold
-//                  valid bytes, so nothing outside a packet is ever touched).
-//   5. stream      the wave walks the flat chunk space, 64 lanes x U chunks
-//                  per step: one dwordx4 load, XOR with the LDS keystream,
-//                  one aligned dwordx4 store per chunk.  Chunk -> packet is a
-//                  ballot/popcount on the prefix sums held in registers.
-// Every payload byte is read once and every output byte written once; the
-// key never leaves LDS/registers.  Measured HBM traffic is 1.05x the
-// algorithmic bytes (boundary lines: DESIGN.md section 5).
+// One wavefront = one unit of kPktPerWave (32) consecutive packets, lane l
+// owning packet l; lanes 32 and 33 hold the packets just after and just
+// before the unit (the neighbours of its boundary blocks).
+//   1. descriptor  offsets, lengths, salt (obfuscate: the salt array;
+//                  deobfuscate: the first S wire bytes), the quirk table.
+//   2. key         each lane hashes its own packet's psk||salt (BLAKE2b-256
+//                  or SHA-256) from the keyring's per-PSK midstate.
+//   3. blocks      every 16-byte-aligned output block is OWNED by the packet
+//                  holding its first byte.  A packet's owned blocks are its
+//                  interior blocks (16 payload bytes: load, XOR, store) and at
+//                  most two special ones: the first (salt bytes) and the last
+//                  (its tail plus the head of the next datagram when the two
+//                  are adjacent), whose 16 bytes are precomputed from the
+//                  packet's head / tail images and the next lane's head image.
+//                  Bytes of blocks no datagram pair covers whole (gaps between
+//                  outputs) are written byte-exactly up front by the owner.
+//   4. stream      the wave walks the flat space of its owned blocks, 64 lanes
+//                  x U blocks per step, 1 KiB per wave instruction: one dwordx4
+//                  load, XOR with the LDS keystream, one aligned dwordx4 store.
+//                  A special block's load is range-checked away (it returns
+//                  zero) and its LDS "keystream" is the block's value.
+// So for back-to-back datagrams (GSO buffers, the bench's dense layout) every
+// output line is written once, whole, in address order, like a plain copy;
+// block -> packet is a ballot/popcount on prefix sums held in registers.
+// Measured on copy probes: leaving the boundary blocks to a separate pass
+// costs 7-12 % (holes) to 30 % (holes filled early) of the HBM rate, and
+// splitting wave instructions into 256-byte pieces (16 lanes per packet)
+// costs 40 %.
 #include <hip/hip_runtime.h>
 
 #include "sq_bytes.h"
@@ -40,42 +45,25 @@
 
 namespace sq {
 
-// Streaming policy of the bulk chunk loads / stores (SQ_NT bit 0: loads,
-// bit 1: stores).  Payload bytes are touched exactly once, so nontemporal
-// (`nt`) accesses keep them from displacing useful L2 lines.
+// Streaming policy of the bulk loads / stores (SQ_NT bit 0: loads, bit 1:
+// stores).  Payload bytes are touched exactly once, so nontemporal (`nt`)
+// accesses keep them from displacing useful L2 lines.
 #ifndef SQ_NT
 #define SQ_NT 3
 #endif
+// Blocks per lane per step (double-buffered: U..2U KiB of loads in flight).
 #ifndef SQ_U
 #define SQ_U 6
 #endif
-
-
-// Timing-only ablation builds (scripts/ablate.sh; never the shipped .so):
-// 1 = skip edge chunks, 2 = skip key derivation, 3 = skip the chunk stream,
-// 4 = skip edges and key derivation.
-#ifndef SQ_ABLATE
-#define SQ_ABLATE 0
-#endif
-// Packets per wavefront (<= 64).  Fewer packets per wave = shorter, more
-// numerous work units: a smaller address window in flight and a shorter
-// tail, at the price of idle lanes during the per-lane key derivation.
+// Packets per wavefront (<= 62: lanes kPktPerWave and kPktPerWave + 1 hold
+// the neighbours).
 #ifndef SQ_PPW
 #define SQ_PPW 32
 #endif
-constexpr int kPktPerWave = SQ_PPW;
-// Full chunks start and end on 64-byte line boundaries (1) or on 16-byte
-// chunk boundaries (0).
-#ifndef SQ_LINE_EDGES
-#define SQ_LINE_EDGES 0
-#endif
-#ifndef SQ_TIMELINE
-#define SQ_TIMELINE 0
-#endif
-// Wave priority experiment (timing builds): 1 = raise the priority of waves
-// once they stream, 2 = raise it while they prepare (descriptor, hash, edges).
-#ifndef SQ_PRIO
-#define SQ_PRIO 0
+// Timing-only ablation builds (never the shipped .so): bit 0 skips the key
+// derivation, bit 1 skips the byte-exact stores.
+#ifndef SQ_ABLATE
+#define SQ_ABLATE 0
 #endif
 
 #define SQ_STR2(x) #x
@@ -85,7 +73,10 @@ extern "C" const char *sqobfs_build_info(void) {
          " block=" SQ_STR(SQ_BLOCK) " ablate=" SQ_STR(SQ_ABLATE);
 }
 
-constexpr uint32_t kMaxPacket = 1u << 26;  // per-packet length bound (u32 chunk math)
+constexpr uint32_t kPktPerWave = SQ_PPW;
+static_assert(kPktPerWave >= 1 && kPktPerWave + 2 <= kWave, "unit + 2 neighbour lanes");
+
+constexpr uint32_t kMaxPacket = 1u << 26;  // per-packet length bound (u32 block math)
 constexpr uint32_t kBadPsk = 0xFFFFFFFFu;
 constexpr uint32_t kBadLen = 0xFFFFFFFEu;
 
@@ -125,7 +116,7 @@ __device__ __forceinline__ void xplus_key(const PskEntry *E,
   for (int i = 0; i < 8; i++) key[i] = __builtin_bswap32(st[i]);
 }
 
-// ------------------------------------------------------------ edge chunks
+// ------------------------------------------------------------ packet job
 
 struct PacketJob {
   uint64_t src_pay;  // address of payload byte 0 in the input
@@ -134,168 +125,7 @@ struct PacketJob {
   uint32_t pre;      // salt bytes written in front of dst_pay (obfs) or 0
 };
 
-// Output bytes [a, b) of the 16-byte output block at A (other bytes zero):
-// salt bytes and/or payload bytes XOR keystream.  Reads only the 16-byte
-// input blocks that hold payload bytes of the range.
-__device__ __forceinline__ void block_val(const PacketJob &J, const uint32_t (&key)[8],
-                                          const uint32_t (&salt)[4], uint64_t A, uint32_t a,
-                                          uint32_t b, uint32_t (&val)[4]) {
-#pragma unroll
-  for (int j = 0; j < 4; j++) val[j] = 0u;
-  const int64_t dp = (int64_t)(J.dst_pay - A);  // payload starts dp bytes into the block
-  const uint32_t pay_lo = dp > (int64_t)a ? (uint32_t)(dp < 16 ? dp : 16) : a;
-  if (pay_lo < b) {
-    const uint64_t X = J.src_pay - (uint64_t)dp;  // input address of output byte A
-    uint32_t win[4], ks[4];
-    load_window(X + pay_lo, X + b, X, win);
-    keywin(key, (uint32_t)(A - J.dst_pay) & 31u, ks);
-#pragma unroll
-    for (int j = 0; j < 4; j++) val[j] = (win[j] ^ ks[j]) & range_mask(pay_lo, b, j);
-  }
-  if (J.pre && dp > (int64_t)a) {
-    const uint32_t se = dp < (int64_t)b ? (uint32_t)dp : b;  // salt bytes [a, se)
-    const uint32_t w[12] = {0u, 0u, 0u, 0u, salt[0], salt[1], salt[2], salt[3], 0u, 0u, 0u, 0u};
-    uint32_t sw[4];
-    win16(w, (uint32_t)(16 + (int64_t)J.pre - dp), sw);
-#pragma unroll
-    for (int j = 0; j < 4; j++) val[j] |= sw[j] & range_mask(a, se, j);
-  }
-}
-
-// Byte-exact store of output bytes [A0, A1) (any alignment, edge chunks of
-// small packets and of packets without an adjacent neighbour).
-__device__ __forceinline__ void edge_span(const PacketJob &J, const uint32_t (&key)[8],
-                                          const uint32_t (&salt)[4], uint64_t A0,
-                                          uint64_t A1) {
-  for (uint64_t A = A0 & ~15ull; A < A1; A += 16) {
-    const uint32_t a = (uint32_t)((A0 > A ? A0 : A) - A);
-    const uint32_t b = (uint32_t)((A1 < A + 16 ? A1 : A + 16) - A);
-    uint32_t val[4];
-    block_val(J, key, salt, A, a, b, val);
-    store_partial(A, val, a, b);
-  }
-}
-
-// ------------------------------------------------------------ chunk stream
-
-// LDS record per packet (48 B): input/output addressing for flat chunk c
-// (addr = base + 16*c) and the keystream for even / odd c.
-struct alignas(16) ChunkRec {
-  uint64_t ssub, dsub;
-  u32x4 ks[2];
-};
-
-// Packet owning flat chunk c = b0 + lane (c < T): the last lane l with
-// start[l] <= c.  b0 is wave-uniform, so this is two ballots, a popcount and
-// a scalar walk over the (few) packets that start inside the 64-chunk window.
-// Always returns a valid record index (0..63), also for c >= T.
-__device__ __forceinline__ uint32_t locate(uint32_t start, uint32_t b0, uint32_t c) {
-  int pp = __popcll(__ballot(start <= b0)) - 1;
-  uint64_t M = __ballot(start > b0 && start < b0 + kWave);
-  while (M) {
-    const int l = __ffsll((unsigned long long)M) - 1;
-    M &= M - 1;
-    const uint32_t sl = __builtin_amdgcn_readlane(start, l);
-    pp += c >= sl ? 1 : 0;
-  }
-  return (uint32_t)pp;
-}
-
-// Buffer-resource streaming.  The wave's input and output spans (all its
-// full chunks) each fit a 32-bit buffer range, described by one SGPR
-// resource per direction.  A chunk past the end gets an offset beyond
-// num_records: the hardware range check returns zeros for its load and
-// drops its store.  So every load/store in the loop is unconditional, with
-// no padding writes and no branches, and the compiler's waitcnt accounting
-// stays exact (a conditional store makes it fall back to draining).
-constexpr uint32_t kOffNone = 0xFFFFFFF0u;
-// cache-policy bits of the stream's buffer ops (gfx950: sc0 = 1, nt = 2,
-// sc1 = 16); SQ_AUXLD / SQ_AUXST override them in timing builds
-#ifdef SQ_AUXLD
-constexpr int kAuxLd = SQ_AUXLD;
-#else
-constexpr int kAuxLd = (SQ_NT & 1) ? 2 : 0;  // nt
-#endif
-#ifdef SQ_AUXST
-constexpr int kAuxSt = SQ_AUXST;
-#else
-constexpr int kAuxSt = (SQ_NT & 2) ? 2 : 0;
-#endif
-
-struct WaveBufs {
-  __amdgpu_buffer_rsrc_t src, dst;
-  uint32_t sbase, dbase;  // low 32 bits of the span bases
-};
-
-__device__ __forceinline__ uint32_t src_off(const ChunkRec *wrec, const WaveBufs &B,
-                                            uint32_t pp, uint32_t c, uint32_t T) {
-  return c < T ? (uint32_t)wrec[pp].ssub - B.sbase + 16u * c : kOffNone;
-}
-
-template <int U>
-__device__ __forceinline__ void stream_issue(const ChunkRec *wrec, const WaveBufs &B,
-                                             uint32_t start, uint32_t T, uint32_t lane,
-                                             uint32_t base, u32x4 (&v)[U], uint32_t (&pp)[U]) {
-  uint32_t off[U];
-  // all packet lookups (SALU + ballots) first, then all LDS reads, then all
-  // loads: one LDS round trip per step instead of one per chunk
-#pragma unroll
-  for (int u = 0; u < U; u++) pp[u] = locate(start, base + u * kWave, base + u * kWave + lane);
-#pragma unroll
-  for (int u = 0; u < U; u++) off[u] = src_off(wrec, B, pp[u], base + u * kWave + lane, T);
-#pragma unroll
-  for (int u = 0; u < U; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b128(B.src, off[u], 0, kAuxLd);
-}
-
-__device__ __forceinline__ void store_chunk(const ChunkRec *wrec, const WaveBufs &B,
-                                            uint32_t pp, uint32_t c, uint32_t T, u32x4 v) {
-  const ChunkRec &R = wrec[pp];
-  const uint32_t off = c < T ? (uint32_t)R.dsub - B.dbase + 16u * c : kOffNone;
-  __builtin_amdgcn_raw_buffer_store_b128(v ^ R.ks[c & 1], B.dst, off, 0, kAuxSt);
-}
-
-// Double-buffered stream loop.  The caller has issued step 0's loads into
-// cur/cpp (before the edge chunks, so the two overlap); each iteration issues
-// step i+1's U loads before step i is XORed and stored, so a wave keeps
-// U..2U KiB of reads outstanding.  Loads past T are range-checked away.
-template <int U>
-__device__ __forceinline__ void stream_loop(const ChunkRec *wrec, const WaveBufs &B,
-                                            uint32_t start, uint32_t T, uint32_t lane,
-                                            u32x4 (&cur)[U], uint32_t (&cpp)[U]) {
-  constexpr uint32_t STEP = kWave * U;
-  for (uint32_t base = 0; base < T; base += STEP) {
-    u32x4 nxt[U];
-    uint32_t npp[U];
-    stream_issue<U>(wrec, B, start, T, lane, base + STEP, nxt, npp);
-#pragma unroll
-    for (int u = 0; u < U; u++) store_chunk(wrec, B, cpp[u], base + u * kWave + lane, T, cur[u]);
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      cur[u] = nxt[u];
-      cpp[u] = npp[u];
-    }
-  }
-}
-
-// Fallback for waves whose spans exceed a 32-bit buffer range or whose
-// input chunks are not 4-byte aligned: global accesses, any alignment
-// (two aligned 16-byte loads + byte funnel per chunk), one chunk per lane.
-__device__ __noinline__ void stream_generic(const ChunkRec *wrec, uint32_t start, uint32_t T,
-                                            uint32_t lane) {
-  for (uint32_t b0 = 0; b0 < T; b0 += kWave) {
-    const uint32_t c = min(b0 + lane, T - 1);
-    const ChunkRec &R = wrec[locate(start, b0, c)];
-    const uint64_t sa = R.ssub + 16ull * c;
-    uint32_t w[4];
-    if ((sa & 3) == 0) {
-      const u32x4 x = gld<u32x4_a4>(sa);
-      w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
-    } else {
-      load_window(sa, sa + 16, sa, w);
-    }
-    if (b0 + lane < T) gst<u32x4>(R.dsub + 16ull * c, u32x4{w[0], w[1], w[2], w[3]} ^ R.ks[c & 1]);
-  }
-}
+// ------------------------------------------------------------ wave helpers
 
 // 64-bit wave min / max (butterfly), result wave-uniform.
 __device__ __forceinline__ uint64_t wave_min64(uint64_t x) {
@@ -318,37 +148,13 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
   return b2_pack(__builtin_amdgcn_readfirstlane((uint32_t)x),
                  __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)));
 }
-
-// Timing-only timeline builds (SQ_TIMELINE=1, never the shipped .so): every
-// stream wave records s_memrealtime (100 MHz) at start, at the start of its
-// stream and at exit; scripts/timeline.py reads them back after one launch.
-#if SQ_TIMELINE
-constexpr uint64_t kTimelineWaves = 1u << 20;
-__device__ uint64_t g_timeline[3 * kTimelineWaves];
-extern "C" int sq_timeline_copy(uint64_t *host, uint64_t waves) {
-  if (waves > kTimelineWaves) waves = kTimelineWaves;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_timeline), 3 * 8 * waves, 0,
-                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+__device__ __forceinline__ uint64_t shfl64(uint64_t x, uint32_t src) {
+  return b2_pack((uint32_t)__shfl((int)(uint32_t)x, (int)src, kWave),
+                 (uint32_t)__shfl((int)(uint32_t)(x >> 32), (int)src, kWave));
 }
-struct TimelineRec {
-  uint64_t t0, t1;
-  __device__ ~TimelineRec() {
-    if ((threadIdx.x & (kWave - 1)) == 0) {
-      const uint64_t w = (uint64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
-      if (w < kTimelineWaves) {
-        g_timeline[3 * w] = t0;
-        g_timeline[3 * w + 1] = t1;
-        g_timeline[3 * w + 2] = __builtin_amdgcn_s_memrealtime();
-      }
-    }
-  }
-};
-#define SQ_TL_START const uint64_t tl0_ = __builtin_amdgcn_s_memrealtime();
-#define SQ_TL_STREAM TimelineRec tl_rec_{tl0_, __builtin_amdgcn_s_memrealtime()};
-#else
-#define SQ_TL_START
-#define SQ_TL_STREAM
-#endif
+__device__ __forceinline__ uint32_t shfl32(uint32_t x, uint32_t src) {
+  return (uint32_t)__shfl((int)x, (int)src, kWave);
+}
 
 // ------------------------------------------------------------ per-packet steps
 
@@ -381,34 +187,63 @@ __device__ __forceinline__ void device_salt(const KParams &P, uint32_t p, uint32
   }
 }
 
-// Step 1, descriptor: packet p's job (addresses and length of the XOR
-// stream, salt bytes to prepend), its salt (obfuscate: the salt array;
-// deobfuscate: the first S wire bytes), whether it needs a key, and its
-// out_len (the quirk table of include/sqobfs.h).
+// Step 1, descriptor, in two halves so the persistent kernel can prefetch
+// it one work unit ahead.  fetch_desc issues the loads of packet p's batch
+// entry (offsets, lengths, psk id, XPlus capacity, obfuscate salt);
+// finalize_desc applies the quirk table of include/sqobfs.h and gives the
+// packet's job (addresses and length of the XOR stream, salt bytes to
+// prepend), its salt (deobfuscate: the first S wire bytes, a dependent
+// load), whether it needs a key, and its out_len.
+struct RawDesc {
+  uint64_t ioff, ooff;
+  uint32_t len, cap, pid;
+  uint32_t salt[4];
+};
+
 template <int KIND, int DIR, bool MULTI>
-__device__ __forceinline__ void describe(const KParams &P, uint32_t p, bool valid, PacketJob &J,
-                                         uint32_t (&salt)[4], bool &do_hash,
-                                         const PskEntry *&E, uint32_t &olen) {
+__device__ __forceinline__ void fetch_desc(const KParams &P, uint32_t p, bool valid, RawDesc &d) {
+  constexpr uint32_t S = KIND == 0 ? kSalamanderSalt : kXPlusSalt;
+  d.ioff = d.ooff = 0;
+  d.len = d.cap = d.pid = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) d.salt[k] = 0u;
+  if (!valid) return;
+  d.ioff = P.in_off[p];
+  d.ooff = P.out_off[p];
+  d.len = P.in_len[p];
+  if (MULTI) d.pid = P.psk_id[p];
+  if (KIND == 1 && DIR == 1 && P.in_cap) d.cap = P.in_cap[p];
+  if (DIR == 0 && !P.device_salt) {
+    const uint32_t *sp = reinterpret_cast<const uint32_t *>(P.salt + (uint64_t)p * S);
+#pragma unroll
+    for (uint32_t k = 0; k < S / 4; k++) d.salt[k] = sp[k];
+  }
+}
+
+template <int KIND, int DIR, bool MULTI>
+__device__ __forceinline__ void finalize_desc(const KParams &P, uint32_t p, bool valid,
+                                              const RawDesc &d, PacketJob &J,
+                                              uint32_t (&salt)[4], bool &do_hash,
+                                              const PskEntry *&E, uint32_t &olen) {
   constexpr uint32_t S = KIND == 0 ? kSalamanderSalt : kXPlusSalt;
   J = {0, 0, 0, 0};
   do_hash = false;
-  E = &P.psk0;
+  // single PSK: the kernarg copy (scalar loads); several: the device table
+  // (never a pointer that may be either: that forces a flat copy of P)
+  E = MULTI ? P.psk_table : &P.psk0;
   olen = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) salt[k] = 0u;
   if (!valid) return;
-  const uint64_t in_base = (uint64_t)P.in + P.in_off[p];
-  const uint64_t out_base = (uint64_t)P.out + P.out_off[p];
-  const uint32_t len = P.in_len[p];
+  const uint64_t in_base = (uint64_t)P.in + d.ioff;
+  const uint64_t out_base = (uint64_t)P.out + d.ooff;
+  const uint32_t len = d.len;
   bool bad = false;
   if (MULTI) {
-    const uint32_t pid = P.psk_id[p];
-    if (pid >= P.n_psk) bad = true;
-    else E = P.psk_table + pid;
+    if (d.pid >= P.n_psk) bad = true;
+    else E = P.psk_table + d.pid;
   }
-  uint32_t cap = len;
-  if (KIND == 1 && DIR == 1 && P.in_cap) {
-    const uint32_t c = P.in_cap[p];
-    cap = c > len ? c : len;
-  }
+  const uint32_t cap = d.cap > len ? d.cap : len;  // xplus.go:55 XORs to len(p)
   if (len > kMaxPacket || cap > kMaxPacket) {
     olen = kBadLen;
   } else if (bad) {
@@ -417,9 +252,8 @@ __device__ __forceinline__ void describe(const KParams &P, uint32_t p, bool vali
     if (P.device_salt) {
       device_salt<S>(P, p, salt);
     } else {
-      const uint32_t *sp = reinterpret_cast<const uint32_t *>(P.salt + (uint64_t)p * S);
 #pragma unroll
-      for (uint32_t k = 0; k < S / 4; k++) salt[k] = sp[k];
+      for (uint32_t k = 0; k < S / 4; k++) salt[k] = d.salt[k];
     }
     J = {in_base, out_base + S, len, S};
     olen = S + len;
@@ -447,139 +281,418 @@ __device__ __forceinline__ void derive_key(bool do_hash, const PskEntry *E,
                                            const uint32_t (&salt)[4], uint32_t (&key)[8]) {
 #pragma unroll
   for (int i = 0; i < 8; i++) key[i] = 0u;
-#if SQ_ABLATE == 2 || SQ_ABLATE == 4  // timing-only build: no key derivation
-  if (do_hash) { key[0] = salt[0]; key[1] = salt[1]; do_hash = false; }
-#endif
+  if (SQ_ABLATE & 1) {
+    key[0] = salt[0];
+    key[1] = salt[1];
+    do_hash = false;
+  }
   if (do_hash) {
     if (KIND == 0) salamander_key(E, salt, key);
     else xplus_key(E, salt, key);
   }
 }
 
-// Steps 3-5 for the packets of one wave (one per lane, any subset of lanes
-// may be idle with J.len == 0):
-//   3. split every packet's output at 16-byte boundaries of the destination
-//      into full chunks (a flat chunk space over the wave, by prefix sum) and
-//      edges (salt bytes, unaligned head, tail);
-//   4. write the edges (owner lane, byte-exact, plain stores);
-//   5. stream the flat chunk space with nt loads and stores.
-// The edge bytes of a boundary line and the nt stream stores of the rest of
-// that line merge in L2: skipping the edges (SQ_ABLATE=1) leaves those lines
-// partial and costs ~10 %.  SQ_LINE_EDGES=1 (timing builds) instead streams
-// only whole 64-byte lines and writes the boundary lines as edges: no
-// partial nt stores at all, but the longer edge phase costs ~3 % more than
-// it saves.
-template <int U>
-__device__ __forceinline__ void transform(const PacketJob &J, const uint32_t (&key)[8],
-                                          const uint32_t (&salt)[4], uint32_t lane,
-                                          ChunkRec *wrec) {
-  // ---- 3. split into full chunks (flat, streamed) and edges (owner lane)
-  constexpr uint64_t kAl = SQ_LINE_EDGES ? 64 : 16;
-  const uint64_t rs = J.dst_pay - J.pre, re = J.dst_pay + J.len;
-  const uint64_t fa = (J.dst_pay + kAl - 1) & ~(kAl - 1), fb = re & ~(kAl - 1);
-  const uint32_t F = (J.len && fb > fa) ? (uint32_t)((fb - fa) >> 4) : 0u;
+// ------------------------------------------------------------ one unit
+
+// Lane roles: lanes 0 .. kPktPerWave-1 own packets; lane kPktPerWave holds
+// the packet right after the unit and lane kPktPerWave + 1 the one right
+// before it (the neighbours of its boundary blocks: they own and write
+// nothing).
+__device__ __forceinline__ uint32_t lane_packet(uint64_t unit, uint32_t lane, uint32_t n,
+                                                bool &valid, bool &owner) {
+  const int64_t base = (int64_t)unit * kPktPerWave;
+  int64_t p = -1;
+  if (lane < kPktPerWave) p = base + lane;
+  else if (lane == kPktPerWave) p = base + kPktPerWave;
+  else if (lane == kPktPerWave + 1) p = base - 1;
+  valid = p >= 0 && p < (int64_t)n;
+  owner = valid && lane < kPktPerWave;
+  return valid ? (uint32_t)p : 0u;
+}
+
+// Output range [rs, re) of a packet's job (empty: ne == false).
+__device__ __forceinline__ void out_range(const PacketJob &J, uint64_t &rs, uint64_t &re,
+                                          bool &ne) {
+  ne = J.len != 0 || J.pre != 0;
+  rs = J.dst_pay - J.pre;
+  re = J.dst_pay + J.len;
+}
+
+__device__ __forceinline__ uint64_t up16(uint64_t a) { return (a + 15) & ~15ull; }
+
+// The last partial output block [BL, re) needs payload bytes the 32-byte
+// head image does not hold.
+__device__ __forceinline__ bool tail_from_window(uint64_t rs, uint64_t re) {
+  return (re & 15) && (re & ~15ull) > rs + 16;
+}
+
+// The input blocks the packet's images need, all loaded together: the head
+// window (payload bytes [0, 32 - pre)) and the tail window (payload bytes of
+// the last partial output block).  Only blocks holding valid bytes are read.
+struct Windows {
+  u32x4 h0, h1, h2, t0, t1;
+};
+
+__device__ __forceinline__ void fetch_windows(const PacketJob &J, Windows &W) {
+  const u32x4 z = {0u, 0u, 0u, 0u};
+  W.h0 = W.h1 = W.h2 = W.t0 = W.t1 = z;
+  uint64_t rs, re;
+  bool ne;
+  out_range(J, rs, re, ne);
+  if (!ne) return;
+  const uint64_t hw = J.len < 32 - J.pre ? J.len : 32 - J.pre;
+  if (hw) {
+    const uint64_t B = J.src_pay & ~15ull, e = J.src_pay + hw;
+    W.h0 = gld<u32x4>(B);
+    if (e > B + 16) W.h1 = gld<u32x4>(B + 16);
+    if (e > B + 32) W.h2 = gld<u32x4>(B + 32);
+  }
+  if (tail_from_window(rs, re)) {
+    const uint64_t ta = J.src_pay + ((re & ~15ull) - J.dst_pay), te = J.src_pay + J.len;
+    const uint64_t B = ta & ~15ull;
+    W.t0 = gld<u32x4>(B);
+    if (te > B + 16) W.t1 = gld<u32x4>(B + 16);
+  }
+}
+
+// LDS record of a packet (96 B).  Flat block c of the unit, owned by this
+// packet, is at input ssub + 16 c and output dsub + 16 c; its keystream is
+// ks[c & 1], except the special blocks c == sidx (first, value vf) and
+// c == eidx (last, value vl), whose loads are range-checked away.
+struct alignas(16) ChunkRec {
+  uint64_t ssub, dsub;
+  uint32_t sidx, eidx, pad0, pad1;
+  u32x4 ks[2];
+  u32x4 vf, vl;
+};
+static_assert(sizeof(ChunkRec) == 96, "ChunkRec layout");
+
+struct WaveBufs {
+  __amdgpu_buffer_rsrc_t src, dst;
+  uint32_t sbase, dbase;  // low 32 bits of the span bases
+};
+
+struct UnitStream {
+  uint32_t start;  // lane: flat index of its packet's first block
+  uint32_t T;      // wave-uniform: blocks in the flat space
+  bool fast;       // wave-uniform: buffer-resource streaming possible
+  WaveBufs B;
+};
+
+constexpr uint32_t kNoIdx = 0xFFFFFFFFu;
+constexpr uint64_t kMaxSpan = 0xFFFFFF00ull;
+
+// Key, images, neighbour exchange, block ownership, special blocks,
+// byte-exact stores, flat prefix sum, LDS records and buffer resources.
+// Every lane of the wave runs it.
+template <int KIND, int DIR, bool MULTI>
+__device__ __forceinline__ UnitStream prepare_unit(const KParams &P, const PacketJob &J,
+                                                   const uint32_t (&salt)[4], bool do_hash,
+                                                   uint32_t pid, const Windows &W, bool owner,
+                                                   uint32_t lane, ChunkRec *recs) {
+  constexpr uint32_t S = KIND == 0 ? kSalamanderSalt : kXPlusSalt;
+  constexpr uint32_t PW = DIR == 0 ? S / 4 : 0;  // salt words in front of the payload
+  uint32_t key[8];
+  // single PSK: the kernarg copy (scalar loads); several: the device table
+  derive_key<KIND>(do_hash, MULTI ? P.psk_table + pid : &P.psk0, salt, key);
+
+  uint64_t rs, re;
+  bool ne;
+  out_range(J, rs, re, ne);
+  // head image: output bytes [rs, rs + 32) = salt || payload ^ key
+  uint32_t hi[8];
+  {
+    const uint32_t o = (uint32_t)(J.src_pay & 15);
+    const uint32_t w0[12] = {0u, 0u, 0u, 0u, W.h0.x, W.h0.y, W.h0.z, W.h0.w,
+                             W.h1.x, W.h1.y, W.h1.z, W.h1.w};
+    const uint32_t w1[12] = {W.h0.x, W.h0.y, W.h0.z, W.h0.w, W.h1.x, W.h1.y,
+                             W.h1.z, W.h1.w, W.h2.x, W.h2.y, W.h2.z, W.h2.w};
+    uint32_t pa[4], pb[4];
+    win16(w0, o + 16, pa);
+    win16(w1, o + 16, pb);
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      if ((uint32_t)i < PW) {
+        hi[i] = salt[i];
+      } else {
+        const int k = i - (int)PW;
+        hi[i] = (k < 4 ? pa[k] : pb[k - 4]) ^ key[k];
+      }
+    }
+  }
+  const uint32_t hx[12] = {hi[0], hi[1], hi[2], hi[3], hi[4], hi[5], hi[6], hi[7], 0u, 0u, 0u, 0u};
+  // tail image: bytes [BL, re) of the last partial output block
+  const uint64_t BL = re & ~15ull;
+  const uint32_t t = (uint32_t)(re & 15);
+  uint32_t ti[4];
+  if (tail_from_window(rs, re)) {
+    const uint64_t ta = J.src_pay + (BL - J.dst_pay);
+    const uint32_t w[12] = {0u, 0u, 0u, 0u, W.t0.x, W.t0.y, W.t0.z, W.t0.w,
+                            W.t1.x, W.t1.y, W.t1.z, W.t1.w};
+    uint32_t ks[4];
+    win16(w, (uint32_t)(ta & 15) + 16, ti);
+    keywin(key, (uint32_t)(BL - J.dst_pay) & 31u, ks);
+#pragma unroll
+    for (int j = 0; j < 4; j++) ti[j] ^= ks[j];
+  } else {
+    win16(hx, (uint32_t)(BL - rs) & 31u, ti);  // BL - rs <= 16 here (or no tail)
+  }
+  // in place (input overlaps its own output blocks): a neighbour in another
+  // wave must not read or write across this packet's blocks
+  const uint64_t oblo = rs & ~15ull, obhi = up16(re);
+  const bool ovl = ne && J.len && J.src_pay < obhi && J.src_pay + J.len > oblo;
+
+  // neighbours: next lane = next packet (lane kPktPerWave for the last one),
+  // previous lane = previous packet (lane kPktPerWave + 1 for the first one)
+  const uint32_t nl = (lane + 1) & (kWave - 1);
+  const uint32_t pl = lane == 0 ? kPktPerWave + 1 : lane - 1;
+  const uint64_t rs_n = shfl64(rs, nl), re_n = shfl64(re, nl);
+  const uint64_t rs_p = shfl64(rs, pl), re_p = shfl64(re, pl);
+  const uint32_t fl = (ne ? 1u : 0u) | (ovl ? 2u : 0u);
+  const uint32_t fl_n = shfl32(fl, nl), fl_p = shfl32(fl, pl);
+  uint32_t hn[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) hn[j] = shfl32(hi[j], nl);
+
+  // owned blocks [B0, E)
+  const uint64_t B0 = up16(rs), E = up16(re);
+  const uint32_t nblk = (owner && ne && E > B0) ? (uint32_t)((E - B0) >> 4) : 0u;
+  const bool hl = nblk && t;  // last owned block partly this packet's
+  const bool hf = nblk && B0 < J.dst_pay && !(hl && B0 == BL);
+  const bool cross_n = lane == kPktPerWave - 1, cross_p = lane == 0;
+  // last block whole: the next datagram starts at re and fills the block
+  const bool lfull = hl && (fl_n & 1) && rs_n == re && re_n >= E && !(cross_n && (fl_n & 2));
+  // leading bytes [rs, B0) covered by the previous packet's whole last block
+  // (the same predicate as the previous lane's lfull)
+  const bool p_hl = (fl_p & 1) && (re_p & 15) && up16(re_p) > up16(rs_p);
+  const bool pfull = p_hl && ne && re_p == rs && re >= B0 && !(cross_p && ovl);
+
+  // byte-exact stores of the bytes no datagram pair covers whole
+  if (!(SQ_ABLATE & 2) && owner && ne) {
+    if ((rs & 15) && !pfull) {
+      const uint64_t lend = re < B0 ? re : B0;
+      const uint32_t v[4] = {hi[0], hi[1], hi[2], hi[3]};
+      store16(rs, v, (uint32_t)(lend - rs));
+    }
+    if (hl && !lfull) store16(BL, ti, t);
+  }
+
+  // special blocks
+  uint32_t vf[4] = {0u, 0u, 0u, 0u}, vl[4] = {0u, 0u, 0u, 0u};
+  if (hf) win16(hx, (uint32_t)(B0 - rs), vf);
+  if (lfull) {
+    const uint32_t w[12] = {0u, 0u, 0u, 0u, hn[0], hn[1], hn[2], hn[3], 0u, 0u, 0u, 0u};
+    uint32_t sh[4];
+    win16(w, 16 - t, sh);
+#pragma unroll
+    for (int j = 0; j < 4; j++) vl[j] = (ti[j] & range_mask(0, (int)t, j)) | sh[j];
+  }
+
+  // the flat block space: this packet's blocks [B0, B0 + 16 F)
+  const uint32_t F = (hl && !lfull) ? nblk - 1 : nblk;
   uint32_t incl = F;
 #pragma unroll
   for (int d = 1; d < kWave; d <<= 1) {
     const uint32_t y = __shfl_up(incl, d, kWave);
     if (lane >= (uint32_t)d) incl += y;
   }
-  const uint32_t start = incl - F;
-  const uint32_t T = __shfl(incl, kWave - 1, kWave);
-  const uint64_t s_first = J.src_pay + (fa - J.dst_pay);  // input of the first full chunk
+  UnitStream U;
+  U.start = incl - F;
+  U.T = __builtin_amdgcn_readfirstlane(__shfl(incl, kWave - 1, kWave));
+  // interior blocks [i_lo, i_hi): the only ones loaded
+  const uint32_t i_lo = hf ? 1u : 0u, i_hi = hl ? nblk - 1 : nblk;
+  const bool has_int = i_hi > i_lo;
+  const uint64_t sabs = B0 + (J.src_pay - J.dst_pay);  // input of block B0
+  const uint64_t s_first = sabs + 16ull * i_lo, s_end = sabs + 16ull * i_hi;
   {
     uint32_t k0[4], k1[4];
-    const uint32_t r0 = (uint32_t)(fa - J.dst_pay) & 31u;
-    keywin(key, r0, k0);
-    keywin(key, r0 + 16, k1);
-    const bool odd = start & 1;
+    const uint32_t ph = (uint32_t)(B0 - J.dst_pay) & 31u;
+    keywin(key, ph, k0);
+    keywin(key, (ph + 16) & 31u, k1);
+    const bool odd = U.start & 1;
     ChunkRec R;
-    R.ssub = s_first - 16ull * start;
-    R.dsub = fa - 16ull * start;
+    R.ssub = sabs - 16ull * U.start;
+    R.dsub = B0 - 16ull * U.start;
+    R.sidx = hf ? U.start : kNoIdx;
+    R.eidx = lfull ? U.start + nblk - 1 : kNoIdx;
+    R.pad0 = R.pad1 = 0;
     R.ks[0] = u32x4{bsel(odd, k1[0], k0[0]), bsel(odd, k1[1], k0[1]),
                     bsel(odd, k1[2], k0[2]), bsel(odd, k1[3], k0[3])};
     R.ks[1] = u32x4{bsel(odd, k0[0], k1[0]), bsel(odd, k0[1], k1[1]),
                     bsel(odd, k0[2], k1[2]), bsel(odd, k0[3], k1[3])};
-    wrec[lane] = R;
+    R.vf = u32x4{vf[0], vf[1], vf[2], vf[3]};
+    R.vl = u32x4{vl[0], vl[1], vl[2], vl[3]};
+    recs[lane] = R;
   }
-  // wave spans of the full chunks, for the two buffer resources
-  const bool has = F != 0;
-  const uint64_t s_lo = uniform64(wave_min64(has ? s_first : ~0ull));
-  const uint64_t s_hi = uniform64(wave_max64(has ? s_first + 16ull * F : 0ull));
-  const uint64_t d_lo = uniform64(wave_min64(has ? fa : ~0ull));
-  const uint64_t d_hi = uniform64(wave_max64(has ? fb : 0ull));
-  const bool mis = has && (s_first & 3);
-  constexpr uint64_t kMaxSpan = 0xFFFFFF00ull;
-  const bool fast = T != 0 && SQ_ABLATE != 3 && __ballot(mis) == 0 &&
-                    s_hi - s_lo <= kMaxSpan && d_hi - d_lo <= kMaxSpan;
+  // spans: output of every flat block, input of every interior block
+  const uint64_t d_lo = uniform64(wave_min64(F ? B0 : ~0ull));
+  const uint64_t d_hi = uniform64(wave_max64(F ? B0 + 16ull * F : 0ull));
+  const uint64_t s_lo = uniform64(wave_min64(has_int ? s_first : ~0ull));
+  const uint64_t s_hi = uniform64(wave_max64(has_int ? s_end : 0ull));
+  const bool mis = has_int && (sabs & 3);
+  const bool sok = s_hi <= s_lo || s_hi - s_lo <= kMaxSpan;
+  U.fast = U.T != 0 && __ballot(mis) == 0 && d_hi - d_lo <= kMaxSpan && sok;
+  if (U.fast) {
+    const bool si = s_hi > s_lo;
+    U.B.src = __builtin_amdgcn_make_buffer_rsrc((void *)(si ? s_lo : d_lo), 0,
+                                                (int)(si ? (uint32_t)(s_hi - s_lo) : 0u),
+                                                0x00020000);
+    U.B.dst = __builtin_amdgcn_make_buffer_rsrc((void *)d_lo, 0, (int)(uint32_t)(d_hi - d_lo),
+                                                0x00020000);
+    U.B.sbase = (uint32_t)(si ? s_lo : d_lo);
+    U.B.dbase = (uint32_t)d_lo;
+  }
   // LDS records visible to the whole wave (same-wave LDS ops are ordered;
   // this is a compiler barrier plus the LDS drain)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  SQ_TL_STREAM
-#if SQ_PRIO == 1
-  __builtin_amdgcn_s_setprio(3);
-#elif SQ_PRIO == 2
-  __builtin_amdgcn_s_setprio(0);
-#endif
-
-  // ---- 4. edges: salt bytes and the partial lines at both ends.  They never
-  // overlap the full chunks' input or output bytes.
-  if (SQ_ABLATE != 1 && SQ_ABLATE != 4 && re > rs) {
-    if (F) {
-      edge_span(J, key, salt, rs, fa);
-      edge_span(J, key, salt, fb, re);
-    } else {
-      edge_span(J, key, salt, rs, re);
-    }
-  }
-
-  WaveBufs B;
-  u32x4 cur[U];
-  uint32_t cpp[U];
-  if (fast) {
-    B.src = __builtin_amdgcn_make_buffer_rsrc((void *)s_lo, 0, (int)(uint32_t)(s_hi - s_lo),
-                                              0x00020000);
-    B.dst = __builtin_amdgcn_make_buffer_rsrc((void *)d_lo, 0, (int)(uint32_t)(d_hi - d_lo),
-                                              0x00020000);
-    B.sbase = (uint32_t)s_lo;
-    B.dbase = (uint32_t)d_lo;
-    stream_issue<U>(wrec, B, start, T, lane, 0, cur, cpp);
-  }
-
-  // ---- 5. stream the flat full-chunk space
-  if (fast) stream_loop<U>(wrec, B, start, T, lane, cur, cpp);
-  else if (T != 0 && SQ_ABLATE != 3) stream_generic(wrec, start, T, lane);
+  return U;
 }
 
-// ------------------------------------------------------------ kernels
+// ------------------------------------------------------------ stream
 
-// The kernel: each wave owns kPktPerWave consecutive packets (descriptor ->
-// key -> transform).  A two-pass variant (a key kernel with 64 hashes per
-// wave, then short stream-only tiles of 4-32 packets per wave) was measured
-// and dropped: its key pass alone took 74-85 us on configs[1] and the stream
-// pass was no faster than this kernel's stream.
+// Packet owning flat block c = b0 + lane (c < T): the last lane l with
+// start[l] <= c.  b0 is wave-uniform, so this is two ballots, a popcount and
+// a scalar walk over the (few) packets that start inside the 64-block window.
+// Always returns a valid record index (0..63), also for c >= T.
+__device__ __forceinline__ uint32_t locate(uint32_t start, uint32_t b0, uint32_t c) {
+  int pp = __popcll(__ballot(start <= b0)) - 1;
+  uint64_t M = __ballot(start > b0 && start < b0 + kWave);
+  while (M) {
+    const int l = __ffsll((unsigned long long)M) - 1;
+    M &= M - 1;
+    const uint32_t sl = __builtin_amdgcn_readlane(start, l);
+    pp += c >= sl ? 1 : 0;
+  }
+  return (uint32_t)pp;
+}
+
+// Buffer-resource streaming.  The wave's input and output spans each fit a
+// 32-bit buffer range, described by one SGPR resource per direction.  A
+// block past the end (or a special block's load) gets an offset beyond
+// num_records: the hardware range check returns zeros for its load and
+// drops its store.  So every load/store in the loop is unconditional, with
+// no branches, and the compiler's waitcnt accounting stays exact (a
+// conditional store makes it fall back to draining).
+constexpr uint32_t kOffNone = 0xFFFFFFF0u;
+// cache-policy bits of the stream's buffer ops (gfx950: sc0 = 1, nt = 2,
+// sc1 = 16); SQ_AUXLD / SQ_AUXST override them in timing builds
+#ifdef SQ_AUXLD
+constexpr int kAuxLd = SQ_AUXLD;
+#else
+constexpr int kAuxLd = (SQ_NT & 1) ? 2 : 0;  // nt
+#endif
+#ifdef SQ_AUXST
+constexpr int kAuxSt = SQ_AUXST;
+#else
+constexpr int kAuxSt = (SQ_NT & 2) ? 2 : 0;
+#endif
+
+template <int U>
+__device__ __forceinline__ void stream_issue(const ChunkRec *wrec, const WaveBufs &B,
+                                             uint32_t start, uint32_t T, uint32_t lane,
+                                             uint32_t base, u32x4 (&v)[U], uint32_t (&pp)[U]) {
+  uint32_t off[U];
+  // all packet lookups (SALU + ballots) first, then all LDS reads, then all
+  // loads: one LDS round trip per step instead of one per block
+#pragma unroll
+  for (int u = 0; u < U; u++) pp[u] = locate(start, base + u * kWave, base + u * kWave + lane);
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const uint32_t c = base + u * kWave + lane;
+    const ChunkRec &R = wrec[pp[u]];
+    const bool ld = c < T && c != R.sidx && c != R.eidx;
+    off[u] = ld ? (uint32_t)R.ssub - B.sbase + 16u * c : kOffNone;
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b128(B.src, off[u], 0, kAuxLd);
+}
+
+__device__ __forceinline__ void store_chunk(const ChunkRec *wrec, const WaveBufs &B,
+                                            uint32_t pp, uint32_t c, uint32_t T, u32x4 v) {
+  const ChunkRec &R = wrec[pp];
+  const uint32_t off = c < T ? (uint32_t)R.dsub - B.dbase + 16u * c : kOffNone;
+  // a special block loaded zero: its "keystream" is its value
+  const u32x4 *kp = c == R.sidx ? &R.vf : (c == R.eidx ? &R.vl : &R.ks[c & 1]);
+  __builtin_amdgcn_raw_buffer_store_b128(v ^ *kp, B.dst, off, 0, kAuxSt);
+}
+
+// Double-buffered stream loop.  The caller has issued step 0's loads into
+// cur/cpp; each iteration issues step i+1's U loads before step i is XORed
+// and stored, so a wave keeps U..2U KiB of reads outstanding.
+template <int U>
+__device__ __forceinline__ void stream_loop(const ChunkRec *wrec, const WaveBufs &B,
+                                            uint32_t start, uint32_t T, uint32_t lane,
+                                            u32x4 (&cur)[U], uint32_t (&cpp)[U]) {
+  constexpr uint32_t STEP = kWave * U;
+  for (uint32_t base = 0; base < T; base += STEP) {
+    u32x4 nxt[U];
+    uint32_t npp[U];
+    stream_issue<U>(wrec, B, start, T, lane, base + STEP, nxt, npp);
+#pragma unroll
+    for (int u = 0; u < U; u++) store_chunk(wrec, B, cpp[u], base + u * kWave + lane, T, cur[u]);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      cur[u] = nxt[u];
+      cpp[u] = npp[u];
+    }
+  }
+}
+
+// Fallback for waves whose spans exceed a 32-bit buffer range or whose
+// input is not 4-byte aligned: global accesses, any alignment (two aligned
+// 16-byte loads + byte funnel per block), one block per lane.
+__device__ __noinline__ void stream_generic(const ChunkRec *wrec, uint32_t start, uint32_t T,
+                                            uint32_t lane) {
+  for (uint32_t b0 = 0; b0 < T; b0 += kWave) {
+    const uint32_t c = min(b0 + lane, T - 1);
+    const ChunkRec &R = wrec[locate(start, b0, c)];
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    u32x4 k = R.ks[c & 1];
+    if (c == R.sidx) {
+      k = R.vf;
+    } else if (c == R.eidx) {
+      k = R.vl;
+    } else {
+      const uint64_t sa = R.ssub + 16ull * c;
+      load_window(sa, sa + 16, sa, w);
+    }
+    if (b0 + lane < T) gst<u32x4>(R.dsub + 16ull * c, u32x4{w[0], w[1], w[2], w[3]} ^ k);
+  }
+}
+
+// ------------------------------------------------------------ the kernel
+
 template <int KIND, int DIR, bool MULTI, int U>
 __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
   __shared__ ChunkRec recs[kWavesPerBlock][kWave];
-  SQ_TL_START
-#if SQ_PRIO == 2
-  __builtin_amdgcn_s_setprio(3);
-#endif
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wv = threadIdx.x / kWave;
-  const uint64_t p64 = ((uint64_t)blockIdx.x * kWavesPerBlock + wv) * kPktPerWave + lane;
-  const bool valid = lane < (uint32_t)kPktPerWave && p64 < P.n;
-  const uint32_t p = (uint32_t)p64;
+  const uint64_t unit = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
+  bool valid, owner;
+  const uint32_t p = lane_packet(unit, lane, P.n, valid, owner);
+  RawDesc d;
+  fetch_desc<KIND, DIR, MULTI>(P, p, valid, d);
   PacketJob J;
-  uint32_t salt[4] = {0u, 0u, 0u, 0u};
+  uint32_t salt[4];
   bool do_hash;
   const PskEntry *E;
   uint32_t olen;
-  describe<KIND, DIR, MULTI>(P, p, valid, J, salt, do_hash, E, olen);
-  if (valid) P.out_len[p] = olen;
-  uint32_t key[8];
-  derive_key<KIND>(do_hash, E, salt, key);
-  transform<U>(J, key, salt, lane, recs[wv]);
+  finalize_desc<KIND, DIR, MULTI>(P, p, valid, d, J, salt, do_hash, E, olen);
+  (void)E;
+  Windows W;
+  fetch_windows(J, W);
+  if (owner) P.out_len[p] = olen;
+  const uint32_t pid = MULTI && d.pid < P.n_psk ? d.pid : 0u;
+  const UnitStream S =
+      prepare_unit<KIND, DIR, MULTI>(P, J, salt, do_hash, pid, W, owner, lane, recs[wv]);
+  u32x4 cur[U];
+  uint32_t cpp[U];
+  if (S.fast) {
+    stream_issue<U>(recs[wv], S.B, S.start, S.T, lane, 0, cur, cpp);
+    stream_loop<U>(recs[wv], S.B, S.start, S.T, lane, cur, cpp);
+  } else if (S.T != 0) {
+    stream_generic(recs[wv], S.start, S.T, lane);
+  }
 }
 
 // ------------------------------------------------------------ PSK prepare

@@ -393,6 +393,7 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
 
   // ---- 1. owner lanes
   bool live = owner;
+  uint64_t pn_dec = 0;  // open: decoded packet number (0 if rejected)
   uint32_t status = 0, len = 0, pno = 0, first = 0, pn_len = 0, hdr = 0, pl = 0;
   uint64_t src = 0, dst = 0;
   const QuicKeyDev *K = &Q.key0;
@@ -486,11 +487,13 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
           trunc = (trunc << 8) | pnb[i];
         }
         pn = decode_pn(pn, trunc, 8 * pn_len);
-        if (Q.pn_out) Q.pn_out[p] = pn;
+        pn_dec = pn;
         pl = len - 16 - hdr;
       }
     }
     if (!live) status = kQEShort;
+    // every owner lane writes its pn_out (0 when the packet was rejected)
+    if (OPEN && owner && Q.pn_out) Q.pn_out[p] = pn_dec;
     if (live) {
       quic_nonce(*K, pn, nonce);
       chacha20_block(K->key, 0, nonce, otk);

@@ -445,7 +445,8 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
 
     // ---- 1. owner lanes
     bool live = owner;
-    uint32_t status = 0, len = 0, pno = 0, first = 0, pn_len = 0, hdr = 0, pl = 0, kid = 0;
+    uint64_t pn_dec = 0;  // open: decoded packet number (0 if rejected)
+  uint32_t status = 0, len = 0, pno = 0, first = 0, pn_len = 0, hdr = 0, pl = 0, kid = 0;
     uint64_t src = 0, dst = 0;
     uint32_t nonce[3] = {0u, 0u, 0u}, rtag[4] = {0u, 0u, 0u, 0u}, y[4] = {0u, 0u, 0u, 0u};
     uint32_t hd[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, pnw = 0;  // packet bytes 0..31; seal: pn bytes
@@ -537,11 +538,13 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
             trunc = (trunc << 8) | pnb[i];
           }
           pn = decode_pn(pn, trunc, 8 * pn_len);
-          if (Q.pn_out) Q.pn_out[p] = pn;
+          pn_dec = pn;
           pl = len - 16 - hdr;
         }
       }
       if (!live) status = kQEShort;
+    // every owner lane writes its pn_out (0 when the packet was rejected)
+    if (OPEN && owner && Q.pn_out) Q.pn_out[p] = pn_dec;
       if (live) {
         const uint32_t iv[3] = {K.iv[0], K.iv[1], K.iv[2]};
         quic_nonce_iv(iv, pn, nonce);
