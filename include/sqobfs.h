@@ -386,8 +386,10 @@ int sqobfs_udp_conn_write(sqobfs_udp_conn *c, uint32_t fd_index, uint32_t n,
  * write_quic: QUIC packet i (header || payload, len[i] bytes, at most
  *   slot_bytes - 24) is written by the caller at sqobfs_udp_conn_tx_payload(i);
  *   packet numbers pn[i], pn field at pn_offset (the connection's short
- *   header: 1 + DCID length); salts from getrandom.  Packets the kernel
- *   rejects are not sent; *sent = datagrams sent.
+ *   header: 1 + DCID length); salts from getrandom.  *sent = datagrams
+ *   sent, a prefix of the batch: when the kernel rejects a packet (too short
+ *   for its packet number and sample), the packets before it are sent and
+ *   the call returns SQ_EINVAL, so packet *sent is the rejected one.
  * read_quic: receive a batch, open it with packet numbers decoded against
  *   largest_pn; view.len[i] = the packet's length (header || plaintext, at
  *   view.base + view.off[i]) or a SQOBFS_QUIC_E* code; *pn_out (optional) =

@@ -38,6 +38,8 @@
 // costs 40 %.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include "sq_bytes.h"
 #include "sq_hash.h"
 #include "sq_internal.h"
@@ -60,6 +62,14 @@ namespace sq {
 #ifndef SQ_PPW
 #define SQ_PPW 32
 #endif
+// 1: persistent grid (SQ_PBLK blocks per CU), each wave software-pipelined
+// over the units w, w + NW, ...; 0: one unit per wave.
+#ifndef SQ_PERSIST
+#define SQ_PERSIST 0
+#endif
+#ifndef SQ_PBLK
+#define SQ_PBLK 2
+#endif
 // Timing-only ablation builds (never the shipped .so): bit 0 skips the key
 // derivation, bit 1 skips the byte-exact stores.
 #ifndef SQ_ABLATE
@@ -70,7 +80,8 @@ namespace sq {
 #define SQ_STR(x) SQ_STR2(x)
 extern "C" const char *sqobfs_build_info(void) {
   return "gfx950 obfs_kernel U=" SQ_STR(SQ_U) " PPW=" SQ_STR(SQ_PPW) " NT=" SQ_STR(SQ_NT)
-         " block=" SQ_STR(SQ_BLOCK) " ablate=" SQ_STR(SQ_ABLATE);
+         " persist=" SQ_STR(SQ_PERSIST) " pblk=" SQ_STR(SQ_PBLK) " block=" SQ_STR(SQ_BLOCK)
+         " ablate=" SQ_STR(SQ_ABLATE);
 }
 
 constexpr uint32_t kPktPerWave = SQ_PPW;
@@ -695,6 +706,87 @@ __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
   }
 }
 
+// The persistent form: each wave walks the units w, w + NW, ... and, while
+// unit u's first step of loads is in flight, prepares unit u + NW (whose
+// descriptors were prefetched a unit earlier and whose salt / window loads
+// were issued before those stream loads, so waiting for them never waits
+// for the stream).
+template <int KIND, int DIR, bool MULTI, int U>
+__global__ __launch_bounds__(kBlock, SQ_PBLK) void obfs_pkernel(const KParams P, uint64_t units) {
+  __shared__ ChunkRec recs[kWavesPerBlock][2][kWave];
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint32_t wv = threadIdx.x / kWave;
+  const uint64_t NW = (uint64_t)gridDim.x * kWavesPerBlock;
+  uint64_t u = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
+  if (u >= units) return;
+  UnitStream S;
+  {
+    bool valid, owner;
+    const uint32_t p = lane_packet(u, lane, P.n, valid, owner);
+    RawDesc d;
+    fetch_desc<KIND, DIR, MULTI>(P, p, valid, d);
+    PacketJob J;
+    uint32_t salt[4], olen;
+    bool do_hash;
+    const PskEntry *E;
+    finalize_desc<KIND, DIR, MULTI>(P, p, valid, d, J, salt, do_hash, E, olen);
+    (void)E;
+    Windows W;
+    fetch_windows(J, W);
+    if (owner) P.out_len[p] = olen;
+    const uint32_t pid = MULTI && d.pid < P.n_psk ? d.pid : 0u;
+    S = prepare_unit<KIND, DIR, MULTI>(P, J, salt, do_hash, pid, W, owner, lane, recs[wv][0]);
+  }
+  RawDesc dn;  // descriptor of the next unit, in flight
+  {
+    bool valid, owner;
+    const uint32_t p = lane_packet(u + NW, lane, P.n, valid, owner);
+    fetch_desc<KIND, DIR, MULTI>(P, p, valid && u + NW < units, dn);
+  }
+  uint32_t buf = 0;
+  for (;;) {
+    const uint64_t un = u + NW;
+    const bool has_next = un < units;  // wave-uniform
+    const ChunkRec *wrec = recs[wv][buf];
+    // ---- unit un: salt (deobfuscate) and window loads, ahead of the stream's
+    bool vn = false, on = false;
+    uint32_t pn = 0, saltn[4] = {0u, 0u, 0u, 0u}, olen = 0, pid = 0;
+    PacketJob JN = {0, 0, 0, 0};
+    bool dh = false;
+    Windows WN;
+    if (has_next) {
+      pn = lane_packet(un, lane, P.n, vn, on);
+      const PskEntry *E;
+      finalize_desc<KIND, DIR, MULTI>(P, pn, vn, dn, JN, saltn, dh, E, olen);
+      (void)E;
+      fetch_windows(JN, WN);
+      pid = MULTI && dn.pid < P.n_psk ? dn.pid : 0u;
+      bool v2, o2;
+      const uint32_t p2 = lane_packet(un + NW, lane, P.n, v2, o2);
+      fetch_desc<KIND, DIR, MULTI>(P, p2, v2 && un + NW < units, dn);  // two units ahead
+    }
+    // ---- unit u: first step's loads
+    u32x4 cur[U];
+    uint32_t cpp[U];
+    if (S.fast) stream_issue<U>(wrec, S.B, S.start, S.T, lane, 0, cur, cpp);
+    // ---- unit un: prepare, while they are in flight
+    UnitStream SN;
+    SN.T = 0;
+    SN.fast = false;
+    if (has_next) {
+      if (on) P.out_len[pn] = olen;
+      SN = prepare_unit<KIND, DIR, MULTI>(P, JN, saltn, dh, pid, WN, on, lane, recs[wv][buf ^ 1]);
+    }
+    // ---- unit u: the stream
+    if (S.fast) stream_loop<U>(wrec, S.B, S.start, S.T, lane, cur, cpp);
+    else if (S.T != 0) stream_generic(wrec, S.start, S.T, lane);
+    if (!has_next) break;
+    u = un;
+    S = SN;
+    buf ^= 1;
+  }
+}
+
 // ------------------------------------------------------------ PSK prepare
 
 __device__ __forceinline__ uint64_t ld64le(const uint8_t *p) {
@@ -768,13 +860,44 @@ __global__ void psk_prepare_kernel(int kind, const uint8_t *blob, const uint64_t
   out[k] = E;
 }
 
+// Compute units of the current device (queried once per device).
+static uint32_t device_cus() {
+  static std::atomic<uint32_t> cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  uint32_t c = cache[dev].load(std::memory_order_relaxed);
+  if (c == 0) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        v <= 0)
+      v = 256;
+    c = (uint32_t)v;
+    cache[dev].store(c, std::memory_order_relaxed);
+  }
+  return c;
+}
+
 template <int KIND, int DIR, bool MULTI>
 static int launch_one(const KParams *kp, hipStream_t s) {
   constexpr int U = SQ_U;
-  constexpr uint64_t per_block = (uint64_t)kWavesPerBlock * kPktPerWave;
-  const uint64_t blocks = ((uint64_t)kp->n + per_block - 1) / per_block;
+  const uint64_t units = ((uint64_t)kp->n + kPktPerWave - 1) / kPktPerWave;
+#if SQ_PERSIST
+  const uint64_t want = (units + kWavesPerBlock - 1) / kWavesPerBlock;
+  const uint64_t cap = (uint64_t)device_cus() * SQ_PBLK;
+  const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
+  // unused dynamic LDS so that no more than SQ_PBLK blocks share a CU (the
+  // grid is sized for exactly that many)
+  constexpr uint32_t kLds = 160u * 1024u;
+  constexpr uint32_t kStatic = sizeof(ChunkRec) * kWavesPerBlock * 2 * kWave;
+  constexpr uint32_t kMin = kLds / (SQ_PBLK + 1) + 1;
+  constexpr uint32_t kPad = kMin > kStatic ? ((kMin - kStatic + 1023) / 1024) * 1024 : 0;
+  hipLaunchKernelGGL((obfs_pkernel<KIND, DIR, MULTI, U>), dim3(blocks), dim3(kBlock), kPad, s,
+                     *kp, units);
+#else
+  const uint64_t blocks = (units + kWavesPerBlock - 1) / kWavesPerBlock;
   hipLaunchKernelGGL((obfs_kernel<KIND, DIR, MULTI, U>), dim3((uint32_t)blocks), dim3(kBlock), 0,
                      s, *kp);
+#endif
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

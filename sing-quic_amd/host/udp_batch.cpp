@@ -95,11 +95,15 @@ struct sqobfs_udp_conn {
   uint32_t *tx_len = nullptr, *tx_out_len = nullptr;
   std::vector<uint32_t> tx_wire_len;
   uint32_t offload = 0;  // SQOBFS_UDP_TX_GSO | SQOBFS_UDP_RX_GRO in effect
-  // QUIC batch arrays (in the mapped block): packet numbers, decoded packet
-  // numbers, packet-number offsets, Salamander salts
-  uint64_t *qpn = nullptr, *qpn_out = nullptr;
-  uint16_t *qpno = nullptr;
-  uint8_t *qsalt = nullptr;
+  // QUIC batch arrays (in the mapped block).  Transmit and receive have
+  // their own (a reader and a writer thread run at once, under different
+  // locks: sharing the packet-number array would let one direction seal
+  // under the other's packet numbers, i.e. reuse an AEAD nonce).
+  uint64_t *qpn_tx = nullptr;               // write_quic: packet numbers
+  uint16_t *qpno_tx = nullptr;              // write_quic: pn offsets
+  uint8_t *qsalt = nullptr;                 // write_quic: Salamander salts
+  uint64_t *qpn_rx = nullptr, *qpn_out = nullptr;  // read_quic: largest pn / decoded
+  uint16_t *qpno_rx = nullptr;              // read_quic: pn offsets
 };
 
 namespace {
@@ -440,10 +444,10 @@ int sqobfs_udp_conn_open(sqobfs_ctx *ctx, const sqobfs_keyring *kr, const int *f
   c->slots = slots;
   c->slot_bytes = slot_bytes;
   c->S = S;
-  // one mapped block: rx slots | tx slots | 6 u64 arrays | 4 u32 arrays |
-  // salts (8 B each) | u16 packet-number offsets
+  // one mapped block: rx slots | tx slots | 7 u64 arrays | 4 u32 arrays |
+  // salts (8 B each) | 2 u16 packet-number offset arrays
   const size_t sb = (size_t)slots * slot_bytes, a64 = 8ull * slots, a32 = 4ull * slots;
-  const size_t bytes = 2 * sb + 6 * a64 + 4 * a32 + 8ull * slots + 2ull * slots;
+  const size_t bytes = 2 * sb + 7 * a64 + 4 * a32 + 8ull * slots + 4ull * slots;
   if (sqobfs_host_alloc(ctx, bytes, &c->block) != SQ_OK) {
     delete c;
     return SQ_ENOMEM;
@@ -462,14 +466,16 @@ int sqobfs_udp_conn_open(sqobfs_ctx *ctx, const sqobfs_keyring *kr, const int *f
   c->rx_out_off = (uint64_t *)p;             p += a64;
   c->tx_in_off = (uint64_t *)p;              p += a64;
   c->tx_out_off = (uint64_t *)p;             p += a64;
-  c->qpn = (uint64_t *)p;                    p += a64;
+  c->qpn_tx = (uint64_t *)p;                 p += a64;
+  c->qpn_rx = (uint64_t *)p;                 p += a64;
   c->qpn_out = (uint64_t *)p;                p += a64;
   c->rx_len = (uint32_t *)p;                 p += a32;
   c->rx_out_len = (uint32_t *)p;             p += a32;
   c->tx_len = (uint32_t *)p;                 p += a32;
   c->tx_out_len = (uint32_t *)p;             p += a32;
   c->qsalt = p;                              p += 8ull * slots;
-  c->qpno = (uint16_t *)p;
+  c->qpno_tx = (uint16_t *)p;                p += 2ull * slots;
+  c->qpno_rx = (uint16_t *)p;
   c->rx_fd.resize(slots);
   c->rx_from.resize(slots);
   c->tx_wire_len.resize(slots);
@@ -579,8 +585,8 @@ int sqobfs_udp_conn_write_quic(sqobfs_udp_conn *c, const sqobfs_quic_keyring *qk
   for (uint32_t i = 0; i < n; i++) {
     if (len[i] + 16 + c->S > c->slot_bytes) return SQ_EINVAL;
     c->tx_len[i] = len[i];
-    c->qpn[i] = pn[i];
-    c->qpno[i] = pn_offset;
+    c->qpn_tx[i] = pn[i];
+    c->qpno_tx[i] = pn_offset;
   }
   // salts: 8 random bytes per datagram (salamander.go:60 buf.WriteRandom)
   for (size_t got = 0, want = 8ull * n; got < want;) {
@@ -600,35 +606,34 @@ int sqobfs_udp_conn_write_quic(sqobfs_udp_conn *c, const sqobfs_quic_keyring *qk
   b.out = c->tx;
   b.out_off = c->tx_out_off;  // ... wire from the slot start (the in-place form)
   b.out_len = c->tx_out_len;
-  b.pn_offset = c->qpno;
-  b.pn = c->qpn;
+  b.pn_offset = c->qpno_tx;
+  b.pn = c->qpn_tx;
   void *s = sqobfs_stream(c->ctx);
   int st = sqobfs_quic_seal_salamander(c->ctx, qkr, c->kr, &b, c->qsalt, s);
   if (st == SQ_OK) st = sqobfs_sync(c->ctx, s);
   if (st != SQ_OK) return st;
-  // packets the kernel rejected (SQOBFS_QUIC_E*) are not sent
-  std::vector<uint64_t> off;
-  std::vector<uint32_t> wl;
-  std::vector<sqobfs_addr> dst;
-  off.reserve(n);
-  wl.reserve(n);
-  dst.reserve(n);
-  for (uint32_t i = 0; i < n; i++) {
-    if (c->tx_out_len[i] != len[i] + 16 + c->S) continue;
-    off.push_back(c->tx_out_off[i]);
-    wl.push_back(c->tx_out_len[i]);
-    dst.push_back(to[i]);
-  }
-  const uint32_t m = (uint32_t)off.size();
-  if (c->offload & SQOBFS_UDP_TX_GSO) {
-    const int g = sqobfs_udp_send_gso(c->fds[fd_index], c->tx, off.data(), wl.data(), dst.data(),
-                                      m, sent);
-    if (g == SQ_OK || *sent > 0 || (g != -EIO && g != -EINVAL && g != -ENOPROTOOPT &&
-                                    g != -EOPNOTSUPP))
+  // *sent stays a prefix count (as for conn_write): the datagrams before the
+  // first packet the kernel rejected (tx_out_len = SQOBFS_QUIC_E*) are sent,
+  // and the call then fails with SQ_EINVAL, so packet *sent is the bad one
+  uint32_t m = 0;
+  while (m < n && c->tx_out_len[m] == len[m] + 16 + c->S) m++;
+  for (uint32_t i = 0; i < m; i++) c->tx_wire_len[i] = c->tx_out_len[i];
+  int g = SQ_OK;
+  if (m && (c->offload & SQOBFS_UDP_TX_GSO)) {
+    g = sqobfs_udp_send_gso(c->fds[fd_index], c->tx, c->tx_out_off, c->tx_wire_len.data(), to, m,
+                            sent);
+    if (!(g == SQ_OK || *sent > 0 || (g != -EIO && g != -EINVAL && g != -ENOPROTOOPT &&
+                                      g != -EOPNOTSUPP)))
+      c->offload &= ~SQOBFS_UDP_TX_GSO;
+    else if (g != SQ_OK)
       return g;
-    c->offload &= ~SQOBFS_UDP_TX_GSO;
   }
-  return sqobfs_udp_send(c->fds[fd_index], c->tx, off.data(), wl.data(), dst.data(), m, sent);
+  if (m && !(c->offload & SQOBFS_UDP_TX_GSO)) {
+    g = sqobfs_udp_send(c->fds[fd_index], c->tx, c->tx_out_off, c->tx_wire_len.data(), to, m,
+                        sent);
+    if (g != SQ_OK) return g;
+  }
+  return m < n ? SQ_EINVAL : SQ_OK;
 }
 
 int sqobfs_udp_conn_read_quic(sqobfs_udp_conn *c, const sqobfs_quic_keyring *qkr,
@@ -646,8 +651,8 @@ int sqobfs_udp_conn_read_quic(sqobfs_udp_conn *c, const sqobfs_quic_keyring *qkr
                                  c->rx_from.data(), &n);
   if (st != SQ_OK || n == 0) return st;
   for (uint32_t i = 0; i < n; i++) {
-    c->qpno[i] = pn_offset;
-    c->qpn[i] = largest_pn;
+    c->qpno_rx[i] = pn_offset;
+    c->qpn_rx[i] = largest_pn;
   }
   sqobfs_quic_batch b;
   memset(&b, 0, sizeof b);
@@ -658,8 +663,8 @@ int sqobfs_udp_conn_read_quic(sqobfs_udp_conn *c, const sqobfs_quic_keyring *qkr
   b.out = c->rx;
   b.out_off = c->rx_in_off;  // in place: the plaintext packet from the datagram start
   b.out_len = c->rx_out_len;
-  b.pn_offset = c->qpno;
-  b.pn = c->qpn;
+  b.pn_offset = c->qpno_rx;
+  b.pn = c->qpn_rx;
   b.pn_out = c->qpn_out;
   void *s = sqobfs_stream(c->ctx);
   st = sqobfs_quic_open_salamander(c->ctx, qkr, c->kr, &b, s);

@@ -472,9 +472,13 @@ class UdpConn:
         pn = np.asarray(pns, dtype=np.uint64)
         arr = (Addr * max(len(to), 1))(*to)
         sent = ctypes.c_uint32(0)
-        _check(lib().sqobfs_udp_conn_write_quic(self.handle, qkr.handle, fd_index, len(packets),
-                                                _ptr(lens), pn_offset, _ptr(pn), arr,
-                                                ctypes.byref(sent)), "sqobfs_udp_conn_write_quic")
+        st = lib().sqobfs_udp_conn_write_quic(self.handle, qkr.handle, fd_index, len(packets),
+                                              _ptr(lens), pn_offset, _ptr(pn), arr,
+                                              ctypes.byref(sent))
+        if st != SQ_OK:
+            e = SqError(st, "sqobfs_udp_conn_write_quic")
+            e.sent = sent.value  # datagrams sent before the failing packet
+            raise e
         return sent.value
 
     def read_quic(self, qkr: "QuicKeyring", pn_offset: int, largest_pn: int,
@@ -496,8 +500,10 @@ class UdpConn:
         addrs = (Addr * v.count).from_address(v.from_)
         for i in range(v.count):
             n = int(ln[i])
-            data = ctypes.string_at(v.base + int(off[i]), n) if n < 0xFFFFFFF0 else None
-            out.append((data, n, int(fi[i]), Addr.from_buffer_copy(addrs[i]), int(pn[i])))
+            ok = n < 0xFFFFFFF0  # else a SQOBFS_QUIC_E* code: no packet, no number
+            data = ctypes.string_at(v.base + int(off[i]), n) if ok else None
+            out.append((data, n, int(fi[i]), Addr.from_buffer_copy(addrs[i]),
+                        int(pn[i]) if ok else None))
         return out
 
     def tx_payload(self, i: int) -> np.ndarray:

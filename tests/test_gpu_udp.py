@@ -255,3 +255,108 @@ def test_conn_quic_fused(ctx, suite, offload):
         assert plain[:n] == want
     for s in (srv_sock, cli_sock, spy):
         s.close()
+
+
+def test_conn_quic_reader_and_writer_threads(ctx):
+    """One endpoint seals + sends in one thread while another thread receives
+    and opens on it (quic-go's send and receive loops, salamander.go:42-70
+    called concurrently).  Each direction has its own packet-number arrays:
+    every datagram on the wire must be sealed under ITS packet number (a
+    shared array would let the reader's largest_pn leak into the writer's
+    nonces)."""
+    import threading
+    rng = np.random.Generator(np.random.PCG64(77))
+    kb = tuple(rng.integers(0, 256, m, dtype=np.uint8).tobytes() for m in (32, 12, 32))
+    a_sock, b_sock, spy = _sock(), _sock(), _sock()
+    dcid = rng.integers(0, 256, 8, dtype=np.uint8).tobytes()
+    pno = 1 + len(dcid)
+    n_bursts, per = 12, 64
+    mk = lambda pn, L: (bytes([0x41]) + dcid + (pn & 0xFFFF).to_bytes(2, "big") +  # noqa: E731
+                        bytes((pn * 7 + i) & 0xFF for i in range(L)))
+    with sqobfs.Keyring(ctx, SALAMANDER, [PSK]) as kr, \
+            sqobfs.QuicKeyring(ctx, [sqobfs.QuicKey.of(*kb)], 0) as qkr, \
+            sqobfs.UdpConn(ctx, kr, [a_sock.fileno()], slots=256) as a, \
+            sqobfs.UdpConn(ctx, kr, [b_sock.fileno()], slots=256) as b:
+        to_spy = Addr.of(*spy.getsockname())
+        to_a = Addr.of(*a_sock.getsockname())
+        sent_pns = []
+        rx = []
+        errs = []
+
+        def writer():
+            try:
+                for k in range(n_bursts):
+                    pns = [10_000 + k * per + i for i in range(per)]
+                    pk = [mk(pn, 300) for pn in pns]
+                    assert a.write_quic(qkr, 0, pk, pno, pns, [to_spy] * per) == per
+                    sent_pns.extend(pns)
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+
+        def reader():
+            try:
+                while len(rx) < n_bursts * per:
+                    got = a.read_quic(qkr, pno, 499, 3000)
+                    assert got, f"reader timed out after {len(rx)}"
+                    rx.extend(got)
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+
+        tw, tr = threading.Thread(target=writer), threading.Thread(target=reader)
+        tr.start()
+        tw.start()
+        for k in range(n_bursts):  # b feeds a's reader meanwhile
+            pns = [500 + k * per + i for i in range(per)]
+            assert b.write_quic(qkr, 0, [mk(pn, 200) for pn in pns], pno, pns,
+                                [to_a] * per) == per
+        tw.join(60)
+        tr.join(60)
+        assert not errs, errs
+        assert [g[4] for g in rx] == [500 + i for i in range(n_bursts * per)]
+        assert [g[0] for g in rx] == [mk(500 + i, 200) for i in range(n_bursts * per)]
+        spy.settimeout(2.0)
+        for pn in sent_pns:
+            w = spy.recv(65536)
+            plain, n = ol.salamander_read(PSK, w)
+            want, _ = ol.quic_seal(*kb, pn, mk(pn, 300), pno, suite=0)
+            assert plain[:n] == want, f"packet {pn} sealed under another packet number"
+    for s in (a_sock, b_sock, spy):
+        s.close()
+
+
+def test_conn_quic_rejects_reported(ctx):
+    """write_quic: a packet too short for its packet number and sample is
+    not sent; the ones before it are, and the call fails with *sent = its
+    index.  read_quic: a datagram that cannot be opened has no packet and
+    no packet number."""
+    rng = np.random.Generator(np.random.PCG64(78))
+    kb = tuple(rng.integers(0, 256, m, dtype=np.uint8).tobytes() for m in (32, 12, 32))
+    a_sock, spy, raw = _sock(), _sock(), _sock()
+    dcid = bytes(8)
+    pno = 9
+    good = [bytes([0x41]) + dcid + bytes([0, i]) + bytes(100) for i in range(3)]
+    short = bytes([0x41]) + dcid + bytes([0, 9, 1])  # pn_offset + 4 > len: no sample
+    with sqobfs.Keyring(ctx, SALAMANDER, [PSK]) as kr, \
+            sqobfs.QuicKeyring(ctx, [sqobfs.QuicKey.of(*kb)], 0) as qkr, \
+            sqobfs.UdpConn(ctx, kr, [a_sock.fileno()], slots=64) as a:
+        with pytest.raises(sqobfs.SqError) as ei:
+            a.write_quic(qkr, 0, good[:2] + [short] + good[2:], pno, [0, 1, 2, 3],
+                         [Addr.of(*spy.getsockname())] * 4)
+        assert ei.value.sent == 2
+        spy.settimeout(1.0)
+        for i in range(2):
+            plain, n = ol.salamander_read(PSK, spy.recv(65536))
+            assert plain[:n] == ol.quic_seal(*kb, i, good[i], pno, suite=0)[0]
+        with pytest.raises(socket.timeout):
+            spy.recv(65536)
+        raw.sendto(b"\x07" * 5, a_sock.getsockname())      # shorter than a salt
+        raw.sendto(bytes(40), a_sock.getsockname())         # tag cannot match
+        got = []
+        while len(got) < 2:
+            b = a.read_quic(qkr, pno, 0, 3000)
+            assert b
+            got += b
+        for data, code, _, _, pn in got:
+            assert data is None and pn is None and code >= 0xFFFFFFF0
+    for s in (a_sock, spy, raw):
+        s.close()
