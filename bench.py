@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=2.0,
                     help="wall seconds of CPU-baseline sampling (x threads = CPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--packets", type=int, default=0,
+                    help="dev: override the config's packet count (scaling probes; not a "
+                         "BASELINE configuration)")
     ap.add_argument("--layout", default="dense", choices=["dense", "slot16", "inplace"],
                     help="dense: wire-dense outputs, wire-sized input slots (default); "
                          "slot16: 16-byte-aligned slots; inplace: obfuscate in the input "
@@ -210,7 +213,7 @@ def cpu_baseline(seconds: float):
     import sqobfs
     import oracle_lib as ol
     n, L, S = 65536, 1200, 8
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    threads = cpu_share()
     rng = np.random.Generator(np.random.PCG64(1))
     data = rng.integers(0, 256, n * L, dtype=np.uint8)
     salt = np.random.Generator(np.random.PCG64(2)).integers(0, 256, n * S, dtype=np.uint8)
@@ -223,28 +226,55 @@ def cpu_baseline(seconds: float):
     b_len = np.zeros(n, np.uint32)
     obf = sqobfs.HostBatch(data, in_off, lens, wire, w_off, w_len, salt)
     deo = sqobfs.HostBatch(wire, w_off, np.full(n, L + S, np.uint32), back, in_off, b_len)
-    t_ob = t_de = 0.0
-    passes = 0
-    t_end = time.perf_counter() + seconds
-    while passes < 2 or time.perf_counter() < t_end:
-        t0 = time.perf_counter()
-        ol.batch_run(0, 0, [PSK], obf, nthreads=threads)
-        t1 = time.perf_counter()
-        ol.batch_run(0, 1, [PSK], deo, nthreads=threads)
-        t2 = time.perf_counter()
-        t_ob += t1 - t0
-        t_de += t2 - t1
-        passes += 1
+    def timed(nthreads, secs):
+        t_ob = t_de = 0.0
+        passes = 0
+        t_end = time.perf_counter() + secs
+        while passes < 2 or time.perf_counter() < t_end:
+            t0 = time.perf_counter()
+            ol.batch_run(0, 0, [PSK], obf, nthreads=nthreads)
+            t1 = time.perf_counter()
+            ol.batch_run(0, 1, [PSK], deo, nthreads=nthreads)
+            t2 = time.perf_counter()
+            t_ob += t1 - t0
+            t_de += t2 - t1
+            passes += 1
+        gib = n * L * passes / 2**30
+        return gib / t_ob, gib / t_de, gib / (t_ob + t_de), passes, t_ob + t_de
+
+    ob, de, rt, passes, wall = timed(threads, seconds)
     ok = bool(np.array_equal(back, data))
-    gib = n * L * passes / 2**30
-    return {"value": gib / t_ob, "unit": "GiB/s", "cores": threads, "kind": "port",
+    ob1, de1, rt1, _, wall1 = timed(1, min(seconds, 2.0))  # one core: the per-core rate
+    host = os.cpu_count() or threads
+    return {"value": ob, "unit": "GiB/s", "cores": threads, "kind": "port",
             "sample": f"configs[0]: {passes} x (65,536 x 1200 B Salamander obfuscate + "
                       f"deobfuscate), one PSK, C restatement (oracle/oracle.c, byte loops as "
-                      f"salamander.go:51-53,62-64) on {threads} threads; value = obfuscate "
-                      f"direction; deobfuscate {gib / t_de:.3f} GiB/s, round trip "
-                      f"{gib / (t_ob + t_de):.3f} GiB/s; round-trip identity {ok}; "
-                      f"Go reference unbuildable (no Go toolchain)",
-            "cpu_seconds": round((t_ob + t_de) * threads, 2)}
+                      f"salamander.go:51-53,62-64) on {threads} threads (this job's CPU "
+                      f"share of the {host}-CPU host); value = obfuscate direction; "
+                      f"deobfuscate {de:.3f} GiB/s, round trip {rt:.3f} GiB/s; round-trip "
+                      f"identity {ok}; Go reference unbuildable (no Go toolchain)",
+            "per_direction": {"obfuscate": round(ob, 3), "deobfuscate": round(de, 3),
+                              "round_trip": round(rt, 3)},
+            "per_core": {"obfuscate": round(ob1, 3), "deobfuscate": round(de1, 3),
+                         "round_trip": round(rt1, 3)},
+            "host_cpus": host,
+            "host_cpus_extrapolated": {
+                "obfuscate": round(ob1 * host, 1), "deobfuscate": round(de1 * host, 1),
+                "round_trip": round(rt1 * host, 1),
+                "note": "per-core rate x host CPUs: a linear upper bound, NOT measured (the "
+                        "GPU pool gives one job a 16-CPU share; SMT siblings and memory "
+                        "bandwidth would cut it)"},
+            "cpu_seconds": round(wall * threads + wall1, 2)}
+
+
+def cpu_share() -> int:
+    """CPUs this job may use: its affinity, capped by the pool's per-job share
+    (OMP_NUM_THREADS is set to it on the GPU boxes)."""
+    n = len(os.sched_getaffinity(0))
+    cap = os.environ.get("OMP_NUM_THREADS")
+    if cap and cap.isdigit() and int(cap) > 0:
+        n = min(n, int(cap))
+    return max(1, n)
 
 
 def host_info(torch, dev) -> dict:
@@ -304,6 +334,8 @@ def main():
     torch.cuda.set_device(dev)
 
     kind, n_total, L, n_psk = CONFIGS[args.config]
+    if args.packets:
+        n_total = args.packets
     n, first = shard(args.config, n_total, world, rank)
     direction = sqobfs.OBFUSCATE if args.direction == "obfuscate" else sqobfs.DEOBFUSCATE
     sh = build_shard(torch, dev, kind, n, L, n_psk, rank, world, args.config, args.layout, first)
@@ -602,7 +634,7 @@ def quic_rate(torch, sqobfs, ctx, dev, steps, n=1 << 20, payload=1350, cpu_secon
     res["parity_spot_check"] = ok
     # CPU legs, threaded: the oracle (scalar C restatement) and OpenSSL
     m = 65536 if suite == 0 else 8192
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    threads = cpu_share()
     cin = np.tile(d[0], m)
     ci_off = np.arange(m, dtype=np.uint64) * ln
     co_off = np.arange(m, dtype=np.uint64) * (ln + 16)

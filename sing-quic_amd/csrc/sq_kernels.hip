@@ -38,8 +38,6 @@
 // costs 40 %.
 #include <hip/hip_runtime.h>
 
-#include <atomic>
-
 #include "sq_bytes.h"
 #include "sq_hash.h"
 #include "sq_internal.h"
@@ -62,13 +60,14 @@ namespace sq {
 #ifndef SQ_PPW
 #define SQ_PPW 32
 #endif
-// 1: persistent grid (SQ_PBLK blocks per CU), each wave software-pipelined
-// over the units w, w + NW, ...; 0: one unit per wave.
-#ifndef SQ_PERSIST
-#define SQ_PERSIST 0
+// Minimum waves per SIMD the register allocation must allow (0 = no bound).
+#ifndef SQ_MINW
+#define SQ_MINW 0
 #endif
-#ifndef SQ_PBLK
-#define SQ_PBLK 2
+// 1: issue the first stream step before the key / contents step (overlap;
+// measured neutral at 3 waves per SIMD, slower when bounded to 4).
+#ifndef SQ_OVERLAP
+#define SQ_OVERLAP 0
 #endif
 // Timing-only ablation builds (never the shipped .so): bit 0 skips the key
 // derivation, bit 1 skips the byte-exact stores.
@@ -80,7 +79,7 @@ namespace sq {
 #define SQ_STR(x) SQ_STR2(x)
 extern "C" const char *sqobfs_build_info(void) {
   return "gfx950 obfs_kernel U=" SQ_STR(SQ_U) " PPW=" SQ_STR(SQ_PPW) " NT=" SQ_STR(SQ_NT)
-         " persist=" SQ_STR(SQ_PERSIST) " pblk=" SQ_STR(SQ_PBLK) " block=" SQ_STR(SQ_BLOCK)
+         " minw=" SQ_STR(SQ_MINW) " overlap=" SQ_STR(SQ_OVERLAP) " block=" SQ_STR(SQ_BLOCK)
          " ablate=" SQ_STR(SQ_ABLATE);
 }
 
@@ -393,23 +392,114 @@ struct UnitStream {
 constexpr uint32_t kNoIdx = 0xFFFFFFFFu;
 constexpr uint64_t kMaxSpan = 0xFFFFFF00ull;
 
-// Key, images, neighbour exchange, block ownership, special blocks,
-// byte-exact stores, flat prefix sum, LDS records and buffer resources.
-// Every lane of the wave runs it.
+// Block geometry of a unit's packets, from their jobs alone.
+struct Geo {
+  uint64_t rs, re, B0;  // output range, first owned block
+  uint32_t nblk;        // owned blocks [B0, B0 + 16 nblk)
+  bool ne;              // non-empty output
+  bool hf;              // first owned block special (holds salt bytes)
+  bool hl;              // last owned block partly this packet's (re unaligned)
+  bool lfull;           // ... and written whole (the next datagram fills it)
+  bool pfull;           // bytes [rs, B0) are in the previous packet's whole block
+};
+
+// Step 3a, the plan: block ownership and special-block roles (no key, no
+// payload bytes needed), the flat prefix sum, the stream half of the LDS
+// records and the buffer resources -- everything the first stream loads
+// need.  Every lane of the wave runs it.
+__device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, uint32_t lane,
+                                                ChunkRec *recs, Geo &G) {
+  out_range(J, G.rs, G.re, G.ne);
+  const uint64_t rs = G.rs, re = G.re;
+  // in place (input overlaps its own output blocks): a neighbour in another
+  // wave must not read or write across this packet's blocks
+  const uint64_t oblo = rs & ~15ull, obhi = up16(re);
+  const bool ovl = G.ne && J.len && J.src_pay < obhi && J.src_pay + J.len > oblo;
+  // neighbours: next lane = next packet (lane kPktPerWave for the last one),
+  // previous lane = previous packet (lane kPktPerWave + 1 for the first one)
+  const uint32_t nl = (lane + 1) & (kWave - 1);
+  const uint32_t pl = lane == 0 ? kPktPerWave + 1 : lane - 1;
+  const uint64_t rs_n = shfl64(rs, nl), re_n = shfl64(re, nl);
+  const uint64_t rs_p = shfl64(rs, pl), re_p = shfl64(re, pl);
+  const uint32_t fl = (G.ne ? 1u : 0u) | (ovl ? 2u : 0u);
+  const uint32_t fl_n = shfl32(fl, nl), fl_p = shfl32(fl, pl);
+
+  const uint64_t B0 = up16(rs), E = up16(re), BL = re & ~15ull;
+  G.B0 = B0;
+  G.nblk = (owner && G.ne && E > B0) ? (uint32_t)((E - B0) >> 4) : 0u;
+  const uint32_t nblk = G.nblk;
+  G.hl = nblk && (re & 15);
+  G.hf = nblk && B0 < J.dst_pay && !(G.hl && B0 == BL);
+  const bool cross_n = lane == kPktPerWave - 1, cross_p = lane == 0;
+  // last block whole: the next datagram starts at re and fills the block
+  G.lfull = G.hl && (fl_n & 1) && rs_n == re && re_n >= E && !(cross_n && (fl_n & 2));
+  // leading bytes [rs, B0) covered by the previous packet's whole last block
+  // (the same predicate as the previous lane's lfull)
+  const bool p_hl = (fl_p & 1) && (re_p & 15) && up16(re_p) > up16(rs_p);
+  G.pfull = p_hl && G.ne && re_p == rs && re >= B0 && !(cross_p && ovl);
+
+  // the flat block space: this packet's blocks [B0, B0 + 16 F)
+  const uint32_t F = (G.hl && !G.lfull) ? nblk - 1 : nblk;
+  uint32_t incl = F;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d, kWave);
+    if (lane >= (uint32_t)d) incl += y;
+  }
+  UnitStream U;
+  U.start = incl - F;
+  U.T = __builtin_amdgcn_readfirstlane(__shfl(incl, kWave - 1, kWave));
+  // interior blocks [i_lo, i_hi): the only ones loaded
+  const uint32_t i_lo = G.hf ? 1u : 0u, i_hi = G.hl ? nblk - 1 : nblk;
+  const bool has_int = i_hi > i_lo;
+  const uint64_t sabs = B0 + (J.src_pay - J.dst_pay);  // input of block B0
+  const uint64_t s_first = sabs + 16ull * i_lo, s_end = sabs + 16ull * i_hi;
+  {
+    ChunkRec &R = recs[lane];
+    R.ssub = sabs - 16ull * U.start;
+    R.dsub = B0 - 16ull * U.start;
+    R.sidx = G.hf ? U.start : kNoIdx;
+    R.eidx = G.lfull ? U.start + nblk - 1 : kNoIdx;
+  }
+  // spans: output of every flat block, input of every interior block
+  const uint64_t d_lo = uniform64(wave_min64(F ? B0 : ~0ull));
+  const uint64_t d_hi = uniform64(wave_max64(F ? B0 + 16ull * F : 0ull));
+  const uint64_t s_lo = uniform64(wave_min64(has_int ? s_first : ~0ull));
+  const uint64_t s_hi = uniform64(wave_max64(has_int ? s_end : 0ull));
+  const bool mis = has_int && (sabs & 3);
+  const bool sok = s_hi <= s_lo || s_hi - s_lo <= kMaxSpan;
+  U.fast = U.T != 0 && __ballot(mis) == 0 && d_hi - d_lo <= kMaxSpan && sok;
+  if (U.fast) {
+    const bool si = s_hi > s_lo;
+    U.B.src = __builtin_amdgcn_make_buffer_rsrc((void *)(si ? s_lo : d_lo), 0,
+                                                (int)(si ? (uint32_t)(s_hi - s_lo) : 0u),
+                                                0x00020000);
+    U.B.dst = __builtin_amdgcn_make_buffer_rsrc((void *)d_lo, 0, (int)(uint32_t)(d_hi - d_lo),
+                                                0x00020000);
+    U.B.sbase = (uint32_t)(si ? s_lo : d_lo);
+    U.B.dbase = (uint32_t)d_lo;
+  }
+  // records visible to the whole wave (same-wave LDS ops are ordered; this
+  // is a compiler barrier plus the LDS drain)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  return U;
+}
+
+// Step 3b, the contents (while the first stream loads are in flight): key,
+// head / tail images, the special blocks' values and the keystreams (the
+// store half of the records), and the byte-exact stores of bytes no
+// datagram pair covers whole.  Every lane of the wave runs it.
 template <int KIND, int DIR, bool MULTI>
-__device__ __forceinline__ UnitStream prepare_unit(const KParams &P, const PacketJob &J,
-                                                   const uint32_t (&salt)[4], bool do_hash,
-                                                   uint32_t pid, const Windows &W, bool owner,
-                                                   uint32_t lane, ChunkRec *recs) {
+__device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
+                                          const uint32_t (&salt)[4], bool do_hash, uint32_t pid,
+                                          const Windows &W, bool owner, uint32_t lane,
+                                          const Geo &G, uint32_t start, ChunkRec *recs) {
   constexpr uint32_t S = KIND == 0 ? kSalamanderSalt : kXPlusSalt;
   constexpr uint32_t PW = DIR == 0 ? S / 4 : 0;  // salt words in front of the payload
   uint32_t key[8];
   // single PSK: the kernarg copy (scalar loads); several: the device table
   derive_key<KIND>(do_hash, MULTI ? P.psk_table + pid : &P.psk0, salt, key);
-
-  uint64_t rs, re;
-  bool ne;
-  out_range(J, rs, re, ne);
+  const uint64_t rs = G.rs, re = G.re;
   // head image: output bytes [rs, rs + 32) = salt || payload ^ key
   uint32_t hi[8];
   {
@@ -448,115 +538,45 @@ __device__ __forceinline__ UnitStream prepare_unit(const KParams &P, const Packe
   } else {
     win16(hx, (uint32_t)(BL - rs) & 31u, ti);  // BL - rs <= 16 here (or no tail)
   }
-  // in place (input overlaps its own output blocks): a neighbour in another
-  // wave must not read or write across this packet's blocks
-  const uint64_t oblo = rs & ~15ull, obhi = up16(re);
-  const bool ovl = ne && J.len && J.src_pay < obhi && J.src_pay + J.len > oblo;
-
-  // neighbours: next lane = next packet (lane kPktPerWave for the last one),
-  // previous lane = previous packet (lane kPktPerWave + 1 for the first one)
+  // the next packet's head image (its salt / first payload bytes)
   const uint32_t nl = (lane + 1) & (kWave - 1);
-  const uint32_t pl = lane == 0 ? kPktPerWave + 1 : lane - 1;
-  const uint64_t rs_n = shfl64(rs, nl), re_n = shfl64(re, nl);
-  const uint64_t rs_p = shfl64(rs, pl), re_p = shfl64(re, pl);
-  const uint32_t fl = (ne ? 1u : 0u) | (ovl ? 2u : 0u);
-  const uint32_t fl_n = shfl32(fl, nl), fl_p = shfl32(fl, pl);
   uint32_t hn[4];
 #pragma unroll
   for (int j = 0; j < 4; j++) hn[j] = shfl32(hi[j], nl);
 
-  // owned blocks [B0, E)
-  const uint64_t B0 = up16(rs), E = up16(re);
-  const uint32_t nblk = (owner && ne && E > B0) ? (uint32_t)((E - B0) >> 4) : 0u;
-  const bool hl = nblk && t;  // last owned block partly this packet's
-  const bool hf = nblk && B0 < J.dst_pay && !(hl && B0 == BL);
-  const bool cross_n = lane == kPktPerWave - 1, cross_p = lane == 0;
-  // last block whole: the next datagram starts at re and fills the block
-  const bool lfull = hl && (fl_n & 1) && rs_n == re && re_n >= E && !(cross_n && (fl_n & 2));
-  // leading bytes [rs, B0) covered by the previous packet's whole last block
-  // (the same predicate as the previous lane's lfull)
-  const bool p_hl = (fl_p & 1) && (re_p & 15) && up16(re_p) > up16(rs_p);
-  const bool pfull = p_hl && ne && re_p == rs && re >= B0 && !(cross_p && ovl);
-
   // byte-exact stores of the bytes no datagram pair covers whole
-  if (!(SQ_ABLATE & 2) && owner && ne) {
-    if ((rs & 15) && !pfull) {
-      const uint64_t lend = re < B0 ? re : B0;
+  if (!(SQ_ABLATE & 2) && owner && G.ne) {
+    if ((rs & 15) && !G.pfull) {
+      const uint64_t lend = re < G.B0 ? re : G.B0;
       const uint32_t v[4] = {hi[0], hi[1], hi[2], hi[3]};
       store16(rs, v, (uint32_t)(lend - rs));
     }
-    if (hl && !lfull) store16(BL, ti, t);
+    if (G.hl && !G.lfull) store16(BL, ti, t);
   }
 
-  // special blocks
+  // special blocks and keystreams
   uint32_t vf[4] = {0u, 0u, 0u, 0u}, vl[4] = {0u, 0u, 0u, 0u};
-  if (hf) win16(hx, (uint32_t)(B0 - rs), vf);
-  if (lfull) {
+  if (G.hf) win16(hx, (uint32_t)(G.B0 - rs), vf);
+  if (G.lfull) {
     const uint32_t w[12] = {0u, 0u, 0u, 0u, hn[0], hn[1], hn[2], hn[3], 0u, 0u, 0u, 0u};
     uint32_t sh[4];
     win16(w, 16 - t, sh);
 #pragma unroll
     for (int j = 0; j < 4; j++) vl[j] = (ti[j] & range_mask(0, (int)t, j)) | sh[j];
   }
-
-  // the flat block space: this packet's blocks [B0, B0 + 16 F)
-  const uint32_t F = (hl && !lfull) ? nblk - 1 : nblk;
-  uint32_t incl = F;
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    const uint32_t y = __shfl_up(incl, d, kWave);
-    if (lane >= (uint32_t)d) incl += y;
-  }
-  UnitStream U;
-  U.start = incl - F;
-  U.T = __builtin_amdgcn_readfirstlane(__shfl(incl, kWave - 1, kWave));
-  // interior blocks [i_lo, i_hi): the only ones loaded
-  const uint32_t i_lo = hf ? 1u : 0u, i_hi = hl ? nblk - 1 : nblk;
-  const bool has_int = i_hi > i_lo;
-  const uint64_t sabs = B0 + (J.src_pay - J.dst_pay);  // input of block B0
-  const uint64_t s_first = sabs + 16ull * i_lo, s_end = sabs + 16ull * i_hi;
-  {
-    uint32_t k0[4], k1[4];
-    const uint32_t ph = (uint32_t)(B0 - J.dst_pay) & 31u;
-    keywin(key, ph, k0);
-    keywin(key, (ph + 16) & 31u, k1);
-    const bool odd = U.start & 1;
-    ChunkRec R;
-    R.ssub = sabs - 16ull * U.start;
-    R.dsub = B0 - 16ull * U.start;
-    R.sidx = hf ? U.start : kNoIdx;
-    R.eidx = lfull ? U.start + nblk - 1 : kNoIdx;
-    R.pad0 = R.pad1 = 0;
-    R.ks[0] = u32x4{bsel(odd, k1[0], k0[0]), bsel(odd, k1[1], k0[1]),
-                    bsel(odd, k1[2], k0[2]), bsel(odd, k1[3], k0[3])};
-    R.ks[1] = u32x4{bsel(odd, k0[0], k1[0]), bsel(odd, k0[1], k1[1]),
-                    bsel(odd, k0[2], k1[2]), bsel(odd, k0[3], k1[3])};
-    R.vf = u32x4{vf[0], vf[1], vf[2], vf[3]};
-    R.vl = u32x4{vl[0], vl[1], vl[2], vl[3]};
-    recs[lane] = R;
-  }
-  // spans: output of every flat block, input of every interior block
-  const uint64_t d_lo = uniform64(wave_min64(F ? B0 : ~0ull));
-  const uint64_t d_hi = uniform64(wave_max64(F ? B0 + 16ull * F : 0ull));
-  const uint64_t s_lo = uniform64(wave_min64(has_int ? s_first : ~0ull));
-  const uint64_t s_hi = uniform64(wave_max64(has_int ? s_end : 0ull));
-  const bool mis = has_int && (sabs & 3);
-  const bool sok = s_hi <= s_lo || s_hi - s_lo <= kMaxSpan;
-  U.fast = U.T != 0 && __ballot(mis) == 0 && d_hi - d_lo <= kMaxSpan && sok;
-  if (U.fast) {
-    const bool si = s_hi > s_lo;
-    U.B.src = __builtin_amdgcn_make_buffer_rsrc((void *)(si ? s_lo : d_lo), 0,
-                                                (int)(si ? (uint32_t)(s_hi - s_lo) : 0u),
-                                                0x00020000);
-    U.B.dst = __builtin_amdgcn_make_buffer_rsrc((void *)d_lo, 0, (int)(uint32_t)(d_hi - d_lo),
-                                                0x00020000);
-    U.B.sbase = (uint32_t)(si ? s_lo : d_lo);
-    U.B.dbase = (uint32_t)d_lo;
-  }
-  // LDS records visible to the whole wave (same-wave LDS ops are ordered;
-  // this is a compiler barrier plus the LDS drain)
+  uint32_t k0[4], k1[4];
+  const uint32_t ph = (uint32_t)(G.B0 - J.dst_pay) & 31u;
+  keywin(key, ph, k0);
+  keywin(key, (ph + 16) & 31u, k1);
+  const bool odd = start & 1;
+  ChunkRec &R = recs[lane];
+  R.ks[0] = u32x4{bsel(odd, k1[0], k0[0]), bsel(odd, k1[1], k0[1]),
+                  bsel(odd, k1[2], k0[2]), bsel(odd, k1[3], k0[3])};
+  R.ks[1] = u32x4{bsel(odd, k0[0], k1[0]), bsel(odd, k0[1], k1[1]),
+                  bsel(odd, k0[2], k1[2]), bsel(odd, k0[3], k1[3])};
+  R.vf = u32x4{vf[0], vf[1], vf[2], vf[3]};
+  R.vl = u32x4{vl[0], vl[1], vl[2], vl[3]};
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  return U;
 }
 
 // ------------------------------------------------------------ stream
@@ -674,13 +694,18 @@ __device__ __noinline__ void stream_generic(const ChunkRec *wrec, uint32_t start
 // ------------------------------------------------------------ the kernel
 
 template <int KIND, int DIR, bool MULTI, int U>
+#if SQ_MINW
+__global__ __launch_bounds__(kBlock, SQ_MINW) void obfs_kernel(const KParams P) {
+#else
 __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
+#endif
   __shared__ ChunkRec recs[kWavesPerBlock][kWave];
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wv = threadIdx.x / kWave;
   const uint64_t unit = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
   bool valid, owner;
   const uint32_t p = lane_packet(unit, lane, P.n, valid, owner);
+  // 1. descriptor (deobfuscate: the salt load) and the image windows: loads
   RawDesc d;
   fetch_desc<KIND, DIR, MULTI>(P, p, valid, d);
   PacketJob J;
@@ -693,98 +718,19 @@ __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
   Windows W;
   fetch_windows(J, W);
   if (owner) P.out_len[p] = olen;
-  const uint32_t pid = MULTI && d.pid < P.n_psk ? d.pid : 0u;
-  const UnitStream S =
-      prepare_unit<KIND, DIR, MULTI>(P, J, salt, do_hash, pid, W, owner, lane, recs[wv]);
+  // 3a. plan, then the first stream loads
+  Geo G;
+  const UnitStream S = plan_unit(J, owner, lane, recs[wv], G);
   u32x4 cur[U];
   uint32_t cpp[U];
-  if (S.fast) {
-    stream_issue<U>(recs[wv], S.B, S.start, S.T, lane, 0, cur, cpp);
-    stream_loop<U>(recs[wv], S.B, S.start, S.T, lane, cur, cpp);
-  } else if (S.T != 0) {
-    stream_generic(recs[wv], S.start, S.T, lane);
-  }
-}
-
-// The persistent form: each wave walks the units w, w + NW, ... and, while
-// unit u's first step of loads is in flight, prepares unit u + NW (whose
-// descriptors were prefetched a unit earlier and whose salt / window loads
-// were issued before those stream loads, so waiting for them never waits
-// for the stream).
-template <int KIND, int DIR, bool MULTI, int U>
-__global__ __launch_bounds__(kBlock, SQ_PBLK) void obfs_pkernel(const KParams P, uint64_t units) {
-  __shared__ ChunkRec recs[kWavesPerBlock][2][kWave];
-  const uint32_t lane = threadIdx.x & (kWave - 1);
-  const uint32_t wv = threadIdx.x / kWave;
-  const uint64_t NW = (uint64_t)gridDim.x * kWavesPerBlock;
-  uint64_t u = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
-  if (u >= units) return;
-  UnitStream S;
-  {
-    bool valid, owner;
-    const uint32_t p = lane_packet(u, lane, P.n, valid, owner);
-    RawDesc d;
-    fetch_desc<KIND, DIR, MULTI>(P, p, valid, d);
-    PacketJob J;
-    uint32_t salt[4], olen;
-    bool do_hash;
-    const PskEntry *E;
-    finalize_desc<KIND, DIR, MULTI>(P, p, valid, d, J, salt, do_hash, E, olen);
-    (void)E;
-    Windows W;
-    fetch_windows(J, W);
-    if (owner) P.out_len[p] = olen;
-    const uint32_t pid = MULTI && d.pid < P.n_psk ? d.pid : 0u;
-    S = prepare_unit<KIND, DIR, MULTI>(P, J, salt, do_hash, pid, W, owner, lane, recs[wv][0]);
-  }
-  RawDesc dn;  // descriptor of the next unit, in flight
-  {
-    bool valid, owner;
-    const uint32_t p = lane_packet(u + NW, lane, P.n, valid, owner);
-    fetch_desc<KIND, DIR, MULTI>(P, p, valid && u + NW < units, dn);
-  }
-  uint32_t buf = 0;
-  for (;;) {
-    const uint64_t un = u + NW;
-    const bool has_next = un < units;  // wave-uniform
-    const ChunkRec *wrec = recs[wv][buf];
-    // ---- unit un: salt (deobfuscate) and window loads, ahead of the stream's
-    bool vn = false, on = false;
-    uint32_t pn = 0, saltn[4] = {0u, 0u, 0u, 0u}, olen = 0, pid = 0;
-    PacketJob JN = {0, 0, 0, 0};
-    bool dh = false;
-    Windows WN;
-    if (has_next) {
-      pn = lane_packet(un, lane, P.n, vn, on);
-      const PskEntry *E;
-      finalize_desc<KIND, DIR, MULTI>(P, pn, vn, dn, JN, saltn, dh, E, olen);
-      (void)E;
-      fetch_windows(JN, WN);
-      pid = MULTI && dn.pid < P.n_psk ? dn.pid : 0u;
-      bool v2, o2;
-      const uint32_t p2 = lane_packet(un + NW, lane, P.n, v2, o2);
-      fetch_desc<KIND, DIR, MULTI>(P, p2, v2 && un + NW < units, dn);  // two units ahead
-    }
-    // ---- unit u: first step's loads
-    u32x4 cur[U];
-    uint32_t cpp[U];
-    if (S.fast) stream_issue<U>(wrec, S.B, S.start, S.T, lane, 0, cur, cpp);
-    // ---- unit un: prepare, while they are in flight
-    UnitStream SN;
-    SN.T = 0;
-    SN.fast = false;
-    if (has_next) {
-      if (on) P.out_len[pn] = olen;
-      SN = prepare_unit<KIND, DIR, MULTI>(P, JN, saltn, dh, pid, WN, on, lane, recs[wv][buf ^ 1]);
-    }
-    // ---- unit u: the stream
-    if (S.fast) stream_loop<U>(wrec, S.B, S.start, S.T, lane, cur, cpp);
-    else if (S.T != 0) stream_generic(wrec, S.start, S.T, lane);
-    if (!has_next) break;
-    u = un;
-    S = SN;
-    buf ^= 1;
-  }
+  const uint32_t pid = MULTI && d.pid < P.n_psk ? d.pid : 0u;
+  if (SQ_OVERLAP && S.fast) stream_issue<U>(recs[wv], S.B, S.start, S.T, lane, 0, cur, cpp);
+  // 2 + 3b. key and block contents
+  fill_unit<KIND, DIR, MULTI>(P, J, salt, do_hash, pid, W, owner, lane, G, S.start, recs[wv]);
+  if (!SQ_OVERLAP && S.fast) stream_issue<U>(recs[wv], S.B, S.start, S.T, lane, 0, cur, cpp);
+  // 4. the stream
+  if (S.fast) stream_loop<U>(recs[wv], S.B, S.start, S.T, lane, cur, cpp);
+  else if (S.T != 0) stream_generic(recs[wv], S.start, S.T, lane);
 }
 
 // ------------------------------------------------------------ PSK prepare
@@ -860,44 +806,13 @@ __global__ void psk_prepare_kernel(int kind, const uint8_t *blob, const uint64_t
   out[k] = E;
 }
 
-// Compute units of the current device (queried once per device).
-static uint32_t device_cus() {
-  static std::atomic<uint32_t> cache[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  uint32_t c = cache[dev].load(std::memory_order_relaxed);
-  if (c == 0) {
-    int v = 0;
-    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        v <= 0)
-      v = 256;
-    c = (uint32_t)v;
-    cache[dev].store(c, std::memory_order_relaxed);
-  }
-  return c;
-}
-
 template <int KIND, int DIR, bool MULTI>
 static int launch_one(const KParams *kp, hipStream_t s) {
   constexpr int U = SQ_U;
   const uint64_t units = ((uint64_t)kp->n + kPktPerWave - 1) / kPktPerWave;
-#if SQ_PERSIST
-  const uint64_t want = (units + kWavesPerBlock - 1) / kWavesPerBlock;
-  const uint64_t cap = (uint64_t)device_cus() * SQ_PBLK;
-  const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
-  // unused dynamic LDS so that no more than SQ_PBLK blocks share a CU (the
-  // grid is sized for exactly that many)
-  constexpr uint32_t kLds = 160u * 1024u;
-  constexpr uint32_t kStatic = sizeof(ChunkRec) * kWavesPerBlock * 2 * kWave;
-  constexpr uint32_t kMin = kLds / (SQ_PBLK + 1) + 1;
-  constexpr uint32_t kPad = kMin > kStatic ? ((kMin - kStatic + 1023) / 1024) * 1024 : 0;
-  hipLaunchKernelGGL((obfs_pkernel<KIND, DIR, MULTI, U>), dim3(blocks), dim3(kBlock), kPad, s,
-                     *kp, units);
-#else
   const uint64_t blocks = (units + kWavesPerBlock - 1) / kWavesPerBlock;
   hipLaunchKernelGGL((obfs_kernel<KIND, DIR, MULTI, U>), dim3((uint32_t)blocks), dim3(kBlock), 0,
                      s, *kp);
-#endif
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
