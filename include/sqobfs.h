@@ -302,6 +302,14 @@ int sqobfs_quic_open_salamander(sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr,
                                 const sqobfs_keyring *okr, const sqobfs_quic_batch *b,
                                 void *stream);
 
+/* Bytes of pinned staging sqobfs_run_host holds (it grows to the largest
+ * batch span seen: the input and output byte ranges the batch touches, not
+ * their offsets). */
+size_t sqobfs_host_staging_bytes(const sqobfs_ctx *ctx);
+/* Test hook: the next sqobfs_run_host whose pipeline reaches chunk `chunk`
+ * fails there with SQ_EDEVICE, as a failed launch would (-1 = off). */
+void sqobfs_debug_fail_chunk(int chunk);
+
 /* ------------------------------------------------------------------------
  * Batched UDP socket I/O (Linux) -- the host side of the path.
  *

@@ -39,6 +39,9 @@ struct sqobfs_ctx {
 
 namespace {
 constexpr uint32_t kHostChunks = 8;  // sqobfs_run_host pipeline depth
+// test hook (sqobfs_debug_fail_chunk): the launch of that pipeline chunk
+// fails as a device error would, once
+std::atomic<int> g_fail_chunk{-1};
 constexpr uint32_t kEvents = 16;
 }
 
@@ -672,6 +675,10 @@ int sqobfs_quic_open(sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr, const sqobf
   return quic_launch(1, ctx, kr, b, stream);
 }
 
+size_t sqobfs_host_staging_bytes(const sqobfs_ctx *ctx) { return ctx ? ctx->pinned_cap : 0; }
+
+void sqobfs_debug_fail_chunk(int chunk) { g_fail_chunk.store(chunk); }
+
 int sqobfs_host_alloc(sqobfs_ctx *ctx, size_t bytes, void **out) {
   if (!ctx || !out) return SQ_EINVAL;
   *out = nullptr;
@@ -697,7 +704,6 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
   // input / output byte ranges it touches
   const uint32_t nchunk = n < 4096 ? 1u : std::min<uint32_t>(kHostChunks, (n + 4095) / 4096);
   std::vector<Range> rin(nchunk), rout(nchunk);
-  size_t in_ext = 0, out_ext = 0;
   for (uint32_t c = 0; c < nchunk; c++) {
     const uint32_t p0 = (uint32_t)((uint64_t)n * c / nchunk);
     const uint32_t p1 = (uint32_t)((uint64_t)n * (c + 1) / nchunk);
@@ -723,8 +729,6 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
     }
     if (ri.lo > ri.hi) ri.lo = ri.hi = 0;
     if (ro.lo > ro.hi) ro.lo = ro.hi = 0;
-    in_ext = std::max(in_ext, ri.hi);
-    out_ext = std::max(out_ext, ro.hi);
     rin[c] = ri;
     rout[c] = ro;
   }
@@ -751,6 +755,15 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
     rout.assign(1, ro);
   }
   const uint32_t nrun = (uint32_t)rin.size();
+  // staging covers only the spans the batch touches, [lo, hi) of each buffer
+  size_t in_lo = SIZE_MAX, in_hi = 0, out_lo = SIZE_MAX, out_hi = 0;
+  for (uint32_t c = 0; c < nrun; c++) {
+    if (rin[c].hi > rin[c].lo) in_lo = std::min(in_lo, rin[c].lo), in_hi = std::max(in_hi, rin[c].hi);
+    if (rout[c].hi > rout[c].lo)
+      out_lo = std::min(out_lo, rout[c].lo), out_hi = std::max(out_hi, rout[c].hi);
+  }
+  if (in_lo > in_hi) in_lo = in_hi = 0;
+  if (out_lo > out_hi) out_lo = out_hi = 0;
   // caller memory that is already pinned (sqobfs_host_alloc, hipHostMalloc)
   // is copied by DMA directly; pageable memory goes through pinned staging
   const bool in_pinned = is_pinned(hb->in), out_pinned = is_pinned(hb->out);
@@ -760,8 +773,8 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
   // for what is pageable)
   const size_t A = 256;
   size_t o = 0;
-  const size_t o_in = o;       o = align_up(o + in_ext, A);
-  const size_t o_out = o;      o = align_up(o + out_ext, A);
+  const size_t o_in = o;       o = align_up(o + (in_hi - in_lo), A);
+  const size_t o_out = o;      o = align_up(o + (out_hi - out_lo), A);
   const size_t o_inoff = o;    o = align_up(o + 8ull * n, A);
   const size_t o_inlen = o;    o = align_up(o + 4ull * n, A);
   const size_t o_outoff = o;   o = align_up(o + 8ull * n, A);
@@ -793,6 +806,25 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
   for (auto &e : ctx->ev)
     if (!e) SQ_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   uint8_t *H = ctx->pinned, *D = ctx->dev;
+  // staged image of buffer byte x: base + o + (x - lo)
+  auto hin = [&](size_t x) { return H + o_in + (x - in_lo); };
+  auto hout = [&](size_t x) { return H + o_out + (x - out_lo); };
+  auto din = [&](size_t x) { return D + o_in + (x - in_lo); };
+  auto dout = [&](size_t x) { return D + o_out + (x - out_lo); };
+  // Every failure past this point drains the three streams first, so no
+  // copy is still writing the caller's or the staging memory on return.
+  auto drain = [&](int code) {
+    (void)hipStreamSynchronize(ctx->h2d);
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipStreamSynchronize(ctx->d2h);
+    (void)hipGetLastError();
+    return code;
+  };
+#define SQ_TRY_DRAIN(x)                                    \
+  do {                                                     \
+    const int st_ = hip_status((x));                       \
+    if (st_ != SQ_OK) return drain(st_);                   \
+  } while (0)
 
   // descriptors: small, copied once up front
   memcpy(H + o_inoff, hb->in_off, 8ull * n);
@@ -801,9 +833,9 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
   if (dir == SQOBFS_OBFUSCATE && !dev_salt) memcpy(H + o_salt, hb->salt, S * n);
   if (hb->psk_id) memcpy(H + o_pid, hb->psk_id, 2ull * n);
   if (hb->in_cap) memcpy(H + o_cap, hb->in_cap, 4ull * n);
-  SQ_TRY(hipMemcpyAsync(D + o_inoff, H + o_inoff, o_outlen - o_inoff, hipMemcpyHostToDevice,
+  SQ_TRY_DRAIN(hipMemcpyAsync(D + o_inoff, H + o_inoff, o_outlen - o_inoff, hipMemcpyHostToDevice,
                         ctx->h2d));
-  SQ_TRY(hipMemcpyAsync(D + o_salt, H + o_salt, total - o_salt, hipMemcpyHostToDevice,
+  SQ_TRY_DRAIN(hipMemcpyAsync(D + o_salt, H + o_salt, total - o_salt, hipMemcpyHostToDevice,
                         ctx->h2d));
 
   // ---- pipeline: H2D(c) on h2d | kernel(c) on the compute stream | D2H(c)
@@ -814,30 +846,30 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
     if (ri.hi > ri.lo) {
       const uint8_t *src = hb->in + ri.lo;
       if (!in_pinned) {
-        par_memcpy(H + o_in + ri.lo, src, ri.hi - ri.lo);
-        src = H + o_in + ri.lo;
+        par_memcpy(hin(ri.lo), src, ri.hi - ri.lo);
+        src = hin(ri.lo);
       }
-      SQ_TRY(hipMemcpyAsync(D + o_in + ri.lo, src, ri.hi - ri.lo, hipMemcpyHostToDevice,
-                            ctx->h2d));
+      SQ_TRY_DRAIN(hipMemcpyAsync(din(ri.lo), src, ri.hi - ri.lo, hipMemcpyHostToDevice,
+                                  ctx->h2d));
     }
     if (preserve && ro.hi > ro.lo) {  // bytes between packets keep their value
       const uint8_t *src = hb->out + ro.lo;
       if (!out_pinned) {
-        par_memcpy(H + o_out + ro.lo, src, ro.hi - ro.lo);
-        src = H + o_out + ro.lo;
+        par_memcpy(hout(ro.lo), src, ro.hi - ro.lo);
+        src = hout(ro.lo);
       }
-      SQ_TRY(hipMemcpyAsync(D + o_out + ro.lo, src, ro.hi - ro.lo, hipMemcpyHostToDevice,
-                            ctx->h2d));
+      SQ_TRY_DRAIN(hipMemcpyAsync(dout(ro.lo), src, ro.hi - ro.lo, hipMemcpyHostToDevice,
+                                  ctx->h2d));
     }
     hipEvent_t ev_in = ctx->ev[(2 * c) % kEvents], ev_k = ctx->ev[(2 * c + 1) % kEvents];
-    SQ_TRY(hipEventRecord(ev_in, ctx->h2d));
-    SQ_TRY(hipStreamWaitEvent(ctx->stream, ev_in, 0));
+    SQ_TRY_DRAIN(hipEventRecord(ev_in, ctx->h2d));
+    SQ_TRY_DRAIN(hipStreamWaitEvent(ctx->stream, ev_in, 0));
     sqobfs_batch db = *hb;
     db.n = ri.p1 - ri.p0;
-    db.in = D + o_in;
+    db.in = din(0);  // in_off[i] >= in_lo for every packet of the batch
     db.in_off = (const uint64_t *)(D + o_inoff) + ri.p0;
     db.in_len = (const uint32_t *)(D + o_inlen) + ri.p0;
-    db.out = D + o_out;
+    db.out = dout(0);
     db.out_off = (const uint64_t *)(D + o_outoff) + ri.p0;
     db.out_len = (uint32_t *)(D + o_outlen) + ri.p0;
     db.salt = dir == SQOBFS_OBFUSCATE && !dev_salt ? D + o_salt + S * ri.p0 : nullptr;
@@ -846,30 +878,33 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
     db.in_cap = hb->in_cap ? (const uint32_t *)(D + o_cap) + ri.p0 : nullptr;
     if (db.n) {
       const sq::KParams kp = make_params(ctx, kr, &db);
-      st = sq_launch_obfs(kind, dir, &kp, ctx->stream);
-      if (st != SQ_OK) return st;
+      int fc = (int)c;
+      st = g_fail_chunk.compare_exchange_strong(fc, -1) ? SQ_EDEVICE
+                                                         : sq_launch_obfs(kind, dir, &kp, ctx->stream);
+      if (st != SQ_OK) return drain(st);
     }
-    SQ_TRY(hipEventRecord(ev_k, ctx->stream));
-    SQ_TRY(hipStreamWaitEvent(ctx->d2h, ev_k, 0));
+    SQ_TRY_DRAIN(hipEventRecord(ev_k, ctx->stream));
+    SQ_TRY_DRAIN(hipStreamWaitEvent(ctx->d2h, ev_k, 0));
     if (ro.hi > ro.lo) {
-      uint8_t *dst = out_pinned ? hb->out + ro.lo : H + o_out + ro.lo;
-      SQ_TRY(hipMemcpyAsync(dst, D + o_out + ro.lo, ro.hi - ro.lo, hipMemcpyDeviceToHost,
-                            ctx->d2h));
+      uint8_t *dst = out_pinned ? hb->out + ro.lo : hout(ro.lo);
+      SQ_TRY_DRAIN(hipMemcpyAsync(dst, dout(ro.lo), ro.hi - ro.lo, hipMemcpyDeviceToHost,
+                                  ctx->d2h));
     }
   }
-  SQ_TRY(hipMemcpyAsync(H + o_outlen, D + o_outlen, 4ull * n, hipMemcpyDeviceToHost, ctx->d2h));
+  SQ_TRY_DRAIN(hipMemcpyAsync(H + o_outlen, D + o_outlen, 4ull * n, hipMemcpyDeviceToHost, ctx->d2h));
   if (dev_salt && hb->salt_out)
-    SQ_TRY(hipMemcpyAsync(H + o_saltout, D + o_saltout, S * n, hipMemcpyDeviceToHost, ctx->d2h));
-  SQ_TRY(hipStreamSynchronize(ctx->d2h));
+    SQ_TRY_DRAIN(hipMemcpyAsync(H + o_saltout, D + o_saltout, S * n, hipMemcpyDeviceToHost, ctx->d2h));
+  SQ_TRY_DRAIN(hipStreamSynchronize(ctx->d2h));
   // pageable output: copy back in chunk order (later chunks win where
   // ranges interleave, matching the device order)
   if (!out_pinned)
     for (uint32_t c = 0; c < nrun; c++)
       if (rout[c].hi > rout[c].lo)
-        par_memcpy(hb->out + rout[c].lo, H + o_out + rout[c].lo, rout[c].hi - rout[c].lo);
+        par_memcpy(hb->out + rout[c].lo, hout(rout[c].lo), rout[c].hi - rout[c].lo);
   memcpy(hb->out_len, H + o_outlen, 4ull * n);
   if (dev_salt && hb->salt_out) memcpy(hb->salt_out, H + o_saltout, S * n);
   return SQ_OK;
+#undef SQ_TRY_DRAIN
 }
 
 }  // extern "C"

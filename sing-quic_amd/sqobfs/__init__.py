@@ -154,6 +154,10 @@ def lib() -> ctypes.CDLL:
     L.sqobfs_build_info.restype = ctypes.c_char_p
     L.sqobfs_build_info.argtypes = []
     L.sqobfs_host_free.restype = None
+    L.sqobfs_host_staging_bytes.argtypes = [vp]
+    L.sqobfs_host_staging_bytes.restype = ctypes.c_size_t
+    L.sqobfs_debug_fail_chunk.argtypes = [i32]
+    L.sqobfs_debug_fail_chunk.restype = None
     u16p, u32p = ctypes.POINTER(ctypes.c_uint16), ctypes.POINTER(ctypes.c_uint32)
     L.sqobfs_udp_recv.argtypes = [vp, u32, vp, u32, u32, u32, i32, vp, vp, vp, u32p]
     L.sqobfs_udp_send.argtypes = [i32, vp, vp, vp, vp, u32, u32p]
@@ -253,6 +257,11 @@ class Context:
     def sync(self, stream: int | None = None) -> None:
         _check(lib().sqobfs_sync(self.handle, stream), "sqobfs_sync")
 
+    @property
+    def staging_bytes(self) -> int:
+        """Pinned staging held by sqobfs_run_host."""
+        return int(lib().sqobfs_host_staging_bytes(self.handle))
+
     def salt_key(self, key: bytes, next_seq: int = 0) -> None:
         """Deterministic device-salt key and sequence (tests / replay)."""
         assert len(key) == 32
@@ -307,6 +316,11 @@ def launch(ctx: Context, kr: Keyring, direction: int, batch: Batch,
     """Device-resident launch (async on `stream`)."""
     _check(lib().sqobfs_launch(ctx.handle, kr.handle, direction, ctypes.byref(batch), stream),
            "sqobfs_launch")
+
+
+def debug_fail_chunk(chunk: int) -> None:
+    """Test hook: the next run_host fails (SQ_EDEVICE) at that pipeline chunk."""
+    lib().sqobfs_debug_fail_chunk(chunk)
 
 
 def run_host(ctx: Context, kr: Keyring, direction: int, batch: Batch) -> None:
