@@ -1,0 +1,235 @@
+//go:build linux && sqobfs
+
+// Package sqobfs binds the MI355X obfuscation library (include/sqobfs.h,
+// libsqobfs.so) for sing-quic's Salamander and XPlus decorators
+// (hysteria2/salamander.go, hysteria/xplus.go in the reference).
+//
+// cgo pointer rules: nothing below passes a Go pointer that holds other Go
+// pointers, and C never keeps a Go pointer after a call returns.  Every
+// batch descriptor and array handed to C is C memory (C.malloc), and the
+// datagram bytes live in page-locked C memory (sqobfs_host_alloc) that Go
+// code reads and writes through unsafe.Slice views.  Go byte slices passed
+// to C directly (the PSK blob) contain no pointers and are not retained.
+//
+// Not compiled in the repository's own image (it has no Go toolchain); the
+// exact C call sequence of this file is replayed by tests/cpp/test_cgo_sequence.c.
+package sqobfs
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../third_party/sqobfs/include
+#cgo LDFLAGS: -L${SRCDIR}/../../third_party/sqobfs/lib -lsqobfs -Wl,-rpath,${SRCDIR}/../../third_party/sqobfs/lib
+#include <stdlib.h>
+#include <string.h>
+#include "sqobfs.h"
+*/
+import "C"
+
+import (
+	"errors"
+	"runtime"
+	"unsafe"
+)
+
+// Kind of obfuscation (include/sqobfs.h enum sqobfs_kind).
+type Kind int
+
+const (
+	Salamander Kind = C.SQOBFS_SALAMANDER // hysteria2/salamander.go
+	XPlus      Kind = C.SQOBFS_XPLUS      // hysteria/xplus.go
+)
+
+// Direction of a batch.
+type Direction int
+
+const (
+	Obfuscate   Direction = C.SQOBFS_OBFUSCATE
+	Deobfuscate Direction = C.SQOBFS_DEOBFUSCATE
+)
+
+// SaltLen is the salt in front of every datagram: 8 (salamander.go:15) or
+// 16 (xplus.go:17).
+func (k Kind) SaltLen() int {
+	if k == Salamander {
+		return C.SQOBFS_SALAMANDER_SALT_LEN
+	}
+	return C.SQOBFS_XPLUS_SALT_LEN
+}
+
+// Error is a negative sqobfs status code.
+type Error int
+
+func (e Error) Error() string { return "sqobfs: " + C.GoString(C.sqobfs_strerror(C.int(e))) }
+
+func check(st C.int) error {
+	if st != C.SQ_OK {
+		return Error(st)
+	}
+	return nil
+}
+
+// Context is one GPU (sqobfs_open).  Safe for concurrent use.
+type Context struct{ c *C.sqobfs_ctx }
+
+func Open(device int) (*Context, error) {
+	var c *C.sqobfs_ctx
+	if err := check(C.sqobfs_open(C.int(device), &c)); err != nil {
+		return nil, err
+	}
+	return &Context{c: c}, nil
+}
+
+func (x *Context) Close() {
+	if x.c != nil {
+		C.sqobfs_close(x.c)
+		x.c = nil
+	}
+}
+
+// Keyring is the device copy of the PSK: the `password` captured by
+// NewSalamanderConn (salamander.go:19-40) or the `key` of NewXPlusPacketConn
+// (xplus.go:19-44).
+type Keyring struct {
+	kr   *C.sqobfs_keyring
+	Kind Kind
+}
+
+func (x *Context) NewKeyring(kind Kind, psk []byte) (*Keyring, error) {
+	// a private C copy: the reference's append(password, salt...) can write
+	// into the password's spare capacity (SURVEY.md section 5); this never does
+	blob := C.malloc(C.size_t(len(psk) + 1))
+	defer C.free(blob)
+	if len(psk) > 0 {
+		C.memcpy(blob, unsafe.Pointer(&psk[0]), C.size_t(len(psk)))
+	}
+	off := (*C.uint64_t)(C.malloc(8))
+	ln := (*C.uint32_t)(C.malloc(4))
+	defer C.free(unsafe.Pointer(off))
+	defer C.free(unsafe.Pointer(ln))
+	*off, *ln = 0, C.uint32_t(len(psk))
+	var kr *C.sqobfs_keyring
+	if err := check(C.sqobfs_keyring_create(x.c, C.int(kind), 1, (*C.uint8_t)(blob), off, ln,
+		&kr)); err != nil {
+		return nil, err
+	}
+	return &Keyring{kr: kr, Kind: kind}, nil
+}
+
+func (k *Keyring) Close() {
+	if k.kr != nil {
+		C.sqobfs_keyring_destroy(k.kr)
+		k.kr = nil
+	}
+}
+
+// Slots is a ragged batch of up to Cap datagrams in C memory: a
+// page-locked data region of Cap fixed slots of SlotBytes (DMA'd by
+// sqobfs_run_host without staging) and the sqobfs_batch descriptor with its
+// arrays, all allocated by C.  Go code fills and reads the slots through
+// unsafe.Slice views; the C side never sees a Go pointer.
+type Slots struct {
+	ctx       *Context
+	Cap       int
+	SlotBytes int
+	data      unsafe.Pointer // sqobfs_host_alloc: Cap*SlotBytes (in) + Cap*SlotBytes (out)
+	b         *C.sqobfs_batch
+	inOff     []uint64 // views of C arrays
+	inLen     []uint32
+	outOff    []uint64
+	outLen    []uint32
+	inCap     []uint32
+	salt      []byte
+}
+
+func (x *Context) NewSlots(capacity, slotBytes int, saltLen int) (*Slots, error) {
+	if capacity <= 0 || slotBytes <= 0 {
+		return nil, errors.New("sqobfs: bad slot geometry")
+	}
+	s := &Slots{ctx: x, Cap: capacity, SlotBytes: slotBytes}
+	if err := check(C.sqobfs_host_alloc(x.c, C.size_t(2*capacity*slotBytes), &s.data)); err != nil {
+		return nil, err
+	}
+	s.b = (*C.sqobfs_batch)(C.calloc(1, C.size_t(unsafe.Sizeof(C.sqobfs_batch{}))))
+	n := C.size_t(capacity)
+	io := (*uint64)(C.malloc(8 * n))
+	oo := (*uint64)(C.malloc(8 * n))
+	il := (*uint32)(C.malloc(4 * n))
+	ol := (*uint32)(C.malloc(4 * n))
+	ic := (*uint32)(C.malloc(4 * n))
+	sl := (*byte)(C.malloc(16 * n)) // malloc alignment >= 16: salts 4-byte aligned
+	s.inOff = unsafe.Slice(io, capacity)
+	s.outOff = unsafe.Slice(oo, capacity)
+	s.inLen = unsafe.Slice(il, capacity)
+	s.outLen = unsafe.Slice(ol, capacity)
+	s.inCap = unsafe.Slice(ic, capacity)
+	s.salt = unsafe.Slice(sl, 16*capacity)
+	for i := 0; i < capacity; i++ {
+		s.inOff[i] = uint64(i * slotBytes)
+		s.outOff[i] = uint64((capacity + i) * slotBytes) // out region after the in region
+	}
+	base := (*C.uint8_t)(s.data)
+	s.b.in = base
+	s.b.out = base
+	s.b.in_off = (*C.uint64_t)(unsafe.Pointer(io))
+	s.b.in_len = (*C.uint32_t)(unsafe.Pointer(il))
+	s.b.out_off = (*C.uint64_t)(unsafe.Pointer(oo))
+	s.b.out_len = (*C.uint32_t)(unsafe.Pointer(ol))
+	s.b.salt = (*C.uint8_t)(unsafe.Pointer(sl))
+	runtime.SetFinalizer(s, (*Slots).Free)
+	return s, nil
+}
+
+// In is input slot i (len SlotBytes); Out is output slot i.
+func (s *Slots) In(i int) []byte {
+	return unsafe.Slice((*byte)(unsafe.Add(s.data, i*s.SlotBytes)), s.SlotBytes)
+}
+func (s *Slots) Out(i int) []byte {
+	return unsafe.Slice((*byte)(unsafe.Add(s.data, (s.Cap+i)*s.SlotBytes)), s.SlotBytes)
+}
+
+// SetLen sets packet i's input length (payload for obfuscate, datagram n for
+// deobfuscate); SetCap sets XPlus's read-buffer length len(p) (xplus.go:55).
+func (s *Slots) SetLen(i, n int) { s.inLen[i] = uint32(n) }
+func (s *Slots) SetCap(i, c int) { s.inCap[i] = uint32(c) }
+
+// Salt is packet i's salt (obfuscate with caller salts).
+func (s *Slots) Salt(i, saltLen int) []byte { return s.salt[i*saltLen : (i+1)*saltLen] }
+
+// OutLen is packet i's output length after Run (the reference's return
+// value rules, include/sqobfs.h).
+func (s *Slots) OutLen(i int) int { return int(s.outLen[i]) }
+
+// Run transforms packets [0, n) in one sqobfs_run_host call (H2D, one
+// launch, D2H).  deviceSalt: obfuscate with salts generated on the GPU
+// (replaces buf.WriteRandom, salamander.go:60, and math/rand, xplus.go:67-69).
+// withCap: XPlus deobfuscate XORs up to SetCap bytes (xplus.go:55).
+func (s *Slots) Run(kr *Keyring, dir Direction, n int, deviceSalt, withCap bool) error {
+	if n < 0 || n > s.Cap {
+		return errors.New("sqobfs: batch larger than its slots")
+	}
+	s.b.n = C.uint32_t(n)
+	s.b.flags = 0
+	if dir == Obfuscate && deviceSalt {
+		s.b.flags = C.SQOBFS_FLAG_DEVICE_SALT
+	}
+	s.b.in_cap = nil
+	if withCap {
+		s.b.in_cap = (*C.uint32_t)(unsafe.Pointer(&s.inCap[0])) // C memory
+	}
+	return check(C.sqobfs_run_host(s.ctx.c, kr.kr, C.int(dir), s.b))
+}
+
+func (s *Slots) Free() {
+	if s.b == nil {
+		return
+	}
+	runtime.SetFinalizer(s, nil)
+	C.free(unsafe.Pointer(s.b.in_off))
+	C.free(unsafe.Pointer(s.b.out_off))
+	C.free(unsafe.Pointer(s.b.in_len))
+	C.free(unsafe.Pointer(s.b.out_len))
+	C.free(unsafe.Pointer(&s.inCap[0]))
+	C.free(unsafe.Pointer(s.b.salt))
+	C.free(unsafe.Pointer(s.b))
+	C.sqobfs_host_free(s.ctx.c, s.data)
+	s.b = nil
+}

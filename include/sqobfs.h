@@ -137,7 +137,9 @@ int sqobfs_device_count(int *count);
 
 /* One context per GPU.  Thread-safe: device launches only read immutable
  * state (and bump an atomic salt sequence number); sqobfs_run_host
- * serialises on an internal lock. */
+ * serialises on an internal lock.  Every entry point makes the context's GPU
+ * current for its own duration and restores the calling thread's current
+ * device before returning (no per-thread side effect). */
 int sqobfs_open(int device, sqobfs_ctx **out);
 void sqobfs_close(sqobfs_ctx *ctx);
 /* the context's own non-blocking HIP stream (as void*), for callers that
@@ -301,6 +303,29 @@ int sqobfs_quic_seal_salamander(sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr,
 int sqobfs_quic_open_salamander(sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr,
                                 const sqobfs_keyring *okr, const sqobfs_quic_batch *b,
                                 void *stream);
+
+/* ------------------------------------------------------------------------
+ * Several GPUs in one process (packets are independent, so a
+ * batch shards into contiguous ranges with no exchange at all).
+ */
+
+/* Contiguous shards of nearly equal work: cut[k] = first packet of shard k
+ * (k < parts), cut[parts] = n, balanced by cumulative bytes (in_len plus a
+ * small per-packet constant), so ragged batches split evenly.  cut has
+ * parts + 1 entries. */
+int sqobfs_shard_cuts(uint32_t n, const uint32_t *in_len, uint32_t parts, uint32_t *cut);
+/* One host-memory batch over nctx contexts (GPUs): shard k (sqobfs_shard_cuts)
+ * runs sqobfs_run_host on ctxs[k] with krs[k] (keyrings of the same kind and
+ * PSKs, one per context), each shard on its own host thread with its own
+ * pinned staging and streams.  Returns the first error, after every shard
+ * has finished.  With SQOBFS_FLAG_DEVICE_SALT each shard draws its salts from
+ * its own context's generator. */
+int sqobfs_run_host_sharded(uint32_t nctx, sqobfs_ctx *const *ctxs,
+                            const sqobfs_keyring *const *krs, int dir, const sqobfs_batch *hb);
+/* Device-resident shards: bs[k] lives on ctxs[k]'s GPU and is launched there
+ * on the context's stream; returns after all shards complete (first error). */
+int sqobfs_shard_run(uint32_t nctx, sqobfs_ctx *const *ctxs, const sqobfs_keyring *const *krs,
+                     int dir, const sqobfs_batch *bs);
 
 /* Bytes of pinned staging sqobfs_run_host holds (it grows to the largest
  * batch span seen: the input and output byte ranges the batch touches, not

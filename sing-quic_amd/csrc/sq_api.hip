@@ -79,6 +79,31 @@ int hip_status(hipError_t e) {
     if (st_ != SQ_OK) return st_;        \
   } while (0)
 
+// Makes `device` current on the calling thread for one entry point and
+// restores the caller's device on return: the ABI leaves no per-thread side
+// effect (a Go host's goroutines migrate between OS threads, and a host
+// running several GPUs keeps its own notion of the current one).
+struct DeviceScope {
+  int prev = -1;
+  bool changed = false;
+  int status = SQ_OK;
+  explicit DeviceScope(int device) {
+    if (hipGetDevice(&prev) != hipSuccess) {
+      (void)hipGetLastError();
+      prev = -1;
+    }
+    if (prev != device) {
+      status = hip_status(hipSetDevice(device));
+      changed = status == SQ_OK;
+    }
+  }
+  ~DeviceScope() {
+    if (changed && prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceScope(const DeviceScope &) = delete;
+  DeviceScope &operator=(const DeviceScope &) = delete;
+};
+
 size_t salt_len(int kind) {
   return kind == SQOBFS_SALAMANDER ? SQOBFS_SALAMANDER_SALT_LEN : SQOBFS_XPLUS_SALT_LEN;
 }
@@ -203,7 +228,8 @@ int sqobfs_open(int device, sqobfs_ctx **out) {
   *out = nullptr;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return SQ_ENODEV;
-  SQ_TRY(hipSetDevice(device));
+  DeviceScope ds_(device);
+  if (ds_.status != SQ_OK) return ds_.status;
   sqobfs_ctx *c = new (std::nothrow) sqobfs_ctx();
   if (!c) return SQ_ENOMEM;
   c->device = device;
@@ -235,7 +261,7 @@ int sqobfs_open(int device, sqobfs_ctx **out) {
 
 void sqobfs_close(sqobfs_ctx *ctx) {
   if (!ctx) return;
-  (void)hipSetDevice(ctx->device);
+  DeviceScope ds_(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   if (ctx->dev) (void)hipFree(ctx->dev);
@@ -260,7 +286,8 @@ void *sqobfs_stream(sqobfs_ctx *ctx) { return ctx ? (void *)ctx->stream : nullpt
 
 int sqobfs_sync(sqobfs_ctx *ctx, void *stream) {
   if (!ctx) return SQ_EINVAL;
-  SQ_TRY(hipSetDevice(ctx->device));
+  DeviceScope ds_(ctx->device);
+  if (ds_.status != SQ_OK) return ds_.status;
   return hip_status(hipStreamSynchronize(pick_stream(ctx, stream)));
 }
 
@@ -272,7 +299,8 @@ int sqobfs_keyring_create(sqobfs_ctx *ctx, int kind, uint32_t count, const uint8
   size_t blob_bytes = 0;
   for (uint32_t k = 0; k < count; k++) blob_bytes = std::max<size_t>(blob_bytes, off[k] + len[k]);
   if (blob_bytes && !blob) return SQ_EINVAL;
-  SQ_TRY(hipSetDevice(ctx->device));
+  DeviceScope ds_(ctx->device);
+  if (ds_.status != SQ_OK) return ds_.status;
   sqobfs_keyring *kr = new (std::nothrow) sqobfs_keyring();
   if (!kr) return SQ_ENOMEM;
   kr->ctx = ctx;
@@ -312,7 +340,7 @@ int sqobfs_keyring_create(sqobfs_ctx *ctx, int kind, uint32_t count, const uint8
 
 void sqobfs_keyring_destroy(sqobfs_keyring *kr) {
   if (!kr) return;
-  (void)hipSetDevice(kr->ctx->device);
+  DeviceScope ds_(kr->ctx->device);
   (void)hipDeviceSynchronize();  // launches on any stream may still read the table
   if (kr->table) (void)hipFree(kr->table);
   delete kr;
@@ -327,7 +355,8 @@ int sqobfs_launch(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir, const sqob
   if (dir != SQOBFS_OBFUSCATE && dir != SQOBFS_DEOBFUSCATE) return SQ_EINVAL;
   const int st = check_batch_shape(b, dir);
   if (st != SQ_OK || b->n == 0) return st;
-  SQ_TRY(hipSetDevice(ctx->device));
+  DeviceScope ds_(ctx->device);
+  if (ds_.status != SQ_OK) return ds_.status;
   const sq::KParams kp = make_params(ctx, kr, b);
   return sq_launch_obfs(kr->kind, dir, &kp, pick_stream(ctx, stream));
 }
@@ -530,7 +559,8 @@ int sqobfs_quic_keyring_create_suite(sqobfs_ctx *ctx, uint32_t suite, uint32_t c
   if (!ctx || !out || count == 0 || !keys) return SQ_EINVAL;
   if (suite != SQOBFS_QUIC_CHACHA20_POLY1305 && suite != SQOBFS_QUIC_AES_128_GCM)
     return SQ_EINVAL;
-  SQ_TRY(hipSetDevice(ctx->device));
+  DeviceScope ds_(ctx->device);
+  if (ds_.status != SQ_OK) return ds_.status;
   sqobfs_quic_keyring *kr = new (std::nothrow) sqobfs_quic_keyring();
   if (!kr) return SQ_ENOMEM;
   kr->ctx = ctx;
@@ -581,7 +611,7 @@ int sqobfs_quic_keyring_create(sqobfs_ctx *ctx, uint32_t count, const sqobfs_qui
 
 void sqobfs_quic_keyring_destroy(sqobfs_quic_keyring *kr) {
   if (!kr) return;
-  (void)hipSetDevice(kr->ctx->device);
+  DeviceScope ds_(kr->ctx->device);
   (void)hipDeviceSynchronize();
   if (kr->table) (void)hipFree(kr->table);
   if (kr->gtable) (void)hipFree(kr->gtable);
@@ -599,7 +629,8 @@ static int quic_launch(int open, sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr,
   if (!b->in || !b->in_off || !b->in_len || !b->out || !b->out_off || !b->out_len ||
       !b->pn_offset || !b->pn)
     return SQ_EINVAL;
-  SQ_TRY(hipSetDevice(ctx->device));
+  DeviceScope ds_(ctx->device);
+  if (ds_.status != SQ_OK) return ds_.status;
   if (kr->suite == SQOBFS_QUIC_AES_128_GCM) {
     sq::QGParams g;
     memset(&g, 0, sizeof g);
@@ -682,7 +713,8 @@ void sqobfs_debug_fail_chunk(int chunk) { g_fail_chunk.store(chunk); }
 int sqobfs_host_alloc(sqobfs_ctx *ctx, size_t bytes, void **out) {
   if (!ctx || !out) return SQ_EINVAL;
   *out = nullptr;
-  SQ_TRY(hipSetDevice(ctx->device));
+  DeviceScope ds_(ctx->device);
+  if (ds_.status != SQ_OK) return ds_.status;
   return hip_status(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
 }
 
@@ -788,7 +820,8 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
   const size_t total = o;
 
   std::lock_guard<std::mutex> lk(ctx->mu);
-  SQ_TRY(hipSetDevice(ctx->device));
+  DeviceScope ds_(ctx->device);
+  if (ds_.status != SQ_OK) return ds_.status;
   if (ctx->pinned_cap < total) {
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
     ctx->pinned = nullptr;
@@ -905,6 +938,91 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
   if (dev_salt && hb->salt_out) memcpy(hb->salt_out, H + o_saltout, S * n);
   return SQ_OK;
 #undef SQ_TRY_DRAIN
+}
+
+// ---------------------------------------------------------------- shards
+
+int sqobfs_shard_cuts(uint32_t n, const uint32_t *in_len, uint32_t parts, uint32_t *cut) {
+  if (!cut || parts == 0 || (n && !in_len)) return SQ_EINVAL;
+  // weight = bytes + a per-packet constant (descriptor, key derivation), so
+  // runs of empty datagrams still spread
+  constexpr uint64_t kPerPacket = 64;
+  uint64_t tot = 0;
+  for (uint32_t i = 0; i < n; i++) tot += in_len[i] + kPerPacket;
+  cut[0] = 0;
+  uint64_t acc = 0;
+  uint32_t i = 0;
+  for (uint32_t k = 1; k < parts; k++) {
+    const uint64_t want = tot * k / parts;
+    while (i < n && acc + in_len[i] + kPerPacket / 2 <= want) acc += in_len[i++] + kPerPacket;
+    cut[k] = i;
+  }
+  cut[parts] = n;
+  return SQ_OK;
+}
+
+namespace {
+// packets [p0, p1) of b as a batch of their own (same buffers)
+sqobfs_batch sub_batch(const sqobfs_batch &b, uint32_t p0, uint32_t p1, size_t S) {
+  sqobfs_batch s = b;
+  s.n = p1 - p0;
+  s.in_off = b.in_off + p0;
+  s.in_len = b.in_len + p0;
+  s.out_off = b.out_off + p0;
+  s.out_len = b.out_len + p0;
+  if (b.salt) s.salt = b.salt + S * p0;
+  if (b.psk_id) s.psk_id = b.psk_id + p0;
+  if (b.in_cap) s.in_cap = b.in_cap + p0;
+  if (b.salt_out) s.salt_out = b.salt_out + S * p0;
+  return s;
+}
+}  // namespace
+
+int sqobfs_run_host_sharded(uint32_t nctx, sqobfs_ctx *const *ctxs,
+                            const sqobfs_keyring *const *krs, int dir, const sqobfs_batch *hb) {
+  if (nctx == 0 || !ctxs || !krs || !hb) return SQ_EINVAL;
+  for (uint32_t k = 0; k < nctx; k++)
+    if (!ctxs[k] || !krs[k] || krs[k]->ctx != ctxs[k] || krs[k]->kind != krs[0]->kind)
+      return SQ_EINVAL;
+  if (nctx == 1) return sqobfs_run_host(ctxs[0], krs[0], dir, hb);
+  const int st0 = check_batch_shape(hb, dir);
+  if (st0 != SQ_OK || hb->n == 0) return st0;
+  std::vector<uint32_t> cut(nctx + 1);
+  const int sc = sqobfs_shard_cuts(hb->n, hb->in_len, nctx, cut.data());
+  if (sc != SQ_OK) return sc;
+  const size_t S = salt_len(krs[0]->kind);
+  std::vector<int> st(nctx, SQ_OK);
+  std::vector<std::thread> th;
+  for (uint32_t k = 0; k < nctx; k++) {
+    if (cut[k + 1] == cut[k]) continue;
+    th.emplace_back([&, k] {
+      const sqobfs_batch sb = sub_batch(*hb, cut[k], cut[k + 1], S);
+      st[k] = sqobfs_run_host(ctxs[k], krs[k], dir, &sb);
+    });
+  }
+  for (auto &t : th) t.join();
+  for (int x : st)
+    if (x != SQ_OK) return x;
+  return SQ_OK;
+}
+
+int sqobfs_shard_run(uint32_t nctx, sqobfs_ctx *const *ctxs, const sqobfs_keyring *const *krs,
+                     int dir, const sqobfs_batch *bs) {
+  if (nctx == 0 || !ctxs || !krs || !bs) return SQ_EINVAL;
+  for (uint32_t k = 0; k < nctx; k++)
+    if (!ctxs[k] || !krs[k] || krs[k]->ctx != ctxs[k]) return SQ_EINVAL;
+  // launches are asynchronous: one host thread issues every shard on its
+  // context's stream, then waits for all of them
+  int st = SQ_OK;
+  uint32_t launched = 0;
+  for (; launched < nctx && st == SQ_OK; launched++)
+    st = sqobfs_launch(ctxs[launched], krs[launched], dir, &bs[launched],
+                       sqobfs_stream(ctxs[launched]));
+  for (uint32_t k = 0; k < launched; k++) {
+    const int s2 = sqobfs_sync(ctxs[k], sqobfs_stream(ctxs[k]));
+    if (st == SQ_OK) st = s2;
+  }
+  return st;
 }
 
 }  // extern "C"

@@ -158,6 +158,9 @@ def lib() -> ctypes.CDLL:
     L.sqobfs_host_staging_bytes.restype = ctypes.c_size_t
     L.sqobfs_debug_fail_chunk.argtypes = [i32]
     L.sqobfs_debug_fail_chunk.restype = None
+    L.sqobfs_shard_cuts.argtypes = [u32, vp, u32, vp]
+    L.sqobfs_run_host_sharded.argtypes = [u32, vp, vp, i32, ctypes.POINTER(Batch)]
+    L.sqobfs_shard_run.argtypes = [u32, vp, vp, i32, vp]
     u16p, u32p = ctypes.POINTER(ctypes.c_uint16), ctypes.POINTER(ctypes.c_uint32)
     L.sqobfs_udp_recv.argtypes = [vp, u32, vp, u32, u32, u32, i32, vp, vp, vp, u32p]
     L.sqobfs_udp_send.argtypes = [i32, vp, vp, vp, vp, u32, u32p]
@@ -316,6 +319,33 @@ def launch(ctx: Context, kr: Keyring, direction: int, batch: Batch,
     """Device-resident launch (async on `stream`)."""
     _check(lib().sqobfs_launch(ctx.handle, kr.handle, direction, ctypes.byref(batch), stream),
            "sqobfs_launch")
+
+
+def shard_cuts(in_len: np.ndarray, parts: int) -> np.ndarray:
+    """sqobfs_shard_cuts: parts + 1 cut points balanced by bytes."""
+    ln = np.ascontiguousarray(in_len, dtype=np.uint32)
+    cut = np.zeros(parts + 1, dtype=np.uint32)
+    _check(lib().sqobfs_shard_cuts(ln.size, _ptr(ln), parts, _ptr(cut)), "sqobfs_shard_cuts")
+    return cut
+
+
+def _handles(objs):
+    return (ctypes.c_void_p * len(objs))(*[o.handle for o in objs])
+
+
+def run_host_sharded(ctxs: list[Context], krs: list[Keyring], direction: int,
+                     batch: Batch) -> None:
+    """One host batch over several contexts, one host thread per shard."""
+    _check(lib().sqobfs_run_host_sharded(len(ctxs), _handles(ctxs), _handles(krs), direction,
+                                         ctypes.byref(batch)), "sqobfs_run_host_sharded")
+
+
+def shard_run(ctxs: list[Context], krs: list[Keyring], direction: int,
+              batches: list[Batch]) -> None:
+    """Device-resident shards, shard k on ctxs[k]'s GPU; returns when all are done."""
+    arr = (Batch * len(batches))(*batches)
+    _check(lib().sqobfs_shard_run(len(ctxs), _handles(ctxs), _handles(krs), direction, arr),
+           "sqobfs_shard_run")
 
 
 def debug_fail_chunk(chunk: int) -> None:

@@ -78,3 +78,22 @@ def test_no_gpu_reports_enodev_not_fallback():
     with pytest.raises(sqobfs.SqError) as e:
         sqobfs.Context(0)
     assert e.value.status == sqobfs.SQ_ENODEV
+
+
+def test_shard_cuts_balance_bytes():
+    """sqobfs_shard_cuts (host logic, no GPU): contiguous, covering, and
+    balanced by cumulative bytes for ragged batches."""
+    import numpy as np
+    rng = np.random.Generator(np.random.PCG64(5))
+    for n, parts in [(0, 3), (1, 4), (7, 8), (100_000, 8), (100_000, 3)]:
+        lens = rng.integers(64, 1453, n).astype(np.uint32)
+        cut = sqobfs.shard_cuts(lens, parts)
+        assert cut[0] == 0 and cut[-1] == n and np.all(np.diff(cut.astype(np.int64)) >= 0)
+        if n >= 1000:
+            w = lens.astype(np.int64) + 64
+            share = np.add.reduceat(w, cut[:-1].astype(np.int64)) if n else w
+            assert share.max() - share.min() <= 2 * (1452 + 64), share
+    # a skewed batch: one half tiny, one half large -> cut far from n/2
+    lens = np.concatenate([np.full(5000, 0, np.uint32), np.full(5000, 1400, np.uint32)])
+    cut = sqobfs.shard_cuts(lens, 2)
+    assert abs(int(cut[1]) - 7391) <= 1  # (5000*64 + 5000*1464) / 2 bytes each side

@@ -37,3 +37,34 @@ def test_host_mirror_against_oracle():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "ok" in r.stdout
+
+
+CGO_SRC = os.path.join(REPO, "tests", "cpp", "test_cgo_sequence.c")
+CGO_OUT = os.path.join(REPO, "build", "test_cgo_sequence")
+
+
+def _compile_cgo_replay() -> str:
+    os.makedirs(os.path.dirname(CGO_OUT), exist_ok=True)
+    subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)
+    lib = os.path.join(REPO, "sing-quic_amd")
+    cmd = ["gcc", "-std=c11", "-O1", "-Wall", "-Wextra", "-I", os.path.join(REPO, "include"),
+           "-I", os.path.join(REPO, "oracle"), CGO_SRC, "-L", lib, "-lsqobfs",
+           "-L", os.path.join(REPO, "oracle"), "-loracle", f"-Wl,-rpath,{lib}",
+           f"-Wl,-rpath,{os.path.join(REPO, 'oracle')}", "-o", CGO_OUT]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    return CGO_OUT
+
+
+def test_cgo_replay_compiles_as_c():
+    """The Go binding's call sequence (tests/cpp/test_cgo_sequence.c) is plain
+    C against include/sqobfs.h: what cgo sees."""
+    _compile_cgo_replay()
+
+
+@pytest.mark.gpu
+def test_cgo_replay_against_oracle():
+    exe = _compile_cgo_replay()
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ok" in r.stdout
