@@ -58,6 +58,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=2.0,
                     help="wall seconds of CPU-baseline sampling (x threads = CPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--inproc", type=int, default=0,
+                    help="in-process sharding: one process, K contexts over the visible GPUs "
+                         "(context k on GPU k mod count), the config's batch cut by bytes "
+                         "(sqobfs_shard_cuts) and launched with sqobfs_shard_run")
     ap.add_argument("--packets", type=int, default=0,
                     help="dev: override the config's packet count (scaling probes; not a "
                          "BASELINE configuration)")
@@ -299,8 +303,8 @@ def host_info(torch, dev) -> dict:
 
 
 def load_traffic(config: str, kernel_bytes: float):
-    """HBM bytes per launch from the committed PMC pass (profiles/)."""
-    path = os.path.join(REPO, "profiles", f"pmc_{config}.json")
+    """HBM bytes per launch from the committed PMC pass (profiles/r02/)."""
+    path = os.path.join(REPO, "profiles", "r02", f"pmc_{config}.json")
     if not os.path.exists(path):
         return None, None
     with open(path) as f:
@@ -308,8 +312,89 @@ def load_traffic(config: str, kernel_bytes: float):
     return d.get("hbm_bytes_per_launch"), d
 
 
+def inproc_bench(args):
+    """sqobfs_shard_run over K contexts in one process (the Go service's
+    multi-GPU path); one JSON line."""
+    import torch
+    import sqobfs
+    ndev = torch.cuda.device_count()
+    assert ndev > 0, "bench.py needs a GPU"
+    kind, n_total, L, n_psk = CONFIGS[args.config]
+    if args.packets:
+        n_total = args.packets
+    K = args.inproc
+    # shard sizes by bytes (fixed-length configs split evenly)
+    lens_all = (torch.randint(64, 1453, (n_total,), generator=torch.Generator().manual_seed(4))
+                if L is None else torch.full((n_total,), L))
+    cut = sqobfs.shard_cuts(lens_all.numpy().astype("uint32"), K)
+    ctxs, krs, bs, shs, devs = [], [], [], [], []
+    payload = 0
+    for k in range(K):
+        g = k % ndev
+        dev = torch.device("cuda", g)
+        n_k = int(cut[k + 1] - cut[k])
+        sh = build_shard(torch, dev, kind, n_k, L, n_psk, k, K, args.config, "dense", int(cut[k]))
+        c = sqobfs.Context(g)
+        kr = sqobfs.Keyring(c, kind, sh["psks"])
+        ctxs.append(c)
+        krs.append(kr)
+        shs.append(sh)
+        devs.append(dev)
+        bs.append(sqobfs.make_batch(n_k, sh["data"], sh["in_off"], sh["lens"], sh["out"],
+                                    sh["out_off"], sh["out_len"], sh["salt"], sh["psk_id"]))
+        payload += sh["payload_bytes"]
+    for d in set(devs):
+        torch.cuda.synchronize(d)
+    for _ in range(args.warmup):
+        sqobfs.shard_run(ctxs, krs, sqobfs.OBFUSCATE, bs)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sqobfs.shard_run(ctxs, krs, sqobfs.OBFUSCATE, bs)
+    el = time.perf_counter() - t0
+    out = {"metric": f"GiB/s payload obfuscated, device-resident, {args.config}, "
+                     f"{K} in-process shards (sqobfs_shard_run)",
+           "value": round(payload * args.steps / el / 2**30, 3), "unit": "GiB/s",
+           "n_gpus": len(set(devs)), "contexts": K, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(el * 1e3 / args.steps, 4),
+           "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
+           "data": "synthetic", "shard_packets": [int(cut[k + 1] - cut[k]) for k in range(K)],
+           "config": {"workload": args.config, "inproc": K}}
+    print(json.dumps(out), flush=True)
+    for kr in krs:
+        kr.close()
+    for c in ctxs:
+        c.close()
+
+
+def quic_valu_roofline(suite_name: str, op: str, kernel_us: float):
+    """VALU roofline of a QUIC kernel from the committed PMC pass
+    (profiles/r02/quic/quic_pmc_summary.json, scripts/r2_quic_pmc.sh): VALU
+    wave-instructions per launch (SQ_INSTS_VALU) over this run's kernel time,
+    against 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction."""
+    f = os.path.join(REPO, "profiles", "r02", "quic", "quic_pmc_summary.json")
+    if not os.path.exists(f):
+        return None
+    d = json.load(open(f))
+    name = {"chacha20_poly1305": "quic_kernel", "aes_128_gcm": "quic_gcm_kernel"}[suite_name]
+    tmpl = {"seal": "<false, false, false>", "open": "<true, false, false>",
+            "fused_seal": "<false, false, true>", "fused_open": "<true, false, true>"}[op]
+    for k, e in d["kernels"].items():
+        if f"sq::{name}{tmpl}" in k:
+            valu = e["counters"]["SQ_INSTS_VALU"]
+            peak = d["peak_valu_wave_instr_per_s"]
+            ach = valu / (kernel_us * 1e-6)
+            return {"bound": "valu", "valu_wave_instr_per_launch": round(valu),
+                    "valu_wave_instr_per_packet": round(valu / (1 << 20), 1),
+                    "achieved": round(ach / 1e12, 4), "peak": round(peak / 1e12, 4),
+                    "unit": "T wave-instr/s", "frac": round(ach / peak, 4),
+                    "source": "profiles/r02/quic/quic_pmc_summary.json (SQ_INSTS_VALU)"}
+    return None
+
+
 def main():
     args = parse()
+    if args.inproc:
+        return inproc_bench(args)
     import torch
     import sqobfs
 
@@ -364,8 +449,10 @@ def main():
                                sh["out_off"], sh["out_len"], sh["salt"], sh["psk_id"])
         sqobfs.launch(ctx, kr, sqobfs.OBFUSCATE, b0, s)
         wire_len = (sh["lens"] + S).to(torch.int32)
-        back = torch.zeros_like(sh["data"])
-        b = sqobfs.make_batch(n, sh["out"], sh["out_off"], wire_len, back, sh["in_off"],
+        # decoded payloads back to back (a compact receive buffer)
+        back_off = torch.cumsum(sh["lens"].to(torch.int64), 0) - sh["lens"].to(torch.int64) + 64
+        back = torch.zeros(int(sh["payload_bytes"]) + 128, device=dev, dtype=torch.uint8)
+        b = sqobfs.make_batch(n, sh["out"], sh["out_off"], wire_len, back, back_off,
                               sh["out_len"], None, sh["psk_id"])
         alg_bytes = 2 * sh["payload_bytes"] + S * n
 
@@ -392,18 +479,6 @@ def main():
     kern_ms = sorted(e0.elapsed_time(e1) for e0, e1 in ev)
     kern_avg_ms = sum(kern_ms) / len(kern_ms)
 
-    tl_out = os.environ.get("SQ_TIMELINE_OUT")  # dev hook: timeline builds only
-    if tl_out and rank == 0:
-        import numpy as np
-        sqobfs.launch(ctx, kr, direction, b, s)
-        torch.cuda.synchronize(dev)
-        waves = (n + 15) // 16 * 4  # >= launched waves for PPW >= 16, block 256
-        tl = np.zeros(3 * waves, np.uint64)
-        fn = sqobfs.lib().sq_timeline_copy
-        fn.argtypes = [sqobfs.ctypes.c_void_p, sqobfs.ctypes.c_uint64]
-        assert fn(tl.ctypes.data, waves) == 0
-        np.save(tl_out, tl.reshape(-1, 3))
-
     tdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     if dist:
         elapsed = max_over_ranks(torch, dist, elapsed, tdev)
@@ -422,7 +497,8 @@ def main():
     else:
         lens = sh["lens"].cpu().numpy()
         offs = sh["in_off"].cpu().numpy()
-        parity = all(torch.equal(back[int(offs[i]):int(offs[i]) + int(lens[i])],
+        boffs = back_off.cpu().numpy()
+        parity = all(torch.equal(back[int(boffs[i]):int(boffs[i]) + int(lens[i])],
                                  sh["data"][int(offs[i]):int(offs[i]) + int(lens[i])])
                      for i in sorted(set([0, n - 1] + list(range(0, n, 4099)))))
     if dist:
@@ -618,9 +694,15 @@ def quic_rate(torch, sqobfs, ctx, dev, steps, n=1 << 20, payload=1350, cpu_secon
             res[name] = {"kernel_avg_us": round(ms * 1e3, 2),
                          "GiB_s_payload": round(n * payload / (ms * 1e-3) / 2**30, 2),
                          "achieved_GBs": round(alg / (ms * 1e-3) / 1e9, 1),
-                         "frac_of_8TBs": round(alg / (ms * 1e-3) / 8e12, 4)}
+                         "frac_of_8TBs": round(alg / (ms * 1e-3) / 8e12, 4),
+                         "valu_roofline": quic_valu_roofline(
+                             "aes_128_gcm" if suite else "chacha20_poly1305", name, ms * 1e3)}
     res["fused_salamander"] = quic_fused_rate(torch, sqobfs, ctx, dev, steps, n, ln, data,
                                               in_off, lens, pno, pn, key, iv, hp, suite)
+    sn = "aes_128_gcm" if suite else "chacha20_poly1305"
+    fs = res["fused_salamander"]
+    fs["valu_roofline_fused_seal"] = quic_valu_roofline(sn, "fused_seal", fs["fused_seal_us"])
+    fs["valu_roofline_fused_open"] = quic_valu_roofline(sn, "fused_open", fs["fused_open_us"])
     # parity on sampled packets
     idx = sorted(set([0, n - 1] + list(range(0, n, 4099))))[:300]
     d = data.view(n, ln)[idx].cpu().numpy()
@@ -664,11 +746,30 @@ def quic_rate(torch, sqobfs, ctx, dev, steps, n=1 << 20, payload=1350, cpu_secon
         m_before = m
         reps, dt = timed(L2.ossl_quic_seal_batch)
         chk = ol.quic_seal(key, iv, hp, 0, d[0].tobytes(), 9, suite=suite)[0]
-        res["cpu_openssl"] = {"value": round(reps * m_before * payload / dt / 2**30, 3),
-                              "unit": "GiB/s", "cores": threads,
-                              "matches_oracle": cout[:ln + 16].tobytes() == chk,
-                              "sample": f"{reps} x {m_before} packets seal, OpenSSL libcrypto "
-                                        "EVP (oracle/ossl_quic.c), one context per thread"}
+        res["cpu_openssl_threads"] = {
+            "value": round(reps * m_before * payload / dt / 2**30, 3),
+            "unit": "GiB/s", "cores": threads,
+            "matches_oracle": cout[:ln + 16].tobytes() == chk,
+            "sample": f"{reps} x {m_before} packets seal, OpenSSL libcrypto EVP "
+                      "(oracle/ossl_quic.c), one context per thread; OpenSSL 3.0 "
+                      "serialises threads, see cpu_openssl"}
+    exe = os.path.join(REPO, "oracle", "ossl_quic_procs")
+    if os.path.exists(exe):
+        import subprocess
+
+        def procs(p):
+            r = subprocess.run([exe, str(suite), str(p), "8192", str(ln), str(cpu_seconds)],
+                               capture_output=True, text=True, timeout=120)
+            assert r.returncode == 0, r.stderr
+            return json.loads(r.stdout)
+        one, many = procs(1), procs(threads)
+        res["cpu_openssl"] = {
+            "value": round(many["gib_s"] * payload / ln, 3), "unit": "GiB/s", "cores": threads,
+            "per_core": round(one["gib_s"] * payload / ln, 3),
+            "sample": f"OpenSSL libcrypto EVP seal (oracle/ossl_quic.c) in {threads} worker "
+                      f"processes x 8192 packets of {ln} B (oracle/ossl_quic_procs); payload "
+                      "GiB/s; processes, because OpenSSL 3.0 threads serialise on the EVP "
+                      "per-call path (16 threads 6.1 vs 16 processes 24.9 GiB/s on this box)"}
     return res
 
 

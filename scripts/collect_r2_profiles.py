@@ -1,0 +1,43 @@
+"""Copy a scripts/r2_profile_all.sh run (gpurun_out/<tag>/) into profiles/r02/:
+per config the kernel-trace stats, the PMC summary and the HBM-traffic file
+bench.py reads (profiles/r02/pmc_<config>.json).
+usage: python scripts/collect_r2_profiles.py TAG"""
+import glob
+import json
+import os
+import shutil
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+src = os.path.join(REPO, "gpurun_out", sys.argv[1])
+dst = os.path.join(REPO, "profiles", "r02")
+os.makedirs(dst, exist_ok=True)
+for d in sorted(glob.glob(os.path.join(src, "*"))):
+    if not os.path.isdir(d):
+        continue
+    cfg = os.path.basename(d)
+    st = glob.glob(os.path.join(d, "kt", "**", "*kernel_stats.csv"), recursive=True)
+    if st:
+        shutil.copy(st[0], os.path.join(dst, f"kernel_stats_{cfg}.csv"))
+    summ = os.path.join(d, "summary.json")
+    if not os.path.exists(summ):
+        continue
+    s = json.load(open(summ))
+    shutil.copy(summ, os.path.join(dst, f"pmc_{cfg}_counters.json"))
+    kt = json.loads(open(os.path.join(d, "kt.json")).read().strip().splitlines()[-1])
+    alg = kt["roofline"]["algorithmic_bytes_per_launch"]
+    out = {"hbm_bytes_per_launch": s["hbm_bytes_per_launch"],
+           "hbm_read_bytes": s["hbm_read_bytes_corrected"],
+           "hbm_write_bytes": s["hbm_write_bytes"],
+           "algorithmic_bytes_per_launch": alg,
+           "traffic_over_algorithmic": round(s["hbm_bytes_per_launch"] / alg, 4),
+           "source": f"profiles/r02/pmc_{cfg}_counters.json: rocprofv3 --pmc FETCH_SIZE and "
+                     "--pmc WRITE_SIZE in separate passes (scripts/r2_profile.sh), bench.py "
+                     "--steps 5; read = 2*FETCH_SIZE*1024 (gfx950 half-count correction), "
+                     "write = WRITE_SIZE*1024",
+           "kernel": kt["roofline"].get("kernel")}
+    json.dump(out, open(os.path.join(dst, f"pmc_{cfg}.json"), "w"), indent=1)
+    print(cfg, out["traffic_over_algorithmic"], kt["roofline"]["kernel_avg_us"], kt["roofline"]["frac"])
+b = os.path.join(src, "bench_default.json")
+if os.path.exists(b):
+    shutil.copy(b, os.path.join(dst, "bench_salamander-1m.json"))
