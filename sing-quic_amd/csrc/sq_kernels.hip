@@ -53,7 +53,7 @@ namespace sq {
 #endif
 // Blocks per lane per step (double-buffered: U..2U KiB of loads in flight).
 #ifndef SQ_U
-#define SQ_U 6
+#define SQ_U 4
 #endif
 // Packets per wavefront (<= 62: lanes kPktPerWave and kPktPerWave + 1 hold
 // the neighbours).
@@ -64,26 +64,55 @@ namespace sq {
 #ifndef SQ_MINW
 #define SQ_MINW 0
 #endif
-// 1: issue the first stream step before the key / contents step (overlap;
-// measured neutral at 3 waves per SIMD, slower when bounded to 4).
-#ifndef SQ_OVERLAP
-#define SQ_OVERLAP 0
-#endif
 // Timing-only ablation builds (never the shipped .so): bit 0 skips the key
-// derivation, bit 1 skips the byte-exact stores.
+// derivation, bit 1 skips the byte-exact stores, bit 3 skips the image
+// windows' loads.
 #ifndef SQ_ABLATE
 #define SQ_ABLATE 0
+#endif
+// Timing knobs: 1 = single-buffered stream loop (U loads, then U stores);
+// extra dynamic LDS per block (bytes) to cap the blocks resident per CU.
+#ifndef SQ_SB
+#define SQ_SB 0
+#endif
+#ifndef SQ_LDSPAD
+#define SQ_LDSPAD 0
+#endif
+// 1: the stream also loads a special block's input block when that block
+// holds a valid input byte (its loaded value is then discarded), so the read
+// stream has no holes at packet boundaries.
+#ifndef SQ_SPLD
+#define SQ_SPLD 1
+#endif
+// Timeline builds (scripts/dev/timeline.py, never shipped): lane 0 of every
+// wave records the constant-rate clock at its phase boundaries.
+#ifndef SQ_TIMELINE
+#define SQ_TIMELINE 0
 #endif
 
 #define SQ_STR2(x) #x
 #define SQ_STR(x) SQ_STR2(x)
 extern "C" const char *sqobfs_build_info(void) {
   return "gfx950 obfs_kernel U=" SQ_STR(SQ_U) " PPW=" SQ_STR(SQ_PPW) " NT=" SQ_STR(SQ_NT)
-         " minw=" SQ_STR(SQ_MINW) " overlap=" SQ_STR(SQ_OVERLAP) " block=" SQ_STR(SQ_BLOCK)
-         " ablate=" SQ_STR(SQ_ABLATE);
+         " minw=" SQ_STR(SQ_MINW) " block=" SQ_STR(SQ_BLOCK)
+         " ablate=" SQ_STR(SQ_ABLATE) " sb=" SQ_STR(SQ_SB) " ldspad=" SQ_STR(SQ_LDSPAD) " spld=" SQ_STR(SQ_SPLD);
 }
 
 constexpr uint32_t kPktPerWave = SQ_PPW;
+
+#if SQ_TIMELINE
+constexpr uint32_t kTlStamps = 6, kTlWaves = 1u << 20;
+__device__ uint64_t g_timeline[kTlWaves * kTlStamps];
+#define SQ_STAMP(k)                                                                   \
+  do {                                                                                \
+    const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                             \
+    if (lane == 0 && unit < kTlWaves) g_timeline[unit * kTlStamps + (k)] = t_;         \
+  } while (0)
+#else
+#define SQ_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
 static_assert(kPktPerWave >= 1 && kPktPerWave + 2 <= kWave, "unit + 2 neighbour lanes");
 
 constexpr uint32_t kMaxPacket = 1u << 26;  // per-packet length bound (u32 block math)
@@ -346,6 +375,7 @@ struct Windows {
 __device__ __forceinline__ void fetch_windows(const PacketJob &J, Windows &W) {
   const u32x4 z = {0u, 0u, 0u, 0u};
   W.h0 = W.h1 = W.h2 = W.t0 = W.t1 = z;
+  if (SQ_ABLATE & 8) return;
   uint64_t rs, re;
   bool ne;
   out_range(J, rs, re, ne);
@@ -365,27 +395,44 @@ __device__ __forceinline__ void fetch_windows(const PacketJob &J, Windows &W) {
   }
 }
 
-// LDS record of a packet (96 B).  Flat block c of the unit, owned by this
-// packet, is at input ssub + 16 c and output dsub + 16 c; its keystream is
-// ks[c & 1], except the special blocks c == sidx (first, value vf) and
-// c == eidx (last, value vl), whose loads are range-checked away.
+// LDS record of a packet with blocks in the flat space (96 B), stored at the
+// packet's rank among such packets.  Flat block c of the unit, owned by this
+// packet, is at input ssub + 16 c and output dsub + 16 c (buffer offsets
+// soff + 16 c, doff + 16 c); its keystream is tab[c & 1], except the special
+// blocks c == sidx (first, value tab[2]) and c == eidx (last, value tab[3]),
+// whose loads are range-checked away.
 struct alignas(16) ChunkRec {
   uint64_t ssub, dsub;
-  uint32_t sidx, eidx, pad0, pad1;
-  u32x4 ks[2];
-  u32x4 vf, vl;
+  uint32_t soff, doff, sidx, eidx;
+  u32x4 tab[4];
 };
 static_assert(sizeof(ChunkRec) == 96, "ChunkRec layout");
 
+// Block -> packet map of a unit whose flat space fits kMapBlocks: one bit per
+// block in four 64-bit words per 64 blocks -- the packet starts, the special
+// first blocks, the special last blocks and the blocks whose input is not
+// loaded.  A block's packet rank is a popcount of the start bits up to it
+// (v_mbcnt), its role three bit tests.
+constexpr uint32_t kMapRows = 64;
+constexpr uint32_t kMapBlocks = kMapRows * kWave;  // 4096 blocks = 64 KiB per unit
+struct alignas(16) MapRow {
+  uint64_t st, sf, sl, nl;
+};
+struct WaveLds {
+  ChunkRec rec[kWave];
+  MapRow row[kMapRows];
+  uint32_t cst[kWave];  // flat start of the packet of each rank
+};
+
 struct WaveBufs {
   __amdgpu_buffer_rsrc_t src, dst;
-  uint32_t sbase, dbase;  // low 32 bits of the span bases
 };
 
 struct UnitStream {
-  uint32_t start;  // lane: flat index of its packet's first block
+  uint32_t cst;    // lane: flat start of the packet of rank `lane` (~0 past the last)
   uint32_t T;      // wave-uniform: blocks in the flat space
   bool fast;       // wave-uniform: buffer-resource streaming possible
+  bool map;        // wave-uniform: the bit map covers the flat space
   WaveBufs B;
 };
 
@@ -396,6 +443,9 @@ constexpr uint64_t kMaxSpan = 0xFFFFFF00ull;
 struct Geo {
   uint64_t rs, re, B0;  // output range, first owned block
   uint32_t nblk;        // owned blocks [B0, B0 + 16 nblk)
+  uint32_t rank;        // record index (packets with flat blocks only)
+  uint32_t start;       // flat index of the first owned block
+  bool flat;            // has blocks in the flat space
   bool ne;              // non-empty output
   bool hf;              // first owned block special (holds salt bytes)
   bool hl;              // last owned block partly this packet's (re unaligned)
@@ -403,12 +453,16 @@ struct Geo {
   bool pfull;           // bytes [rs, B0) are in the previous packet's whole block
 };
 
+__device__ __forceinline__ void lds_or64(uint64_t *w, uint64_t bits) {
+  __hip_atomic_fetch_or(w, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // Step 3a, the plan: block ownership and special-block roles (no key, no
 // payload bytes needed), the flat prefix sum, the stream half of the LDS
-// records and the buffer resources -- everything the first stream loads
-// need.  Every lane of the wave runs it.
+// records, the block map and the buffer resources -- everything the first
+// stream loads need.  Every lane of the wave runs it.
 __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, uint32_t lane,
-                                                ChunkRec *recs, Geo &G) {
+                                                WaveLds &L, Geo &G) {
   out_range(J, G.rs, G.re, G.ne);
   const uint64_t rs = G.rs, re = G.re;
   // in place (input overlaps its own output blocks): a neighbour in another
@@ -447,20 +501,26 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
     if (lane >= (uint32_t)d) incl += y;
   }
   UnitStream U;
-  U.start = incl - F;
+  const uint32_t start = incl - F;
+  G.start = start;
+  G.flat = F != 0;
+  const uint64_t fm = __ballot(G.flat);
+  G.rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
+  const uint32_t K = (uint32_t)__popcll(fm);
   U.T = __builtin_amdgcn_readfirstlane(__shfl(incl, kWave - 1, kWave));
-  // interior blocks [i_lo, i_hi): the only ones loaded
-  const uint32_t i_lo = G.hf ? 1u : 0u, i_hi = G.hl ? nblk - 1 : nblk;
+  U.map = U.T <= kMapBlocks;
+  // loaded blocks [i_lo, i_hi): the interior ones, and a special one whose
+  // input block is 16-byte aligned and holds a payload byte (so it cannot
+  // reach past a mapped page).  The last block always holds one (re is
+  // unaligned, re > dst_pay); the first only if the salt does not fill it
+  // (an aligned XPlus salt is a whole block).
+  const bool al16 = SQ_SPLD && J.len != 0 && ((J.src_pay - J.dst_pay) & 15) == 0;
+  const bool ldf = G.hf && al16 && B0 + 16 > J.dst_pay, ldl = G.lfull && al16;
+  const uint32_t i_lo = G.hf && !ldf ? 1u : 0u, i_hi = G.hl && !ldl ? nblk - 1 : nblk;
   const bool has_int = i_hi > i_lo;
   const uint64_t sabs = B0 + (J.src_pay - J.dst_pay);  // input of block B0
   const uint64_t s_first = sabs + 16ull * i_lo, s_end = sabs + 16ull * i_hi;
-  {
-    ChunkRec &R = recs[lane];
-    R.ssub = sabs - 16ull * U.start;
-    R.dsub = B0 - 16ull * U.start;
-    R.sidx = G.hf ? U.start : kNoIdx;
-    R.eidx = G.lfull ? U.start + nblk - 1 : kNoIdx;
-  }
   // spans: output of every flat block, input of every interior block
   const uint64_t d_lo = uniform64(wave_min64(F ? B0 : ~0ull));
   const uint64_t d_hi = uniform64(wave_max64(F ? B0 + 16ull * F : 0ull));
@@ -469,19 +529,41 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
   const bool mis = has_int && (sabs & 3);
   const bool sok = s_hi <= s_lo || s_hi - s_lo <= kMaxSpan;
   U.fast = U.T != 0 && __ballot(mis) == 0 && d_hi - d_lo <= kMaxSpan && sok;
+  const bool si = s_hi > s_lo;
+  const uint64_t sb = si ? s_lo : d_lo;
   if (U.fast) {
-    const bool si = s_hi > s_lo;
-    U.B.src = __builtin_amdgcn_make_buffer_rsrc((void *)(si ? s_lo : d_lo), 0,
+    U.B.src = __builtin_amdgcn_make_buffer_rsrc((void *)sb, 0,
                                                 (int)(si ? (uint32_t)(s_hi - s_lo) : 0u),
                                                 0x00020000);
     U.B.dst = __builtin_amdgcn_make_buffer_rsrc((void *)d_lo, 0, (int)(uint32_t)(d_hi - d_lo),
                                                 0x00020000);
-    U.B.sbase = (uint32_t)(si ? s_lo : d_lo);
-    U.B.dbase = (uint32_t)d_lo;
+  }
+  if (U.map) L.row[lane] = MapRow{0ull, 0ull, 0ull, 0ull};
+  if (G.flat) {
+    ChunkRec &R = L.rec[G.rank];
+    R.ssub = sabs - 16ull * start;
+    R.dsub = B0 - 16ull * start;
+    R.soff = (uint32_t)(sabs - sb) - 16u * start;
+    R.doff = (uint32_t)(B0 - d_lo) - 16u * start;
+    R.sidx = G.hf ? start : kNoIdx;
+    R.eidx = G.lfull ? start + nblk - 1 : kNoIdx;
+    L.cst[G.rank] = start;
+    if (U.map) {
+      const uint64_t bs = 1ull << (start & 63);
+      lds_or64(&L.row[start >> 6].st, bs);
+      if (G.hf) lds_or64(&L.row[start >> 6].sf, bs);
+      if (G.hf && !ldf) lds_or64(&L.row[start >> 6].nl, bs);
+      if (G.lfull) {
+        const uint32_t e = start + nblk - 1;
+        lds_or64(&L.row[e >> 6].sl, 1ull << (e & 63));
+        if (!ldl) lds_or64(&L.row[e >> 6].nl, 1ull << (e & 63));
+      }
+    }
   }
   // records visible to the whole wave (same-wave LDS ops are ordered; this
   // is a compiler barrier plus the LDS drain)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  U.cst = lane < K ? L.cst[lane] : kNoIdx;
   return U;
 }
 
@@ -493,7 +575,7 @@ template <int KIND, int DIR, bool MULTI>
 __device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
                                           const uint32_t (&salt)[4], bool do_hash, uint32_t pid,
                                           const Windows &W, bool owner, uint32_t lane,
-                                          const Geo &G, uint32_t start, ChunkRec *recs) {
+                                          const Geo &G, WaveLds &L) {
   constexpr uint32_t S = KIND == 0 ? kSalamanderSalt : kXPlusSalt;
   constexpr uint32_t PW = DIR == 0 ? S / 4 : 0;  // salt words in front of the payload
   uint32_t key[8];
@@ -568,33 +650,37 @@ __device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
   const uint32_t ph = (uint32_t)(G.B0 - J.dst_pay) & 31u;
   keywin(key, ph, k0);
   keywin(key, (ph + 16) & 31u, k1);
-  const bool odd = start & 1;
-  ChunkRec &R = recs[lane];
-  R.ks[0] = u32x4{bsel(odd, k1[0], k0[0]), bsel(odd, k1[1], k0[1]),
-                  bsel(odd, k1[2], k0[2]), bsel(odd, k1[3], k0[3])};
-  R.ks[1] = u32x4{bsel(odd, k0[0], k1[0]), bsel(odd, k0[1], k1[1]),
-                  bsel(odd, k0[2], k1[2]), bsel(odd, k0[3], k1[3])};
-  R.vf = u32x4{vf[0], vf[1], vf[2], vf[3]};
-  R.vl = u32x4{vl[0], vl[1], vl[2], vl[3]};
+  // tab[c & 1] is the keystream of flat block c
+  const bool odd = G.start & 1;
+  if (G.flat) {
+    ChunkRec &R = L.rec[G.rank];
+    R.tab[0] = u32x4{bsel(odd, k1[0], k0[0]), bsel(odd, k1[1], k0[1]),
+                     bsel(odd, k1[2], k0[2]), bsel(odd, k1[3], k0[3])};
+    R.tab[1] = u32x4{bsel(odd, k0[0], k1[0]), bsel(odd, k0[1], k1[1]),
+                     bsel(odd, k0[2], k1[2]), bsel(odd, k0[3], k1[3])};
+    R.tab[2] = u32x4{vf[0], vf[1], vf[2], vf[3]};
+    R.tab[3] = u32x4{vl[0], vl[1], vl[2], vl[3]};
+  }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
 // ------------------------------------------------------------ stream
 
-// Packet owning flat block c = b0 + lane (c < T): the last lane l with
-// start[l] <= c.  b0 is wave-uniform, so this is two ballots, a popcount and
-// a scalar walk over the (few) packets that start inside the 64-block window.
-// Always returns a valid record index (0..63), also for c >= T.
-__device__ __forceinline__ uint32_t locate(uint32_t start, uint32_t b0, uint32_t c) {
-  int pp = __popcll(__ballot(start <= b0)) - 1;
-  uint64_t M = __ballot(start > b0 && start < b0 + kWave);
+// Record of flat block c = b0 + lane (c < T) without the block map: the
+// last rank r with cst[r] <= c.  b0 is wave-uniform, so this is two ballots,
+// a popcount and a scalar walk over the (few) packets that start inside the
+// 64-block window.  Always returns a valid record index (0..63), also for
+// c >= T.
+__device__ __forceinline__ uint32_t locate(uint32_t cst, uint32_t b0, uint32_t c) {
+  int pp = __popcll(__ballot(cst <= b0)) - 1;
+  uint64_t M = __ballot(cst > b0 && cst < b0 + kWave);
   while (M) {
     const int l = __ffsll((unsigned long long)M) - 1;
     M &= M - 1;
-    const uint32_t sl = __builtin_amdgcn_readlane(start, l);
+    const uint32_t sl = __builtin_amdgcn_readlane(cst, l);
     pp += c >= sl ? 1 : 0;
   }
-  return (uint32_t)pp;
+  return (uint32_t)(pp < 0 ? 0 : pp);
 }
 
 // Buffer-resource streaming.  The wave's input and output spans each fit a
@@ -618,71 +704,112 @@ constexpr int kAuxSt = SQ_AUXST;
 constexpr int kAuxSt = (SQ_NT & 2) ? 2 : 0;
 #endif
 
+// One stream step in flight: U blocks per lane with their keystreams (or
+// special values) and output offsets.
 template <int U>
-__device__ __forceinline__ void stream_issue(const ChunkRec *wrec, const WaveBufs &B,
-                                             uint32_t start, uint32_t T, uint32_t lane,
-                                             uint32_t base, u32x4 (&v)[U], uint32_t (&pp)[U]) {
-  uint32_t off[U];
-  // all packet lookups (SALU + ballots) first, then all LDS reads, then all
-  // loads: one LDS round trip per step instead of one per block
+struct Step {
+  u32x4 v[U], k[U];
+  uint32_t doff[U];
+  uint32_t spm;  // bit u: block u is special (its loaded value is discarded)
+};
+
+// Issue step `base` (a multiple of 64): per block its record (block map:
+// v_mbcnt over the start bits; otherwise `locate`), role and offsets, then
+// the U loads.  `run` counts the start bits of the rows before `base`.
+template <int U, bool MAP>
+__device__ __forceinline__ void stream_issue(const WaveLds &L, const WaveBufs &B, uint32_t cst,
+                                             uint32_t T, uint32_t lane, uint32_t base,
+                                             uint32_t &run, Step<U> &S) {
+  uint32_t pp[U], off[U];
+  bool isf[U], isl[U], nld[U];
 #pragma unroll
-  for (int u = 0; u < U; u++) pp[u] = locate(start, base + u * kWave, base + u * kWave + lane);
+  for (int u = 0; u < U; u++) {
+    const uint32_t b0 = base + u * kWave;
+    if (MAP) {
+      const uint32_t w = min(b0 >> 6, kMapRows - 1);
+      const MapRow m = L.row[w];
+      const uint64_t st = m.st, sf = m.sf, sl = m.sl;
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+          (uint32_t)(st >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)st, 0u));
+      const uint32_t r = run + below + (uint32_t)((st >> lane) & 1u) - 1u;
+      run += (uint32_t)__popcll(st);
+      pp[u] = min(r, kWave - 1);
+      isf[u] = (sf >> lane) & 1u;
+      isl[u] = (sl >> lane) & 1u;
+      nld[u] = (m.nl >> lane) & 1u;
+    } else {
+      pp[u] = locate(cst, b0, b0 + lane);
+    }
+  }
 #pragma unroll
   for (int u = 0; u < U; u++) {
     const uint32_t c = base + u * kWave + lane;
-    const ChunkRec &R = wrec[pp[u]];
-    const bool ld = c < T && c != R.sidx && c != R.eidx;
-    off[u] = ld ? (uint32_t)R.ssub - B.sbase + 16u * c : kOffNone;
+    const ChunkRec &R = L.rec[pp[u]];
+    if (!MAP) {
+      isf[u] = c == R.sidx;
+      isl[u] = c == R.eidx;
+      nld[u] = isf[u] || isl[u];
+    }
+    // a special block loads zero: its "keystream" is its value
+    const uint32_t idx = isf[u] ? 2u : (isl[u] ? 3u : (c & 1u));
+    S.k[u] = R.tab[idx];
+    S.doff[u] = c < T ? R.doff + 16u * c : kOffNone;
+    off[u] = c < T && !nld[u] ? R.soff + 16u * c : kOffNone;
   }
+  S.spm = 0u;
 #pragma unroll
-  for (int u = 0; u < U; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b128(B.src, off[u], 0, kAuxLd);
+  for (int u = 0; u < U; u++) S.spm |= (isf[u] || isl[u]) ? 1u << u : 0u;
+#pragma unroll
+  for (int u = 0; u < U; u++) S.v[u] = __builtin_amdgcn_raw_buffer_load_b128(B.src, off[u], 0, kAuxLd);
 }
 
-__device__ __forceinline__ void store_chunk(const ChunkRec *wrec, const WaveBufs &B,
-                                            uint32_t pp, uint32_t c, uint32_t T, u32x4 v) {
-  const ChunkRec &R = wrec[pp];
-  const uint32_t off = c < T ? (uint32_t)R.dsub - B.dbase + 16u * c : kOffNone;
-  // a special block loaded zero: its "keystream" is its value
-  const u32x4 *kp = c == R.sidx ? &R.vf : (c == R.eidx ? &R.vl : &R.ks[c & 1]);
-  __builtin_amdgcn_raw_buffer_store_b128(v ^ *kp, B.dst, off, 0, kAuxSt);
+template <int U>
+__device__ __forceinline__ void stream_store(const WaveBufs &B, const Step<U> &S) {
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    const u32x4 v = (S.spm >> u) & 1u ? z : S.v[u];
+    __builtin_amdgcn_raw_buffer_store_b128(v ^ S.k[u], B.dst, S.doff[u], 0, kAuxSt);
+  }
 }
 
 // Double-buffered stream loop.  The caller has issued step 0's loads into
-// cur/cpp; each iteration issues step i+1's U loads before step i is XORed
-// and stored, so a wave keeps U..2U KiB of reads outstanding.
-template <int U>
-__device__ __forceinline__ void stream_loop(const ChunkRec *wrec, const WaveBufs &B,
-                                            uint32_t start, uint32_t T, uint32_t lane,
-                                            u32x4 (&cur)[U], uint32_t (&cpp)[U]) {
+// cur; each iteration issues step i+1's U loads before step i is XORed and
+// stored, so a wave keeps U..2U KiB of reads outstanding.
+template <int U, bool MAP>
+__device__ __forceinline__ void stream_loop(const WaveLds &L, const WaveBufs &B, uint32_t cst,
+                                            uint32_t T, uint32_t lane, uint32_t &run,
+                                            Step<U> &cur) {
   constexpr uint32_t STEP = kWave * U;
-  for (uint32_t base = 0; base < T; base += STEP) {
-    u32x4 nxt[U];
-    uint32_t npp[U];
-    stream_issue<U>(wrec, B, start, T, lane, base + STEP, nxt, npp);
-#pragma unroll
-    for (int u = 0; u < U; u++) store_chunk(wrec, B, cpp[u], base + u * kWave + lane, T, cur[u]);
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      cur[u] = nxt[u];
-      cpp[u] = npp[u];
+  if (SQ_SB) {
+    for (uint32_t base = 0; base < T; base += STEP) {
+      if (base) stream_issue<U, MAP>(L, B, cst, T, lane, base, run, cur);
+      stream_store<U>(B, cur);
     }
+    return;
+  }
+  for (uint32_t base = 0; base < T; base += STEP) {
+    Step<U> nxt;
+    stream_issue<U, MAP>(L, B, cst, T, lane, base + STEP, run, nxt);
+    stream_store<U>(B, cur);
+    cur = nxt;
   }
 }
 
 // Fallback for waves whose spans exceed a 32-bit buffer range or whose
 // input is not 4-byte aligned: global accesses, any alignment (two aligned
 // 16-byte loads + byte funnel per block), one block per lane.
-__device__ __noinline__ void stream_generic(const ChunkRec *wrec, uint32_t start, uint32_t T,
+__device__ __noinline__ void stream_generic(const WaveLds &L, uint32_t cst, uint32_t T,
                                             uint32_t lane) {
   for (uint32_t b0 = 0; b0 < T; b0 += kWave) {
     const uint32_t c = min(b0 + lane, T - 1);
-    const ChunkRec &R = wrec[locate(start, b0, c)];
+    const ChunkRec &R = L.rec[locate(cst, b0, c)];
     uint32_t w[4] = {0u, 0u, 0u, 0u};
-    u32x4 k = R.ks[c & 1];
+    u32x4 k = R.tab[c & 1];
     if (c == R.sidx) {
-      k = R.vf;
+      k = R.tab[2];
     } else if (c == R.eidx) {
-      k = R.vl;
+      k = R.tab[3];
     } else {
       const uint64_t sa = R.ssub + 16ull * c;
       load_window(sa, sa + 16, sa, w);
@@ -699,10 +826,11 @@ __global__ __launch_bounds__(kBlock, SQ_MINW) void obfs_kernel(const KParams P) 
 #else
 __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
 #endif
-  __shared__ ChunkRec recs[kWavesPerBlock][kWave];
+  __shared__ WaveLds lds[kWavesPerBlock];
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wv = threadIdx.x / kWave;
   const uint64_t unit = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
+  SQ_STAMP(0);
   bool valid, owner;
   const uint32_t p = lane_packet(unit, lane, P.n, valid, owner);
   // 1. descriptor (deobfuscate: the salt load) and the image windows: loads
@@ -715,22 +843,38 @@ __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
   uint32_t olen;
   finalize_desc<KIND, DIR, MULTI>(P, p, valid, d, J, salt, do_hash, E, olen);
   (void)E;
+  SQ_STAMP(1);
   Windows W;
   fetch_windows(J, W);
   if (owner) P.out_len[p] = olen;
-  // 3a. plan, then the first stream loads
+  // 3a. plan
   Geo G;
-  const UnitStream S = plan_unit(J, owner, lane, recs[wv], G);
-  u32x4 cur[U];
-  uint32_t cpp[U];
+  WaveLds &L = lds[wv];
+  const UnitStream S = plan_unit(J, owner, lane, L, G);
+  SQ_STAMP(2);
   const uint32_t pid = MULTI && d.pid < P.n_psk ? d.pid : 0u;
-  if (SQ_OVERLAP && S.fast) stream_issue<U>(recs[wv], S.B, S.start, S.T, lane, 0, cur, cpp);
   // 2 + 3b. key and block contents
-  fill_unit<KIND, DIR, MULTI>(P, J, salt, do_hash, pid, W, owner, lane, G, S.start, recs[wv]);
-  if (!SQ_OVERLAP && S.fast) stream_issue<U>(recs[wv], S.B, S.start, S.T, lane, 0, cur, cpp);
+  fill_unit<KIND, DIR, MULTI>(P, J, salt, do_hash, pid, W, owner, lane, G, L);
+  SQ_STAMP(3);
   // 4. the stream
-  if (S.fast) stream_loop<U>(recs[wv], S.B, S.start, S.T, lane, cur, cpp);
-  else if (S.T != 0) stream_generic(recs[wv], S.start, S.T, lane);
+  uint32_t run = 0;
+  if (S.fast && S.map) {
+    Step<U> cur;
+    stream_issue<U, true>(L, S.B, S.cst, S.T, lane, 0, run, cur);
+    stream_loop<U, true>(L, S.B, S.cst, S.T, lane, run, cur);
+  } else if (S.fast) {
+    Step<U> cur;
+    stream_issue<U, false>(L, S.B, S.cst, S.T, lane, 0, run, cur);
+    stream_loop<U, false>(L, S.B, S.cst, S.T, lane, run, cur);
+  } else if (S.T != 0) {
+    stream_generic(L, S.cst, S.T, lane);
+  }
+#if SQ_TIMELINE
+  SQ_STAMP(4);
+  // when the wave's last store has left (the end of its life)
+  __builtin_amdgcn_s_waitcnt(0);
+  SQ_STAMP(5);
+#endif
 }
 
 // ------------------------------------------------------------ PSK prepare
@@ -811,8 +955,8 @@ static int launch_one(const KParams *kp, hipStream_t s) {
   constexpr int U = SQ_U;
   const uint64_t units = ((uint64_t)kp->n + kPktPerWave - 1) / kPktPerWave;
   const uint64_t blocks = (units + kWavesPerBlock - 1) / kWavesPerBlock;
-  hipLaunchKernelGGL((obfs_kernel<KIND, DIR, MULTI, U>), dim3((uint32_t)blocks), dim3(kBlock), 0,
-                     s, *kp);
+  hipLaunchKernelGGL((obfs_kernel<KIND, DIR, MULTI, U>), dim3((uint32_t)blocks), dim3(kBlock),
+                     SQ_LDSPAD, s, *kp);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -836,6 +980,16 @@ extern "C" int sq_launch_obfs(int kind, int dir, const sq::KParams *kp, void *st
   }
   return -1;
 }
+
+#if SQ_TIMELINE
+extern "C" int sqobfs_debug_timeline(uint64_t *host, uint64_t words) {
+  const uint64_t cap = (uint64_t)sq::kTlWaves * sq::kTlStamps;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(sq::g_timeline),
+                             (words < cap ? words : cap) * sizeof(uint64_t)) == hipSuccess
+             ? 0
+             : -3;
+}
+#endif
 
 extern "C" int sq_launch_psk_prepare(int kind, const uint8_t *blob, const uint64_t *off,
                                      const uint32_t *len, uint32_t count, sq::PskEntry *out,
