@@ -12,10 +12,11 @@
 // owning packet l; lanes 32 and 33 hold the packets just after and just
 // before the unit (the neighbours of its boundary blocks).
 //   1. descriptor  offsets, lengths, salt (obfuscate: the salt array;
-//                  deobfuscate: the first S wire bytes), the quirk table.
+//                  deobfuscate: the first S wire bytes), the quirk table; the
+//                  loads of the head / tail image windows.
 //   2. key         each lane hashes its own packet's psk||salt (BLAKE2b-256
 //                  or SHA-256) from the keyring's per-PSK midstate.
-//   3. blocks      every 16-byte-aligned output block is OWNED by the packet
+//   3. plan        every 16-byte-aligned output block is OWNED by the packet
 //                  holding its first byte.  A packet's owned blocks are its
 //                  interior blocks (16 payload bytes: load, XOR, store) and at
 //                  most two special ones: the first (salt bytes) and the last
@@ -24,14 +25,19 @@
 //                  packet's head / tail images and the next lane's head image.
 //                  Bytes of blocks no datagram pair covers whole (gaps between
 //                  outputs) are written byte-exactly up front by the owner.
-//   4. stream      the wave walks the flat space of its owned blocks, 64 lanes
-//                  x U blocks per step, 1 KiB per wave instruction: one dwordx4
-//                  load, XOR with the LDS keystream, one aligned dwordx4 store.
-//                  A special block's load is range-checked away (it returns
-//                  zero) and its LDS "keystream" is the block's value.
+//                  The owned blocks of the unit form one flat space; per
+//                  packet an LDS record (offsets, keystream phases, special
+//                  values) and, per 64 blocks, four bit rows (packet starts,
+//                  special first / last blocks, blocks not loaded).
+//   4. stream      the wave walks the flat space, 64 lanes x U blocks per
+//                  step, 1 KiB per wave instruction: one dwordx4 load, XOR
+//                  with the record's keystream, one aligned dwordx4 store.
+//                  A block's record is a v_mbcnt over the start bits; a
+//                  special block's loaded value is discarded for its
+//                  precomputed one (its load is kept when its input block
+//                  holds a payload byte, so the read stream has no holes).
 // So for back-to-back datagrams (GSO buffers, the bench's dense layout) every
-// output line is written once, whole, in address order, like a plain copy;
-// block -> packet is a ballot/popcount on prefix sums held in registers.
+// output line is written once, whole, in address order, like a plain copy.
 // Measured on copy probes: leaving the boundary blocks to a separate pass
 // costs 7-12 % (holes) to 30 % (holes filled early) of the HBM rate, and
 // splitting wave instructions into 256-byte pieces (16 lanes per packet)
@@ -70,11 +76,8 @@ namespace sq {
 #ifndef SQ_ABLATE
 #define SQ_ABLATE 0
 #endif
-// Timing knobs: 1 = single-buffered stream loop (U loads, then U stores);
-// extra dynamic LDS per block (bytes) to cap the blocks resident per CU.
-#ifndef SQ_SB
-#define SQ_SB 0
-#endif
+// Extra dynamic LDS per block in timing builds (bytes): pins the resident
+// blocks per CU when an ablation changes the register count.
 #ifndef SQ_LDSPAD
 #define SQ_LDSPAD 0
 #endif
@@ -95,7 +98,7 @@ namespace sq {
 extern "C" const char *sqobfs_build_info(void) {
   return "gfx950 obfs_kernel U=" SQ_STR(SQ_U) " PPW=" SQ_STR(SQ_PPW) " NT=" SQ_STR(SQ_NT)
          " minw=" SQ_STR(SQ_MINW) " block=" SQ_STR(SQ_BLOCK)
-         " ablate=" SQ_STR(SQ_ABLATE) " sb=" SQ_STR(SQ_SB) " ldspad=" SQ_STR(SQ_LDSPAD) " spld=" SQ_STR(SQ_SPLD);
+         " ablate=" SQ_STR(SQ_ABLATE)  " spld=" SQ_STR(SQ_SPLD);
 }
 
 constexpr uint32_t kPktPerWave = SQ_PPW;
@@ -333,19 +336,18 @@ __device__ __forceinline__ void derive_key(bool do_hash, const PskEntry *E,
 
 // ------------------------------------------------------------ one unit
 
-// Lane roles: lanes 0 .. kPktPerWave-1 own packets; lane kPktPerWave holds
-// the packet right after the unit and lane kPktPerWave + 1 the one right
-// before it (the neighbours of its boundary blocks: they own and write
-// nothing).
-__device__ __forceinline__ uint32_t lane_packet(uint64_t unit, uint32_t lane, uint32_t n,
-                                                bool &valid, bool &owner) {
-  const int64_t base = (int64_t)unit * kPktPerWave;
+// Lane roles: lanes 0 .. ppw-1 own packets first + lane; lane ppw holds the
+// packet right after the unit and lane ppw + 1 the one right before it (the
+// neighbours of its boundary blocks: they own and write nothing).
+__device__ __forceinline__ uint32_t lane_packet(uint64_t first, uint32_t ppw, uint32_t lane,
+                                                uint32_t n, bool &valid, bool &owner) {
+  const int64_t base = (int64_t)first;
   int64_t p = -1;
-  if (lane < kPktPerWave) p = base + lane;
-  else if (lane == kPktPerWave) p = base + kPktPerWave;
-  else if (lane == kPktPerWave + 1) p = base - 1;
+  if (lane < ppw) p = base + lane;
+  else if (lane == ppw) p = base + ppw;
+  else if (lane == ppw + 1) p = base - 1;
   valid = p >= 0 && p < (int64_t)n;
-  owner = valid && lane < kPktPerWave;
+  owner = valid && lane < ppw;
   return valid ? (uint32_t)p : 0u;
 }
 
@@ -462,17 +464,17 @@ __device__ __forceinline__ void lds_or64(uint64_t *w, uint64_t bits) {
 // records, the block map and the buffer resources -- everything the first
 // stream loads need.  Every lane of the wave runs it.
 __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, uint32_t lane,
-                                                WaveLds &L, Geo &G) {
+                                                uint32_t ppw, WaveLds &L, Geo &G) {
   out_range(J, G.rs, G.re, G.ne);
   const uint64_t rs = G.rs, re = G.re;
   // in place (input overlaps its own output blocks): a neighbour in another
   // wave must not read or write across this packet's blocks
   const uint64_t oblo = rs & ~15ull, obhi = up16(re);
   const bool ovl = G.ne && J.len && J.src_pay < obhi && J.src_pay + J.len > oblo;
-  // neighbours: next lane = next packet (lane kPktPerWave for the last one),
-  // previous lane = previous packet (lane kPktPerWave + 1 for the first one)
+  // neighbours: next lane = next packet (lane ppw for the last one),
+  // previous lane = previous packet (lane ppw + 1 for the first one)
   const uint32_t nl = (lane + 1) & (kWave - 1);
-  const uint32_t pl = lane == 0 ? kPktPerWave + 1 : lane - 1;
+  const uint32_t pl = lane == 0 ? ppw + 1 : lane - 1;
   const uint64_t rs_n = shfl64(rs, nl), re_n = shfl64(re, nl);
   const uint64_t rs_p = shfl64(rs, pl), re_p = shfl64(re, pl);
   const uint32_t fl = (G.ne ? 1u : 0u) | (ovl ? 2u : 0u);
@@ -484,7 +486,7 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
   const uint32_t nblk = G.nblk;
   G.hl = nblk && (re & 15);
   G.hf = nblk && B0 < J.dst_pay && !(G.hl && B0 == BL);
-  const bool cross_n = lane == kPktPerWave - 1, cross_p = lane == 0;
+  const bool cross_n = lane == ppw - 1, cross_p = lane == 0;
   // last block whole: the next datagram starts at re and fills the block
   G.lfull = G.hl && (fl_n & 1) && rs_n == re && re_n >= E && !(cross_n && (fl_n & 2));
   // leading bytes [rs, B0) covered by the previous packet's whole last block
@@ -781,13 +783,6 @@ __device__ __forceinline__ void stream_loop(const WaveLds &L, const WaveBufs &B,
                                             uint32_t T, uint32_t lane, uint32_t &run,
                                             Step<U> &cur) {
   constexpr uint32_t STEP = kWave * U;
-  if (SQ_SB) {
-    for (uint32_t base = 0; base < T; base += STEP) {
-      if (base) stream_issue<U, MAP>(L, B, cst, T, lane, base, run, cur);
-      stream_store<U>(B, cur);
-    }
-    return;
-  }
   for (uint32_t base = 0; base < T; base += STEP) {
     Step<U> nxt;
     stream_issue<U, MAP>(L, B, cst, T, lane, base + STEP, run, nxt);
@@ -830,9 +825,12 @@ __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wv = threadIdx.x / kWave;
   const uint64_t unit = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
+  const uint32_t ppw = kPktPerWave;
+  const uint64_t first = unit * ppw;
+  if (first >= P.n) return;
   SQ_STAMP(0);
   bool valid, owner;
-  const uint32_t p = lane_packet(unit, lane, P.n, valid, owner);
+  const uint32_t p = lane_packet(first, ppw, lane, P.n, valid, owner);
   // 1. descriptor (deobfuscate: the salt load) and the image windows: loads
   RawDesc d;
   fetch_desc<KIND, DIR, MULTI>(P, p, valid, d);
@@ -850,7 +848,7 @@ __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
   // 3a. plan
   Geo G;
   WaveLds &L = lds[wv];
-  const UnitStream S = plan_unit(J, owner, lane, L, G);
+  const UnitStream S = plan_unit(J, owner, lane, ppw, L, G);
   SQ_STAMP(2);
   const uint32_t pid = MULTI && d.pid < P.n_psk ? d.pid : 0u;
   // 2 + 3b. key and block contents
@@ -858,12 +856,11 @@ __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
   SQ_STAMP(3);
   // 4. the stream
   uint32_t run = 0;
+  Step<U> cur;
   if (S.fast && S.map) {
-    Step<U> cur;
     stream_issue<U, true>(L, S.B, S.cst, S.T, lane, 0, run, cur);
     stream_loop<U, true>(L, S.B, S.cst, S.T, lane, run, cur);
   } else if (S.fast) {
-    Step<U> cur;
     stream_issue<U, false>(L, S.B, S.cst, S.T, lane, 0, run, cur);
     stream_loop<U, false>(L, S.B, S.cst, S.T, lane, run, cur);
   } else if (S.T != 0) {
