@@ -410,6 +410,7 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
   if (live && !pick_key<MULTI>(Q, p, K)) {
     status = kQEKey;
     live = false;
+    if (OPEN && Q.pn_out) Q.pn_out[p] = 0;  // rejected: pn_out 0 (as below)
   }
   if (live) {
     src = (uint64_t)Q.in + Q.in_off[p];

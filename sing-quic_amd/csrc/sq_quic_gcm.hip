@@ -459,6 +459,7 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
         status = kQEKey;
         live = false;
         kid = 0;
+        if (OPEN && Q.pn_out) Q.pn_out[p] = 0;  // rejected: pn_out 0 (as below)
       }
     }
     const GKey<MULTI> K = key_of<MULTI>(Q, kid, tP, tH, tK);

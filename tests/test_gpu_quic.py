@@ -35,7 +35,7 @@ def _place(sizes, align, gap):
 
 
 def run(ctx, keys, seal, pkts, pn_offsets, pns, key_ids=None, align=1, inplace=False,
-        suite=0):
+        suite=0, pn_out_fill=0):
     """One device batch; returns (out buffer, out offsets, out_len, pn_out)."""
     import torch
     dev = torch.device("cuda", 0)
@@ -58,7 +58,7 @@ def run(ctx, keys, seal, pkts, pn_offsets, pns, key_ids=None, align=1, inplace=F
              out_off=t(out_off), out_len=t(np.zeros(n, np.uint32)),
              pno=t(np.asarray(pn_offsets, np.uint16)), pn=t(np.asarray(pns, np.uint64)),
              kid=t(None if key_ids is None else np.asarray(key_ids, np.uint16)),
-             pn_out=t(np.zeros(n, np.uint64)))
+             pn_out=t(np.full(n, pn_out_fill, np.uint64)))
     b = sqobfs.quic_batch(n, d_data, d["in_off"], d["in_len"], d_out, d["out_off"], d["out_len"],
                           d["pno"], d["pn"], d["kid"], d["pn_out"])
     with sqobfs.QuicKeyring(ctx, keys, suite) as kr:
@@ -171,6 +171,20 @@ def test_open_rejects_tampering_and_bad_input(ctx):
     _, _, ol_, _, _ = run(ctx, [QuicKey.of(*kb)], True, [b"\x40\x01\x02", b"\x43" + bytes(40)],
                           [1, 1], [1, 2], key_ids=[0, 5])
     assert ol_[0] == sqobfs.QUIC_ESHORT and ol_[1] == sqobfs.QUIC_EKEY
+
+
+@pytest.mark.parametrize("suite", [0, 1])
+def test_open_rejects_write_pn_out_zero(ctx, suite):
+    """Every rejected packet of an open gets pn_out = 0 (too short, and an
+    out-of-range key id), not whatever the buffer held before."""
+    rng = np.random.Generator(np.random.PCG64(17 + suite))
+    kl = 16 if suite else 32
+    kb = tuple(rng.integers(0, 256, m, dtype=np.uint8).tobytes() for m in (kl, 12, kl))
+    pkts = [b"\x40\x01\x02", b"\x43" + bytes(60)]
+    _, _, ol_, pno_, _ = run(ctx, [QuicKey.of(*kb)], False, pkts, [1, 1], [1, 2], key_ids=[0, 5],
+                             suite=suite, pn_out_fill=0xDEADBEEF)
+    assert ol_[0] == sqobfs.QUIC_ESHORT and ol_[1] == sqobfs.QUIC_EKEY
+    assert list(pno_) == [0, 0]
 
 
 def test_long_payloads_owner_path(ctx):
