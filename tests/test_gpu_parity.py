@@ -118,6 +118,61 @@ def test_ragged_single_psk(ctx, kind, direction, dist):
     check(ctx, kind, direction, [PSK], hb, f"{kind}/{direction}/{dist}")
 
 
+def wire_dense_case(rng, kind, direction, lens, lead=0):
+    """The bench's dense layout: obfuscate outputs (wire datagrams) back to
+    back, each payload at the same position of an input buffer of the same
+    shape (S bytes of headroom in front); deobfuscate reads such a wire
+    buffer and writes the payloads back to back.  One uniform, 16-byte
+    aligned input/output shift for every packet: the stream also loads the
+    special blocks' inputs here."""
+    S = sqobfs.SALT_LEN[kind]
+    lens = np.asarray(lens, np.int64)
+    wire = lens + S
+    w_off = (np.cumsum(wire) - wire + lead).astype(np.uint64)
+    end = int(wire.sum()) + lead
+    if direction == OBFUSCATE:
+        data = rng.integers(0, 256, end + 64, dtype=np.uint8)  # headroom holds junk
+        out = np.full(end + 64, gh.SENTINEL, np.uint8)
+        salt = rng.integers(0, 256, len(lens) * S, dtype=np.uint8)
+        return sqobfs.HostBatch(data, w_off + S, lens.astype(np.uint32), out, w_off,
+                                np.zeros(len(lens), np.uint32), salt)
+    data = rng.integers(0, 256, end + 64, dtype=np.uint8)
+    # output slots by the reference's return lengths (a datagram of <= 8
+    # bytes comes back whole, salamander.go:47-49)
+    osz = np.array([gh.out_size(kind, direction, int(w), int(w)) for w in wire], np.int64)
+    p_off = (np.cumsum(osz) - osz + lead).astype(np.uint64)
+    out = np.full(int(osz.sum()) + lead + 64, gh.SENTINEL, np.uint8)
+    return sqobfs.HostBatch(data, w_off, wire.astype(np.uint32), out, p_off,
+                            np.zeros(len(lens), np.uint32))
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("direction", DIRS)
+@pytest.mark.parametrize("lead", [0, 8, 16])
+def test_wire_dense_layout(ctx, kind, direction, lead):
+    rng = np.random.Generator(np.random.PCG64(700 + 10 * kind + direction + lead))
+    lens = np.concatenate([np.arange(0, 40), rng.integers(0, 1500, 1500),
+                           np.full(300, 1350)])
+    hb = wire_dense_case(rng, kind, direction, lens, lead)
+    check(ctx, kind, direction, [PSK], hb, f"{kind}/{direction}/dense{lead}")
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("direction", DIRS)
+def test_jumbo_units(ctx, kind, direction):
+    """Units whose flat block space exceeds the block map (4,096 blocks per
+    32 packets): jumbo datagrams and a few 70 KB buffers (GSO-sized), next to
+    MTU-sized units, so both stream lookups run in one launch."""
+    rng = np.random.Generator(np.random.PCG64(800 + 10 * kind + direction))
+    lens = np.concatenate([rng.integers(1500, 9001, 200), rng.integers(0, 1500, 100),
+                           rng.integers(60000, 70001, 6), rng.integers(0, 200, 40)])
+    rng.shuffle(lens[:200])
+    hb = gh.make_case(rng, kind, direction, lens, [PSK], in_align=1, out_align=16, out_lead=3)
+    check(ctx, kind, direction, [PSK], hb, f"{kind}/{direction}/jumbo")
+    hb = wire_dense_case(rng, kind, direction, lens)
+    check(ctx, kind, direction, [PSK], hb, f"{kind}/{direction}/jumbo-dense")
+
+
 @pytest.mark.parametrize("kind", KINDS)
 @pytest.mark.parametrize("direction", DIRS)
 @pytest.mark.parametrize("in_align,in_lead,out_align,out_lead",
