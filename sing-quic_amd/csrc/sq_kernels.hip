@@ -81,12 +81,6 @@ namespace sq {
 #ifndef SQ_LDSPAD
 #define SQ_LDSPAD 0
 #endif
-// 1: the stream also loads a special block's input block when that block
-// holds a valid input byte (its loaded value is then discarded), so the read
-// stream has no holes at packet boundaries.
-#ifndef SQ_SPLD
-#define SQ_SPLD 1
-#endif
 // Timeline builds (scripts/dev/timeline.py, never shipped): lane 0 of every
 // wave records the constant-rate clock at its phase boundaries.
 #ifndef SQ_TIMELINE
@@ -98,7 +92,7 @@ namespace sq {
 extern "C" const char *sqobfs_build_info(void) {
   return "gfx950 obfs_kernel U=" SQ_STR(SQ_U) " PPW=" SQ_STR(SQ_PPW) " NT=" SQ_STR(SQ_NT)
          " minw=" SQ_STR(SQ_MINW) " block=" SQ_STR(SQ_BLOCK)
-         " ablate=" SQ_STR(SQ_ABLATE)  " spld=" SQ_STR(SQ_SPLD);
+         " ablate=" SQ_STR(SQ_ABLATE);
 }
 
 constexpr uint32_t kPktPerWave = SQ_PPW;
@@ -410,20 +404,18 @@ struct alignas(16) ChunkRec {
 };
 static_assert(sizeof(ChunkRec) == 96, "ChunkRec layout");
 
-// Block -> packet map of a unit whose flat space fits kMapBlocks: one bit per
-// block in four 64-bit words per 64 blocks -- the packet starts, the special
-// first blocks, the special last blocks and the blocks whose input is not
-// loaded.  A block's packet rank is a popcount of the start bits up to it
-// (v_mbcnt), its role three bit tests.
-constexpr uint32_t kMapRows = 64;
-constexpr uint32_t kMapBlocks = kMapRows * kWave;  // 4096 blocks = 64 KiB per unit
-struct alignas(16) MapRow {
-  uint64_t st, sf, sl, nl;
-};
+// Block -> packet map of a unit whose flat space fits kMapBlocks: one byte
+// per flat block, the owning packet's record index (bits 0-5) and the
+// block's role (bit 6: special first block, bit 7: special last block).
+// The stream reads one byte per block: no search, no cross-lane work.
+constexpr uint32_t kMapBlocks = 4096;  // 64 KiB of output per unit
+constexpr uint32_t kRoleFirst = 64, kRoleLast = 128;
+// slack for the steps the double-buffered loop issues past the end
+constexpr uint32_t kMapSlack = 2 * kWave * SQ_U;
 struct WaveLds {
   ChunkRec rec[kWave];
-  MapRow row[kMapRows];
   uint32_t cst[kWave];  // flat start of the packet of each rank
+  uint8_t role[kMapBlocks + kMapSlack];
 };
 
 struct WaveBufs {
@@ -454,10 +446,6 @@ struct Geo {
   bool lfull;           // ... and written whole (the next datagram fills it)
   bool pfull;           // bytes [rs, B0) are in the previous packet's whole block
 };
-
-__device__ __forceinline__ void lds_or64(uint64_t *w, uint64_t bits) {
-  __hip_atomic_fetch_or(w, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 
 // Step 3a, the plan: block ownership and special-block roles (no key, no
 // payload bytes needed), the flat prefix sum, the stream half of the LDS
@@ -512,14 +500,8 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
   const uint32_t K = (uint32_t)__popcll(fm);
   U.T = __builtin_amdgcn_readfirstlane(__shfl(incl, kWave - 1, kWave));
   U.map = U.T <= kMapBlocks;
-  // loaded blocks [i_lo, i_hi): the interior ones, and a special one whose
-  // input block is 16-byte aligned and holds a payload byte (so it cannot
-  // reach past a mapped page).  The last block always holds one (re is
-  // unaligned, re > dst_pay); the first only if the salt does not fill it
-  // (an aligned XPlus salt is a whole block).
-  const bool al16 = SQ_SPLD && J.len != 0 && ((J.src_pay - J.dst_pay) & 15) == 0;
-  const bool ldf = G.hf && al16 && B0 + 16 > J.dst_pay, ldl = G.lfull && al16;
-  const uint32_t i_lo = G.hf && !ldf ? 1u : 0u, i_hi = G.hl && !ldl ? nblk - 1 : nblk;
+  // interior blocks [i_lo, i_hi): the only ones loaded
+  const uint32_t i_lo = G.hf ? 1u : 0u, i_hi = G.hl ? nblk - 1 : nblk;
   const bool has_int = i_hi > i_lo;
   const uint64_t sabs = B0 + (J.src_pay - J.dst_pay);  // input of block B0
   const uint64_t s_first = sabs + 16ull * i_lo, s_end = sabs + 16ull * i_hi;
@@ -540,7 +522,6 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
     U.B.dst = __builtin_amdgcn_make_buffer_rsrc((void *)d_lo, 0, (int)(uint32_t)(d_hi - d_lo),
                                                 0x00020000);
   }
-  if (U.map) L.row[lane] = MapRow{0ull, 0ull, 0ull, 0ull};
   if (G.flat) {
     ChunkRec &R = L.rec[G.rank];
     R.ssub = sabs - 16ull * start;
@@ -551,15 +532,15 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
     R.eidx = G.lfull ? start + nblk - 1 : kNoIdx;
     L.cst[G.rank] = start;
     if (U.map) {
-      const uint64_t bs = 1ull << (start & 63);
-      lds_or64(&L.row[start >> 6].st, bs);
-      if (G.hf) lds_or64(&L.row[start >> 6].sf, bs);
-      if (G.hf && !ldf) lds_or64(&L.row[start >> 6].nl, bs);
-      if (G.lfull) {
-        const uint32_t e = start + nblk - 1;
-        lds_or64(&L.row[e >> 6].sl, 1ull << (e & 63));
-        if (!ldl) lds_or64(&L.row[e >> 6].nl, 1ull << (e & 63));
-      }
+      // the role bytes of this packet's flat blocks [start, start + F)
+      uint8_t *rb = L.role;
+      const uint32_t e = start + F, rk = G.rank;
+      uint32_t c = start;
+      for (; c < e && (c & 3); c++) rb[c] = (uint8_t)rk;
+      for (; c + 4 <= e; c += 4) *reinterpret_cast<uint32_t *>(rb + c) = rk * 0x01010101u;
+      for (; c < e; c++) rb[c] = (uint8_t)rk;
+      if (G.hf) rb[start] = (uint8_t)(rk | kRoleFirst);
+      if (G.lfull) rb[e - 1] = (uint8_t)(rk | kRoleLast);
     }
   }
   // records visible to the whole wave (same-wave LDS ops are ordered; this
@@ -712,55 +693,51 @@ template <int U>
 struct Step {
   u32x4 v[U], k[U];
   uint32_t doff[U];
-  uint32_t spm;  // bit u: block u is special (its loaded value is discarded)
 };
 
 // Issue step `base` (a multiple of 64): per block its record (block map:
-// v_mbcnt over the start bits; otherwise `locate`), role and offsets, then
-// the U loads.  `run` counts the start bits of the rows before `base`.
+// one role byte; otherwise `locate`), role and offsets, then the U loads.
+// A special block's load is range-checked away (it reads zero) and its
+// "keystream" is its precomputed value.
 template <int U, bool MAP>
 __device__ __forceinline__ void stream_issue(const WaveLds &L, const WaveBufs &B, uint32_t cst,
                                              uint32_t T, uint32_t lane, uint32_t base,
-                                             uint32_t &run, Step<U> &S) {
-  uint32_t pp[U], off[U];
-  bool isf[U], isl[U], nld[U];
+                                             Step<U> &S) {
+  uint32_t pp[U], off[U], rl[U];
+  // every LDS read of the step first, then the arithmetic, then the loads
+  if (MAP) {
 #pragma unroll
-  for (int u = 0; u < U; u++) {
-    const uint32_t b0 = base + u * kWave;
-    if (MAP) {
-      const uint32_t w = min(b0 >> 6, kMapRows - 1);
-      const MapRow m = L.row[w];
-      const uint64_t st = m.st, sf = m.sf, sl = m.sl;
-      const uint32_t below = __builtin_amdgcn_mbcnt_hi(
-          (uint32_t)(st >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)st, 0u));
-      const uint32_t r = run + below + (uint32_t)((st >> lane) & 1u) - 1u;
-      run += (uint32_t)__popcll(st);
-      pp[u] = min(r, kWave - 1);
-      isf[u] = (sf >> lane) & 1u;
-      isl[u] = (sl >> lane) & 1u;
-      nld[u] = (m.nl >> lane) & 1u;
-    } else {
-      pp[u] = locate(cst, b0, b0 + lane);
-    }
+    for (int u = 0; u < U; u++) rl[u] = L.role[base + u * kWave + lane];
+#pragma unroll
+    for (int u = 0; u < U; u++) pp[u] = rl[u] & (kWave - 1);  // (past T: garbage, in range)
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) pp[u] = locate(cst, base + u * kWave, base + u * kWave + lane);
   }
+  uint64_t sd[U];
+  uint32_t idx[U];
 #pragma unroll
   for (int u = 0; u < U; u++) {
     const uint32_t c = base + u * kWave + lane;
     const ChunkRec &R = L.rec[pp[u]];
-    if (!MAP) {
-      isf[u] = c == R.sidx;
-      isl[u] = c == R.eidx;
-      nld[u] = isf[u] || isl[u];
+    // unconditional record reads (pp is always a valid index), then selects:
+    // no divergent branches around the LDS reads
+    sd[u] = *reinterpret_cast<const uint64_t *>(&R.soff);
+    if (MAP) {
+      idx[u] = (rl[u] & kRoleFirst) ? 2u : ((rl[u] & kRoleLast) ? 3u : (c & 1u));
+    } else {
+      const uint64_t se = *reinterpret_cast<const uint64_t *>(&R.sidx);
+      idx[u] = c == (uint32_t)se ? 2u : (c == (uint32_t)(se >> 32) ? 3u : (c & 1u));
     }
-    // a special block loads zero: its "keystream" is its value
-    const uint32_t idx = isf[u] ? 2u : (isl[u] ? 3u : (c & 1u));
-    S.k[u] = R.tab[idx];
-    S.doff[u] = c < T ? R.doff + 16u * c : kOffNone;
-    off[u] = c < T && !nld[u] ? R.soff + 16u * c : kOffNone;
+    S.k[u] = R.tab[idx[u]];
   }
-  S.spm = 0u;
 #pragma unroll
-  for (int u = 0; u < U; u++) S.spm |= (isf[u] || isl[u]) ? 1u << u : 0u;
+  for (int u = 0; u < U; u++) {
+    const uint32_t c = base + u * kWave + lane;
+    const bool in = c < T;
+    S.doff[u] = in ? (uint32_t)(sd[u] >> 32) + 16u * c : kOffNone;
+    off[u] = in && idx[u] < 2u ? (uint32_t)sd[u] + 16u * c : kOffNone;
+  }
 #pragma unroll
   for (int u = 0; u < U; u++) S.v[u] = __builtin_amdgcn_raw_buffer_load_b128(B.src, off[u], 0, kAuxLd);
 }
@@ -768,11 +745,8 @@ __device__ __forceinline__ void stream_issue(const WaveLds &L, const WaveBufs &B
 template <int U>
 __device__ __forceinline__ void stream_store(const WaveBufs &B, const Step<U> &S) {
 #pragma unroll
-  for (int u = 0; u < U; u++) {
-    const u32x4 z = {0u, 0u, 0u, 0u};
-    const u32x4 v = (S.spm >> u) & 1u ? z : S.v[u];
-    __builtin_amdgcn_raw_buffer_store_b128(v ^ S.k[u], B.dst, S.doff[u], 0, kAuxSt);
-  }
+  for (int u = 0; u < U; u++)
+    __builtin_amdgcn_raw_buffer_store_b128(S.v[u] ^ S.k[u], B.dst, S.doff[u], 0, kAuxSt);
 }
 
 // Double-buffered stream loop.  The caller has issued step 0's loads into
@@ -780,14 +754,17 @@ __device__ __forceinline__ void stream_store(const WaveBufs &B, const Step<U> &S
 // stored, so a wave keeps U..2U KiB of reads outstanding.
 template <int U, bool MAP>
 __device__ __forceinline__ void stream_loop(const WaveLds &L, const WaveBufs &B, uint32_t cst,
-                                            uint32_t T, uint32_t lane, uint32_t &run,
-                                            Step<U> &cur) {
+                                            uint32_t T, uint32_t lane, Step<U> &cur) {
   constexpr uint32_t STEP = kWave * U;
-  for (uint32_t base = 0; base < T; base += STEP) {
-    Step<U> nxt;
-    stream_issue<U, MAP>(L, B, cst, T, lane, base + STEP, run, nxt);
+  // unrolled by two with two named steps, so no register copies between them
+  Step<U> nxt;
+  for (uint32_t base = 0;; base += 2 * STEP) {
+    stream_issue<U, MAP>(L, B, cst, T, lane, base + STEP, nxt);
     stream_store<U>(B, cur);
-    cur = nxt;
+    if (base + STEP >= T) break;
+    stream_issue<U, MAP>(L, B, cst, T, lane, base + 2 * STEP, cur);
+    stream_store<U>(B, nxt);
+    if (base + 2 * STEP >= T) break;
   }
 }
 
@@ -797,7 +774,7 @@ __device__ __forceinline__ void stream_loop(const WaveLds &L, const WaveBufs &B,
 __device__ __noinline__ void stream_generic(const WaveLds &L, uint32_t cst, uint32_t T,
                                             uint32_t lane) {
   for (uint32_t b0 = 0; b0 < T; b0 += kWave) {
-    const uint32_t c = min(b0 + lane, T - 1);
+    const uint32_t c = b0 + lane < T - 1 ? b0 + lane : T - 1;
     const ChunkRec &R = L.rec[locate(cst, b0, c)];
     uint32_t w[4] = {0u, 0u, 0u, 0u};
     u32x4 k = R.tab[c & 1];
@@ -855,14 +832,13 @@ __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
   fill_unit<KIND, DIR, MULTI>(P, J, salt, do_hash, pid, W, owner, lane, G, L);
   SQ_STAMP(3);
   // 4. the stream
-  uint32_t run = 0;
   Step<U> cur;
   if (S.fast && S.map) {
-    stream_issue<U, true>(L, S.B, S.cst, S.T, lane, 0, run, cur);
-    stream_loop<U, true>(L, S.B, S.cst, S.T, lane, run, cur);
+    stream_issue<U, true>(L, S.B, S.cst, S.T, lane, 0, cur);
+    stream_loop<U, true>(L, S.B, S.cst, S.T, lane, cur);
   } else if (S.fast) {
-    stream_issue<U, false>(L, S.B, S.cst, S.T, lane, 0, run, cur);
-    stream_loop<U, false>(L, S.B, S.cst, S.T, lane, run, cur);
+    stream_issue<U, false>(L, S.B, S.cst, S.T, lane, 0, cur);
+    stream_loop<U, false>(L, S.B, S.cst, S.T, lane, cur);
   } else if (S.T != 0) {
     stream_generic(L, S.cst, S.T, lane);
   }
