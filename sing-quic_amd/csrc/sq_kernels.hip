@@ -81,6 +81,18 @@ namespace sq {
 #ifndef SQ_LDSPAD
 #define SQ_LDSPAD 0
 #endif
+// 1: the first packet of a unit gives the blocks it owns in the 64-byte line
+// its output starts in to the previous unit's wave (which holds it as its
+// look-ahead lane), so no output line is written by two waves.
+#ifndef SQ_DONATE
+#define SQ_DONATE 1
+#endif
+// Stream alignment (map path): the flat space starts (d_lo / 16) mod 2^SQ_ALIGN
+// slots in, so for back-to-back outputs every 1 KiB wave instruction covers
+// whole 2^(SQ_ALIGN+4)-byte lines (0: off; 3: 128-byte L2 lines).
+#ifndef SQ_ALIGN
+#define SQ_ALIGN 3
+#endif
 // Timeline builds (scripts/dev/timeline.py, never shipped): lane 0 of every
 // wave records the constant-rate clock at its phase boundaries.
 #ifndef SQ_TIMELINE
@@ -92,7 +104,7 @@ namespace sq {
 extern "C" const char *sqobfs_build_info(void) {
   return "gfx950 obfs_kernel U=" SQ_STR(SQ_U) " PPW=" SQ_STR(SQ_PPW) " NT=" SQ_STR(SQ_NT)
          " minw=" SQ_STR(SQ_MINW) " block=" SQ_STR(SQ_BLOCK)
-         " ablate=" SQ_STR(SQ_ABLATE);
+         " ablate=" SQ_STR(SQ_ABLATE) " donate=" SQ_STR(SQ_DONATE) " align=" SQ_STR(SQ_ALIGN);
 }
 
 constexpr uint32_t kPktPerWave = SQ_PPW;
@@ -411,7 +423,10 @@ static_assert(sizeof(ChunkRec) == 96, "ChunkRec layout");
 constexpr uint32_t kMapBlocks = 4096;  // 64 KiB of output per unit
 constexpr uint32_t kRoleFirst = 64, kRoleLast = 128;
 // slack for the steps the double-buffered loop issues past the end
-constexpr uint32_t kMapSlack = 2 * kWave * SQ_U;
+constexpr uint32_t kMapSlack = 2 * kWave * SQ_U + 64;
+// record index of the phase slots (below): no packet (ranks are <= 62)
+constexpr uint32_t kRankNone = kWave - 1;
+constexpr uint32_t kOffPhase = 0xFFFFF000u;  // + 16 c (c < 64) stays past any span
 struct WaveLds {
   ChunkRec rec[kWave];
   uint32_t cst[kWave];  // flat start of the packet of each rank
@@ -431,7 +446,9 @@ struct UnitStream {
 };
 
 constexpr uint32_t kNoIdx = 0xFFFFFFFFu;
-constexpr uint64_t kMaxSpan = 0xFFFFFF00ull;
+constexpr uint64_t kMaxSpan = 0xFFFFE000ull;
+static_assert(kOffPhase >= kMaxSpan && kOffPhase + 16ull * kWave <= 0xFFFFFFF0ull,
+              "phase-slot offsets must be out of range and must not wrap");
 
 // Block geometry of a unit's packets, from their jobs alone.
 struct Geo {
@@ -452,7 +469,8 @@ struct Geo {
 // records, the block map and the buffer resources -- everything the first
 // stream loads need.  Every lane of the wave runs it.
 __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, uint32_t lane,
-                                                uint32_t ppw, WaveLds &L, Geo &G) {
+                                                uint32_t ppw, bool has_prev, WaveLds &L,
+                                                Geo &G) {
   out_range(J, G.rs, G.re, G.ne);
   const uint64_t rs = G.rs, re = G.re;
   // in place (input overlaps its own output blocks): a neighbour in another
@@ -468,19 +486,32 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
   const uint32_t fl = (G.ne ? 1u : 0u) | (ovl ? 2u : 0u);
   const uint32_t fl_n = shfl32(fl, nl), fl_p = shfl32(fl, pl);
 
-  const uint64_t B0 = up16(rs), E = up16(re), BL = re & ~15ull;
-  G.B0 = B0;
-  G.nblk = (owner && G.ne && E > B0) ? (uint32_t)((E - B0) >> 4) : 0u;
-  const uint32_t nblk = G.nblk;
-  G.hl = nblk && (re & 15);
-  G.hf = nblk && B0 < J.dst_pay && !(G.hl && B0 == BL);
+  const uint64_t B0r = up16(rs), E = up16(re), BL = re & ~15ull;
+  const uint32_t nraw = (G.ne && E > B0r) ? (uint32_t)((E - B0r) >> 4) : 0u;
   const bool cross_n = lane == ppw - 1, cross_p = lane == 0;
-  // last block whole: the next datagram starts at re and fills the block
-  G.lfull = G.hl && (fl_n & 1) && rs_n == re && re_n >= E && !(cross_n && (fl_n & 2));
   // leading bytes [rs, B0) covered by the previous packet's whole last block
   // (the same predicate as the previous lane's lfull)
   const bool p_hl = (fl_p & 1) && (re_p & 15) && up16(re_p) > up16(rs_p);
-  G.pfull = p_hl && G.ne && re_p == rs && re >= B0 && !(cross_p && ovl);
+  G.pfull = p_hl && G.ne && re_p == rs && re >= B0r && !(cross_p && ovl);
+  // Donation.  A unit's first packet p gives its blocks in the 64-byte line
+  // its output starts in ([B0, LE)) to the previous unit's wave, which holds
+  // p as its look-ahead lane (key, head image and job already there): every
+  // output line is then written whole by one wave.  Both waves decide from
+  // the same data (p's job and p-1's end); only when p continues past LE, is
+  // not in place, and its leading bytes are a whole junction block or none.
+  const bool ahead = lane == ppw, head = lane == 0 && has_prev;
+  const uint64_t LE = (rs + 63) & ~63ull;
+  const bool donate = SQ_DONATE && (ahead || head) && G.ne && !ovl && LE > B0r &&
+                      B0r + 16ull * nraw > LE && ((rs & 15) == 0 || G.pfull);
+  const uint32_t don = donate ? (uint32_t)((LE - B0r) >> 4) : 0u;
+  const uint64_t B0 = donate && head ? LE : B0r;
+  G.B0 = B0;
+  G.nblk = owner ? nraw - (donate ? don : 0u) : (donate ? don : 0u);
+  const uint32_t nblk = G.nblk;
+  G.hl = nblk && (re & 15) && !(donate && ahead);
+  G.hf = nblk && B0 < J.dst_pay && !(G.hl && B0 == BL);
+  // last block whole: the next datagram starts at re and fills the block
+  G.lfull = G.hl && (fl_n & 1) && rs_n == re && re_n >= E && !(cross_n && (fl_n & 2));
 
   // the flat block space: this packet's blocks [B0, B0 + 16 F)
   const uint32_t F = (G.hl && !G.lfull) ? nblk - 1 : nblk;
@@ -491,15 +522,14 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
     if (lane >= (uint32_t)d) incl += y;
   }
   UnitStream U;
-  const uint32_t start = incl - F;
-  G.start = start;
+  const uint32_t start0 = incl - F;
   G.flat = F != 0;
   const uint64_t fm = __ballot(G.flat);
   G.rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32),
                                      __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
   const uint32_t K = (uint32_t)__popcll(fm);
-  U.T = __builtin_amdgcn_readfirstlane(__shfl(incl, kWave - 1, kWave));
-  U.map = U.T <= kMapBlocks;
+  const uint32_t T0 = __builtin_amdgcn_readfirstlane(__shfl(incl, kWave - 1, kWave));
+  U.map = T0 + (1u << SQ_ALIGN) <= kMapBlocks;
   // interior blocks [i_lo, i_hi): the only ones loaded
   const uint32_t i_lo = G.hf ? 1u : 0u, i_hi = G.hl ? nblk - 1 : nblk;
   const bool has_int = i_hi > i_lo;
@@ -512,7 +542,15 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
   const uint64_t s_hi = uniform64(wave_max64(has_int ? s_end : 0ull));
   const bool mis = has_int && (sabs & 3);
   const bool sok = s_hi <= s_lo || s_hi - s_lo <= kMaxSpan;
-  U.fast = U.T != 0 && __ballot(mis) == 0 && d_hi - d_lo <= kMaxSpan && sok;
+  U.fast = T0 != 0 && __ballot(mis) == 0 && d_hi - d_lo <= kMaxSpan && sok;
+  // map path (buffer streaming only: the generic path walks [0, T) by
+  // `locate`): shift the flat space so that slot c sits at d_lo's line phase
+  const uint32_t phase = U.map && U.fast && SQ_ALIGN
+                             ? (uint32_t)(d_lo >> 4) & ((1u << SQ_ALIGN) - 1u)
+                             : 0u;
+  const uint32_t start = start0 + phase;
+  G.start = start;
+  U.T = T0 + phase;
   const bool si = s_hi > s_lo;
   const uint64_t sb = si ? s_lo : d_lo;
   if (U.fast) {
@@ -521,6 +559,11 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
                                                 0x00020000);
     U.B.dst = __builtin_amdgcn_make_buffer_rsrc((void *)d_lo, 0, (int)(uint32_t)(d_hi - d_lo),
                                                 0x00020000);
+  }
+  if (U.map && lane < phase) L.role[lane] = (uint8_t)kRankNone;
+  if (U.map && lane == kRankNone) {
+    L.rec[kRankNone].soff = kOffPhase;
+    L.rec[kRankNone].doff = kOffPhase;
   }
   if (G.flat) {
     ChunkRec &R = L.rec[G.rank];
@@ -825,7 +868,7 @@ __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
   // 3a. plan
   Geo G;
   WaveLds &L = lds[wv];
-  const UnitStream S = plan_unit(J, owner, lane, ppw, L, G);
+  const UnitStream S = plan_unit(J, owner, lane, ppw, first != 0, L, G);
   SQ_STAMP(2);
   const uint32_t pid = MULTI && d.pid < P.n_psk ? d.pid : 0u;
   // 2 + 3b. key and block contents
