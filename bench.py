@@ -62,6 +62,8 @@ def parse():
                     help="in-process sharding: one process, K contexts over the visible GPUs "
                          "(context k on GPU k mod count), the config's batch cut by bytes "
                          "(sqobfs_shard_cuts) and launched with sqobfs_shard_run")
+    ap.add_argument("--unit-packets", type=int, default=0,
+                    help="obfuscation kernel unit size, packets per wavefront (0 = default)")
     ap.add_argument("--packets", type=int, default=0,
                     help="dev: override the config's packet count (scaling probes; not a "
                          "BASELINE configuration)")
@@ -427,6 +429,7 @@ def main():
     S = sh["S"]
     ctx = sqobfs.Context(gpu)
     kr = sqobfs.Keyring(ctx, kind, sh["psks"])
+    ctx.unit_packets = args.unit_packets
     stream = torch.cuda.current_stream(dev)
     s = stream.cuda_stream
 
@@ -542,6 +545,7 @@ def main():
             "packets_per_gpu": n,
             "payload_bytes_per_gpu": sh["payload_bytes"],
             "layout": args.layout,
+            "unit_packets": ctx.unit_packets,
             "parallelism": f"shard{world} (independent packets, no collective)",
         },
         "roofline": {

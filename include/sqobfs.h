@@ -155,6 +155,15 @@ int sqobfs_salt_key(sqobfs_ctx *ctx, const uint8_t key[32], uint64_t next_seq);
 /* The sequence number the next SQOBFS_FLAG_DEVICE_SALT launch will use. */
 uint64_t sqobfs_salt_seq(const sqobfs_ctx *ctx);
 
+/* Tuning: the obfuscation kernel's unit, the number of consecutive packets
+ * one wavefront derives keys for and streams (1 .. 62; 0 = the built-in
+ * default, 32).  Results are identical for every value; only the speed
+ * changes (shorter units raise the per-byte prologue,
+ * longer ones the per-wave stream).  Takes effect on later launches. */
+int sqobfs_set_unit_packets(sqobfs_ctx *ctx, uint32_t packets);
+/* the unit size later launches will use (the default when 0 was set) */
+uint32_t sqobfs_unit_packets(const sqobfs_ctx *ctx);
+
 /* Upload `count` pre-shared keys (host memory: psk k = blob[off[k] .. +len[k]])
  * and derive each one's per-PSK hash state on the GPU.  kind selects the
  * hash (BLAKE2b for Salamander, SHA-256 for XPlus).  Any PSK length works,

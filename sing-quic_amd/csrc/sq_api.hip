@@ -35,6 +35,8 @@ struct sqobfs_ctx {
   // SQOBFS_FLAG_DEVICE_SALT: ChaCha20 key and the next launch sequence number
   uint32_t salt_key[8] = {};
   std::atomic<uint64_t> salt_seq{0};
+  // obfuscation kernel unit size (packets per wavefront); 0 = built-in default
+  std::atomic<uint32_t> unit_packets{0};
 };
 
 namespace {
@@ -149,6 +151,7 @@ sq::KParams make_params(sqobfs_ctx *ctx, const sqobfs_keyring *kr, const sqobfs_
   kp.n = b->n;
   kp.n_psk = kr->count;
   kp.psk0 = kr->host0;
+  kp.ppw = ctx->unit_packets.load(std::memory_order_relaxed);
   if (b->flags & SQOBFS_FLAG_DEVICE_SALT) {
     const uint64_t seq = ctx->salt_seq.fetch_add(1);
     kp.device_salt = 1;
@@ -281,6 +284,17 @@ int sqobfs_salt_key(sqobfs_ctx *ctx, const uint8_t key[32], uint64_t next_seq) {
 }
 
 uint64_t sqobfs_salt_seq(const sqobfs_ctx *ctx) { return ctx ? ctx->salt_seq.load() : 0; }
+
+int sqobfs_set_unit_packets(sqobfs_ctx *ctx, uint32_t packets) {
+  if (!ctx || packets > sq::kMaxUnitPackets) return SQ_EINVAL;
+  ctx->unit_packets.store(packets, std::memory_order_relaxed);
+  return SQ_OK;
+}
+
+uint32_t sqobfs_unit_packets(const sqobfs_ctx *ctx) {
+  const uint32_t v = ctx ? ctx->unit_packets.load(std::memory_order_relaxed) : 0u;
+  return v ? v : sq::kDefaultUnitPackets;
+}
 
 void *sqobfs_stream(sqobfs_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
 

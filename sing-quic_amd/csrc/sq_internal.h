@@ -13,6 +13,13 @@ constexpr int kWave = 64;           // CDNA wavefront
 #define SQ_BLOCK 256
 #endif
 constexpr int kBlock = SQ_BLOCK;    // 4 waves per workgroup
+// Obfuscation kernel unit: packets per wavefront (sqobfs_set_unit_packets);
+// two more lanes hold the unit's neighbour packets.
+#ifndef SQ_PPW
+#define SQ_PPW 32
+#endif
+constexpr uint32_t kDefaultUnitPackets = SQ_PPW;
+constexpr uint32_t kMaxUnitPackets = 62;
 constexpr int kWavesPerBlock = kBlock / kWave;
 
 // Per-PSK hash state, derived once per keyring on the GPU (psk_prepare).
@@ -57,6 +64,7 @@ struct KParams {
   uint32_t n;
   uint32_t n_psk;
   uint32_t device_salt;     // 1: obfuscate salts from ChaCha20(salt_key, salt_nonce)
+  uint32_t ppw;             // packets per wavefront (unit size), 1 .. 62; 0 = default
   uint32_t salt_key[8];
   uint32_t salt_nonce[3];
   PskEntry psk0;

@@ -8,9 +8,9 @@
 //   VectorisedXPlusConn.WriteTo               hysteria/xplus.go:86-98
 // for a whole ragged batch of datagrams per launch.
 //
-// One wavefront = one unit of kPktPerWave (32) consecutive packets, lane l
-// owning packet l; lanes 32 and 33 hold the packets just after and just
-// before the unit (the neighbours of its boundary blocks).
+// One wavefront = one unit of ppw (default 32, sqobfs_set_unit_packets)
+// consecutive packets, lane l owning packet l; lanes ppw and ppw + 1 hold the
+// packets just after and just before the unit (its boundary neighbours).
 //   1. descriptor  offsets, lengths, salt (obfuscate: the salt array;
 //                  deobfuscate: the first S wire bytes), the quirk table; the
 //                  loads of the head / tail image windows.
@@ -61,11 +61,6 @@ namespace sq {
 #ifndef SQ_U
 #define SQ_U 4
 #endif
-// Packets per wavefront (<= 62: lanes kPktPerWave and kPktPerWave + 1 hold
-// the neighbours).
-#ifndef SQ_PPW
-#define SQ_PPW 32
-#endif
 // Minimum waves per SIMD the register allocation must allow (0 = no bound).
 #ifndef SQ_MINW
 #define SQ_MINW 0
@@ -93,6 +88,20 @@ namespace sq {
 #ifndef SQ_ALIGN
 #define SQ_ALIGN 3
 #endif
+// 1: a stream step keeps only the LDS address of each block's keystream and
+// reads it when the block is stored (16 fewer VGPRs per U blocks in flight).
+#ifndef SQ_KLATE
+#define SQ_KLATE 0
+#endif
+// 1: Salamander keys from lane pairs (sq_hash.h b2_compress_pair) when the
+// unit leaves half the wave for them (ppw < 32).
+#ifndef SQ_HASH2
+#define SQ_HASH2 0
+#endif
+// Flat blocks a unit's block map covers (its role bytes live in LDS).
+#ifndef SQ_MAPBLK
+#define SQ_MAPBLK 4096
+#endif
 // Timeline builds (scripts/dev/timeline.py, never shipped): lane 0 of every
 // wave records the constant-rate clock at its phase boundaries.
 #ifndef SQ_TIMELINE
@@ -104,10 +113,12 @@ namespace sq {
 extern "C" const char *sqobfs_build_info(void) {
   return "gfx950 obfs_kernel U=" SQ_STR(SQ_U) " PPW=" SQ_STR(SQ_PPW) " NT=" SQ_STR(SQ_NT)
          " minw=" SQ_STR(SQ_MINW) " block=" SQ_STR(SQ_BLOCK)
-         " ablate=" SQ_STR(SQ_ABLATE) " donate=" SQ_STR(SQ_DONATE) " align=" SQ_STR(SQ_ALIGN);
+         " ablate=" SQ_STR(SQ_ABLATE) " donate=" SQ_STR(SQ_DONATE) " align=" SQ_STR(SQ_ALIGN)
+         " klate=" SQ_STR(SQ_KLATE) " map=" SQ_STR(SQ_MAPBLK) " hash2=" SQ_STR(SQ_HASH2);
 }
 
-constexpr uint32_t kPktPerWave = SQ_PPW;
+// default unit size (KParams.ppw == 0); any 1 .. kMaxUnitPackets works
+constexpr uint32_t kPktPerWave = kDefaultUnitPackets;
 
 #if SQ_TIMELINE
 constexpr uint32_t kTlStamps = 6, kTlWaves = 1u << 20;
@@ -122,7 +133,8 @@ __device__ uint64_t g_timeline[kTlWaves * kTlStamps];
   do {              \
   } while (0)
 #endif
-static_assert(kPktPerWave >= 1 && kPktPerWave + 2 <= kWave, "unit + 2 neighbour lanes");
+static_assert(kPktPerWave >= 1 && kPktPerWave <= kMaxUnitPackets && kMaxUnitPackets + 2 <= kWave,
+              "unit + 2 neighbour lanes");
 
 constexpr uint32_t kMaxPacket = 1u << 26;  // per-packet length bound (u32 block math)
 constexpr uint32_t kBadPsk = 0xFFFFFFFFu;
@@ -420,7 +432,7 @@ static_assert(sizeof(ChunkRec) == 96, "ChunkRec layout");
 // per flat block, the owning packet's record index (bits 0-5) and the
 // block's role (bit 6: special first block, bit 7: special last block).
 // The stream reads one byte per block: no search, no cross-lane work.
-constexpr uint32_t kMapBlocks = 4096;  // 64 KiB of output per unit
+constexpr uint32_t kMapBlocks = SQ_MAPBLK;  // 64 KiB of output per unit (4096)
 constexpr uint32_t kRoleFirst = 64, kRoleLast = 128;
 // slack for the steps the double-buffered loop issues past the end
 constexpr uint32_t kMapSlack = 2 * kWave * SQ_U + 64;
@@ -601,12 +613,28 @@ template <int KIND, int DIR, bool MULTI>
 __device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
                                           const uint32_t (&salt)[4], bool do_hash, uint32_t pid,
                                           const Windows &W, bool owner, uint32_t lane,
-                                          const Geo &G, WaveLds &L) {
+                                          uint32_t ppw, const Geo &G, WaveLds &L) {
   constexpr uint32_t S = KIND == 0 ? kSalamanderSalt : kXPlusSalt;
   constexpr uint32_t PW = DIR == 0 ? S / 4 : 0;  // salt words in front of the payload
   uint32_t key[8];
-  // single PSK: the kernarg copy (scalar loads); several: the device table
-  derive_key<KIND>(do_hash, MULTI ? P.psk_table + pid : &P.psk0, salt, key);
+  if (KIND == 0 && SQ_HASH2 && !(SQ_ABLATE & 1) && ppw + 1 <= kWave / 2) {
+    // lanes 0 .. ppw need keys: hash lanes 2k and 2k + 1 take packet lane k
+    const uint32_t k = lane >> 1;
+    const uint32_t s2[2] = {shfl32(salt[0], k), shfl32(salt[1], k)};
+    const uint32_t pk = MULTI ? shfl32(pid, k) : 0u;
+    uint32_t kw[4];
+    salamander_key_pair(MULTI ? P.psk_table + pk : &P.psk0, s2, lane & 1, kw);
+    const uint32_t le = (2 * lane) & (kWave - 1);
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t x = shfl32(kw[j], le), y = shfl32(kw[j], le + 1);
+      key[j] = do_hash ? x : 0u;
+      key[4 + j] = do_hash ? y : 0u;
+    }
+  } else {
+    // single PSK: the kernarg copy (scalar loads); several: the device table
+    derive_key<KIND>(do_hash, MULTI ? P.psk_table + pid : &P.psk0, salt, key);
+  }
   const uint64_t rs = G.rs, re = G.re;
   // head image: output bytes [rs, rs + 32) = salt || payload ^ key
   uint32_t hi[8];
@@ -734,7 +762,12 @@ constexpr int kAuxSt = (SQ_NT & 2) ? 2 : 0;
 // special values) and output offsets.
 template <int U>
 struct Step {
-  u32x4 v[U], k[U];
+  u32x4 v[U];
+#if SQ_KLATE
+  uint32_t ka[U];  // byte offset of the block's keystream in the WaveLds
+#else
+  u32x4 k[U];
+#endif
   uint32_t doff[U];
 };
 
@@ -772,7 +805,12 @@ __device__ __forceinline__ void stream_issue(const WaveLds &L, const WaveBufs &B
       const uint64_t se = *reinterpret_cast<const uint64_t *>(&R.sidx);
       idx[u] = c == (uint32_t)se ? 2u : (c == (uint32_t)(se >> 32) ? 3u : (c & 1u));
     }
+#if SQ_KLATE
+    S.ka[u] = (uint32_t)(reinterpret_cast<const char *>(&R.tab[idx[u]]) -
+                         reinterpret_cast<const char *>(&L));
+#else
     S.k[u] = R.tab[idx[u]];
+#endif
   }
 #pragma unroll
   for (int u = 0; u < U; u++) {
@@ -786,10 +824,19 @@ __device__ __forceinline__ void stream_issue(const WaveLds &L, const WaveBufs &B
 }
 
 template <int U>
-__device__ __forceinline__ void stream_store(const WaveBufs &B, const Step<U> &S) {
+__device__ __forceinline__ void stream_store(const WaveLds &L, const WaveBufs &B,
+                                             const Step<U> &S) {
+#if SQ_KLATE
+  u32x4 k[U];
 #pragma unroll
   for (int u = 0; u < U; u++)
-    __builtin_amdgcn_raw_buffer_store_b128(S.v[u] ^ S.k[u], B.dst, S.doff[u], 0, kAuxSt);
+    k[u] = *reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>(&L) + S.ka[u]);
+#else
+  const u32x4(&k)[U] = S.k;
+#endif
+#pragma unroll
+  for (int u = 0; u < U; u++)
+    __builtin_amdgcn_raw_buffer_store_b128(S.v[u] ^ k[u], B.dst, S.doff[u], 0, kAuxSt);
 }
 
 // Double-buffered stream loop.  The caller has issued step 0's loads into
@@ -803,10 +850,10 @@ __device__ __forceinline__ void stream_loop(const WaveLds &L, const WaveBufs &B,
   Step<U> nxt;
   for (uint32_t base = 0;; base += 2 * STEP) {
     stream_issue<U, MAP>(L, B, cst, T, lane, base + STEP, nxt);
-    stream_store<U>(B, cur);
+    stream_store<U>(L, B, cur);
     if (base + STEP >= T) break;
     stream_issue<U, MAP>(L, B, cst, T, lane, base + 2 * STEP, cur);
-    stream_store<U>(B, nxt);
+    stream_store<U>(L, B, nxt);
     if (base + 2 * STEP >= T) break;
   }
 }
@@ -845,7 +892,7 @@ __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wv = threadIdx.x / kWave;
   const uint64_t unit = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
-  const uint32_t ppw = kPktPerWave;
+  const uint32_t ppw = P.ppw;
   const uint64_t first = unit * ppw;
   if (first >= P.n) return;
   SQ_STAMP(0);
@@ -872,7 +919,7 @@ __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
   SQ_STAMP(2);
   const uint32_t pid = MULTI && d.pid < P.n_psk ? d.pid : 0u;
   // 2 + 3b. key and block contents
-  fill_unit<KIND, DIR, MULTI>(P, J, salt, do_hash, pid, W, owner, lane, G, L);
+  fill_unit<KIND, DIR, MULTI>(P, J, salt, do_hash, pid, W, owner, lane, ppw, G, L);
   SQ_STAMP(3);
   // 4. the stream
   Step<U> cur;
@@ -969,10 +1016,13 @@ __global__ void psk_prepare_kernel(int kind, const uint8_t *blob, const uint64_t
 template <int KIND, int DIR, bool MULTI>
 static int launch_one(const KParams *kp, hipStream_t s) {
   constexpr int U = SQ_U;
-  const uint64_t units = ((uint64_t)kp->n + kPktPerWave - 1) / kPktPerWave;
+  KParams P = *kp;
+  if (P.ppw == 0) P.ppw = kPktPerWave;
+  if (P.ppw > kMaxUnitPackets) return -1;
+  const uint64_t units = ((uint64_t)P.n + P.ppw - 1) / P.ppw;
   const uint64_t blocks = (units + kWavesPerBlock - 1) / kWavesPerBlock;
   hipLaunchKernelGGL((obfs_kernel<KIND, DIR, MULTI, U>), dim3((uint32_t)blocks), dim3(kBlock),
-                     SQ_LDSPAD, s, *kp);
+                     SQ_LDSPAD, s, P);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

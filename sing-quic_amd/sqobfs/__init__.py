@@ -188,6 +188,10 @@ def lib() -> ctypes.CDLL:
     L.sqobfs_salt_key.argtypes = [vp, vp, ctypes.c_uint64]
     L.sqobfs_salt_seq.argtypes = [vp]
     L.sqobfs_salt_seq.restype = ctypes.c_uint64
+    L.sqobfs_set_unit_packets.argtypes = [vp, ctypes.c_uint32]
+    L.sqobfs_set_unit_packets.restype = ctypes.c_int
+    L.sqobfs_unit_packets.argtypes = [vp]
+    L.sqobfs_unit_packets.restype = ctypes.c_uint32
     _lib = L
     return L
 
@@ -273,6 +277,15 @@ class Context:
     @property
     def salt_seq(self) -> int:
         return lib().sqobfs_salt_seq(self.handle)
+
+    @property
+    def unit_packets(self) -> int:
+        """Packets per wavefront of the obfuscation kernel (tuning only)."""
+        return lib().sqobfs_unit_packets(self.handle)
+
+    @unit_packets.setter
+    def unit_packets(self, packets: int) -> None:
+        _check(lib().sqobfs_set_unit_packets(self.handle, packets), "sqobfs_set_unit_packets")
 
 
 class Keyring:

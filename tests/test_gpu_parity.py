@@ -175,6 +175,35 @@ def test_jumbo_units(ctx, kind, direction):
 
 @pytest.mark.parametrize("kind", KINDS)
 @pytest.mark.parametrize("direction", DIRS)
+def test_unit_sizes(ctx, kind, direction):
+    """Every unit size gives the same bytes (sqobfs_set_unit_packets): unit
+    boundaries, donation and the neighbour lanes move with it.  Ragged and
+    dense layouts, a 256-entry keyring, 1..62 packets per wavefront."""
+    rng = np.random.Generator(np.random.PCG64(900 + 10 * kind + direction))
+    lens = np.concatenate([np.arange(0, 40), rng.integers(0, 1500, 900), np.full(200, 1350)])
+    psks = [rng.integers(0, 256, int(k), dtype=np.uint8).tobytes()
+            for k in rng.integers(0, 140, 256)]
+    ids = rng.integers(0, 256, len(lens)).astype(np.uint16)
+    default = ctx.unit_packets
+    try:
+        for ppw in (1, 2, 7, 16, 26, 31, 33, 40, 62):
+            ctx.unit_packets = ppw
+            assert ctx.unit_packets == ppw
+            hb = gh.make_case(rng, kind, direction, lens, [PSK], in_align=4, out_lead=8)
+            check(ctx, kind, direction, [PSK], hb, f"{kind}/{direction}/ppw{ppw}")
+            hb = wire_dense_case(rng, kind, direction, lens, lead=8)
+            check(ctx, kind, direction, [PSK], hb, f"{kind}/{direction}/ppw{ppw}/dense")
+            hb = gh.make_case(rng, kind, direction, lens, psks, psk_ids=ids)
+            check(ctx, kind, direction, psks, hb, f"{kind}/{direction}/ppw{ppw}/multi")
+    finally:
+        ctx.unit_packets = 0
+    assert ctx.unit_packets == default
+    with pytest.raises(sqobfs.SqError):
+        ctx.unit_packets = 63
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("direction", DIRS)
 @pytest.mark.parametrize("in_align,in_lead,out_align,out_lead",
                          [(1, 0, 1, 0), (1, 3, 16, 0), (16, 0, 1, 5), (16, 8, 16, 8),
                           (16, 4, 16, 12), (4, 0, 8, 0)])
