@@ -63,7 +63,13 @@ def parse():
                          "(context k on GPU k mod count), the config's batch cut by bytes "
                          "(sqobfs_shard_cuts) and launched with sqobfs_shard_run")
     ap.add_argument("--unit-packets", type=int, default=0,
-                    help="obfuscation kernel unit size, packets per wavefront (0 = default)")
+                    help="obfuscation kernel unit size, packets per wavefront (0 = sized "
+                         "from the batch's bytes by sqobfs_unit_packets_for, as a caller "
+                         "that built the batch does)")
+    ap.add_argument("--warmup-s", type=float, default=0.15,
+                    help="keep warming up (untimed) until this much wall time has passed "
+                         "and at least --warmup launches ran: a fresh process's first "
+                         "~25 launches run up to 10 %% slower (scripts/dev/warm_curve.py)")
     ap.add_argument("--packets", type=int, default=0,
                     help="dev: override the config's packet count (scaling probes; not a "
                          "BASELINE configuration)")
@@ -337,6 +343,8 @@ def inproc_bench(args):
         n_k = int(cut[k + 1] - cut[k])
         sh = build_shard(torch, dev, kind, n_k, L, n_psk, k, K, args.config, "dense", int(cut[k]))
         c = sqobfs.Context(g)
+        c.unit_packets = args.unit_packets or sqobfs.unit_packets_for(
+            sh["payload_bytes"], n_k, n_psk > 1)
         kr = sqobfs.Keyring(c, kind, sh["psks"])
         ctxs.append(c)
         krs.append(kr)
@@ -429,7 +437,8 @@ def main():
     S = sh["S"]
     ctx = sqobfs.Context(gpu)
     kr = sqobfs.Keyring(ctx, kind, sh["psks"])
-    ctx.unit_packets = args.unit_packets
+    ctx.unit_packets = args.unit_packets or sqobfs.unit_packets_for(
+        sh["payload_bytes"], n, n_psk > 1)
     stream = torch.cuda.current_stream(dev)
     s = stream.cuda_stream
 
@@ -460,8 +469,12 @@ def main():
         alg_bytes = 2 * sh["payload_bytes"] + S * n
 
     saved = save_samples(sh, n) if direction == sqobfs.OBFUSCATE else None
-    for _ in range(args.warmup):
+    warm, wt0 = 0, time.perf_counter()
+    while warm < args.warmup or time.perf_counter() - wt0 < args.warmup_s:
         sqobfs.launch(ctx, kr, direction, b, s)
+        warm += 1
+        if warm % 8 == 0:
+            torch.cuda.synchronize(dev)  # wall time follows the GPU
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
@@ -496,7 +509,7 @@ def main():
         salts = np.frombuffer(ol.device_salts(SALT_KEY, last, n, S), np.uint8)
         sh["salt"] = torch.from_numpy(salts.copy()).to(dev)
     if direction == sqobfs.OBFUSCATE:
-        parity = spot_check(torch, sh, kind, n, sh["out"], saved, args.warmup + args.steps)
+        parity = spot_check(torch, sh, kind, n, sh["out"], saved, warm + args.steps)
     else:
         lens = sh["lens"].cpu().numpy()
         offs = sh["in_off"].cpu().numpy()
@@ -526,6 +539,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "warmup_launches": warm,
         "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
         "higher_is_better": True,
         "scaling": "weak" if args.config != "salamander-16m-256psk" else "strong",
@@ -546,6 +560,9 @@ def main():
             "payload_bytes_per_gpu": sh["payload_bytes"],
             "layout": args.layout,
             "unit_packets": ctx.unit_packets,
+            "unit_rule": ("--unit-packets" if args.unit_packets else
+                          "sqobfs_unit_packets_for(payload bytes, n): ~20 KB per wavefront "
+                          "(36 KB with a multi-PSK keyring)"),
             "parallelism": f"shard{world} (independent packets, no collective)",
         },
         "roofline": {

@@ -1,0 +1,14 @@
+#!/bin/bash
+# GPU box: the whole GPU suite, smoke, then the driver's bench command and
+# every config / direction with the shipped lib.
+export TMPDIR=/tmp
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r3c3; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver.json 2> $O/bench_driver.err || { tail -20 $O/bench_driver.err; exit 1; }
+cat $O/bench_driver.json
+timeout -k 10 900 bash scripts/r2_configs.sh r3c3/cfg > $O/cfg.txt 2>&1 || { tail -20 $O/cfg.txt; exit 1; }
+cat $O/cfg.txt

@@ -291,6 +291,13 @@ int sqobfs_set_unit_packets(sqobfs_ctx *ctx, uint32_t packets) {
   return SQ_OK;
 }
 
+uint32_t sqobfs_unit_packets_for(uint64_t bytes, uint32_t n, int multi_psk) {
+  if (n == 0) return sq::kDefaultUnitPackets;
+  const uint64_t target = multi_psk ? sq::kUnitBytesMultiPsk : sq::kUnitBytes;
+  const uint64_t u = bytes ? target * n / bytes : sq::kMaxUnitPackets;  // floor(target / mean)
+  return (uint32_t)std::min<uint64_t>(std::max<uint64_t>(u, 1), sq::kMaxUnitPackets);
+}
+
 uint32_t sqobfs_unit_packets(const sqobfs_ctx *ctx) {
   const uint32_t v = ctx ? ctx->unit_packets.load(std::memory_order_relaxed) : 0u;
   return v ? v : sq::kDefaultUnitPackets;
@@ -924,7 +931,12 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
     db.psk_id = hb->psk_id ? (const uint16_t *)(D + o_pid) + ri.p0 : nullptr;
     db.in_cap = hb->in_cap ? (const uint32_t *)(D + o_cap) + ri.p0 : nullptr;
     if (db.n) {
-      const sq::KParams kp = make_params(ctx, kr, &db);
+      sq::KParams kp = make_params(ctx, kr, &db);
+      if (kp.ppw == 0) {  // lengths are on the host: size the units by bytes
+        uint64_t bytes = 0;
+        for (uint32_t i = ri.p0; i < ri.p1; i++) bytes += hb->in_len[i];
+        kp.ppw = sqobfs_unit_packets_for(bytes, db.n, hb->psk_id != nullptr);
+      }
       int fc = (int)c;
       st = g_fail_chunk.compare_exchange_strong(fc, -1) ? SQ_EDEVICE
                                                          : sq_launch_obfs(kind, dir, &kp, ctx->stream);

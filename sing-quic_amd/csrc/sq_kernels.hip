@@ -8,7 +8,7 @@
 //   VectorisedXPlusConn.WriteTo               hysteria/xplus.go:86-98
 // for a whole ragged batch of datagrams per launch.
 //
-// One wavefront = one unit of ppw (default 32, sqobfs_set_unit_packets)
+// One wavefront = one unit of ppw (sqobfs_set_unit_packets; ~20 KB of payload)
 // consecutive packets, lane l owning packet l; lanes ppw and ppw + 1 hold the
 // packets just after and just before the unit (its boundary neighbours).
 //   1. descriptor  offsets, lengths, salt (obfuscate: the salt array;

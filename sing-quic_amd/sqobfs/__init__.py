@@ -192,8 +192,16 @@ def lib() -> ctypes.CDLL:
     L.sqobfs_set_unit_packets.restype = ctypes.c_int
     L.sqobfs_unit_packets.argtypes = [vp]
     L.sqobfs_unit_packets.restype = ctypes.c_uint32
+    L.sqobfs_unit_packets_for.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int]
+    L.sqobfs_unit_packets_for.restype = ctypes.c_uint32
     _lib = L
     return L
+
+
+def unit_packets_for(total_bytes: int, n: int, multi_psk: bool = False) -> int:
+    """Unit size (packets per wavefront) for a batch of n packets holding
+    total_bytes bytes: sqobfs_unit_packets_for."""
+    return lib().sqobfs_unit_packets_for(total_bytes, n, int(multi_psk))
 
 
 def build_info() -> str:

@@ -97,3 +97,20 @@ def test_shard_cuts_balance_bytes():
     lens = np.concatenate([np.full(5000, 0, np.uint32), np.full(5000, 1400, np.uint32)])
     cut = sqobfs.shard_cuts(lens, 2)
     assert abs(int(cut[1]) - 7391) <= 1  # (5000*64 + 5000*1464) / 2 bytes each side
+
+
+def test_unit_packets_for_sizes_units_by_bytes():
+    """sqobfs_unit_packets_for (host logic, no GPU): ~20 KB of payload per
+    wavefront, 36 KB with a multi-PSK keyring, clamped to 1..62; the BASELINE
+    configs get the unit sizes the in-process sweeps measured best
+    (DESIGN.md section 5)."""
+    f = sqobfs.unit_packets_for
+    assert f(1350 << 20, 1 << 20) == 14          # configs[1]
+    assert f(1200 << 20, 1 << 20) == 16          # configs[2]
+    assert f(758 * (4 << 20), 4 << 20) == 26     # configs[3] (mean of U[64, 1452])
+    assert f(1350 * (16 << 20), 16 << 20, True) == 26  # configs[4]
+    assert f(64 * 1000, 1000) == 62 and f(0, 7) == 62
+    assert f(70_000 * 8, 8) == 1
+    for mean in range(1, 100_000, 997):
+        u = f(mean * 1000, 1000)
+        assert 1 <= u <= 62
