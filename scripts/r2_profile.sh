@@ -15,7 +15,7 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
            "GRBM_GUI_ACTIVE GRBM_COUNT"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $O/p$i -o p -- \
-    python bench.py --steps 5 --warmup 1 --no-cpu-baseline "$@" > $O/p$i.log 2>&1 \
+    python bench.py --steps 5 --warmup 1 --warmup-s 0 --no-cpu-baseline "$@" > $O/p$i.log 2>&1 \
     || { echo "pass $i ($grp) failed"; tail -5 $O/p$i.log; exit 1; }
 done
 python scripts/pmc_summary.py $O
