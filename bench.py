@@ -561,7 +561,7 @@ def main():
             "layout": args.layout,
             "unit_packets": ctx.unit_packets,
             "unit_rule": ("--unit-packets" if args.unit_packets else
-                          "sqobfs_unit_packets_for(payload bytes, n): ~20 KB per wavefront "
+                          "sqobfs_unit_packets_for(payload bytes, n): ~21.7 KB per wavefront "
                           "(36 KB with a multi-PSK keyring)"),
             "parallelism": f"shard{world} (independent packets, no collective)",
         },

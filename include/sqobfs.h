@@ -158,7 +158,7 @@ uint64_t sqobfs_salt_seq(const sqobfs_ctx *ctx);
 /* Tuning: the obfuscation kernel's unit, the number of consecutive packets
  * one wavefront derives keys for and streams (1 .. 62; 0 = automatic).
  * Results are identical for every value; only the speed changes (DESIGN.md
- * section 5: ~20 KB of payload per wavefront streams best).  Automatic means
+ * section 5: ~21.7 KB of payload per wavefront streams best).  Automatic means
  * sized by bytes where the library sees the lengths (sqobfs_run_host, per
  * chunk) and the built-in default (26) for device batches, whose lengths
  * stay on the GPU: a caller that knows its batch sets
@@ -167,7 +167,7 @@ int sqobfs_set_unit_packets(sqobfs_ctx *ctx, uint32_t packets);
 /* the unit size device launches will use (the default when 0 was set) */
 uint32_t sqobfs_unit_packets(const sqobfs_ctx *ctx);
 /* The unit size for a batch of n packets holding `bytes` payload (or
- * datagram) bytes in total: about 20 KB per wavefront, 36 KB when packets
+ * datagram) bytes in total: about 21.7 KB per wavefront, 36 KB when packets
  * select keyring entries (psk_id != NULL), clamped to 1 .. 62. */
 uint32_t sqobfs_unit_packets_for(uint64_t bytes, uint32_t n, int multi_psk);
 

@@ -17,7 +17,7 @@ import sqobfs  # noqa: E402
 import bench  # noqa: E402
 
 cfg = sys.argv[1]
-ppws = [int(x) for x in sys.argv[2].split()]
+ppws = sys.argv[2].split()
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 5
 deo = len(sys.argv) > 4 and sys.argv[4] == "deobfuscate"
 dev = torch.device("cuda", 0)
@@ -61,9 +61,9 @@ for _ in range(60):
 torch.cuda.synchronize()
 for r in range(rounds):
     for w in ppws:
-        ctx.unit_packets = w
+        ctx.unit_packets = int(w)
         res[w].append(round(timed(), 1))
     print(f"round {r} done", flush=True)
 for w in ppws:
     med = statistics.median(res[w])
-    print(f"{cfg:24s} {'deo' if deo else 'obf'} ppw {w:3d} median {med:8.1f} us  frac {alg / med / 8e6:.3f}  all {res[w]}")
+    print(f"{cfg:24s} {'deo' if deo else 'obf'} ppw {w:>4s} median {med:8.1f} us  frac {alg / med / 8e6:.3f}  all {res[w]}")

@@ -106,114 +106,6 @@ __device__ __forceinline__ void b2_compress(uint64_t h[8], const uint64_t m[16],
   h[7] ^= v7 ^ v15;
 }
 
-// ---------------------------------------------------------------- BLAKE2b, two lanes per state
-//
-// Lanes 2k and 2k + 1 compress the SAME message, each holding two of the
-// four columns of the 4x4 state (even lane: columns 0, 1; odd lane: columns
-// 2, 3) as a[s], b[s], c[s], d[s] = rows 0-3 of its column 2h + s.  The
-// column step is two independent G per lane.  For the diagonal step each
-// lane needs diagonals 2h and 2h + 1: row 1 gives one word to the partner
-// lane, row 2 both, row 3 one (4 words each way through DPP quad_perm
-// [1,0,3,2], one v_mov_b32_dpp per dword), and the same moves undo it.
-// The message word of each G is the lane's choice between two schedule
-// entries (v_cndmask).  Per round: 4 G + 16 DPP moves + 16 selects per lane
-// against 8 G for one lane per state, with every lane of the wave busy.
-
-constexpr uint8_t kB2Sigma[12][16] = {
-    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
-    {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
-    {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4},
-    {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
-    {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13},
-    {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
-    {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11},
-    {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
-    {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5},
-    {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0},
-    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
-    {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3}};
-
-__device__ __forceinline__ void b2_g(uint64_t &a, uint64_t &b, uint64_t &c, uint64_t &d,
-                                     uint64_t x, uint64_t y) {
-  a = a + b + x;
-  d = b2_rotr32(d ^ a);
-  c = c + d;
-  b = b2_rotr_lt32<24>(b ^ c);
-  a = a + b + y;
-  d = b2_rotr_lt32<16>(d ^ a);
-  c = c + d;
-  b = b2_rotr63(b ^ c);
-}
-
-// the partner lane's (lane ^ 1) value: DPP quad_perm [1,0,3,2]
-__device__ __forceinline__ uint64_t b2_partner(uint64_t x) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)x, 0xB1, 0xF, 0xF, true);
-  const uint32_t hi =
-      (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(x >> 32), 0xB1, 0xF, 0xF, true);
-  return b2_pack(lo, hi);
-}
-
-// One round over the lane pair (schedule row R, compile-time indices).
-template <int R>
-__device__ __forceinline__ void b2_pair_round(uint64_t (&a)[2], uint64_t (&b)[2], uint64_t (&c)[2],
-                                              uint64_t (&d)[2], uint64_t (&m)[16], bool odd) {
-  constexpr int s0 = kB2Sigma[R][0], s1 = kB2Sigma[R][1], s2 = kB2Sigma[R][2],
-                s3 = kB2Sigma[R][3], s4 = kB2Sigma[R][4], s5 = kB2Sigma[R][5],
-                s6 = kB2Sigma[R][6], s7 = kB2Sigma[R][7], s8 = kB2Sigma[R][8],
-                s9 = kB2Sigma[R][9], s10 = kB2Sigma[R][10], s11 = kB2Sigma[R][11],
-                s12 = kB2Sigma[R][12], s13 = kB2Sigma[R][13], s14 = kB2Sigma[R][14],
-                s15 = kB2Sigma[R][15];
-  // opaque per round: keeps the compiler from sharing (and so keeping
-  // alive) message selects of different rounds
-#pragma unroll
-  for (int j = 0; j < 16; j++) asm volatile("" : "+v"(m[j]));
-  // columns 2h, 2h + 1 (G 0, 1 on the even lane, G 2, 3 on the odd one)
-  b2_g(a[0], b[0], c[0], d[0], odd ? m[s4] : m[s0], odd ? m[s5] : m[s1]);
-  b2_g(a[1], b[1], c[1], d[1], odd ? m[s6] : m[s2], odd ? m[s7] : m[s3]);
-  // diagonals 2h, 2h + 1 (G 4, 5 / 6, 7)
-  uint64_t b0 = b[1], b1 = b2_partner(b[0]);
-  uint64_t c0 = b2_partner(c[0]), c1 = b2_partner(c[1]);
-  uint64_t d0 = b2_partner(d[1]), d1 = d[0];
-  b2_g(a[0], b0, c0, d0, odd ? m[s12] : m[s8], odd ? m[s13] : m[s9]);
-  b2_g(a[1], b1, c1, d1, odd ? m[s14] : m[s10], odd ? m[s15] : m[s11]);
-  b[1] = b0;
-  b[0] = b2_partner(b1);
-  c[0] = b2_partner(c0);
-  c[1] = b2_partner(c1);
-  d[0] = d1;
-  d[1] = b2_partner(d0);
-}
-
-// Compression F over the lane pair.  hh = this lane's chaining words
-// {h[2h], h[2h + 1], h[4 + 2h], h[5 + 2h]} (odd = lane parity h), updated in
-// place: exactly the words the next block starts from, so multi-block
-// messages need no exchange.  Both lanes of a pair must be active.
-__device__ __forceinline__ void b2_compress_pair(uint64_t (&hh)[4], const uint64_t (&mi)[16],
-                                                 uint64_t t, bool last, bool odd) {
-  uint64_t m[16];
-#pragma unroll
-  for (int j = 0; j < 16; j++) m[j] = mi[j];
-  uint64_t a[2] = {hh[0], hh[1]}, b[2] = {hh[2], hh[3]};
-  uint64_t c[2] = {odd ? kB2IV2 : kB2IV0, odd ? kB2IV3 : kB2IV1};
-  uint64_t d[2] = {odd ? (last ? ~kB2IV6 : kB2IV6) : (kB2IV4 ^ t), odd ? kB2IV7 : kB2IV5};
-  b2_pair_round<0>(a, b, c, d, m, odd);
-  b2_pair_round<1>(a, b, c, d, m, odd);
-  b2_pair_round<2>(a, b, c, d, m, odd);
-  b2_pair_round<3>(a, b, c, d, m, odd);
-  b2_pair_round<4>(a, b, c, d, m, odd);
-  b2_pair_round<5>(a, b, c, d, m, odd);
-  b2_pair_round<6>(a, b, c, d, m, odd);
-  b2_pair_round<7>(a, b, c, d, m, odd);
-  b2_pair_round<8>(a, b, c, d, m, odd);
-  b2_pair_round<9>(a, b, c, d, m, odd);
-  b2_pair_round<10>(a, b, c, d, m, odd);
-  b2_pair_round<11>(a, b, c, d, m, odd);
-  hh[0] ^= a[0] ^ c[0];
-  hh[1] ^= a[1] ^ c[1];
-  hh[2] ^= b[0] ^ d[0];
-  hh[3] ^= b[1] ^ d[1];
-}
-
 // BLAKE2b-256 initial chaining value: IV ^ parameter block (digest 32, key 0,
 // fanout 1, depth 1).
 __device__ __host__ inline void b2_init256(uint64_t h[8]) {

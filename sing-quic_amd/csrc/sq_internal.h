@@ -21,9 +21,9 @@ constexpr int kBlock = SQ_BLOCK;    // 4 waves per workgroup
 constexpr uint32_t kDefaultUnitPackets = SQ_PPW;
 constexpr uint32_t kMaxUnitPackets = 62;
 // Sized by bytes when the batch's lengths are known (sqobfs_unit_packets_for):
-// about this many payload bytes per wavefront (~20 KB
+// about this many payload bytes per wavefront (~21.7 KB
 // per wave streams best; per-packet keyring gathers want longer units).
-constexpr uint64_t kUnitBytes = 20000, kUnitBytesMultiPsk = 36000;
+constexpr uint64_t kUnitBytes = 21700, kUnitBytesMultiPsk = 36000;
 constexpr int kWavesPerBlock = kBlock / kWave;
 
 // Per-PSK hash state, derived once per keyring on the GPU (psk_prepare).

@@ -8,7 +8,7 @@
 //   VectorisedXPlusConn.WriteTo               hysteria/xplus.go:86-98
 // for a whole ragged batch of datagrams per launch.
 //
-// One wavefront = one unit of ppw (sqobfs_set_unit_packets; ~20 KB of payload)
+// One wavefront = one unit of ppw (sqobfs_set_unit_packets; ~21.7 KB of payload)
 // consecutive packets, lane l owning packet l; lanes ppw and ppw + 1 hold the
 // packets just after and just before the unit (its boundary neighbours).
 //   1. descriptor  offsets, lengths, salt (obfuscate: the salt array;
@@ -93,11 +93,6 @@ namespace sq {
 #ifndef SQ_KLATE
 #define SQ_KLATE 0
 #endif
-// 1: Salamander keys from lane pairs (sq_hash.h b2_compress_pair) when the
-// unit leaves half the wave for them (ppw < 32).
-#ifndef SQ_HASH2
-#define SQ_HASH2 0
-#endif
 // Flat blocks a unit's block map covers (its role bytes live in LDS).
 #ifndef SQ_MAPBLK
 #define SQ_MAPBLK 4096
@@ -114,7 +109,7 @@ extern "C" const char *sqobfs_build_info(void) {
   return "gfx950 obfs_kernel U=" SQ_STR(SQ_U) " PPW=" SQ_STR(SQ_PPW) " NT=" SQ_STR(SQ_NT)
          " minw=" SQ_STR(SQ_MINW) " block=" SQ_STR(SQ_BLOCK)
          " ablate=" SQ_STR(SQ_ABLATE) " donate=" SQ_STR(SQ_DONATE) " align=" SQ_STR(SQ_ALIGN)
-         " klate=" SQ_STR(SQ_KLATE) " map=" SQ_STR(SQ_MAPBLK) " hash2=" SQ_STR(SQ_HASH2);
+         " klate=" SQ_STR(SQ_KLATE) " map=" SQ_STR(SQ_MAPBLK);
 }
 
 // default unit size (KParams.ppw == 0); any 1 .. kMaxUnitPackets works
@@ -613,28 +608,12 @@ template <int KIND, int DIR, bool MULTI>
 __device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
                                           const uint32_t (&salt)[4], bool do_hash, uint32_t pid,
                                           const Windows &W, bool owner, uint32_t lane,
-                                          uint32_t ppw, const Geo &G, WaveLds &L) {
+                                          const Geo &G, WaveLds &L) {
   constexpr uint32_t S = KIND == 0 ? kSalamanderSalt : kXPlusSalt;
   constexpr uint32_t PW = DIR == 0 ? S / 4 : 0;  // salt words in front of the payload
   uint32_t key[8];
-  if (KIND == 0 && SQ_HASH2 && !(SQ_ABLATE & 1) && ppw + 1 <= kWave / 2) {
-    // lanes 0 .. ppw need keys: hash lanes 2k and 2k + 1 take packet lane k
-    const uint32_t k = lane >> 1;
-    const uint32_t s2[2] = {shfl32(salt[0], k), shfl32(salt[1], k)};
-    const uint32_t pk = MULTI ? shfl32(pid, k) : 0u;
-    uint32_t kw[4];
-    salamander_key_pair(MULTI ? P.psk_table + pk : &P.psk0, s2, lane & 1, kw);
-    const uint32_t le = (2 * lane) & (kWave - 1);
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const uint32_t x = shfl32(kw[j], le), y = shfl32(kw[j], le + 1);
-      key[j] = do_hash ? x : 0u;
-      key[4 + j] = do_hash ? y : 0u;
-    }
-  } else {
-    // single PSK: the kernarg copy (scalar loads); several: the device table
-    derive_key<KIND>(do_hash, MULTI ? P.psk_table + pid : &P.psk0, salt, key);
-  }
+  // single PSK: the kernarg copy (scalar loads); several: the device table
+  derive_key<KIND>(do_hash, MULTI ? P.psk_table + pid : &P.psk0, salt, key);
   const uint64_t rs = G.rs, re = G.re;
   // head image: output bytes [rs, rs + 32) = salt || payload ^ key
   uint32_t hi[8];
@@ -919,7 +898,7 @@ __global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
   SQ_STAMP(2);
   const uint32_t pid = MULTI && d.pid < P.n_psk ? d.pid : 0u;
   // 2 + 3b. key and block contents
-  fill_unit<KIND, DIR, MULTI>(P, J, salt, do_hash, pid, W, owner, lane, ppw, G, L);
+  fill_unit<KIND, DIR, MULTI>(P, J, salt, do_hash, pid, W, owner, lane, G, L);
   SQ_STAMP(3);
   // 4. the stream
   Step<U> cur;

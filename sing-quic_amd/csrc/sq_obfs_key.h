@@ -43,41 +43,4 @@ __device__ __forceinline__ void salamander_key(const PskEntry *E,
   }
 }
 
-// The same key from a lane pair (b2_compress_pair): lanes 2k and 2k + 1
-// both pass packet k's keyring entry and salt; the even lane returns key
-// words 0-3, the odd lane words 4-7.  Every lane must take part.
-__device__ __forceinline__ void salamander_key_pair(const PskEntry *E,
-                                                    const uint32_t (&salt)[2], bool odd,
-                                                    uint32_t (&kw)[4]) {
-  uint64_t hh[4];
-#pragma unroll
-  for (int i = 0; i < 2; i++) {
-    hh[i] = odd ? E->h[2 + i] : E->h[i];
-    hh[2 + i] = odd ? E->h[6 + i] : E->h[4 + i];
-  }
-  const uint32_t nb = E->nblocks, t = E->salt_pos;
-  const uint64_t sv = b2_pack(salt[0], salt[1]);
-  const uint32_t w = t >> 3, sh = (t & 7) * 8;
-  const uint64_t lo = sv << sh;
-  const uint64_t hi = sh ? (sv >> (64 - sh)) : 0ull;
-  for (uint32_t blk = 0; blk < nb; blk++) {
-    uint64_t m[16];
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-      const uint32_t idx = 16 * blk + j;
-      uint64_t x = E->m[idx];
-      x |= (idx == w) ? lo : 0ull;
-      x |= (idx == w + 1) ? hi : 0ull;
-      m[j] = x;
-    }
-    const bool last = blk + 1 == nb;
-    b2_compress_pair(hh, m, last ? E->t_last : E->t_first, last, odd);
-  }
-#pragma unroll
-  for (int i = 0; i < 2; i++) {
-    kw[2 * i] = (uint32_t)hh[i];
-    kw[2 * i + 1] = (uint32_t)(hh[i] >> 32);
-  }
-}
-
 }  // namespace sq
