@@ -2,7 +2,9 @@
 ONE process on ONE buffer set, interleaved rounds, so that box and
 allocation effects cancel, after a 60-launch warm-up (the GPU's first
 ~25 launches of a process run up to 10 % slower).
-usage: unit_sweep.py CONFIG "ppw ..." [ROUNDS] [obfuscate|deobfuscate]"""
+usage: unit_sweep.py CONFIG "ppw ..." [ROUNDS] [obfuscate|deobfuscate]
+A token PPWuU (e.g. 16u6) also sets SQOBFS_DEV_U=U (timing builds with
+SQ_DEVVAR: stream step of U blocks per lane)."""
 import os
 import statistics
 import sys
@@ -61,7 +63,9 @@ for _ in range(60):
 torch.cuda.synchronize()
 for r in range(rounds):
     for w in ppws:
-        ctx.unit_packets = int(w)
+        ppw, _, u = w.partition("u")
+        ctx.unit_packets = int(ppw)
+        os.environ["SQOBFS_DEV_U"] = u or "4"
         res[w].append(round(timed(), 1))
     print(f"round {r} done", flush=True)
 for w in ppws:

@@ -43,6 +43,7 @@
 // splitting wave instructions into 256-byte pieces (16 lanes per packet)
 // costs 40 %.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "sq_bytes.h"
 #include "sq_hash.h"
@@ -96,6 +97,11 @@ namespace sq {
 // Flat blocks a unit's block map covers (its role bytes live in LDS).
 #ifndef SQ_MAPBLK
 #define SQ_MAPBLK 4096
+#endif
+// Timing builds (never shipped): extra kernel instantiations picked at run
+// time by SQOBFS_DEV_* variables, for in-process A/B comparisons.
+#ifndef SQ_DEVVAR
+#define SQ_DEVVAR 0
 #endif
 // Timeline builds (scripts/dev/timeline.py, never shipped): lane 0 of every
 // wave records the constant-rate clock at its phase boundaries.
@@ -1000,6 +1006,30 @@ static int launch_one(const KParams *kp, hipStream_t s) {
   if (P.ppw > kMaxUnitPackets) return -1;
   const uint64_t units = ((uint64_t)P.n + P.ppw - 1) / P.ppw;
   const uint64_t blocks = (units + kWavesPerBlock - 1) / kWavesPerBlock;
+#if SQ_DEVVAR
+  // timing builds only: SQOBFS_DEV_U picks another stream step size for
+  // Salamander obfuscate, single PSK (in-process A/B; SQ_U sizes the slack)
+  if (KIND == 0 && DIR == 0 && !MULTI) {
+    const char *e = getenv("SQOBFS_DEV_U");
+    const int u = e ? atoi(e) : U;
+#define SQ_DEV_U(UU)                                                                       \
+  case UU:                                                                                 \
+    static_assert(UU <= SQ_U, "slack");                                                    \
+    hipLaunchKernelGGL((obfs_kernel<KIND, DIR, MULTI, UU>), dim3((uint32_t)blocks),         \
+                       dim3(kBlock), SQ_LDSPAD, s, P);                                     \
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+    switch (u) {
+      SQ_DEV_U(2)
+      SQ_DEV_U(3)
+      SQ_DEV_U(4)
+      SQ_DEV_U(5)
+      SQ_DEV_U(6)
+      SQ_DEV_U(8)
+      default: break;
+    }
+#undef SQ_DEV_U
+  }
+#endif
   hipLaunchKernelGGL((obfs_kernel<KIND, DIR, MULTI, U>), dim3((uint32_t)blocks), dim3(kBlock),
                      SQ_LDSPAD, s, P);
   return hipGetLastError() == hipSuccess ? 0 : -3;
