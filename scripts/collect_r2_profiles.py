@@ -19,6 +19,24 @@ for d in sorted(glob.glob(os.path.join(src, "*"))):
     st = glob.glob(os.path.join(d, "kt", "**", "*kernel_stats.csv"), recursive=True)
     if st:
         shutil.copy(st[0], os.path.join(dst, f"kernel_stats_{cfg}.csv"))
+    tr = glob.glob(os.path.join(d, "kt", "**", "*kernel_trace.csv"), recursive=True)
+    if tr:
+        # the timed launches are the last `steps` obfs_kernel dispatches (the
+        # kernel-stats average also holds the cold first launches of warm-up)
+        import csv
+        rows = [r for r in csv.DictReader(open(tr[0])) if "obfs_kernel" in r["Kernel_Name"]]
+        rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+        kt = json.loads(open(os.path.join(d, "kt.json")).read().strip().splitlines()[-1])
+        last = rows[-kt["steps"]:]
+        us = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in last]
+        json.dump({"kernel": last[-1]["Kernel_Name"], "dispatches": len(rows),
+                   "timed_dispatches": len(us), "timed_avg_us": round(sum(us) / len(us), 2),
+                   "timed_min_us": round(min(us), 2), "timed_max_us": round(max(us), 2),
+                   "bench_kernel_avg_us_same_run": kt["roofline"]["kernel_avg_us"],
+                   "lds_bytes": last[-1]["LDS_Block_Size"],
+                   "grid": last[-1]["Grid_Size_X"], "workgroup": last[-1]["Workgroup_Size_X"],
+                   "source": "rocprofv3 --kernel-trace --stats (scripts/r2_profile.sh)"},
+                  open(os.path.join(dst, f"kernel_trace_timed_{cfg}.json"), "w"), indent=1)
     summ = os.path.join(d, "summary.json")
     if not os.path.exists(summ):
         continue
