@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <mutex>
 #include <new>
 #include <thread>
@@ -41,6 +42,7 @@ struct sqobfs_ctx {
 
 namespace {
 constexpr uint32_t kHostChunks = 8;  // sqobfs_run_host pipeline depth
+constexpr int kSpinMs = 4;           // sqobfs_sync: poll this long, then block
 // test hook (sqobfs_debug_fail_chunk): the launch of that pipeline chunk
 // fails as a device error would, once
 std::atomic<int> g_fail_chunk{-1};
@@ -309,7 +311,20 @@ int sqobfs_sync(sqobfs_ctx *ctx, void *stream) {
   if (!ctx) return SQ_EINVAL;
   DeviceScope ds_(ctx->device);
   if (ds_.status != SQ_OK) return ds_.status;
-  return hip_status(hipStreamSynchronize(pick_stream(ctx, stream)));
+  hipStream_t s = pick_stream(ctx, stream);
+  // A batch takes about a millisecond: poll for that long before blocking.
+  // hipStreamSynchronize's blocking wake-up left the GPU idle ~80 us between
+  // synchronous batches (bench --inproc 1: 0.56 ms per step against 0.48 ms
+  // for queued launches of the same batch).
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t q = hipStreamQuery(s);
+    if (q == hipSuccess) return SQ_OK;
+    if (q != hipErrorNotReady) return hip_status(q);
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(kSpinMs)) break;
+    __builtin_ia32_pause();
+  }
+  return hip_status(hipStreamSynchronize(s));
 }
 
 int sqobfs_keyring_create(sqobfs_ctx *ctx, int kind, uint32_t count, const uint8_t *blob,
