@@ -3,8 +3,9 @@ ONE process on ONE buffer set, interleaved rounds, so that box and
 allocation effects cancel, after a 60-launch warm-up (the GPU's first
 ~25 launches of a process run up to 10 % slower).
 usage: unit_sweep.py CONFIG "ppw ..." [ROUNDS] [obfuscate|deobfuscate]
-A token PPWuU (e.g. 16u6) also sets SQOBFS_DEV_U=U (timing builds with
-SQ_DEVVAR: stream step of U blocks per lane)."""
+A token PPWuU (e.g. 16u6) also sets SQOBFS_DEV_U=U, and PPWuUlP (16u4l10240)
+SQOBFS_DEV_LDSPAD=P (timing builds with SQ_DEVVAR: stream step of U blocks
+per lane, P bytes of extra LDS per block)."""
 import os
 import statistics
 import sys
@@ -64,8 +65,10 @@ torch.cuda.synchronize()
 for r in range(rounds):
     for w in ppws:
         ppw, _, u = w.partition("u")
+        u, _, pad = u.partition("l")
         ctx.unit_packets = int(ppw)
         os.environ["SQOBFS_DEV_U"] = u or "4"
+        os.environ["SQOBFS_DEV_LDSPAD"] = pad or "0"
         res[w].append(round(timed(), 1))
     print(f"round {r} done", flush=True)
 for w in ppws:

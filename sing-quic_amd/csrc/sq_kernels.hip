@@ -1008,15 +1008,18 @@ static int launch_one(const KParams *kp, hipStream_t s) {
   const uint64_t blocks = (units + kWavesPerBlock - 1) / kWavesPerBlock;
 #if SQ_DEVVAR
   // timing builds only: SQOBFS_DEV_U picks another stream step size for
-  // Salamander obfuscate, single PSK (in-process A/B; SQ_U sizes the slack)
+  // Salamander obfuscate, single PSK (in-process A/B; SQ_U sizes the slack);
+  // SQOBFS_DEV_LDSPAD adds dynamic LDS per block (caps the resident blocks)
   if (KIND == 0 && DIR == 0 && !MULTI) {
     const char *e = getenv("SQOBFS_DEV_U");
     const int u = e ? atoi(e) : U;
+    const char *lp = getenv("SQOBFS_DEV_LDSPAD");
+    const unsigned pad = lp ? (unsigned)atoi(lp) : (unsigned)SQ_LDSPAD;
 #define SQ_DEV_U(UU)                                                                       \
   case UU:                                                                                 \
     static_assert(UU <= SQ_U, "slack");                                                    \
     hipLaunchKernelGGL((obfs_kernel<KIND, DIR, MULTI, UU>), dim3((uint32_t)blocks),         \
-                       dim3(kBlock), SQ_LDSPAD, s, P);                                     \
+                       dim3(kBlock), pad, s, P);                                           \
     return hipGetLastError() == hipSuccess ? 0 : -3;
     switch (u) {
       SQ_DEV_U(2)
