@@ -10,7 +10,6 @@ wave start to the end).  Stamps: 0 start, 1 descriptor, 2 plan, 3 contents
 import ctypes
 import json
 import os
-import re
 import sys
 
 import numpy as np
@@ -41,9 +40,12 @@ def main():
     lib = sqobfs.lib()
     lib.sqobfs_build_info.restype = ctypes.c_char_p
     info = lib.sqobfs_build_info().decode()
-    ppw = int(re.search(r"PPW=(\d+)", info).group(1))
+    # unit size: argv[2], else sized by bytes as bench.py does
+    ctx.unit_packets = (int(sys.argv[2]) if len(sys.argv) > 2 else
+                        sqobfs.unit_packets_for(sh["payload_bytes"], n, n_psk > 1))
+    ppw = ctx.unit_packets
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for _ in range(4):
+    for _ in range(60):  # past the first-launch ramp
         sqobfs.launch(ctx, kr, sqobfs.OBFUSCATE, b, s)
     e0.record()
     sqobfs.launch(ctx, kr, sqobfs.OBFUSCATE, b, s)
@@ -62,7 +64,7 @@ def main():
     t = (t - t0) * tick_us
     ph = np.diff(t, axis=1)
     names = ["desc", "plan", "contents", "stream", "drain"]
-    out = {"build": info, "config": cfg, "kernel_us": round(us, 1),
+    out = {"build": info, "config": cfg, "unit_packets": ppw, "kernel_us": round(us, 1),
            "tick_ns": round(tick_us * 1e3, 3), "waves": units}
     out["phase_us"] = {nm: {"p10": round(float(np.percentile(ph[:, i], 10)), 2),
                             "median": round(float(np.median(ph[:, i])), 2),

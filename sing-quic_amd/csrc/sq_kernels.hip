@@ -1017,10 +1017,12 @@ static int launch_one(const KParams *kp, hipStream_t s) {
     const unsigned pad = lp ? (unsigned)atoi(lp) : (unsigned)SQ_LDSPAD;
 #define SQ_DEV_U(UU)                                                                       \
   case UU:                                                                                 \
-    static_assert(UU <= SQ_U, "slack");                                                    \
-    hipLaunchKernelGGL((obfs_kernel<KIND, DIR, MULTI, UU>), dim3((uint32_t)blocks),         \
-                       dim3(kBlock), pad, s, P);                                           \
-    return hipGetLastError() == hipSuccess ? 0 : -3;
+    if constexpr (UU <= SQ_U) { /* the role map's slack covers SQ_U */                     \
+      hipLaunchKernelGGL((obfs_kernel<KIND, DIR, MULTI, UU>), dim3((uint32_t)blocks),       \
+                         dim3(kBlock), pad, s, P);                                         \
+      return hipGetLastError() == hipSuccess ? 0 : -3;                                     \
+    }                                                                                      \
+    break;
     switch (u) {
       SQ_DEV_U(2)
       SQ_DEV_U(3)

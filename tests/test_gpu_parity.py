@@ -175,6 +175,23 @@ def test_jumbo_units(ctx, kind, direction):
 
 @pytest.mark.parametrize("kind", KINDS)
 @pytest.mark.parametrize("direction", DIRS)
+def test_single_psk_lengths(ctx, kind, direction):
+    """One-entry keyrings (no psk_id: the single-PSK kernels, whose BLAKE2b
+    is specialised on the salt's message word) for PSK lengths that put the
+    salt at every word position of a one-block final message, across the
+    one/two-block boundary (PSK tail 120 / 121 / 127 B) and past whole
+    blocks."""
+    rng = np.random.Generator(np.random.PCG64(950 + 10 * kind + direction))
+    lens = np.concatenate([np.arange(0, 24), rng.integers(0, 1500, 120)])
+    for k in list(range(0, 136, 3)) + [119, 120, 121, 122, 126, 127, 128, 129,
+                                       247, 248, 249, 255, 256, 300]:
+        psk = rng.integers(0, 256, k, dtype=np.uint8).tobytes()
+        hb = gh.make_case(rng, kind, direction, lens, [psk], in_align=4, out_lead=8)
+        check(ctx, kind, direction, [psk], hb, f"{kind}/{direction}/psk{k}")
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("direction", DIRS)
 def test_unit_sizes(ctx, kind, direction):
     """Every unit size gives the same bytes (sqobfs_set_unit_packets): unit
     boundaries, donation and the neighbour lanes move with it.  Ragged and
