@@ -3,10 +3,12 @@ ONE process on ONE buffer set, interleaved rounds, so that box and
 allocation effects cancel, after a 60-launch warm-up (the GPU's first
 ~25 launches of a process run up to 10 % slower).
 usage: unit_sweep.py CONFIG "ppw ..." [ROUNDS] [obfuscate|deobfuscate]
-A token PPWuU (e.g. 16u6) also sets SQOBFS_DEV_U=U, and PPWuUlP (16u4l10240)
-SQOBFS_DEV_LDSPAD=P (timing builds with SQ_DEVVAR: stream step of U blocks
-per lane, P bytes of extra LDS per block)."""
+Tokens PPW[uU][lP][wW] (e.g. 16u6, 16u4l10240, 16w1) also set
+SQOBFS_DEV_U=U, SQOBFS_DEV_LDSPAD=P and SQOBFS_DEV_WPB=W (timing builds with
+SQ_DEVVAR: stream step of U blocks per lane, P bytes of extra LDS per
+workgroup, W waves per workgroup)."""
 import os
+import re
 import statistics
 import sys
 
@@ -64,11 +66,11 @@ for _ in range(60):
 torch.cuda.synchronize()
 for r in range(rounds):
     for w in ppws:
-        ppw, _, u = w.partition("u")
-        u, _, pad = u.partition("l")
-        ctx.unit_packets = int(ppw)
-        os.environ["SQOBFS_DEV_U"] = u or "4"
-        os.environ["SQOBFS_DEV_LDSPAD"] = pad or "0"
+        m = re.fullmatch(r"(\d+)(?:u(\d+))?(?:l(\d+))?(?:w(\d+))?", w)
+        ctx.unit_packets = int(m.group(1))
+        os.environ["SQOBFS_DEV_U"] = m.group(2) or "4"
+        os.environ["SQOBFS_DEV_LDSPAD"] = m.group(3) or "0"
+        os.environ["SQOBFS_DEV_WPB"] = m.group(4) or "0"
         res[w].append(round(timed(), 1))
     print(f"round {r} done", flush=True)
 for w in ppws:

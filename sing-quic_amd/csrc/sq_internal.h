@@ -9,10 +9,6 @@ namespace sq {
 constexpr int kSalamanderSalt = 8;  // hysteria2/salamander.go:15
 constexpr int kXPlusSalt = 16;      // hysteria/xplus.go:17
 constexpr int kWave = 64;           // CDNA wavefront
-#ifndef SQ_BLOCK
-#define SQ_BLOCK 256
-#endif
-constexpr int kBlock = SQ_BLOCK;    // 4 waves per workgroup
 // Obfuscation kernel unit: packets per wavefront (sqobfs_set_unit_packets);
 // two more lanes hold the unit's neighbour packets.
 #ifndef SQ_PPW
@@ -24,7 +20,6 @@ constexpr uint32_t kMaxUnitPackets = 62;
 // about this many payload bytes per wavefront (~21.7 KB
 // per wave streams best; per-packet keyring gathers want longer units).
 constexpr uint64_t kUnitBytes = 21700, kUnitBytesMultiPsk = 36000;
-constexpr int kWavesPerBlock = kBlock / kWave;
 
 // Per-PSK hash state, derived once per keyring on the GPU (psk_prepare).
 //

@@ -113,7 +113,7 @@ namespace sq {
 #define SQ_STR(x) SQ_STR2(x)
 extern "C" const char *sqobfs_build_info(void) {
   return "gfx950 obfs_kernel U=" SQ_STR(SQ_U) " PPW=" SQ_STR(SQ_PPW) " NT=" SQ_STR(SQ_NT)
-         " minw=" SQ_STR(SQ_MINW) " block=" SQ_STR(SQ_BLOCK)
+         " minw=" SQ_STR(SQ_MINW) " wpb=2"
          " ablate=" SQ_STR(SQ_ABLATE) " donate=" SQ_STR(SQ_DONATE) " align=" SQ_STR(SQ_ALIGN)
          " klate=" SQ_STR(SQ_KLATE) " map=" SQ_STR(SQ_MAPBLK);
 }
@@ -867,16 +867,17 @@ __device__ __noinline__ void stream_generic(const WaveLds &L, uint32_t cst, uint
 
 // ------------------------------------------------------------ the kernel
 
-template <int KIND, int DIR, bool MULTI, int U>
+// WPB: wavefronts per workgroup (independent units; they share nothing).
+template <int KIND, int DIR, bool MULTI, int U, int WPB>
 #if SQ_MINW
-__global__ __launch_bounds__(kBlock, SQ_MINW) void obfs_kernel(const KParams P) {
+__global__ __launch_bounds__(WPB * kWave, SQ_MINW) void obfs_kernel(const KParams P) {
 #else
-__global__ __launch_bounds__(kBlock) void obfs_kernel(const KParams P) {
+__global__ __launch_bounds__(WPB * kWave) void obfs_kernel(const KParams P) {
 #endif
-  __shared__ WaveLds lds[kWavesPerBlock];
+  __shared__ WaveLds lds[WPB];
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wv = threadIdx.x / kWave;
-  const uint64_t unit = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
+  const uint64_t unit = (uint64_t)blockIdx.x * WPB + wv;
   const uint32_t ppw = P.ppw;
   const uint64_t first = unit * ppw;
   if (first >= P.n) return;
@@ -998,46 +999,67 @@ __global__ void psk_prepare_kernel(int kind, const uint8_t *blob, const uint64_t
   out[k] = E;
 }
 
+// Wavefronts per workgroup.  A workgroup's slots are released only when all
+// of its waves have ended, so a 4-wave group holds its finished waves' slots
+// until its slowest sibling is done; 1-wave groups avoid that but leave the
+// wave-to-SIMD placement to the dispatcher.  Measured per kernel in one
+// process: 2-wave groups are the fastest or within
+// 1.5 % of it for every kernel and direction (Salamander obfuscate 2.6 %
+// faster than 4-wave groups, XPlus obfuscate 3.4 % faster than 1-wave ones).
+template <int KIND, int DIR>
+constexpr int kWavesPerGroup = 2;
+
+template <int KIND, int DIR, bool MULTI, int U, int WPB>
+static int launch_k(const KParams &P, uint32_t pad, hipStream_t s) {
+  const uint64_t units = ((uint64_t)P.n + P.ppw - 1) / P.ppw;
+  const uint64_t blocks = (units + WPB - 1) / WPB;
+  hipLaunchKernelGGL((obfs_kernel<KIND, DIR, MULTI, U, WPB>), dim3((uint32_t)blocks),
+                     dim3(WPB * kWave), pad, s, P);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
 template <int KIND, int DIR, bool MULTI>
 static int launch_one(const KParams *kp, hipStream_t s) {
   constexpr int U = SQ_U;
   KParams P = *kp;
   if (P.ppw == 0) P.ppw = kPktPerWave;
   if (P.ppw > kMaxUnitPackets) return -1;
-  const uint64_t units = ((uint64_t)P.n + P.ppw - 1) / P.ppw;
-  const uint64_t blocks = (units + kWavesPerBlock - 1) / kWavesPerBlock;
 #if SQ_DEVVAR
-  // timing builds only: SQOBFS_DEV_U picks another stream step size for
-  // Salamander obfuscate, single PSK (in-process A/B; SQ_U sizes the slack);
-  // SQOBFS_DEV_LDSPAD adds dynamic LDS per block (caps the resident blocks)
-  if (KIND == 0 && DIR == 0 && !MULTI) {
-    const char *e = getenv("SQOBFS_DEV_U");
-    const int u = e ? atoi(e) : U;
+  // timing builds only, for in-process A/B: SQOBFS_DEV_WPB = 1 / 2 / 4 waves
+  // per workgroup (any kernel); SQOBFS_DEV_U another stream step size and
+  // SQOBFS_DEV_LDSPAD dynamic LDS per workgroup (caps the resident groups),
+  // both for Salamander obfuscate, single PSK (SQ_U sizes the map's slack)
+  {
+    const char *ew = getenv("SQOBFS_DEV_WPB");
+    const int wpb = ew ? atoi(ew) : 0;
     const char *lp = getenv("SQOBFS_DEV_LDSPAD");
-    const unsigned pad = lp ? (unsigned)atoi(lp) : (unsigned)SQ_LDSPAD;
-#define SQ_DEV_U(UU)                                                                       \
-  case UU:                                                                                 \
-    if constexpr (UU <= SQ_U) { /* the role map's slack covers SQ_U */                     \
-      hipLaunchKernelGGL((obfs_kernel<KIND, DIR, MULTI, UU>), dim3((uint32_t)blocks),       \
-                         dim3(kBlock), pad, s, P);                                         \
-      return hipGetLastError() == hipSuccess ? 0 : -3;                                     \
-    }                                                                                      \
+    const uint32_t pad = lp ? (uint32_t)atoi(lp) : (uint32_t)SQ_LDSPAD;
+    if (wpb == 1) return launch_k<KIND, DIR, MULTI, U, 1>(P, pad, s);
+    if (wpb == 2) return launch_k<KIND, DIR, MULTI, U, 2>(P, pad, s);
+    if (wpb == 4) return launch_k<KIND, DIR, MULTI, U, 4>(P, pad, s);
+    if (KIND == 0 && DIR == 0 && !MULTI) {
+      const char *e = getenv("SQOBFS_DEV_U");
+      const int u = e ? atoi(e) : U;
+      constexpr int W = kWavesPerGroup<KIND, DIR>;
+#define SQ_DEV_U(UU)                                                          \
+  case UU:                                                                    \
+    if constexpr (UU <= SQ_U) /* the role map's slack covers SQ_U */          \
+      return launch_k<KIND, DIR, MULTI, UU, W>(P, pad, s);                    \
     break;
-    switch (u) {
-      SQ_DEV_U(2)
-      SQ_DEV_U(3)
-      SQ_DEV_U(4)
-      SQ_DEV_U(5)
-      SQ_DEV_U(6)
-      SQ_DEV_U(8)
-      default: break;
-    }
+      switch (u) {
+        SQ_DEV_U(2)
+        SQ_DEV_U(3)
+        SQ_DEV_U(5)
+        SQ_DEV_U(6)
+        SQ_DEV_U(8)
+        default: break;
+      }
 #undef SQ_DEV_U
+    }
+    return launch_k<KIND, DIR, MULTI, U, kWavesPerGroup<KIND, DIR>>(P, pad, s);
   }
 #endif
-  hipLaunchKernelGGL((obfs_kernel<KIND, DIR, MULTI, U>), dim3((uint32_t)blocks), dim3(kBlock),
-                     SQ_LDSPAD, s, P);
-  return hipGetLastError() == hipSuccess ? 0 : -3;
+  return launch_k<KIND, DIR, MULTI, U, kWavesPerGroup<KIND, DIR>>(P, SQ_LDSPAD, s);
 }
 
 }  // namespace sq
