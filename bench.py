@@ -655,6 +655,19 @@ def e2e_rate(torch, sqobfs, ctx, kr, kind, n, L):
     return res
 
 
+def warm_up(torch, dev, call, seconds: float = 0.15, least: int = 2) -> int:
+    """Untimed launches for at least `seconds` of wall time (a fresh process's
+    first launches run slower); returns the count."""
+    k, t0 = 0, time.perf_counter()
+    while k < least or time.perf_counter() - t0 < seconds:
+        call()
+        k += 1
+        if k % 4 == 0:
+            torch.cuda.synchronize(dev)
+    torch.cuda.synchronize(dev)
+    return k
+
+
 def quic_rate(torch, sqobfs, ctx, dev, steps, n=1 << 20, payload=1350, cpu_seconds=2.0,
               suite=0):
     """QUIC 1-RTT packet protection: seal and open
@@ -702,8 +715,7 @@ def quic_rate(torch, sqobfs, ctx, dev, steps, n=1 << 20, payload=1350, cpu_secon
                                pn_out=pn_out)
         for name, fn, b, alg in (("seal", sqobfs.quic_seal, bs, n * (2 * ln + 16)),
                                  ("open", sqobfs.quic_open, bo, n * (2 * ln + 16))):
-            for _ in range(2):
-                fn(ctx, kr, b, s)
+            warm_up(torch, dev, lambda: fn(ctx, kr, b, s))
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                   for _ in range(steps)]
             for e0, e1 in ev:
@@ -830,8 +842,7 @@ def quic_fused_rate(torch, sqobfs, ctx, dev, steps, n, ln, data, in_off, lens, p
         b_fopen = sqobfs.quic_batch(n, wire1, w_off, wlens, opened, in_off, o5, pno, largest)
 
         def timed(fn):
-            for _ in range(2):
-                fn()
+            warm_up(torch, dev, fn)
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                   for _ in range(steps)]
             for e0, e1 in ev:

@@ -188,12 +188,14 @@ def test_open_rejects_write_pn_out_zero(ctx, suite):
 
 
 def test_long_payloads_owner_path(ctx):
-    """Payloads either side of the cooperative limit (2,048 B), walked by the
-    owner lane above it, mixed in one batch with short packets."""
+    """Payloads either side of the cooperative limit (1,536 B; 2,048 B before),
+    walked by the owner lane above it, mixed in one batch with short
+    packets."""
     rng = np.random.Generator(np.random.PCG64(991))
     kb = tuple(rng.integers(0, 256, m, dtype=np.uint8).tobytes() for m in (32, 12, 32))
     pkts, pnos, pns = [], [], []
-    for plen in [2030, 2047, 2048, 2049, 2050, 2064, 3000, 9000, 65, 2, 4000, 1350]:
+    for plen in [1500, 1535, 1536, 1537, 1538, 1552, 2030, 2047, 2048, 2049, 2050, 2064,
+                 3000, 9000, 65, 2, 4000, 1350]:
         pn_len = 2
         pkt = bytes([0x41]) + bytes(8) + (7).to_bytes(pn_len, "big") + \
             rng.integers(0, 256, plen, dtype=np.uint8).tobytes()

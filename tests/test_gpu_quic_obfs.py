@@ -141,7 +141,7 @@ def test_long_payloads_and_rejects(ctx, suite):  # noqa: F811
     kb, keys = _keys(rng, 1, suite)
     pkts = [bytes([0x41]) + bytes(8) + (7).to_bytes(2, "big") +
             rng.integers(0, 256, plen, dtype=np.uint8).tobytes()
-            for plen in [2047, 2048, 2049, 3000, 9000, 65, 2, 1350]]
+            for plen in [1535, 1536, 1537, 2047, 2048, 2049, 3000, 9000, 65, 2, 1350]]
     pnos, pns = [9] * len(pkts), [7] * len(pkts)
     salts = [rng.integers(0, 256, 8, dtype=np.uint8).tobytes() for _ in pkts]
     with sqobfs.Keyring(ctx, sqobfs.SALAMANDER, [PSK]) as kr_o:
