@@ -14,7 +14,6 @@ import (
 	"github.com/sagernet/sing/common/buf"
 	"github.com/sagernet/sing/common/bufio"
 	M "github.com/sagernet/sing/common/metadata"
-	N "github.com/sagernet/sing/common/network"
 )
 
 const xplusSaltLen = 16 // xplus.go:17
@@ -29,26 +28,26 @@ func NewXPlusPacketConn(conn net.PacketConn, key []byte) net.PacketConn {
 	if err != nil {
 		panic("sqobfs: " + err.Error())
 	}
-	if writer, isVectorised := bufio.CreateVectorisedPacketWriter(conn); isVectorised {
-		return &VectorisedXPlusConn{Conn: c, writer: writer}
+	if _, isVectorised := bufio.CreateVectorisedPacketWriter(conn); isVectorised {
+		return &VectorisedXPlusConn{Conn: c} // the engine sends: no inner writer kept
 	}
 	return c
 }
 
 // VectorisedXPlusConn: xplus.go:81-118 (one running keystream over the
-// buffers, as :108-115).
+// buffers, as :108-115).  WriteTo copies p (xplus.go:94-96 XORs it in place).
 type VectorisedXPlusConn struct {
 	*sqobfs.Conn
-	writer N.VectorisedPacketWriter
 }
 
 func (v *VectorisedXPlusConn) WriteVectorisedPacket(buffers []*buf.Buffer,
 	destination M.Socksaddr) error {
 	defer buf.ReleaseMulti(buffers)
-	p := make([]byte, 0, buf.LenMulti(buffers))
+	p := buf.NewSize(buf.LenMulti(buffers))
+	defer p.Release()
 	for _, b := range buffers {
-		p = append(p, b.Bytes()...)
+		_, _ = p.Write(b.Bytes())
 	}
-	_, err := v.Conn.WriteTo(p, destination.UDPAddr())
+	_, err := v.Conn.WriteTo(p.Bytes(), destination.UDPAddr())
 	return err
 }

@@ -5,8 +5,8 @@
 // with the same exported names and signatures, so the construction sites
 // (hysteria2/client.go:133-135, hysteria2/service.go:118-120) compile
 // unchanged.  Byte work: libsqobfs on the GPU, batched (go/sqobfs).
-// Uncompiled here (no Go toolchain in this image); the C call sequence is
-// replayed by tests/cpp/test_cgo_sequence.c.
+// Uncompiled here (no Go toolchain in this image); the engine under
+// sqobfs.Conn is tested natively by tests/cpp/test_pconn.c.
 package hysteria2
 
 import (
@@ -16,7 +16,6 @@ import (
 	"github.com/sagernet/sing/common/buf"
 	"github.com/sagernet/sing/common/bufio"
 	M "github.com/sagernet/sing/common/metadata"
-	N "github.com/sagernet/sing/common/network"
 )
 
 const salamanderSaltLen = 8 // salamander.go:15
@@ -33,29 +32,34 @@ func NewSalamanderConn(conn net.PacketConn, password []byte) net.PacketConn {
 	if err != nil {
 		panic("sqobfs: " + err.Error())
 	}
-	if writer, isVectorised := bufio.CreateVectorisedPacketWriter(conn); isVectorised {
-		return &VectorisedSalamanderPacketConn{Conn: c, writer: writer}
+	if _, isVectorised := bufio.CreateVectorisedPacketWriter(conn); isVectorised {
+		// the reference keeps the inner vectorised writer (salamander.go:25-
+		// 33); here the engine sends, so only the method set is kept
+		return &VectorisedSalamanderPacketConn{Conn: c}
 	}
 	return c
 }
 
-// VectorisedSalamanderPacketConn: salamander.go:76-109.
+// VectorisedSalamanderPacketConn: salamander.go:76-109.  Its WriteTo is
+// sqobfs.Conn's, which copies p instead of XORing it in place
+// (salamander.go:85-87 mutates the caller's p; callers do not read it back).
 type VectorisedSalamanderPacketConn struct {
 	*sqobfs.Conn
-	writer N.VectorisedPacketWriter
 }
 
 // WriteVectorisedPacket obfuscates the concatenation of buffers under one
 // key: the intent of salamander.go:95-109 (its line 104 mis-indexes any
-// buffer after the first; XPlus's xplus.go:100-118 does it right).
+// buffer after the first; XPlus's xplus.go:100-118 does it right).  The
+// buffers are gathered into a pooled buffer; WriteTo copies it into the
+// transmit batch.
 func (v *VectorisedSalamanderPacketConn) WriteVectorisedPacket(buffers []*buf.Buffer,
 	destination M.Socksaddr) error {
 	defer buf.ReleaseMulti(buffers)
-	n := buf.LenMulti(buffers)
-	p := make([]byte, 0, n)
+	p := buf.NewSize(buf.LenMulti(buffers))
+	defer p.Release()
 	for _, b := range buffers {
-		p = append(p, b.Bytes()...)
+		_, _ = p.Write(b.Bytes())
 	}
-	_, err := v.Conn.WriteTo(p, destination.UDPAddr())
+	_, err := v.Conn.WriteTo(p.Bytes(), destination.UDPAddr())
 	return err
 }

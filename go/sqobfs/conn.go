@@ -2,53 +2,60 @@
 
 package sqobfs
 
+/*
+#include <stdlib.h>
+#include "sqobfs.h"
+*/
+import "C"
+
 import (
 	"errors"
 	"net"
+	"net/netip"
 	"os"
 	"sync"
 	"sync/atomic"
+	"syscall"
 	"time"
+	"unsafe"
 )
 
 // Options of a Conn.
 type Options struct {
 	Device    int           // GPU
-	Batch     int           // datagrams per launch (default 256)
+	Batch     int           // datagrams per launch at most (default 256)
 	SlotBytes int           // per-datagram slot (default 2048, hop.go:19)
-	Linger    time.Duration // longest a datagram waits for its batch (default 50us)
-}
-
-func (o *Options) defaults() {
-	if o.Batch <= 0 {
-		o.Batch = 256
-	}
-	if o.SlotBytes <= 0 {
-		o.SlotBytes = 2048
-	}
-	if o.Linger <= 0 {
-		o.Linger = 50 * time.Microsecond
-	}
+	Linger    time.Duration // an idle GPU waits this long for a batch to grow (default 0)
+	Pump      bool          // move datagrams through the wrapped conn even when it is a *net.UDPConn
 }
 
 // Conn is the obfuscating net.PacketConn of SalamanderPacketConn
 // (hysteria2/salamander.go:19-74) and XPlusPacketConn (hysteria/xplus.go:39-79)
-// with the byte work batched onto the GPU:
+// with the byte work batched onto the GPU by the engine of include/sqobfs.h
+// (sqobfs_pconn_*; its behaviour is tested natively by tests/cpp/test_pconn.c):
 //
-//   - WriteTo (salamander.go:57-70, xplus.go:62-75) copies the payload into
-//     the transmit batch being filled and returns; a flusher obfuscates the
-//     batch in ONE launch (salts generated on the GPU) as soon as it is full
-//     or Linger after its first datagram, then writes the datagrams to the
-//     wrapped conn in order.  An error of those writes is returned by the
-//     next WriteTo (UDP is best-effort; quic-go reuses p after WriteTo, so p
-//     is always copied).
-//   - ReadFrom (salamander.go:42-55, xplus.go:46-60) is fed by a reader
-//     goroutine that drains the wrapped conn into receive batches and
-//     de-obfuscates each batch in ONE launch.  Returned lengths follow the
-//     reference exactly (Salamander n <= 8 returns the raw datagram; XPlus
-//     n < 16 returns 0).  Not reproduced: XPlus's ReadFrom also XORs p past
-//     the returned length up to len(p) (xplus.go:55), garbage bytes no
-//     caller reads; the C ABI reproduces it (in_cap) when asked.
+//   - WriteTo (salamander.go:57-70, xplus.go:62-75) copies p into the transmit
+//     batch being filled and returns (p is never mutated, also not by the
+//     vectorised variants, unlike salamander.go:85-87); the engine obfuscates
+//     the batch in ONE launch (salts from the GPU's generator) as soon as it
+//     is idle and sends it.  A send error is returned by the next WriteTo.
+//   - ReadFrom (salamander.go:42-55, xplus.go:46-60) returns the next datagram
+//     of a batch the engine received and de-obfuscated in ONE launch, with
+//     the reference's lengths: for a datagram of w bytes and m = min(w,
+//     len(p)), Salamander returns the m raw bytes if m <= 8, else the first
+//     m - 8 payload bytes; XPlus returns 0 if m < 16, else m - 16 bytes.  Not
+//     reproduced: XPlus's ReadFrom also XORs p past the returned length up to
+//     len(p) (xplus.go:55), bytes no caller reads.
+//   - SetDeadline / SetReadDeadline / SetWriteDeadline apply to these calls
+//     (a blocked ReadFrom returns os.ErrDeadlineExceeded when its deadline
+//     passes), not to the wrapped conn, which the engine drives itself.
+//   - Close sends what was written, then fails every blocked call with
+//     net.ErrClosed and frees the engine.
+//
+// When the wrapped conn is a *net.UDPConn the engine works its socket with
+// recvmmsg / sendmmsg (socket mode, SURVEY.md 8(f) rank 1).  Any other
+// PacketConn (HopPacketConn, a test double) is driven by two goroutines
+// that feed the engine (pump mode).
 type Conn struct {
 	net.PacketConn
 	kind Kind
@@ -56,44 +63,41 @@ type Conn struct {
 	kr   *Keyring
 	opt  Options
 
-	txMu    sync.Mutex
-	txFill  *Slots
-	txAddr  []net.Addr
-	txN     int
-	txFirst time.Time
-	txFree  chan *Slots
-	txWork  chan txJob
-	txErr   atomic.Value // error
-
-	rx     chan rxItem
-	rxErr  atomic.Value // error
-	closed chan struct{}
+	mu     sync.RWMutex // RLock: a call on pc is in progress; Lock: pc is freed
+	pc     *C.sqobfs_pconn
+	closed atomic.Bool
 	once   sync.Once
-	wg     sync.WaitGroup
+	cerr   error
+
+	socket bool
+	wg     sync.WaitGroup // pump goroutines
+	addrMu sync.Mutex     // pump: the net.Addr of every datagram in flight
+	addrs  map[uint64]net.Addr
+	tag    uint64
+	errMu  sync.Mutex
+	txErr  error // pump: the wrapped conn's write error, for the next WriteTo
+	rxErr  error // pump: the wrapped conn's read error (SQ_EIO)
 }
 
-type txJob struct {
-	s    *Slots
-	addr []net.Addr
-	n    int
+func (c *Conn) setErr(dst *error, e error) {
+	c.errMu.Lock()
+	*dst = e
+	c.errMu.Unlock()
 }
 
-type rxItem struct {
-	s    *rxBatch
-	i    int
-	addr net.Addr
-}
-
-type rxBatch struct {
-	s    *Slots
-	left int32 // datagrams not yet consumed
-	free chan *rxBatch
+func (c *Conn) getErr(src *error, clear bool) error {
+	c.errMu.Lock()
+	defer c.errMu.Unlock()
+	e := *src
+	if clear {
+		*src = nil
+	}
+	return e
 }
 
 // NewConn wraps conn; psk is the password (Salamander) or key (XPlus).
 func NewConn(conn net.PacketConn, kind Kind, psk []byte, opt Options) (*Conn, error) {
-	opt.defaults()
-	ctx, err := Open(opt.Device)
+	ctx, err := Shared(opt.Device)
 	if err != nil {
 		return nil, err
 	}
@@ -102,191 +106,313 @@ func NewConn(conn net.PacketConn, kind Kind, psk []byte, opt Options) (*Conn, er
 		ctx.Close()
 		return nil, err
 	}
-	c := &Conn{PacketConn: conn, kind: kind, ctx: ctx, kr: kr, opt: opt,
-		txFree: make(chan *Slots, 2), txWork: make(chan txJob, 2),
-		rx: make(chan rxItem, 4*opt.Batch), closed: make(chan struct{})}
-	for i := 0; i < 2; i++ {
-		s, err := ctx.NewSlots(opt.Batch, opt.SlotBytes, kind.SaltLen())
-		if err != nil {
-			c.free()
-			return nil, err
+	c := &Conn{PacketConn: conn, kind: kind, ctx: ctx, kr: kr, opt: opt}
+	var o C.sqobfs_pconn_opts
+	o.batch = C.uint32_t(opt.Batch)
+	o.slot_bytes = C.uint32_t(opt.SlotBytes)
+	o.linger_us = C.uint32_t(opt.Linger / time.Microsecond)
+	st := C.int(C.SQ_EINVAL)
+	if uc, ok := conn.(*net.UDPConn); ok && !opt.Pump {
+		// socket mode: the engine dup()s the fd inside Control, so it never
+		// uses a descriptor the runtime may have closed
+		if raw, e := uc.SyscallConn(); e == nil {
+			_ = raw.Control(func(fd uintptr) {
+				st = C.sqobfs_pconn_open(ctx.c, kr.kr, C.int(fd), &o, &c.pc)
+			})
+			c.socket = st == C.SQ_OK
 		}
-		c.txFree <- s
 	}
-	rxFree := make(chan *rxBatch, 3)
-	for i := 0; i < 3; i++ {
-		s, err := ctx.NewSlots(opt.Batch, opt.SlotBytes, kind.SaltLen())
-		if err != nil {
-			c.free()
-			return nil, err
-		}
-		rxFree <- &rxBatch{s: s, free: rxFree}
+	if !c.socket {
+		c.addrs = map[uint64]net.Addr{}
+		st = C.sqobfs_pconn_open(ctx.c, kr.kr, -1, &o, &c.pc)
 	}
-	c.wg.Add(2)
-	go c.flusher()
-	go c.reader(rxFree)
+	if err := check(st); err != nil {
+		kr.Close()
+		ctx.Close()
+		return nil, err
+	}
+	if !c.socket {
+		c.wg.Add(2)
+		go c.pumpRx()
+		go c.pumpTx()
+	}
 	return c, nil
 }
 
-// ---- transmit
+// ---- errors
 
+func (c *Conn) opErr(op string, st C.int, addr net.Addr) error {
+	var e error
+	switch {
+	case st == C.SQ_ETIMEDOUT:
+		e = os.ErrDeadlineExceeded
+	case st == C.SQ_ECLOSED:
+		e = net.ErrClosed
+	case st == C.SQ_EIO:
+		if x := c.getErr(&c.rxErr, false); x != nil {
+			return x // the wrapped conn's own error, verbatim (salamander.go:43-46)
+		}
+		e = Error(st)
+	case st <= -1000:
+		e = os.NewSyscallError(op, syscall.Errno(-1000-int(st)))
+	default:
+		e = Error(st)
+	}
+	return &net.OpError{Op: op, Net: "udp", Source: c.LocalAddr(), Addr: addr, Err: e}
+}
+
+// ---- addresses
+
+func toCAddr(a net.Addr) (C.sqobfs_addr, bool) {
+	var ca C.sqobfs_addr
+	var ap netip.AddrPort
+	switch x := a.(type) {
+	case *net.UDPAddr:
+		ap = x.AddrPort()
+	default:
+		p, err := netip.ParseAddrPort(a.String())
+		if err != nil {
+			return ca, false
+		}
+		ap = p
+	}
+	ip := ap.Addr()
+	ca.port = C.uint16_t(ap.Port())
+	if ip.Is4() || ip.Is4In6() {
+		ca.family = C.uint16_t(syscall.AF_INET)
+		b := ip.Unmap().As4()
+		for i := 0; i < 4; i++ {
+			ca.addr[i] = C.uint8_t(b[i])
+		}
+	} else {
+		ca.family = C.uint16_t(syscall.AF_INET6)
+		b := ip.As16()
+		for i := 0; i < 16; i++ {
+			ca.addr[i] = C.uint8_t(b[i])
+		}
+		if z := ip.Zone(); z != "" {
+			if ifi, err := net.InterfaceByName(z); err == nil {
+				ca.scope_id = C.uint32_t(ifi.Index)
+			}
+		}
+	}
+	return ca, true
+}
+
+func fromCAddr(ca *C.sqobfs_addr) net.Addr {
+	if ca.family == C.uint16_t(syscall.AF_INET6) {
+		var b [16]byte
+		for i := range b {
+			b[i] = byte(ca.addr[i])
+		}
+		ua := &net.UDPAddr{IP: net.IP(b[:]), Port: int(ca.port)}
+		if ca.scope_id != 0 {
+			if ifi, err := net.InterfaceByIndex(int(ca.scope_id)); err == nil {
+				ua.Zone = ifi.Name
+			}
+		}
+		return ua
+	}
+	return &net.UDPAddr{IP: net.IPv4(byte(ca.addr[0]), byte(ca.addr[1]), byte(ca.addr[2]),
+		byte(ca.addr[3])), Port: int(ca.port)}
+}
+
+func (c *Conn) putAddr(a net.Addr) uint64 {
+	c.addrMu.Lock()
+	c.tag++
+	t := c.tag
+	c.addrs[t] = a
+	c.addrMu.Unlock()
+	return t
+}
+
+func (c *Conn) takeAddr(t uint64) net.Addr {
+	c.addrMu.Lock()
+	a := c.addrs[t]
+	delete(c.addrs, t)
+	c.addrMu.Unlock()
+	return a
+}
+
+func bytePtr(p []byte) *C.uint8_t {
+	if len(p) == 0 {
+		return nil
+	}
+	return (*C.uint8_t)(unsafe.Pointer(&p[0]))
+}
+
+// ---- net.PacketConn
+
+// WriteTo returns len(p) for Salamander (salamander.go:69) and len(p) + 16
+// for XPlus (xplus.go:74 returns the inner write's n).
 func (c *Conn) WriteTo(p []byte, addr net.Addr) (int, error) {
-	if e, _ := c.txErr.Load().(error); e != nil {
+	if e := c.getErr(&c.txErr, true); e != nil {
 		return 0, e
 	}
-	S := c.kind.SaltLen()
-	if len(p)+S > c.opt.SlotBytes {
-		return 0, errors.New("sqobfs: datagram larger than the slot")
+	c.mu.RLock()
+	defer c.mu.RUnlock()
+	if c.pc == nil {
+		return 0, c.opErr("write", C.SQ_ECLOSED, addr)
 	}
-	c.txMu.Lock()
-	if c.txFill == nil {
-		select {
-		case c.txFill = <-c.txFree:
-		case <-c.closed:
-			c.txMu.Unlock()
-			return 0, net.ErrClosed
+	var st C.int
+	if c.socket {
+		ca, ok := toCAddr(addr)
+		if !ok {
+			return 0, &net.OpError{Op: "write", Net: "udp", Addr: addr,
+				Err: errors.New("sqobfs: not a UDP address")}
 		}
-		c.txN = 0
-		c.txAddr = c.txAddr[:0]
-		c.txFirst = time.Now()
-		go c.lingerKick(c.txFill)
+		st = C.sqobfs_pconn_write(c.pc, bytePtr(p), C.uint32_t(len(p)), &ca, 0)
+	} else {
+		t := c.putAddr(addr)
+		st = C.sqobfs_pconn_write(c.pc, bytePtr(p), C.uint32_t(len(p)), nil, C.uint64_t(t))
+		if st != C.SQ_OK {
+			c.takeAddr(t)
+		}
 	}
-	i := c.txN
-	c.txFill.SetLen(i, copy(c.txFill.In(i), p))
-	c.txAddr = append(c.txAddr, addr)
-	c.txN++
-	if c.txN == c.txFill.Cap {
-		c.handOff()
+	if st != C.SQ_OK {
+		return 0, c.opErr("write", st, addr)
 	}
-	c.txMu.Unlock()
 	if c.kind == XPlus {
-		return len(p) + S, nil // xplus.go:74 returns the inner write's n
+		return len(p) + XPlus.SaltLen(), nil
 	}
-	return len(p), nil // salamander.go:69
-}
-
-// handOff passes the filling batch to the flusher (txMu held).
-func (c *Conn) handOff() {
-	c.txWork <- txJob{s: c.txFill, addr: append([]net.Addr(nil), c.txAddr...), n: c.txN}
-	c.txFill = nil
-}
-
-// lingerKick flushes a partly filled batch Linger after its first datagram.
-func (c *Conn) lingerKick(s *Slots) {
-	t := time.NewTimer(c.opt.Linger)
-	defer t.Stop()
-	select {
-	case <-t.C:
-	case <-c.closed:
-		return
-	}
-	c.txMu.Lock()
-	if c.txFill == s && c.txN > 0 {
-		c.handOff()
-	}
-	c.txMu.Unlock()
-}
-
-func (c *Conn) flusher() {
-	defer c.wg.Done()
-	for {
-		var j txJob
-		select {
-		case j = <-c.txWork:
-		case <-c.closed:
-			return
-		}
-		err := j.s.Run(c.kr, Obfuscate, j.n, true, false)
-		for i := 0; i < j.n && err == nil; i++ {
-			_, err = c.PacketConn.WriteTo(j.s.Out(i)[:j.s.OutLen(i)], j.addr[i])
-		}
-		if err != nil {
-			c.txErr.Store(err)
-		}
-		c.txFree <- j.s
-	}
-}
-
-// ---- receive
-
-func (c *Conn) reader(free chan *rxBatch) {
-	defer c.wg.Done()
-	for {
-		var rb *rxBatch
-		select {
-		case rb = <-free:
-		case <-c.closed:
-			return
-		}
-		s := rb.s
-		addrs := make([]net.Addr, 0, s.Cap)
-		n := 0
-		for n < s.Cap {
-			if n == 1 { // batch what is already queued, for at most Linger
-				_ = c.PacketConn.SetReadDeadline(time.Now().Add(c.opt.Linger))
-			}
-			m, addr, err := c.PacketConn.ReadFrom(s.In(n))
-			if err != nil {
-				if n > 0 && errors.Is(err, os.ErrDeadlineExceeded) {
-					break
-				}
-				c.rxErr.Store(err)
-				close(c.rx)
-				return
-			}
-			s.SetLen(n, m)
-			addrs = append(addrs, addr)
-			n++
-		}
-		_ = c.PacketConn.SetReadDeadline(time.Time{})
-		if err := s.Run(c.kr, Deobfuscate, n, false, false); err != nil {
-			c.rxErr.Store(err)
-			close(c.rx)
-			return
-		}
-		rb.left = int32(n)
-		for i := 0; i < n; i++ {
-			c.rx <- rxItem{s: rb, i: i, addr: addrs[i]}
-		}
-	}
+	return len(p), nil
 }
 
 func (c *Conn) ReadFrom(p []byte) (int, net.Addr, error) {
-	it, ok := <-c.rx
-	if !ok {
-		if e, _ := c.rxErr.Load().(error); e != nil {
-			return 0, nil, e
-		}
-		return 0, nil, net.ErrClosed
+	c.mu.RLock()
+	defer c.mu.RUnlock()
+	if c.pc == nil {
+		return 0, nil, c.opErr("read", C.SQ_ECLOSED, nil)
 	}
-	n := copy(p, it.s.s.Out(it.i)[:it.s.s.OutLen(it.i)])
-	if atomic.AddInt32(&it.s.left, -1) == 0 {
-		it.s.free <- it.s
+	var n C.uint32_t
+	var from C.sqobfs_addr
+	var tag C.uint64_t
+	st := C.sqobfs_pconn_read(c.pc, bytePtr(p), C.uint32_t(len(p)), &n, &from, &tag)
+	if st != C.SQ_OK {
+		return 0, nil, c.opErr("read", st, nil)
 	}
-	return n, it.addr, nil
+	if c.socket {
+		return int(n), fromCAddr(&from), nil
+	}
+	return int(n), c.takeAddr(uint64(tag)), nil
 }
+
+func deadlineNs(t time.Time) C.int64_t {
+	if t.IsZero() {
+		return 0
+	}
+	if ns := t.UnixNano(); ns > 0 {
+		return C.int64_t(ns)
+	}
+	return 1 // before the epoch: passed
+}
+
+func (c *Conn) setDeadline(which C.uint32_t, t time.Time) error {
+	c.mu.RLock()
+	defer c.mu.RUnlock()
+	if c.pc == nil {
+		return c.opErr("set", C.SQ_ECLOSED, nil)
+	}
+	return check(C.sqobfs_pconn_set_deadline(c.pc, which, deadlineNs(t)))
+}
+
+func (c *Conn) SetDeadline(t time.Time) error {
+	return c.setDeadline(C.SQOBFS_PCONN_READ|C.SQOBFS_PCONN_WRITE, t)
+}
+func (c *Conn) SetReadDeadline(t time.Time) error  { return c.setDeadline(C.SQOBFS_PCONN_READ, t) }
+func (c *Conn) SetWriteDeadline(t time.Time) error { return c.setDeadline(C.SQOBFS_PCONN_WRITE, t) }
 
 // Upstream is the sing unwrap convention (salamander.go:72-74, xplus.go:77-79).
 func (c *Conn) Upstream() any { return c.PacketConn }
 
+// Close: writes already made are sent (bounded, 200 ms), blocked calls fail
+// with net.ErrClosed, the wrapped conn is closed, then the engine, the
+// keyring and the context reference are released.
 func (c *Conn) Close() error {
-	c.once.Do(func() { close(c.closed) })
-	err := c.PacketConn.Close()
-	c.wg.Wait()
-	c.free()
-	return err
+	c.once.Do(func() {
+		c.closed.Store(true)
+		c.mu.RLock()
+		C.sqobfs_pconn_shutdown(c.pc) // wakes every blocked call, ends the workers
+		c.mu.RUnlock()
+		c.cerr = c.PacketConn.Close() // ends the pump reader's inner ReadFrom
+		c.wg.Wait()
+		c.mu.Lock() // no call on pc is in progress past this point
+		C.sqobfs_pconn_close(c.pc)
+		c.pc = nil
+		c.mu.Unlock()
+		c.kr.Close()
+		c.ctx.Close()
+	})
+	return c.cerr
 }
 
-func (c *Conn) free() {
+// ---- pump mode: the wrapped conn's I/O on two goroutines
+
+func (c *Conn) pumpRx() {
+	defer c.wg.Done()
+	buf := make([]byte, 65536) // a whole UDP datagram; the engine cuts to its slot
 	for {
-		select {
-		case s := <-c.txFree:
-			s.Free()
+		n, addr, err := c.PacketConn.ReadFrom(buf)
+		if err != nil {
+			if c.closed.Load() {
+				return
+			}
+			c.setErr(&c.rxErr, err)
+			// a timeout or an ICMP-reported refusal is per call: the next read
+			// works; anything else ends the receive side
+			var ne net.Error
+			once := errors.As(err, &ne) && ne.Timeout() ||
+				errors.Is(err, syscall.ECONNREFUSED)
+			c.mu.RLock()
+			_ = C.sqobfs_pconn_rx_fail(c.pc, C.SQ_EIO, boolInt(once))
+			c.mu.RUnlock()
+			if !once {
+				return
+			}
 			continue
-		default:
 		}
-		break
+		t := c.putAddr(addr)
+		c.mu.RLock()
+		st := C.sqobfs_pconn_rx_push(c.pc, bytePtr(buf[:n]), C.uint32_t(n), nil, C.uint64_t(t))
+		c.mu.RUnlock()
+		if st != C.SQ_OK {
+			c.takeAddr(t)
+			if st == C.SQ_ECLOSED {
+				return
+			}
+		}
 	}
-	c.kr.Close()
-	c.ctx.Close()
+}
+
+func (c *Conn) pumpTx() {
+	defer c.wg.Done()
+	for {
+		var v C.sqobfs_pconn_tx
+		c.mu.RLock()
+		st := C.sqobfs_pconn_tx_take(c.pc, -1, &v)
+		c.mu.RUnlock()
+		if st != C.SQ_OK {
+			return // SQ_ECLOSED: shut down
+		}
+		n := int(v.count)
+		offs := unsafe.Slice((*uint64)(unsafe.Pointer(v.off)), n)
+		lens := unsafe.Slice((*uint32)(unsafe.Pointer(v.len)), n)
+		tags := unsafe.Slice((*uint64)(unsafe.Pointer(v.tag)), n)
+		for i := 0; i < n; i++ {
+			wire := unsafe.Slice((*byte)(unsafe.Add(unsafe.Pointer(v.base), offs[i])), lens[i])
+			if _, err := c.PacketConn.WriteTo(wire, c.takeAddr(tags[i])); err != nil {
+				c.setErr(&c.txErr, err)
+			}
+		}
+		c.mu.RLock()
+		_ = C.sqobfs_pconn_tx_done(c.pc)
+		c.mu.RUnlock()
+	}
+}
+
+func boolInt(b bool) C.int {
+	if b {
+		return 1
+	}
+	return 0
 }

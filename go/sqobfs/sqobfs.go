@@ -5,14 +5,22 @@
 // (hysteria2/salamander.go, hysteria/xplus.go in the reference).
 //
 // cgo pointer rules: nothing below passes a Go pointer that holds other Go
-// pointers, and C never keeps a Go pointer after a call returns.  Every
-// batch descriptor and array handed to C is C memory (C.malloc), and the
-// datagram bytes live in page-locked C memory (sqobfs_host_alloc) that Go
-// code reads and writes through unsafe.Slice views.  Go byte slices passed
-// to C directly (the PSK blob) contain no pointers and are not retained.
+// pointers, and C never keeps a Go pointer after a call returns.  Byte
+// slices passed to C (payloads, the PSK, read buffers) contain no pointers
+// and are only used for the duration of the call; batch descriptors and
+// datagram slots are C memory.
 //
-// Not compiled in the repository's own image (it has no Go toolchain); the
-// exact C call sequence of this file is replayed by tests/cpp/test_cgo_sequence.c.
+// Lifetimes: a Context is reference counted.  Open returns one with a single
+// reference (the caller's); every Keyring and Slots made from it holds
+// another, so the C context is closed only after the last of them is closed
+// or freed, whatever the order the caller (or a finalizer) uses.  Shared
+// hands out one context per GPU to every Conn of the process (Hysteria's
+// port hopping re-dials every 30 s, hysteria/hop.go:114; a connection costs
+// no new context and no device-wide synchronisation).
+//
+// Not compiled in the repository's own image (it has no Go toolchain): the C
+// call sequences of this package are replayed by tests/cpp/test_cgo_sequence.c
+// (Slots) and tests/cpp/test_pconn.c (Conn's engine, sqobfs_pconn_*).
 package sqobfs
 
 /*
@@ -27,6 +35,7 @@ import "C"
 import (
 	"errors"
 	"runtime"
+	"sync"
 	"unsafe"
 )
 
@@ -67,33 +76,103 @@ func check(st C.int) error {
 	return nil
 }
 
-// Context is one GPU (sqobfs_open).  Safe for concurrent use.
-type Context struct{ c *C.sqobfs_ctx }
+// ErrClosed is returned by calls on a released Context.
+var ErrClosed = errors.New("sqobfs: context closed")
 
+// Context is one GPU (sqobfs_open).  Safe for concurrent use.
+type Context struct {
+	mu     sync.Mutex
+	c      *C.sqobfs_ctx
+	refs   int
+	device int
+	shared bool
+}
+
+// Open makes a context of its own on a GPU; Close releases the caller's
+// reference.
 func Open(device int) (*Context, error) {
 	var c *C.sqobfs_ctx
 	if err := check(C.sqobfs_open(C.int(device), &c)); err != nil {
 		return nil, err
 	}
-	return &Context{c: c}, nil
+	return &Context{c: c, refs: 1, device: device}, nil
 }
 
-func (x *Context) Close() {
-	if x.c != nil {
-		C.sqobfs_close(x.c)
+var shared struct {
+	sync.Mutex
+	m map[int]*Context
+}
+
+// Shared returns the process's context on a GPU with a new reference (Close
+// releases it); it is opened on first use and closed with its last user.
+func Shared(device int) (*Context, error) {
+	shared.Lock()
+	defer shared.Unlock()
+	if x := shared.m[device]; x != nil && x.ref() {
+		return x, nil
+	}
+	x, err := Open(device)
+	if err != nil {
+		return nil, err
+	}
+	x.shared = true
+	if shared.m == nil {
+		shared.m = map[int]*Context{}
+	}
+	shared.m[device] = x
+	return x, nil
+}
+
+// ref takes a reference; false once the context is gone.
+func (x *Context) ref() bool {
+	x.mu.Lock()
+	defer x.mu.Unlock()
+	if x.c == nil {
+		return false
+	}
+	x.refs++
+	return true
+}
+
+// unref drops a reference and closes the C context with the last one.
+func (x *Context) unref() {
+	x.mu.Lock()
+	x.refs--
+	last := x.refs == 0 && x.c != nil
+	c := x.c
+	if last {
 		x.c = nil
 	}
+	x.mu.Unlock()
+	if !last {
+		return
+	}
+	if x.shared {
+		shared.Lock()
+		if shared.m[x.device] == x {
+			delete(shared.m, x.device)
+		}
+		shared.Unlock()
+	}
+	C.sqobfs_close(c)
 }
+
+// Close releases the reference Open or Shared returned.
+func (x *Context) Close() { x.unref() }
 
 // Keyring is the device copy of the PSK: the `password` captured by
 // NewSalamanderConn (salamander.go:19-40) or the `key` of NewXPlusPacketConn
 // (xplus.go:19-44).
 type Keyring struct {
+	ctx  *Context
 	kr   *C.sqobfs_keyring
 	Kind Kind
 }
 
 func (x *Context) NewKeyring(kind Kind, psk []byte) (*Keyring, error) {
+	if !x.ref() {
+		return nil, ErrClosed
+	}
 	// a private C copy: the reference's append(password, salt...) can write
 	// into the password's spare capacity (SURVEY.md section 5); this never does
 	blob := C.malloc(C.size_t(len(psk) + 1))
@@ -109,15 +188,20 @@ func (x *Context) NewKeyring(kind Kind, psk []byte) (*Keyring, error) {
 	var kr *C.sqobfs_keyring
 	if err := check(C.sqobfs_keyring_create(x.c, C.int(kind), 1, (*C.uint8_t)(blob), off, ln,
 		&kr)); err != nil {
+		x.unref()
 		return nil, err
 	}
-	return &Keyring{kr: kr, Kind: kind}, nil
+	return &Keyring{ctx: x, kr: kr, Kind: kind}, nil
 }
 
+// Close releases the keyring (sqobfs_keyring_destroy does not block: its
+// device memory goes after the launches that used it) and its context
+// reference.
 func (k *Keyring) Close() {
 	if k.kr != nil {
 		C.sqobfs_keyring_destroy(k.kr)
 		k.kr = nil
+		k.ctx.unref()
 	}
 }
 
@@ -125,7 +209,8 @@ func (k *Keyring) Close() {
 // page-locked data region of Cap fixed slots of SlotBytes (DMA'd by
 // sqobfs_run_host without staging) and the sqobfs_batch descriptor with its
 // arrays, all allocated by C.  Go code fills and reads the slots through
-// unsafe.Slice views; the C side never sees a Go pointer.
+// unsafe.Slice views; the C side never sees a Go pointer.  For batches a
+// caller assembles itself; Conn uses the engine (sqobfs_pconn) instead.
 type Slots struct {
 	ctx       *Context
 	Cap       int
@@ -138,14 +223,19 @@ type Slots struct {
 	outLen    []uint32
 	inCap     []uint32
 	salt      []byte
+	once      sync.Once
 }
 
 func (x *Context) NewSlots(capacity, slotBytes int, saltLen int) (*Slots, error) {
 	if capacity <= 0 || slotBytes <= 0 {
 		return nil, errors.New("sqobfs: bad slot geometry")
 	}
+	if !x.ref() {
+		return nil, ErrClosed
+	}
 	s := &Slots{ctx: x, Cap: capacity, SlotBytes: slotBytes}
 	if err := check(C.sqobfs_host_alloc(x.c, C.size_t(2*capacity*slotBytes), &s.data)); err != nil {
+		x.unref()
 		return nil, err
 	}
 	s.b = (*C.sqobfs_batch)(C.calloc(1, C.size_t(unsafe.Sizeof(C.sqobfs_batch{}))))
@@ -174,6 +264,8 @@ func (x *Context) NewSlots(capacity, slotBytes int, saltLen int) (*Slots, error)
 	s.b.out_off = (*C.uint64_t)(unsafe.Pointer(oo))
 	s.b.out_len = (*C.uint32_t)(unsafe.Pointer(ol))
 	s.b.salt = (*C.uint8_t)(unsafe.Pointer(sl))
+	// the finalizer only frees C memory; the context stays open until this
+	// runs (it holds a reference), so it is never used after sqobfs_close
 	runtime.SetFinalizer(s, (*Slots).Free)
 	return s, nil
 }
@@ -201,15 +293,17 @@ func (s *Slots) OutLen(i int) int { return int(s.outLen[i]) }
 // Run transforms packets [0, n) in one sqobfs_run_host call (H2D, one
 // launch, D2H).  deviceSalt: obfuscate with salts generated on the GPU
 // (replaces buf.WriteRandom, salamander.go:60, and math/rand, xplus.go:67-69).
-// withCap: XPlus deobfuscate XORs up to SetCap bytes (xplus.go:55).
+// withCap: XPlus deobfuscate XORs up to SetCap bytes (xplus.go:55).  Output
+// bytes are only read up to OutLen, so the output slots are declared
+// uninitialised (no copy-in of the output span).
 func (s *Slots) Run(kr *Keyring, dir Direction, n int, deviceSalt, withCap bool) error {
 	if n < 0 || n > s.Cap {
 		return errors.New("sqobfs: batch larger than its slots")
 	}
 	s.b.n = C.uint32_t(n)
-	s.b.flags = 0
+	s.b.flags = C.SQOBFS_FLAG_OUT_UNINIT
 	if dir == Obfuscate && deviceSalt {
-		s.b.flags = C.SQOBFS_FLAG_DEVICE_SALT
+		s.b.flags |= C.SQOBFS_FLAG_DEVICE_SALT
 	}
 	s.b.in_cap = nil
 	if withCap {
@@ -218,18 +312,20 @@ func (s *Slots) Run(kr *Keyring, dir Direction, n int, deviceSalt, withCap bool)
 	return check(C.sqobfs_run_host(s.ctx.c, kr.kr, C.int(dir), s.b))
 }
 
+// Free releases the C memory and the context reference (once; also the
+// finalizer's path).
 func (s *Slots) Free() {
-	if s.b == nil {
-		return
-	}
-	runtime.SetFinalizer(s, nil)
-	C.free(unsafe.Pointer(s.b.in_off))
-	C.free(unsafe.Pointer(s.b.out_off))
-	C.free(unsafe.Pointer(s.b.in_len))
-	C.free(unsafe.Pointer(s.b.out_len))
-	C.free(unsafe.Pointer(&s.inCap[0]))
-	C.free(unsafe.Pointer(s.b.salt))
-	C.free(unsafe.Pointer(s.b))
-	C.sqobfs_host_free(s.ctx.c, s.data)
-	s.b = nil
+	s.once.Do(func() {
+		runtime.SetFinalizer(s, nil)
+		C.free(unsafe.Pointer(s.b.in_off))
+		C.free(unsafe.Pointer(s.b.out_off))
+		C.free(unsafe.Pointer(s.b.in_len))
+		C.free(unsafe.Pointer(s.b.out_len))
+		C.free(unsafe.Pointer(&s.inCap[0]))
+		C.free(unsafe.Pointer(s.b.salt))
+		C.free(unsafe.Pointer(s.b))
+		C.sqobfs_host_free(s.ctx.c, s.data)
+		s.b = nil
+		s.ctx.unref()
+	})
 }

@@ -64,7 +64,7 @@
 extern "C" {
 #endif
 
-#define SQOBFS_ABI_VERSION 3
+#define SQOBFS_ABI_VERSION 4
 
 #define SQOBFS_SALAMANDER_SALT_LEN 8 /* hysteria2/salamander.go:15 */
 #define SQOBFS_XPLUS_SALT_LEN 16     /* hysteria/xplus.go:17 */
@@ -77,6 +77,11 @@ extern "C" {
 #define SQ_EDEVICE (-3)  /* HIP runtime / kernel launch error */
 #define SQ_ENODEV (-4)   /* no such GPU */
 #define SQ_EPSK (-5)     /* a psk_id was out of range (host-staged path) */
+#define SQ_ETIMEDOUT (-6) /* a deadline passed (sqobfs_pconn_*: os.ErrDeadlineExceeded) */
+#define SQ_ECLOSED (-7)   /* the endpoint is closed (sqobfs_pconn_*: net.ErrClosed) */
+#define SQ_EIO (-8)       /* the wrapped conn's read failed (sqobfs_pconn_rx_fail) */
+/* sqobfs_pconn_*: a socket call failed with errno e */
+#define SQOBFS_ERRNO(e) (-1000 - (e))
 
 /* batch flag (sqobfs_run_host): output bytes outside the packets' output
  * regions need not be preserved (skips copying the output range in) */
@@ -147,6 +152,10 @@ void sqobfs_close(sqobfs_ctx *ctx);
 void *sqobfs_stream(sqobfs_ctx *ctx);
 /* wait for all work on `stream` (NULL = the HIP null stream) */
 int sqobfs_sync(sqobfs_ctx *ctx, void *stream);
+/* sqobfs_sync polls the stream for up to `us` microseconds before it blocks
+ * (default 0: block at once).  Polling holds the calling CPU for that long;
+ * it shortens the wake-up after short launches. */
+int sqobfs_set_sync_spin(sqobfs_ctx *ctx, uint32_t us);
 
 /* Set the context's salt key and next launch sequence number for
  * SQOBFS_FLAG_DEVICE_SALT (replay / tests; sqobfs_open draws a random key and
@@ -178,6 +187,9 @@ uint32_t sqobfs_unit_packets_for(uint64_t bytes, uint32_t n, int multi_psk);
 int sqobfs_keyring_create(sqobfs_ctx *ctx, int kind, uint32_t count,
                           const uint8_t *blob, const uint64_t *off,
                           const uint32_t *len, sqobfs_keyring **out);
+/* Does not block: the keyring's device memory is released in stream order
+ * after the launches that used it (never waits for other keyrings' or
+ * contexts' work).  The context must outlive its keyrings. */
 void sqobfs_keyring_destroy(sqobfs_keyring *kr);
 int sqobfs_keyring_kind(const sqobfs_keyring *kr);
 uint32_t sqobfs_keyring_count(const sqobfs_keyring *kr);
@@ -470,6 +482,117 @@ int sqobfs_udp_send_gso(int fd, const uint8_t *base, const uint64_t *off, const 
  * message if the first GSO send is refused.  Returns the flags in effect
  * (>= 0) or SQ_EINVAL. */
 int sqobfs_udp_conn_set_offload(sqobfs_udp_conn *c, uint32_t flags);
+
+/* ------------------------------------------------------------------------
+ * Obfuscating packet conn: the engine behind the Go decorators (go/sqobfs).
+ *
+ * The reference's SalamanderPacketConn / XPlusPacketConn (hysteria2/
+ * salamander.go:19-109, hysteria/xplus.go:39-118) transform one datagram per
+ * ReadFrom / WriteTo, synchronously.  A pconn keeps their per-call contract
+ * -- ReadFrom returns one datagram with the reference's length rules,
+ * WriteTo takes one -- and batches the byte work underneath:
+ *   WriteTo  copies the payload into the transmit batch being filled and
+ *            returns; a worker obfuscates the batch in ONE launch (device
+ *            salts, in place behind S bytes of headroom) and sends it.
+ *            The worker launches as soon as it is idle (or linger_us after
+ *            the batch's first datagram), so a lone packet goes out at once
+ *            and a burst that arrives during a launch becomes the next batch.
+ *   ReadFrom returns the next datagram of a de-obfuscated receive batch; a
+ *            worker receives and de-obfuscates whole batches in ONE launch.
+ * Batches live in page-locked, GPU-mapped slots (zero copy, as
+ * sqobfs_udp_conn).  Two modes:
+ *   socket (fd >= 0): the pconn dup()s a UDP socket and moves the datagrams
+ *            itself with recvmmsg / sendmmsg (a Go *net.UDPConn's fd);
+ *   pump   (fd < 0):  the caller moves them over any PacketConn: its reader
+ *            hands each received datagram to sqobfs_pconn_rx_push, its
+ *            writer sends what sqobfs_pconn_tx_take returns.
+ * Addresses are sqobfs_addr (socket mode) and an opaque 64-bit tag that rides
+ * with every datagram (pump mode: the caller's handle on its own address
+ * object).  All calls are thread-safe; read and write may block, and honour
+ * the deadlines of sqobfs_pconn_set_deadline. */
+typedef struct sqobfs_pconn sqobfs_pconn;
+
+typedef struct sqobfs_pconn_opts {
+  uint32_t batch;      /* datagrams per launch at most (0 = 256) */
+  uint32_t slot_bytes; /* per-datagram slot, multiple of 16 (0 = 2048, hop.go:19);
+                          longer received datagrams are cut to it, as a
+                          ReadFrom into a buffer of that size cuts them */
+  uint32_t tx_batches; /* transmit batches (0 = 3) */
+  uint32_t rx_batches; /* receive batches (0 = 3) */
+  uint32_t linger_us;  /* an idle worker waits this long for a partly filled
+                          batch to grow (0: launch at once) */
+  uint32_t spin_us;    /* workers poll a launch this long before blocking
+                          (0 = 200; they are dedicated threads) */
+  uint32_t flags;      /* 0 */
+  uint32_t reserved;
+} sqobfs_pconn_opts;
+
+typedef struct sqobfs_pconn_stats {
+  uint64_t tx_datagrams, tx_batches; /* obfuscated and handed to the socket / taker */
+  uint64_t rx_datagrams, rx_batches; /* received and de-obfuscated */
+  uint64_t rx_truncated;             /* datagrams longer than a slot (cut) */
+  uint64_t tx_send_errors;           /* datagrams the socket refused */
+  uint32_t tx_max_batch, rx_max_batch;
+} sqobfs_pconn_stats;
+
+/* kr's kind picks Salamander or XPlus.  ctx and kr must outlive the pconn. */
+int sqobfs_pconn_open(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int fd,
+                      const sqobfs_pconn_opts *opts, sqobfs_pconn **out);
+/* Graceful stop (net.PacketConn.Close): later writes fail with SQ_ECLOSED;
+ * datagrams already written are still obfuscated and sent (taken, in pump
+ * mode) for up to 200 ms; then every blocked call returns SQ_ECLOSED and the
+ * workers end.  Idempotent; may run concurrently with other calls. */
+void sqobfs_pconn_shutdown(sqobfs_pconn *pc);
+/* shutdown, then free everything; no call may be in progress or follow */
+void sqobfs_pconn_close(sqobfs_pconn *pc);
+/* WriteTo (salamander.go:57-70 / 81-93, xplus.go:62-75 / 86-98): queue the
+ * payload p[0..len) for `to` (socket mode) with `tag`.  Returns SQ_OK, SQ_EINVAL
+ * (longer than slot_bytes - S), SQ_ECLOSED, SQ_ETIMEDOUT (write deadline, while
+ * every transmit batch is busy), or an earlier datagram's send error (once). */
+int sqobfs_pconn_write(sqobfs_pconn *pc, const uint8_t *p, uint32_t len, const sqobfs_addr *to,
+                       uint64_t tag);
+/* ReadFrom (salamander.go:42-55, xplus.go:46-60) into p[0..cap): *n is what
+ * the reference's ReadFrom returns for a datagram of w bytes read into a
+ * buffer of cap bytes, m = min(w, cap): Salamander m <= 8: the m raw bytes,
+ * else the first m - 8 payload bytes; XPlus m < 16: 0, else the first m - 16
+ * payload bytes (XPlus's XOR of p past the returned length, xplus.go:55, is
+ * not reproduced: those bytes are not defined).  from / tag: the datagram's
+ * source and tag (either may be NULL).  Blocks until a datagram, the read
+ * deadline (SQ_ETIMEDOUT), shutdown (SQ_ECLOSED) or a receive error. */
+int sqobfs_pconn_read(sqobfs_pconn *pc, uint8_t *p, uint32_t cap, uint32_t *n,
+                      sqobfs_addr *from, uint64_t *tag);
+#define SQOBFS_PCONN_READ 1u
+#define SQOBFS_PCONN_WRITE 2u
+/* SetReadDeadline / SetWriteDeadline / SetDeadline: `which` = READ | WRITE;
+ * unix_ns = wall-clock time in ns since the epoch, 0 = none.  Wakes blocked
+ * calls, which fail with SQ_ETIMEDOUT once the deadline has passed. */
+int sqobfs_pconn_set_deadline(sqobfs_pconn *pc, uint32_t which, int64_t unix_ns);
+/* pump mode: a datagram the caller read from the wrapped conn (copied; cut
+ * to slot_bytes).  Blocks while every receive batch is full and unread. */
+int sqobfs_pconn_rx_push(sqobfs_pconn *pc, const uint8_t *wire, uint32_t n,
+                         const sqobfs_addr *from, uint64_t tag);
+/* pump mode: the wrapped conn's read failed: readers get `status` (e.g.
+ * SQ_EIO) once the queued datagrams are read -- one reader when `once` (a
+ * per-datagram error such as an ICMP-reported refusal, after which the
+ * wrapped conn reads on), every later reader otherwise. */
+int sqobfs_pconn_rx_fail(sqobfs_pconn *pc, int status, int once);
+/* pump mode: the next obfuscated batch to send.  Datagram i is
+ * base[off[i] .. +len[i]) (salt || payload ^ key) for to[i] / tag[i].  Valid
+ * until sqobfs_pconn_tx_done.  One taker at a time.  SQ_ETIMEDOUT after
+ * timeout_ms (-1 = forever), SQ_ECLOSED after shutdown. */
+typedef struct sqobfs_pconn_tx {
+  uint32_t count;
+  const uint8_t *base;
+  const uint64_t *off;
+  const uint32_t *len;
+  const sqobfs_addr *to;
+  const uint64_t *tag;
+} sqobfs_pconn_tx;
+int sqobfs_pconn_tx_take(sqobfs_pconn *pc, int timeout_ms, sqobfs_pconn_tx *out);
+int sqobfs_pconn_tx_done(sqobfs_pconn *pc);
+int sqobfs_pconn_stats_get(const sqobfs_pconn *pc, sqobfs_pconn_stats *out);
+/* live sqobfs_host_alloc blocks in the process (leak checks) */
+int64_t sqobfs_debug_host_allocs(void);
 
 #ifdef __cplusplus
 }

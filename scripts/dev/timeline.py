@@ -37,18 +37,31 @@ def main():
     s = torch.cuda.current_stream(dev).cuda_stream
     b = sqobfs.make_batch(n, sh["data"], sh["in_off"], sh["lens"], sh["out"], sh["out_off"],
                           sh["out_len"], sh["salt"], sh["psk_id"])
+    d = sqobfs.OBFUSCATE
+    per_pkt_salt = 2 * sh["S"]
+    if len(sys.argv) > 3 and sys.argv[3] == "deobfuscate":
+        # decode the obfuscated shard into a compact buffer, as bench.py does
+        sqobfs.launch(ctx, kr, sqobfs.OBFUSCATE, b, s)
+        wl = (sh["lens"] + sh["S"]).to(torch.int32)
+        lens64 = sh["lens"].to(torch.int64)
+        back_off = torch.cumsum(lens64, 0) - lens64 + 64
+        back = torch.zeros(int(sh["payload_bytes"]) + 128, device=dev, dtype=torch.uint8)
+        b = sqobfs.make_batch(n, sh["out"], sh["out_off"], wl, back, back_off, sh["out_len"],
+                              None, sh["psk_id"])
+        d = sqobfs.DEOBFUSCATE
+        per_pkt_salt = sh["S"]
     lib = sqobfs.lib()
     lib.sqobfs_build_info.restype = ctypes.c_char_p
     info = lib.sqobfs_build_info().decode()
     # unit size: argv[2], else sized by bytes as bench.py does
-    ctx.unit_packets = (int(sys.argv[2]) if len(sys.argv) > 2 else
+    ctx.unit_packets = (int(sys.argv[2]) if len(sys.argv) > 2 and int(sys.argv[2]) else
                         sqobfs.unit_packets_for(sh["payload_bytes"], n, n_psk > 1))
     ppw = ctx.unit_packets
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(60):  # past the first-launch ramp
-        sqobfs.launch(ctx, kr, sqobfs.OBFUSCATE, b, s)
+        sqobfs.launch(ctx, kr, d, b, s)
     e0.record()
-    sqobfs.launch(ctx, kr, sqobfs.OBFUSCATE, b, s)
+    sqobfs.launch(ctx, kr, d, b, s)
     e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3
@@ -64,7 +77,7 @@ def main():
     t = (t - t0) * tick_us
     ph = np.diff(t, axis=1)
     names = ["desc", "plan", "contents", "stream", "drain"]
-    out = {"build": info, "config": cfg, "unit_packets": ppw, "kernel_us": round(us, 1),
+    out = {"build": info, "config": cfg, "direction": "deobfuscate" if d else "obfuscate", "unit_packets": ppw, "kernel_us": round(us, 1),
            "tick_ns": round(tick_us * 1e3, 3), "waves": units}
     out["phase_us"] = {nm: {"p10": round(float(np.percentile(ph[:, i], 10)), 2),
                             "median": round(float(np.median(ph[:, i])), 2),
@@ -79,7 +92,7 @@ def main():
     # waves per phase over time, and the streaming share of the bytes
     bins = np.arange(0.0, float(t[:, 5].max()) + 10.0, 10.0)
     rows = []
-    per_wave = (2 * sh["payload_bytes"] + 2 * sh["S"] * n) / units
+    per_wave = (2 * sh["payload_bytes"] + per_pkt_salt * n) / units
     for lo in bins:
         hi = lo + 10.0
         pro = int(((t[:, 0] < hi) & (t[:, 3] > lo)).sum())

@@ -27,6 +27,9 @@ struct sqobfs_ctx {
   hipStream_t stream = nullptr;  // compute (and sqobfs_stream)
   hipStream_t h2d = nullptr;     // sqobfs_run_host copy-in
   hipStream_t d2h = nullptr;     // sqobfs_run_host copy-out
+  hipStream_t rel = nullptr;     // keyring releases (stream-ordered frees)
+  // sqobfs_sync: poll the stream this long before blocking (0 = block)
+  std::atomic<uint32_t> spin_us{0};
   std::mutex mu;  // guards the staging buffers of sqobfs_run_host
   uint8_t *pinned = nullptr;
   size_t pinned_cap = 0;
@@ -42,15 +45,52 @@ struct sqobfs_ctx {
 
 namespace {
 constexpr uint32_t kHostChunks = 8;  // sqobfs_run_host pipeline depth
-constexpr int kSpinMs = 4;           // sqobfs_sync: poll this long, then block
 // test hook (sqobfs_debug_fail_chunk): the launch of that pipeline chunk
 // fails as a device error would, once
 std::atomic<int> g_fail_chunk{-1};
+// live sqobfs_host_alloc blocks (sqobfs_debug_host_allocs: leak checks)
+std::atomic<int64_t> g_host_allocs{0};
 constexpr uint32_t kEvents = 16;
 }
 
+// The streams a keyring's table was last read on: an event recorded after the
+// keyring's latest launch on each.  Destroying the keyring frees its device
+// memory in stream order after those events (hipFreeAsync on the context's
+// release stream), so it neither blocks the caller nor waits for launches
+// that do not use it (another connection's, another context's).
+struct KeyringUses {
+  std::mutex mu;
+  std::vector<std::pair<hipStream_t, hipEvent_t>> ev;
+  void note(hipStream_t s) {
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto &e : ev)
+      if (e.first == s) {
+        (void)hipEventRecord(e.second, s);
+        return;
+      }
+    hipEvent_t x = nullptr;
+    if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess) {
+      (void)hipGetLastError();
+      (void)hipStreamSynchronize(s);  // no event: wait for this stream instead
+      return;
+    }
+    (void)hipEventRecord(x, s);
+    ev.emplace_back(s, x);
+  }
+  // the release stream waits for every use, then the events go
+  void fence(hipStream_t rel) {
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto &e : ev) {
+      (void)hipStreamWaitEvent(rel, e.second, 0);
+      (void)hipEventDestroy(e.second);
+    }
+    ev.clear();
+  }
+};
+
 struct sqobfs_quic_keyring {
   sqobfs_ctx *ctx = nullptr;
+  mutable KeyringUses uses;
   uint32_t suite = SQOBFS_QUIC_CHACHA20_POLY1305;
   uint32_t count = 0;
   sq::QuicKeyDev *table = nullptr;  // device (ChaCha20-Poly1305)
@@ -62,6 +102,7 @@ struct sqobfs_quic_keyring {
 
 struct sqobfs_keyring {
   sqobfs_ctx *ctx = nullptr;
+  mutable KeyringUses uses;
   int kind = 0;
   uint32_t count = 0;
   sq::PskEntry *table = nullptr;  // device
@@ -108,9 +149,74 @@ struct DeviceScope {
   DeviceScope &operator=(const DeviceScope &) = delete;
 };
 
+inline void cpu_relax() {
+#if defined(__x86_64__) || defined(__i386__)
+  __builtin_ia32_pause();
+#else
+  std::this_thread::yield();
+#endif
+}
+
 size_t salt_len(int kind) {
   return kind == SQOBFS_SALAMANDER ? SQOBFS_SALAMANDER_SALT_LEN : SQOBFS_XPLUS_SALT_LEN;
 }
+
+}  // namespace
+
+// Polls `s` for up to `us` microseconds: SQ_OK when it drained, 1 when it is
+// still busy (the caller then blocks), or an error.  Shared with the host
+// side (udp_batch.cpp, pconn.cpp).
+int sq_spin_wait(void *stream, uint32_t us) {
+  if (us == 0) return 1;
+  hipStream_t s = (hipStream_t)stream;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t q = hipStreamQuery(s);
+    if (q == hipSuccess) return SQ_OK;
+    if (q != hipErrorNotReady) return hip_status(q);
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(us)) return 1;
+    cpu_relax();
+  }
+}
+
+// A private non-blocking stream on the context's GPU (host engines:
+// pconn.cpp), and its release.
+int sq_ctx_stream_create(sqobfs_ctx *ctx, void **out) {
+  *out = nullptr;
+  DeviceScope ds_(ctx->device);
+  if (ds_.status != SQ_OK) return ds_.status;
+  hipStream_t s = nullptr;
+  const int st = hip_status(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  if (st == SQ_OK) *out = (void *)s;
+  return st;
+}
+
+void sq_ctx_stream_destroy(sqobfs_ctx *ctx, void *s) {
+  if (!s) return;
+  DeviceScope ds_(ctx->device);
+  (void)hipStreamSynchronize((hipStream_t)s);
+  (void)hipStreamDestroy((hipStream_t)s);
+}
+
+// Wait for `s`: poll up to spin_us, then block.
+int sq_ctx_stream_wait(sqobfs_ctx *ctx, void *s, uint32_t spin_us) {
+  DeviceScope ds_(ctx->device);
+  if (ds_.status != SQ_OK) return ds_.status;
+  const int st = sq_spin_wait(s, spin_us);
+  if (st != 1) return st;
+  return hip_status(hipStreamSynchronize((hipStream_t)s));
+}
+
+// Default unit (packets per wavefront) of a device batch whose lengths the
+// library cannot see: the built-in default, but small batches are spread so
+// that the launch has at least kMinUnits wavefronts (a 256-datagram socket
+// batch is 256 one-packet waves over the CUs, not 10 waves of 26 packets).
+uint32_t sq_unit_packets_default(uint32_t n) {
+  const uint32_t spread = (n + sq::kMinUnits - 1) / sq::kMinUnits;
+  return std::max<uint32_t>(1u, std::min<uint32_t>(sq::kDefaultUnitPackets, spread));
+}
+
+namespace {
 
 // NULL is the HIP null stream (HIP convention; torch's default stream), so a
 // caller's events and copies on that stream order with our kernels.
@@ -173,6 +279,53 @@ struct Range {
   uint32_t p0, p1;   // packets of the chunk
 };
 
+// The input and output byte ranges packets [p0, p1) of hb touch (empty
+// ranges are {0, 0}), per the output-length rules of include/sqobfs.h.
+void packet_spans(const sqobfs_batch *hb, int kind, int dir, uint32_t p0, uint32_t p1,
+                  Range &ri, Range &ro) {
+  const size_t S = salt_len(kind);
+  ri = Range{SIZE_MAX, 0, p0, p1};
+  ro = Range{SIZE_MAX, 0, p0, p1};
+  for (uint32_t i = p0; i < p1; i++) {
+    const size_t len = hb->in_len[i];
+    size_t cap = len;
+    if (kind == SQOBFS_XPLUS && dir == SQOBFS_DEOBFUSCATE && hb->in_cap)
+      cap = std::max<size_t>(len, hb->in_cap[i]);
+    size_t osz;
+    if (dir == SQOBFS_OBFUSCATE) osz = S + len;
+    else if (kind == SQOBFS_SALAMANDER) osz = len <= S ? len : len - S;
+    else osz = len < S ? 0 : cap - S;
+    if (cap) {
+      ri.lo = std::min<size_t>(ri.lo, hb->in_off[i]);
+      ri.hi = std::max<size_t>(ri.hi, hb->in_off[i] + cap);
+    }
+    if (osz) {
+      ro.lo = std::min<size_t>(ro.lo, hb->out_off[i]);
+      ro.hi = std::max<size_t>(ro.hi, hb->out_off[i] + osz);
+    }
+  }
+  if (ri.lo > ri.hi) ri.lo = ri.hi = 0;
+  if (ro.lo > ro.hi) ro.lo = ro.hi = 0;
+}
+
+// byte range ra of buffer a and rb of buffer b overlap
+bool spans_meet(const uint8_t *a, const Range &ra, const uint8_t *b, const Range &rb) {
+  return ra.hi > ra.lo && rb.hi > rb.lo && a + ra.lo < b + rb.hi && b + rb.lo < a + ra.hi;
+}
+
+// Some part's output range overlaps another part's input or output range:
+// the parts cannot run concurrently, each copying its whole span.
+bool parts_clash(const sqobfs_batch *hb, const std::vector<Range> &rin,
+                 const std::vector<Range> &rout) {
+  const size_t k = rin.size();
+  for (size_t x = 0; x < k; x++)
+    for (size_t y = 0; y < k; y++)
+      if (x != y && (spans_meet(hb->out, rout[x], hb->out, rout[y]) ||
+                     spans_meet(hb->out, rout[x], hb->in, rin[y])))
+        return true;
+  return false;
+}
+
 bool is_pinned(const void *p) {
   hipPointerAttribute_t a;
   if (hipPointerGetAttributes(&a, p) != hipSuccess) {
@@ -213,6 +366,9 @@ const char *sqobfs_strerror(int status) {
     case SQ_EDEVICE: return "HIP runtime or kernel launch error";
     case SQ_ENODEV: return "no such GPU";
     case SQ_EPSK: return "psk_id out of range";
+    case SQ_ETIMEDOUT: return "deadline exceeded";
+    case SQ_ECLOSED: return "closed";
+    case SQ_EIO: return "the wrapped connection failed";
   }
   return "unknown status";
 }
@@ -254,9 +410,11 @@ int sqobfs_open(int device, sqobfs_ctx **out) {
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->h2d, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->rel, hipStreamNonBlocking);
   if (e != hipSuccess) {
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->h2d) (void)hipStreamDestroy(c->h2d);
+    if (c->d2h) (void)hipStreamDestroy(c->d2h);
     delete c;
     return hip_status(e);
   }
@@ -268,11 +426,13 @@ void sqobfs_close(sqobfs_ctx *ctx) {
   if (!ctx) return;
   DeviceScope ds_(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
+  (void)hipStreamSynchronize(ctx->rel);  // keyrings released before the context
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   if (ctx->dev) (void)hipFree(ctx->dev);
   (void)hipStreamDestroy(ctx->stream);
   (void)hipStreamDestroy(ctx->h2d);
   (void)hipStreamDestroy(ctx->d2h);
+  (void)hipStreamDestroy(ctx->rel);
   for (auto &e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   delete ctx;
@@ -297,10 +457,15 @@ uint32_t sqobfs_unit_packets_for(uint64_t bytes, uint32_t n, int multi_psk) {
   if (n == 0) return sq::kDefaultUnitPackets;
   const uint64_t target = multi_psk ? sq::kUnitBytesMultiPsk : sq::kUnitBytes;
   const uint64_t u = bytes ? target * n / bytes : sq::kMaxUnitPackets;  // floor(target / mean)
-  return (uint32_t)std::min<uint64_t>(std::max<uint64_t>(u, 1), sq::kMaxUnitPackets);
+  // and at least kMinUnits wavefronts for small batches
+  const uint64_t spread = ((uint64_t)n + sq::kMinUnits - 1) / sq::kMinUnits;
+  return (uint32_t)std::min<uint64_t>(std::max<uint64_t>(std::min(u, spread), 1),
+                                      sq::kMaxUnitPackets);
 }
 
 uint32_t sqobfs_unit_packets(const sqobfs_ctx *ctx) {
+  // (device batches below kMinUnits * default packets are spread further:
+  // sq_unit_packets_default)
   const uint32_t v = ctx ? ctx->unit_packets.load(std::memory_order_relaxed) : 0u;
   return v ? v : sq::kDefaultUnitPackets;
 }
@@ -312,19 +477,21 @@ int sqobfs_sync(sqobfs_ctx *ctx, void *stream) {
   DeviceScope ds_(ctx->device);
   if (ds_.status != SQ_OK) return ds_.status;
   hipStream_t s = pick_stream(ctx, stream);
-  // A batch takes about a millisecond: poll for that long before blocking.
-  // hipStreamSynchronize's blocking wake-up left the GPU idle ~80 us between
-  // synchronous batches (bench --inproc 1: 0.56 ms per step against 0.48 ms
-  // for queued launches of the same batch).
-  const auto t0 = std::chrono::steady_clock::now();
-  for (;;) {
-    const hipError_t q = hipStreamQuery(s);
-    if (q == hipSuccess) return SQ_OK;
-    if (q != hipErrorNotReady) return hip_status(q);
-    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(kSpinMs)) break;
-    __builtin_ia32_pause();
-  }
+  // Opt-in (sqobfs_set_sync_spin): poll before blocking.  hipStreamSynchronize's
+  // blocking wake-up left the GPU idle ~80 us between synchronous
+  // 1M-packet batches (bench --inproc 1: 0.56 ms per step against 0.48 ms for
+  // queued launches), but a poll holds a CPU for its whole length, so only a
+  // caller with a thread to spare turns it on.
+  const uint32_t spin = ctx->spin_us.load(std::memory_order_relaxed);
+  const int st = sq_spin_wait(s, spin);
+  if (st != 1) return st;
   return hip_status(hipStreamSynchronize(s));
+}
+
+int sqobfs_set_sync_spin(sqobfs_ctx *ctx, uint32_t us) {
+  if (!ctx) return SQ_EINVAL;
+  ctx->spin_us.store(us, std::memory_order_relaxed);
+  return SQ_OK;
 }
 
 int sqobfs_keyring_create(sqobfs_ctx *ctx, int kind, uint32_t count, const uint8_t *blob,
@@ -345,7 +512,7 @@ int sqobfs_keyring_create(sqobfs_ctx *ctx, int kind, uint32_t count, const uint8
   uint8_t *d_blob = nullptr;
   uint64_t *d_off = nullptr;
   uint32_t *d_len = nullptr;
-  hipError_t e = hipMalloc(&kr->table, sizeof(sq::PskEntry) * count);
+  hipError_t e = hipMallocAsync((void **)&kr->table, sizeof(sq::PskEntry) * count, ctx->stream);
   if (e == hipSuccess) e = hipMalloc(&d_blob, blob_bytes ? blob_bytes : 1);
   if (e == hipSuccess) e = hipMalloc(&d_off, sizeof(uint64_t) * count);
   if (e == hipSuccess) e = hipMalloc(&d_len, sizeof(uint32_t) * count);
@@ -366,7 +533,9 @@ int sqobfs_keyring_create(sqobfs_ctx *ctx, int kind, uint32_t count, const uint8
   if (d_off) (void)hipFree(d_off);
   if (d_len) (void)hipFree(d_len);
   if (st != SQ_OK) {
-    if (kr->table) (void)hipFree(kr->table);
+    (void)hipStreamSynchronize(ctx->stream);
+    if (kr->table) (void)hipFreeAsync(kr->table, ctx->stream);
+    (void)hipStreamSynchronize(ctx->stream);
     delete kr;
     return st;
   }
@@ -377,8 +546,10 @@ int sqobfs_keyring_create(sqobfs_ctx *ctx, int kind, uint32_t count, const uint8
 void sqobfs_keyring_destroy(sqobfs_keyring *kr) {
   if (!kr) return;
   DeviceScope ds_(kr->ctx->device);
-  (void)hipDeviceSynchronize();  // launches on any stream may still read the table
-  if (kr->table) (void)hipFree(kr->table);
+  // launches that used the table may still run: free it after them, in
+  // stream order, without blocking (and without a device-wide sync)
+  kr->uses.fence(kr->ctx->rel);
+  if (kr->table) (void)hipFreeAsync(kr->table, kr->ctx->rel);
   delete kr;
 }
 
@@ -393,8 +564,12 @@ int sqobfs_launch(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir, const sqob
   if (st != SQ_OK || b->n == 0) return st;
   DeviceScope ds_(ctx->device);
   if (ds_.status != SQ_OK) return ds_.status;
-  const sq::KParams kp = make_params(ctx, kr, b);
-  return sq_launch_obfs(kr->kind, dir, &kp, pick_stream(ctx, stream));
+  sq::KParams kp = make_params(ctx, kr, b);
+  if (kp.ppw == 0) kp.ppw = sq_unit_packets_default(b->n);
+  hipStream_t s = pick_stream(ctx, stream);
+  const int st2 = sq_launch_obfs(kr->kind, dir, &kp, s);
+  if (st2 == SQ_OK) kr->uses.note(s);
+  return st2;
 }
 
 int sqobfs_salamander_obfuscate(sqobfs_ctx *ctx, const sqobfs_keyring *kr,
@@ -612,27 +787,33 @@ int sqobfs_quic_keyring_create_suite(sqobfs_ctx *ctx, uint32_t suite, uint32_t c
       for (int i = 0; i < 8; i++) h[k].hp[i] = le32(keys[k].hp + 4 * i);
     }
     kr->host0 = h[0];
-    e = hipMalloc(&kr->table, sizeof(sq::QuicKeyDev) * count);
+    e = hipMallocAsync((void **)&kr->table, sizeof(sq::QuicKeyDev) * count, ctx->stream);
     if (e == hipSuccess)
-      e = hipMemcpy(kr->table, h.data(), sizeof(sq::QuicKeyDev) * count, hipMemcpyHostToDevice);
+      e = hipMemcpyAsync(kr->table, h.data(), sizeof(sq::QuicKeyDev) * count,
+                         hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   } else {
     std::vector<sq::QuicGcmKeyDev> h(count);
     for (uint32_t k = 0; k < count; k++) gcm_key(keys[k], h[k]);
     memcpy(kr->grk0, h[0].rk, sizeof kr->grk0);
     memcpy(kr->ghrk0, h[0].hrk, sizeof kr->ghrk0);
     memcpy(kr->giv0, h[0].iv, sizeof kr->giv0);
-    e = hipMalloc(&kr->gtable, sizeof(sq::QuicGcmKeyDev) * count);
+    e = hipMallocAsync((void **)&kr->gtable, sizeof(sq::QuicGcmKeyDev) * count, ctx->stream);
     if (e == hipSuccess)
-      e = hipMemcpy(kr->gtable, h.data(), sizeof(sq::QuicGcmKeyDev) * count,
-                    hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc(&kr->t0, sizeof(uint32_t) * 256);
+      e = hipMemcpyAsync(kr->gtable, h.data(), sizeof(sq::QuicGcmKeyDev) * count,
+                         hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipMallocAsync((void **)&kr->t0, sizeof(uint32_t) * 256, ctx->stream);
     if (e == hipSuccess)
-      e = hipMemcpy(kr->t0, aes_tables().t0, sizeof(uint32_t) * 256, hipMemcpyHostToDevice);
+      e = hipMemcpyAsync(kr->t0, aes_tables().t0, sizeof(uint32_t) * 256, hipMemcpyHostToDevice,
+                         ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   }
   if (e != hipSuccess) {
-    if (kr->table) (void)hipFree(kr->table);
-    if (kr->gtable) (void)hipFree(kr->gtable);
-    if (kr->t0) (void)hipFree(kr->t0);
+    (void)hipStreamSynchronize(ctx->stream);
+    if (kr->table) (void)hipFreeAsync(kr->table, ctx->stream);
+    if (kr->gtable) (void)hipFreeAsync(kr->gtable, ctx->stream);
+    if (kr->t0) (void)hipFreeAsync(kr->t0, ctx->stream);
+    (void)hipStreamSynchronize(ctx->stream);
     delete kr;
     return hip_status(e);
   }
@@ -648,10 +829,10 @@ int sqobfs_quic_keyring_create(sqobfs_ctx *ctx, uint32_t count, const sqobfs_qui
 void sqobfs_quic_keyring_destroy(sqobfs_quic_keyring *kr) {
   if (!kr) return;
   DeviceScope ds_(kr->ctx->device);
-  (void)hipDeviceSynchronize();
-  if (kr->table) (void)hipFree(kr->table);
-  if (kr->gtable) (void)hipFree(kr->gtable);
-  if (kr->t0) (void)hipFree(kr->t0);
+  kr->uses.fence(kr->ctx->rel);  // as sqobfs_keyring_destroy: stream-ordered, no wait
+  if (kr->table) (void)hipFreeAsync(kr->table, kr->ctx->rel);
+  if (kr->gtable) (void)hipFreeAsync(kr->gtable, kr->ctx->rel);
+  if (kr->t0) (void)hipFreeAsync(kr->t0, kr->ctx->rel);
   delete kr;
 }
 
@@ -692,7 +873,13 @@ static int quic_launch(int open, sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr,
       g.osalt = salt;
       g.opsk = okr->host0;
     }
-    return sq_launch_quic_gcm(open, &g, pick_stream(ctx, stream));
+    hipStream_t s = pick_stream(ctx, stream);
+    const int st = sq_launch_quic_gcm(open, &g, s);
+    if (st == SQ_OK) {
+      kr->uses.note(s);
+      if (okr) okr->uses.note(s);
+    }
+    return st;
   }
   sq::QParams q;
   memset(&q, 0, sizeof q);
@@ -715,7 +902,13 @@ static int quic_launch(int open, sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr,
     q.osalt = salt;
     q.opsk = okr->host0;
   }
-  return sq_launch_quic(open, &q, pick_stream(ctx, stream));
+  hipStream_t s = pick_stream(ctx, stream);
+  const int st = sq_launch_quic(open, &q, s);
+  if (st == SQ_OK) {
+    kr->uses.note(s);
+    if (okr) okr->uses.note(s);
+  }
+  return st;
 }
 
 int sqobfs_quic_seal_salamander(sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr,
@@ -751,13 +944,20 @@ int sqobfs_host_alloc(sqobfs_ctx *ctx, size_t bytes, void **out) {
   *out = nullptr;
   DeviceScope ds_(ctx->device);
   if (ds_.status != SQ_OK) return ds_.status;
-  return hip_status(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+  const int st = hip_status(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+  if (st == SQ_OK) g_host_allocs.fetch_add(1);
+  return st;
 }
 
 void sqobfs_host_free(sqobfs_ctx *ctx, void *p) {
   (void)ctx;
-  if (p) (void)hipHostFree(p);
+  if (p) {
+    (void)hipHostFree(p);
+    g_host_allocs.fetch_sub(1);
+  }
 }
+
+int64_t sqobfs_debug_host_allocs(void) { return g_host_allocs.load(); }
 
 int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
                     const sqobfs_batch *hb) {
@@ -770,48 +970,20 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
   const size_t S = salt_len(kind);
   // ---- pass over the descriptors: psk ids, and per chunk of packets the
   // input / output byte ranges it touches
+  if (hb->psk_id)
+    for (uint32_t i = 0; i < n; i++)
+      if (hb->psk_id[i] >= kr->count) return SQ_EPSK;
   const uint32_t nchunk = n < 4096 ? 1u : std::min<uint32_t>(kHostChunks, (n + 4095) / 4096);
   std::vector<Range> rin(nchunk), rout(nchunk);
   for (uint32_t c = 0; c < nchunk; c++) {
     const uint32_t p0 = (uint32_t)((uint64_t)n * c / nchunk);
     const uint32_t p1 = (uint32_t)((uint64_t)n * (c + 1) / nchunk);
-    Range ri{SIZE_MAX, 0, p0, p1}, ro{SIZE_MAX, 0, p0, p1};
-    for (uint32_t i = p0; i < p1; i++) {
-      const size_t len = hb->in_len[i];
-      size_t cap = len;
-      if (kind == SQOBFS_XPLUS && dir == SQOBFS_DEOBFUSCATE && hb->in_cap)
-        cap = std::max<size_t>(len, hb->in_cap[i]);
-      size_t osz;
-      if (dir == SQOBFS_OBFUSCATE) osz = S + len;
-      else if (kind == SQOBFS_SALAMANDER) osz = len <= S ? len : len - S;
-      else osz = len < S ? 0 : cap - S;
-      if (cap) {
-        ri.lo = std::min<size_t>(ri.lo, hb->in_off[i]);
-        ri.hi = std::max<size_t>(ri.hi, hb->in_off[i] + cap);
-      }
-      if (osz) {
-        ro.lo = std::min<size_t>(ro.lo, hb->out_off[i]);
-        ro.hi = std::max<size_t>(ro.hi, hb->out_off[i] + osz);
-      }
-      if (hb->psk_id && hb->psk_id[i] >= kr->count) return SQ_EPSK;
-    }
-    if (ri.lo > ri.hi) ri.lo = ri.hi = 0;
-    if (ro.lo > ro.hi) ro.lo = ro.hi = 0;
-    rin[c] = ri;
-    rout[c] = ro;
+    packet_spans(hb, kind, dir, p0, p1, rin[c], rout[c]);
   }
   // Chunks run concurrently: if one chunk's output bytes overlap another
   // chunk's input or output bytes (in-place or interleaved layouts), run
   // the batch as a single chunk instead.
-  auto meet = [](const uint8_t *a, const Range &ra, const uint8_t *b, const Range &rb) {
-    return ra.hi > ra.lo && rb.hi > rb.lo && a + ra.lo < b + rb.hi && b + rb.lo < a + ra.hi;
-  };
-  bool clash = false;
-  for (uint32_t x = 0; x < nchunk && !clash; x++)
-    for (uint32_t y = 0; y < nchunk && !clash; y++)
-      clash = x != y && (meet(hb->out, rout[x], hb->out, rout[y]) ||
-                         meet(hb->out, rout[x], hb->in, rin[y]));
-  if (clash) {
+  if (parts_clash(hb, rin, rout)) {
     Range ri{SIZE_MAX, 0, 0, n}, ro{SIZE_MAX, 0, 0, n};
     for (uint32_t c = 0; c < nchunk; c++) {
       if (rin[c].hi > rin[c].lo) ri.lo = std::min(ri.lo, rin[c].lo), ri.hi = std::max(ri.hi, rin[c].hi);
@@ -959,6 +1131,7 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
     }
     SQ_TRY_DRAIN(hipEventRecord(ev_k, ctx->stream));
     SQ_TRY_DRAIN(hipStreamWaitEvent(ctx->d2h, ev_k, 0));
+    if (c + 1 == nrun) kr->uses.note(ctx->stream);
     if (ro.hi > ro.lo) {
       uint8_t *dst = out_pinned ? hb->out + ro.lo : hout(ro.lo);
       SQ_TRY_DRAIN(hipMemcpyAsync(dst, dout(ro.lo), ro.hi - ro.lo, hipMemcpyDeviceToHost,
@@ -1032,6 +1205,16 @@ int sqobfs_run_host_sharded(uint32_t nctx, sqobfs_ctx *const *ctxs,
   const int sc = sqobfs_shard_cuts(hb->n, hb->in_len, nctx, cut.data());
   if (sc != SQ_OK) return sc;
   const size_t S = salt_len(krs[0]->kind);
+  // Each shard copies its whole input / output span: when one shard's output
+  // span meets another shard's span (interleaved, shuffled or in-place
+  // layouts) they cannot run at once, and the batch runs on one context
+  // (whose own chunking makes the same check).
+  {
+    std::vector<Range> rin(nctx), rout(nctx);
+    for (uint32_t k = 0; k < nctx; k++)
+      packet_spans(hb, krs[0]->kind, dir, cut[k], cut[k + 1], rin[k], rout[k]);
+    if (parts_clash(hb, rin, rout)) return sqobfs_run_host(ctxs[0], krs[0], dir, hb);
+  }
   std::vector<int> st(nctx, SQ_OK);
   std::vector<std::thread> th;
   for (uint32_t k = 0; k < nctx; k++) {

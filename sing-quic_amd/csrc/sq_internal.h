@@ -20,6 +20,9 @@ constexpr uint32_t kMaxUnitPackets = 62;
 // about this many payload bytes per wavefront (~21.7 KB
 // per wave streams best; per-packet keyring gathers want longer units).
 constexpr uint64_t kUnitBytes = 21700, kUnitBytesMultiPsk = 36000;
+// ... but at least this many wavefronts per launch when the batch is small
+// (latency: a socket batch of 256 datagrams runs as 256 one-packet waves)
+constexpr uint32_t kMinUnits = 2048;
 
 // Per-PSK hash state, derived once per keyring on the GPU (psk_prepare).
 //
@@ -148,6 +151,17 @@ struct QGParams {
 };
 
 }  // namespace sq
+
+// host helpers implemented in sq_api.hip
+// poll a stream for up to `us` microseconds: 0 = drained, 1 = still busy, <0 error
+int sq_spin_wait(void *stream, uint32_t us);
+// packets per wavefront of a device batch of n packets (lengths unknown)
+uint32_t sq_unit_packets_default(uint32_t n);
+// private streams of host engines (pconn.cpp) on a context's GPU
+struct sqobfs_ctx;
+int sq_ctx_stream_create(sqobfs_ctx *ctx, void **out);
+void sq_ctx_stream_destroy(sqobfs_ctx *ctx, void *s);
+int sq_ctx_stream_wait(sqobfs_ctx *ctx, void *s, uint32_t spin_us);
 
 // launchers implemented in sq_quic_gcm.hip
 extern "C" int sq_launch_quic_gcm(int open, const sq::QGParams *qp, void *stream);

@@ -31,6 +31,8 @@
 #include <new>
 #include <vector>
 
+#include "sq_internal.h"
+#include "sq_sockaddr.h"
 #include "sqobfs.h"
 
 namespace {
@@ -41,39 +43,8 @@ constexpr uint32_t kGsoMaxSegs = 64;     // UDP_MAX_SEGMENTS of older kernels
 constexpr uint32_t kGsoMaxBytes = 65000; // one GSO send stays below 64 KiB of IP payload
 constexpr uint32_t kGroBuf = 65536;      // one coalesced receive
 
-void to_sockaddr(const sqobfs_addr &a, sockaddr_storage *ss, socklen_t *sl) {
-  memset(ss, 0, sizeof *ss);
-  if (a.family == AF_INET6) {
-    auto *s6 = reinterpret_cast<sockaddr_in6 *>(ss);
-    s6->sin6_family = AF_INET6;
-    s6->sin6_port = htons(a.port);
-    s6->sin6_scope_id = a.scope_id;
-    memcpy(&s6->sin6_addr, a.addr, 16);
-    *sl = sizeof(sockaddr_in6);
-  } else {
-    auto *s4 = reinterpret_cast<sockaddr_in *>(ss);
-    s4->sin_family = AF_INET;
-    s4->sin_port = htons(a.port);
-    memcpy(&s4->sin_addr, a.addr, 4);
-    *sl = sizeof(sockaddr_in);
-  }
-}
-
-void from_sockaddr(const sockaddr_storage &ss, sqobfs_addr *a) {
-  memset(a, 0, sizeof *a);
-  if (ss.ss_family == AF_INET6) {
-    const auto *s6 = reinterpret_cast<const sockaddr_in6 *>(&ss);
-    a->family = AF_INET6;
-    a->port = ntohs(s6->sin6_port);
-    a->scope_id = s6->sin6_scope_id;
-    memcpy(a->addr, &s6->sin6_addr, 16);
-  } else if (ss.ss_family == AF_INET) {
-    const auto *s4 = reinterpret_cast<const sockaddr_in *>(&ss);
-    a->family = AF_INET;
-    a->port = ntohs(s4->sin_port);
-    memcpy(a->addr, &s4->sin_addr, 4);
-  }
-}
+using sq::from_sockaddr;
+using sq::to_sockaddr;
 
 }  // namespace
 
@@ -108,11 +79,13 @@ struct sqobfs_udp_conn {
 
 namespace {
 
-// one launch on the mapped block + wait (the conn's batches are small)
+// one launch on the mapped block + wait (the conn's batches are small: poll
+// the stream for a while instead of paying the blocking wake-up)
+constexpr uint32_t kLaunchSpinUs = 200;
 int launch_sync(sqobfs_udp_conn *c, int dir, const sqobfs_batch &b) {
   void *s = sqobfs_stream(c->ctx);
   const int st = sqobfs_launch(c->ctx, c->kr, dir, &b, s);
-  return st != SQ_OK ? st : sqobfs_sync(c->ctx, s);
+  return st != SQ_OK ? st : sq_ctx_stream_wait(c->ctx, s, kLaunchSpinUs);
 }
 
 // sendmmsg of msg[0..n), waiting while the socket buffer is full.  Returns
@@ -610,7 +583,7 @@ int sqobfs_udp_conn_write_quic(sqobfs_udp_conn *c, const sqobfs_quic_keyring *qk
   b.pn = c->qpn_tx;
   void *s = sqobfs_stream(c->ctx);
   int st = sqobfs_quic_seal_salamander(c->ctx, qkr, c->kr, &b, c->qsalt, s);
-  if (st == SQ_OK) st = sqobfs_sync(c->ctx, s);
+  if (st == SQ_OK) st = sq_ctx_stream_wait(c->ctx, s, kLaunchSpinUs);
   if (st != SQ_OK) return st;
   // *sent stays a prefix count (as for conn_write): the datagrams before the
   // first packet the kernel rejected (tx_out_len = SQOBFS_QUIC_E*) are sent,
@@ -668,7 +641,7 @@ int sqobfs_udp_conn_read_quic(sqobfs_udp_conn *c, const sqobfs_quic_keyring *qkr
   b.pn_out = c->qpn_out;
   void *s = sqobfs_stream(c->ctx);
   st = sqobfs_quic_open_salamander(c->ctx, qkr, c->kr, &b, s);
-  if (st == SQ_OK) st = sqobfs_sync(c->ctx, s);
+  if (st == SQ_OK) st = sq_ctx_stream_wait(c->ctx, s, kLaunchSpinUs);
   if (st != SQ_OK) return st;
   out->count = n;
   out->base = c->rx;

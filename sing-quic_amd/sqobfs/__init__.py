@@ -29,6 +29,7 @@ SALT_LEN = {SALAMANDER: 8, XPLUS: 16}
 OBFS_TYPE_SALAMANDER = "salamander"  # hysteria2/salamander.go:17
 
 SQ_OK, SQ_EINVAL, SQ_ENOMEM, SQ_EDEVICE, SQ_ENODEV, SQ_EPSK = 0, -1, -2, -3, -4, -5
+SQ_ETIMEDOUT, SQ_ECLOSED, SQ_EIO = -6, -7, -8
 BAD_PSK = 0xFFFFFFFF
 FLAG_OUT_UNINIT = 1  # run_host: bytes between output regions need not be kept
 FLAG_DEVICE_SALT = 2  # obfuscate: salts from the GPU's ChaCha20 generator
@@ -194,6 +195,22 @@ def lib() -> ctypes.CDLL:
     L.sqobfs_unit_packets.restype = ctypes.c_uint32
     L.sqobfs_unit_packets_for.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int]
     L.sqobfs_unit_packets_for.restype = ctypes.c_uint32
+    L.sqobfs_set_sync_spin.argtypes = [vp, u32]
+    L.sqobfs_debug_host_allocs.argtypes = []
+    L.sqobfs_debug_host_allocs.restype = ctypes.c_int64
+    L.sqobfs_pconn_open.argtypes = [vp, vp, i32, vp, ctypes.POINTER(vp)]
+    L.sqobfs_pconn_shutdown.argtypes = [vp]
+    L.sqobfs_pconn_shutdown.restype = None
+    L.sqobfs_pconn_close.argtypes = [vp]
+    L.sqobfs_pconn_close.restype = None
+    L.sqobfs_pconn_write.argtypes = [vp, vp, u32, vp, ctypes.c_uint64]
+    L.sqobfs_pconn_read.argtypes = [vp, vp, u32, u32p, vp, vp]
+    L.sqobfs_pconn_set_deadline.argtypes = [vp, u32, ctypes.c_int64]
+    L.sqobfs_pconn_rx_push.argtypes = [vp, vp, u32, vp, ctypes.c_uint64]
+    L.sqobfs_pconn_rx_fail.argtypes = [vp, i32, i32]
+    L.sqobfs_pconn_tx_take.argtypes = [vp, i32, vp]
+    L.sqobfs_pconn_tx_done.argtypes = [vp]
+    L.sqobfs_pconn_stats_get.argtypes = [vp, vp]
     _lib = L
     return L
 

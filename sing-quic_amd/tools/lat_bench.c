@@ -1,0 +1,345 @@
+/* lat_bench.c -- per-datagram latency of the host-memory paths (DESIGN.md
+ * section 9.5), against the reference's synchronous per-datagram WriteTo /
+ * ReadFrom (hysteria2/salamander.go:42-70).
+ *
+ * For batches of 1, 16, 64 and 256 Salamander datagrams of 1350 B:
+ *   run_host   sqobfs_run_host on page-locked slots (staged H2D | kernel | D2H),
+ *              one call per batch: every datagram of the batch waits the whole
+ *              call
+ *   mapped     one launch on page-locked, GPU-mapped slots + stream wait (what
+ *              sqobfs_udp_conn and sqobfs_pconn do per batch), and the same
+ *              over unit sizes 1..26 packets per wave for the 256 batch
+ *   endpoint   sqobfs_udp_conn_write of the batch to a loopback socket: from
+ *              the call to the last datagram's arrival
+ *   pconn      n back-to-back sqobfs_pconn_write calls (the Go Conn's
+ *              WriteTo): per datagram, its write call to its arrival at a
+ *              plain loopback socket; and the receive side, a peer's burst of
+ *              n datagrams to each sqobfs_pconn_read's return
+ *   cpu        the oracle's byte-loop WriteTo of one datagram (the
+ *              reference's per-call work on one core, no socket)
+ * Prints one JSON object (p50 / p99 in microseconds).  Built by
+ * `make -C sing-quic_amd tools`; run by bench.py --latency. */
+#define _GNU_SOURCE
+#include <arpa/inet.h>
+#include <errno.h>
+#include <netinet/in.h>
+#include <poll.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/socket.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "sqobfs.h"
+
+/* oracle restatement of SalamanderPacketConn.WriteTo (checker / CPU timing) */
+long or_salamander_write(const uint8_t *psk, size_t psk_len, const uint8_t salt[8],
+                         const uint8_t *p, size_t len, uint8_t *wire);
+
+#define CHECK(x)                                                                   \
+  do {                                                                             \
+    int st_ = (x);                                                                 \
+    if (st_ != SQ_OK) {                                                            \
+      fprintf(stderr, "%s:%d %s -> %d (%s)\n", __FILE__, __LINE__, #x, st_,        \
+              sqobfs_strerror(st_));                                               \
+      exit(1);                                                                     \
+    }                                                                              \
+  } while (0)
+
+static const uint8_t PSK[] = "sing-quic-mi355x-bench-psk";
+#define PL (sizeof PSK - 1)
+#define L 1350
+#define SLOT 2048
+#define MAXN 256
+
+static double now_us(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
+}
+
+static int cmpd(const void *a, const void *b) {
+  const double x = *(const double *)a, y = *(const double *)b;
+  return x < y ? -1 : x > y;
+}
+static double pct(double *v, int n, double q) {
+  qsort(v, (size_t)n, sizeof *v, cmpd);
+  int i = (int)(q * (n - 1) + 0.5);
+  return v[i];
+}
+
+static int udp_socket(uint16_t *port) {
+  int fd = socket(AF_INET, SOCK_DGRAM, 0);
+  int big = 8 << 20;
+  setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &big, sizeof big);
+  setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &big, sizeof big);
+  struct sockaddr_in a;
+  memset(&a, 0, sizeof a);
+  a.sin_family = AF_INET;
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  bind(fd, (struct sockaddr *)&a, sizeof a);
+  socklen_t sl = sizeof a;
+  getsockname(fd, (struct sockaddr *)&a, &sl);
+  *port = ntohs(a.sin_port);
+  return fd;
+}
+
+static sqobfs_addr loop_addr(uint16_t port) {
+  sqobfs_addr x;
+  memset(&x, 0, sizeof x);
+  x.family = AF_INET;
+  x.port = port;
+  x.addr[0] = 127;
+  x.addr[3] = 1;
+  return x;
+}
+
+static long recv_to(int fd, uint8_t *buf, size_t cap, int ms) {
+  struct pollfd p = {fd, POLLIN, 0};
+  if (poll(&p, 1, ms) <= 0) return -1;
+  return recv(fd, buf, cap, 0);
+}
+
+static const int SIZES[] = {1, 16, 64, 256};
+#define NS 4
+static int iters_for(int n) { return n <= 16 ? 400 : n <= 64 ? 200 : 100; }
+
+static void print_stat(const char *name, double *v, int n, int last) {
+  const double p50 = pct(v, n, 0.5), p99 = pct(v, n, 0.99);
+  printf("\"%s\": {\"p50_us\": %.1f, \"p99_us\": %.1f, \"samples\": %d}%s", name, p50, p99, n,
+         last ? "" : ", ");
+}
+
+int main(void) {
+  sqobfs_ctx *ctx;
+  CHECK(sqobfs_open(0, &ctx));
+  uint64_t off0 = 0;
+  uint32_t len0 = PL;
+  sqobfs_keyring *kr;
+  CHECK(sqobfs_keyring_create(ctx, SQOBFS_SALAMANDER, 1, PSK, &off0, &len0, &kr));
+  static double v[MAXN * 400];
+  printf("{");
+
+  /* ---- run_host on page-locked slots (the Go Slots.Run path) */
+  {
+    uint8_t *data;
+    CHECK(sqobfs_host_alloc(ctx, 2ull * MAXN * SLOT, (void **)&data));
+    static uint64_t in_off[MAXN], out_off[MAXN];
+    static uint32_t in_len[MAXN], out_len[MAXN];
+    static uint8_t salt[8 * MAXN];
+    for (int i = 0; i < MAXN; i++) {
+      in_off[i] = (uint64_t)i * SLOT;
+      out_off[i] = (uint64_t)(MAXN + i) * SLOT;
+      in_len[i] = L;
+    }
+    memset(data, 7, 2ull * MAXN * SLOT);
+    printf("\"run_host\": {");
+    for (int k = 0; k < NS; k++) {
+      const int n = SIZES[k], it = iters_for(n);
+      sqobfs_batch b;
+      memset(&b, 0, sizeof b);
+      b.n = (uint32_t)n;
+      b.flags = SQOBFS_FLAG_OUT_UNINIT;
+      b.in = data;
+      b.in_off = in_off;
+      b.in_len = in_len;
+      b.out = data;
+      b.out_off = out_off;
+      b.out_len = out_len;
+      b.salt = salt;
+      for (int w = 0; w < 20; w++) CHECK(sqobfs_run_host(ctx, kr, SQOBFS_OBFUSCATE, &b));
+      for (int i = 0; i < it; i++) {
+        const double t0 = now_us();
+        CHECK(sqobfs_run_host(ctx, kr, SQOBFS_OBFUSCATE, &b));
+        v[i] = now_us() - t0;
+      }
+      char nm[16];
+      snprintf(nm, sizeof nm, "%d", n);
+      print_stat(nm, v, it, k == NS - 1);
+    }
+    printf("}, ");
+    sqobfs_host_free(ctx, data);
+  }
+
+  /* ---- one launch on mapped slots + wait, per unit size */
+  {
+    uint8_t *blk;
+    const size_t slots = (size_t)MAXN * SLOT;
+    CHECK(sqobfs_host_alloc(ctx, slots + (size_t)MAXN * 24, (void **)&blk));
+    uint64_t *in_off = (uint64_t *)(blk + slots), *out_off = in_off + MAXN;
+    uint32_t *len = (uint32_t *)(out_off + MAXN), *out_len = len + MAXN;
+    for (int i = 0; i < MAXN; i++) {
+      in_off[i] = (uint64_t)i * SLOT + 8;
+      out_off[i] = (uint64_t)i * SLOT;
+      len[i] = L;
+    }
+    void *s = sqobfs_stream(ctx);
+    CHECK(sqobfs_set_sync_spin(ctx, 500));
+    static const uint32_t units[] = {0, 1, 2, 4, 8, 16, 26};
+    printf("\"mapped\": {");
+    for (int u = 0; u < 7; u++) {
+      CHECK(sqobfs_set_unit_packets(ctx, units[u]));
+      if (units[u]) printf("\"unit_%u\": {", units[u]);
+      else printf("\"unit_auto\": {");
+      for (int k = 0; k < NS; k++) {
+        const int n = SIZES[k], it = iters_for(n);
+        if (units[u] && n != MAXN) continue; /* the sweep is for the 256 batch */
+        sqobfs_batch b;
+        memset(&b, 0, sizeof b);
+        b.n = (uint32_t)n;
+        b.flags = SQOBFS_FLAG_DEVICE_SALT;
+        b.in = blk;
+        b.in_off = in_off;
+        b.in_len = len;
+        b.out = blk;
+        b.out_off = out_off;
+        b.out_len = out_len;
+        for (int w = 0; w < 20; w++) {
+          CHECK(sqobfs_launch(ctx, kr, SQOBFS_OBFUSCATE, &b, s));
+          CHECK(sqobfs_sync(ctx, s));
+        }
+        for (int i = 0; i < it; i++) {
+          const double t0 = now_us();
+          CHECK(sqobfs_launch(ctx, kr, SQOBFS_OBFUSCATE, &b, s));
+          CHECK(sqobfs_sync(ctx, s));
+          v[i] = now_us() - t0;
+        }
+        char nm[16];
+        snprintf(nm, sizeof nm, "%d", n);
+        print_stat(nm, v, it, units[u] || k == NS - 1);
+      }
+      printf("}%s", u == 6 ? "" : ", ");
+    }
+    printf("}, ");
+    CHECK(sqobfs_set_unit_packets(ctx, 0));
+    CHECK(sqobfs_set_sync_spin(ctx, 0));
+    sqobfs_host_free(ctx, blk);
+  }
+
+  /* ---- endpoint: sqobfs_udp_conn_write to a loopback socket */
+  {
+    uint16_t pa, pp;
+    int fa = udp_socket(&pa), fp = udp_socket(&pp);
+    sqobfs_udp_conn *c;
+    CHECK(sqobfs_udp_conn_open(ctx, kr, &fa, 1, MAXN, SLOT, &c));
+    static sqobfs_addr to[MAXN];
+    static uint32_t len[MAXN];
+    for (int i = 0; i < MAXN; i++) {
+      to[i] = loop_addr(pp);
+      len[i] = L;
+      memset(sqobfs_udp_conn_tx_payload(c, (uint32_t)i), 3, L);
+    }
+    uint8_t buf[4096];
+    printf("\"endpoint\": {");
+    for (int k = 0; k < NS; k++) {
+      const int n = SIZES[k], it = iters_for(n) / 2;
+      for (int i = 0; i < it + 10; i++) {
+        uint32_t sent;
+        const double t0 = now_us();
+        CHECK(sqobfs_udp_conn_write(c, 0, (uint32_t)n, len, to, &sent));
+        for (int j = 0; j < n; j++)
+          if (recv_to(fp, buf, sizeof buf, 2000) < 0) exit(2);
+        if (i >= 10) v[i - 10] = now_us() - t0;
+      }
+      char nm[16];
+      snprintf(nm, sizeof nm, "%d", n);
+      print_stat(nm, v, it, k == NS - 1);
+    }
+    printf("}, ");
+    sqobfs_udp_conn_close(c);
+    close(fa);
+    close(fp);
+  }
+
+  /* ---- pconn: WriteTo bursts -> arrival; peer bursts -> ReadFrom */
+  {
+    uint16_t pa, pp;
+    int fa = udp_socket(&pa), fp = udp_socket(&pp);
+    sqobfs_pconn *pc;
+    CHECK(sqobfs_pconn_open(ctx, kr, fa, NULL, &pc));
+    const sqobfs_addr to = loop_addr(pp);
+    static uint8_t pay[L], buf[4096], wire[MAXN][L + 8];
+    memset(pay, 5, L);
+    static double tw[MAXN];
+    printf("\"pconn_write\": {");
+    for (int k = 0; k < NS; k++) {
+      const int n = SIZES[k], it = iters_for(n) / 4 + 1;
+      int m = 0;
+      for (int i = 0; i < it + 5; i++) {
+        for (int j = 0; j < n; j++) {
+          tw[j] = now_us();
+          CHECK(sqobfs_pconn_write(pc, pay, L, &to, 0));
+        }
+        for (int j = 0; j < n; j++) {
+          if (recv_to(fp, buf, sizeof buf, 2000) < 0) exit(3);
+          if (i >= 5) v[m++] = now_us() - tw[j];
+        }
+      }
+      char nm[16];
+      snprintf(nm, sizeof nm, "%d", n);
+      print_stat(nm, v, m, k == NS - 1);
+    }
+    printf("}, ");
+    sqobfs_pconn_stats st0;
+    CHECK(sqobfs_pconn_stats_get(pc, &st0));
+    /* receive side: obfuscated datagrams from the peer */
+    for (int j = 0; j < MAXN; j++) {
+      uint8_t salt[8] = {(uint8_t)j, 1, 2, 3, 4, 5, 6, 7};
+      or_salamander_write(PSK, PL, salt, pay, L, wire[j]);
+    }
+    struct sockaddr_in a;
+    memset(&a, 0, sizeof a);
+    a.sin_family = AF_INET;
+    a.sin_port = htons(pa);
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    printf("\"pconn_read\": {");
+    for (int k = 0; k < NS; k++) {
+      const int n = SIZES[k], it = iters_for(n) / 4 + 1;
+      int m = 0;
+      for (int i = 0; i < it + 5; i++) {
+        const double t0 = now_us();
+        for (int j = 0; j < n; j++)
+          sendto(fp, wire[j], L + 8, 0, (struct sockaddr *)&a, sizeof a);
+        for (int j = 0; j < n; j++) {
+          uint32_t got;
+          CHECK(sqobfs_pconn_read(pc, buf, sizeof buf, &got, NULL, NULL));
+          if (got != L) exit(4);
+          if (i >= 5) v[m++] = now_us() - t0;
+        }
+      }
+      char nm[16];
+      snprintf(nm, sizeof nm, "%d", n);
+      print_stat(nm, v, m, k == NS - 1);
+    }
+    printf("}, ");
+    sqobfs_pconn_stats st;
+    CHECK(sqobfs_pconn_stats_get(pc, &st));
+    printf("\"pconn_stats\": {\"tx_datagrams\": %llu, \"tx_batches\": %llu, \"rx_datagrams\": %llu, "
+           "\"rx_batches\": %llu}, ",
+           (unsigned long long)st.tx_datagrams, (unsigned long long)st.tx_batches,
+           (unsigned long long)st.rx_datagrams, (unsigned long long)st.rx_batches);
+    sqobfs_pconn_close(pc);
+    close(fa);
+    close(fp);
+  }
+
+  /* ---- the reference's per-datagram work, one core (oracle byte loops) */
+  {
+    static uint8_t pay[L], wire[L + 8];
+    uint8_t salt[8] = {1};
+    for (int i = 0; i < 2000; i++) {
+      const double t0 = now_us();
+      or_salamander_write(PSK, PL, salt, pay, L, wire);
+      v[i] = now_us() - t0;
+    }
+    printf("\"cpu_oracle_write_1350B\": {\"p50_us\": %.2f, \"p99_us\": %.2f}", pct(v, 2000, 0.5),
+           pct(v, 2000, 0.99));
+  }
+  printf("}\n");
+  sqobfs_keyring_destroy(kr);
+  sqobfs_close(ctx);
+  return 0;
+}

@@ -1,0 +1,588 @@
+/* Threaded tests of the obfuscating packet conn engine (sqobfs_pconn_*, the
+ * core under go/sqobfs.Conn) over loopback UDP, checked against the oracle's
+ * restatement of the reference decorators (oracle/oracle.c:
+ * SalamanderPacketConn / XPlusPacketConn ReadFrom / WriteTo,
+ * hysteria2/salamander.go:42-93, hysteria/xplus.go:46-98).
+ *
+ *   wire      socket mode: every datagram written is, byte for byte, the
+ *             reference's WriteTo output for its (device) salt
+ *   read      socket mode: every datagram a peer sends (oracle-obfuscated,
+ *             short, cut by a small read buffer) reads back exactly as the
+ *             reference's ReadFrom returns it
+ *   roundtrip two pconns talking to each other, concurrent reader
+ *   deadline  a deadline set while ReadFrom blocks unblocks it with
+ *             SQ_ETIMEDOUT; a passed deadline fails at once, even with data
+ *             queued (net.Conn semantics); clearing it restores reads
+ *   shutdown  a blocked ReadFrom returns SQ_ECLOSED; Close with every
+ *             receive batch full and no reader returns promptly; writes
+ *             queued before Close still go out
+ *   pump      the generic-PacketConn mode (tx_take / rx_push) with tags
+ *   memory    sqobfs_host_alloc blocks balance after every Close
+ * Build and run: tests/test_pconn.py (gcc, -lsqobfs -loracle -lpthread). */
+#define _GNU_SOURCE
+#include <arpa/inet.h>
+#include <errno.h>
+#include <netinet/in.h>
+#include <poll.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/socket.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "oracle.h"
+#include "sqobfs.h"
+
+#define FAIL(...)                                            \
+  do {                                                       \
+    fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__);     \
+    fprintf(stderr, __VA_ARGS__);                            \
+    fputc('\n', stderr);                                     \
+    exit(1);                                                 \
+  } while (0)
+#define CHECK(x)                                                           \
+  do {                                                                     \
+    int st_ = (x);                                                         \
+    if (st_ != SQ_OK) FAIL("%s -> %d (%s)", #x, st_, sqobfs_strerror(st_)); \
+  } while (0)
+#define EXPECT(c, ...) \
+  do {                 \
+    if (!(c)) FAIL(__VA_ARGS__); \
+  } while (0)
+
+static const uint8_t PSK[] = "sing-quic-mi355x-bench-psk";
+#define PL (sizeof PSK - 1)
+#define MAXW 4096
+
+static sqobfs_ctx *g_ctx;
+
+static double now_s(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+static int64_t unix_ns(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  return (int64_t)ts.tv_sec * 1000000000 + ts.tv_nsec;
+}
+static void sleep_ms(int ms) {
+  struct timespec ts = {ms / 1000, (long)(ms % 1000) * 1000000};
+  nanosleep(&ts, NULL);
+}
+
+static uint64_t rng_state = 0x9E3779B97F4A7C15ull;
+static uint32_t rnd(void) {
+  rng_state ^= rng_state << 13;
+  rng_state ^= rng_state >> 7;
+  rng_state ^= rng_state << 17;
+  return (uint32_t)rng_state;
+}
+
+static int udp_socket(uint16_t *port) {
+  int fd = socket(AF_INET, SOCK_DGRAM, 0);
+  if (fd < 0) FAIL("socket: %s", strerror(errno));
+  int big = 8 << 20;
+  setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &big, sizeof big);
+  setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &big, sizeof big);
+  struct sockaddr_in a;
+  memset(&a, 0, sizeof a);
+  a.sin_family = AF_INET;
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  if (bind(fd, (struct sockaddr *)&a, sizeof a)) FAIL("bind: %s", strerror(errno));
+  socklen_t sl = sizeof a;
+  getsockname(fd, (struct sockaddr *)&a, &sl);
+  *port = ntohs(a.sin_port);
+  return fd;
+}
+
+static sqobfs_addr loop_addr(uint16_t port) {
+  sqobfs_addr x;
+  memset(&x, 0, sizeof x);
+  x.family = AF_INET;
+  x.port = port;
+  x.addr[0] = 127;
+  x.addr[3] = 1;
+  return x;
+}
+
+static void send_to(int fd, uint16_t port, const uint8_t *p, size_t n) {
+  struct sockaddr_in a;
+  memset(&a, 0, sizeof a);
+  a.sin_family = AF_INET;
+  a.sin_port = htons(port);
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  if (sendto(fd, p, n, 0, (struct sockaddr *)&a, sizeof a) != (ssize_t)n)
+    FAIL("sendto: %s", strerror(errno));
+}
+
+/* recv with a timeout: -1 on timeout */
+static long recv_to(int fd, uint8_t *buf, size_t cap, int ms) {
+  struct pollfd p = {fd, POLLIN, 0};
+  if (poll(&p, 1, ms) <= 0) return -1;
+  return recv(fd, buf, cap, 0);
+}
+
+static sqobfs_keyring *keyring(int kind) {
+  uint64_t off = 0;
+  uint32_t len = PL;
+  sqobfs_keyring *kr = NULL;
+  CHECK(sqobfs_keyring_create(g_ctx, kind, 1, PSK, &off, &len, &kr));
+  return kr;
+}
+
+static int salt_len(int kind) { return kind == SQOBFS_SALAMANDER ? 8 : 16; }
+
+/* the reference's WriteTo for this salt: wire must equal it byte for byte */
+static long ref_write(int kind, const uint8_t *salt, const uint8_t *p, size_t n, uint8_t *wire) {
+  return kind == SQOBFS_SALAMANDER ? or_salamander_write(PSK, PL, salt, p, n, wire)
+                                   : or_xplus_write(PSK, PL, salt, p, n, wire);
+}
+
+/* the reference's ReadFrom of datagram w (w_len bytes) into a buffer of cap
+ * bytes: returns its n, and p[0..n) */
+static long ref_read(int kind, const uint8_t *w, size_t w_len, size_t cap, uint8_t *p) {
+  const size_t m = w_len < cap ? w_len : cap;
+  static uint8_t buf[MAXW + 64];
+  memset(buf, 0, sizeof buf);
+  memcpy(buf, w, m);
+  long r = kind == SQOBFS_SALAMANDER ? or_salamander_read(PSK, PL, buf, m)
+                                     : or_xplus_read(PSK, PL, buf, m, cap < MAXW ? cap : MAXW);
+  if (r > 0) memcpy(p, buf, (size_t)r);
+  return r;
+}
+
+static uint32_t pick_len(int i, int S, uint32_t slot) {
+  static const uint32_t edge[] = {0, 1, 7, 8, 9, 15, 16, 17, 31, 32, 33, 63, 64, 65, 127, 128, 129};
+  const uint32_t ne = sizeof edge / sizeof edge[0];
+  if ((uint32_t)i < ne) return edge[i];
+  if (i % 97 == 0) return slot - (uint32_t)S; /* the largest payload a slot takes */
+  if (i % 5 == 0) return 1200 + rnd() % 253;  /* QUIC-sized */
+  return rnd() % (slot - (uint32_t)S + 1);
+}
+
+/* ------------------------------------------------------------ wire */
+typedef struct {
+  int fd, n;
+  uint8_t (*wire)[MAXW];
+  long *wlen;
+} PeerRx;
+
+static void *peer_rx(void *arg) {
+  PeerRx *r = arg;
+  for (int i = 0; i < r->n; i++) {
+    r->wlen[i] = recv_to(r->fd, r->wire[i], MAXW, 5000);
+    if (r->wlen[i] < 0) {
+      r->n = i;
+      break;
+    }
+  }
+  return NULL;
+}
+
+static void t_wire(int kind) {
+  const int S = salt_len(kind), N = 1500;
+  const int64_t a0 = sqobfs_debug_host_allocs();
+  sqobfs_keyring *kr = keyring(kind);
+  uint16_t pa, pp;
+  int fa = udp_socket(&pa), fp = udp_socket(&pp);
+  sqobfs_pconn *pc = NULL;
+  CHECK(sqobfs_pconn_open(g_ctx, kr, fa, NULL, &pc));
+  static uint8_t pay[1500][MAXW], wire[1500][MAXW];
+  static uint32_t plen[1500];
+  static long wlen[1500];
+  PeerRx r = {fp, N, wire, wlen};
+  pthread_t th;
+  pthread_create(&th, NULL, peer_rx, &r);
+  const sqobfs_addr to = loop_addr(pp);
+  for (int i = 0; i < N; i++) {
+    plen[i] = pick_len(i, S, 2048);
+    for (uint32_t j = 0; j < plen[i]; j++) pay[i][j] = (uint8_t)rnd();
+    CHECK(sqobfs_pconn_write(pc, pay[i], plen[i], &to, (uint64_t)i));
+    if (i % 200 == 199) sleep_ms(2); /* bursts with gaps: small and large batches */
+  }
+  pthread_join(th, NULL);
+  EXPECT(r.n == N, "kind %d: peer got %d of %d datagrams", kind, r.n, N);
+  for (int i = 0; i < N; i++) {
+    EXPECT(wlen[i] == (long)plen[i] + S, "kind %d dgram %d: wire %ld for payload %u", kind, i,
+           wlen[i], plen[i]);
+    uint8_t ref[MAXW];
+    ref_write(kind, wire[i], pay[i], plen[i], ref); /* its salt, the reference's bytes */
+    EXPECT(!memcmp(ref, wire[i], (size_t)wlen[i]), "kind %d dgram %d: wire differs", kind, i);
+  }
+  sqobfs_pconn_stats st;
+  CHECK(sqobfs_pconn_stats_get(pc, &st));
+  EXPECT(st.tx_datagrams == (uint64_t)N, "tx_datagrams %llu", (unsigned long long)st.tx_datagrams);
+  printf("  wire kind %d: %d datagrams in %llu batches (max %u), wire == reference\n", kind, N,
+         (unsigned long long)st.tx_batches, st.tx_max_batch);
+  sqobfs_pconn_close(pc);
+  close(fa);
+  close(fp);
+  sqobfs_keyring_destroy(kr);
+  EXPECT(sqobfs_debug_host_allocs() == a0, "host allocs %lld -> %lld", (long long)a0,
+         (long long)sqobfs_debug_host_allocs());
+}
+
+/* ------------------------------------------------------------ read */
+static void t_read(int kind) {
+  const int S = salt_len(kind), N = 1200;
+  const int64_t a0 = sqobfs_debug_host_allocs();
+  sqobfs_keyring *kr = keyring(kind);
+  uint16_t pa, pp;
+  int fa = udp_socket(&pa), fp = udp_socket(&pp);
+  sqobfs_pconn *pc = NULL;
+  sqobfs_pconn_opts o;
+  memset(&o, 0, sizeof o);
+  o.batch = 64; /* several batches per burst */
+  CHECK(sqobfs_pconn_open(g_ctx, kr, fa, &o, &pc));
+  static uint8_t wire[1200][MAXW];
+  static uint32_t wl[1200];
+  int sent = 0;
+  for (int burst = 0; sent < N; burst++) {
+    const int k = burst % 3 == 0 ? 1 : 1 + (int)(rnd() % 150);
+    const int base = sent;
+    for (int j = 0; j < k && sent < N; j++, sent++) {
+      const int i = sent;
+      if (i % 9 == 4) { /* short datagrams: n <= 8 (Salamander), n < 16 (XPlus) */
+        wl[i] = rnd() % (uint32_t)(S + 3);
+        for (uint32_t b = 0; b < wl[i]; b++) wire[i][b] = (uint8_t)rnd();
+      } else {
+        uint8_t salt[16], pay[MAXW];
+        for (int b = 0; b < 16; b++) salt[b] = (uint8_t)rnd();
+        const uint32_t L = pick_len(i, S, 2048);
+        for (uint32_t b = 0; b < L; b++) pay[b] = (uint8_t)rnd();
+        ref_write(kind, salt, pay, L, wire[i]);
+        wl[i] = L + (uint32_t)S;
+      }
+      send_to(fp, pa, wire[i], wl[i]);
+    }
+    /* read the burst back with varying buffer sizes (len(p)) */
+    for (int i = base; i < sent; i++) {
+      uint32_t cap = 4096;
+      if (i % 13 == 6) cap = 1 + rnd() % 40;     /* cut inside / near the salt */
+      else if (i % 11 == 3) cap = 64 + rnd() % 600;
+      uint8_t got[MAXW], ref[MAXW];
+      uint32_t n = 0;
+      sqobfs_addr from;
+      uint64_t tag;
+      CHECK(sqobfs_pconn_read(pc, got, cap, &n, &from, &tag));
+      const long want = ref_read(kind, wire[i], wl[i], cap, ref);
+      EXPECT((long)n == want, "kind %d dgram %d (wire %u, cap %u): n %u want %ld", kind, i, wl[i],
+             cap, n, want);
+      EXPECT(!n || !memcmp(got, ref, n), "kind %d dgram %d: payload differs", kind, i);
+      EXPECT(from.port == pp && from.family == AF_INET, "kind %d: source address", kind);
+    }
+  }
+  sqobfs_pconn_stats st;
+  CHECK(sqobfs_pconn_stats_get(pc, &st));
+  printf("  read kind %d: %d datagrams in %llu batches (max %u), == reference ReadFrom\n", kind, N,
+         (unsigned long long)st.rx_batches, st.rx_max_batch);
+  sqobfs_pconn_close(pc);
+  close(fa);
+  close(fp);
+  sqobfs_keyring_destroy(kr);
+  EXPECT(sqobfs_debug_host_allocs() == a0, "host allocs leak");
+}
+
+/* ------------------------------------------------------------ roundtrip */
+typedef struct {
+  sqobfs_pconn *pc;
+  int kind, n, got, bad;
+  uint32_t *plen;
+  uint8_t (*pay)[2048];
+} Reader;
+
+static void *reader(void *arg) {
+  Reader *r = arg;
+  CHECK(sqobfs_pconn_set_deadline(r->pc, SQOBFS_PCONN_READ, unix_ns() + 5000000000ll));
+  for (int i = 0; i < r->n; i++) {
+    uint8_t buf[MAXW];
+    uint32_t n;
+    const int st = sqobfs_pconn_read(r->pc, buf, sizeof buf, &n, NULL, NULL);
+    if (st != SQ_OK) break;
+    if (r->kind == SQOBFS_SALAMANDER && r->plen[i] == 0) {
+      /* an empty payload's datagram is the bare 8-byte salt, and
+       * salamander.go:47-49 returns datagrams of n <= 8 as they are */
+      if (n != 8) r->bad++;
+    } else if (n != r->plen[i] || memcmp(buf, r->pay[i], n)) {
+      r->bad++;
+    }
+    r->got++;
+  }
+  return NULL;
+}
+
+static void t_roundtrip(int kind) {
+  const int S = salt_len(kind), N = 3000;
+  const int64_t a0 = sqobfs_debug_host_allocs();
+  sqobfs_keyring *kr = keyring(kind);
+  uint16_t pa, pb;
+  int fa = udp_socket(&pa), fb = udp_socket(&pb);
+  sqobfs_pconn *A = NULL, *B = NULL;
+  CHECK(sqobfs_pconn_open(g_ctx, kr, fa, NULL, &A));
+  CHECK(sqobfs_pconn_open(g_ctx, kr, fb, NULL, &B));
+  static uint8_t pay[3000][2048];
+  static uint32_t plen[3000];
+  for (int i = 0; i < N; i++) {
+    plen[i] = pick_len(i, S, 2048);
+    for (uint32_t j = 0; j < plen[i]; j++) pay[i][j] = (uint8_t)rnd();
+  }
+  Reader r = {B, kind, N, 0, 0, plen, pay};
+  pthread_t th;
+  pthread_create(&th, NULL, reader, &r);
+  const sqobfs_addr to = loop_addr(pb);
+  const double t0 = now_s();
+  for (int i = 0; i < N; i++) {
+    CHECK(sqobfs_pconn_write(A, pay[i], plen[i], &to, 0));
+    if (i % 256 == 255) sleep_ms(1); /* stay inside the socket buffers */
+  }
+  pthread_join(th, NULL);
+  const double dt = now_s() - t0;
+  EXPECT(r.got == N && r.bad == 0, "kind %d roundtrip: got %d bad %d of %d", kind, r.got, r.bad, N);
+  printf("  roundtrip kind %d: %d datagrams A -> B in %.1f ms\n", kind, N, dt * 1e3);
+  sqobfs_pconn_close(A);
+  sqobfs_pconn_close(B);
+  close(fa);
+  close(fb);
+  sqobfs_keyring_destroy(kr);
+  EXPECT(sqobfs_debug_host_allocs() == a0, "host allocs leak");
+}
+
+/* ------------------------------------------------------------ deadlines */
+typedef struct {
+  sqobfs_pconn *pc;
+  int st;
+  double t;
+} Blocked;
+
+static void *blocked_read(void *arg) {
+  Blocked *b = arg;
+  uint8_t buf[MAXW];
+  uint32_t n;
+  const double t0 = now_s();
+  b->st = sqobfs_pconn_read(b->pc, buf, sizeof buf, &n, NULL, NULL);
+  b->t = now_s() - t0;
+  return NULL;
+}
+
+static void t_deadline(void) {
+  const int64_t a0 = sqobfs_debug_host_allocs();
+  sqobfs_keyring *kr = keyring(SQOBFS_SALAMANDER);
+  uint16_t pa, pp;
+  int fa = udp_socket(&pa), fp = udp_socket(&pp);
+  sqobfs_pconn *pc = NULL;
+  CHECK(sqobfs_pconn_open(g_ctx, kr, fa, NULL, &pc));
+  /* 1. ReadFrom blocks; a deadline set meanwhile unblocks it */
+  Blocked b = {pc, 1, 0};
+  pthread_t th;
+  pthread_create(&th, NULL, blocked_read, &b);
+  sleep_ms(50);
+  CHECK(sqobfs_pconn_set_deadline(pc, SQOBFS_PCONN_READ, unix_ns() + 40 * 1000000ll));
+  pthread_join(th, NULL);
+  EXPECT(b.st == SQ_ETIMEDOUT, "blocked read returned %d, want SQ_ETIMEDOUT", b.st);
+  EXPECT(b.t > 0.08 && b.t < 2.0, "blocked read took %.3f s", b.t);
+  /* 2. a passed deadline fails at once, even with a datagram queued */
+  uint8_t w[64], salt[8] = {1, 2, 3, 4, 5, 6, 7, 8}, p[32] = {9};
+  ref_write(SQOBFS_SALAMANDER, salt, p, 32, w);
+  send_to(fp, pa, w, 40);
+  sleep_ms(50);
+  CHECK(sqobfs_pconn_set_deadline(pc, SQOBFS_PCONN_READ, unix_ns() - 1));
+  uint8_t buf[MAXW];
+  uint32_t n;
+  double t0 = now_s();
+  EXPECT(sqobfs_pconn_read(pc, buf, sizeof buf, &n, NULL, NULL) == SQ_ETIMEDOUT,
+         "passed deadline must fail");
+  EXPECT(now_s() - t0 < 0.05, "passed deadline must fail at once");
+  /* 3. cleared: the queued datagram reads */
+  CHECK(sqobfs_pconn_set_deadline(pc, SQOBFS_PCONN_READ, 0));
+  CHECK(sqobfs_pconn_read(pc, buf, sizeof buf, &n, NULL, NULL));
+  EXPECT(n == 32 && !memcmp(buf, p, 32), "datagram after clearing the deadline");
+  /* 4. write deadline (SetWriteDeadline): passed -> SQ_ETIMEDOUT, cleared -> ok */
+  const sqobfs_addr to = loop_addr(pp);
+  CHECK(sqobfs_pconn_set_deadline(pc, SQOBFS_PCONN_WRITE, unix_ns() - 1));
+  EXPECT(sqobfs_pconn_write(pc, p, 32, &to, 0) == SQ_ETIMEDOUT, "passed write deadline");
+  CHECK(sqobfs_pconn_set_deadline(pc, SQOBFS_PCONN_READ | SQOBFS_PCONN_WRITE, 0));
+  CHECK(sqobfs_pconn_write(pc, p, 32, &to, 0));
+  EXPECT(recv_to(fp, buf, sizeof buf, 2000) == 40, "write after clearing the deadline");
+  /* 5. SetDeadline in the future does not disturb a read that completes */
+  CHECK(sqobfs_pconn_set_deadline(pc, SQOBFS_PCONN_READ, unix_ns() + 2000000000ll));
+  send_to(fp, pa, w, 40);
+  CHECK(sqobfs_pconn_read(pc, buf, sizeof buf, &n, NULL, NULL));
+  EXPECT(n == 32, "read under a future deadline");
+  printf("  deadline: blocked ReadFrom unblocked after %.0f ms (deadline set at 50 + 40 ms)\n",
+         b.t * 1e3);
+  sqobfs_pconn_close(pc);
+  close(fa);
+  close(fp);
+  sqobfs_keyring_destroy(kr);
+  EXPECT(sqobfs_debug_host_allocs() == a0, "host allocs leak");
+}
+
+/* ------------------------------------------------------------ shutdown */
+static void t_shutdown(void) {
+  const int64_t a0 = sqobfs_debug_host_allocs();
+  sqobfs_keyring *kr = keyring(SQOBFS_XPLUS);
+  uint16_t pa, pp;
+  int fa = udp_socket(&pa), fp = udp_socket(&pp);
+  /* 1. Close wakes a blocked ReadFrom with SQ_ECLOSED */
+  sqobfs_pconn *pc = NULL;
+  CHECK(sqobfs_pconn_open(g_ctx, kr, fa, NULL, &pc));
+  Blocked b = {pc, 1, 0};
+  pthread_t th;
+  pthread_create(&th, NULL, blocked_read, &b);
+  sleep_ms(30);
+  double t0 = now_s();
+  sqobfs_pconn_shutdown(pc);
+  pthread_join(th, NULL);
+  EXPECT(b.st == SQ_ECLOSED, "read after shutdown returned %d", b.st);
+  EXPECT(now_s() - t0 < 1.0, "shutdown took %.3f s", now_s() - t0);
+  uint8_t buf[MAXW];
+  uint32_t n;
+  EXPECT(sqobfs_pconn_read(pc, buf, sizeof buf, &n, NULL, NULL) == SQ_ECLOSED, "read after close");
+  const sqobfs_addr to = loop_addr(pp);
+  EXPECT(sqobfs_pconn_write(pc, buf, 10, &to, 0) == SQ_ECLOSED, "write after close");
+  sqobfs_pconn_close(pc);
+  /* 2. Close while every receive batch is full and nobody reads */
+  sqobfs_pconn_opts o;
+  memset(&o, 0, sizeof o);
+  o.batch = 32;
+  o.rx_batches = 2;
+  CHECK(sqobfs_pconn_open(g_ctx, kr, fa, &o, &pc));
+  uint8_t w[1216], salt[16] = {7}, p[1200] = {3};
+  ref_write(SQOBFS_XPLUS, salt, p, 1200, w);
+  for (int i = 0; i < 400; i++) send_to(fp, pa, w, sizeof w);
+  sqobfs_pconn_stats st;
+  for (int k = 0; k < 200; k++) {
+    CHECK(sqobfs_pconn_stats_get(pc, &st));
+    if (st.rx_batches >= 2) break; /* both receive batches ready, none read */
+    sleep_ms(5);
+  }
+  EXPECT(st.rx_batches >= 2, "receive batches did not fill (%llu)",
+         (unsigned long long)st.rx_batches);
+  sleep_ms(20);
+  t0 = now_s();
+  sqobfs_pconn_close(pc);
+  const double tc = now_s() - t0;
+  EXPECT(tc < 1.0, "close with full receive batches took %.3f s", tc);
+  /* drain the socket */
+  while (recv_to(fa, buf, sizeof buf, 10) >= 0) {
+  }
+  /* 3. datagrams written just before Close still go out */
+  CHECK(sqobfs_pconn_open(g_ctx, kr, fa, NULL, &pc));
+  for (int i = 0; i < 100; i++) CHECK(sqobfs_pconn_write(pc, p, 1200, &to, 0));
+  sqobfs_pconn_close(pc);
+  int got = 0;
+  while (recv_to(fp, buf, sizeof buf, 200) == 1216) got++;
+  EXPECT(got == 100, "%d of 100 datagrams written before Close were sent", got);
+  printf("  shutdown: blocked read -> SQ_ECLOSED; close with full rx batches %.1f ms; "
+         "writes before close sent\n", tc * 1e3);
+  close(fa);
+  close(fp);
+  sqobfs_keyring_destroy(kr);
+  EXPECT(sqobfs_debug_host_allocs() == a0, "host allocs leak");
+}
+
+/* ------------------------------------------------------------ pump */
+typedef struct {
+  sqobfs_pconn *pc;
+  int kind, count, bad;
+  uint8_t (*pay)[2048];
+  uint32_t *plen;
+} Taker;
+
+static void *taker(void *arg) {
+  Taker *t = arg;
+  for (;;) {
+    sqobfs_pconn_tx v;
+    const int st = sqobfs_pconn_tx_take(t->pc, 100, &v);
+    if (st == SQ_ETIMEDOUT) continue;
+    if (st != SQ_OK) break;
+    for (uint32_t i = 0; i < v.count; i++) {
+      const uint8_t *w = v.base + v.off[i];
+      const uint64_t id = v.tag[i];
+      uint8_t ref[MAXW];
+      ref_write(t->kind, w, t->pay[id], t->plen[id], ref);
+      if (v.len[i] != t->plen[id] + (uint32_t)salt_len(t->kind) || memcmp(ref, w, v.len[i]))
+        t->bad++;
+      t->count++;
+    }
+    CHECK(sqobfs_pconn_tx_done(t->pc));
+  }
+  return NULL;
+}
+
+static void t_pump(int kind) {
+  const int S = salt_len(kind), N = 2000;
+  const int64_t a0 = sqobfs_debug_host_allocs();
+  sqobfs_keyring *kr = keyring(kind);
+  sqobfs_pconn *pc = NULL;
+  CHECK(sqobfs_pconn_open(g_ctx, kr, -1, NULL, &pc));
+  static uint8_t pay[2000][2048];
+  static uint32_t plen[2000];
+  for (int i = 0; i < N; i++) {
+    plen[i] = pick_len(i, S, 2048);
+    for (uint32_t j = 0; j < plen[i]; j++) pay[i][j] = (uint8_t)rnd();
+  }
+  Taker t = {pc, kind, 0, 0, pay, plen};
+  pthread_t th;
+  pthread_create(&th, NULL, taker, &t);
+  /* transmit: tags carry the caller's address handle */
+  for (int i = 0; i < N; i++) CHECK(sqobfs_pconn_write(pc, pay[i], plen[i], NULL, (uint64_t)i));
+  /* receive: pushed datagrams read back as the reference's ReadFrom */
+  for (int i = 0; i < N; i++) {
+    uint8_t salt[16], w[MAXW], got[MAXW], ref[MAXW];
+    for (int b = 0; b < 16; b++) salt[b] = (uint8_t)rnd();
+    ref_write(kind, salt, pay[i], plen[i], w);
+    const uint32_t wl = (i % 17 == 5) ? (uint32_t)(rnd() % (unsigned)S) : plen[i] + (uint32_t)S;
+    CHECK(sqobfs_pconn_rx_push(pc, w, wl, NULL, 1000000 + (uint64_t)i));
+    uint32_t n;
+    uint64_t tag;
+    CHECK(sqobfs_pconn_read(pc, got, MAXW, &n, NULL, &tag));
+    const long want = ref_read(kind, w, wl, MAXW, ref);
+    EXPECT((long)n == want && (!n || !memcmp(got, ref, n)), "pump kind %d dgram %d", kind, i);
+    EXPECT(tag == 1000000 + (uint64_t)i, "pump tag");
+  }
+  /* Close drains what was written (the taker still runs) */
+  sqobfs_pconn_shutdown(pc);
+  pthread_join(th, NULL);
+  EXPECT(t.count == N && t.bad == 0, "pump kind %d: taken %d bad %d of %d", kind, t.count, t.bad, N);
+  /* the wrapped conn failed: readers get its status */
+  sqobfs_pconn_close(pc);
+  CHECK(sqobfs_pconn_open(g_ctx, kr, -1, NULL, &pc));
+  CHECK(sqobfs_pconn_rx_fail(pc, SQ_EIO, 1)); /* once: one reader sees it, reads go on */
+  uint8_t buf[64], w[40], s8[8] = {5}, p8[32] = {6};
+  uint32_t n;
+  EXPECT(sqobfs_pconn_read(pc, buf, sizeof buf, &n, NULL, NULL) == SQ_EIO, "rx_fail once");
+  ref_write(kind, s8, p8, (size_t)(40 - S), w);
+  CHECK(sqobfs_pconn_rx_push(pc, w, 40, NULL, 7));
+  CHECK(sqobfs_pconn_read(pc, buf, sizeof buf, &n, NULL, NULL));
+  EXPECT(n == (uint32_t)(40 - S), "read after a once error");
+  CHECK(sqobfs_pconn_rx_fail(pc, SQ_EIO, 0)); /* for good */
+  EXPECT(sqobfs_pconn_read(pc, buf, sizeof buf, &n, NULL, NULL) == SQ_EIO, "rx_fail status");
+  EXPECT(sqobfs_pconn_read(pc, buf, sizeof buf, &n, NULL, NULL) == SQ_EIO, "rx_fail sticky");
+  sqobfs_pconn_close(pc);
+  printf("  pump kind %d: %d datagrams taken == reference WriteTo, %d pushed == ReadFrom\n", kind,
+         N, N);
+  sqobfs_keyring_destroy(kr);
+  EXPECT(sqobfs_debug_host_allocs() == a0, "host allocs leak");
+}
+
+int main(int argc, char **argv) {
+  (void)argc;
+  (void)argv;
+  CHECK(sqobfs_open(0, &g_ctx));
+  for (int kind = 0; kind < 2; kind++) {
+    t_wire(kind);
+    t_read(kind);
+    t_roundtrip(kind);
+    t_pump(kind);
+  }
+  t_deadline();
+  t_shutdown();
+  sqobfs_close(g_ctx);
+  printf("ok: pconn engine (socket + pump modes, deadlines, shutdown, memory)\n");
+  return 0;
+}

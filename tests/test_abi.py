@@ -54,8 +54,8 @@ int main(void){printf("%zu %zu %zu %zu %zu\n", sizeof(sqobfs_batch),
 
 def test_abi_version_and_strerror():
     L = sqobfs.lib()
-    assert L.sqobfs_abi_version() == 3
-    for st in (0, -1, -2, -3, -4, -5):
+    assert L.sqobfs_abi_version() == 4
+    for st in (0, -1, -2, -3, -4, -5, -6, -7, -8):
         assert sqobfs.strerror(st) != "unknown status"
 
 
@@ -109,8 +109,19 @@ def test_unit_packets_for_sizes_units_by_bytes():
     assert f(1200 << 20, 1 << 20) == 18          # configs[2]
     assert f(758 * (4 << 20), 4 << 20) == 28     # configs[3] (mean of U[64, 1452])
     assert f(1350 * (16 << 20), 16 << 20, True) == 26  # configs[4]
-    assert f(64 * 1000, 1000) == 62 and f(0, 7) == 62
+    assert f(64 * 100_000, 100_000) == 49 and f(0, 1 << 20) == 62
     assert f(70_000 * 8, 8) == 1
     for mean in range(1, 100_000, 997):
         u = f(mean * 1000, 1000)
         assert 1 <= u <= 62
+
+
+def test_unit_packets_spread_small_batches():
+    """Small batches run as at least 2,048 wavefronts (latency: a 256-datagram
+    socket batch is 256 one-packet waves, not 10 waves of 26 packets)."""
+    f = sqobfs.unit_packets_for
+    for n in (1, 16, 64, 256, 1024, 2048):
+        assert f(1350 * n, n) == 1
+    assert f(1350 * 4096, 4096) == 2
+    assert f(1350 * 16384, 16384) == 8
+    assert f(64 * 8192, 8192) == 4  # short packets: the spread rule binds

@@ -29,12 +29,27 @@ def ctxs():
 
 @pytest.mark.parametrize("kind", [SALAMANDER, XPLUS])
 @pytest.mark.parametrize("direction", [OBFUSCATE, DEOBFUSCATE])
-def test_run_host_sharded_matches_single(ctxs, kind, direction):
+@pytest.mark.parametrize("layout", ["dense", "shuffled", "inplace"])
+def test_run_host_sharded_matches_single(ctxs, kind, direction, layout):
+    """'shuffled' permutes the packets so the shards' byte spans interleave and
+    'inplace' decodes / encodes in the input buffer: shards whose output span
+    meets another shard's span must not run at once (each copies its whole
+    span), so the batch runs on one context -- the result is the same."""
     rng = np.random.Generator(np.random.PCG64(500 + 2 * kind + direction))
     n = 30000
     lens = rng.integers(0, 1500, n)
     ids = rng.integers(0, len(PSKS), n)
-    hb = gh.make_case(rng, kind, direction, lens, PSKS, psk_ids=ids, in_align=1, out_align=1)
+    hb = gh.make_case(rng, kind, direction, lens, PSKS, psk_ids=ids, in_align=1, out_align=1,
+                      inplace=layout == "inplace")
+    if layout == "shuffled":
+        perm = rng.permutation(n)
+        S = sqobfs.SALT_LEN[kind]
+        hb.in_off, hb.in_len, hb.out_off = hb.in_off[perm], hb.in_len[perm], hb.out_off[perm]
+        if hb.salt is not None:
+            hb.salt = hb.salt.reshape(n, S)[perm].reshape(-1).copy()
+        hb.psk_id = hb.psk_id[perm]
+        if hb.in_cap is not None:
+            hb.in_cap = hb.in_cap[perm]
     ref = gh.run_oracle(kind, direction, PSKS, hb)
     one = gh.clone(hb)
     krs = [sqobfs.Keyring(c, kind, PSKS) for c in ctxs]
