@@ -73,10 +73,14 @@ def parse():
     ap.add_argument("--packets", type=int, default=0,
                     help="dev: override the config's packet count (scaling probes; not a "
                          "BASELINE configuration)")
-    ap.add_argument("--layout", default="dense", choices=["dense", "slot16", "inplace"],
+    ap.add_argument("--layout", default="dense",
+                    choices=["dense", "slot16", "slot2048", "inplace"],
                     help="dense: wire-dense outputs, wire-sized input slots (default); "
-                         "slot16: 16-byte-aligned slots; inplace: obfuscate in the input "
-                         "buffer (headroom layout, vectorised WriteTo semantics)")
+                         "slot16: every packet in its own 16-byte-aligned slot (inputs and "
+                         "outputs), launched with SQOBFS_FLAG_OUT_BLOCKS; slot2048: fixed "
+                         "2048-byte slots (the Go Slots / UDP endpoint geometry), same flag; "
+                         "inplace: obfuscate in the input buffer (headroom layout, "
+                         "vectorised WriteTo semantics)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL) for the timing barrier/max; gloo lets several "
                          "ranks share one GPU in tests")
@@ -121,10 +125,15 @@ def build_shard(torch, dev, kind, n, L, n_psk, rank, world, config, layout, firs
     else:
         lens = torch.full((n,), L, device=dev, dtype=torch.int64)
     lead = 64  # buffers start with 64 spare bytes
-    if layout == "slot16":
-        # every packet in its own 16-byte-aligned slot (pad bytes untouched)
-        in_slot = (lens + 15) // 16 * 16
-        out_slot = (lens + S + 15) // 16 * 16
+    if layout in ("slot16", "slot2048"):
+        # every packet in its own 16-byte-aligned slot (16 B-
+        # aligned input offsets), or in fixed 2048-byte slots
+        if layout == "slot16":
+            in_slot = (lens + 15) // 16 * 16
+            out_slot = (lens + S + 15) // 16 * 16
+        else:
+            in_slot = torch.full_like(lens, 2048)
+            out_slot = torch.full_like(lens, 2048)
         in_off = torch.cumsum(in_slot, 0) - in_slot + lead
         out_off = torch.cumsum(out_slot, 0) - out_slot + lead
     else:
@@ -144,7 +153,8 @@ def build_shard(torch, dev, kind, n, L, n_psk, rank, world, config, layout, firs
     # non-payload input bytes (lead, headroom / slot padding) are zero, so a
     # decoded batch can be compared with `data` as a whole buffer
     gap = in_slot - lens
-    gstart = (in_off - S) if layout != "slot16" else (in_off + lens)
+    slotted = layout in ("slot16", "slot2048")
+    gstart = (in_off - S) if not slotted else (in_off + lens)
     gidx = torch.repeat_interleave(gstart, gap) + (
         torch.arange(int(gap.sum().item()), device=dev)
         - torch.repeat_interleave(torch.cumsum(gap, 0) - gap, gap))
@@ -164,7 +174,7 @@ def build_shard(torch, dev, kind, n, L, n_psk, rank, world, config, layout, firs
     return dict(lens=lens.to(torch.int32), in_off=in_off, out_off=out_off, data=data, salt=salt,
                 out=out, out_len=torch.zeros(n, device=dev, dtype=torch.int32), psk_id=psk_id,
                 psks=psks, S=S, payload_bytes=int(lens.sum().item()),
-                inplace=layout == "inplace")
+                inplace=layout == "inplace", slotted=slotted)
 
 
 def sample_idx(n):
@@ -204,6 +214,19 @@ def spot_check(torch, sh, kind, n, direction_out, saved, launches):
         if got != w:
             return False
     return bool((sh["out_len"].cpu().numpy() == lens + S).all())
+
+
+def kernel_name(kind: int, direction: int, multi: bool, ppw: int) -> str:
+    """The dispatched template, obfs_kernel<KIND, DIR, MULTI, U, WPB>
+    (sq_kernels.hip: U and waves per workgroup from the build), and the unit
+    the launch used."""
+    import re
+    import sqobfs
+    info = sqobfs.build_info()
+    u = re.search(r"\bU=(\d+)", info)
+    w = re.search(r"\bwpb=(\d+)", info)
+    return (f"obfs_kernel<{kind}, {direction}, {'true' if multi else 'false'}, "
+            f"{u.group(1) if u else '?'}, {w.group(1) if w else '?'}> at {ppw} packets per wave")
 
 
 def max_over_ranks(torch, dist, x: float, dev) -> float:
@@ -258,13 +281,28 @@ def cpu_baseline(seconds: float):
     ok = bool(np.array_equal(back, data))
     ob1, de1, rt1, _, wall1 = timed(1, min(seconds, 2.0))  # one core: the per-core rate
     host = os.cpu_count() or threads
+    share = {}
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and 0 < int(omp) < threads:
+        # the pool's per-job share (OMP_NUM_THREADS), as a secondary figure
+        o_ob, o_de, o_rt, _, o_wall = timed(int(omp), min(seconds, 2.0))
+        wall1 += o_wall * int(omp)
+        share = {"threads": int(omp), "obfuscate": round(o_ob, 3), "deobfuscate": round(o_de, 3),
+                 "round_trip": round(o_rt, 3), "why": "OMP_NUM_THREADS (the pool's per-job "
+                 "share, not enforced by the cgroup quota when that allows more)"}
+    quota = cgroup_cpu_quota()
     return {"value": ob, "unit": "GiB/s", "cores": threads, "kind": "port",
             "sample": f"configs[0]: {passes} x (65,536 x 1200 B Salamander obfuscate + "
                       f"deobfuscate), one PSK, C restatement (oracle/oracle.c, byte loops as "
-                      f"salamander.go:51-53,62-64) on {threads} threads (this job's CPU "
-                      f"share of the {host}-CPU host); value = obfuscate direction; "
-                      f"deobfuscate {de:.3f} GiB/s, round trip {rt:.3f} GiB/s; round-trip "
-                      f"identity {ok}; Go reference unbuildable (no Go toolchain)",
+                      f"salamander.go:51-53,62-64) on {threads} threads (every CPU this "
+                      f"process may run on: affinity {len(os.sched_getaffinity(0))}, cgroup "
+                      f"quota {quota if quota is not None else 'none'}; host {host} CPUs); "
+                      f"value = obfuscate direction; deobfuscate {de:.3f} GiB/s, round trip "
+                      f"{rt:.3f} GiB/s; round-trip identity {ok}; Go reference unbuildable "
+                      f"(no Go toolchain)",
+            "cgroup_cpu_quota": quota,
+            "omp_num_threads": int(omp) if omp and omp.isdigit() else None,
+            "job_share": share or None,
             "per_direction": {"obfuscate": round(ob, 3), "deobfuscate": round(de, 3),
                               "round_trip": round(rt, 3)},
             "per_core": {"obfuscate": round(ob1, 3), "deobfuscate": round(de1, 3),
@@ -279,13 +317,32 @@ def cpu_baseline(seconds: float):
             "cpu_seconds": round(wall * threads + wall1, 2)}
 
 
+def cgroup_cpu_quota():
+    """CPUs the cgroup's CPU quota allows (cgroup v2 cpu.max "quota period",
+    v1 cfs_quota_us / cfs_period_us), or None when unlimited / unreadable."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return round(q / per, 2) if q > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_share() -> int:
-    """CPUs this job may use: its affinity, capped by the pool's per-job share
-    (OMP_NUM_THREADS is set to it on the GPU boxes)."""
+    """CPUs this process may use: its affinity, capped by the cgroup CPU quota
+    when there is one (the CPU baseline runs on the host's
+    cores).  OMP_NUM_THREADS, the pool's advisory per-job share, is timed as a
+    secondary figure."""
+    import math
     n = len(os.sched_getaffinity(0))
-    cap = os.environ.get("OMP_NUM_THREADS")
-    if cap and cap.isdigit() and int(cap) > 0:
-        n = min(n, int(cap))
+    q = cgroup_cpu_quota()
+    if q is not None:
+        n = min(n, max(1, math.ceil(q)))
     return max(1, n)
 
 
@@ -378,7 +435,7 @@ def inproc_bench(args):
 
 def quic_valu_roofline(suite_name: str, op: str, kernel_us: float):
     """VALU roofline of a QUIC kernel from the committed PMC pass
-    (profiles/r02/quic/quic_pmc_summary.json, scripts/r2_quic_pmc.sh): VALU
+    (profiles/r02/quic/quic_pmc_summary.json, scripts/quic_pmc.sh): VALU
     wave-instructions per launch (SQ_INSTS_VALU) over this run's kernel time,
     against 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction."""
     f = os.path.join(REPO, "profiles", "r02", "quic", "quic_pmc_summary.json")
@@ -446,26 +503,34 @@ def main():
         raise SystemExit("--layout inplace is for obfuscate")
     if args.device_salt and (direction != sqobfs.OBFUSCATE or sh["inplace"]):
         raise SystemExit("--device-salt is for obfuscate, not in place")
+    # slotted layouts: every output owns its 16-byte blocks
+    ob = sqobfs.FLAG_OUT_BLOCKS if sh["slotted"] else 0
     if direction == sqobfs.OBFUSCATE and args.device_salt:
         ctx.salt_key(SALT_KEY, 0)
         b = sqobfs.make_batch(n, sh["data"], sh["in_off"], sh["lens"], sh["out"], sh["out_off"],
-                              sh["out_len"], None, sh["psk_id"], flags=sqobfs.FLAG_DEVICE_SALT)
+                              sh["out_len"], None, sh["psk_id"],
+                              flags=sqobfs.FLAG_DEVICE_SALT | ob)
         alg_bytes = 2 * sh["payload_bytes"] + S * n  # no salt array read
     elif direction == sqobfs.OBFUSCATE:
         b = sqobfs.make_batch(n, sh["data"], sh["in_off"], sh["lens"], sh["out"], sh["out_off"],
-                              sh["out_len"], sh["salt"], sh["psk_id"])
+                              sh["out_len"], sh["salt"], sh["psk_id"], flags=ob)
         alg_bytes = 2 * sh["payload_bytes"] + 2 * S * n
     else:
         # decode the obfuscated shard (made once, untimed)
         b0 = sqobfs.make_batch(n, sh["data"], sh["in_off"], sh["lens"], sh["out"],
-                               sh["out_off"], sh["out_len"], sh["salt"], sh["psk_id"])
+                               sh["out_off"], sh["out_len"], sh["salt"], sh["psk_id"], flags=ob)
         sqobfs.launch(ctx, kr, sqobfs.OBFUSCATE, b0, s)
         wire_len = (sh["lens"] + S).to(torch.int32)
-        # decoded payloads back to back (a compact receive buffer)
-        back_off = torch.cumsum(sh["lens"].to(torch.int64), 0) - sh["lens"].to(torch.int64) + 64
-        back = torch.zeros(int(sh["payload_bytes"]) + 128, device=dev, dtype=torch.uint8)
+        if sh["slotted"]:
+            # decoded payloads into slots like the input's (16-byte aligned)
+            back_off = sh["in_off"]
+            back = torch.zeros_like(sh["data"])
+        else:
+            # decoded payloads back to back (a compact receive buffer)
+            back_off = torch.cumsum(sh["lens"].to(torch.int64), 0) - sh["lens"].to(torch.int64) + 64
+            back = torch.zeros(int(sh["payload_bytes"]) + 128, device=dev, dtype=torch.uint8)
         b = sqobfs.make_batch(n, sh["out"], sh["out_off"], wire_len, back, back_off,
-                              sh["out_len"], None, sh["psk_id"])
+                              sh["out_len"], None, sh["psk_id"], flags=ob)
         alg_bytes = 2 * sh["payload_bytes"] + S * n
 
     saved = save_samples(sh, n) if direction == sqobfs.OBFUSCATE else None
@@ -572,7 +637,8 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / PEAK_HBM_GBS, 4),
             "traffic": traffic,
-            "kernel": f"obfs_kernel<{kind},{direction},{int(n_psk > 1)}> ({sqobfs.build_info()})",
+            "kernel": kernel_name(kind, direction, n_psk > 1, ctx.unit_packets),
+            "build": sqobfs.build_info(),
             "kernel_avg_us": round(kern_avg_ms * 1e3, 2),
             "kernel_min_us": round(kern_ms[0] * 1e3, 2),
             "kernel_median_us": round(kern_ms[len(kern_ms) // 2] * 1e3, 2),

@@ -295,13 +295,19 @@ func (s *Slots) OutLen(i int) int { return int(s.outLen[i]) }
 // (replaces buf.WriteRandom, salamander.go:60, and math/rand, xplus.go:67-69).
 // withCap: XPlus deobfuscate XORs up to SetCap bytes (xplus.go:55).  Output
 // bytes are only read up to OutLen, so the output slots are declared
-// uninitialised (no copy-in of the output span).
+// uninitialised (no copy-in of the output span), and with 16-byte-multiple
+// slots as owning their blocks (SQOBFS_FLAG_OUT_BLOCKS).
 func (s *Slots) Run(kr *Keyring, dir Direction, n int, deviceSalt, withCap bool) error {
 	if n < 0 || n > s.Cap {
 		return errors.New("sqobfs: batch larger than its slots")
 	}
 	s.b.n = C.uint32_t(n)
 	s.b.flags = C.SQOBFS_FLAG_OUT_UNINIT
+	if s.SlotBytes%16 == 0 {
+		// every output in a slot of its own: the kernel writes whole blocks
+		// (the slot padding is scratch)
+		s.b.flags |= C.SQOBFS_FLAG_OUT_BLOCKS
+	}
 	if dir == Obfuscate && deviceSalt {
 		s.b.flags |= C.SQOBFS_FLAG_DEVICE_SALT
 	}

@@ -104,6 +104,16 @@ extern "C" {
  * `salt_out`, if not NULL, receives the n*S generated salts. */
 #define SQOBFS_FLAG_DEVICE_SALT 2u
 
+/* batch flag: outputs own their 16-byte blocks.  The caller promises that no
+ * 16-byte-aligned block of `out` that holds output bytes of packet i holds
+ * input or output bytes of any other packet of the batch (true of slotted
+ * layouts whose slots are multiples of 16 bytes: the Go Slots, the UDP
+ * endpoint, sqobfs_pconn).  The launch may then write every such block whole:
+ * the bytes of those blocks outside packet i's output (slot padding, and in
+ * place the packet's own consumed salt) are left with unspecified values.
+ * Every output byte is as without the flag. */
+#define SQOBFS_FLAG_OUT_BLOCKS 4u
+
 /* out_len value written for a packet whose psk_id is out of range */
 #define SQOBFS_BAD_PSK 0xFFFFFFFFu
 

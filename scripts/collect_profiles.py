@@ -1,4 +1,4 @@
-"""Copy a scripts/r2_profile_all.sh run (gpurun_out/<tag>/) into profiles/r02/:
+"""Copy a scripts/profile_configs.sh run (gpurun_out/<tag>/) into profiles/r02/:
 per config the kernel-trace stats, the PMC summary and the HBM-traffic file
 bench.py reads (profiles/r02/pmc_<config>.json).
 usage: python scripts/collect_r2_profiles.py TAG"""
@@ -35,7 +35,7 @@ for d in sorted(glob.glob(os.path.join(src, "*"))):
                    "bench_kernel_avg_us_same_run": kt["roofline"]["kernel_avg_us"],
                    "lds_bytes": last[-1]["LDS_Block_Size"],
                    "grid": last[-1]["Grid_Size_X"], "workgroup": last[-1]["Workgroup_Size_X"],
-                   "source": "rocprofv3 --kernel-trace --stats (scripts/r2_profile.sh)"},
+                   "source": "rocprofv3 --kernel-trace --stats (scripts/profile.sh)"},
                   open(os.path.join(dst, f"kernel_trace_timed_{cfg}.json"), "w"), indent=1)
     summ = os.path.join(d, "summary.json")
     if not os.path.exists(summ):
@@ -50,7 +50,7 @@ for d in sorted(glob.glob(os.path.join(src, "*"))):
            "algorithmic_bytes_per_launch": alg,
            "traffic_over_algorithmic": round(s["hbm_bytes_per_launch"] / alg, 4),
            "source": f"profiles/r02/pmc_{cfg}_counters.json: rocprofv3 --pmc FETCH_SIZE and "
-                     "--pmc WRITE_SIZE in separate passes (scripts/r2_profile.sh), bench.py "
+                     "--pmc WRITE_SIZE in separate passes (scripts/profile.sh), bench.py "
                      "--steps 5; read = 2*FETCH_SIZE*1024 (gfx950 half-count correction), "
                      "write = WRITE_SIZE*1024",
            "kernel": kt["roofline"].get("kernel")}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU box: every BASELINE config x direction, layouts, device salts, and the
-# in-process shard mode, with the shipped lib.  usage: r2_configs.sh OUTDIR
+# in-process shard mode, with the shipped lib.  usage: scripts/configs.sh OUTDIR
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/${1:-cfg}; mkdir -p $O

@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU box: kernel time vs unit size (SQOBFS_TUNE_PPW) per config, REPS
-# interleaved passes; usage: r3_ppw_sweep.sh OUTDIR "ppw list" config...
+# interleaved passes; usage: scripts/ppw_sweep.sh OUTDIR "ppw list" config...
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/$1; shift; PPWS=$1; shift

@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU box: kernel trace (+stats) and PMC passes of bench.py for one config.
-# usage: scripts/r2_profile.sh OUTDIR [bench args]   (each pass its own run)
+# usage: scripts/profile.sh OUTDIR [bench args]   (each pass its own run)
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/$1; shift

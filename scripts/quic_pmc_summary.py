@@ -1,4 +1,4 @@
-"""Per-kernel averages of the QUIC PMC passes (scripts/r2_quic_pmc.sh) and
+"""Per-kernel averages of the QUIC PMC passes (scripts/quic_pmc.sh) and
 the VALU roofline of each QUIC kernel: VALU wave-instructions per launch
 over the kernel's average duration (kernel trace), against the MI355X VALU
 issue rate: 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction.

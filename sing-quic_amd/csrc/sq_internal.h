@@ -67,6 +67,7 @@ struct KParams {
   uint32_t n_psk;
   uint32_t device_salt;     // 1: obfuscate salts from ChaCha20(salt_key, salt_nonce)
   uint32_t ppw;             // packets per wavefront (unit size), 1 .. 62; 0 = default
+  uint32_t out_blocks;      // 1: SQOBFS_FLAG_OUT_BLOCKS (outputs own their 16-byte blocks)
   uint32_t salt_key[8];
   uint32_t salt_nonce[3];
   PskEntry psk0;

@@ -112,7 +112,7 @@ namespace sq {
 #define SQ_STR2(x) #x
 #define SQ_STR(x) SQ_STR2(x)
 extern "C" const char *sqobfs_build_info(void) {
-  return "gfx950 obfs_kernel U=" SQ_STR(SQ_U) " PPW=" SQ_STR(SQ_PPW) " NT=" SQ_STR(SQ_NT)
+  return "gfx950 obfs_kernel U=" SQ_STR(SQ_U) " default_ppw=" SQ_STR(SQ_PPW) " NT=" SQ_STR(SQ_NT)
          " minw=" SQ_STR(SQ_MINW) " wpb=2"
          " ablate=" SQ_STR(SQ_ABLATE) " donate=" SQ_STR(SQ_DONATE) " align=" SQ_STR(SQ_ALIGN)
          " klate=" SQ_STR(SQ_KLATE) " map=" SQ_STR(SQ_MAPBLK);
@@ -475,15 +475,23 @@ struct Geo {
   bool hl;              // last owned block partly this packet's (re unaligned)
   bool lfull;           // ... and written whole (the next datagram fills it)
   bool pfull;           // bytes [rs, B0) are in the previous packet's whole block
+  bool obh;             // out_blocks head: the first block starts at rs rounded down
 };
 
 // Step 3a, the plan: block ownership and special-block roles (no key, no
 // payload bytes needed), the flat prefix sum, the stream half of the LDS
 // records, the block map and the buffer resources -- everything the first
 // stream loads need.  Every lane of the wave runs it.
+// With out_blocks (SQOBFS_FLAG_OUT_BLOCKS) every block an output touches is
+// the packet's own: its last block is always written whole (bytes past re
+// scratch), and its first block starts at rs rounded down (a special block
+// whose bytes before rs are scratch) -- unless the salt would then spill into
+// a second block (obfuscate with rs % 16 + S > 16), which keeps the
+// byte-exact head.  Slotted layouts (outputs at 16-byte-aligned slot starts,
+// or decoded in place behind the salt) never need it.
 __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, uint32_t lane,
-                                                uint32_t ppw, bool has_prev, WaveLds &L,
-                                                Geo &G) {
+                                                uint32_t ppw, bool has_prev, bool ob,
+                                                WaveLds &L, Geo &G) {
   out_range(J, G.rs, G.re, G.ne);
   const uint64_t rs = G.rs, re = G.re;
   // in place (input overlaps its own output blocks): a neighbour in another
@@ -499,13 +507,14 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
   const uint32_t fl = (G.ne ? 1u : 0u) | (ovl ? 2u : 0u);
   const uint32_t fl_n = shfl32(fl, nl), fl_p = shfl32(fl, pl);
 
-  const uint64_t B0r = up16(rs), E = up16(re), BL = re & ~15ull;
+  G.obh = ob && (uint32_t)(rs & 15) + J.pre <= 16u;
+  const uint64_t B0r = G.obh ? (rs & ~15ull) : up16(rs), E = up16(re), BL = re & ~15ull;
   const uint32_t nraw = (G.ne && E > B0r) ? (uint32_t)((E - B0r) >> 4) : 0u;
   const bool cross_n = lane == ppw - 1, cross_p = lane == 0;
   // leading bytes [rs, B0) covered by the previous packet's whole last block
   // (the same predicate as the previous lane's lfull)
   const bool p_hl = (fl_p & 1) && (re_p & 15) && up16(re_p) > up16(rs_p);
-  G.pfull = p_hl && G.ne && re_p == rs && re >= B0r && !(cross_p && ovl);
+  G.pfull = !ob && p_hl && G.ne && re_p == rs && re >= B0r && !(cross_p && ovl);
   // Donation.  A unit's first packet p gives its blocks in the 64-byte line
   // its output starts in ([B0, LE)) to the previous unit's wave, which holds
   // p as its look-ahead lane (key, head image and job already there): every
@@ -515,7 +524,7 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
   const bool ahead = lane == ppw, head = lane == 0 && has_prev;
   const uint64_t LE = (rs + 63) & ~63ull;
   const bool donate = SQ_DONATE && (ahead || head) && G.ne && !ovl && LE > B0r &&
-                      B0r + 16ull * nraw > LE && ((rs & 15) == 0 || G.pfull);
+                      B0r + 16ull * nraw > LE && (G.obh || (rs & 15) == 0 || G.pfull);
   const uint32_t don = donate ? (uint32_t)((LE - B0r) >> 4) : 0u;
   const uint64_t B0 = donate && head ? LE : B0r;
   G.B0 = B0;
@@ -524,7 +533,8 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
   G.hl = nblk && (re & 15) && !(donate && ahead);
   G.hf = nblk && B0 < J.dst_pay && !(G.hl && B0 == BL);
   // last block whole: the next datagram starts at re and fills the block
-  G.lfull = G.hl && (fl_n & 1) && rs_n == re && re_n >= E && !(cross_n && (fl_n & 2));
+  // (or, with out_blocks, the bytes past re are scratch)
+  G.lfull = G.hl && (ob || ((fl_n & 1) && rs_n == re && re_n >= E && !(cross_n && (fl_n & 2))));
 
   // the flat block space: this packet's blocks [B0, B0 + 16 F)
   const uint32_t F = (G.hl && !G.lfull) ? nblk - 1 : nblk;
@@ -614,7 +624,7 @@ template <int KIND, int DIR, bool MULTI>
 __device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
                                           const uint32_t (&salt)[4], bool do_hash, uint32_t pid,
                                           const Windows &W, bool owner, uint32_t lane,
-                                          const Geo &G, WaveLds &L) {
+                                          bool ob, const Geo &G, WaveLds &L) {
   constexpr uint32_t S = KIND == 0 ? kSalamanderSalt : kXPlusSalt;
   constexpr uint32_t PW = DIR == 0 ? S / 4 : 0;  // salt words in front of the payload
   uint32_t key[8];
@@ -643,6 +653,8 @@ __device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
     }
   }
   const uint32_t hx[12] = {hi[0], hi[1], hi[2], hi[3], hi[4], hi[5], hi[6], hi[7], 0u, 0u, 0u, 0u};
+  // the same image 16 bytes later (blocks that start before rs: out_blocks)
+  const uint32_t hp[12] = {0u, 0u, 0u, 0u, hi[0], hi[1], hi[2], hi[3], hi[4], hi[5], hi[6], hi[7]};
   // tail image: bytes [BL, re) of the last partial output block
   const uint64_t BL = re & ~15ull;
   const uint32_t t = (uint32_t)(re & 15);
@@ -656,6 +668,8 @@ __device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
     keywin(key, (uint32_t)(BL - J.dst_pay) & 31u, ks);
 #pragma unroll
     for (int j = 0; j < 4; j++) ti[j] ^= ks[j];
+  } else if (BL < rs) {  // out_blocks: one block holds the whole output
+    win16(hp, (uint32_t)(BL + 16 - rs), ti);
   } else {
     win16(hx, (uint32_t)(BL - rs) & 31u, ti);  // BL - rs <= 16 here (or no tail)
   }
@@ -667,7 +681,7 @@ __device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
 
   // byte-exact stores of the bytes no datagram pair covers whole
   if (!(SQ_ABLATE & 2) && owner && G.ne) {
-    if ((rs & 15) && !G.pfull) {
+    if ((rs & 15) && !G.pfull && !G.obh) {
       const uint64_t lend = re < G.B0 ? re : G.B0;
       const uint32_t v[4] = {hi[0], hi[1], hi[2], hi[3]};
       store16(rs, v, (uint32_t)(lend - rs));
@@ -677,13 +691,16 @@ __device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
 
   // special blocks and keystreams
   uint32_t vf[4] = {0u, 0u, 0u, 0u}, vl[4] = {0u, 0u, 0u, 0u};
-  if (G.hf) win16(hx, (uint32_t)(G.B0 - rs), vf);
+  if (G.hf) {
+    if (G.B0 < rs) win16(hp, (uint32_t)(G.B0 + 16 - rs), vf);  // out_blocks
+    else win16(hx, (uint32_t)(G.B0 - rs), vf);
+  }
   if (G.lfull) {
     const uint32_t w[12] = {0u, 0u, 0u, 0u, hn[0], hn[1], hn[2], hn[3], 0u, 0u, 0u, 0u};
     uint32_t sh[4];
     win16(w, 16 - t, sh);
 #pragma unroll
-    for (int j = 0; j < 4; j++) vl[j] = (ti[j] & range_mask(0, (int)t, j)) | sh[j];
+    for (int j = 0; j < 4; j++) vl[j] = (ti[j] & range_mask(0, (int)t, j)) | (ob ? 0u : sh[j]);
   }
   uint32_t k0[4], k1[4];
   const uint32_t ph = (uint32_t)(G.B0 - J.dst_pay) & 31u;
@@ -901,11 +918,12 @@ __global__ __launch_bounds__(WPB * kWave) void obfs_kernel(const KParams P) {
   // 3a. plan
   Geo G;
   WaveLds &L = lds[wv];
-  const UnitStream S = plan_unit(J, owner, lane, ppw, first != 0, L, G);
+  const bool ob = P.out_blocks != 0;
+  const UnitStream S = plan_unit(J, owner, lane, ppw, first != 0, ob, L, G);
   SQ_STAMP(2);
   const uint32_t pid = MULTI && d.pid < P.n_psk ? d.pid : 0u;
   // 2 + 3b. key and block contents
-  fill_unit<KIND, DIR, MULTI>(P, J, salt, do_hash, pid, W, owner, lane, G, L);
+  fill_unit<KIND, DIR, MULTI>(P, J, salt, do_hash, pid, W, owner, lane, ob, G, L);
   SQ_STAMP(3);
   // 4. the stream
   Step<U> cur;

@@ -80,6 +80,7 @@ struct PBatch {
   uint32_t *len = nullptr, *out_len = nullptr;
   std::vector<sqobfs_addr> addr;
   std::vector<uint64_t> tag;
+  std::vector<uint8_t> head;  // rx: the first 16 wire bytes of each datagram
 };
 
 }  // namespace
@@ -149,7 +150,9 @@ int launch_wait(sqobfs_pconn *pc, void *stream, int dir, PBatch &b) {
   sqobfs_batch d;
   memset(&d, 0, sizeof d);
   d.n = b.n;
-  d.flags = dir == SQOBFS_OBFUSCATE ? SQOBFS_FLAG_DEVICE_SALT : 0u;
+  // slots are multiples of 16 bytes: every output owns its blocks, so the
+  // kernel writes them whole (SQOBFS_FLAG_OUT_BLOCKS)
+  d.flags = SQOBFS_FLAG_OUT_BLOCKS | (dir == SQOBFS_OBFUSCATE ? SQOBFS_FLAG_DEVICE_SALT : 0u);
   d.in = b.slots;
   d.in_off = b.in_off;
   d.in_len = b.len;
@@ -296,6 +299,7 @@ void rx_worker_socket(sqobfs_pconn *pc) {
     uint64_t trunc = 0;
     for (int j = 0; j < m; j++) {
       b.len[j] = std::min<uint32_t>(pc->rmsg[j].msg_len, pc->o.slot_bytes);
+      memcpy(&b.head[16ull * j], pc->slot(b, (uint32_t)j), 16);
       if (pc->rmsg[j].msg_hdr.msg_flags & MSG_TRUNC) trunc++;
       sq::from_sockaddr(pc->rss[j], &b.addr[j]);
       b.tag[j] = 0;
@@ -440,6 +444,7 @@ int sqobfs_pconn_open(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int fd,
     b.out_len = (uint32_t *)a;  a += 4ull * B;
     b.addr.resize(B);
     b.tag.resize(B);
+    if (!tx) b.head.resize(16ull * B);
     for (uint32_t i = 0; i < B; i++) {
       const uint64_t s0 = (uint64_t)i * o.slot_bytes;
       // tx: payload behind S bytes of headroom, wire = salt || payload in
@@ -597,8 +602,8 @@ int sqobfs_pconn_read(sqobfs_pconn *pc, uint8_t *p, uint32_t cap, uint32_t *n,
   uint32_t r = 0;
   const uint8_t *src = nullptr;
   if (pc->kind == SQOBFS_SALAMANDER && m <= S) {
-    r = m;                  // salamander.go:47-49: returned as is
-    src = pc->slot(b, i);   // the raw bytes (in place decoding starts at S)
+    r = m;                       // salamander.go:47-49: returned as is
+    src = &b.head[16ull * i];    // the raw bytes (the decode wrote the slot's head)
   } else if (pc->kind == SQOBFS_XPLUS && m < S) {
     r = 0;                  // xplus.go:50-52
   } else {
@@ -638,6 +643,7 @@ int sqobfs_pconn_rx_push(sqobfs_pconn *pc, const uint8_t *wire, uint32_t n,
   const uint32_t m = std::min(n, pc->o.slot_bytes);
   if (m < n) pc->st.rx_truncated++;
   if (m) memcpy(pc->slot(b, i), wire, m);
+  memcpy(&b.head[16ull * i], pc->slot(b, i), 16);
   b.len[i] = m;
   if (from) b.addr[i] = *from;
   else memset(&b.addr[i], 0, sizeof b.addr[i]);

@@ -487,6 +487,9 @@ int sqobfs_udp_conn_read(sqobfs_udp_conn *c, int timeout_ms, sqobfs_udp_view *ou
   b.out = c->rx;
   b.out_off = c->rx_out_off;
   b.out_len = c->rx_out_len;
+  // fixed slots (multiples of 16 bytes): outputs own their blocks; GRO
+  // buffers pack datagrams back to back, so not there
+  if (!(c->offload & SQOBFS_UDP_RX_GRO)) b.flags = SQOBFS_FLAG_OUT_BLOCKS;
   st = launch_sync(c, SQOBFS_DEOBFUSCATE, b);
   if (st != SQ_OK) return st;
   out->count = n;
@@ -518,7 +521,7 @@ int sqobfs_udp_conn_write(sqobfs_udp_conn *c, uint32_t fd_index, uint32_t n,
   sqobfs_batch b;
   memset(&b, 0, sizeof b);
   b.n = n;
-  b.flags = SQOBFS_FLAG_DEVICE_SALT;
+  b.flags = SQOBFS_FLAG_DEVICE_SALT | SQOBFS_FLAG_OUT_BLOCKS;  // slots of 16-byte multiples
   b.in = c->tx;
   b.in_off = c->tx_in_off;
   b.in_len = c->tx_len;

@@ -33,6 +33,7 @@ SQ_ETIMEDOUT, SQ_ECLOSED, SQ_EIO = -6, -7, -8
 BAD_PSK = 0xFFFFFFFF
 FLAG_OUT_UNINIT = 1  # run_host: bytes between output regions need not be kept
 FLAG_DEVICE_SALT = 2  # obfuscate: salts from the GPU's ChaCha20 generator
+FLAG_OUT_BLOCKS = 4  # outputs own their 16-byte blocks (slot padding is scratch)
 
 
 class SqError(RuntimeError):

@@ -1,5 +1,6 @@
 /* Replays, in C, the exact libsqobfs call sequence and memory ownership of
- * the Go binding (go/sqobfs/sqobfs.go, go/sqobfs/conn.go) -- the Go code
+ * the Go binding's Slots (go/sqobfs/sqobfs.go; its Conn drives the engine
+ * tested by tests/cpp/test_pconn.c) -- the Go code
  * cannot be compiled here (no Go toolchain), so this pins what it does:
  *
  *   Open            sqobfs_open
@@ -9,8 +10,9 @@
  *                   out slots); calloc'd sqobfs_batch; malloc'd in_off,
  *                   out_off, in_len, out_len, in_cap, salt; offsets filled
  *   WriteTo x k     payload copied into In(i), SetLen
- *   flusher         Slots.Run(Obfuscate, n, deviceSalt): b->n, flags =
- *                   DEVICE_SALT, in_cap = NULL -> sqobfs_run_host
+ *   Run             Slots.Run(Obfuscate, n, deviceSalt): b->n, flags =
+ *                   OUT_UNINIT | OUT_BLOCKS | DEVICE_SALT, in_cap = NULL ->
+ *                   sqobfs_run_host
  *   reader          datagrams copied into In(i) of another Slots, SetLen ->
  *                   Slots.Run(Deobfuscate) -> Out(i)[:out_len[i]]
  *   Free / Close    free every array, the batch, sqobfs_host_free,
@@ -96,7 +98,10 @@ static uint8_t *out_slot(Slots *s, int i) { return s->data + (size_t)(s->cap + i
 
 static int run(Slots *s, const sqobfs_keyring *kr, int dir, int n, int device_salt) {
   s->b->n = (uint32_t)n;
-  s->b->flags = (dir == SQOBFS_OBFUSCATE && device_salt) ? SQOBFS_FLAG_DEVICE_SALT : 0;
+  /* Slots.Run: output slots are read only up to out_len (OUT_UNINIT), and
+   * 16-byte-multiple slots own their blocks (OUT_BLOCKS) */
+  s->b->flags = SQOBFS_FLAG_OUT_UNINIT | (s->slot % 16 == 0 ? SQOBFS_FLAG_OUT_BLOCKS : 0u) |
+                ((dir == SQOBFS_OBFUSCATE && device_salt) ? SQOBFS_FLAG_DEVICE_SALT : 0u);
   s->b->in_cap = NULL;
   return sqobfs_run_host(s->ctx, kr, dir, s->b);
 }

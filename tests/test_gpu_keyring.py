@@ -38,15 +38,16 @@ def test_destroy_does_not_wait_for_another_contexts_work():
     try:
         kra = sqobfs.Keyring(a, SALAMANDER, [PSK])
         batch, keep = _big_batch(torch, dev)
-        torch.cuda.synchronize(dev)
-        busy = torch.cuda.ExternalStream(a.stream, device=dev)
-        for _ in range(30):  # ~15 ms of work queued on context A
-            sqobfs.launch(a, kra, OBFUSCATE, batch, a.stream)
-        # context B: a connection opens, runs a small batch and closes
+        # context B: a connection opens and runs a small batch ...
         rng = np.random.Generator(np.random.PCG64(9))
         hb = gh.make_case(rng, SALAMANDER, OBFUSCATE, rng.integers(0, 1500, 64), [PSK])
         krb = sqobfs.Keyring(b, SALAMANDER, [PSK])
         gh.run_host(b, krb, OBFUSCATE, hb)
+        torch.cuda.synchronize(dev)
+        busy = torch.cuda.ExternalStream(a.stream, device=dev)
+        for _ in range(100):  # ~50 ms of work queued on context A
+            sqobfs.launch(a, kra, OBFUSCATE, batch, a.stream)
+        # ... and closes while A is busy
         t0 = time.perf_counter()
         krb.close()
         dt = time.perf_counter() - t0

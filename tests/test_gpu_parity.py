@@ -176,9 +176,9 @@ def test_jumbo_units(ctx, kind, direction):
 @pytest.mark.parametrize("kind", KINDS)
 @pytest.mark.parametrize("direction", DIRS)
 def test_single_psk_lengths(ctx, kind, direction):
-    """One-entry keyrings (no psk_id: the single-PSK kernels, whose BLAKE2b
-    is specialised on the salt's message word) for PSK lengths that put the
-    salt at every word position of a one-block final message, across the
+    """One-entry keyrings (no psk_id: the single-PSK kernels, which read the
+    keyring's entry 0 from the kernel arguments) for PSK lengths that put the
+    salt at every byte position of a one-block final message, across the
     one/two-block boundary (PSK tail 120 / 121 / 127 B) and past whole
     blocks."""
     rng = np.random.Generator(np.random.PCG64(950 + 10 * kind + direction))
