@@ -93,6 +93,10 @@ def parse():
     ap.add_argument("--udp", action="store_true",
                     help="also time loopback UDP end to end through the batched socket "
                          "layer (sqobfs_udp_conn: sendmmsg/recvmmsg + GPU)")
+    ap.add_argument("--latency", action="store_true",
+                    help="also run sing-quic_amd/bin/lat_bench: per-datagram p50/p99 latency of "
+                         "run_host, a mapped launch, the UDP endpoint and the packet conn "
+                         "engine at batches of 1/16/64/256, and the engine's loopback rate")
     ap.add_argument("--e2e", action="store_true",
                     help="also time the host-staged path (pinned H2D + kernel + D2H)")
     return ap.parse_args()
@@ -650,6 +654,8 @@ def main():
     }
     if pmc:
         out["roofline"]["traffic_source"] = pmc.get("source")
+    if args.latency and rank == 0:
+        out["latency"] = latency_bench()
     if args.e2e and rank == 0:
         out["e2e"] = e2e_rate(torch, sqobfs, ctx, kr, kind, min(n, 1 << 18), L or 758)
     if args.quic and rank == 0:
@@ -676,6 +682,19 @@ def main():
     ctx.close()
     if dist:
         dist.destroy_process_group()
+
+
+def latency_bench():
+    """sing-quic_amd/bin/lat_bench (built by `make -C sing-quic_amd tools`):
+    DESIGN.md section 9.5."""
+    import subprocess
+    exe = os.path.join(REPO, "sing-quic_amd", "bin", "lat_bench")
+    if not os.path.exists(exe):
+        return {"error": f"{exe} missing: make -C sing-quic_amd tools"}
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=240)
+    if r.returncode != 0:
+        return {"error": r.stderr[-500:]}
+    return json.loads(r.stdout)
 
 
 def e2e_rate(torch, sqobfs, ctx, kr, kind, n, L):

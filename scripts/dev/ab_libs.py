@@ -1,0 +1,98 @@
+"""Dev probe (GPU box): kernel time of several libsqobfs builds in ONE process
+on ONE buffer set, interleaved rounds (box and allocation effects cancel).
+usage: ab_libs.py CONFIG DIRECTION ROUNDS lib1.so lib2.so ...
+Prints per lib the median kernel time and frac of 8 TB/s, and checks every
+build's output against the first one's (parity of the variants)."""
+import os
+import statistics
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+for p in (REPO, os.path.join(REPO, "sing-quic_amd")):
+    sys.path.insert(0, p)
+
+import torch  # noqa: E402
+import sqobfs  # noqa: E402
+import bench  # noqa: E402
+
+cfg, direction, rounds = sys.argv[1], sys.argv[2], int(sys.argv[3])
+paths = sys.argv[4:]
+dev = torch.device("cuda", 0)
+kind, n, L, n_psk = bench.CONFIGS[cfg]
+layout = os.environ.get("AB_LAYOUT", "dense")
+sh = bench.build_shard(torch, dev, kind, n, L, n_psk, 0, 1, cfg, layout)
+S = sh["S"]
+ob = sqobfs.FLAG_OUT_BLOCKS if sh["slotted"] else 0
+s = torch.cuda.current_stream(dev).cuda_stream
+variants = []
+for path in paths:
+    sqobfs._lib = sqobfs.load(path)
+    ctx = sqobfs.Context(0)
+    kr = sqobfs.Keyring(ctx, kind, sh["psks"])
+    ctx.unit_packets = int(os.environ.get("AB_PPW", "0")) or sqobfs.unit_packets_for(
+        sh["payload_bytes"], n, n_psk > 1)
+    variants.append((path, sqobfs._lib, ctx, kr))
+b = sqobfs.make_batch(n, sh["data"], sh["in_off"], sh["lens"], sh["out"], sh["out_off"],
+                      sh["out_len"], sh["salt"], sh["psk_id"], flags=ob)
+d = sqobfs.OBFUSCATE
+alg = 2 * sh["payload_bytes"] + 2 * S * n
+outs = []
+if direction == "deobfuscate":
+    sqobfs._lib = variants[0][1]
+    sqobfs.launch(variants[0][2], variants[0][3], sqobfs.OBFUSCATE, b, s)
+    wl = (sh["lens"] + S).to(torch.int32)
+    lens64 = sh["lens"].to(torch.int64)
+    back_off = torch.cumsum(lens64, 0) - lens64 + 64
+    back = torch.zeros(int(sh["payload_bytes"]) + 128, device=dev, dtype=torch.uint8)
+    b = sqobfs.make_batch(n, sh["out"], sh["out_off"], wl, back, back_off, sh["out_len"], None,
+                          sh["psk_id"], flags=ob)
+    d = sqobfs.DEOBFUSCATE
+    alg = 2 * sh["payload_bytes"] + S * n
+    outs = [back]
+else:
+    outs = [sh["out"]]
+
+
+def timed(v, steps=15):
+    sqobfs._lib = v[1]
+    for _ in range(2):
+        sqobfs.launch(v[2], v[3], d, b, s)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    for e0, e1 in ev:
+        e0.record()
+        sqobfs.launch(v[2], v[3], d, b, s)
+        e1.record()
+    torch.cuda.synchronize()
+    return sum(e0.elapsed_time(e1) for e0, e1 in ev) / steps * 1e3
+
+
+# parity of the variants: each one's output equals the first's
+ref = None
+for v in variants:
+    sqobfs._lib = v[1]
+    outs[0].zero_()
+    sqobfs.launch(v[2], v[3], d, b, s)
+    torch.cuda.synchronize()
+    if ref is None:
+        ref = outs[0].clone()
+    else:
+        same = torch.equal(ref, outs[0])
+        print(f"parity {os.path.basename(v[0])} vs {os.path.basename(variants[0][0])}: {same}",
+              flush=True)
+        if not same:
+            sys.exit(1)
+for v in variants:
+    sqobfs._lib = v[1]
+    for _ in range(40):
+        sqobfs.launch(v[2], v[3], d, b, s)
+torch.cuda.synchronize()
+res = {v[0]: [] for v in variants}
+for r in range(rounds):
+    for v in variants:
+        res[v[0]].append(round(timed(v), 1))
+for v in variants:
+    med = statistics.median(res[v[0]])
+    print(f"{cfg:24s} {direction[:3]} {os.path.basename(v[0]):24s} median {med:8.1f} us  "
+          f"frac {alg / med / 8e6:.4f}  all {res[v[0]]}", flush=True)

@@ -103,6 +103,17 @@ namespace sq {
 #ifndef SQ_DEVVAR
 #define SQ_DEVVAR 0
 #endif
+// 1: deobfuscate reads the salt with the head window (one round trip after
+// the descriptor instead of two); 0: a dependent salt load first (round 2)
+#ifndef SQ_SALTWIN
+#define SQ_SALTWIN 1
+#endif
+// 1: multi-PSK kernels load each lane's keyring entry (chaining value and
+// first message block) right after the descriptor, so the gather overlaps
+// the plan step; 0: loaded by the hash itself (round 2)
+#ifndef SQ_PSKPRE
+#define SQ_PSKPRE 0
+#endif
 // Timeline builds (scripts/dev/timeline.py, never shipped): lane 0 of every
 // wave records the constant-rate clock at its phase boundaries.
 #ifndef SQ_TIMELINE
@@ -326,19 +337,111 @@ __device__ __forceinline__ void finalize_desc(const KParams &P, uint32_t p, bool
   } else if (KIND == 1 && len < S) {
     olen = 0;  // xplus.go:50-52: dropped as empty
   } else {  // deobfuscate: salt = first S wire bytes
+#if !SQ_SALTWIN
     uint32_t w[4];
     load_window(in_base, in_base + S, in_base, w);
 #pragma unroll
     for (uint32_t k = 0; k < S / 4; k++) salt[k] = w[k];
+#endif
+    // (SQ_SALTWIN: the salt comes with the head window, fetch_windows)
     J = {in_base + S, out_base, (uint64_t)cap - S, 0};
     olen = len - S;
     do_hash = true;
   }
 }
 
-// Step 2, key: lane-parallel, one packet per lane.
+// The words of a keyring entry one compression needs (SQ_PSKPRE): loaded
+// early, consumed by the hash.
+struct PskHot {
+  uint64_t h[8];   // BLAKE2b chaining value | SHA-256 state (first 32 bytes)
+  uint64_t m[16];  // first final block: BLAKE2b 16 words | SHA-256 16 BE words
+  uint64_t t_first, t_last;
+  uint32_t nblocks, salt_pos;
+};
+
 template <int KIND>
-__device__ __forceinline__ void derive_key(bool do_hash, const PskEntry *E,
+__device__ __forceinline__ void load_hot(const PskEntry *E, PskHot &H) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) H.h[i] = KIND == 0 || i < 4 ? E->h[i] : 0ull;
+#pragma unroll
+  for (int i = 0; i < 16; i++) H.m[i] = KIND == 0 || i < 8 ? E->m[i] : 0ull;
+  H.t_first = KIND == 0 ? E->t_first : 0ull;
+  H.t_last = KIND == 0 ? E->t_last : 0ull;
+  H.nblocks = E->nblocks;
+  H.salt_pos = E->salt_pos;
+}
+
+// Salamander key from a preloaded entry (the second block, PSK tails over
+// 120 bytes, is read from the table)
+__device__ __forceinline__ void salamander_key_hot(const PskHot &H, const PskEntry *E,
+                                                   const uint32_t (&salt)[4], uint32_t (&key)[8]) {
+  uint64_t h[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) h[i] = H.h[i];
+  const uint32_t nb = H.nblocks, t = H.salt_pos;
+  const uint64_t sv = b2_pack(salt[0], salt[1]);
+  const uint32_t w = t >> 3, sh = (t & 7) * 8;
+  const uint64_t lo = sv << sh;
+  const uint64_t hi = sh ? (sv >> (64 - sh)) : 0ull;
+  for (uint32_t blk = 0; blk < nb; blk++) {
+    uint64_t m[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const uint32_t idx = 16 * blk + j;
+      uint64_t x = blk == 0 ? H.m[j] : E->m[idx];
+      x |= (idx == w) ? lo : 0ull;
+      x |= (idx == w + 1) ? hi : 0ull;
+      m[j] = x;
+    }
+    const bool last = blk + 1 == nb;
+    b2_compress(h, m, last ? H.t_last : H.t_first, last);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    key[2 * i] = (uint32_t)h[i];
+    key[2 * i + 1] = (uint32_t)(h[i] >> 32);
+  }
+}
+
+// XPlus key from a preloaded entry (second block from the table)
+__device__ __forceinline__ void xplus_key_hot(const PskHot &H, const PskEntry *E,
+                                              const uint32_t (&salt)[4], uint32_t (&key)[8]) {
+  const uint32_t *m32 = reinterpret_cast<const uint32_t *>(E->m);
+  uint32_t st[8];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    st[2 * i] = (uint32_t)H.h[i];
+    st[2 * i + 1] = (uint32_t)(H.h[i] >> 32);
+  }
+  const uint32_t nb = H.nblocks, t = H.salt_pos;
+  const uint32_t w = t >> 2, sh = (t & 3) * 8;
+  uint32_t c[5];
+#pragma unroll
+  for (int k = 0; k < 5; k++) {
+    const uint32_t cur = k < 4 ? __builtin_bswap32(salt[k]) : 0u;
+    const uint32_t prev = k > 0 ? __builtin_bswap32(salt[k - 1]) : 0u;
+    c[k] = (cur >> sh) | (sh ? (prev << (32 - sh)) : 0u);
+  }
+  for (uint32_t blk = 0; blk < nb; blk++) {
+    uint32_t m[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const uint32_t idx = 16 * blk + j;
+      const uint64_t hv = H.m[j >> 1];
+      uint32_t x = blk == 0 ? (uint32_t)(j & 1 ? hv >> 32 : hv) : m32[idx];
+#pragma unroll
+      for (int k = 0; k < 5; k++) x |= (idx == w + k) ? c[k] : 0u;
+      m[j] = x;
+    }
+    s2_compress(st, m);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) key[i] = __builtin_bswap32(st[i]);
+}
+
+// Step 2, key: lane-parallel, one packet per lane.
+template <int KIND, bool HOT>
+__device__ __forceinline__ void derive_key(bool do_hash, const PskEntry *E, const PskHot &H,
                                            const uint32_t (&salt)[4], uint32_t (&key)[8]) {
 #pragma unroll
   for (int i = 0; i < 8; i++) key[i] = 0u;
@@ -348,8 +451,13 @@ __device__ __forceinline__ void derive_key(bool do_hash, const PskEntry *E,
     do_hash = false;
   }
   if (do_hash) {
-    if (KIND == 0) salamander_key(E, salt, key);
-    else xplus_key(E, salt, key);
+    if (HOT) {
+      if (KIND == 0) salamander_key_hot(H, E, salt, key);
+      else xplus_key_hot(H, E, salt, key);
+    } else {
+      if (KIND == 0) salamander_key(E, salt, key);
+      else xplus_key(E, salt, key);
+    }
   }
 }
 
@@ -391,11 +499,16 @@ __device__ __forceinline__ bool tail_from_window(uint64_t rs, uint64_t re) {
 // the last partial output block).  Only blocks holding valid bytes are read.
 struct Windows {
   u32x4 h0, h1, h2, t0, t1;
+  u32x4 s0;  // deobfuscate: the block before h0 when it holds salt bytes
 };
 
-__device__ __forceinline__ void fetch_windows(const PacketJob &J, Windows &W) {
+// Deobfuscate with a key (wire_salt): the salt is the S wire bytes before
+// the payload, [src_pay - S, src_pay); it lies in h0 and, when src_pay % 16 <
+// S, the block before it, loaded here with the head window.
+template <int DIR, uint32_t S>
+__device__ __forceinline__ void fetch_windows(const PacketJob &J, bool wire_salt, Windows &W) {
   const u32x4 z = {0u, 0u, 0u, 0u};
-  W.h0 = W.h1 = W.h2 = W.t0 = W.t1 = z;
+  W.h0 = W.h1 = W.h2 = W.t0 = W.t1 = W.s0 = z;
   if (SQ_ABLATE & 8) return;
   uint64_t rs, re;
   bool ne;
@@ -404,6 +517,7 @@ __device__ __forceinline__ void fetch_windows(const PacketJob &J, Windows &W) {
   const uint64_t hw = J.len < 32 - J.pre ? J.len : 32 - J.pre;
   if (hw) {
     const uint64_t B = J.src_pay & ~15ull, e = J.src_pay + hw;
+    if (SQ_SALTWIN && DIR == 1 && wire_salt && (J.src_pay & 15) < S) W.s0 = gld<u32x4>(B - 16);
     W.h0 = gld<u32x4>(B);
     if (e > B + 16) W.h1 = gld<u32x4>(B + 16);
     if (e > B + 32) W.h2 = gld<u32x4>(B + 32);
@@ -623,13 +737,21 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
 template <int KIND, int DIR, bool MULTI>
 __device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
                                           const uint32_t (&salt)[4], bool do_hash, uint32_t pid,
+                                          const PskHot &hot,
                                           const Windows &W, bool owner, uint32_t lane,
                                           bool ob, const Geo &G, WaveLds &L) {
   constexpr uint32_t S = KIND == 0 ? kSalamanderSalt : kXPlusSalt;
   constexpr uint32_t PW = DIR == 0 ? S / 4 : 0;  // salt words in front of the payload
   uint32_t key[8];
+  uint32_t sl[4] = {salt[0], salt[1], salt[2], salt[3]};
+  if (SQ_SALTWIN && DIR == 1) {  // the wire salt, from the head window
+    const uint32_t w[12] = {W.s0.x, W.s0.y, W.s0.z, W.s0.w, W.h0.x, W.h0.y,
+                            W.h0.z, W.h0.w, W.h1.x, W.h1.y, W.h1.z, W.h1.w};
+    win16(w, (uint32_t)(J.src_pay & 15) + 16 - S, sl);
+  }
   // single PSK: the kernarg copy (scalar loads); several: the device table
-  derive_key<KIND>(do_hash, MULTI ? P.psk_table + pid : &P.psk0, salt, key);
+  derive_key<KIND, MULTI && SQ_PSKPRE>(do_hash, MULTI ? P.psk_table + pid : &P.psk0, hot, sl,
+                                        key);
   const uint64_t rs = G.rs, re = G.re;
   // head image: output bytes [rs, rs + 32) = salt || payload ^ key
   uint32_t hi[8];
@@ -910,10 +1032,13 @@ __global__ __launch_bounds__(WPB * kWave) void obfs_kernel(const KParams P) {
   const PskEntry *E;
   uint32_t olen;
   finalize_desc<KIND, DIR, MULTI>(P, p, valid, d, J, salt, do_hash, E, olen);
-  (void)E;
+  PskHot hot;
+  if constexpr (MULTI && SQ_PSKPRE) {
+    load_hot<KIND>(E, hot);  // in flight during the plan
+  }
   SQ_STAMP(1);
   Windows W;
-  fetch_windows(J, W);
+  fetch_windows<DIR, KIND == 0 ? kSalamanderSalt : kXPlusSalt>(J, do_hash, W);
   if (owner) P.out_len[p] = olen;
   // 3a. plan
   Geo G;
@@ -923,7 +1048,7 @@ __global__ __launch_bounds__(WPB * kWave) void obfs_kernel(const KParams P) {
   SQ_STAMP(2);
   const uint32_t pid = MULTI && d.pid < P.n_psk ? d.pid : 0u;
   // 2 + 3b. key and block contents
-  fill_unit<KIND, DIR, MULTI>(P, J, salt, do_hash, pid, W, owner, lane, ob, G, L);
+  fill_unit<KIND, DIR, MULTI>(P, J, salt, do_hash, pid, hot, W, owner, lane, ob, G, L);
   SQ_STAMP(3);
   // 4. the stream
   Step<U> cur;

@@ -128,7 +128,14 @@ def lib() -> ctypes.CDLL:
         raise RuntimeError(
             f"{LIB_PATH} is missing: build it with `make -C sing-quic_amd` "
             "(or __graft_entry__.build()); there is no CPU fallback")
-    L = ctypes.CDLL(LIB_PATH)
+    _lib = load(LIB_PATH)
+    return _lib
+
+
+def load(path: str) -> ctypes.CDLL:
+    """A libsqobfs build at `path` with its prototypes declared (lib() loads
+    the in-tree one; dev A/B scripts load timing variants side by side)."""
+    L = ctypes.CDLL(path)
     vp, u32, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
     L.sqobfs_abi_version.restype = i32
     L.sqobfs_strerror.restype = ctypes.c_char_p
@@ -212,7 +219,6 @@ def lib() -> ctypes.CDLL:
     L.sqobfs_pconn_tx_take.argtypes = [vp, i32, vp]
     L.sqobfs_pconn_tx_done.argtypes = [vp]
     L.sqobfs_pconn_stats_get.argtypes = [vp, vp]
-    _lib = L
     return L
 
 

@@ -113,6 +113,27 @@ static void print_stat(const char *name, double *v, int n, int last) {
          last ? "" : ", ");
 }
 
+/* pconn throughput reader: reads until 300 ms pass without a datagram */
+void *tput_reader(void *arg) {
+  struct rd {
+    sqobfs_pconn *pc;
+    long got;
+    double last_us;
+  } *r = arg;
+  static uint8_t buf[4096];
+  for (;;) {
+    struct timespec ts;
+    clock_gettime(CLOCK_REALTIME, &ts);
+    sqobfs_pconn_set_deadline(r->pc, SQOBFS_PCONN_READ,
+                              (int64_t)ts.tv_sec * 1000000000 + ts.tv_nsec + 300000000);
+    uint32_t n;
+    if (sqobfs_pconn_read(r->pc, buf, sizeof buf, &n, NULL, NULL) != SQ_OK) break;
+    r->got++;
+    r->last_us = now_us();
+  }
+  return NULL;
+}
+
 int main(void) {
   sqobfs_ctx *ctx;
   CHECK(sqobfs_open(0, &ctx));
@@ -324,6 +345,53 @@ int main(void) {
     sqobfs_pconn_close(pc);
     close(fa);
     close(fp);
+  }
+
+  /* ---- pconn throughput: pconn A -> pconn B over loopback, one writer
+   * thread (the Go Conn's WriteTo callers), one reader thread */
+  {
+    uint16_t pa, pb;
+    int fa = udp_socket(&pa), fb = udp_socket(&pb);
+    sqobfs_pconn *A, *B;
+    CHECK(sqobfs_pconn_open(ctx, kr, fa, NULL, &A));
+    CHECK(sqobfs_pconn_open(ctx, kr, fb, NULL, &B));
+    const sqobfs_addr to = loop_addr(pb);
+    static uint8_t pay[L];
+    memset(pay, 9, L);
+    struct rd {
+      sqobfs_pconn *pc;
+      long got;
+      double last_us;
+    } r = {B, 0, 0};
+    pthread_t th;
+    extern void *tput_reader(void *);
+    pthread_create(&th, NULL, tput_reader, &r);
+    const long N = 200000;
+    const double t0 = now_us();
+    for (long i = 0; i < N; i++) {
+      CHECK(sqobfs_pconn_write(A, pay, L, &to, 0));
+      if ((i & 1023) == 1023) {
+        /* stay inside the loopback socket buffers (UDP drops, the test
+         * counts what arrives) */
+        struct timespec ts = {0, 200000};
+        nanosleep(&ts, NULL);
+      }
+    }
+    CHECK(sqobfs_pconn_set_deadline(B, SQOBFS_PCONN_READ, 0));
+    pthread_join(th, NULL);
+    const double dt = (r.last_us - t0) * 1e-6;  /* to the last datagram's arrival */
+    sqobfs_pconn_stats sa, sb;
+    CHECK(sqobfs_pconn_stats_get(A, &sa));
+    CHECK(sqobfs_pconn_stats_get(B, &sb));
+    printf("\"pconn_throughput\": {\"datagrams\": %ld, \"received\": %ld, \"seconds\": %.3f, "
+           "\"datagrams_per_s\": %.0f, \"payload_gib_s\": %.3f, \"tx_batches\": %llu, "
+           "\"rx_batches\": %llu}, ",
+           N, r.got, dt, r.got / dt, r.got * (double)L / dt / (1 << 30),
+           (unsigned long long)sa.tx_batches, (unsigned long long)sb.rx_batches);
+    sqobfs_pconn_close(A);
+    sqobfs_pconn_close(B);
+    close(fa);
+    close(fb);
   }
 
   /* ---- the reference's per-datagram work, one core (oracle byte loops) */
