@@ -81,6 +81,8 @@ def parse():
                          "2048-byte slots (the Go Slots / UDP endpoint geometry), same flag; "
                          "inplace: obfuscate in the input buffer (headroom layout, "
                          "vectorised WriteTo semantics)")
+    ap.add_argument("--slot-bytes", type=int, default=2048,
+                    help="slot stride of --layout slot2048 (a multiple of 16)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL) for the timing barrier/max; gloo lets several "
                          "ranks share one GPU in tests")
@@ -117,7 +119,8 @@ def shard(config, n_total, world, rank):
     return n_total, rank * n_total
 
 
-def build_shard(torch, dev, kind, n, L, n_psk, rank, world, config, layout, first=0):
+def build_shard(torch, dev, kind, n, L, n_psk, rank, world, config, layout, first=0,
+                slot_bytes=2048):
     """Synthetic shard in HBM: payload/salt bytes from torch's Philox RNG
     seeded per rank; 16-byte-aligned slots for inputs and outputs."""
     import numpy as np
@@ -136,8 +139,8 @@ def build_shard(torch, dev, kind, n, L, n_psk, rank, world, config, layout, firs
             in_slot = (lens + 15) // 16 * 16
             out_slot = (lens + S + 15) // 16 * 16
         else:
-            in_slot = torch.full_like(lens, 2048)
-            out_slot = torch.full_like(lens, 2048)
+            in_slot = torch.full_like(lens, slot_bytes)
+            out_slot = torch.full_like(lens, slot_bytes)
         in_off = torch.cumsum(in_slot, 0) - in_slot + lead
         out_off = torch.cumsum(out_slot, 0) - out_slot + lead
     else:
@@ -372,9 +375,15 @@ def host_info(torch, dev) -> dict:
 
 
 def load_traffic(config: str, kernel_bytes: float):
-    """HBM bytes per launch from the committed PMC pass (profiles/r02/)."""
-    path = os.path.join(REPO, "profiles", "r02", f"pmc_{config}.json")
-    if not os.path.exists(path):
+    """HBM bytes per launch from the committed PMC pass (the latest round's
+    profiles/rNN/pmc_<config>.json)."""
+    path = None
+    for rnd in ("r03", "r02"):
+        p = os.path.join(REPO, "profiles", rnd, f"pmc_{config}.json")
+        if os.path.exists(p):
+            path = p
+            break
+    if path is None:
         return None, None
     with open(path) as f:
         d = json.load(f)
@@ -494,7 +503,8 @@ def main():
         n_total = args.packets
     n, first = shard(args.config, n_total, world, rank)
     direction = sqobfs.OBFUSCATE if args.direction == "obfuscate" else sqobfs.DEOBFUSCATE
-    sh = build_shard(torch, dev, kind, n, L, n_psk, rank, world, args.config, args.layout, first)
+    sh = build_shard(torch, dev, kind, n, L, n_psk, rank, world, args.config, args.layout, first,
+                     args.slot_bytes)
     S = sh["S"]
     ctx = sqobfs.Context(gpu)
     kr = sqobfs.Keyring(ctx, kind, sh["psks"])
@@ -594,10 +604,11 @@ def main():
         total_payload = sum_over_ranks(torch, dist, total_payload, tdev)
     value = total_payload / elapsed / 2**30
     achieved = alg_bytes / (kern_avg_ms * 1e-3) / 1e9
-    # the committed PMC passes are for host-salt obfuscate on the dense layout
+    # the committed PMC passes are for host salts on the dense layout
     traffic, pmc = (None, None)
-    if not args.device_salt and direction == sqobfs.OBFUSCATE and args.layout == "dense":
-        traffic, pmc = load_traffic(args.config, alg_bytes)
+    if not args.device_salt and args.layout == "dense":
+        key = args.config if direction == sqobfs.OBFUSCATE else f"{args.config}-deobfuscate"
+        traffic, pmc = load_traffic(key, alg_bytes)
     out = {
         "metric": METRIC if args.config == "salamander-1m" and direction == 0
         and not args.device_salt else
@@ -627,7 +638,8 @@ def main():
             "salts": "device ChaCha20 (SQOBFS_FLAG_DEVICE_SALT)" if args.device_salt else "host array",
             "packets_per_gpu": n,
             "payload_bytes_per_gpu": sh["payload_bytes"],
-            "layout": args.layout,
+            "layout": args.layout + (f" ({args.slot_bytes}-byte slots)"
+                                     if args.layout == "slot2048" else ""),
             "unit_packets": ctx.unit_packets,
             "unit_rule": ("--unit-packets" if args.unit_packets else
                           "sqobfs_unit_packets_for(payload bytes, n): ~21.7 KB per wavefront "

@@ -199,7 +199,9 @@ int sqobfs_keyring_create(sqobfs_ctx *ctx, int kind, uint32_t count,
                           const uint32_t *len, sqobfs_keyring **out);
 /* Does not block: the keyring's device memory is released in stream order
  * after the launches that used it (never waits for other keyrings' or
- * contexts' work).  The context must outlive its keyrings. */
+ * contexts' work).  The context must outlive its keyrings, and so must the
+ * caller's streams the keyring was launched on (the release is ordered
+ * after the work on each of them). */
 void sqobfs_keyring_destroy(sqobfs_keyring *kr);
 int sqobfs_keyring_kind(const sqobfs_keyring *kr);
 uint32_t sqobfs_keyring_count(const sqobfs_keyring *kr);

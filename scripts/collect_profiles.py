@@ -1,7 +1,7 @@
-"""Copy a scripts/profile_configs.sh run (gpurun_out/<tag>/) into profiles/r02/:
+"""Copy a scripts/profile_configs.sh run (gpurun_out/<tag>/) into profiles/<round>/:
 per config the kernel-trace stats, the PMC summary and the HBM-traffic file
-bench.py reads (profiles/r02/pmc_<config>.json).
-usage: python scripts/collect_r2_profiles.py TAG"""
+bench.py reads (profiles/<round>/pmc_<config>.json).
+usage: python scripts/collect_profiles.py TAG [ROUND (default r03)]"""
 import glob
 import json
 import os
@@ -10,7 +10,8 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 src = os.path.join(REPO, "gpurun_out", sys.argv[1])
-dst = os.path.join(REPO, "profiles", "r02")
+rnd = sys.argv[2] if len(sys.argv) > 2 else "r03"
+dst = os.path.join(REPO, "profiles", rnd)
 os.makedirs(dst, exist_ok=True)
 for d in sorted(glob.glob(os.path.join(src, "*"))):
     if not os.path.isdir(d):
@@ -49,7 +50,7 @@ for d in sorted(glob.glob(os.path.join(src, "*"))):
            "hbm_write_bytes": s["hbm_write_bytes"],
            "algorithmic_bytes_per_launch": alg,
            "traffic_over_algorithmic": round(s["hbm_bytes_per_launch"] / alg, 4),
-           "source": f"profiles/r02/pmc_{cfg}_counters.json: rocprofv3 --pmc FETCH_SIZE and "
+           "source": f"profiles/{rnd}/pmc_{cfg}_counters.json: rocprofv3 --pmc FETCH_SIZE and "
                      "--pmc WRITE_SIZE in separate passes (scripts/profile.sh), bench.py "
                      "--steps 5; read = 2*FETCH_SIZE*1024 (gfx950 half-count correction), "
                      "write = WRITE_SIZE*1024",

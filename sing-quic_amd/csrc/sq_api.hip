@@ -53,38 +53,44 @@ std::atomic<int64_t> g_host_allocs{0};
 constexpr uint32_t kEvents = 16;
 }
 
-// The streams a keyring's table was last read on: an event recorded after the
-// keyring's latest launch on each.  Destroying the keyring frees its device
-// memory in stream order after those events (hipFreeAsync on the context's
-// release stream), so it neither blocks the caller nor waits for launches
-// that do not use it (another connection's, another context's).
+// The streams a keyring's table was read on.  Destroying the keyring records
+// an event on each of them (after every launch enqueued there so far, the
+// keyring's last ones included) and frees its device memory in stream order
+// after those events (hipFreeAsync on the context's release stream): the
+// call neither blocks nor waits for launches that do not use the keyring
+// (another connection's, another context's).  Launches only remember their
+// stream -- a per-launch event would cost the stream ~5 us between kernels
+// (profiles/r03/ab/event_cost.txt) -- so those streams must still exist at
+// destroy time; the library's own streams forget themselves when they are
+// synchronised and destroyed (sq_keyring_forget).
 struct KeyringUses {
   std::mutex mu;
-  std::vector<std::pair<hipStream_t, hipEvent_t>> ev;
+  std::vector<hipStream_t> streams;
   void note(hipStream_t s) {
     std::lock_guard<std::mutex> lk(mu);
-    for (auto &e : ev)
-      if (e.first == s) {
-        (void)hipEventRecord(e.second, s);
-        return;
-      }
-    hipEvent_t x = nullptr;
-    if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess) {
-      (void)hipGetLastError();
-      (void)hipStreamSynchronize(s);  // no event: wait for this stream instead
-      return;
-    }
-    (void)hipEventRecord(x, s);
-    ev.emplace_back(s, x);
+    for (hipStream_t x : streams)
+      if (x == s) return;
+    streams.push_back(s);
   }
-  // the release stream waits for every use, then the events go
+  void forget(hipStream_t s) {
+    std::lock_guard<std::mutex> lk(mu);
+    streams.erase(std::remove(streams.begin(), streams.end(), s), streams.end());
+  }
+  // the release stream waits for every stream's work so far
   void fence(hipStream_t rel) {
     std::lock_guard<std::mutex> lk(mu);
-    for (auto &e : ev) {
-      (void)hipStreamWaitEvent(rel, e.second, 0);
-      (void)hipEventDestroy(e.second);
+    for (hipStream_t s : streams) {
+      hipEvent_t e = nullptr;
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess &&
+          hipEventRecord(e, s) == hipSuccess) {
+        (void)hipStreamWaitEvent(rel, e, 0);
+      } else {
+        (void)hipGetLastError();
+        (void)hipStreamSynchronize(s);  // no event: wait for the stream instead
+      }
+      if (e) (void)hipEventDestroy(e);
     }
-    ev.clear();
+    streams.clear();
   }
 };
 
@@ -199,6 +205,12 @@ void sq_ctx_stream_destroy(sqobfs_ctx *ctx, void *s) {
 }
 
 // Wait for `s`: poll up to spin_us, then block.
+// A library stream that is about to be destroyed, synchronised: the
+// keyring no longer needs to fence it.
+void sq_keyring_forget(const sqobfs_keyring *kr, void *s) {
+  if (kr) kr->uses.forget((hipStream_t)s);
+}
+
 int sq_ctx_stream_wait(sqobfs_ctx *ctx, void *s, uint32_t spin_us) {
   DeviceScope ds_(ctx->device);
   if (ds_.status != SQ_OK) return ds_.status;

@@ -163,6 +163,10 @@ struct sqobfs_ctx;
 int sq_ctx_stream_create(sqobfs_ctx *ctx, void **out);
 void sq_ctx_stream_destroy(sqobfs_ctx *ctx, void *s);
 int sq_ctx_stream_wait(sqobfs_ctx *ctx, void *s, uint32_t spin_us);
+// a synchronised library stream about to be destroyed: drop it from the
+// keyring's release fence (sqobfs_keyring_destroy)
+struct sqobfs_keyring;
+void sq_keyring_forget(const sqobfs_keyring *kr, void *s);
 
 // launchers implemented in sq_quic_gcm.hip
 extern "C" int sq_launch_quic_gcm(int open, const sq::QGParams *qp, void *stream);

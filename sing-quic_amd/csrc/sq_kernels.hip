@@ -110,9 +110,11 @@ namespace sq {
 #endif
 // 1: multi-PSK kernels load each lane's keyring entry (chaining value and
 // first message block) right after the descriptor, so the gather overlaps
-// the plan step; 0: loaded by the hash itself (round 2)
+// the plan step (192 VGPRs: 2 waves per SIMD, still 2-3 % faster on the
+// 256-PSK batch in-process, profiles/r03/ab); 0: loaded by the hash itself
+// (round 2)
 #ifndef SQ_PSKPRE
-#define SQ_PSKPRE 0
+#define SQ_PSKPRE 1
 #endif
 // Timeline builds (scripts/dev/timeline.py, never shipped): lane 0 of every
 // wave records the constant-rate clock at its phase boundaries.

@@ -367,8 +367,14 @@ void rx_worker_pump(sqobfs_pconn *pc) {
 }
 
 void free_pconn(sqobfs_pconn *pc) {
-  if (pc->txs) sq_ctx_stream_destroy(pc->ctx, pc->txs);
-  if (pc->rxs) sq_ctx_stream_destroy(pc->ctx, pc->rxs);
+  if (pc->txs) {
+    sq_ctx_stream_destroy(pc->ctx, pc->txs);  // synchronises first
+    sq_keyring_forget(pc->kr, pc->txs);
+  }
+  if (pc->rxs) {
+    sq_ctx_stream_destroy(pc->ctx, pc->rxs);
+    sq_keyring_forget(pc->kr, pc->rxs);
+  }
   if (pc->block) sqobfs_host_free(pc->ctx, pc->block);
   if (pc->fd >= 0) close(pc->fd);
   if (pc->wake >= 0) close(pc->wake);

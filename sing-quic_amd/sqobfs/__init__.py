@@ -203,6 +203,8 @@ def load(path: str) -> ctypes.CDLL:
     L.sqobfs_unit_packets.restype = ctypes.c_uint32
     L.sqobfs_unit_packets_for.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int]
     L.sqobfs_unit_packets_for.restype = ctypes.c_uint32
+    if not hasattr(L, "sqobfs_pconn_open"):
+        return L  # an older build (dev A/B against earlier rounds' libraries)
     L.sqobfs_set_sync_spin.argtypes = [vp, u32]
     L.sqobfs_debug_host_allocs.argtypes = []
     L.sqobfs_debug_host_allocs.restype = ctypes.c_int64
