@@ -413,6 +413,9 @@ def inproc_bench(args):
         n_k = int(cut[k + 1] - cut[k])
         sh = build_shard(torch, dev, kind, n_k, L, n_psk, k, K, args.config, "dense", int(cut[k]))
         c = sqobfs.Context(g)
+        # synchronous shard steps: poll the streams rather than pay the
+        # blocking wake-up (~80 us) after every step
+        c.set_sync_spin(4000)
         c.unit_packets = args.unit_packets or sqobfs.unit_packets_for(
             sh["payload_bytes"], n_k, n_psk > 1)
         kr = sqobfs.Keyring(c, kind, sh["psks"])
@@ -643,7 +646,7 @@ def main():
             "unit_packets": ctx.unit_packets,
             "unit_rule": ("--unit-packets" if args.unit_packets else
                           "sqobfs_unit_packets_for(payload bytes, n): ~21.7 KB per wavefront "
-                          "(36 KB with a multi-PSK keyring)"),
+                          "(33 KB with a multi-PSK keyring; at least 2,048 wavefronts)"),
             "parallelism": f"shard{world} (independent packets, no collective)",
         },
         "roofline": {

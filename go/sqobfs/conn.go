@@ -27,6 +27,7 @@ type Options struct {
 	SlotBytes int           // per-datagram slot (default 2048, hop.go:19)
 	Linger    time.Duration // an idle GPU waits this long for a batch to grow (default 0)
 	Pump      bool          // move datagrams through the wrapped conn even when it is a *net.UDPConn
+	NoOffload bool          // socket mode: no UDP GSO on send / GRO on receive
 }
 
 // Conn is the obfuscating net.PacketConn of SalamanderPacketConn
@@ -111,6 +112,11 @@ func NewConn(conn net.PacketConn, kind Kind, psk []byte, opt Options) (*Conn, er
 	o.batch = C.uint32_t(opt.Batch)
 	o.slot_bytes = C.uint32_t(opt.SlotBytes)
 	o.linger_us = C.uint32_t(opt.Linger / time.Microsecond)
+	if !opt.NoOffload {
+		// UDP_SEGMENT / UDP_GRO, as quic-go uses on its own sockets
+		// (sys_conn_oob.go); the engine falls back if the socket refuses
+		o.flags = C.SQOBFS_UDP_TX_GSO | C.SQOBFS_UDP_RX_GRO
+	}
 	st := C.int(C.SQ_EINVAL)
 	if uc, ok := conn.(*net.UDPConn); ok && !opt.Pump {
 		// socket mode: the engine dup()s the fd inside Control, so it never
@@ -124,6 +130,7 @@ func NewConn(conn net.PacketConn, kind Kind, psk []byte, opt Options) (*Conn, er
 	}
 	if !c.socket {
 		c.addrs = map[uint64]net.Addr{}
+		o.flags = 0 // offloads are socket mode's
 		st = C.sqobfs_pconn_open(ctx.c, kr.kr, -1, &o, &c.pc)
 	}
 	if err := check(st); err != nil {

@@ -186,8 +186,9 @@ int sqobfs_set_unit_packets(sqobfs_ctx *ctx, uint32_t packets);
 /* the unit size device launches will use (the default when 0 was set) */
 uint32_t sqobfs_unit_packets(const sqobfs_ctx *ctx);
 /* The unit size for a batch of n packets holding `bytes` payload (or
- * datagram) bytes in total: about 21.7 KB per wavefront, 36 KB when packets
- * select keyring entries (psk_id != NULL), clamped to 1 .. 62. */
+ * datagram) bytes in total: about 21.7 KB per wavefront, 33 KB when packets
+ * select keyring entries (psk_id != NULL), at least 2,048 wavefronts for
+ * small batches, clamped to 1 .. 62. */
 uint32_t sqobfs_unit_packets_for(uint64_t bytes, uint32_t n, int multi_psk);
 
 /* Upload `count` pre-shared keys (host memory: psk k = blob[off[k] .. +len[k]])
@@ -535,7 +536,11 @@ typedef struct sqobfs_pconn_opts {
                           batch to grow (0: launch at once) */
   uint32_t spin_us;    /* workers poll a launch this long before blocking
                           (0 = 200; they are dedicated threads) */
-  uint32_t flags;      /* 0 */
+  uint32_t flags;      /* socket mode: SQOBFS_UDP_TX_GSO (runs of equal-length
+                          datagrams to one address go out as UDP_SEGMENT
+                          messages; off by itself if the socket refuses) |
+                          SQOBFS_UDP_RX_GRO (coalesced receives, split into
+                          the batch) */
   uint32_t reserved;
 } sqobfs_pconn_opts;
 

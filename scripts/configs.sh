@@ -11,6 +11,11 @@ for c in salamander-1m xplus-1m salamander-ragged-4m salamander-16m-256psk; do
   done
 done
 run --layout slot16 > $O/salamander-1m_slot16.json 2>> $O/err.txt || exit 1
+run --layout slot16 --direction deobfuscate > $O/salamander-1m_slot16_deobfuscate.json 2>> $O/err.txt || exit 1
+run --layout slot2048 > $O/salamander-1m_slot2048.json 2>> $O/err.txt || exit 1
+run --layout slot2048 --direction deobfuscate > $O/salamander-1m_slot2048_deobfuscate.json 2>> $O/err.txt || exit 1
+run --config salamander-ragged-4m --layout slot16 > $O/salamander-ragged-4m_slot16.json 2>> $O/err.txt || exit 1
+run --config salamander-ragged-4m --layout slot16 --direction deobfuscate > $O/salamander-ragged-4m_slot16_deobfuscate.json 2>> $O/err.txt || exit 1
 run --layout inplace > $O/salamander-1m_inplace.json 2>> $O/err.txt || exit 1
 run --device-salt > $O/salamander-1m_devsalt.json 2>> $O/err.txt || exit 1
 run --inproc 2 > $O/salamander-1m_inproc2.json 2>> $O/err.txt || exit 1

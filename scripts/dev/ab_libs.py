@@ -26,13 +26,20 @@ S = sh["S"]
 ob = sqobfs.FLAG_OUT_BLOCKS if sh["slotted"] else 0
 s = torch.cuda.current_stream(dev).cuda_stream
 variants = []
-for path in paths:
-    sqobfs._lib = sqobfs.load(path)
+# AB_PPWS="18,20,..." with one library: one variant per unit size instead
+ppws = [int(x) for x in os.environ.get("AB_PPWS", "").split(",") if x]
+specs = [(paths[0], u) for u in ppws] if ppws else [(p, 0) for p in paths]
+loaded = {}
+for path, u in specs:
+    if path not in loaded:
+        loaded[path] = sqobfs.load(path)
+    sqobfs._lib = loaded[path]
     ctx = sqobfs.Context(0)
     kr = sqobfs.Keyring(ctx, kind, sh["psks"])
-    ctx.unit_packets = int(os.environ.get("AB_PPW", "0")) or sqobfs.unit_packets_for(
+    ctx.unit_packets = u or int(os.environ.get("AB_PPW", "0")) or sqobfs.unit_packets_for(
         sh["payload_bytes"], n, n_psk > 1)
-    variants.append((path, sqobfs._lib, ctx, kr))
+    name = f"{path}@ppw{ctx.unit_packets}" if ppws else path
+    variants.append((name, sqobfs._lib, ctx, kr))
 b = sqobfs.make_batch(n, sh["data"], sh["in_off"], sh["lens"], sh["out"], sh["out_off"],
                       sh["out_len"], sh["salt"], sh["psk_id"], flags=ob)
 d = sqobfs.OBFUSCATE

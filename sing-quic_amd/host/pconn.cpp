@@ -23,6 +23,8 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <netinet/in.h>
+#include <netinet/udp.h>
 #include <poll.h>
 #include <string.h>
 #include <sys/eventfd.h>
@@ -49,6 +51,10 @@ constexpr uint32_t kDefBatch = 256, kDefSlot = 2048, kDefBatches = 3, kDefSpinUs
 constexpr uint32_t kMaxBatch = 1u << 16;
 constexpr int64_t kDrainNs = 200'000'000;  // shutdown: time given to queued writes
 constexpr uint32_t kMmsg = 256;            // messages per sendmmsg / recvmmsg call
+constexpr uint32_t kGsoMaxSegs = 64;       // UDP_MAX_SEGMENTS of older kernels
+constexpr uint32_t kGsoMaxBytes = 65000;   // one GSO send stays below 64 KiB of IP payload
+constexpr uint32_t kGroBuf = 65536;        // one coalesced receive
+constexpr size_t kCtlWords = (CMSG_SPACE(sizeof(uint16_t)) + 7) / 8;
 
 int64_t unix_ns() {
   timespec ts;
@@ -122,6 +128,9 @@ struct sqobfs_pconn {
   std::vector<mmsghdr> tmsg, rmsg;
   std::vector<iovec> tiov, riov;
   std::vector<sockaddr_storage> tss, rss;
+  std::vector<uint64_t> tctl, rctl;  // UDP_SEGMENT / UDP_GRO control messages
+  std::vector<uint32_t> tfirst;      // first datagram of each transmit message
+  bool gso = false, gro = false;     // offloads in effect (socket mode)
 
   bool socket_mode() const { return fd >= 0; }
   uint8_t *slot(PBatch &b, uint32_t i) { return b.slots + (size_t)i * o.slot_bytes; }
@@ -146,13 +155,15 @@ bool wait_dl(std::unique_lock<std::mutex> &lk, std::condition_variable &cv, cons
   return true;
 }
 
-int launch_wait(sqobfs_pconn *pc, void *stream, int dir, PBatch &b) {
+int launch_wait(sqobfs_pconn *pc, void *stream, int dir, PBatch &b, bool slotted = true) {
   sqobfs_batch d;
   memset(&d, 0, sizeof d);
   d.n = b.n;
   // slots are multiples of 16 bytes: every output owns its blocks, so the
-  // kernel writes them whole (SQOBFS_FLAG_OUT_BLOCKS)
-  d.flags = SQOBFS_FLAG_OUT_BLOCKS | (dir == SQOBFS_OBFUSCATE ? SQOBFS_FLAG_DEVICE_SALT : 0u);
+  // kernel writes them whole (SQOBFS_FLAG_OUT_BLOCKS); GRO buffers pack the
+  // datagrams back to back (no flag)
+  d.flags = (slotted ? SQOBFS_FLAG_OUT_BLOCKS : 0u) |
+            (dir == SQOBFS_OBFUSCATE ? SQOBFS_FLAG_DEVICE_SALT : 0u);
   d.in = b.slots;
   d.in_off = b.in_off;
   d.in_len = b.len;
@@ -164,27 +175,60 @@ int launch_wait(sqobfs_pconn *pc, void *stream, int dir, PBatch &b) {
   return sq_ctx_stream_wait(pc->ctx, stream, pc->o.spin_us);
 }
 
-// sendmmsg of a transmitted batch.  A datagram the socket refuses is
-// skipped (UDP is best effort; the reference's per-datagram WriteTo would
-// have returned its error) and its error reported by the next write.
-// Returns SQ_ECLOSED when shutdown interrupts a wait for socket space.
-int send_batch(sqobfs_pconn *pc, PBatch &b, int *first_err, uint64_t *errors) {
-  uint32_t done = 0;
-  while (done < b.n) {
-    const uint32_t k = std::min(b.n - done, kMmsg);
-    for (uint32_t j = 0; j < k; j++) {
-      const uint32_t i = done + j;
-      pc->tiov[j].iov_base = pc->slot(b, i);
-      pc->tiov[j].iov_len = b.out_len[i];
-      memset(&pc->tmsg[j], 0, sizeof pc->tmsg[j]);
-      socklen_t sl;
-      sq::to_sockaddr(b.addr[i], &pc->tss[j], &sl);
-      pc->tmsg[j].msg_hdr.msg_iov = &pc->tiov[j];
-      pc->tmsg[j].msg_hdr.msg_iovlen = 1;
-      pc->tmsg[j].msg_hdr.msg_name = &pc->tss[j];
-      pc->tmsg[j].msg_hdr.msg_namelen = sl;
+// sendmmsg of a transmitted batch.  With GSO, consecutive datagrams to one
+// address whose lengths are equal (the last of a run may be shorter) go out
+// as one message with a UDP_SEGMENT control message (at most 64 datagrams /
+// 65,000 bytes), each datagram still its own iovec in its slot; a socket
+// that refuses turns GSO off and the rest goes one datagram per message.  A
+// datagram (message) the socket refuses is skipped -- UDP is best effort;
+// the reference's per-datagram WriteTo would have returned its error -- and
+// its error is reported by the next write.  SQ_ECLOSED when shutdown
+// interrupts a wait for socket space.
+int send_batch(sqobfs_pconn *pc, PBatch &b, uint32_t from, int *first_err, uint64_t *errors) {
+  // messages over datagrams [from, n)
+  uint32_t nm = 0;
+  for (uint32_t i = from; i < b.n;) {
+    uint32_t j = i + 1;
+    if (pc->gso) {
+      const uint32_t g = b.out_len[i];
+      uint32_t bytes = g;
+      while (j < b.n && j - i < kGsoMaxSegs && g > 0 && b.out_len[j] <= g && b.out_len[j] > 0 &&
+             bytes + b.out_len[j] <= kGsoMaxBytes &&
+             memcmp(&b.addr[j], &b.addr[i], sizeof b.addr[i]) == 0) {
+        bytes += b.out_len[j];
+        j++;
+        if (b.out_len[j - 1] < g) break;
+      }
     }
-    const int m = sendmmsg(pc->fd, pc->tmsg.data(), k, MSG_DONTWAIT);
+    for (uint32_t k = i; k < j; k++) {
+      pc->tiov[k].iov_base = pc->slot(b, k);
+      pc->tiov[k].iov_len = b.out_len[k];
+    }
+    mmsghdr &h = pc->tmsg[nm];
+    memset(&h, 0, sizeof h);
+    socklen_t sl;
+    sq::to_sockaddr(b.addr[i], &pc->tss[nm], &sl);
+    h.msg_hdr.msg_name = &pc->tss[nm];
+    h.msg_hdr.msg_namelen = sl;
+    h.msg_hdr.msg_iov = &pc->tiov[i];
+    h.msg_hdr.msg_iovlen = j - i;
+    if (j - i > 1) {
+      h.msg_hdr.msg_control = &pc->tctl[kCtlWords * nm];
+      h.msg_hdr.msg_controllen = CMSG_SPACE(sizeof(uint16_t));
+      cmsghdr *cm = CMSG_FIRSTHDR(&h.msg_hdr);
+      cm->cmsg_level = SOL_UDP;
+      cm->cmsg_type = UDP_SEGMENT;
+      cm->cmsg_len = CMSG_LEN(sizeof(uint16_t));
+      const uint16_t gs = (uint16_t)b.out_len[i];
+      memcpy(CMSG_DATA(cm), &gs, sizeof gs);
+    }
+    pc->tfirst[nm++] = i;
+    i = j;
+  }
+  uint32_t done = 0;
+  while (done < nm) {
+    const uint32_t k = std::min(nm - done, kMmsg);
+    const int m = sendmmsg(pc->fd, &pc->tmsg[done], k, MSG_DONTWAIT);
     if (m < 0) {
       const int e = errno;
       if (e == EINTR) continue;
@@ -194,9 +238,14 @@ int send_batch(sqobfs_pconn *pc, PBatch &b, int *first_err, uint64_t *errors) {
         if (p[1].revents & POLLIN) return SQ_ECLOSED;
         continue;
       }
+      if (pc->gso && pc->tmsg[done].msg_hdr.msg_iovlen > 1 &&
+          (e == EIO || e == EINVAL || e == ENOPROTOOPT || e == EOPNOTSUPP)) {
+        pc->gso = false;  // no segmentation offload here: one datagram per message
+        return send_batch(pc, b, pc->tfirst[done], first_err, errors);
+      }
       if (!*first_err) *first_err = SQOBFS_ERRNO(e);
-      ++*errors;
-      done++;  // the datagram at `done` failed: go on with the next
+      *errors += pc->tmsg[done].msg_hdr.msg_iovlen;
+      done++;  // this message failed: go on with the next
       continue;
     }
     done += (uint32_t)m;
@@ -233,7 +282,7 @@ void tx_worker(sqobfs_pconn *pc) {
     int st = launch_wait(pc, pc->txs, SQOBFS_OBFUSCATE, b);
     int send_err = 0;
     uint64_t nerr = 0;
-    if (st == SQ_OK && pc->socket_mode()) st = send_batch(pc, b, &send_err, &nerr);
+    if (st == SQ_OK && pc->socket_mode()) st = send_batch(pc, b, 0, &send_err, &nerr);
     lk.lock();
     pc->tx_busy = false;
     if (st != SQ_OK && st != SQ_ECLOSED && !pc->tx_err) pc->tx_err = st;
@@ -268,20 +317,30 @@ void rx_worker_socket(sqobfs_pconn *pc) {
     }
     PBatch &b = pc->rb[idx];
     int m = 0;
+    // GRO: the batch's slot region as 64 KiB buffers of up to 64 coalesced
+    // datagrams each (so the batch arrays always have room)
+    const uint32_t ngro = pc->gro ? std::max<uint32_t>(1, std::min<uint64_t>(
+                                        (uint64_t)pc->o.batch * pc->o.slot_bytes / kGroBuf,
+                                        pc->o.batch / kGsoMaxSegs))
+                                  : 0;
     for (;;) {
       pollfd p[2] = {{pc->fd, POLLIN, 0}, {pc->wake, POLLIN, 0}};
       const int r = poll(p, 2, -1);
       if (r < 0 && errno == EINTR) continue;
       if (p[1].revents & POLLIN) return;  // shutdown
-      const uint32_t want = pc->o.batch;
+      const uint32_t want = pc->gro ? ngro : pc->o.batch;
       for (uint32_t j = 0; j < want; j++) {
-        pc->riov[j].iov_base = pc->slot(b, j);
-        pc->riov[j].iov_len = pc->o.slot_bytes;
+        pc->riov[j].iov_base = pc->gro ? b.slots + (size_t)j * kGroBuf : pc->slot(b, j);
+        pc->riov[j].iov_len = pc->gro ? kGroBuf : pc->o.slot_bytes;
         memset(&pc->rmsg[j], 0, sizeof pc->rmsg[j]);
         pc->rmsg[j].msg_hdr.msg_iov = &pc->riov[j];
         pc->rmsg[j].msg_hdr.msg_iovlen = 1;
         pc->rmsg[j].msg_hdr.msg_name = &pc->rss[j];
         pc->rmsg[j].msg_hdr.msg_namelen = sizeof pc->rss[j];
+        if (pc->gro) {
+          pc->rmsg[j].msg_hdr.msg_control = &pc->rctl[8ull * j];
+          pc->rmsg[j].msg_hdr.msg_controllen = 8 * sizeof(uint64_t);
+        }
       }
       m = recvmmsg(pc->fd, pc->rmsg.data(), want, MSG_DONTWAIT, nullptr);
       if (m > 0) break;
@@ -297,16 +356,50 @@ void rx_worker_socket(sqobfs_pconn *pc) {
       if (!transient) return;
     }
     uint64_t trunc = 0;
-    for (int j = 0; j < m; j++) {
-      b.len[j] = std::min<uint32_t>(pc->rmsg[j].msg_len, pc->o.slot_bytes);
-      memcpy(&b.head[16ull * j], pc->slot(b, (uint32_t)j), 16);
-      if (pc->rmsg[j].msg_hdr.msg_flags & MSG_TRUNC) trunc++;
-      sq::from_sockaddr(pc->rss[j], &b.addr[j]);
-      b.tag[j] = 0;
+    uint32_t n = 0;
+    if (pc->gro) {
+      // split every coalesced message into its datagrams (cmsg UDP_GRO gives
+      // the segment size; the last may be shorter), decoded in place
+      for (int j = 0; j < m; j++) {
+        const uint32_t total = pc->rmsg[j].msg_len;
+        uint32_t seg = total;
+        for (cmsghdr *cm = CMSG_FIRSTHDR(&pc->rmsg[j].msg_hdr); cm;
+             cm = CMSG_NXTHDR(&pc->rmsg[j].msg_hdr, cm))
+          if (cm->cmsg_level == SOL_UDP && cm->cmsg_type == UDP_GRO) {
+            int v;
+            memcpy(&v, CMSG_DATA(cm), sizeof v);
+            if (v > 0) seg = (uint32_t)v;
+          }
+        if (pc->rmsg[j].msg_hdr.msg_flags & MSG_TRUNC) trunc++;
+        sqobfs_addr from;
+        sq::from_sockaddr(pc->rss[j], &from);
+        const uint64_t base = (uint64_t)j * kGroBuf;
+        for (uint32_t o = 0; (o < total || (total == 0 && o == 0)) && n < pc->o.batch;
+             o += seg ? seg : 1) {
+          const uint32_t l = std::min(seg, total - o);
+          b.in_off[n] = base + o;
+          b.out_off[n] = base + o + pc->S;
+          b.len[n] = l;
+          memcpy(&b.head[16ull * n], b.slots + base + o, std::min<uint32_t>(16, l));
+          b.addr[n] = from;
+          b.tag[n] = 0;
+          n++;
+          if (total == 0) break;
+        }
+      }
+    } else {
+      for (int j = 0; j < m; j++) {
+        b.len[j] = std::min<uint32_t>(pc->rmsg[j].msg_len, pc->o.slot_bytes);
+        memcpy(&b.head[16ull * j], pc->slot(b, (uint32_t)j), 16);
+        if (pc->rmsg[j].msg_hdr.msg_flags & MSG_TRUNC) trunc++;
+        sq::from_sockaddr(pc->rss[j], &b.addr[j]);
+        b.tag[j] = 0;
+      }
+      n = (uint32_t)m;
     }
-    b.n = (uint32_t)m;
+    b.n = n;
     b.next = 0;
-    const int st = launch_wait(pc, pc->rxs, SQOBFS_DEOBFUSCATE, b);
+    const int st = launch_wait(pc, pc->rxs, SQOBFS_DEOBFUSCATE, b, !pc->gro);
     std::lock_guard<std::mutex> lk(pc->mu);
     pc->st.rx_truncated += trunc;
     if (st != SQ_OK) {
@@ -398,8 +491,9 @@ int sqobfs_pconn_open(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int fd,
   if (o.spin_us == 0) o.spin_us = kDefSpinUs;
   const int kind = sqobfs_keyring_kind(kr);
   const uint32_t S = kind == SQOBFS_SALAMANDER ? SQOBFS_SALAMANDER_SALT_LEN : SQOBFS_XPLUS_SALT_LEN;
-  if (o.batch > kMaxBatch || o.slot_bytes % 16 || o.slot_bytes <= S || o.flags ||
-      o.tx_batches > 64 || o.rx_batches > 64)
+  if (o.batch > kMaxBatch || o.slot_bytes % 16 || o.slot_bytes <= S ||
+      (o.flags & ~(uint32_t)(SQOBFS_UDP_TX_GSO | SQOBFS_UDP_RX_GRO)) || o.tx_batches > 64 ||
+      o.rx_batches > 64)
     return SQ_EINVAL;
   sqobfs_pconn *pc = new (std::nothrow) sqobfs_pconn();
   if (!pc) return SQ_ENOMEM;
@@ -464,12 +558,21 @@ int sqobfs_pconn_open(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int fd,
     else pc->rfree.push_back(k - o.tx_batches);
   }
   if (pc->socket_mode()) {
-    pc->tmsg.resize(kMmsg);
-    pc->tiov.resize(kMmsg);
-    pc->tss.resize(kMmsg);
+    pc->tmsg.resize(B);
+    pc->tiov.resize(B);
+    pc->tss.resize(B);
+    pc->tctl.assign(kCtlWords * B, 0);
+    pc->tfirst.resize(B);
     pc->rmsg.resize(B);
     pc->riov.resize(B);
     pc->rss.resize(B);
+    pc->gso = o.flags & SQOBFS_UDP_TX_GSO;  // probed by the first send
+    if ((o.flags & SQOBFS_UDP_RX_GRO) && B >= kGsoMaxSegs &&
+        (uint64_t)B * o.slot_bytes >= kGroBuf) {
+      const int one = 1;
+      pc->gro = setsockopt(pc->fd, SOL_UDP, UDP_GRO, &one, sizeof one) == 0;
+      if (pc->gro) pc->rctl.assign(8ull * B, 0);
+    }
   }
   try {
     pc->txw = std::thread(tx_worker, pc);
@@ -614,7 +717,7 @@ int sqobfs_pconn_read(sqobfs_pconn *pc, uint8_t *p, uint32_t cap, uint32_t *n,
     r = 0;                  // xplus.go:50-52
   } else {
     r = m - S;              // the first m - S payload bytes
-    src = pc->slot(b, i) + S;
+    src = b.slots + b.out_off[i];
   }
   if (r) memcpy(p, src, r);
   *n = r;

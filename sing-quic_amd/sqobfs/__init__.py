@@ -312,6 +312,10 @@ class Context:
     def salt_seq(self) -> int:
         return lib().sqobfs_salt_seq(self.handle)
 
+    def set_sync_spin(self, us: int) -> None:
+        """sqobfs_sync polls the stream this long before blocking (opt-in)."""
+        _check(lib().sqobfs_set_sync_spin(self.handle, us), "sqobfs_set_sync_spin")
+
     @property
     def unit_packets(self) -> int:
         """Packets per wavefront of the obfuscation kernel (tuning only)."""

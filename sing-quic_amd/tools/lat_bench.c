@@ -348,13 +348,19 @@ int main(void) {
   }
 
   /* ---- pconn throughput: pconn A -> pconn B over loopback, one writer
-   * thread (the Go Conn's WriteTo callers), one reader thread */
-  {
+   * thread (the Go Conn's WriteTo callers), one reader thread; without and
+   * with UDP GSO (A) / GRO (B) */
+  for (int off = 0; off < 2; off++) {
     uint16_t pa, pb;
     int fa = udp_socket(&pa), fb = udp_socket(&pb);
     sqobfs_pconn *A, *B;
-    CHECK(sqobfs_pconn_open(ctx, kr, fa, NULL, &A));
-    CHECK(sqobfs_pconn_open(ctx, kr, fb, NULL, &B));
+    sqobfs_pconn_opts oa, ob;
+    memset(&oa, 0, sizeof oa);
+    memset(&ob, 0, sizeof ob);
+    oa.flags = off ? SQOBFS_UDP_TX_GSO : 0u;
+    ob.flags = off ? SQOBFS_UDP_RX_GRO : 0u;
+    CHECK(sqobfs_pconn_open(ctx, kr, fa, &oa, &A));
+    CHECK(sqobfs_pconn_open(ctx, kr, fb, &ob, &B));
     const sqobfs_addr to = loop_addr(pb);
     static uint8_t pay[L];
     memset(pay, 9, L);
@@ -383,10 +389,10 @@ int main(void) {
     sqobfs_pconn_stats sa, sb;
     CHECK(sqobfs_pconn_stats_get(A, &sa));
     CHECK(sqobfs_pconn_stats_get(B, &sb));
-    printf("\"pconn_throughput\": {\"datagrams\": %ld, \"received\": %ld, \"seconds\": %.3f, "
+    printf("\"pconn_throughput%s\": {\"datagrams\": %ld, \"received\": %ld, \"seconds\": %.3f, "
            "\"datagrams_per_s\": %.0f, \"payload_gib_s\": %.3f, \"tx_batches\": %llu, "
            "\"rx_batches\": %llu}, ",
-           N, r.got, dt, r.got / dt, r.got * (double)L / dt / (1 << 30),
+           off ? "_gso_gro" : "", N, r.got, dt, r.got / dt, r.got * (double)L / dt / (1 << 30),
            (unsigned long long)sa.tx_batches, (unsigned long long)sb.rx_batches);
     sqobfs_pconn_close(A);
     sqobfs_pconn_close(B);

@@ -183,14 +183,17 @@ static void *peer_rx(void *arg) {
   return NULL;
 }
 
-static void t_wire(int kind) {
+static void t_wire(int kind, uint32_t offload) {
   const int S = salt_len(kind), N = 1500;
   const int64_t a0 = sqobfs_debug_host_allocs();
   sqobfs_keyring *kr = keyring(kind);
   uint16_t pa, pp;
   int fa = udp_socket(&pa), fp = udp_socket(&pp);
   sqobfs_pconn *pc = NULL;
-  CHECK(sqobfs_pconn_open(g_ctx, kr, fa, NULL, &pc));
+  sqobfs_pconn_opts o;
+  memset(&o, 0, sizeof o);
+  o.flags = offload;
+  CHECK(sqobfs_pconn_open(g_ctx, kr, fa, &o, &pc));
   static uint8_t pay[1500][MAXW], wire[1500][MAXW];
   static uint32_t plen[1500];
   static long wlen[1500];
@@ -200,6 +203,7 @@ static void t_wire(int kind) {
   const sqobfs_addr to = loop_addr(pp);
   for (int i = 0; i < N; i++) {
     plen[i] = pick_len(i, S, 2048);
+    if (offload && i % 3) plen[i] = 1300; /* runs of equal lengths: GSO messages */
     for (uint32_t j = 0; j < plen[i]; j++) pay[i][j] = (uint8_t)rnd();
     CHECK(sqobfs_pconn_write(pc, pay[i], plen[i], &to, (uint64_t)i));
     if (i % 200 == 199) sleep_ms(2); /* bursts with gaps: small and large batches */
@@ -216,8 +220,8 @@ static void t_wire(int kind) {
   sqobfs_pconn_stats st;
   CHECK(sqobfs_pconn_stats_get(pc, &st));
   EXPECT(st.tx_datagrams == (uint64_t)N, "tx_datagrams %llu", (unsigned long long)st.tx_datagrams);
-  printf("  wire kind %d: %d datagrams in %llu batches (max %u), wire == reference\n", kind, N,
-         (unsigned long long)st.tx_batches, st.tx_max_batch);
+  printf("  wire kind %d%s: %d datagrams in %llu batches (max %u), wire == reference\n", kind,
+         offload ? " (GSO)" : "", N, (unsigned long long)st.tx_batches, st.tx_max_batch);
   sqobfs_pconn_close(pc);
   close(fa);
   close(fp);
@@ -315,19 +319,25 @@ static void *reader(void *arg) {
   return NULL;
 }
 
-static void t_roundtrip(int kind) {
+static void t_roundtrip(int kind, uint32_t offload) {
   const int S = salt_len(kind), N = 3000;
   const int64_t a0 = sqobfs_debug_host_allocs();
   sqobfs_keyring *kr = keyring(kind);
   uint16_t pa, pb;
   int fa = udp_socket(&pa), fb = udp_socket(&pb);
   sqobfs_pconn *A = NULL, *B = NULL;
-  CHECK(sqobfs_pconn_open(g_ctx, kr, fa, NULL, &A));
-  CHECK(sqobfs_pconn_open(g_ctx, kr, fb, NULL, &B));
+  sqobfs_pconn_opts oa, ob;
+  memset(&oa, 0, sizeof oa);
+  memset(&ob, 0, sizeof ob);
+  oa.flags = offload & SQOBFS_UDP_TX_GSO; /* A sends with GSO, B receives with GRO */
+  ob.flags = offload & SQOBFS_UDP_RX_GRO;
+  CHECK(sqobfs_pconn_open(g_ctx, kr, fa, &oa, &A));
+  CHECK(sqobfs_pconn_open(g_ctx, kr, fb, &ob, &B));
   static uint8_t pay[3000][2048];
   static uint32_t plen[3000];
   for (int i = 0; i < N; i++) {
     plen[i] = pick_len(i, S, 2048);
+    if (offload && i % 4) plen[i] = 1350; /* equal-length runs: GSO out, GRO in */
     for (uint32_t j = 0; j < plen[i]; j++) pay[i][j] = (uint8_t)rnd();
   }
   Reader r = {B, kind, N, 0, 0, plen, pay};
@@ -342,7 +352,12 @@ static void t_roundtrip(int kind) {
   pthread_join(th, NULL);
   const double dt = now_s() - t0;
   EXPECT(r.got == N && r.bad == 0, "kind %d roundtrip: got %d bad %d of %d", kind, r.got, r.bad, N);
-  printf("  roundtrip kind %d: %d datagrams A -> B in %.1f ms\n", kind, N, dt * 1e3);
+  sqobfs_pconn_stats sa, sb;
+  CHECK(sqobfs_pconn_stats_get(A, &sa));
+  CHECK(sqobfs_pconn_stats_get(B, &sb));
+  printf("  roundtrip kind %d%s: %d datagrams A -> B in %.1f ms (%llu tx / %llu rx batches)\n",
+         kind, offload ? " (GSO -> GRO)" : "", N, dt * 1e3, (unsigned long long)sa.tx_batches,
+         (unsigned long long)sb.rx_batches);
   sqobfs_pconn_close(A);
   sqobfs_pconn_close(B);
   close(fa);
@@ -575,9 +590,11 @@ int main(int argc, char **argv) {
   (void)argv;
   CHECK(sqobfs_open(0, &g_ctx));
   for (int kind = 0; kind < 2; kind++) {
-    t_wire(kind);
+    t_wire(kind, 0);
+    t_wire(kind, SQOBFS_UDP_TX_GSO);
     t_read(kind);
-    t_roundtrip(kind);
+    t_roundtrip(kind, 0);
+    t_roundtrip(kind, SQOBFS_UDP_TX_GSO | SQOBFS_UDP_RX_GRO);
     t_pump(kind);
   }
   t_deadline();
