@@ -19,3 +19,16 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
     || { echo "pass $i ($grp) failed"; tail -5 $O/p$i.log; exit 1; }
 done
 python scripts/pmc_summary.py $O
+# keep the outputs small (gpurun returns at most 64 MiB): the obfs_kernel rows
+# of every CSV, nothing else
+python - "$O" <<'PY'
+import csv, glob, os, sys
+for f in glob.glob(os.path.join(sys.argv[1], "**", "*.csv"), recursive=True):
+    rows = list(csv.reader(open(f)))
+    if not rows or "Kernel_Name" not in rows[0]:
+        continue
+    k = rows[0].index("Kernel_Name")
+    keep = [rows[0]] + [r for r in rows[1:] if len(r) > k and "obfs_kernel" in r[k]]
+    csv.writer(open(f, "w", newline="")).writerows(keep)
+PY
+du -sh $O
