@@ -131,7 +131,9 @@ def build_shard(torch, dev, kind, n, L, n_psk, rank, world, config, layout, firs
         lens = torch.randint(64, 1453, (n,), generator=g, device=dev, dtype=torch.int64)
     else:
         lens = torch.full((n,), L, device=dev, dtype=torch.int64)
-    lead = 64  # buffers start with 64 spare bytes
+    # buffers start with 64 spare bytes (dev probe SQ_BENCH_LEAD: slot phase
+    # within the 128-byte line)
+    lead = int(os.environ.get("SQ_BENCH_LEAD", "64"))
     if layout in ("slot16", "slot2048"):
         # every packet in its own 16-byte-aligned slot (16 B-
         # aligned input offsets), or in fixed 2048-byte slots

@@ -361,12 +361,18 @@ struct PskHot {
   uint32_t nblocks, salt_pos;
 };
 
+// message words of the first block loaded early (timing builds vary it; the
+// rest are read by the hash)
+#ifndef SQ_PSKPRE_M
+#define SQ_PSKPRE_M 16
+#endif
 template <int KIND>
 __device__ __forceinline__ void load_hot(const PskEntry *E, PskHot &H) {
 #pragma unroll
   for (int i = 0; i < 8; i++) H.h[i] = KIND == 0 || i < 4 ? E->h[i] : 0ull;
 #pragma unroll
-  for (int i = 0; i < 16; i++) H.m[i] = KIND == 0 || i < 8 ? E->m[i] : 0ull;
+  for (int i = 0; i < 16; i++)
+    H.m[i] = (KIND == 0 || i < 8) && i < SQ_PSKPRE_M ? E->m[i] : 0ull;
   H.t_first = KIND == 0 ? E->t_first : 0ull;
   H.t_last = KIND == 0 ? E->t_last : 0ull;
   H.nblocks = E->nblocks;
@@ -390,7 +396,7 @@ __device__ __forceinline__ void salamander_key_hot(const PskHot &H, const PskEnt
 #pragma unroll
     for (int j = 0; j < 16; j++) {
       const uint32_t idx = 16 * blk + j;
-      uint64_t x = blk == 0 ? H.m[j] : E->m[idx];
+      uint64_t x = blk == 0 && j < SQ_PSKPRE_M ? H.m[j] : E->m[idx];
       x |= (idx == w) ? lo : 0ull;
       x |= (idx == w + 1) ? hi : 0ull;
       m[j] = x;
@@ -430,7 +436,8 @@ __device__ __forceinline__ void xplus_key_hot(const PskHot &H, const PskEntry *E
     for (int j = 0; j < 16; j++) {
       const uint32_t idx = 16 * blk + j;
       const uint64_t hv = H.m[j >> 1];
-      uint32_t x = blk == 0 ? (uint32_t)(j & 1 ? hv >> 32 : hv) : m32[idx];
+      uint32_t x = blk == 0 && (j >> 1) < SQ_PSKPRE_M ? (uint32_t)(j & 1 ? hv >> 32 : hv)
+                                                     : m32[idx];
 #pragma unroll
       for (int k = 0; k < 5; k++) x |= (idx == w + k) ? c[k] : 0u;
       m[j] = x;
