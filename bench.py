@@ -832,6 +832,44 @@ def quic_rate(torch, sqobfs, ctx, dev, steps, n=1 << 20, payload=1350, cpu_secon
                          "frac_of_8TBs": round(alg / (ms * 1e-3) / 8e12, 4),
                          "valu_roofline": quic_valu_roofline(
                              "aes_128_gcm" if suite else "chacha20_poly1305", name, ms * 1e3)}
+    # several connections in one launch (the multi-key kernels: key_id per
+    # packet, keys gathered from the device keyring): 16 keys, key_id = i mod 16
+    nk = 16
+    mk = [tuple(rng.integers(0, 256, m, dtype=np.uint8).tobytes() for m in (kl, 12, kl))
+          for _ in range(nk)]
+    kid = (torch.arange(n, device=dev, dtype=torch.int64) % nk).to(torch.int16)
+    msealed = torch.zeros_like(sealed)
+    mopened = torch.zeros_like(opened)
+    molen = torch.zeros_like(olen)
+    molen2 = torch.zeros_like(olen2)
+    mpn_out = torch.zeros_like(pn_out)
+    with sqobfs.QuicKeyring(ctx, [sqobfs.QuicKey.of(*k) for k in mk], suite) as kr:
+        bs = sqobfs.quic_batch(n, data, in_off, lens, msealed, out_off, molen, pno, pn, key_id=kid)
+        bo = sqobfs.quic_batch(n, msealed, out_off, slens, mopened, in_off, molen2, pno, largest,
+                               key_id=kid, pn_out=mpn_out)
+        mres = {"keys": nk}
+        for name, fn, b in (("seal", sqobfs.quic_seal, bs), ("open", sqobfs.quic_open, bo)):
+            warm_up(torch, dev, lambda: fn(ctx, kr, b, s))
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(steps):
+                fn(ctx, kr, b, s)
+            e1.record()
+            torch.cuda.synchronize(dev)
+            ms = e0.elapsed_time(e1) / steps
+            mres[name] = {"kernel_avg_us": round(ms * 1e3, 2),
+                          "GiB_s_payload": round(n * payload / (ms * 1e-3) / 2**30, 2)}
+        midx = sorted(set([0, n - 1] + list(range(0, n, 8191))))[:150]
+        dm = data.view(n, ln)[midx].cpu().numpy()
+        slm = msealed.view(n, ln + 16)[midx].cpu().numpy()
+        opm = mopened.view(n, ln)[midx].cpu().numpy()
+        mok = bool((molen.cpu().numpy() == ln + 16).all() and (molen2.cpu().numpy() == ln).all())
+        for k, i in enumerate(midx):
+            kk = mk[i % nk]
+            want, _ = ol.quic_seal(kk[0], kk[1], kk[2], 1000 + i, dm[k].tobytes(), 9, suite=suite)
+            mok = mok and slm[k].tobytes() == want and opm[k].tobytes() == dm[k].tobytes()
+        mres["parity_spot_check"] = mok
+    res["multi_key"] = mres
     res["fused_salamander"] = quic_fused_rate(torch, sqobfs, ctx, dev, steps, n, ln, data,
                                               in_off, lens, pno, pn, key, iv, hp, suite)
     sn = "aes_128_gcm" if suite else "chacha20_poly1305"

@@ -2,7 +2,9 @@
 on ONE buffer set, interleaved rounds (box and allocation effects cancel).
 usage: ab_libs.py CONFIG DIRECTION ROUNDS lib1.so lib2.so ...
 Prints per lib the median kernel time and frac of 8 TB/s, and checks every
-build's output against the first one's (parity of the variants)."""
+build's output against the first one's (parity of the variants).
+AB_KR=k: k contexts + keyrings per build (keyring tables at k different
+addresses; per-instance medians are printed, the build's median is over all)."""
 import os
 import statistics
 import sys
@@ -29,6 +31,7 @@ variants = []
 # AB_PPWS="18,20,..." with one library: one variant per unit size instead
 ppws = [int(x) for x in os.environ.get("AB_PPWS", "").split(",") if x]
 specs = [(paths[0], u) for u in ppws] if ppws else [(p, 0) for p in paths]
+specs = specs * int(os.environ.get("AB_KR", "1"))
 loaded = {}
 for path, u in specs:
     if path not in loaded:
@@ -40,6 +43,7 @@ for path, u in specs:
         sh["payload_bytes"], n, n_psk > 1)
     name = f"{path}@ppw{ctx.unit_packets}" if ppws else path
     variants.append((name, sqobfs._lib, ctx, kr))
+names = list(dict.fromkeys(v[0] for v in variants))
 b = sqobfs.make_batch(n, sh["data"], sh["in_off"], sh["lens"], sh["out"], sh["out_off"],
                       sh["out_len"], sh["salt"], sh["psk_id"], flags=ob)
 d = sqobfs.OBFUSCATE
@@ -95,11 +99,18 @@ for v in variants:
     for _ in range(40):
         sqobfs.launch(v[2], v[3], d, b, s)
 torch.cuda.synchronize()
-res = {v[0]: [] for v in variants}
+res = {nm: [] for nm in names}
+inst = [[] for _ in variants]
 for r in range(rounds):
-    for v in variants:
-        res[v[0]].append(round(timed(v), 1))
-for v in variants:
-    med = statistics.median(res[v[0]])
-    print(f"{cfg:24s} {direction[:3]} {os.path.basename(v[0]):24s} median {med:8.1f} us  "
-          f"frac {alg / med / 8e6:.4f}  all {res[v[0]]}", flush=True)
+    for i, v in enumerate(variants):
+        t = round(timed(v), 1)
+        res[v[0]].append(t)
+        inst[i].append(t)
+if len(variants) > len(names):
+    for i, v in enumerate(variants):
+        print(f"  instance {i} {os.path.basename(v[0])}: median {statistics.median(inst[i]):8.1f}",
+              flush=True)
+for nm in names:
+    med = statistics.median(res[nm])
+    print(f"{cfg:24s} {direction[:3]} {os.path.basename(nm):24s} median {med:8.1f} us  "
+          f"frac {alg / med / 8e6:.4f}  all {res[nm]}", flush=True)

@@ -113,6 +113,9 @@ struct sqobfs_keyring {
   uint32_t count = 0;
   sq::PskEntry *table = nullptr;  // device
   sq::PskEntry host0;             // entry 0, passed by value to the kernels
+  sq::PskHotLine *hot = nullptr;  // device, one line per entry (same allocation as table)
+  uint32_t hot_m = 16;            // block-0 message words any entry needs
+  uint32_t hot_iv = 0;            // 1: every entry starts from the hash's initial state
 };
 
 namespace {
@@ -273,6 +276,11 @@ sq::KParams make_params(sqobfs_ctx *ctx, const sqobfs_keyring *kr, const sqobfs_
   kp.n = b->n;
   kp.n_psk = kr->count;
   kp.psk0 = kr->host0;
+  kp.psk_hot_m = kr->hot_m;
+  kp.psk_hot_iv = kr->hot_iv;
+  // one-line entries when every PSK is short (no chaining value to load, the
+  // first block's live words fit the line)
+  kp.psk_hotl = kr->hot_iv && kr->hot_m <= sq::kHotLineWords ? kr->hot : nullptr;
   kp.ppw = ctx->unit_packets.load(std::memory_order_relaxed);
   kp.out_blocks = (b->flags & SQOBFS_FLAG_OUT_BLOCKS) ? 1u : 0u;
   if (b->flags & SQOBFS_FLAG_DEVICE_SALT) {
@@ -509,6 +517,36 @@ int sqobfs_set_sync_spin(sqobfs_ctx *ctx, uint32_t us) {
   return SQ_OK;
 }
 
+namespace {
+
+// What the multi-PSK kernels gather per packet from an entry (sq_kernels.hip
+// load_hot), from the PSK lengths alone (the entry layout of
+// psk_prepare_kernel): `m` = the message words of the first compressed
+// block any entry has non-zero -- BLAKE2b: PSK tail || salt, zero padded,
+// all 16 when the salt spills into a second block; SHA-256: all 8 (its
+// length field ends the block) -- and `iv` = 1 when no PSK has a PSK-only
+// leading block, so every chaining value is the hash's initial state and is
+// not loaded.  Keyrings of short PSKs (the common 8-64 bytes) then gather
+// ~96 instead of ~216 bytes per packet.
+void keyring_hot_words(int kind, uint32_t count, const uint32_t *len, uint32_t &m,
+                       uint32_t &iv) {
+  m = 0;
+  iv = 1;
+  for (uint32_t k = 0; k < count; k++) {
+    const uint32_t L = len[k];
+    if (kind == SQOBFS_SALAMANDER) {
+      const uint32_t tot = L % 128 + SQOBFS_SALAMANDER_SALT_LEN;
+      m = std::max<uint32_t>(m, tot > 128 ? 16u : (tot + 7) / 8);
+      if (L >= 128) iv = 0;
+    } else {
+      m = 8;
+      if (L >= 64) iv = 0;
+    }
+  }
+}
+
+}  // namespace
+
 int sqobfs_keyring_create(sqobfs_ctx *ctx, int kind, uint32_t count, const uint8_t *blob,
                           const uint64_t *off, const uint32_t *len, sqobfs_keyring **out) {
   if (!ctx || !out || count == 0 || !off || !len) return SQ_EINVAL;
@@ -524,10 +562,15 @@ int sqobfs_keyring_create(sqobfs_ctx *ctx, int kind, uint32_t count, const uint8
   kr->ctx = ctx;
   kr->kind = kind;
   kr->count = count;
+  keyring_hot_words(kind, count, len, kr->hot_m, kr->hot_iv);
   uint8_t *d_blob = nullptr;
   uint64_t *d_off = nullptr;
   uint32_t *d_len = nullptr;
-  hipError_t e = hipMallocAsync((void **)&kr->table, sizeof(sq::PskEntry) * count, ctx->stream);
+  // the entries, then their one-line copies (128-byte aligned)
+  const size_t tbytes = align_up(sizeof(sq::PskEntry) * count, 128);
+  hipError_t e = hipMallocAsync((void **)&kr->table, tbytes + sizeof(sq::PskHotLine) * count,
+                                ctx->stream);
+  if (e == hipSuccess) kr->hot = (sq::PskHotLine *)((char *)kr->table + tbytes);
   if (e == hipSuccess) e = hipMalloc(&d_blob, blob_bytes ? blob_bytes : 1);
   if (e == hipSuccess) e = hipMalloc(&d_off, sizeof(uint64_t) * count);
   if (e == hipSuccess) e = hipMalloc(&d_len, sizeof(uint32_t) * count);
@@ -539,7 +582,8 @@ int sqobfs_keyring_create(sqobfs_ctx *ctx, int kind, uint32_t count, const uint8
     e = hipMemcpyAsync(d_len, len, sizeof(uint32_t) * count, hipMemcpyHostToDevice, ctx->stream);
   int st = hip_status(e);
   if (st == SQ_OK)
-    st = sq_launch_psk_prepare(kind, d_blob, d_off, d_len, count, kr->table, ctx->stream);
+    st = sq_launch_psk_prepare(kind, d_blob, d_off, d_len, count, kr->table, kr->hot,
+                               ctx->stream);
   if (st == SQ_OK)
     st = hip_status(hipMemcpyAsync(&kr->host0, kr->table, sizeof(sq::PskEntry),
                                    hipMemcpyDeviceToHost, ctx->stream));

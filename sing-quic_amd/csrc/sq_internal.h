@@ -50,6 +50,22 @@ struct alignas(16) PskEntry {
 };
 static_assert(sizeof(PskEntry) == 352, "PskEntry layout");
 
+// The words one compression of a short-PSK entry needs, in one 128-byte
+// line (the multi-PSK kernels' per-packet gather; sq_kernels.hip load_hot):
+// the first block's message words (BLAKE2b: PSK tail || salt placeholder,
+// zero padded; SHA-256: words 0-7 = the 64-byte block), the final byte
+// counter, the block count and the salt's position.  Used when every entry
+// of the keyring starts from the hash's initial state and its first block
+// fits 14 words (sq_api.hip keyring_hot_words).
+constexpr uint32_t kHotLineWords = 14;
+struct alignas(128) PskHotLine {
+  uint64_t m[kHotLineWords];
+  uint64_t t_last;
+  uint32_t nblocks;
+  uint32_t salt_pos;
+};
+static_assert(sizeof(PskHotLine) == 128, "PskHotLine layout");
+
 // Kernel arguments.  psk0 is the keyring's entry 0 passed by value, so the
 // single-PSK kernels read the hash state from the kernarg segment (scalar
 // loads, wave-uniform) instead of gathering it per lane.
@@ -64,12 +80,15 @@ struct KParams {
   const uint16_t *psk_id;
   const uint32_t *in_cap;
   const PskEntry *psk_table;
+  const PskHotLine *psk_hotl;  // multi-PSK: one-line entries (NULL: gather from psk_table)
   uint8_t *salt_out;        // device salts: [n*S] copy of the generated salts, or NULL
   uint32_t n;
   uint32_t n_psk;
   uint32_t device_salt;     // 1: obfuscate salts from ChaCha20(salt_key, salt_nonce)
   uint32_t ppw;             // packets per wavefront (unit size), 1 .. 62; 0 = default
   uint32_t out_blocks;      // 1: SQOBFS_FLAG_OUT_BLOCKS (outputs own their 16-byte blocks)
+  uint32_t psk_hot_m;       // multi-PSK: words of entry block 0 any entry needs (the rest are 0)
+  uint32_t psk_hot_iv;      // multi-PSK: 1 when no entry has PSK-only blocks (h = initial state)
   uint32_t salt_key[8];
   uint32_t salt_nonce[3];
   PskEntry psk0;
@@ -182,4 +201,4 @@ extern "C" int sq_launch_obfs(int kind, int dir, const sq::KParams *kp,
 extern "C" int sq_launch_psk_prepare(int kind, const uint8_t *blob,
                                      const uint64_t *off, const uint32_t *len,
                                      uint32_t count, sq::PskEntry *out,
-                                     void *stream);
+                                     sq::PskHotLine *hot, void *stream);

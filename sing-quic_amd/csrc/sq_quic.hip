@@ -281,9 +281,12 @@ __device__ __forceinline__ void poly_lengths(Poly &P, uint32_t aad, uint32_t ct)
 
 // ---------------------------------------------------------------- kernels
 
+// Multi-key launches never point K at the kernarg copy: a pointer that may
+// be either kernarg or global memory makes the compiler copy the whole
+// QParams to scratch (576 bytes per lane measured) to form a flat pointer.
 template <bool MULTI>
 __device__ __forceinline__ bool pick_key(const QParams &Q, uint32_t p, const QuicKeyDev *&K) {
-  K = &Q.key0;
+  K = MULTI ? Q.keys : &Q.key0;
   if (!MULTI) return true;
   const uint32_t kid = Q.key_id[p];
   if (kid >= Q.n_keys) return false;
@@ -410,7 +413,7 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
   uint64_t pn_dec = 0;  // open: decoded packet number (0 if rejected)
   uint32_t status = 0, len = 0, pno = 0, first = 0, pn_len = 0, hdr = 0, pl = 0;
   uint64_t src = 0, dst = 0;
-  const QuicKeyDev *K = &Q.key0;
+  const QuicKeyDev *K = MULTI ? Q.keys : &Q.key0;
   uint32_t nonce[3] = {0u, 0u, 0u}, otk[16], rtag[4] = {0u, 0u, 0u, 0u};
   uint32_t hd[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, pnw = 0;  // packet bytes 0..31; seal: pn bytes
   // fused Salamander layer (OB): wire = salt8 || QUIC packet ^ okey

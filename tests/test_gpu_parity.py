@@ -269,6 +269,24 @@ def test_long_and_empty_psks(ctx, kind):
         check(ctx, kind, direction, psks, hb, "long psk")
 
 
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("longest", [0, 1, 8, 24, 55, 56, 63, 64, 119, 120, 121, 127, 128])
+def test_keyring_hot_bounds(ctx, kind, longest):
+    """The multi-PSK kernels load only the entry words the keyring's longest
+    PSK needs, and no chaining value when no PSK has a PSK-only block
+    (sq_api.hip keyring_hot_words): keyrings whose longest PSK sits at each
+    boundary of those bounds (one more message word; BLAKE2b's one/two-block
+    final at tail 120/121; a PSK-only block at 64 / 128 bytes)."""
+    rng = np.random.Generator(np.random.PCG64(1300 + longest + 7 * kind))
+    ks = list(rng.integers(0, longest + 1, 40)) + [longest]
+    psks = [rng.integers(0, 256, int(k), dtype=np.uint8).tobytes() for k in ks]
+    n = 700
+    ids = rng.integers(0, len(psks), n).astype(np.uint16)
+    for direction in DIRS:
+        hb = gh.make_case(rng, kind, direction, rng.integers(0, 600, n), psks, psk_ids=ids)
+        check(ctx, kind, direction, psks, hb, f"hot bounds {longest}")
+
+
 def test_xplus_read_buffer_quirk(ctx):
     """xplus.go:55 XORs up to len(p) - 16, not n - 16."""
     rng = np.random.Generator(np.random.PCG64(12))
