@@ -145,6 +145,13 @@ def build_shard(torch, dev, kind, n, L, n_psk, rank, world, config, layout, firs
             out_slot = torch.full_like(lens, slot_bytes)
         in_off = torch.cumsum(in_slot, 0) - in_slot + lead
         out_off = torch.cumsum(out_slot, 0) - out_slot + lead
+        if layout == "slot2048":
+            # payload position in its slot (dev probe SQ_BENCH_SLOT_PHASE; S =
+            # the engine's geometry: payload behind the salt headroom, so the
+            # payload sits at the same 16-byte phase as in the wire slot)
+            phase = int(os.environ.get("SQ_BENCH_SLOT_PHASE", "0"))
+            assert 0 <= phase and phase % 4 == 0 and int(lens.max().item()) + phase <= slot_bytes
+            in_off = in_off + phase
     else:
         # wire-dense: datagrams back to back (every output byte written);
         # each payload sits behind S bytes of headroom in a wire-sized input
@@ -153,7 +160,8 @@ def build_shard(torch, dev, kind, n, L, n_psk, rank, world, config, layout, firs
         out_off = torch.cumsum(out_slot, 0) - out_slot + lead
         in_slot = out_slot
         in_off = out_off + S
-    in_bytes = int(in_slot.sum().item()) + 2 * lead
+    # (+ 16: the slot phase probe shifts the last slot's gap past the end)
+    in_bytes = int(in_slot.sum().item()) + 2 * lead + 16
     # dev probe of output placement (no effect measured)
     shift = int(os.environ.get("SQ_BENCH_OUT_SHIFT", "0")) if layout != "inplace" else 0
     out_off = out_off + shift
@@ -167,6 +175,9 @@ def build_shard(torch, dev, kind, n, L, n_psk, rank, world, config, layout, firs
     gidx = torch.repeat_interleave(gstart, gap) + (
         torch.arange(int(gap.sum().item()), device=dev)
         - torch.repeat_interleave(torch.cumsum(gap, 0) - gap, gap))
+    # host-side bounds check before the indexed write (an out-of-range index
+    # faults the GPU)
+    assert gidx.numel() == 0 or int(gidx.max().item()) < in_bytes
     data[gidx] = 0
     data[:lead] = 0
     data[int((in_off[-1] + lens[-1]).item()):] = 0

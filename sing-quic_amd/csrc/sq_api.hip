@@ -113,7 +113,6 @@ struct sqobfs_keyring {
   uint32_t count = 0;
   sq::PskEntry *table = nullptr;  // device
   sq::PskEntry host0;             // entry 0, passed by value to the kernels
-  sq::PskHotLine *hot = nullptr;  // device, one line per entry (same allocation as table)
   uint32_t hot_m = 16;            // block-0 message words any entry needs
   uint32_t hot_iv = 0;            // 1: every entry starts from the hash's initial state
 };
@@ -278,9 +277,6 @@ sq::KParams make_params(sqobfs_ctx *ctx, const sqobfs_keyring *kr, const sqobfs_
   kp.psk0 = kr->host0;
   kp.psk_hot_m = kr->hot_m;
   kp.psk_hot_iv = kr->hot_iv;
-  // one-line entries when every PSK is short (no chaining value to load, the
-  // first block's live words fit the line)
-  kp.psk_hotl = kr->hot_iv && kr->hot_m <= sq::kHotLineWords ? kr->hot : nullptr;
   kp.ppw = ctx->unit_packets.load(std::memory_order_relaxed);
   kp.out_blocks = (b->flags & SQOBFS_FLAG_OUT_BLOCKS) ? 1u : 0u;
   if (b->flags & SQOBFS_FLAG_DEVICE_SALT) {
@@ -566,11 +562,7 @@ int sqobfs_keyring_create(sqobfs_ctx *ctx, int kind, uint32_t count, const uint8
   uint8_t *d_blob = nullptr;
   uint64_t *d_off = nullptr;
   uint32_t *d_len = nullptr;
-  // the entries, then their one-line copies (128-byte aligned)
-  const size_t tbytes = align_up(sizeof(sq::PskEntry) * count, 128);
-  hipError_t e = hipMallocAsync((void **)&kr->table, tbytes + sizeof(sq::PskHotLine) * count,
-                                ctx->stream);
-  if (e == hipSuccess) kr->hot = (sq::PskHotLine *)((char *)kr->table + tbytes);
+  hipError_t e = hipMallocAsync((void **)&kr->table, sizeof(sq::PskEntry) * count, ctx->stream);
   if (e == hipSuccess) e = hipMalloc(&d_blob, blob_bytes ? blob_bytes : 1);
   if (e == hipSuccess) e = hipMalloc(&d_off, sizeof(uint64_t) * count);
   if (e == hipSuccess) e = hipMalloc(&d_len, sizeof(uint32_t) * count);
@@ -582,8 +574,7 @@ int sqobfs_keyring_create(sqobfs_ctx *ctx, int kind, uint32_t count, const uint8
     e = hipMemcpyAsync(d_len, len, sizeof(uint32_t) * count, hipMemcpyHostToDevice, ctx->stream);
   int st = hip_status(e);
   if (st == SQ_OK)
-    st = sq_launch_psk_prepare(kind, d_blob, d_off, d_len, count, kr->table, kr->hot,
-                               ctx->stream);
+    st = sq_launch_psk_prepare(kind, d_blob, d_off, d_len, count, kr->table, ctx->stream);
   if (st == SQ_OK)
     st = hip_status(hipMemcpyAsync(&kr->host0, kr->table, sizeof(sq::PskEntry),
                                    hipMemcpyDeviceToHost, ctx->stream));

@@ -50,22 +50,6 @@ struct alignas(16) PskEntry {
 };
 static_assert(sizeof(PskEntry) == 352, "PskEntry layout");
 
-// The words one compression of a short-PSK entry needs, in one 128-byte
-// line (the multi-PSK kernels' per-packet gather; sq_kernels.hip load_hot):
-// the first block's message words (BLAKE2b: PSK tail || salt placeholder,
-// zero padded; SHA-256: words 0-7 = the 64-byte block), the final byte
-// counter, the block count and the salt's position.  Used when every entry
-// of the keyring starts from the hash's initial state and its first block
-// fits 14 words (sq_api.hip keyring_hot_words).
-constexpr uint32_t kHotLineWords = 14;
-struct alignas(128) PskHotLine {
-  uint64_t m[kHotLineWords];
-  uint64_t t_last;
-  uint32_t nblocks;
-  uint32_t salt_pos;
-};
-static_assert(sizeof(PskHotLine) == 128, "PskHotLine layout");
-
 // Kernel arguments.  psk0 is the keyring's entry 0 passed by value, so the
 // single-PSK kernels read the hash state from the kernarg segment (scalar
 // loads, wave-uniform) instead of gathering it per lane.
@@ -80,7 +64,6 @@ struct KParams {
   const uint16_t *psk_id;
   const uint32_t *in_cap;
   const PskEntry *psk_table;
-  const PskHotLine *psk_hotl;  // multi-PSK: one-line entries (NULL: gather from psk_table)
   uint8_t *salt_out;        // device salts: [n*S] copy of the generated salts, or NULL
   uint32_t n;
   uint32_t n_psk;
@@ -201,4 +184,4 @@ extern "C" int sq_launch_obfs(int kind, int dir, const sq::KParams *kp,
 extern "C" int sq_launch_psk_prepare(int kind, const uint8_t *blob,
                                      const uint64_t *off, const uint32_t *len,
                                      uint32_t count, sq::PskEntry *out,
-                                     sq::PskHotLine *hot, void *stream);
+                                     void *stream);

@@ -367,31 +367,11 @@ struct PskHot {
 #define SQ_PSKPRE_M 16
 #endif
 template <int KIND>
-__device__ __forceinline__ void load_hot(const KParams &P, const PskEntry *E, uint32_t pid,
-                                         PskHot &H) {
+__device__ __forceinline__ void load_hot(const KParams &P, const PskEntry *E, PskHot &H) {
   // the keyring's uniform bounds (sq_api.hip keyring_hot_words): words no
   // entry needs are zero and not loaded, the chaining value of a keyring of
   // short PSKs is the initial state
   const uint32_t mw = P.psk_hot_m < SQ_PSKPRE_M ? P.psk_hot_m : SQ_PSKPRE_M;
-  if (P.psk_hotl) {  // short PSKs: everything in the entry's 128-byte line
-    const PskHotLine *Lh = P.psk_hotl + pid;
-    if (KIND == 0) {
-      b2_init256(H.h);
-    } else {
-      uint32_t st[8];
-      s2_init(st);
-#pragma unroll
-      for (int i = 0; i < 8; i++) H.h[i] = i < 4 ? b2_pack(st[2 * i], st[2 * i + 1]) : 0ull;
-    }
-#pragma unroll
-    for (int i = 0; i < 16; i++)
-      H.m[i] = (KIND == 0 || i < 8) && i < (int)kHotLineWords && (uint32_t)i < mw ? Lh->m[i] : 0ull;
-    H.t_first = 0ull;
-    H.t_last = KIND == 0 ? Lh->t_last : 0ull;
-    H.nblocks = Lh->nblocks;
-    H.salt_pos = Lh->salt_pos;
-    return;
-  }
   if (P.psk_hot_iv) {
     if (KIND == 0) {
       b2_init256(H.h);
@@ -1078,7 +1058,7 @@ __global__ __launch_bounds__(WPB * kWave) void obfs_kernel(const KParams P) {
   finalize_desc<KIND, DIR, MULTI>(P, p, valid, d, J, salt, do_hash, E, olen);
   PskHot hot;
   if constexpr (MULTI && SQ_PSKPRE) {
-    load_hot<KIND>(P, E, MULTI && d.pid < P.n_psk ? d.pid : 0u, hot);  // in flight during the plan
+    load_hot<KIND>(P, E, hot);  // in flight during the plan
   }
   SQ_STAMP(1);
   Windows W;
@@ -1127,8 +1107,7 @@ __device__ __forceinline__ uint32_t ld32be(const uint8_t *p) {
 // One thread per PSK: compress the PSK-only leading blocks, lay out the final
 // block template.  Runs once per keyring (connection setup), not per packet.
 __global__ void psk_prepare_kernel(int kind, const uint8_t *blob, const uint64_t *off,
-                                   const uint32_t *len, uint32_t count, PskEntry *out,
-                                   PskHotLine *hot) {
+                                   const uint32_t *len, uint32_t count, PskEntry *out) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= count) return;
   const uint8_t *psk = blob + off[k];
@@ -1185,14 +1164,6 @@ __global__ void psk_prepare_kernel(int kind, const uint8_t *blob, const uint64_t
     E.t_last = 0;
   }
   out[k] = E;
-  if (hot) {  // the one-line copy (read only when the keyring qualifies)
-    PskHotLine Hl;
-    for (uint32_t j = 0; j < kHotLineWords; j++) Hl.m[j] = E.m[j];
-    Hl.t_last = E.t_last;
-    Hl.nblocks = E.nblocks;
-    Hl.salt_pos = E.salt_pos;
-    hot[k] = Hl;
-  }
 }
 
 // Wavefronts per workgroup.  A workgroup's slots are released only when all
@@ -1291,11 +1262,10 @@ extern "C" int sqobfs_debug_timeline(uint64_t *host, uint64_t words) {
 
 extern "C" int sq_launch_psk_prepare(int kind, const uint8_t *blob, const uint64_t *off,
                                      const uint32_t *len, uint32_t count, sq::PskEntry *out,
-                                     sq::PskHotLine *hot, void *stream) {
+                                     void *stream) {
   if (count == 0) return 0;
   const uint32_t threads = 64;
   hipLaunchKernelGGL(sq::psk_prepare_kernel, dim3((count + threads - 1) / threads),
-                     dim3(threads), 0, (hipStream_t)stream, kind, blob, off, len, count, out,
-                     hot);
+                     dim3(threads), 0, (hipStream_t)stream, kind, blob, off, len, count, out);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
