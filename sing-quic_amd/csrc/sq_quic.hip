@@ -48,9 +48,10 @@ constexpr uint32_t kQBlock = SQ_QBLOCK;
 constexpr uint32_t kQWaves = kQBlock / kWave;
 // Packets per wave (owner lanes of phases 1 and 3).  32 with a 1,536-byte
 // cooperative range (MTU-sized packets; longer ones take the owner lane's
-// sequential pass) keeps 3 waves per SIMD within the LDS and halves the
-// idle lanes of the owner phases: seal 1,570 -> 1,406 us against 16 packets
-// and 2,048 B (24: 1,545; 40: 1,677, 2 waves per SIMD).
+// sequential pass) needs 20 KB of LDS per wave (8 waves per CU, 2 per
+// SIMD; the 2,048-byte range needed 25 KB, 6 per CU) and halves the idle
+// lanes of the owner phases: seal 1,570 -> 1,406 us against 16 packets and
+// 2,048 B (24: 1,545; 40: 1,677).
 #ifndef SQ_QPPW
 #define SQ_QPPW 32
 #endif
@@ -63,6 +64,17 @@ constexpr uint32_t kQPpw = SQ_QPPW;
 #endif
 constexpr uint32_t kQCoopMax = SQ_QCOOPMAX;  // payloads up to this size take the cooperative pass
 constexpr uint32_t kQMaxBlk = kQPpw * (kQCoopMax / 64);
+// Pairs (SQ_QPAIR): every packet's flat blocks start at an even index, and
+// the even lane of each pair of lanes folds its neighbour's partial MAC into
+// its own (P_b r^k + P_b+1, k = the chunks of block b+1), so LDS holds one
+// partial per two blocks: 13 KB per wave instead of 20 KB, 12 waves per CU
+// instead of 8.
+#ifndef SQ_QPAIR
+#define SQ_QPAIR 1
+#endif
+static_assert((kQCoopMax / 64) % 2 == 0, "pairs: a packet's padded block count stays in range");
+static_assert(!(SQ_QPAIR && SQ_QPREFETCH), "the prefetching loop is not paired");
+constexpr uint32_t kQParts = SQ_QPAIR ? kQMaxBlk / 2 : kQMaxBlk;
 
 // ---------------------------------------------------------------- Poly1305
 
@@ -294,16 +306,19 @@ __device__ __forceinline__ bool pick_key(const QParams &Q, uint32_t p, const Qui
   return true;
 }
 
-// Per-packet record in LDS for the cooperative payload pass.
+// Per-packet record in LDS for the cooperative payload pass (176 bytes).
 struct alignas(16) QRec {
   uint64_t src, dst;      // payload start in the input / output
   uint32_t pl, start;     // payload bytes; first flat keystream block
-  uint32_t kid, pad0;
-  uint32_t nonce[3], pad1;
-  uint32_t r[5], s[4], pad2[3];
+  uint32_t kid, nblk;     // key index; keystream blocks (64 bytes each)
+  uint32_t nonce[3];
+  uint32_t r[5];          // Poly1305 r (26-bit limbs; the 5 r terms are formed on use)
+  uint32_t r4[5], rl[5];  // pairs: r^4 and r^klast (chunks of the last block)
+  uint32_t pad[2];
   uint32_t ct32[8];       // ciphertext bytes 0..31 (the header-protection sample)
   uint32_t okr[8];        // fused Salamander layer: key rotated to the payload start
 };
+static_assert(sizeof(QRec) == 176, "QRec layout");
 
 // One 64-byte keystream block of one packet (cooperative pass, any lane):
 // XOR up to 64 payload bytes, Horner their <= 4 MAC blocks from h = 0 with
@@ -334,7 +349,7 @@ __device__ __forceinline__ void coop_block(const QuicKeyDev &K, QRec &R, uint32_
   const uint32_t ib = (uint32_t)((R.src + off0) & 15);
   Poly L;
   L.r0 = R.r[0]; L.r1 = R.r[1]; L.r2 = R.r[2]; L.r3 = R.r[3]; L.r4 = R.r[4];
-  L.s1 = R.s[0]; L.s2 = R.s[1]; L.s3 = R.s[2]; L.s4 = R.s[3];
+  L.s1 = L.r1 * 5; L.s2 = L.r2 * 5; L.s3 = L.r3 * 5; L.s4 = L.r4 * 5;
   L.h0 = L.h1 = L.h2 = L.h3 = L.h4 = 0;
   uint32_t o[4][4];
 #pragma unroll
@@ -402,7 +417,7 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
 #endif
 (const QParams Q) {
   __shared__ QRec recs[kQWaves][kQPpw];
-  __shared__ uint32_t parts[kQWaves][kQMaxBlk][5];
+  __shared__ uint32_t parts[kQWaves][kQParts][5];
   const uint32_t lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
   const uint64_t p64 = ((uint64_t)blockIdx.x * kQWaves + wv) * kQPpw + lane;
   const bool owner = lane < kQPpw && p64 < Q.n;
@@ -547,13 +562,16 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
   }
   const bool coop = live && pl <= kQCoopMax;
   const uint32_t nblk = coop ? (pl + 63) / 64 : 0u;
-  uint32_t incl = nblk;
+  // chunks of the last block (1..4) and, for pairs, r^2..r^4
+  const uint32_t klast = nblk ? ((pl - 64 * (nblk - 1)) + 15) / 16 : 1u;
+  const uint32_t nflat = SQ_QPAIR ? (nblk + 1) & ~1u : nblk;
+  uint32_t incl = nflat;
 #pragma unroll
   for (int d = 1; d < kWave; d <<= 1) {
     const uint32_t y = __shfl_up(incl, d, kWave);
     if (lane >= (uint32_t)d) incl += y;
   }
-  const uint32_t start = incl - nblk, T = __shfl(incl, kWave - 1, kWave);
+  const uint32_t start = incl - nflat, T = __shfl(incl, kWave - 1, kWave);
   if (lane < kQPpw) {
     QRec &R = recs[wv][lane];
     R.src = src + hdr;
@@ -561,10 +579,23 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
     R.pl = pl;
     R.start = start;
     R.kid = MULTI && live ? (uint32_t)(K - Q.keys) : 0u;
+    R.nblk = nblk;
 #pragma unroll
     for (int i = 0; i < 3; i++) R.nonce[i] = nonce[i];
     R.r[0] = P.r0; R.r[1] = P.r1; R.r[2] = P.r2; R.r[3] = P.r3; R.r[4] = P.r4;
-    R.s[0] = P.s1; R.s[1] = P.s2; R.s[2] = P.s3; R.s[3] = P.s4;
+    if (SQ_QPAIR && nblk) {
+      // X.h = r^k for k = 2, 3, 4 (X.r = r)
+      Poly X = P;
+      X.h0 = P.r0; X.h1 = P.r1; X.h2 = P.r2; X.h3 = P.r3; X.h4 = P.r4;
+      uint32_t l0 = X.h0, l1 = X.h1, l2 = X.h2, l3 = X.h3, l4 = X.h4;  // r^klast
+#pragma unroll
+      for (uint32_t k = 2; k <= 4; k++) {
+        poly_mul(X);
+        if (klast == k) { l0 = X.h0; l1 = X.h1; l2 = X.h2; l3 = X.h3; l4 = X.h4; }
+      }
+      R.r4[0] = X.h0; R.r4[1] = X.h1; R.r4[2] = X.h2; R.r4[3] = X.h3; R.r4[4] = X.h4;
+      R.rl[0] = l0; R.rl[1] = l1; R.rl[2] = l2; R.rl[3] = l3; R.rl[4] = l4;
+    }
 #pragma unroll
     for (int i = 0; i < 8; i++) R.ct32[i] = 0u;
     if (OB) {
@@ -606,6 +637,39 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
 #pragma unroll
       for (int w = 0; w < 4; w++) blk[i][w] = nblk5[i][w];
   }
+#elif SQ_QPAIR
+  for (uint32_t base = 0; base < T; base += kWave) {
+    const uint32_t f = base + lane;
+    const uint32_t pp = q_locate(start, base, f < T ? f : T - 1);
+    QRec &R = recs[wv][pp];
+    const uint32_t b = f - R.start;
+    uint32_t c5[5] = {0u, 0u, 0u, 0u, 0u};
+    if (f < T && b < R.nblk) {  // (b == nblk: an odd packet's padding block)
+      const QuicKeyDev &KB = MULTI ? Q.keys[R.kid] : Q.key0;
+      uint32_t blk[5][4];
+      coop_load(R, b, blk);
+      coop_block<OPEN, OB>(KB, R, b, blk, c5);
+    }
+    // the odd neighbour's partial (the same packet: pairs start even)
+    uint32_t n5[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++) n5[i] = __shfl_down(c5[i], 1, kWave);
+    if (!(lane & 1) && f < T) {
+      if (b + 1 < R.nblk) {
+        // P_b r^k + P_b+1, k = 4, or klast for the packet's last block
+        const uint32_t *m = b + 2 == R.nblk ? R.rl : R.r4;
+        Poly X;
+        X.r0 = m[0]; X.r1 = m[1]; X.r2 = m[2]; X.r3 = m[3]; X.r4 = m[4];
+        X.s1 = X.r1 * 5; X.s2 = X.r2 * 5; X.s3 = X.r3 * 5; X.s4 = X.r4 * 5;
+        X.h0 = c5[0]; X.h1 = c5[1]; X.h2 = c5[2]; X.h3 = c5[3]; X.h4 = c5[4];
+        poly_mul(X);
+        c5[0] = X.h0 + n5[0]; c5[1] = X.h1 + n5[1]; c5[2] = X.h2 + n5[2];
+        c5[3] = X.h3 + n5[3]; c5[4] = X.h4 + n5[4];
+      }
+#pragma unroll
+      for (int i = 0; i < 5; i++) parts[wv][f >> 1][i] = c5[i];
+    }
+  }
 #else
   for (uint32_t base = 0; base < T; base += kWave) {
     const uint32_t f = base + lane;
@@ -630,7 +694,44 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
     return;
   }
   uint32_t ct32[8];
-  if (coop) {
+  if (coop && SQ_QPAIR) {
+    // pairs: h = h r^c + E_j, c = 8 chunks for a whole pair, r^klast for a
+    // last pair of one block, r^(4 + klast) for one of two
+    const QRec &Rq = recs[wv][lane];
+    Poly R1;
+    R1.r0 = P.r0; R1.r1 = P.r1; R1.r2 = P.r2; R1.r3 = P.r3; R1.r4 = P.r4;
+    R1.s1 = P.s1; R1.s2 = P.s2; R1.s3 = P.s3; R1.s4 = P.s4;
+    Poly X;
+    X.r0 = Rq.r4[0]; X.r1 = Rq.r4[1]; X.r2 = Rq.r4[2]; X.r3 = Rq.r4[3]; X.r4 = Rq.r4[4];
+    X.s1 = X.r1 * 5; X.s2 = X.r2 * 5; X.s3 = X.r3 * 5; X.s4 = X.r4 * 5;
+    Poly Y = X;
+    X.h0 = X.r0; X.h1 = X.r1; X.h2 = X.r2; X.h3 = X.r3; X.h4 = X.r4;
+    poly_mul(X);  // r^8
+    Y.h0 = Rq.rl[0]; Y.h1 = Rq.rl[1]; Y.h2 = Rq.rl[2]; Y.h3 = Rq.rl[3]; Y.h4 = Rq.rl[4];
+    poly_mul(Y);  // r^(4 + klast)
+    const bool one = nblk & 1;  // the last pair holds one block
+    const uint32_t M0 = one ? Rq.rl[0] : Y.h0, M1 = one ? Rq.rl[1] : Y.h1,
+                   M2 = one ? Rq.rl[2] : Y.h2, M3 = one ? Rq.rl[3] : Y.h3,
+                   M4 = one ? Rq.rl[4] : Y.h4;
+    const uint32_t npair = nflat / 2;
+    for (uint32_t j = 0; j < npair; j++) {
+      const bool lastp = j + 1 == npair;
+      P.r0 = lastp ? M0 : X.h0;
+      P.r1 = lastp ? M1 : X.h1;
+      P.r2 = lastp ? M2 : X.h2;
+      P.r3 = lastp ? M3 : X.h3;
+      P.r4 = lastp ? M4 : X.h4;
+      P.s1 = P.r1 * 5; P.s2 = P.r2 * 5; P.s3 = P.r3 * 5; P.s4 = P.r4 * 5;
+      poly_mul(P);
+      const uint32_t *c5 = parts[wv][start / 2 + j];
+      P.h0 += c5[0]; P.h1 += c5[1]; P.h2 += c5[2]; P.h3 += c5[3]; P.h4 += c5[4];
+    }
+    // restore r for the lengths block
+    P.r0 = R1.r0; P.r1 = R1.r1; P.r2 = R1.r2; P.r3 = R1.r3; P.r4 = R1.r4;
+    P.s1 = R1.s1; P.s2 = R1.s2; P.s3 = R1.s3; P.s4 = R1.s4;
+#pragma unroll
+    for (int i = 0; i < 8; i++) ct32[i] = Rq.ct32[i];
+  } else if (coop) {
     // r^1..r^4 as multipliers
     Poly X = P, R1, R2, R3, R4;
     X.h0 = P.r0; X.h1 = P.r1; X.h2 = P.r2; X.h3 = P.r3; X.h4 = P.r4;
@@ -641,7 +742,6 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
     poly_set_r(R3, X);
     poly_mul(X);
     poly_set_r(R4, X);
-    const uint32_t klast = ((pl - 64 * (nblk ? nblk - 1 : 0)) + 15) / 16;  // 1..4 chunks
     // the last block's multiplier r^klast, selected limb by limb
     const uint32_t L0 = klast == 4 ? R4.r0 : klast == 3 ? R3.r0 : klast == 2 ? R2.r0 : R1.r0;
     const uint32_t L1 = klast == 4 ? R4.r1 : klast == 3 ? R3.r1 : klast == 2 ? R2.r1 : R1.r1;
