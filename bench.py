@@ -464,11 +464,14 @@ def inproc_bench(args):
 
 def quic_valu_roofline(suite_name: str, op: str, kernel_us: float):
     """VALU roofline of a QUIC kernel from the committed PMC pass
-    (profiles/r02/quic/quic_pmc_summary.json, scripts/quic_pmc.sh): VALU
+    (profiles/r0N/quic/quic_pmc_summary.json, scripts/quic_pmc.sh): VALU
     wave-instructions per launch (SQ_INSTS_VALU) over this run's kernel time,
     against 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction."""
-    f = os.path.join(REPO, "profiles", "r02", "quic", "quic_pmc_summary.json")
-    if not os.path.exists(f):
+    for rnd in ("r03", "r02"):  # the newest committed pass
+        f = os.path.join(REPO, "profiles", rnd, "quic", "quic_pmc_summary.json")
+        if os.path.exists(f):
+            break
+    else:
         return None
     d = json.load(open(f))
     name = {"chacha20_poly1305": "quic_kernel", "aes_128_gcm": "quic_gcm_kernel"}[suite_name]
@@ -483,7 +486,7 @@ def quic_valu_roofline(suite_name: str, op: str, kernel_us: float):
                     "valu_wave_instr_per_packet": round(valu / (1 << 20), 1),
                     "achieved": round(ach / 1e12, 4), "peak": round(peak / 1e12, 4),
                     "unit": "T wave-instr/s", "frac": round(ach / peak, 4),
-                    "source": "profiles/r02/quic/quic_pmc_summary.json (SQ_INSTS_VALU)"}
+                    "source": os.path.relpath(f, REPO) + " (SQ_INSTS_VALU)"}
     return None
 
 
