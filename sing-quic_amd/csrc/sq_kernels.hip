@@ -94,6 +94,13 @@ namespace sq {
 #ifndef SQ_KLATE
 #define SQ_KLATE 0
 #endif
+// 1: the first stream step's loads are issued right after the plan, before
+// the contents (key and images), so they are in flight during the hash
+// (needs SQ_KLATE: the keystreams are read when the blocks are stored).
+#ifndef SQ_EARLY
+#define SQ_EARLY 0
+#endif
+static_assert(!SQ_EARLY || SQ_KLATE, "SQ_EARLY needs SQ_KLATE");
 // Flat blocks a unit's block map covers (its role bytes live in LDS).
 #ifndef SQ_MAPBLK
 #define SQ_MAPBLK 4096
@@ -122,13 +129,18 @@ namespace sq {
 #define SQ_TIMELINE 0
 #endif
 
+#ifndef SQ_WINSAFE
+#define SQ_WINSAFE 1  // unconditional window loads (fetch_windows)
+#endif
+
 #define SQ_STR2(x) #x
 #define SQ_STR(x) SQ_STR2(x)
 extern "C" const char *sqobfs_build_info(void) {
   return "gfx950 obfs_kernel U=" SQ_STR(SQ_U) " default_ppw=" SQ_STR(SQ_PPW) " NT=" SQ_STR(SQ_NT)
          " minw=" SQ_STR(SQ_MINW) " wpb=2"
          " ablate=" SQ_STR(SQ_ABLATE) " donate=" SQ_STR(SQ_DONATE) " align=" SQ_STR(SQ_ALIGN)
-         " klate=" SQ_STR(SQ_KLATE) " map=" SQ_STR(SQ_MAPBLK);
+         " klate=" SQ_STR(SQ_KLATE) " early=" SQ_STR(SQ_EARLY) " map=" SQ_STR(SQ_MAPBLK)
+         " winsafe=" SQ_STR(SQ_WINSAFE);
 }
 
 // default unit size (KParams.ppw == 0); any 1 .. kMaxUnitPackets works
@@ -520,38 +532,89 @@ __device__ __forceinline__ bool tail_from_window(uint64_t rs, uint64_t re) {
 
 // The input blocks the packet's images need, all loaded together: the head
 // window (payload bytes [0, 32 - pre)) and the tail window (payload bytes of
-// the last partial output block).  Only blocks holding valid bytes are read.
+// the last partial output block).
+//
+// SQ_WINSAFE: every lane issues all six loads unconditionally; a block the
+// packet does not need is read from `safe` (the aligned 16 bytes around its
+// descriptor entry, readable by construction: an aligned block holding one
+// readable byte lies in one page) and masked off at its use (ok bits) in
+// fill_unit.  Conditional loads left phi copies that the compiler resolved
+// with a full `s_waitcnt vmcnt(0)` right after the second head block, so
+// every wave waited for its windows (and, multi-PSK, its keyring entry)
+// before the plan instead of planning while they were in flight.
+// Measured per kernel in one process, three passes on two boxes (DESIGN.md
+// section 5, profiles/r03/ab/winsafe): Salamander obfuscate, one PSK,
+// -1.0 / -2.2 / -3.2 % on configs[1] and -0.5 / -0.6 / -0.9 % ragged; XPlus
+// deobfuscate -0.8 / -1.1 %; Salamander deobfuscate +0.3 / +1.0 / +1.2 %;
+// the multi-PSK obfuscate +5.7 %.  SQ_WINSAFE=1: the two kernels that gain;
+// 2: every kernel; 0: none.
+#ifndef SQ_WINSAFE
+#define SQ_WINSAFE 1
+#endif
+template <int KIND, int DIR, bool MULTI>
+constexpr bool kWinSafe =
+    SQ_WINSAFE == 2 || (SQ_WINSAFE == 1 && !MULTI && (KIND == 0) == (DIR == 0));
 struct Windows {
   u32x4 h0, h1, h2, t0, t1;
-  u32x4 s0;  // deobfuscate: the block before h0 when it holds salt bytes
+  u32x4 s0;     // deobfuscate: the block before h0 when it holds salt bytes
+  uint32_t ok;  // bits: h0 1, h1 2, h2 4, t0 8, t1 16, s0 32 (SQ_WINSAFE)
 };
+constexpr uint32_t kWinH0 = 1, kWinH1 = 2, kWinH2 = 4, kWinT0 = 8, kWinT1 = 16, kWinS0 = 32;
 
 // Deobfuscate with a key (wire_salt): the salt is the S wire bytes before
 // the payload, [src_pay - S, src_pay); it lies in h0 and, when src_pay % 16 <
 // S, the block before it, loaded here with the head window.
-template <int DIR, uint32_t S>
-__device__ __forceinline__ void fetch_windows(const PacketJob &J, bool wire_salt, Windows &W) {
+template <int DIR, uint32_t S, bool WS>
+__device__ __forceinline__ void fetch_windows(const PacketJob &J, bool wire_salt, uint64_t safe,
+                                              Windows &W) {
   const u32x4 z = {0u, 0u, 0u, 0u};
   W.h0 = W.h1 = W.h2 = W.t0 = W.t1 = W.s0 = z;
+  W.ok = 0u;
   if (SQ_ABLATE & 8) return;
   uint64_t rs, re;
   bool ne;
   out_range(J, rs, re, ne);
-  if (!ne) return;
-  const uint64_t hw = J.len < 32 - J.pre ? J.len : 32 - J.pre;
-  if (hw) {
-    const uint64_t B = J.src_pay & ~15ull, e = J.src_pay + hw;
-    if (SQ_SALTWIN && DIR == 1 && wire_salt && (J.src_pay & 15) < S) W.s0 = gld<u32x4>(B - 16);
-    W.h0 = gld<u32x4>(B);
-    if (e > B + 16) W.h1 = gld<u32x4>(B + 16);
-    if (e > B + 32) W.h2 = gld<u32x4>(B + 32);
+  const uint64_t hw = !ne ? 0ull : (J.len < 32 - J.pre ? J.len : 32 - J.pre);
+  const uint64_t B = J.src_pay & ~15ull, e = J.src_pay + hw;
+  const bool c_h0 = hw != 0, c_h1 = c_h0 && e > B + 16, c_h2 = c_h0 && e > B + 32;
+  const bool c_s0 = SQ_SALTWIN && DIR == 1 && c_h0 && wire_salt && (J.src_pay & 15) < S;
+  const bool c_t0 = ne && tail_from_window(rs, re);
+  const uint64_t ta = J.src_pay + ((re & ~15ull) - J.dst_pay), te = J.src_pay + J.len;
+  const uint64_t TB = ta & ~15ull;
+  const bool c_t1 = c_t0 && te > TB + 16;
+  if (WS) {
+    const uint64_t a_s0 = c_s0 ? B - 16 : safe, a_h0 = c_h0 ? B : safe,
+                   a_h1 = c_h1 ? B + 16 : safe, a_h2 = c_h2 ? B + 32 : safe,
+                   a_t0 = c_t0 ? TB : safe, a_t1 = c_t1 ? TB + 16 : safe;
+    // every address before the first load: otherwise the scheduler issues a
+    // load and then computes another address into that load's destination
+    // registers, which costs a wait for the load
+    asm volatile("" ::"v"(a_s0), "v"(a_h0), "v"(a_h1), "v"(a_h2), "v"(a_t0), "v"(a_t1)
+                 : "memory");
+    W.s0 = gld<u32x4>(a_s0);
+    W.h0 = gld<u32x4>(a_h0);
+    W.h1 = gld<u32x4>(a_h1);
+    W.h2 = gld<u32x4>(a_h2);
+    W.t0 = gld<u32x4>(a_t0);
+    W.t1 = gld<u32x4>(a_t1);
+    W.ok = (c_h0 ? kWinH0 : 0u) | (c_h1 ? kWinH1 : 0u) | (c_h2 ? kWinH2 : 0u) |
+           (c_t0 ? kWinT0 : 0u) | (c_t1 ? kWinT1 : 0u) | (c_s0 ? kWinS0 : 0u);
+  } else {
+    if (c_s0) W.s0 = gld<u32x4>(B - 16);
+    if (c_h0) W.h0 = gld<u32x4>(B);
+    if (c_h1) W.h1 = gld<u32x4>(B + 16);
+    if (c_h2) W.h2 = gld<u32x4>(B + 32);
+    if (c_t0) W.t0 = gld<u32x4>(TB);
+    if (c_t1) W.t1 = gld<u32x4>(TB + 16);
+    W.ok = ~0u;
   }
-  if (tail_from_window(rs, re)) {
-    const uint64_t ta = J.src_pay + ((re & ~15ull) - J.dst_pay), te = J.src_pay + J.len;
-    const uint64_t B = ta & ~15ull;
-    W.t0 = gld<u32x4>(B);
-    if (te > B + 16) W.t1 = gld<u32x4>(B + 16);
-  }
+}
+
+// A window block, zero unless the packet needed it (applied where the
+// images are built, after the plan).
+__device__ __forceinline__ u32x4 win_blk(const Windows &W, const u32x4 &v, uint32_t bit) {
+  const u32x4 z = {0u, 0u, 0u, 0u};
+  return (W.ok & bit) ? v : z;
 }
 
 // LDS record of a packet with blocks in the flat space (96 B), stored at the
@@ -768,9 +831,20 @@ __device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
   constexpr uint32_t PW = DIR == 0 ? S / 4 : 0;  // salt words in front of the payload
   uint32_t key[8];
   uint32_t sl[4] = {salt[0], salt[1], salt[2], salt[3]};
+  // every window register stays allocated until here: a component no image
+  // uses would otherwise be handed to the plan while its load is in flight,
+  // and overwriting it waits for the load (SQ_WINSAFE)
+  constexpr bool WS = kWinSafe<KIND, DIR, MULTI>;
+  if (WS && DIR == 1)
+    asm volatile("" ::"v"(W.h0), "v"(W.h1), "v"(W.h2), "v"(W.t0), "v"(W.t1), "v"(W.s0));
+  else if (WS)  // (obfuscate loads no salt block)
+    asm volatile("" ::"v"(W.h0), "v"(W.h1), "v"(W.h2), "v"(W.t0), "v"(W.t1));
+  const u32x4 wh0 = win_blk(W, W.h0, kWinH0), wh1 = win_blk(W, W.h1, kWinH1),
+              wh2 = win_blk(W, W.h2, kWinH2);
   if (SQ_SALTWIN && DIR == 1) {  // the wire salt, from the head window
-    const uint32_t w[12] = {W.s0.x, W.s0.y, W.s0.z, W.s0.w, W.h0.x, W.h0.y,
-                            W.h0.z, W.h0.w, W.h1.x, W.h1.y, W.h1.z, W.h1.w};
+    const u32x4 ws0 = win_blk(W, W.s0, kWinS0);
+    const uint32_t w[12] = {ws0.x, ws0.y, ws0.z, ws0.w, wh0.x, wh0.y,
+                            wh0.z, wh0.w, wh1.x, wh1.y, wh1.z, wh1.w};
     win16(w, (uint32_t)(J.src_pay & 15) + 16 - S, sl);
   }
   // single PSK: the kernarg copy (scalar loads); several: the device table
@@ -781,10 +855,10 @@ __device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
   uint32_t hi[8];
   {
     const uint32_t o = (uint32_t)(J.src_pay & 15);
-    const uint32_t w0[12] = {0u, 0u, 0u, 0u, W.h0.x, W.h0.y, W.h0.z, W.h0.w,
-                             W.h1.x, W.h1.y, W.h1.z, W.h1.w};
-    const uint32_t w1[12] = {W.h0.x, W.h0.y, W.h0.z, W.h0.w, W.h1.x, W.h1.y,
-                             W.h1.z, W.h1.w, W.h2.x, W.h2.y, W.h2.z, W.h2.w};
+    const uint32_t w0[12] = {0u, 0u, 0u, 0u, wh0.x, wh0.y, wh0.z, wh0.w,
+                             wh1.x, wh1.y, wh1.z, wh1.w};
+    const uint32_t w1[12] = {wh0.x, wh0.y, wh0.z, wh0.w, wh1.x, wh1.y,
+                             wh1.z, wh1.w, wh2.x, wh2.y, wh2.z, wh2.w};
     uint32_t pa[4], pb[4];
     win16(w0, o + 16, pa);
     win16(w1, o + 16, pb);
@@ -807,8 +881,9 @@ __device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
   uint32_t ti[4];
   if (tail_from_window(rs, re)) {
     const uint64_t ta = J.src_pay + (BL - J.dst_pay);
-    const uint32_t w[12] = {0u, 0u, 0u, 0u, W.t0.x, W.t0.y, W.t0.z, W.t0.w,
-                            W.t1.x, W.t1.y, W.t1.z, W.t1.w};
+    const u32x4 wt0 = win_blk(W, W.t0, kWinT0), wt1 = win_blk(W, W.t1, kWinT1);
+    const uint32_t w[12] = {0u, 0u, 0u, 0u, wt0.x, wt0.y, wt0.z, wt0.w,
+                            wt1.x, wt1.y, wt1.z, wt1.w};
     uint32_t ks[4];
     win16(w, (uint32_t)(ta & 15) + 16, ti);
     keywin(key, (uint32_t)(BL - J.dst_pay) & 31u, ks);
@@ -1062,7 +1137,8 @@ __global__ __launch_bounds__(WPB * kWave) void obfs_kernel(const KParams P) {
   }
   SQ_STAMP(1);
   Windows W;
-  fetch_windows<DIR, KIND == 0 ? kSalamanderSalt : kXPlusSalt>(J, do_hash, W);
+  fetch_windows<DIR, KIND == 0 ? kSalamanderSalt : kXPlusSalt, kWinSafe<KIND, DIR, MULTI>>(
+      J, do_hash, (uint64_t)(P.in_off + p) & ~15ull, W);
   if (owner) P.out_len[p] = olen;
   // 3a. plan
   Geo G;
@@ -1070,14 +1146,15 @@ __global__ __launch_bounds__(WPB * kWave) void obfs_kernel(const KParams P) {
   const bool ob = P.out_blocks != 0;
   const UnitStream S = plan_unit(J, owner, lane, ppw, first != 0, ob, L, G);
   SQ_STAMP(2);
+  Step<U> cur;
+  if (SQ_EARLY && S.fast && S.map) stream_issue<U, true>(L, S.B, S.cst, S.T, lane, 0, cur);
   const uint32_t pid = MULTI && d.pid < P.n_psk ? d.pid : 0u;
   // 2 + 3b. key and block contents
   fill_unit<KIND, DIR, MULTI>(P, J, salt, do_hash, pid, hot, W, owner, lane, ob, G, L);
   SQ_STAMP(3);
   // 4. the stream
-  Step<U> cur;
   if (S.fast && S.map) {
-    stream_issue<U, true>(L, S.B, S.cst, S.T, lane, 0, cur);
+    if (!SQ_EARLY) stream_issue<U, true>(L, S.B, S.cst, S.T, lane, 0, cur);
     stream_loop<U, true>(L, S.B, S.cst, S.T, lane, cur);
   } else if (S.fast) {
     stream_issue<U, false>(L, S.B, S.cst, S.T, lane, 0, cur);
