@@ -662,7 +662,7 @@ def main():
             "unit_packets": ctx.unit_packets,
             "unit_rule": ("--unit-packets" if args.unit_packets else
                           "sqobfs_unit_packets_for(payload bytes, n): ~21.7 KB per wavefront "
-                          "(33 KB with a multi-PSK keyring; at least 2,048 wavefronts)"),
+                          "(31.5 KB with a multi-PSK keyring; at least 2,048 wavefronts)"),
             "parallelism": f"shard{world} (independent packets, no collective)",
         },
         "roofline": {

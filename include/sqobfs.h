@@ -186,7 +186,7 @@ int sqobfs_set_unit_packets(sqobfs_ctx *ctx, uint32_t packets);
 /* the unit size device launches will use (the default when 0 was set) */
 uint32_t sqobfs_unit_packets(const sqobfs_ctx *ctx);
 /* The unit size for a batch of n packets holding `bytes` payload (or
- * datagram) bytes in total: about 21.7 KB per wavefront, 33 KB when packets
+ * datagram) bytes in total: about 21.7 KB per wavefront, 31.5 KB when packets
  * select keyring entries (psk_id != NULL), at least 2,048 wavefronts for
  * small batches, clamped to 1 .. 62. */
 uint32_t sqobfs_unit_packets_for(uint64_t bytes, uint32_t n, int multi_psk);

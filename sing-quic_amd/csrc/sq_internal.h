@@ -19,9 +19,11 @@ constexpr uint32_t kMaxUnitPackets = 62;
 // Sized by bytes when the batch's lengths are known (sqobfs_unit_packets_for):
 // about this many payload bytes per wavefront (~21.7 KB
 // per wave streams best; per-packet keyring gathers want longer units).
-// (multi-PSK: 24 packets of 1,350 B; in-process sweeps, profiles/r03/ab:
-// obfuscate 0.72 at 24 against 0.70 at 26 on two boxes)
-constexpr uint64_t kUnitBytes = 21700, kUnitBytesMultiPsk = 33000;
+// (multi-PSK: 23 packets of 1,350 B.  In-process sweeps on three boxes,
+// profiles/r03/ab/unit_sweep_256psk_*: 23 within 1.2 % of each box's best
+// in both directions; 24 -- ~32 KB, consecutive waves' spans close to a
+// power of two apart -- the slowest point on two of the three boxes.)
+constexpr uint64_t kUnitBytes = 21700, kUnitBytesMultiPsk = 31500;
 // ... but at least this many wavefronts per launch when the batch is small
 // (latency: a socket batch of 256 datagrams runs as 256 one-packet waves)
 constexpr uint32_t kMinUnits = 2048;

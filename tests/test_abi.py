@@ -101,14 +101,14 @@ def test_shard_cuts_balance_bytes():
 
 def test_unit_packets_for_sizes_units_by_bytes():
     """sqobfs_unit_packets_for (host logic, no GPU): ~21.7 KB of payload per
-    wavefront, 33 KB with a multi-PSK keyring, clamped to 1..62; the BASELINE
+    wavefront, 31.5 KB with a multi-PSK keyring, clamped to 1..62; the BASELINE
     configs get the unit sizes the in-process sweeps measured best
     (DESIGN.md section 5)."""
     f = sqobfs.unit_packets_for
     assert f(1350 << 20, 1 << 20) == 16          # configs[1]
     assert f(1200 << 20, 1 << 20) == 18          # configs[2]
     assert f(758 * (4 << 20), 4 << 20) == 28     # configs[3] (mean of U[64, 1452])
-    assert f(1350 * (16 << 20), 16 << 20, True) == 24  # configs[4]
+    assert f(1350 * (16 << 20), 16 << 20, True) == 23  # configs[4]
     assert f(64 * 100_000, 100_000) == 49 and f(0, 1 << 20) == 62
     assert f(70_000 * 8, 8) == 1
     for mean in range(1, 100_000, 997):
