@@ -78,11 +78,16 @@ def parse():
                     help="dense: wire-dense outputs, wire-sized input slots (default); "
                          "slot16: every packet in its own 16-byte-aligned slot (inputs and "
                          "outputs), launched with SQOBFS_FLAG_OUT_BLOCKS; slot2048: fixed "
-                         "2048-byte slots (the Go Slots / UDP endpoint geometry), same flag; "
+                         "2048-byte slots on 128-byte lines (the Go Slots geometry), launched "
+                         "with SQOBFS_FLAG_OUT_LINES (--slot-flag); "
                          "inplace: obfuscate in the input buffer (headroom layout, "
                          "vectorised WriteTo semantics)")
     ap.add_argument("--slot-bytes", type=int, default=2048,
                     help="slot stride of --layout slot2048 (a multiple of 16)")
+    ap.add_argument("--slot-flag", default="lines", choices=["lines", "blocks"],
+                    help="--layout slot2048: SQOBFS_FLAG_OUT_LINES (every output written "
+                         "through to the end of its last 128-byte line; default) or "
+                         "SQOBFS_FLAG_OUT_BLOCKS only (whole 16-byte blocks)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL) for the timing barrier/max; gloo lets several "
                          "ranks share one GPU in tests")
@@ -132,8 +137,9 @@ def build_shard(torch, dev, kind, n, L, n_psk, rank, world, config, layout, firs
     else:
         lens = torch.full((n,), L, device=dev, dtype=torch.int64)
     # buffers start with 64 spare bytes (dev probe SQ_BENCH_LEAD: slot phase
-    # within the 128-byte line)
-    lead = int(os.environ.get("SQ_BENCH_LEAD", "64"))
+    # within the 128-byte line); 2048-byte slots start
+    # on 128-byte lines, as the Go Slots' page-aligned memory
+    lead = int(os.environ.get("SQ_BENCH_LEAD", "128" if layout == "slot2048" else "64"))
     if layout in ("slot16", "slot2048"):
         # every packet in its own 16-byte-aligned slot (16 B-
         # aligned input offsets), or in fixed 2048-byte slots
@@ -536,8 +542,12 @@ def main():
         raise SystemExit("--layout inplace is for obfuscate")
     if args.device_salt and (direction != sqobfs.OBFUSCATE or sh["inplace"]):
         raise SystemExit("--device-salt is for obfuscate, not in place")
-    # slotted layouts: every output owns its 16-byte blocks
+    # slotted layouts: every output owns its 16-byte blocks; 2048-byte slots
+    # also the rest of its last 128-byte line (slot padding)
     ob = sqobfs.FLAG_OUT_BLOCKS if sh["slotted"] else 0
+    if args.layout == "slot2048" and args.slot_flag == "lines":
+        assert args.slot_bytes % 128 == 0 and S + (L or 1452) + 128 <= args.slot_bytes
+        ob = sqobfs.FLAG_OUT_LINES
     if direction == sqobfs.OBFUSCATE and args.device_salt:
         ctx.salt_key(SALT_KEY, 0)
         b = sqobfs.make_batch(n, sh["data"], sh["in_off"], sh["lens"], sh["out"], sh["out_off"],
@@ -659,6 +669,8 @@ def main():
             "payload_bytes_per_gpu": sh["payload_bytes"],
             "layout": args.layout + (f" ({args.slot_bytes}-byte slots)"
                                      if args.layout == "slot2048" else ""),
+            "batch_flags": {0: "none", sqobfs.FLAG_OUT_BLOCKS: "SQOBFS_FLAG_OUT_BLOCKS",
+                            sqobfs.FLAG_OUT_LINES: "SQOBFS_FLAG_OUT_LINES"}[ob],
             "unit_packets": ctx.unit_packets,
             "unit_rule": ("--unit-packets" if args.unit_packets else
                           "sqobfs_unit_packets_for(payload bytes, n): ~21.7 KB per wavefront "

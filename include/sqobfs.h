@@ -114,6 +114,19 @@ extern "C" {
  * Every output byte is as without the flag. */
 #define SQOBFS_FLAG_OUT_BLOCKS 4u
 
+/* batch flag: outputs own their 128-byte lines to the end (implies
+ * SQOBFS_FLAG_OUT_BLOCKS).  The caller also promises that the bytes from the
+ * end of packet i's output to the next 128-byte boundary of `out` hold no
+ * input or output bytes of any packet of the batch (slots whose stride is a
+ * multiple of 128 and whose bases are 128-byte aligned: the Go Slots and the
+ * packet conn engine's 2,048-byte slots).  The launch then writes every output
+ * through to the end of its last 128-byte line: a line written in part is
+ * merged by the memory controller with what HBM holds (a read-modify-write),
+ * which costs a slotted batch ~15 % of the HBM rate.
+ * Those padding bytes are left with unspecified values (copies of the
+ * packet's last output block); every output byte is as without the flag. */
+#define SQOBFS_FLAG_OUT_LINES 8u
+
 /* out_len value written for a packet whose psk_id is out of range */
 #define SQOBFS_BAD_PSK 0xFFFFFFFFu
 

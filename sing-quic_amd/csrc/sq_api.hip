@@ -242,7 +242,7 @@ hipStream_t pick_stream(sqobfs_ctx *ctx, void *stream) {
 int check_batch_shape(const sqobfs_batch *b, int dir) {
   if (!b) return SQ_EINVAL;
   if (b->flags & ~(uint32_t)(SQOBFS_FLAG_OUT_UNINIT | SQOBFS_FLAG_DEVICE_SALT |
-                             SQOBFS_FLAG_OUT_BLOCKS))
+                             SQOBFS_FLAG_OUT_BLOCKS | SQOBFS_FLAG_OUT_LINES))
     return SQ_EINVAL;
   const bool dev_salt = b->flags & SQOBFS_FLAG_DEVICE_SALT;
   if (dev_salt && dir != SQOBFS_OBFUSCATE) return SQ_EINVAL;
@@ -278,7 +278,8 @@ sq::KParams make_params(sqobfs_ctx *ctx, const sqobfs_keyring *kr, const sqobfs_
   kp.psk_hot_m = kr->hot_m;
   kp.psk_hot_iv = kr->hot_iv;
   kp.ppw = ctx->unit_packets.load(std::memory_order_relaxed);
-  kp.out_blocks = (b->flags & SQOBFS_FLAG_OUT_BLOCKS) ? 1u : 0u;
+  kp.out_lines = (b->flags & SQOBFS_FLAG_OUT_LINES) ? 1u : 0u;
+  kp.out_blocks = (b->flags & SQOBFS_FLAG_OUT_BLOCKS) || kp.out_lines ? 1u : 0u;
   if (b->flags & SQOBFS_FLAG_DEVICE_SALT) {
     const uint64_t seq = ctx->salt_seq.fetch_add(1);
     kp.device_salt = 1;
@@ -1063,13 +1064,16 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
   // for what is pageable)
   // each staged byte keeps its address modulo 16 (the kernel's 16-byte
   // blocks are the caller's: aligned outputs stay the fast case, and
-  // SQOBFS_FLAG_OUT_BLOCKS's promise holds on the device copy)
+  // SQOBFS_FLAG_OUT_BLOCKS's promise holds on the device copy); with
+  // SQOBFS_FLAG_OUT_LINES output bytes keep their address modulo 128, and the
+  // last output line's padding, which the kernel writes, is staged too
   const size_t A = 256;
+  const bool lines = hb->flags & SQOBFS_FLAG_OUT_LINES;
   size_t o = 0;
   const size_t o_in = o + (((uintptr_t)hb->in + in_lo) & 15);
   o = align_up(o_in + (in_hi - in_lo), A);
-  const size_t o_out = o + (((uintptr_t)hb->out + out_lo) & 15);
-  o = align_up(o_out + (out_hi - out_lo), A);
+  const size_t o_out = o + (((uintptr_t)hb->out + out_lo) & (lines ? 127 : 15));
+  o = align_up(o_out + (out_hi - out_lo) + (lines ? 128 : 0), A);
   const size_t o_inoff = o;    o = align_up(o + 8ull * n, A);
   const size_t o_inlen = o;    o = align_up(o + 4ull * n, A);
   const size_t o_outoff = o;   o = align_up(o + 8ull * n, A);

@@ -621,7 +621,8 @@ __device__ __forceinline__ u32x4 win_blk(const Windows &W, const u32x4 &v, uint3
 // packet's rank among such packets.  Flat block c of the unit, owned by this
 // packet, is at input ssub + 16 c and output dsub + 16 c (buffer offsets
 // soff + 16 c, doff + 16 c); its keystream is tab[c & 1], except the special
-// blocks c == sidx (first, value tab[2]) and c == eidx (last, value tab[3]),
+// blocks c == sidx (first, value tab[2]) and c >= eidx (last, and out_lines
+// pad blocks: value tab[3]),
 // whose loads are range-checked away.
 struct alignas(16) ChunkRec {
   uint64_t ssub, dsub;
@@ -668,6 +669,7 @@ static_assert(kOffPhase >= kMaxSpan && kOffPhase + 16ull * kWave <= 0xFFFFFFF0ul
 struct Geo {
   uint64_t rs, re, B0;  // output range, first owned block
   uint32_t nblk;        // owned blocks [B0, B0 + 16 nblk)
+  uint32_t npad;        // out_lines: pad blocks after them (to the 128-byte line's end)
   uint32_t rank;        // record index (packets with flat blocks only)
   uint32_t start;       // flat index of the first owned block
   bool flat;            // has blocks in the flat space
@@ -690,8 +692,12 @@ struct Geo {
 // a second block (obfuscate with rs % 16 + S > 16), which keeps the
 // byte-exact head.  Slotted layouts (outputs at 16-byte-aligned slot starts,
 // or decoded in place behind the salt) never need it.
+// With out_lines (SQOBFS_FLAG_OUT_LINES, implies out_blocks) the owner also
+// writes the blocks from its last block to the end of that 128-byte line
+// (pad blocks: not loaded, value the last block's, like the special last
+// block), so no line is written in part.
 __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, uint32_t lane,
-                                                uint32_t ppw, bool has_prev, bool ob,
+                                                uint32_t ppw, bool has_prev, bool ob, bool ol,
                                                 WaveLds &L, Geo &G) {
   out_range(J, G.rs, G.re, G.ne);
   const uint64_t rs = G.rs, re = G.re;
@@ -736,9 +742,13 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
   // last block whole: the next datagram starts at re and fills the block
   // (or, with out_blocks, the bytes past re are scratch)
   G.lfull = G.hl && (ob || ((fl_n & 1) && rs_n == re && re_n >= E && !(cross_n && (fl_n & 2))));
+  // out_lines: pad blocks [E, re rounded up to 128) after the owned ones
+  const uint32_t npad =
+      ol && owner && nblk ? (uint32_t)((((re + 127) & ~127ull) - E) >> 4) : 0u;
+  G.npad = npad;
 
   // the flat block space: this packet's blocks [B0, B0 + 16 F)
-  const uint32_t F = (G.hl && !G.lfull) ? nblk - 1 : nblk;
+  const uint32_t F = ((G.hl && !G.lfull) ? nblk - 1 : nblk) + npad;
   uint32_t incl = F;
 #pragma unroll
   for (int d = 1; d < kWave; d <<= 1) {
@@ -796,7 +806,9 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
     R.soff = (uint32_t)(sabs - sb) - 16u * start;
     R.doff = (uint32_t)(B0 - d_lo) - 16u * start;
     R.sidx = G.hf ? start : kNoIdx;
-    R.eidx = G.lfull ? start + nblk - 1 : kNoIdx;
+    // blocks c >= eidx take tab[3]: the special last block and the pad blocks
+    const uint32_t eidx = G.lfull ? start + nblk - 1 : (npad ? start + nblk : kNoIdx);
+    R.eidx = eidx;
     L.cst[G.rank] = start;
     if (U.map) {
       // the role bytes of this packet's flat blocks [start, start + F)
@@ -807,7 +819,7 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
       for (; c + 4 <= e; c += 4) *reinterpret_cast<uint32_t *>(rb + c) = rk * 0x01010101u;
       for (; c < e; c++) rb[c] = (uint8_t)rk;
       if (G.hf) rb[start] = (uint8_t)(rk | kRoleFirst);
-      if (G.lfull) rb[e - 1] = (uint8_t)(rk | kRoleLast);
+      for (c = eidx; c < e; c++) rb[c] = (uint8_t)(rk | kRoleLast);
     }
   }
   // records visible to the whole wave (same-wave LDS ops are ordered; this
@@ -1026,7 +1038,7 @@ __device__ __forceinline__ void stream_issue(const WaveLds &L, const WaveBufs &B
       idx[u] = (rl[u] & kRoleFirst) ? 2u : ((rl[u] & kRoleLast) ? 3u : (c & 1u));
     } else {
       const uint64_t se = *reinterpret_cast<const uint64_t *>(&R.sidx);
-      idx[u] = c == (uint32_t)se ? 2u : (c == (uint32_t)(se >> 32) ? 3u : (c & 1u));
+      idx[u] = c == (uint32_t)se ? 2u : (c >= (uint32_t)(se >> 32) ? 3u : (c & 1u));
     }
 #if SQ_KLATE
     S.ka[u] = (uint32_t)(reinterpret_cast<const char *>(&R.tab[idx[u]]) -
@@ -1093,7 +1105,7 @@ __device__ __noinline__ void stream_generic(const WaveLds &L, uint32_t cst, uint
     u32x4 k = R.tab[c & 1];
     if (c == R.sidx) {
       k = R.tab[2];
-    } else if (c == R.eidx) {
+    } else if (c >= R.eidx) {  // the special last block or a pad block
       k = R.tab[3];
     } else {
       const uint64_t sa = R.ssub + 16ull * c;
@@ -1144,7 +1156,7 @@ __global__ __launch_bounds__(WPB * kWave) void obfs_kernel(const KParams P) {
   Geo G;
   WaveLds &L = lds[wv];
   const bool ob = P.out_blocks != 0;
-  const UnitStream S = plan_unit(J, owner, lane, ppw, first != 0, ob, L, G);
+  const UnitStream S = plan_unit(J, owner, lane, ppw, first != 0, ob, P.out_lines != 0, L, G);
   SQ_STAMP(2);
   Step<U> cur;
   if (SQ_EARLY && S.fast && S.map) stream_issue<U, true>(L, S.B, S.cst, S.T, lane, 0, cur);

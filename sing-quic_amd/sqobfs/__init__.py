@@ -34,6 +34,7 @@ BAD_PSK = 0xFFFFFFFF
 FLAG_OUT_UNINIT = 1  # run_host: bytes between output regions need not be kept
 FLAG_DEVICE_SALT = 2  # obfuscate: salts from the GPU's ChaCha20 generator
 FLAG_OUT_BLOCKS = 4  # outputs own their 16-byte blocks (slot padding is scratch)
+FLAG_OUT_LINES = 8  # ... and their last 128-byte line to its end (no line written in part)
 
 
 class SqError(RuntimeError):

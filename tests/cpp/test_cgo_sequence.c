@@ -11,7 +11,8 @@
  *                   out_off, in_len, out_len, in_cap, salt; offsets filled
  *   WriteTo x k     payload copied into In(i), SetLen
  *   Run             Slots.Run(Obfuscate, n, deviceSalt): b->n, flags =
- *                   OUT_UNINIT | OUT_BLOCKS | DEVICE_SALT, in_cap = NULL ->
+ *                   OUT_UNINIT | OUT_LINES (128-byte-multiple slots) or
+ *                   OUT_BLOCKS (16-byte multiples) | DEVICE_SALT, in_cap = NULL ->
  *                   sqobfs_run_host
  *   reader          datagrams copied into In(i) of another Slots, SetLen ->
  *                   Slots.Run(Deobfuscate) -> Out(i)[:out_len[i]]
@@ -99,8 +100,12 @@ static uint8_t *out_slot(Slots *s, int i) { return s->data + (size_t)(s->cap + i
 static int run(Slots *s, const sqobfs_keyring *kr, int dir, int n, int device_salt) {
   s->b->n = (uint32_t)n;
   /* Slots.Run: output slots are read only up to out_len (OUT_UNINIT), and
-   * 16-byte-multiple slots own their blocks (OUT_BLOCKS) */
-  s->b->flags = SQOBFS_FLAG_OUT_UNINIT | (s->slot % 16 == 0 ? SQOBFS_FLAG_OUT_BLOCKS : 0u) |
+   * 128-byte-multiple slots own their last lines (OUT_LINES), 16-byte
+   * multiples their blocks (OUT_BLOCKS) */
+  s->b->flags = SQOBFS_FLAG_OUT_UNINIT |
+                (s->slot % 128 == 0   ? SQOBFS_FLAG_OUT_LINES
+                 : s->slot % 16 == 0 ? SQOBFS_FLAG_OUT_BLOCKS
+                                     : 0u) |
                 ((dir == SQOBFS_OBFUSCATE && device_salt) ? SQOBFS_FLAG_DEVICE_SALT : 0u);
   s->b->in_cap = NULL;
   return sqobfs_run_host(s->ctx, kr, dir, s->b);

@@ -121,3 +121,83 @@ def test_out_blocks_run_host(ctx, kind, direction, pinned):
     finally:
         for p in keep:
             p.free()
+
+
+def make_lines(rng, kind, direction, multi, lead, n=3000):
+    """Fixed 2048-byte slots (the Go Slots / the packet conn engine), outputs
+    short enough that the padding to the next 128-byte line stays in the
+    slot wherever the buffer lies."""
+    S = sqobfs.SALT_LEN[kind]
+    lens = np.concatenate([np.arange(0, 48), rng.integers(0, 2048 - S - 128, n - 48)])
+    lens[48:80] = 2048 - S - 128 - np.arange(32)  # the longest ones
+    ids = rng.integers(0, len(PSKS), lens.size) if multi else None
+    psks = PSKS if multi else [PSK]
+    hb = gh.make_case(rng, kind, direction, lens, psks, psk_ids=ids, in_align=2048,
+                      out_align=2048, in_lead=lead, out_lead=lead)
+    return hb, psks
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("direction", DIRS)
+@pytest.mark.parametrize("lead", [0, 64, 8])
+@pytest.mark.parametrize("multi", [False, True])
+def test_out_lines_device(ctx, kind, direction, lead, multi):
+    """Every output byte and out_len equal the oracle's; only the packet's own
+    head block and its last line's padding may change; the padding is
+    written (the lines are whole)."""
+    rng = np.random.Generator(np.random.PCG64(7700 + 100 * kind + 10 * direction + multi + lead))
+    hb, psks = make_lines(rng, kind, direction, multi, lead)
+    ref = gh.run_oracle(kind, direction, psks, hb)
+    hb.flags = sqobfs.FLAG_OUT_LINES
+    with sqobfs.Keyring(ctx, kind, psks) as kr:
+        gh.run_device(ctx, kr, direction, hb)
+    assert np.array_equal(hb.out_len, ref.out_len)
+    # the device copy lies 128-byte aligned (torch): line ends by buffer offset
+    m = np.zeros(hb.out.size, dtype=bool)
+    for o, n in zip(hb.out_off.astype(np.int64), ref.out_len.astype(np.int64)):
+        if 0 < n < 0xFFFFFFF0:
+            m[o & ~15:o] = True
+            m[o + n:(o + n + 127) & ~127] = True
+    bad = np.nonzero((hb.out != ref.out) & ~m)[0]
+    assert bad.size == 0, f"{bad.size} bytes outside the scratch padding differ, first at {bad[0]}"
+    # the padding past the 16-byte block is written somewhere (pad blocks ran)
+    past = np.zeros(hb.out.size, dtype=bool)
+    for o, n in zip(hb.out_off.astype(np.int64), ref.out_len.astype(np.int64)):
+        if 0 < n < 0xFFFFFFF0:
+            past[(o + n + 15) & ~15:(o + n + 127) & ~127] = True
+    assert ((hb.out != ref.out) & past).any()
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("direction", DIRS)
+@pytest.mark.parametrize("pinned", [False, True])
+def test_out_lines_run_host(ctx, kind, direction, pinned):
+    """Through sqobfs_run_host: the staging keeps output addresses modulo 128
+    and stages the last line's padding."""
+    rng = np.random.Generator(np.random.PCG64(7900 + 10 * kind + direction + 4 * pinned))
+    hb, psks = make_lines(rng, kind, direction, True, 64, n=20000)
+    ref = gh.run_oracle(kind, direction, psks, hb)
+    hb.flags = sqobfs.FLAG_OUT_LINES | sqobfs.FLAG_OUT_UNINIT
+    keep = []
+    try:
+        if pinned:
+            for name in ("data", "out"):
+                a = getattr(hb, name)
+                p = sqobfs.PinnedArray(ctx, a.size + 128)
+                sh = (a.ctypes.data - p.array.ctypes.data) % 128
+                v = p.array[sh:sh + a.size]
+                v[:] = a
+                keep.append(p)
+                setattr(hb, name, v)
+        with sqobfs.Keyring(ctx, kind, psks) as kr:
+            gh.run_host(ctx, kr, direction, hb)
+        assert np.array_equal(hb.out_len, ref.out_len)
+        inside = np.zeros(hb.out.size, dtype=bool)
+        for o, n in zip(hb.out_off.astype(np.int64), ref.out_len.astype(np.int64)):
+            if 0 < n < 0xFFFFFFF0:
+                inside[o:o + n] = True
+        bad = np.nonzero((hb.out != ref.out) & inside)[0]
+        assert bad.size == 0, f"{bad.size} output bytes differ, first at {bad[0]}"
+    finally:
+        for p in keep:
+            p.free()
