@@ -270,13 +270,16 @@ def test_long_and_empty_psks(ctx, kind):
 
 
 @pytest.mark.parametrize("kind", KINDS)
-@pytest.mark.parametrize("longest", [0, 1, 8, 24, 55, 56, 63, 64, 119, 120, 121, 127, 128])
+@pytest.mark.parametrize("longest", [0, 1, 8, 24, 39, 40, 55, 56, 63, 64, 72, 73, 119, 120, 121,
+                                     127, 128])
 def test_keyring_hot_bounds(ctx, kind, longest):
     """The multi-PSK kernels load only the entry words the keyring's longest
     PSK needs, and no chaining value when no PSK has a PSK-only block
     (sq_api.hip keyring_hot_words): keyrings whose longest PSK sits at each
     boundary of those bounds (one more message word; BLAKE2b's one/two-block
-    final at tail 120/121; a PSK-only block at 64 / 128 bytes)."""
+    final at tail 120/121; a PSK-only block at 64 / 128 bytes; SHA-256's
+    one/two-block final at 39/40 and BLAKE2b's ten/eleven message words at
+    72/73)."""
     rng = np.random.Generator(np.random.PCG64(1300 + longest + 7 * kind))
     ks = list(rng.integers(0, longest + 1, 40)) + [longest]
     psks = [rng.integers(0, 256, int(k), dtype=np.uint8).tobytes() for k in ks]
