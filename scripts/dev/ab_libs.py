@@ -35,7 +35,7 @@ ppws = [int(x) for x in os.environ.get("AB_PPWS", "").split(",") if x]
 fsets = [int(x) for x in os.environ.get("AB_FLAGS", "").split(",") if x]
 specs = [(paths[0], u) for u in ppws] if ppws else [(p, 0) for p in paths]
 if fsets:
-    specs = [(paths[0], -f) for f in fsets]  # (negative: a flag set, default unit)
+    specs = [(paths[0], -f - 1) for f in fsets]  # (negative: a flag set, default unit)
 specs = specs * int(os.environ.get("AB_KR", "1"))
 loaded = {}
 for path, u in specs:
@@ -44,7 +44,7 @@ for path, u in specs:
     sqobfs._lib = loaded[path]
     ctx = sqobfs.Context(0)
     kr = sqobfs.Keyring(ctx, kind, sh["psks"])
-    fl = -u if u < 0 else None
+    fl = -u - 1 if u < 0 else None
     u = max(u, 0)
     ctx.unit_packets = u or int(os.environ.get("AB_PPW", "0")) or sqobfs.unit_packets_for(
         sh["payload_bytes"], n, n_psk > 1)

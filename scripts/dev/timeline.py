@@ -85,7 +85,11 @@ def main():
                        for i, nm in enumerate(names)}
     life = t[:, 5] - t[:, 0]
     out["life_us"] = {"median": round(float(np.median(life)), 1),
+                      "mean": round(float(life.mean()), 2),
                       "p90": round(float(np.percentile(life, 90)), 1)}
+    # resident waves on average (Little: sum of lives / span), and the gaps
+    # between a slot's waves are not visible here
+    out["mean_resident_waves"] = round(float(life.sum() / (t[:, 5].max())), 1)
     out["last_start_us"] = round(float(t[:, 0].max()), 1)
     out["first_end_us"] = round(float(t[:, 5].min()), 1)
     out["tail_us"] = round(float(t[:, 5].max() - t[:, 0].max()), 1)
