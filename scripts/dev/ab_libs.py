@@ -24,6 +24,7 @@ cfg, direction, rounds = sys.argv[1], sys.argv[2], int(sys.argv[3])
 paths = sys.argv[4:]
 dev = torch.device("cuda", 0)
 kind, n, L, n_psk = bench.CONFIGS[cfg]
+n = int(os.environ.get("AB_PACKETS", n))  # (dev: another batch size)
 layout = os.environ.get("AB_LAYOUT", "dense")
 sh = bench.build_shard(torch, dev, kind, n, L, n_psk, 0, 1, cfg, layout)
 S = sh["S"]

@@ -73,6 +73,7 @@ struct KParams {
   uint32_t ppw;             // packets per wavefront (unit size), 1 .. 62; 0 = default
   uint32_t out_blocks;      // 1: SQOBFS_FLAG_OUT_BLOCKS (outputs own their 16-byte blocks)
   uint32_t out_lines;       // 1: SQOBFS_FLAG_OUT_LINES (... and their last 128-byte line)
+  uint32_t xcd;             // 1: XCD-contiguous units (set by the launcher: large batches)
   uint32_t psk_hot_m;       // multi-PSK: words of entry block 0 any entry needs (the rest are 0)
   uint32_t psk_hot_iv;      // multi-PSK: 1 when no entry has PSK-only blocks (h = initial state)
   uint32_t salt_key[8];

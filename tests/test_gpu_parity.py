@@ -192,6 +192,35 @@ def test_single_psk_lengths(ctx, kind, direction):
 
 @pytest.mark.parametrize("kind", KINDS)
 @pytest.mark.parametrize("direction", DIRS)
+def test_xcd_remapped_launch(ctx, kind, direction):
+    """Launches of at least 2^19 units take the XCD-contiguous unit order
+    (sq_kernels.hip kXcdMinUnits): one-packet units over 600,001 short
+    datagrams (an odd grid, not a multiple of 8 workgroups) give the
+    oracle's bytes, neighbours and out_len for every packet."""
+    S = sqobfs.SALT_LEN[kind]
+    rng = np.random.Generator(np.random.PCG64(4400 + 10 * kind + direction))
+    n = 600_001
+    lens = rng.integers(0, 96, n).astype(np.int64)
+    if direction == DEOBFUSCATE:
+        lens += S // 2  # some below S (passthrough / dropped), most above
+    in_off = np.cumsum(lens) - lens + 5
+    data = rng.integers(0, 256, int(lens.sum()) + 64, dtype=np.uint8)
+    osz = np.array([gh.out_size(kind, direction, int(L), int(L)) for L in lens], dtype=np.int64)
+    out_off = np.cumsum(osz) - osz + 3
+    out = np.full(int(osz.sum()) + 64, gh.SENTINEL, dtype=np.uint8)
+    salt = rng.integers(0, 256, n * S, dtype=np.uint8) if direction == OBFUSCATE else None
+    hb = sqobfs.HostBatch(data, in_off.astype(np.uint64), lens.astype(np.uint32), out,
+                          out_off.astype(np.uint64), np.zeros(n, dtype=np.uint32), salt, None,
+                          None)
+    ctx.unit_packets = 1
+    try:
+        check(ctx, kind, direction, [PSK], hb, "xcd-remapped launch")
+    finally:
+        ctx.unit_packets = 0
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("direction", DIRS)
 def test_unit_sizes(ctx, kind, direction):
     """Every unit size gives the same bytes (sqobfs_set_unit_packets): unit
     boundaries, donation and the neighbour lanes move with it.  Ragged and
