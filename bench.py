@@ -672,9 +672,9 @@ def main():
             "batch_flags": {0: "none", sqobfs.FLAG_OUT_BLOCKS: "SQOBFS_FLAG_OUT_BLOCKS",
                             sqobfs.FLAG_OUT_LINES: "SQOBFS_FLAG_OUT_LINES"}[ob],
             "unit_packets": ctx.unit_packets,
-            # sq_kernels.hip kXcdMinUnits: launches of >= 2^19 units remap
+            # sq_kernels.hip kXcdMinUnits: launches of >= 2^18 units remap
             # workgroups so each XCD walks a contiguous eighth of the batch
-            "unit_order": ("XCD-contiguous" if -(-n // ctx.unit_packets) >= 1 << 19
+            "unit_order": ("XCD-contiguous" if -(-n // ctx.unit_packets) >= 1 << 18
                            else "dispatch order"),
             "unit_rule": ("--unit-packets" if args.unit_packets else
                           "sqobfs_unit_packets_for(payload bytes, n): ~21.7 KB per wavefront "

@@ -24,11 +24,12 @@ cfg, direction, rounds = sys.argv[1], sys.argv[2], int(sys.argv[3])
 paths = sys.argv[4:]
 dev = torch.device("cuda", 0)
 kind, n, L, n_psk = bench.CONFIGS[cfg]
-n = int(os.environ.get("AB_PACKETS", n))  # (dev: another batch size)
+n = int(os.environ.get("AB_PACKETS", "0")) or n  # (dev: another batch size)
 layout = os.environ.get("AB_LAYOUT", "dense")
 sh = bench.build_shard(torch, dev, kind, n, L, n_psk, 0, 1, cfg, layout)
 S = sh["S"]
 ob = sqobfs.FLAG_OUT_BLOCKS if sh["slotted"] else 0
+ob = int(os.environ.get("AB_OB", ob))  # (e.g. 8: SQOBFS_FLAG_OUT_LINES for slot2048)
 s = torch.cuda.current_stream(dev).cuda_stream
 variants = []
 # AB_PPWS="18,20,..." with one library: one variant per unit size instead

@@ -136,15 +136,19 @@ static_assert(!SQ_EARLY || SQ_KLATE, "SQ_EARLY needs SQ_KLATE");
 // XCDs, so block b runs on XCD b % 8 and, unmapped, the XCDs share one
 // moving window of the batch.  Remapped, each XCD walks its own contiguous
 // eighth (its L2 and its address translation see one window 1/8 the size).
-// Measured in one process (profiles/r03/ab/xcd): -5 %
-// on 16M x 1350 B batches (45 GB of buffers), -2 to -3.5 % on the 16M
-// 256-PSK batch, -1 % at 8M, but +1.3 to +2.9 % at 1M-4M packets of 1350 B.
-// So launches of at least kXcdMinUnits units remap (KParams.xcd).  SQ_XCD
-// (timing builds): -1 that rule, 0 never, 1 always.
+// Measured in one process on three boxes (DESIGN.md section 5,
+// profiles/r03/ab/xcd): 16M x 1350 B batches (45 GB of buffers) -5 to -7 %,
+// the 16M 256-PSK batch -2 to -5.5 %, 4M x 1350 B +1.9 % on one box and
+// -5 % on another, 1M +1.3 to +2.9 % (the gain follows the address-
+// translation load, which depends on the box's memory as well as the
+// size).  So launches of at least kXcdMinUnits units (~5.7 GB of payload at
+// the byte-sized units) remap (KParams.xcd).  Runs of 32-768 blocks per XCD
+// inside 8-run windows instead of eighths gained less at 16M and nothing at
+// 1M.  SQ_XCD (timing builds): -1 that rule, 0 never, 1 always.
 #ifndef SQ_XCD
 #define SQ_XCD -1
 #endif
-constexpr uint64_t kXcdMinUnits = 1u << 19;
+constexpr uint64_t kXcdMinUnits = 1u << 18;
 
 #define SQ_STR2(x) #x
 #define SQ_STR(x) SQ_STR2(x)
@@ -1141,7 +1145,7 @@ __global__ __launch_bounds__(WPB * kWave) void obfs_kernel(const KParams P) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wv = threadIdx.x / kWave;
   uint32_t lb = blockIdx.x;
-  if (P.xcd) {  // (a bijection of [0, gridDim.x) for any grid size)
+  if (P.xcd) {  // eighths (a bijection of [0, gridDim.x) for any grid size)
     const uint32_t ng = gridDim.x, q = ng / 8, r = ng % 8, xcd = lb % 8, ix = lb / 8;
     lb = xcd < r ? xcd * (q + 1) + ix : r * (q + 1) + (xcd - r) * q + ix;
   }

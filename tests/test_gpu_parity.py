@@ -193,7 +193,7 @@ def test_single_psk_lengths(ctx, kind, direction):
 @pytest.mark.parametrize("kind", KINDS)
 @pytest.mark.parametrize("direction", DIRS)
 def test_xcd_remapped_launch(ctx, kind, direction):
-    """Launches of at least 2^19 units take the XCD-contiguous unit order
+    """Launches of at least 2^18 units take the XCD-contiguous unit order
     (sq_kernels.hip kXcdMinUnits): one-packet units over 600,001 short
     datagrams (an odd grid, not a multiple of 8 workgroups) give the
     oracle's bytes, neighbours and out_len for every packet."""
