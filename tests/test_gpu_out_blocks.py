@@ -123,30 +123,38 @@ def test_out_blocks_run_host(ctx, kind, direction, pinned):
             p.free()
 
 
-def make_lines(rng, kind, direction, multi, lead, n=3000):
+def make_lines(rng, kind, direction, multi, lead, n=3000, inplace=False):
     """Fixed 2048-byte slots (the Go Slots / the packet conn engine), outputs
     short enough that the padding to the next 128-byte line stays in the
-    slot wherever the buffer lies."""
+    slot wherever the buffer lies; `inplace`: each packet transformed in its
+    own slot (the vectorised WriteTo's headroom layout, or decoded behind
+    its salt)."""
     S = sqobfs.SALT_LEN[kind]
     lens = np.concatenate([np.arange(0, 48), rng.integers(0, 2048 - S - 128, n - 48)])
     lens[48:80] = 2048 - S - 128 - np.arange(32)  # the longest ones
     ids = rng.integers(0, len(PSKS), lens.size) if multi else None
     psks = PSKS if multi else [PSK]
-    hb = gh.make_case(rng, kind, direction, lens, psks, psk_ids=ids, in_align=2048,
-                      out_align=2048, in_lead=lead, out_lead=lead)
+    if inplace:
+        hb = gh.make_case(rng, kind, direction, lens, psks, psk_ids=ids, in_align=2048,
+                          in_lead=lead, inplace=True)
+    else:
+        hb = gh.make_case(rng, kind, direction, lens, psks, psk_ids=ids, in_align=2048,
+                          out_align=2048, in_lead=lead, out_lead=lead)
     return hb, psks
 
 
 @pytest.mark.parametrize("kind", KINDS)
 @pytest.mark.parametrize("direction", DIRS)
-@pytest.mark.parametrize("lead", [0, 64, 8])
+@pytest.mark.parametrize("lead,inplace", [(0, False), (64, False), (8, False), (0, True),
+                                          (8, True)])
 @pytest.mark.parametrize("multi", [False, True])
-def test_out_lines_device(ctx, kind, direction, lead, multi):
+def test_out_lines_device(ctx, kind, direction, lead, inplace, multi):
     """Every output byte and out_len equal the oracle's; only the packet's own
     head block and its last line's padding may change; the padding is
     written (the lines are whole)."""
-    rng = np.random.Generator(np.random.PCG64(7700 + 100 * kind + 10 * direction + multi + lead))
-    hb, psks = make_lines(rng, kind, direction, multi, lead)
+    rng = np.random.Generator(np.random.PCG64(7700 + 100 * kind + 10 * direction + multi + lead +
+                                              5 * inplace))
+    hb, psks = make_lines(rng, kind, direction, multi, lead, inplace=inplace)
     ref = gh.run_oracle(kind, direction, psks, hb)
     hb.flags = sqobfs.FLAG_OUT_LINES
     with sqobfs.Keyring(ctx, kind, psks) as kr:
