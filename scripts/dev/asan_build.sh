@@ -1,0 +1,19 @@
+#!/bin/bash
+# Dev: AddressSanitizer build of the HOST code of libsqobfs (the device code
+# is not instrumented: GPU sanitizers are not used on this pool) and of the
+# threaded C tests that drive it (packet conn engine, cgo call-sequence
+# replay).  Built here on the CPU; run on the GPU box by scripts/dev/asan_run.sh.
+set -e
+cd "$(dirname "$0")/../.."
+O=build/asan; mkdir -p $O
+CL=/opt/rocm/llvm/bin/clang
+SAN="-fsanitize=address -fno-omit-frame-pointer"
+/opt/rocm/bin/hipcc -O1 -g -std=c++17 -fPIC --offload-arch=gfx950 -Xarch_host -fsanitize=address \
+  -Xarch_host -fno-omit-frame-pointer -Iinclude -Ising-quic_amd/csrc -Ising-quic_amd/host \
+  -shared -shared-libasan -Wl,-rpath,/opt/rocm/llvm/lib/clang/22/lib/linux -o $O/libsqobfs.so sing-quic_amd/csrc/*.hip sing-quic_amd/host/*.cpp -lpthread
+make -s -C oracle
+for t in test_pconn test_cgo_sequence; do
+  $CL -std=c11 -O1 -g $SAN -shared-libasan -Iinclude -Ioracle tests/cpp/$t.c -L$O -lsqobfs \
+    -Loracle -loracle -lpthread -Wl,-rpath,$PWD/$O -Wl,-rpath,$PWD/oracle -Wl,-rpath,/opt/rocm/llvm/lib/clang/22/lib/linux -o $O/$t
+done
+ls -la $O
