@@ -16,4 +16,11 @@ for t in test_pconn test_cgo_sequence; do
   $CL -std=c11 -O1 -g $SAN -shared-libasan -Iinclude -Ioracle tests/cpp/$t.c -L$O -lsqobfs \
     -Loracle -loracle -lpthread -Wl,-rpath,$PWD/$O -Wl,-rpath,$PWD/oracle -Wl,-rpath,/opt/rocm/llvm/lib/clang/22/lib/linux -o $O/$t
 done
+$CL++ -std=c++17 -O1 -g $SAN -shared-libasan -Iinclude -Ising-quic_amd/host -Ioracle \
+  tests/cpp/test_packet_conn.cpp -L$O -lsqobfs -Loracle -loracle -lpthread -Wl,-rpath,$PWD/$O \
+  -Wl,-rpath,$PWD/oracle -Wl,-rpath,/opt/rocm/llvm/lib/clang/22/lib/linux -o $O/test_packet_conn
+# the latency tool drives the UDP endpoint (sqobfs_udp_conn_*) and the engine
+$CL -std=c11 -O1 -g $SAN -shared-libasan -Iinclude sing-quic_amd/tools/lat_bench.c -L$O -lsqobfs \
+  -Loracle -loracle -lpthread -Wl,-rpath,$PWD/$O -Wl,-rpath,$PWD/oracle \
+  -Wl,-rpath,/opt/rocm/llvm/lib/clang/22/lib/linux -o $O/lat_bench
 ls -la $O
