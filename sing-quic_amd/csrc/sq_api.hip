@@ -44,7 +44,10 @@ struct sqobfs_ctx {
 };
 
 namespace {
-constexpr uint32_t kHostChunks = 8;  // sqobfs_run_host pipeline depth
+#ifndef SQ_HOSTCHUNKS
+#define SQ_HOSTCHUNKS 8
+#endif
+constexpr uint32_t kHostChunks = SQ_HOSTCHUNKS;  // sqobfs_run_host pipeline depth
 // test hook (sqobfs_debug_fail_chunk): the launch of that pipeline chunk
 // fails as a device error would, once
 std::atomic<int> g_fail_chunk{-1};
