@@ -16,9 +16,11 @@ import bench  # noqa: E402
 
 SETS = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 cfg = sys.argv[2] if len(sys.argv) > 2 else "salamander-1m"
+layout = sys.argv[3] if len(sys.argv) > 3 else "dense"
+flags = {"slot2048": sqobfs.FLAG_OUT_LINES, "slot16": sqobfs.FLAG_OUT_BLOCKS}.get(layout, 0)
 dev = torch.device("cuda", 0)
 kind, n, L, n_psk = bench.CONFIGS[cfg]
-sh = bench.build_shard(torch, dev, kind, n, L, n_psk, 0, 1, cfg, "dense")
+sh = bench.build_shard(torch, dev, kind, n, L, n_psk, 0, 1, cfg, layout)
 ctx = sqobfs.Context(0)
 kr = sqobfs.Keyring(ctx, kind, sh["psks"])
 s = torch.cuda.current_stream(dev).cuda_stream
@@ -27,7 +29,7 @@ for k in range(SETS):
     data = sh["data"].clone()
     out = torch.zeros_like(sh["out"])
     b = sqobfs.make_batch(n, data, sh["in_off"], sh["lens"], out, sh["out_off"],
-                          sh["out_len"], sh["salt"], sh["psk_id"])
+                          sh["out_len"], sh["salt"], sh["psk_id"], flags=flags)
     sets.append((data, out, b))
 
 
