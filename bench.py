@@ -759,7 +759,28 @@ def e2e_rate(torch, sqobfs, ctx, kr, kind, n, L):
     salt = rng.integers(0, 256, n * S, dtype=np.uint8)
     res = {"packets": n, "payload_bytes": L}
     pins = []
-    for mode in ("pageable", "pinned", "pinned_out_uninit"):
+    for mode in ("pageable", "pinned", "pinned_out_uninit", "slots2048"):
+        if mode == "slots2048":
+            # the Go Slots.Run geometry: fixed 2,048-byte slots in page-locked
+            # memory, outputs read up to out_len (OUT_UNINIT), whole lines
+            # (OUT_LINES): run_host stages the datagrams' bytes only
+            pd, po = sqobfs.PinnedArray(ctx, n * 2048), sqobfs.PinnedArray(ctx, n * 2048)
+            pins += [pd, po]
+            pd.array[:] = rng.integers(0, 256, n * 2048, dtype=np.uint8)
+            offs = np.arange(n, dtype=np.uint64) * 2048
+            hb = sqobfs.HostBatch(pd.array, offs, np.full(n, L, np.uint32), po.array, offs,
+                                  np.zeros(n, np.uint32), salt,
+                                  flags=sqobfs.FLAG_OUT_UNINIT | sqobfs.FLAG_OUT_LINES)
+            b = hb.as_batch()
+            sqobfs.run_host(ctx, kr, sqobfs.OBFUSCATE, b)
+            reps = 5
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                sqobfs.run_host(ctx, kr, sqobfs.OBFUSCATE, b)
+            dt = (time.perf_counter() - t0) / reps
+            res[mode] = {"GiB_s_payload": round(n * L / dt / 2**30, 3),
+                         "ms_per_batch": round(dt * 1e3, 3)}
+            continue
         if mode == "pageable":
             data = rng.integers(0, 256, nin, dtype=np.uint8)
             out = np.zeros(nout, np.uint8)
@@ -783,7 +804,8 @@ def e2e_rate(torch, sqobfs, ctx, kr, kind, n, L):
                      "ms_per_batch": round(dt * 1e3, 3)}
     for p in pins:
         p.free()
-    res["path"] = "sqobfs_run_host: 8-chunk H2D | kernel | D2H pipeline on 3 HIP streams"
+    res["path"] = ("sqobfs_run_host: 8-chunk H2D | kernel | D2H pipeline on 3 HIP streams; "
+                   "fixed-stride page-locked slots staged as packed rows (2-D copies)")
     return res
 
 

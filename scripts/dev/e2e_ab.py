@@ -26,7 +26,7 @@ for r in range(rounds):
     for name, lib, ctx, kr in libs:
         sqobfs._lib = lib
         out = bench.e2e_rate(torch, sqobfs, ctx, kr, 0, n, 1350)
-        for mode in ("pageable", "pinned", "pinned_out_uninit"):
+        for mode in ("pageable", "pinned", "pinned_out_uninit", "slots2048"):
             res.setdefault((name, mode), []).append(out[mode]["GiB_s_payload"])
 for (name, mode), v in res.items():
     print(f"{name:20s} {mode:18s} median {statistics.median(v):7.2f} GiB/s  all {v}", flush=True)

@@ -375,6 +375,63 @@ void par_memcpy(void *dst, const void *src, size_t n) {
   for (auto &x : th) x.join();
 }
 
+// Fixed-stride slots (the Go Slots, socket batches): packet i's input at
+// in_off[0] + i si and its output at out_off[0] + i so.  sqobfs_run_host then
+// stages only the first wi / wo bytes of every slot, rows packed at pitches
+// pi / po, with 2-D copies (hipMemcpy2DAsync moves rows of ~1.4 KB at the
+// PCIe rate of a contiguous copy): a 2,048-byte slot
+// holding a 1,358-byte datagram costs 1,358 bytes of PCIe each way, not
+// 2,048.  Used when both buffers are page-locked, the strides hold the rows,
+// the input and output spans are apart, output rows keep their phase modulo
+// 16 / 128 (for SQOBFS_FLAG_OUT_BLOCKS / _LINES) and the packing saves at
+// least an eighth of a span.
+struct SlotPack {
+  bool on = false;
+  size_t si = 0, so = 0;    // caller's strides
+  size_t wi = 0, wo = 0;    // bytes staged per slot (the widest input / output)
+  size_t phi = 0, pho = 0;  // staged row offset of the input / output (address phase)
+  size_t pi = 0, po = 0;    // staged pitches
+};
+
+SlotPack slot_pack(const sqobfs_batch *hb, int kind, int dir, size_t in_lo, size_t in_hi,
+                   size_t out_lo, size_t out_hi, bool pinned) {
+  SlotPack sp;
+  const uint32_t n = hb->n;
+  if (!pinned || n < 64 || (hb->flags & SQOBFS_FLAG_DEVICE_SALT)) return sp;
+  if (hb->in_off[1] <= hb->in_off[0] || hb->out_off[1] <= hb->out_off[0]) return sp;
+  sp.si = hb->in_off[1] - hb->in_off[0];
+  sp.so = hb->out_off[1] - hb->out_off[0];
+  const size_t S = salt_len(kind);
+  for (uint32_t i = 0; i < n; i++) {
+    if (hb->in_off[i] != hb->in_off[0] + sp.si * i || hb->out_off[i] != hb->out_off[0] + sp.so * i)
+      return sp;
+    const size_t len = hb->in_len[i];
+    size_t cap = len;
+    if (kind == SQOBFS_XPLUS && dir == SQOBFS_DEOBFUSCATE && hb->in_cap)
+      cap = std::max<size_t>(len, hb->in_cap[i]);
+    size_t osz;
+    if (dir == SQOBFS_OBFUSCATE) osz = S + len;
+    else if (kind == SQOBFS_SALAMANDER) osz = len <= S ? len : len - S;
+    else osz = len < S ? 0 : cap - S;
+    sp.wi = std::max(sp.wi, cap);
+    sp.wo = std::max(sp.wo, osz);
+  }
+  const bool lines = hb->flags & SQOBFS_FLAG_OUT_LINES;
+  const bool blocks = lines || (hb->flags & SQOBFS_FLAG_OUT_BLOCKS);
+  const size_t oa = lines ? 128 : 16;
+  if (sp.wi > sp.si || sp.wo > sp.so || (blocks && sp.so % oa)) return sp;
+  // the input and output spans must be apart (no in-place slots)
+  if (in_hi > in_lo && out_hi > out_lo && hb->in + in_lo < hb->out + out_hi &&
+      hb->out + out_lo < hb->in + in_hi)
+    return sp;
+  sp.phi = ((uintptr_t)hb->in + hb->in_off[0]) & 15;
+  sp.pho = ((uintptr_t)hb->out + hb->out_off[0]) & (oa - 1);
+  sp.pi = align_up(sp.phi + sp.wi, 16);
+  sp.po = align_up(sp.pho + sp.wo, oa);
+  sp.on = 8 * (sp.pi + sp.po) <= 7 * (sp.si + sp.so);
+  return sp;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1072,11 +1129,15 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
   // last output line's padding, which the kernel writes, is staged too
   const size_t A = 256;
   const bool lines = hb->flags & SQOBFS_FLAG_OUT_LINES;
+  // fixed-stride slots: packed rows instead of the spans (slot_pack)
+  const SlotPack sp = nrun == nchunk ? slot_pack(hb, kind, dir, in_lo, in_hi, out_lo, out_hi,
+                                                 in_pinned && out_pinned)
+                                     : SlotPack{};
   size_t o = 0;
-  const size_t o_in = o + (((uintptr_t)hb->in + in_lo) & 15);
-  o = align_up(o_in + (in_hi - in_lo), A);
-  const size_t o_out = o + (((uintptr_t)hb->out + out_lo) & (lines ? 127 : 15));
-  o = align_up(o_out + (out_hi - out_lo) + (lines ? 128 : 0), A);
+  const size_t o_in = sp.on ? 0 : o + (((uintptr_t)hb->in + in_lo) & 15);
+  o = align_up(sp.on ? sp.pi * n : o_in + (in_hi - in_lo), A);
+  const size_t o_out = sp.on ? o : o + (((uintptr_t)hb->out + out_lo) & (lines ? 127 : 15));
+  o = align_up(sp.on ? o_out + sp.po * n : o_out + (out_hi - out_lo) + (lines ? 128 : 0), A);
   const size_t o_inoff = o;    o = align_up(o + 8ull * n, A);
   const size_t o_inlen = o;    o = align_up(o + 4ull * n, A);
   const size_t o_outoff = o;   o = align_up(o + 8ull * n, A);
@@ -1130,9 +1191,17 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
   } while (0)
 
   // descriptors: small, copied once up front
-  memcpy(H + o_inoff, hb->in_off, 8ull * n);
+  if (sp.on) {  // packed rows: packet i's bytes at row i, phase kept
+    uint64_t *io = (uint64_t *)(H + o_inoff), *oo = (uint64_t *)(H + o_outoff);
+    for (uint32_t i = 0; i < n; i++) {
+      io[i] = sp.pi * i + sp.phi;
+      oo[i] = sp.po * i + sp.pho;
+    }
+  } else {
+    memcpy(H + o_inoff, hb->in_off, 8ull * n);
+    memcpy(H + o_outoff, hb->out_off, 8ull * n);
+  }
   memcpy(H + o_inlen, hb->in_len, 4ull * n);
-  memcpy(H + o_outoff, hb->out_off, 8ull * n);
   if (dir == SQOBFS_OBFUSCATE && !dev_salt) memcpy(H + o_salt, hb->salt, S * n);
   if (hb->psk_id) memcpy(H + o_pid, hb->psk_id, 2ull * n);
   if (hb->in_cap) memcpy(H + o_cap, hb->in_cap, 4ull * n);
@@ -1146,7 +1215,17 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
   // kernel and chunk c-1's copy-out.
   for (uint32_t c = 0; c < nrun; c++) {
     const Range &ri = rin[c], &ro = rout[c];
-    if (ri.hi > ri.lo) {
+    const uint32_t rows = ri.p1 - ri.p0;
+    if (sp.on) {  // rows [p0, p1): the first wi / wo bytes of each slot
+      if (sp.wi && rows)
+        SQ_TRY_DRAIN(hipMemcpy2DAsync(D + o_in + sp.pi * ri.p0 + sp.phi, sp.pi,
+                                      hb->in + hb->in_off[ri.p0], sp.si, sp.wi, rows,
+                                      hipMemcpyHostToDevice, ctx->h2d));
+      if (preserve && sp.wo && rows)
+        SQ_TRY_DRAIN(hipMemcpy2DAsync(D + o_out + sp.po * ri.p0 + sp.pho, sp.po,
+                                      hb->out + hb->out_off[ri.p0], sp.so, sp.wo, rows,
+                                      hipMemcpyHostToDevice, ctx->h2d));
+    } else if (ri.hi > ri.lo) {
       const uint8_t *src = hb->in + ri.lo;
       if (!in_pinned) {
         par_memcpy(hin(ri.lo), src, ri.hi - ri.lo);
@@ -1155,7 +1234,7 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
       SQ_TRY_DRAIN(hipMemcpyAsync(din(ri.lo), src, ri.hi - ri.lo, hipMemcpyHostToDevice,
                                   ctx->h2d));
     }
-    if (preserve && ro.hi > ro.lo) {  // bytes between packets keep their value
+    if (!sp.on && preserve && ro.hi > ro.lo) {  // bytes between packets keep their value
       const uint8_t *src = hb->out + ro.lo;
       if (!out_pinned) {
         par_memcpy(hout(ro.lo), src, ro.hi - ro.lo);
@@ -1169,10 +1248,10 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
     SQ_TRY_DRAIN(hipStreamWaitEvent(ctx->stream, ev_in, 0));
     sqobfs_batch db = *hb;
     db.n = ri.p1 - ri.p0;
-    db.in = din(0);  // in_off[i] >= in_lo for every packet of the batch
+    db.in = sp.on ? D + o_in : din(0);  // in_off[i] >= in_lo for every packet of the batch
     db.in_off = (const uint64_t *)(D + o_inoff) + ri.p0;
     db.in_len = (const uint32_t *)(D + o_inlen) + ri.p0;
-    db.out = dout(0);
+    db.out = sp.on ? D + o_out : dout(0);
     db.out_off = (const uint64_t *)(D + o_outoff) + ri.p0;
     db.out_len = (uint32_t *)(D + o_outlen) + ri.p0;
     db.salt = dir == SQOBFS_OBFUSCATE && !dev_salt ? D + o_salt + S * ri.p0 : nullptr;
@@ -1194,7 +1273,12 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
     SQ_TRY_DRAIN(hipEventRecord(ev_k, ctx->stream));
     SQ_TRY_DRAIN(hipStreamWaitEvent(ctx->d2h, ev_k, 0));
     if (c + 1 == nrun) kr->uses.note(ctx->stream);
-    if (ro.hi > ro.lo) {
+    if (sp.on) {
+      if (sp.wo && rows)
+        SQ_TRY_DRAIN(hipMemcpy2DAsync(hb->out + hb->out_off[ri.p0], sp.so,
+                                      D + o_out + sp.po * ri.p0 + sp.pho, sp.po, sp.wo, rows,
+                                      hipMemcpyDeviceToHost, ctx->d2h));
+    } else if (ro.hi > ro.lo) {
       uint8_t *dst = out_pinned ? hb->out + ro.lo : hout(ro.lo);
       SQ_TRY_DRAIN(hipMemcpyAsync(dst, dout(ro.lo), ro.hi - ro.lo, hipMemcpyDeviceToHost,
                                   ctx->d2h));
