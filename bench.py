@@ -546,7 +546,10 @@ def main():
     # also the rest of its last 128-byte line (slot padding)
     ob = sqobfs.FLAG_OUT_BLOCKS if sh["slotted"] else 0
     if args.layout == "slot2048" and args.slot_flag == "lines":
-        assert args.slot_bytes % 128 == 0 and S + (L or 1452) + 128 <= args.slot_bytes
+        # every output's last line, padding included, inside its slot
+        lead = int(os.environ.get("SQ_BENCH_LEAD", "128")) % 128
+        assert args.slot_bytes % 128 == 0 and (lead + S + (L or 1452) + 127) // 128 * 128 <= \
+            args.slot_bytes, "--slot-flag lines needs slots holding the outputs' last lines"
         ob = sqobfs.FLAG_OUT_LINES
     if direction == sqobfs.OBFUSCATE and args.device_salt:
         ctx.salt_key(SALT_KEY, 0)
