@@ -125,3 +125,15 @@ def test_unit_packets_spread_small_batches():
     assert f(1350 * 4096, 4096) == 2
     assert f(1350 * 16384, 16384) == 8
     assert f(64 * 8192, 8192) == 4  # short packets: the spread rule binds
+
+
+def test_batch_flags_match_header():
+    """The ctypes binding's batch flags are the header's (the Go binding
+    takes them from the header through cgo)."""
+    import re
+    text = open(os.path.join(REPO, "include", "sqobfs.h")).read()
+    defs = {m.group(1): int(m.group(2)) for m in
+            re.finditer(r"#define SQOBFS_FLAG_(\w+) (\d+)u", text)}
+    assert defs == {"OUT_UNINIT": 1, "DEVICE_SALT": 2, "OUT_BLOCKS": 4, "OUT_LINES": 8}
+    for name, v in defs.items():
+        assert getattr(sqobfs, "FLAG_" + name) == v, name
