@@ -188,6 +188,122 @@ __device__ __forceinline__ void hp_mask(const QuicKeyDev &K, const uint32_t (&sa
   m1 = blk[1] & 0xFFu;
 }
 
+// ------------------------------------------------- lane-pair ChaCha20 blocks
+// The owner phases run one ChaCha20 block per packet at a time (the Poly1305
+// key block; the header-protection mask block) on the 32 owner lanes while
+// lanes 32-63 idle, and a wave instruction costs the same whatever its exec
+// mask.  Lane pairs (SQ_QSPLIT): owner lane l and lane l + 32 share the
+// block.  The low lane holds state columns 0-1, the high lane columns 2-3
+// (4 x 4 state, words x0..x15 row-major, RFC 8439 2.3).  The column round
+// is local; the diagonal round runs on the pair's diagonals after a swap of
+// 4 words with the partner (v_permlane32_swap, a VALU op: b = (b1, b0'),
+// c = (c0', c1'), d = (d1', d0), where ' is the partner's) and swaps 4 back
+// after it.  Per lane 40 quarter rounds and 80 word swaps instead of 80
+// quarter rounds.
+#ifndef SQ_QSPLIT
+#define SQ_QSPLIT 1
+#endif
+static_assert(!SQ_QSPLIT || kQPpw == kWave / 2, "lane pairs are lanes l and l + 32");
+
+// the partner lane's x (lane l <-> lane l + 32); every lane must be active
+__device__ __forceinline__ uint32_t xhalf(uint32_t x, bool hi) {
+  const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return hi ? r[0] : r[1];
+}
+
+// the low lane's pointer in both lanes of a pair
+template <typename T>
+__device__ __forceinline__ T *xlow_ptr(T *p, bool hi) {
+  const uint64_t v = (uint64_t)p;
+  const uint32_t lo = xhalf((uint32_t)v, hi), up = xhalf((uint32_t)(v >> 32), hi);
+  return hi ? (T *)(((uint64_t)up << 32) | lo) : p;
+}
+
+#define SQ_CC_QR2(a, b, c, d)                 \
+  a += b; d ^= a; d = cc_rotl(d, 16);         \
+  c += d; b ^= c; b = cc_rotl(b, 12);         \
+  a += b; d ^= a; d = cc_rotl(d, 8);          \
+  c += d; b ^= c; b = cc_rotl(b, 7);
+
+// One block over a lane pair.  key: the block's key (read in full by both
+// lanes); counter, n0..n2: the low lane's (the high lane's are ignored).
+// o = this lane's two columns of the output: low lane words
+// 0,1,4,5,8,9,12,13, high lane 2,3,6,7,10,11,14,15.
+__device__ __forceinline__ void chacha20_pair(const uint32_t (&key)[8], uint32_t counter,
+                                              uint32_t n0, uint32_t n1, uint32_t n2, bool hi,
+                                              uint32_t (&o)[8]) {
+  const uint32_t y1 = xhalf(n1, hi), y2 = xhalf(n2, hi);
+  uint32_t in[8];
+  in[0] = hi ? 0x79622d32u : 0x61707865u;
+  in[1] = hi ? 0x6b206574u : 0x3320646eu;
+  in[2] = hi ? key[2] : key[0];
+  in[3] = hi ? key[3] : key[1];
+  in[4] = hi ? key[6] : key[4];
+  in[5] = hi ? key[7] : key[5];
+  in[6] = hi ? y1 : counter;
+  in[7] = hi ? y2 : n0;
+  uint32_t a0 = in[0], a1 = in[1], b0 = in[2], b1 = in[3], c0 = in[4], c1 = in[5], d0 = in[6],
+           d1 = in[7];
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    SQ_CC_QR2(a0, b0, c0, d0)
+    SQ_CC_QR2(a1, b1, c1, d1)
+    // diagonalise: low lane (x0, x5, x10, x15), (x1, x6, x11, x12); high
+    // lane (x2, x7, x8, x13), (x3, x4, x9, x14)
+    uint32_t e0 = b1, e1 = xhalf(b0, hi), f0 = xhalf(c0, hi), f1 = xhalf(c1, hi),
+             g0 = xhalf(d1, hi), g1 = d0;
+    SQ_CC_QR2(a0, e0, f0, g0)
+    SQ_CC_QR2(a1, e1, f1, g1)
+    b0 = xhalf(e1, hi); b1 = e0;
+    c0 = xhalf(f0, hi); c1 = xhalf(f1, hi);
+    d0 = g1; d1 = xhalf(g0, hi);
+  }
+  o[0] = a0 + in[0]; o[1] = a1 + in[1]; o[2] = b0 + in[2]; o[3] = b1 + in[3];
+  o[4] = c0 + in[4]; o[5] = c1 + in[5]; o[6] = d0 + in[6]; o[7] = d1 + in[7];
+}
+#undef SQ_CC_QR2
+
+// The header-protection mask of every live owner lane (hp_mask); with lane
+// pairs, every lane of the wave must call it.
+template <bool MULTI>
+__device__ __forceinline__ void hp_mask_lanes(const QuicKeyDev *K, const uint32_t (&sample)[4],
+                                              bool live, uint32_t lane, uint32_t &m0,
+                                              uint32_t &m1) {
+#if SQ_QSPLIT
+  const bool hi = lane >= kWave / 2;
+  const QuicKeyDev *KP = MULTI ? xlow_ptr(K, hi) : K;
+  uint32_t o[8];
+  chacha20_pair(KP->hp, sample[0], sample[1], sample[2], sample[3], hi, o);
+  m0 = o[0];
+  m1 = o[1] & 0xFFu;
+#else
+  if (live) hp_mask(*K, sample, m0, m1);
+#endif
+}
+
+// The Poly1305 one-time key, otk[0..8) = ChaCha20(key, 0, nonce) words 0-7,
+// of every live owner lane; with lane pairs, every lane must call it.
+template <bool MULTI>
+__device__ __forceinline__ void otk_lanes(const QuicKeyDev *K, const uint32_t (&nonce)[3],
+                                          bool live, uint32_t lane, uint32_t (&otk)[16]) {
+#if SQ_QSPLIT
+  const bool hi = lane >= kWave / 2;
+  const QuicKeyDev *KP = MULTI ? xlow_ptr(K, hi) : K;
+  uint32_t o[8];
+  chacha20_pair(KP->key, 0u, nonce[0], nonce[1], nonce[2], hi, o);
+  otk[0] = o[0];
+  otk[1] = o[1];
+  otk[2] = xhalf(o[0], hi);
+  otk[3] = xhalf(o[1], hi);
+  otk[4] = o[2];
+  otk[5] = o[3];
+  otk[6] = xhalf(o[2], hi);
+  otk[7] = xhalf(o[3], hi);
+#else
+  if (live) chacha20_block(K->key, 0, nonce, otk);
+#endif
+}
+
 // Payload pass shared by seal (MAC over the output) and open (MAC over the
 // input): XOR `len` bytes from src with the keystream from counter 1, MAC
 // the ciphertext side, store to dst.  A streaming realigner: one aligned
@@ -448,13 +564,20 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
     live = false;
     if (OPEN && Q.pn_out) Q.pn_out[p] = 0;  // rejected: pn_out 0 (as below)
   }
+  const bool entered = live;
+  uint64_t pn = 0;
+  uint32_t pnb[4] = {0u, 0u, 0u, 0u}, hs[4] = {0u, 0u, 0u, 0u};  // open: pn bytes, hp sample
+  // packet byte k (de-obfuscated when the fused layer is on)
+  auto hb = [&](uint32_t k) -> uint32_t {
+    const uint32_t b = head_byte(hd, src, k);
+    return (OB && OPEN && k >= 32) ? b ^ byte32(okey, k & 31) : b;
+  };
   if (live) {
     src = (uint64_t)Q.in + Q.in_off[p];
     dst = (uint64_t)Q.out + Q.out_off[p];
     len = Q.in_len[p];
     pno = Q.pn_offset[p];
-    uint64_t pn = Q.pn[p];
-    uint32_t pnb[4] = {0u, 0u, 0u, 0u};
+    pn = Q.pn[p];
     if (OB) {
       if (!OPEN) {  // wire = salt || protected packet ^ key
         wire = dst;
@@ -472,11 +595,6 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
       }
       salamander_key(&Q.opsk, osalt, okey);
     }
-    // packet byte k (de-obfuscated when the fused layer is on)
-    auto hb = [&](uint32_t k) -> uint32_t {
-      const uint32_t b = head_byte(hd, src, k);
-      return (OB && OPEN && k >= 32) ? b ^ byte32(okey, k & 31) : b;
-    };
     if (!OPEN) {
       if (len) load_head32(src, len, hd);
       first = hd[0] & 0xFFu;
@@ -491,15 +609,14 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
     } else if (len < 16 || len > kQMaxPacket || pno + 4 + 16 > len) {
       live = false;
     } else {
-      uint32_t sample[4], m0, m1;
-      load16(src + pno + 4, src + len, sample);
+      load16(src + pno + 4, src + len, hs);
       load16(src + len - 16, src + len, rtag);  // before any in-place write
       load_head32(src, len, hd);
       if (OB) {  // de-obfuscate what was read: key byte of QUIC offset k is okey[k % 32]
         uint32_t k4[4];
         keywin(okey, (pno + 4) & 31, k4);
 #pragma unroll
-        for (int w = 0; w < 4; w++) sample[w] ^= k4[w];
+        for (int w = 0; w < 4; w++) hs[w] ^= k4[w];
         keywin(okey, (len - 16) & 31, k4);
 #pragma unroll
         for (int w = 0; w < 4; w++) rtag[w] ^= k4[w];
@@ -510,7 +627,12 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
 #pragma unroll
         for (int w = 0; w < 4; w++) hd[4 + w] ^= k4[w];
       }
-      hp_mask(*K, sample, m0, m1);
+    }
+  }
+  if (OPEN) {  // header protection off (every lane: lane pairs)
+    uint32_t m0 = 0u, m1 = 0u;
+    hp_mask_lanes<MULTI>(K, hs, live, lane, m0, m1);
+    if (live) {
       const uint32_t pfirst = hd[0] & 0xFFu;
       first = pfirst ^ (m0 & ((pfirst & 0x80) ? 0x0Fu : 0x1Fu));
       pn_len = (first & 3) + 1;
@@ -528,40 +650,42 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
         pl = len - 16 - hdr;
       }
     }
+  }
+  if (entered) {
     if (!live) status = kQEShort;
     // every owner lane writes its pn_out (0 when the packet was rejected)
-    if (OPEN && owner && Q.pn_out) Q.pn_out[p] = pn_dec;
-    if (live) {
-      quic_nonce(*K, pn, nonce);
-      chacha20_block(K->key, 0, nonce, otk);
-      poly_init(P, otk);
-      // AAD = the unprotected header; seal copies it unchanged (protection
-      // is applied in phase 3), open writes the unprotected header
-      for (uint32_t q = 0; q < hdr; q += 16) {
-        uint32_t w[4];
-        head_block(hd, src, q, hdr, w);
-        if (OB && OPEN && q >= 32) {
-          uint32_t k4[4];
-          keywin(okey, q & 31, k4);
+    if (OPEN && Q.pn_out) Q.pn_out[p] = pn_dec;
+  }
+  if (live) quic_nonce(*K, pn, nonce);
+  otk_lanes<MULTI>(K, nonce, live, lane, otk);  // every lane: lane pairs
+  if (live) {
+    poly_init(P, otk);
+    // AAD = the unprotected header; seal copies it unchanged (protection
+    // is applied in phase 3), open writes the unprotected header
+    for (uint32_t q = 0; q < hdr; q += 16) {
+      uint32_t w[4];
+      head_block(hd, src, q, hdr, w);
+      if (OB && OPEN && q >= 32) {
+        uint32_t k4[4];
+        keywin(okey, q & 31, k4);
 #pragma unroll
-          for (int j = 0; j < 4; j++) w[j] ^= k4[j] & range_mask(0, (int)(hdr - q), j);
-        }
-        if (OPEN) {
-          if (q == 0) set_byte(w, 0, first);
-          for (uint32_t i = 0; i < pn_len; i++) {
-            const uint32_t pos = pno + i;
-            if (pos >= q && pos < q + 16) set_byte(w, pos - q, pnb[i]);
-          }
-        }
-        poly_block(P, w);
-        if (OB && !OPEN) {  // the wire carries the (still unprotected) header ^ key
-          uint32_t k4[4];
-          keywin(okey, q & 31, k4);
-#pragma unroll
-          for (int j = 0; j < 4; j++) w[j] ^= k4[j];
-        }
-        if (OPEN || OB || dst != src) store16(dst + q, w, hdr - q < 16 ? hdr - q : 16);
+        for (int j = 0; j < 4; j++) w[j] ^= k4[j] & range_mask(0, (int)(hdr - q), j);
       }
+      if (OPEN) {
+        if (q == 0) set_byte(w, 0, first);
+        for (uint32_t i = 0; i < pn_len; i++) {
+          const uint32_t pos = pno + i;
+          if (pos >= q && pos < q + 16) set_byte(w, pos - q, pnb[i]);
+        }
+      }
+      poly_block(P, w);
+      if (OB && !OPEN) {  // the wire carries the (still unprotected) header ^ key
+        uint32_t k4[4];
+        keywin(okey, q & 31, k4);
+#pragma unroll
+        for (int j = 0; j < 4; j++) w[j] ^= k4[j];
+      }
+      if (OPEN || OB || dst != src) store16(dst + q, w, hdr - q < 16 ? hdr - q : 16);
     }
   }
   const bool coop = live && pl <= kQCoopMax;
@@ -691,127 +815,129 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
 #endif
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
-  // ---- 3. owner lanes: combine, tag, header protection
-  if (!owner) return;
-  if (!live) {
-    Q.out_len[p] = status;
-    return;
+  // ---- 3. owner lanes: combine, tag, header protection (seal with lane
+  // pairs: every lane stays for the mask block)
+  const bool fin = owner && live;
+  if (owner && !live) Q.out_len[p] = status;
+  if (OPEN || !SQ_QSPLIT) {
+    if (!fin) return;
   }
-  uint32_t ct32[8];
-  if (coop && SQ_QPAIR) {
-    // pairs: h = h r^c + E_j, c = 8 chunks for a whole pair, r^klast for a
-    // last pair of one block, r^(4 + klast) for one of two
-    const QRec &Rq = recs[wv][lane];
-    Poly R1;
-    R1.r0 = P.r0; R1.r1 = P.r1; R1.r2 = P.r2; R1.r3 = P.r3; R1.r4 = P.r4;
-    R1.s1 = P.s1; R1.s2 = P.s2; R1.s3 = P.s3; R1.s4 = P.s4;
-    Poly X;
-    X.r0 = Rq.r4[0]; X.r1 = Rq.r4[1]; X.r2 = Rq.r4[2]; X.r3 = Rq.r4[3]; X.r4 = Rq.r4[4];
-    X.s1 = X.r1 * 5; X.s2 = X.r2 * 5; X.s3 = X.r3 * 5; X.s4 = X.r4 * 5;
-    Poly Y = X;
-    X.h0 = X.r0; X.h1 = X.r1; X.h2 = X.r2; X.h3 = X.r3; X.h4 = X.r4;
-    poly_mul(X);  // r^8
-    Y.h0 = Rq.rl[0]; Y.h1 = Rq.rl[1]; Y.h2 = Rq.rl[2]; Y.h3 = Rq.rl[3]; Y.h4 = Rq.rl[4];
-    poly_mul(Y);  // r^(4 + klast)
-    const bool one = nblk & 1;  // the last pair holds one block
-    const uint32_t M0 = one ? Rq.rl[0] : Y.h0, M1 = one ? Rq.rl[1] : Y.h1,
-                   M2 = one ? Rq.rl[2] : Y.h2, M3 = one ? Rq.rl[3] : Y.h3,
-                   M4 = one ? Rq.rl[4] : Y.h4;
-    const uint32_t npair = nflat / 2;
-    for (uint32_t j = 0; j < npair; j++) {
-      const bool lastp = j + 1 == npair;
-      P.r0 = lastp ? M0 : X.h0;
-      P.r1 = lastp ? M1 : X.h1;
-      P.r2 = lastp ? M2 : X.h2;
-      P.r3 = lastp ? M3 : X.h3;
-      P.r4 = lastp ? M4 : X.h4;
-      P.s1 = P.r1 * 5; P.s2 = P.r2 * 5; P.s3 = P.r3 * 5; P.s4 = P.r4 * 5;
-      poly_mul(P);
-      const uint32_t *c5 = parts[wv][start / 2 + j];
-      P.h0 += c5[0]; P.h1 += c5[1]; P.h2 += c5[2]; P.h3 += c5[3]; P.h4 += c5[4];
+  uint32_t ct32[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+  uint32_t tag[4] = {0u, 0u, 0u, 0u}, sample[4] = {0u, 0u, 0u, 0u};
+  if (fin) {
+    if (coop && SQ_QPAIR) {
+      // pairs: h = h r^c + E_j, c = 8 chunks for a whole pair, r^klast for a
+      // last pair of one block, r^(4 + klast) for one of two
+      const QRec &Rq = recs[wv][lane];
+      Poly R1;
+      R1.r0 = P.r0; R1.r1 = P.r1; R1.r2 = P.r2; R1.r3 = P.r3; R1.r4 = P.r4;
+      R1.s1 = P.s1; R1.s2 = P.s2; R1.s3 = P.s3; R1.s4 = P.s4;
+      Poly X;
+      X.r0 = Rq.r4[0]; X.r1 = Rq.r4[1]; X.r2 = Rq.r4[2]; X.r3 = Rq.r4[3]; X.r4 = Rq.r4[4];
+      X.s1 = X.r1 * 5; X.s2 = X.r2 * 5; X.s3 = X.r3 * 5; X.s4 = X.r4 * 5;
+      Poly Y = X;
+      X.h0 = X.r0; X.h1 = X.r1; X.h2 = X.r2; X.h3 = X.r3; X.h4 = X.r4;
+      poly_mul(X);  // r^8
+      Y.h0 = Rq.rl[0]; Y.h1 = Rq.rl[1]; Y.h2 = Rq.rl[2]; Y.h3 = Rq.rl[3]; Y.h4 = Rq.rl[4];
+      poly_mul(Y);  // r^(4 + klast)
+      const bool one = nblk & 1;  // the last pair holds one block
+      const uint32_t M0 = one ? Rq.rl[0] : Y.h0, M1 = one ? Rq.rl[1] : Y.h1,
+                     M2 = one ? Rq.rl[2] : Y.h2, M3 = one ? Rq.rl[3] : Y.h3,
+                     M4 = one ? Rq.rl[4] : Y.h4;
+      const uint32_t npair = nflat / 2;
+      for (uint32_t j = 0; j < npair; j++) {
+        const bool lastp = j + 1 == npair;
+        P.r0 = lastp ? M0 : X.h0;
+        P.r1 = lastp ? M1 : X.h1;
+        P.r2 = lastp ? M2 : X.h2;
+        P.r3 = lastp ? M3 : X.h3;
+        P.r4 = lastp ? M4 : X.h4;
+        P.s1 = P.r1 * 5; P.s2 = P.r2 * 5; P.s3 = P.r3 * 5; P.s4 = P.r4 * 5;
+        poly_mul(P);
+        const uint32_t *c5 = parts[wv][start / 2 + j];
+        P.h0 += c5[0]; P.h1 += c5[1]; P.h2 += c5[2]; P.h3 += c5[3]; P.h4 += c5[4];
+      }
+      // restore r for the lengths block
+      P.r0 = R1.r0; P.r1 = R1.r1; P.r2 = R1.r2; P.r3 = R1.r3; P.r4 = R1.r4;
+      P.s1 = R1.s1; P.s2 = R1.s2; P.s3 = R1.s3; P.s4 = R1.s4;
+#pragma unroll
+      for (int i = 0; i < 8; i++) ct32[i] = Rq.ct32[i];
+    } else if (coop) {
+      // r^1..r^4 as multipliers
+      Poly X = P, R1, R2, R3, R4;
+      X.h0 = P.r0; X.h1 = P.r1; X.h2 = P.r2; X.h3 = P.r3; X.h4 = P.r4;
+      poly_set_r(R1, X);
+      poly_mul(X);
+      poly_set_r(R2, X);
+      poly_mul(X);
+      poly_set_r(R3, X);
+      poly_mul(X);
+      poly_set_r(R4, X);
+      // the last block's multiplier r^klast, selected limb by limb
+      const uint32_t L0 = klast == 4 ? R4.r0 : klast == 3 ? R3.r0 : klast == 2 ? R2.r0 : R1.r0;
+      const uint32_t L1 = klast == 4 ? R4.r1 : klast == 3 ? R3.r1 : klast == 2 ? R2.r1 : R1.r1;
+      const uint32_t L2 = klast == 4 ? R4.r2 : klast == 3 ? R3.r2 : klast == 2 ? R2.r2 : R1.r2;
+      const uint32_t L3 = klast == 4 ? R4.r3 : klast == 3 ? R3.r3 : klast == 2 ? R2.r3 : R1.r3;
+      const uint32_t L4 = klast == 4 ? R4.r4 : klast == 3 ? R3.r4 : klast == 2 ? R2.r4 : R1.r4;
+      for (uint32_t b = 0; b < nblk; b++) {
+        const bool lastb = b + 1 == nblk;
+        P.r0 = lastb ? L0 : R4.r0;
+        P.r1 = lastb ? L1 : R4.r1;
+        P.r2 = lastb ? L2 : R4.r2;
+        P.r3 = lastb ? L3 : R4.r3;
+        P.r4 = lastb ? L4 : R4.r4;
+        P.s1 = P.r1 * 5; P.s2 = P.r2 * 5; P.s3 = P.r3 * 5; P.s4 = P.r4 * 5;
+        poly_mul(P);
+        const uint32_t *c5 = parts[wv][start + b];
+        P.h0 += c5[0]; P.h1 += c5[1]; P.h2 += c5[2]; P.h3 += c5[3]; P.h4 += c5[4];
+      }
+      // restore r for the lengths block
+      P.r0 = R1.r0; P.r1 = R1.r1; P.r2 = R1.r2; P.r3 = R1.r3; P.r4 = R1.r4;
+      P.s1 = R1.s1; P.s2 = R1.s2; P.s3 = R1.s3; P.s4 = R1.s4;
+#pragma unroll
+      for (int i = 0; i < 8; i++) ct32[i] = recs[wv][lane].ct32[i];
+    } else {
+      uint32_t okr[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) okr[i] = OB ? recs[wv][lane].okr[i] : 0u;
+      payload_pass<!OPEN, OB>(*K, nonce, src + hdr, dst + hdr, pl, P, ct32, okr);
     }
-    // restore r for the lengths block
-    P.r0 = R1.r0; P.r1 = R1.r1; P.r2 = R1.r2; P.r3 = R1.r3; P.r4 = R1.r4;
-    P.s1 = R1.s1; P.s2 = R1.s2; P.s3 = R1.s3; P.s4 = R1.s4;
-#pragma unroll
-    for (int i = 0; i < 8; i++) ct32[i] = Rq.ct32[i];
-  } else if (coop) {
-    // r^1..r^4 as multipliers
-    Poly X = P, R1, R2, R3, R4;
-    X.h0 = P.r0; X.h1 = P.r1; X.h2 = P.r2; X.h3 = P.r3; X.h4 = P.r4;
-    poly_set_r(R1, X);
-    poly_mul(X);
-    poly_set_r(R2, X);
-    poly_mul(X);
-    poly_set_r(R3, X);
-    poly_mul(X);
-    poly_set_r(R4, X);
-    // the last block's multiplier r^klast, selected limb by limb
-    const uint32_t L0 = klast == 4 ? R4.r0 : klast == 3 ? R3.r0 : klast == 2 ? R2.r0 : R1.r0;
-    const uint32_t L1 = klast == 4 ? R4.r1 : klast == 3 ? R3.r1 : klast == 2 ? R2.r1 : R1.r1;
-    const uint32_t L2 = klast == 4 ? R4.r2 : klast == 3 ? R3.r2 : klast == 2 ? R2.r2 : R1.r2;
-    const uint32_t L3 = klast == 4 ? R4.r3 : klast == 3 ? R3.r3 : klast == 2 ? R2.r3 : R1.r3;
-    const uint32_t L4 = klast == 4 ? R4.r4 : klast == 3 ? R3.r4 : klast == 2 ? R2.r4 : R1.r4;
-    for (uint32_t b = 0; b < nblk; b++) {
-      const bool lastb = b + 1 == nblk;
-      P.r0 = lastb ? L0 : R4.r0;
-      P.r1 = lastb ? L1 : R4.r1;
-      P.r2 = lastb ? L2 : R4.r2;
-      P.r3 = lastb ? L3 : R4.r3;
-      P.r4 = lastb ? L4 : R4.r4;
-      P.s1 = P.r1 * 5; P.s2 = P.r2 * 5; P.s3 = P.r3 * 5; P.s4 = P.r4 * 5;
-      poly_mul(P);
-      const uint32_t *c5 = parts[wv][start + b];
-      P.h0 += c5[0]; P.h1 += c5[1]; P.h2 += c5[2]; P.h3 += c5[3]; P.h4 += c5[4];
+    poly_lengths(P, hdr, pl);
+    poly_finish(P, otk, tag);
+    if (OPEN) {
+      const bool ok = ((tag[0] ^ rtag[0]) | (tag[1] ^ rtag[1]) | (tag[2] ^ rtag[2]) |
+                       (tag[3] ^ rtag[3])) == 0;
+      Q.out_len[p] = ok ? len - 16 : kQEAuth;
+      return;
     }
-    // restore r for the lengths block
-    P.r0 = R1.r0; P.r1 = R1.r1; P.r2 = R1.r2; P.r3 = R1.r3; P.r4 = R1.r4;
-    P.s1 = R1.s1; P.s2 = R1.s2; P.s3 = R1.s3; P.s4 = R1.s4;
+    if (OB) {
+      uint32_t k4[4], t4[4];
+      keywin(okey, len & 31, k4);
 #pragma unroll
-    for (int i = 0; i < 8; i++) ct32[i] = recs[wv][lane].ct32[i];
-  } else {
-    uint32_t okr[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) okr[i] = OB ? recs[wv][lane].okr[i] : 0u;
-    payload_pass<!OPEN, OB>(*K, nonce, src + hdr, dst + hdr, pl, P, ct32, okr);
-  }
-  poly_lengths(P, hdr, pl);
-  uint32_t tag[4];
-  poly_finish(P, otk, tag);
-  if (OPEN) {
-    const bool ok = ((tag[0] ^ rtag[0]) | (tag[1] ^ rtag[1]) | (tag[2] ^ rtag[2]) |
-                     (tag[3] ^ rtag[3])) == 0;
-    Q.out_len[p] = ok ? len - 16 : kQEAuth;
-    return;
-  }
-  if (OB) {
-    uint32_t k4[4], t4[4];
-    keywin(okey, len & 31, k4);
-#pragma unroll
-    for (int w = 0; w < 4; w++) t4[w] = tag[w] ^ k4[w];
-    store16(dst + len, t4, 16);
-    store16(wire, osalt, kSalamanderSalt);
-  } else {
-    store16(dst + len, tag, 16);
-  }
-  // header protection: sample = (ciphertext || tag)[4 - pn_len ..][0..16)
-  const uint32_t so = 4 - pn_len;
-  uint32_t sample[4];
-  if (pl >= so + 16) {
-#pragma unroll
-    for (int j = 0; j < 4; j++) sample[j] = __builtin_amdgcn_alignbyte(ct32[j + 1], ct32[j], so);
-  } else {  // short payload: the sample reaches into the tag
-    const uint32_t t8[8] = {tag[0], tag[1], tag[2], tag[3], 0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int j = 0; j < 4; j++) sample[j] = 0u;
-    for (uint32_t i = 0; i < 16; i++) {
-      const uint32_t k = so + i;
-      const uint32_t bb = k < pl ? byte32(ct32, k) : byte32(t8, k - pl);
-      sample[i >> 2] |= bb << (8 * (i & 3));
+      for (int w = 0; w < 4; w++) t4[w] = tag[w] ^ k4[w];
+      store16(dst + len, t4, 16);
+      store16(wire, osalt, kSalamanderSalt);
+    } else {
+      store16(dst + len, tag, 16);
     }
-  }
-  uint32_t m0, m1;
-  hp_mask(*K, sample, m0, m1);
+    // header protection: sample = (ciphertext || tag)[4 - pn_len ..][0..16)
+    const uint32_t so = 4 - pn_len;
+    if (pl >= so + 16) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) sample[j] = __builtin_amdgcn_alignbyte(ct32[j + 1], ct32[j], so);
+    } else {  // short payload: the sample reaches into the tag
+      const uint32_t t8[8] = {tag[0], tag[1], tag[2], tag[3], 0u, 0u, 0u, 0u};
+      for (uint32_t i = 0; i < 16; i++) {
+        const uint32_t k = so + i;
+        const uint32_t bb = k < pl ? byte32(ct32, k) : byte32(t8, k - pl);
+        sample[i >> 2] |= bb << (8 * (i & 3));
+      }
+    }
+  }  // fin
+  if (OPEN) return;
+  uint32_t m0 = 0u, m1 = 0u;
+  hp_mask_lanes<MULTI>(K, sample, fin, lane, m0, m1);  // every lane: lane pairs
+  if (!fin) return;
   // protected header bytes; with the fused layer also ^ the key byte of
   // their position
   const uint32_t kb0 = OB ? okey[0] & 0xFFu : 0u;
