@@ -6,7 +6,8 @@ usage: unit_sweep.py CONFIG "ppw ..." [ROUNDS] [obfuscate|deobfuscate]
 Tokens PPW[uU][lP][wW] (e.g. 16u6, 16u4l10240, 16w1) also set
 SQOBFS_DEV_U=U, SQOBFS_DEV_LDSPAD=P and SQOBFS_DEV_WPB=W (timing builds with
 SQ_DEVVAR: stream step of U blocks per lane, P bytes of extra LDS per
-workgroup, W waves per workgroup)."""
+workgroup, W waves per workgroup).  SWEEP_LAYOUT=slot16 runs bench.py's
+16-byte-slot layout (SQOBFS_FLAG_OUT_BLOCKS) instead of the dense one."""
 import os
 import re
 import statistics
@@ -27,22 +28,27 @@ rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 5
 deo = len(sys.argv) > 4 and sys.argv[4] == "deobfuscate"
 dev = torch.device("cuda", 0)
 kind, n, L, n_psk = bench.CONFIGS[cfg]
-sh = bench.build_shard(torch, dev, kind, n, L, n_psk, 0, 1, cfg, "dense")
+layout = os.environ.get("SWEEP_LAYOUT", "dense")
+sh = bench.build_shard(torch, dev, kind, n, L, n_psk, 0, 1, cfg, layout)
+ob = sqobfs.FLAG_OUT_BLOCKS if sh["slotted"] else 0
 ctx = sqobfs.Context(0)
 kr = sqobfs.Keyring(ctx, kind, sh["psks"])
 s = torch.cuda.current_stream(dev).cuda_stream
 b = sqobfs.make_batch(n, sh["data"], sh["in_off"], sh["lens"], sh["out"], sh["out_off"],
-                      sh["out_len"], sh["salt"], sh["psk_id"])
+                      sh["out_len"], sh["salt"], sh["psk_id"], flags=ob)
 d = sqobfs.OBFUSCATE
 alg = 2 * sh["payload_bytes"] + 2 * sh["S"] * n
 if deo:
     sqobfs.launch(ctx, kr, sqobfs.OBFUSCATE, b, s)
     wl = (sh["lens"] + sh["S"]).to(torch.int32)
     lens64 = sh["lens"].to(torch.int64)
-    back_off = torch.cumsum(lens64, 0) - lens64 + 64
-    back = torch.zeros(int(sh["payload_bytes"]) + 128, device=dev, dtype=torch.uint8)
+    if sh["slotted"]:  # decoded payloads into slots like the input's (as bench.py)
+        back_off, back = sh["in_off"], torch.zeros_like(sh["data"])
+    else:
+        back_off = torch.cumsum(lens64, 0) - lens64 + 64
+        back = torch.zeros(int(sh["payload_bytes"]) + 128, device=dev, dtype=torch.uint8)
     b = sqobfs.make_batch(n, sh["out"], sh["out_off"], wl, back, back_off, sh["out_len"], None,
-                          sh["psk_id"])
+                          sh["psk_id"], flags=ob)
     d = sqobfs.DEOBFUSCATE
     alg = 2 * sh["payload_bytes"] + sh["S"] * n
 
@@ -75,4 +81,4 @@ for r in range(rounds):
     print(f"round {r} done", flush=True)
 for w in ppws:
     med = statistics.median(res[w])
-    print(f"{cfg:24s} {'deo' if deo else 'obf'} ppw {w:>4s} median {med:8.1f} us  frac {alg / med / 8e6:.3f}  all {res[w]}")
+    print(f"{cfg:24s} {layout} {'deo' if deo else 'obf'} ppw {w:>4s} median {med:8.1f} us  frac {alg / med / 8e6:.3f}  all {res[w]}")
