@@ -11,17 +11,20 @@
 // Appendix A.3.  The CPU checker is oracle/oracle.c (or_quic_seal / open),
 // pinned by RFC 9001 Appendix A.5 and OpenSSL (tests/golden/quic.json).
 //
-// Decomposition: one lane per packet, 64 packets per wave.  Each lane walks
-// its packet once in 64-byte steps: one ChaCha20 keystream block (counter
-// 1..) XORs four 16-byte chunks, every ciphertext chunk goes straight into
-// the Poly1305 accumulator (26-bit limbs, v_mad_u64_u32 products), the tag
-// is appended, and the header-protection mask is taken from the sample of
-// the ciphertext still held in registers.  The input is read as aligned
-// 16-byte blocks one step ahead and realigned in registers, the output is
-// written as aligned 16-byte blocks (streaming realigner), so any packet
-// alignment costs one load and one store per 16 bytes.  VALU-heavy (~25K
-// instructions per 1350-byte packet): 64 independent packets per wave keep
-// every lane busy.
+// Decomposition (quic_kernel below): 32 packets per wave, three phases.
+//   1. owner lane per packet: descriptor, header protection off (open), the
+//      Poly1305 key block and the MAC over the header;
+//   2. all 64 lanes: the packets' 64-byte ChaCha20 keystream blocks
+//      (counter 1..) as one flat space, one block per lane per step, so
+//      consecutive lanes read and write consecutive bytes; each lane's four
+//      ciphertext chunks are Horner-ed into a partial MAC (26-bit limbs,
+//      v_mad_u64_u32 products) and lane pairs fold theirs;
+//   3. owner lane: the partials combined with powers of r, the tag, and
+//      (seal) the header-protection mask from the ciphertext sample.
+// The owner phases' ChaCha20 blocks are shared by lanes l and l + 32
+// (SQ_QSPLIT).  Payloads past the cooperative range are walked by their
+// owner lane with a streaming realigner (payload_pass): aligned 16-byte
+// loads one step ahead, realigned in registers, aligned 16-byte stores.
 #include <hip/hip_runtime.h>
 
 #include "sq_bytes.h"
