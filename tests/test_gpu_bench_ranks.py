@@ -1,0 +1,51 @@
+"""bench.py's multi-rank path on the one-GPU box: two ranks launched by
+torch.distributed.run share GPU 0 over gloo (RCCL refuses two ranks on one
+device; the driver's 1/2/4/8-GPU runs use nccl, one rank per GPU).  Covers
+what N > 1 adds to the single-GPU bench: the barrier-bracketed timing, the
+max over ranks, the whole-job sum of payload bytes, the parity AND over
+ranks, rank 0 printing one line, and configs[4]'s contiguous shards (strong
+scaling) next to the weak-scaling configs[1]."""
+from __future__ import annotations
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("config,packets,scaling", [("salamander-1m", 65536, "weak"),
+                                                    ("salamander-16m-256psk", 131072, "strong")])
+def test_bench_two_ranks(config, packets, scaling):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(REPO, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+           "--steps", "3", "--warmup", "1", "--warmup-s", "0", "--no-cpu-baseline",
+           "--config", config, "--packets", str(packets)]
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 3 and d["scaling"] == scaling
+    assert d["parity_spot_check"] is True
+    assert d["value"] > 0 and d["ms_per_step"] > 0
+    # whole-job payload over the max-over-ranks wall time
+    per_rank = packets if scaling == "weak" else packets // 2
+    total = 2 * per_rank * 1350 * d["steps"]
+    assert abs(d["value"] - total / (d["ms_per_step"] * d["steps"] * 1e-3) / 2**30) \
+        <= 0.01 * d["value"]  # ms_per_step is rounded to 0.1 us
+    assert d["config"]["packets_per_gpu"] == per_rank
