@@ -468,11 +468,22 @@ def inproc_bench(args):
         c.close()
 
 
+# Measured integer VALU ceiling (scripts/probe_valu.hip,
+# profiles/r03/valu/probe_valu.txt): v_add_u32 / v_xor_b32 / v_alignbit_b32
+# chains issue 0.633 T wave-instructions/s on the whole chip at 8 waves per
+# SIMD: 3.9 cycles per wave64 instruction per SIMD at the nominal 2.4 GHz
+# (the clock under load is not measured; packed f32 FMAs ran 4.8), about half
+# the rate of the 2-cycle figure the spec-based peak assumes.
+VALU_INT_MEASURED = 0.633e12
+
+
 def quic_valu_roofline(suite_name: str, op: str, kernel_us: float):
     """VALU roofline of a QUIC kernel from the committed PMC pass
     (profiles/r0N/quic/quic_pmc_summary.json, scripts/quic_pmc.sh): VALU
     wave-instructions per launch (SQ_INSTS_VALU) over this run's kernel time,
-    against 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction."""
+    against 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction
+    (`frac`) and against the measured integer issue rate
+    (`frac_of_measured_int_rate`)."""
     for rnd in ("r03", "r02"):  # the newest committed pass
         f = os.path.join(REPO, "profiles", rnd, "quic", "quic_pmc_summary.json")
         if os.path.exists(f):
@@ -492,6 +503,10 @@ def quic_valu_roofline(suite_name: str, op: str, kernel_us: float):
                     "valu_wave_instr_per_packet": round(valu / (1 << 20), 1),
                     "achieved": round(ach / 1e12, 4), "peak": round(peak / 1e12, 4),
                     "unit": "T wave-instr/s", "frac": round(ach / peak, 4),
+                    "measured_int_rate": VALU_INT_MEASURED / 1e12,
+                    "frac_of_measured_int_rate": round(ach / VALU_INT_MEASURED, 4),
+                    "measured_int_rate_source": "scripts/probe_valu.hip, "
+                                                "profiles/r03/valu/probe_valu.txt",
                     "source": os.path.relpath(f, REPO) + " (SQ_INSTS_VALU)"}
     return None
 
