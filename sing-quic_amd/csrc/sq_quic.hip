@@ -81,6 +81,10 @@ constexpr uint32_t kQMaxBlk = kQPpw * (kQCoopMax / 64);
 #endif
 static_assert((kQCoopMax / 64) % 2 == 0, "pairs: a packet's padded block count stays in range");
 static_assert(!(SQ_QPAIR && SQ_QPREFETCH), "the prefetching loop is not paired");
+// Junction stores (coop_block; the paired loop only)
+#ifndef SQ_QJUNC
+#define SQ_QJUNC 1
+#endif
 constexpr uint32_t kQParts = SQ_QPAIR ? kQMaxBlk / 2 : kQMaxBlk;
 
 // ---------------------------------------------------------------- Poly1305
@@ -463,9 +467,18 @@ __device__ __forceinline__ void coop_load(const QRec &R, uint32_t b, uint32_t (&
   }
 }
 
+// Junctions (SQ_QJUNC): the aligned output block a lane shares with the lane
+// holding the packet's next keystream block is written whole, once, by the
+// later lane (its head bytes OR the earlier lane's tail bytes, over a lane
+// shuffle) instead of as two byte-exact partial stores.  merge_head: this
+// lane's first output block is such a junction (skip it here; `head` = its
+// bytes [oa, 16), zero below); give_tail: its last one is (skip it; `tail` =
+// its bytes [0, oa), zero above).
 template <bool OPEN, bool OB>
 __device__ __forceinline__ void coop_block(const QuicKeyDev &K, QRec &R, uint32_t b,
-                                           const uint32_t (&blk)[5][4], uint32_t (&contrib)[5]) {
+                                           const uint32_t (&blk)[5][4], uint32_t (&contrib)[5],
+                                           bool merge_head, bool give_tail, uint32_t (&head)[4],
+                                           uint32_t (&tail)[4]) {
   uint32_t ks[16];
   chacha20_block(K.key, 1 + b, R.nonce, ks);
   const uint32_t off0 = 64 * b, nv = R.pl - off0 < 64 ? R.pl - off0 : 64;
@@ -512,7 +525,16 @@ __device__ __forceinline__ void coop_block(const QuicKeyDev &K, QRec &R, uint32_
     const uint32_t lo = j == 0 ? oa : 0u;
     const int hi_i = (int)(oa + nv) - 16 * (int)j;
     const uint32_t hi = hi_i < 16 ? (uint32_t)(hi_i > 0 ? hi_i : 0) : 16u;
-    if (hi > lo) {
+    if (j == 0) {
+#pragma unroll
+      for (int w = 0; w < 4; w++) head[w] = ob[w];
+    }
+    if (j == 4) {
+#pragma unroll
+      for (int w = 0; w < 4; w++) tail[w] = ob[w];
+    }
+    const bool skip = (j == 0 && merge_head) || (j == 4 && give_tail);
+    if (hi > lo && !skip) {
       if (lo == 0 && hi == 16) gst<u32x4>(D - oa + 16ull * j, u32x4{ob[0], ob[1], ob[2], ob[3]});
       else store_partial(D - oa + 16ull * j, ob, lo, hi);
     }
@@ -756,8 +778,8 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
     if (f < T) {
       QRec &R = recs[wv][pp];
       const QuicKeyDev &KB = MULTI ? Q.keys[R.kid] : Q.key0;
-      uint32_t c5[5];
-      coop_block<OPEN, OB>(KB, R, f - R.start, blk, c5);
+      uint32_t c5[5], h4[4], t4[4];
+      coop_block<OPEN, OB>(KB, R, f - R.start, blk, c5, false, false, h4, t4);
 #pragma unroll
       for (int i = 0; i < 5; i++) parts[wv][f][i] = c5[i];
     }
@@ -775,12 +797,32 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
     QRec &R = recs[wv][pp];
     const uint32_t b = f - R.start;
     uint32_t c5[5] = {0u, 0u, 0u, 0u, 0u};
+    uint32_t h4[4] = {0u, 0u, 0u, 0u}, t4[4] = {0u, 0u, 0u, 0u};
+    bool mh = false;
+    uint64_t jaddr = 0;
     if (f < T && b < R.nblk) {  // (b == nblk: an odd packet's padding block)
       const QuicKeyDev &KB = MULTI ? Q.keys[R.kid] : Q.key0;
+      // junctions: both neighbours in this step and in this packet, and the
+      // block whole inside the packet's output (a packet's last block may
+      // end inside it: the tag or another packet's bytes follow)
+      const uint32_t oa = (uint32_t)(R.dst & 15);
+      const uint32_t rem = R.pl - 64 * b, rem1 = rem > 64 ? rem - 64 : 0u;
+      mh = SQ_QJUNC && b > 0 && lane > 0 && oa + (rem < 64 ? rem : 64u) >= 16;
+      const bool gt = SQ_QJUNC && b + 1 < R.nblk && lane + 1 < kWave &&
+                      oa + (rem1 < 64 ? rem1 : 64u) >= 16;
+      jaddr = R.dst + 64ull * b - oa;
       uint32_t blk[5][4];
       coop_load(R, b, blk);
-      coop_block<OPEN, OB>(KB, R, b, blk, c5);
+      coop_block<OPEN, OB>(KB, R, b, blk, c5, mh, gt, h4, t4);
     }
+#if SQ_QJUNC
+    {  // the junction: this lane's head bytes | the previous lane's tail bytes
+      uint32_t pt[4];
+#pragma unroll
+      for (int w = 0; w < 4; w++) pt[w] = __shfl_up(t4[w], 1, kWave);
+      if (mh) gst<u32x4>(jaddr, u32x4{h4[0] | pt[0], h4[1] | pt[1], h4[2] | pt[2], h4[3] | pt[3]});
+    }
+#endif
     // the odd neighbour's partial (the same packet: pairs start even)
     uint32_t n5[5];
 #pragma unroll
@@ -808,9 +850,9 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
     if (f < T) {
       QRec &R = recs[wv][pp];
       const QuicKeyDev &KB = MULTI ? Q.keys[R.kid] : Q.key0;
-      uint32_t c5[5], blk[5][4];
+      uint32_t c5[5], blk[5][4], h4[4], t4[4];
       coop_load(R, f - R.start, blk);
-      coop_block<OPEN, OB>(KB, R, f - R.start, blk, c5);
+      coop_block<OPEN, OB>(KB, R, f - R.start, blk, c5, false, false, h4, t4);
 #pragma unroll
       for (int i = 0; i < 5; i++) parts[wv][f][i] = c5[i];
     }
