@@ -18,11 +18,14 @@ import (
 
 const xplusSaltLen = 16 // xplus.go:17
 
-// XPlusPacketConn: xplus.go:39-44.  Its salts come from the GPU's ChaCha20
-// generator instead of a mutex-guarded math/rand (xplus.go:26,34,67-69).
+// XPlusPacketConn: xplus.go:39-44.  Its salts come from the context's
+// ChaCha20 generator (on the GPU, or the same stream on the CPU path) instead
+// of a mutex-guarded math/rand (xplus.go:26,34,67-69).
 type XPlusPacketConn = sqobfs.Conn
 
-// NewXPlusPacketConn keeps xplus.go:19's signature.
+// NewXPlusPacketConn keeps xplus.go:19's signature and, like it, does not
+// fail for want of a GPU (the CPU path then does every batch); only a process
+// out of memory or threads panics here.
 func NewXPlusPacketConn(conn net.PacketConn, key []byte) net.PacketConn {
 	c, err := sqobfs.NewConn(conn, sqobfs.XPlus, key, sqobfs.Options{})
 	if err != nil {

@@ -4,7 +4,8 @@
 // hysteria2/salamander.go (which the maintainer tags `//go:build !sqobfs`)
 // with the same exported names and signatures, so the construction sites
 // (hysteria2/client.go:133-135, hysteria2/service.go:118-120) compile
-// unchanged.  Byte work: libsqobfs on the GPU, batched (go/sqobfs).
+// unchanged.  Byte work: libsqobfs on the GPU, batched (go/sqobfs), or on its
+// CPU path for small batches and when there is no GPU.
 // Uncompiled here (no Go toolchain in this image); the engine under
 // sqobfs.Conn is tested natively by tests/cpp/test_pconn.c.
 package hysteria2
@@ -25,8 +26,10 @@ const ObfsTypeSalamander = "salamander" // salamander.go:17
 // SalamanderPacketConn: salamander.go:19-22, the byte work on the GPU.
 type SalamanderPacketConn = sqobfs.Conn
 
-// NewSalamanderConn keeps salamander.go:24's signature.  There is no CPU
-// fallback: without a GPU it panics, as a misconfigured build should.
+// NewSalamanderConn keeps salamander.go:24's signature, and like it cannot
+// fail for want of a device: without a usable GPU the Conn runs every batch
+// on the library's CPU path (sqobfs.NewConn).  Only a process out of memory
+// or threads panics here, as the Go runtime itself would.
 func NewSalamanderConn(conn net.PacketConn, password []byte) net.PacketConn {
 	c, err := sqobfs.NewConn(conn, sqobfs.Salamander, password, sqobfs.Options{})
 	if err != nil {

@@ -23,11 +23,19 @@ import (
 // Options of a Conn.
 type Options struct {
 	Device    int           // GPU
+	NoGPU     bool          // every batch on the CPU path (also the fallback when the GPU cannot be opened)
 	Batch     int           // datagrams per launch at most (default 256)
 	SlotBytes int           // per-datagram slot (default 2048, hop.go:19)
-	Linger    time.Duration // an idle GPU waits this long for a batch to grow (default 0)
+	Linger    time.Duration // an idle engine waits this long for a batch to grow (default 0)
 	Pump      bool          // move datagrams through the wrapped conn even when it is a *net.UDPConn
 	NoOffload bool          // socket mode: no UDP GSO on send / GRO on receive
+	// CPUMax: batches costing at most this (payload bytes + 1 KiB per
+	// datagram) run on the CPU path, not a launch (0: 64 KiB; < 0: always launch)
+	CPUMax int
+	// InlineGap: a WriteTo made while the engine is idle, at least this long
+	// after the previous one, is obfuscated and sent on the calling goroutine
+	// and returns its own send error, as the reference's (0: 100 us; < 0: never)
+	InlineGap time.Duration
 }
 
 // Conn is the obfuscating net.PacketConn of SalamanderPacketConn
@@ -39,7 +47,13 @@ type Options struct {
 //     batch being filled and returns (p is never mutated, also not by the
 //     vectorised variants, unlike salamander.go:85-87); the engine obfuscates
 //     the batch in ONE launch (salts from the GPU's generator) as soon as it
-//     is idle and sends it.  A send error is returned by the next WriteTo.
+//     is idle and sends it, and a send error is returned by the next WriteTo.
+//     A WriteTo made while the engine is idle (a handshake, an ACK) is
+//     instead obfuscated on the CPU and sent by the calling goroutine, and
+//     returns its own send error, as the reference's (Options.InlineGap).
+//   - Small batches run on the CPU path (Options.CPUMax); with no usable GPU
+//     every batch does, so NewConn does not fail for want of a device, and a
+//     failed launch moves the engine to the CPU instead of failing the Conn.
 //   - ReadFrom (salamander.go:42-55, xplus.go:46-60) returns the next datagram
 //     of a batch the engine received and de-obfuscated in ONE launch, with
 //     the reference's lengths: for a datagram of w bytes and m = min(w,
@@ -60,7 +74,7 @@ type Options struct {
 type Conn struct {
 	net.PacketConn
 	kind Kind
-	ctx  *Context
+	ctx  *Context // nil: no GPU, every batch on the CPU path
 	kr   *Keyring
 	opt  Options
 
@@ -96,22 +110,57 @@ func (c *Conn) getErr(src *error, clear bool) error {
 	return e
 }
 
-// NewConn wraps conn; psk is the password (Salamander) or key (XPlus).
+// NewConn wraps conn; psk is the password (Salamander) or key (XPlus).  It
+// uses the GPU when one can be opened and the CPU path otherwise, so it
+// fails only when the process is out of memory or threads.
 func NewConn(conn net.PacketConn, kind Kind, psk []byte, opt Options) (*Conn, error) {
-	ctx, err := Shared(opt.Device)
-	if err != nil {
-		return nil, err
+	if !opt.NoGPU {
+		if c, err := newConn(conn, kind, psk, opt, true); err == nil {
+			return c, nil
+		}
 	}
-	kr, err := ctx.NewKeyring(kind, psk)
+	return newConn(conn, kind, psk, opt, false)
+}
+
+func newConn(conn net.PacketConn, kind Kind, psk []byte, opt Options, gpu bool) (*Conn, error) {
+	var ctx *Context
+	var kr *Keyring
+	var err error
+	if gpu {
+		if ctx, err = Shared(opt.Device); err != nil {
+			return nil, err
+		}
+		kr, err = ctx.NewKeyring(kind, psk)
+	} else {
+		kr, err = NewHostKeyring(kind, psk)
+	}
 	if err != nil {
-		ctx.Close()
+		if ctx != nil {
+			ctx.Close()
+		}
 		return nil, err
 	}
 	c := &Conn{PacketConn: conn, kind: kind, ctx: ctx, kr: kr, opt: opt}
+	var cc *C.sqobfs_ctx
+	if ctx != nil {
+		cc = ctx.c
+	}
 	var o C.sqobfs_pconn_opts
 	o.batch = C.uint32_t(opt.Batch)
 	o.slot_bytes = C.uint32_t(opt.SlotBytes)
 	o.linger_us = C.uint32_t(opt.Linger / time.Microsecond)
+	switch {
+	case opt.CPUMax < 0:
+		o.cpu_max = C.SQOBFS_PCONN_NEVER
+	case opt.CPUMax > 0:
+		o.cpu_max = C.uint32_t(opt.CPUMax)
+	}
+	switch {
+	case opt.InlineGap < 0:
+		o.inline_gap_us = C.SQOBFS_PCONN_NEVER
+	case opt.InlineGap > 0:
+		o.inline_gap_us = C.uint32_t((opt.InlineGap + time.Microsecond - 1) / time.Microsecond)
+	}
 	if !opt.NoOffload {
 		// UDP_SEGMENT / UDP_GRO, as quic-go uses on its own sockets
 		// (sys_conn_oob.go); the engine falls back if the socket refuses
@@ -123,7 +172,7 @@ func NewConn(conn net.PacketConn, kind Kind, psk []byte, opt Options) (*Conn, er
 		// uses a descriptor the runtime may have closed
 		if raw, e := uc.SyscallConn(); e == nil {
 			_ = raw.Control(func(fd uintptr) {
-				st = C.sqobfs_pconn_open(ctx.c, kr.kr, C.int(fd), &o, &c.pc)
+				st = C.sqobfs_pconn_open(cc, kr.kr, C.int(fd), &o, &c.pc)
 			})
 			c.socket = st == C.SQ_OK
 		}
@@ -131,11 +180,13 @@ func NewConn(conn net.PacketConn, kind Kind, psk []byte, opt Options) (*Conn, er
 	if !c.socket {
 		c.addrs = map[uint64]net.Addr{}
 		o.flags = 0 // offloads are socket mode's
-		st = C.sqobfs_pconn_open(ctx.c, kr.kr, -1, &o, &c.pc)
+		st = C.sqobfs_pconn_open(cc, kr.kr, -1, &o, &c.pc)
 	}
 	if err := check(st); err != nil {
 		kr.Close()
-		ctx.Close()
+		if ctx != nil {
+			ctx.Close()
+		}
 		return nil, err
 	}
 	if !c.socket {
@@ -228,7 +279,9 @@ func (c *Conn) putAddr(a net.Addr) uint64 {
 	c.addrMu.Lock()
 	c.tag++
 	t := c.tag
-	c.addrs[t] = a
+	if c.addrs != nil { // (nil after Close)
+		c.addrs[t] = a
+	}
 	c.addrMu.Unlock()
 	return t
 }
@@ -347,8 +400,15 @@ func (c *Conn) Close() error {
 		C.sqobfs_pconn_close(c.pc)
 		c.pc = nil
 		c.mu.Unlock()
+		// pump mode: addresses of datagrams that never reached a ReadFrom or
+		// the wrapped conn (queued at Close, or lost with a failed launch)
+		c.addrMu.Lock()
+		c.addrs = nil
+		c.addrMu.Unlock()
 		c.kr.Close()
-		c.ctx.Close()
+		if c.ctx != nil {
+			c.ctx.Close()
+		}
 	})
 	return c.cerr
 }

@@ -160,11 +160,12 @@ func (x *Context) unref() {
 // Close releases the reference Open or Shared returned.
 func (x *Context) Close() { x.unref() }
 
-// Keyring is the device copy of the PSK: the `password` captured by
+// Keyring is the copy of the PSK: the `password` captured by
 // NewSalamanderConn (salamander.go:19-40) or the `key` of NewXPlusPacketConn
-// (xplus.go:19-44).
+// (xplus.go:19-44) -- on the GPU with its host copy, or host only
+// (NewHostKeyring: no GPU needed).
 type Keyring struct {
-	ctx  *Context
+	ctx  *Context // nil: a host keyring
 	kr   *C.sqobfs_keyring
 	Kind Kind
 }
@@ -173,6 +174,26 @@ func (x *Context) NewKeyring(kind Kind, psk []byte) (*Keyring, error) {
 	if !x.ref() {
 		return nil, ErrClosed
 	}
+	kr, err := newKeyring(x.c, kind, psk)
+	if err != nil {
+		x.unref()
+		return nil, err
+	}
+	return &Keyring{ctx: x, kr: kr, Kind: kind}, nil
+}
+
+// NewHostKeyring makes a keyring that needs no GPU (sqobfs_keyring_create
+// with no context): the PSK's hash state on the host, for Conns on the CPU
+// path.
+func NewHostKeyring(kind Kind, psk []byte) (*Keyring, error) {
+	kr, err := newKeyring(nil, kind, psk)
+	if err != nil {
+		return nil, err
+	}
+	return &Keyring{kr: kr, Kind: kind}, nil
+}
+
+func newKeyring(c *C.sqobfs_ctx, kind Kind, psk []byte) (*C.sqobfs_keyring, error) {
 	// a private C copy: the reference's append(password, salt...) can write
 	// into the password's spare capacity (SURVEY.md section 5); this never does
 	blob := C.malloc(C.size_t(len(psk) + 1))
@@ -186,12 +207,11 @@ func (x *Context) NewKeyring(kind Kind, psk []byte) (*Keyring, error) {
 	defer C.free(unsafe.Pointer(ln))
 	*off, *ln = 0, C.uint32_t(len(psk))
 	var kr *C.sqobfs_keyring
-	if err := check(C.sqobfs_keyring_create(x.c, C.int(kind), 1, (*C.uint8_t)(blob), off, ln,
+	if err := check(C.sqobfs_keyring_create(c, C.int(kind), 1, (*C.uint8_t)(blob), off, ln,
 		&kr)); err != nil {
-		x.unref()
 		return nil, err
 	}
-	return &Keyring{ctx: x, kr: kr, Kind: kind}, nil
+	return kr, nil
 }
 
 // Close releases the keyring (sqobfs_keyring_destroy does not block: its
@@ -201,7 +221,9 @@ func (k *Keyring) Close() {
 	if k.kr != nil {
 		C.sqobfs_keyring_destroy(k.kr)
 		k.kr = nil
-		k.ctx.unref()
+		if k.ctx != nil {
+			k.ctx.unref()
+		}
 	}
 }
 

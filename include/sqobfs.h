@@ -64,7 +64,7 @@
 extern "C" {
 #endif
 
-#define SQOBFS_ABI_VERSION 4
+#define SQOBFS_ABI_VERSION 5
 
 #define SQOBFS_SALAMANDER_SALT_LEN 8 /* hysteria2/salamander.go:15 */
 #define SQOBFS_XPLUS_SALT_LEN 16     /* hysteria/xplus.go:17 */
@@ -207,18 +207,43 @@ uint32_t sqobfs_unit_packets_for(uint64_t bytes, uint32_t n, int multi_psk);
 /* Upload `count` pre-shared keys (host memory: psk k = blob[off[k] .. +len[k]])
  * and derive each one's per-PSK hash state on the GPU.  kind selects the
  * hash (BLAKE2b for Salamander, SHA-256 for XPlus).  Any PSK length works,
- * including 0.  Synchronous. */
+ * including 0.  Synchronous.  Every keyring also keeps the host copy of that
+ * state (sqobfs_cpu_run, the packet conn engine's CPU path).
+ * ctx == NULL makes a HOST keyring: no GPU is touched (none need exist); it
+ * serves sqobfs_cpu_run and packet conns opened without a context. */
 int sqobfs_keyring_create(sqobfs_ctx *ctx, int kind, uint32_t count,
                           const uint8_t *blob, const uint64_t *off,
                           const uint32_t *len, sqobfs_keyring **out);
 /* Does not block: the keyring's device memory is released in stream order
  * after the launches that used it (never waits for other keyrings' or
- * contexts' work).  The context must outlive its keyrings, and so must the
- * caller's streams the keyring was launched on (the release is ordered
- * after the work on each of them). */
+ * contexts' work).  The context must outlive its keyrings.  A caller's
+ * stream the keyring was launched on must either outlive the keyring or be
+ * released from it first with sqobfs_keyring_release_stream (the release is
+ * ordered after the work on each stream still listed). */
 void sqobfs_keyring_destroy(sqobfs_keyring *kr);
+/* The caller is about to destroy `stream`, on which it launched with kr:
+ * waits for the stream's work so far and drops it from kr's release fence,
+ * so sqobfs_keyring_destroy never touches the destroyed handle.  SQ_OK also
+ * when kr was never launched on it. */
+int sqobfs_keyring_release_stream(const sqobfs_keyring *kr, void *stream);
 int sqobfs_keyring_kind(const sqobfs_keyring *kr);
 uint32_t sqobfs_keyring_count(const sqobfs_keyring *kr);
+/* Test hook: compare the keyring's device hash state with its host copy
+ * (entry by entry, byte for byte).  Returns the number of entries that
+ * differ (0 = identical), or a negative status (SQ_EINVAL for a host
+ * keyring). */
+int sqobfs_debug_keyring_check(const sqobfs_keyring *kr);
+
+/* The same transform on the CPU, synchronously, on the calling thread: a
+ * batch in host memory with the semantics of a launch (every pointer a host
+ * pointer; per-packet results identical to the GPU's, out_len codes
+ * included).  SQOBFS_FLAG_DEVICE_SALT draws the salts from the keyring's
+ * context generator (the same ChaCha20 stream, consuming one sequence number
+ * as a launch does), or for a host keyring from a process generator keyed
+ * from getrandom(2).  Works with no GPU present.  The byte work of the
+ * reference's per-datagram ReadFrom / WriteTo (salamander.go:42-70,
+ * xplus.go:46-75) for callers with few datagrams. */
+int sqobfs_cpu_run(const sqobfs_keyring *kr, int dir, const sqobfs_batch *host_batch);
 
 /* Device-resident batch launches: asynchronous on `stream` (a hipStream_t
  * passed as void*; NULL = the HIP null stream, as in HIP itself).  All batch
@@ -547,25 +572,44 @@ typedef struct sqobfs_pconn_opts {
   uint32_t rx_batches; /* receive batches (0 = 3) */
   uint32_t linger_us;  /* an idle worker waits this long for a partly filled
                           batch to grow (0: launch at once) */
-  uint32_t spin_us;    /* workers poll a launch this long before blocking
-                          (0 = 200; they are dedicated threads) */
+  uint32_t spin_us;    /* a worker polls a launch at most this long before it
+                          blocks (0 = 200); the engine polls about twice the
+                          launches' recent completion time, within that bound */
   uint32_t flags;      /* socket mode: SQOBFS_UDP_TX_GSO (runs of equal-length
                           datagrams to one address go out as UDP_SEGMENT
                           messages; off by itself if the socket refuses) |
                           SQOBFS_UDP_RX_GRO (coalesced receives, split into
                           the batch) */
-  uint32_t reserved;
+  uint32_t cpu_max;    /* batches whose cost (payload bytes + 1024 per
+                          datagram, a key derivation's worth) is at most this
+                          run on the CPU path instead of a launch (0 = 65536;
+                          SQOBFS_PCONN_NEVER = always launch while the GPU
+                          works) */
+  uint32_t inline_gap_us; /* socket mode: a write made when the transmit side
+                          is idle and the previous write is at least this old
+                          is obfuscated on the CPU and sent on the writer's own
+                          thread, its send error returned by that same call, as
+                          the reference's WriteTo does (0 = 100;
+                          SQOBFS_PCONN_NEVER = every write is batched) */
 } sqobfs_pconn_opts;
+#define SQOBFS_PCONN_NEVER 0xFFFFFFFFu
 
 typedef struct sqobfs_pconn_stats {
   uint64_t tx_datagrams, tx_batches; /* obfuscated and handed to the socket / taker */
   uint64_t rx_datagrams, rx_batches; /* received and de-obfuscated */
   uint64_t rx_truncated;             /* datagrams longer than a slot (cut) */
-  uint64_t tx_send_errors;           /* datagrams the socket refused */
+  uint64_t tx_send_errors;           /* datagrams the socket refused (batched sends) */
   uint32_t tx_max_batch, rx_max_batch;
+  uint64_t cpu_batches;   /* batches (tx + rx) transformed on the CPU path */
+  uint64_t inline_writes; /* datagrams sent on the writer's thread (inline_gap_us) */
+  uint64_t gpu_failures;  /* launches that failed; the engine then stays on the CPU */
+  uint64_t dropped;       /* datagrams lost with a launch that failed after it started */
 } sqobfs_pconn_stats;
 
-/* kr's kind picks Salamander or XPlus.  ctx and kr must outlive the pconn. */
+/* kr's kind picks Salamander or XPlus.  ctx and kr must outlive the pconn.
+ * ctx == NULL (with a host keyring): no GPU; every batch runs on the CPU
+ * path, with the same results -- so a drop-in constructor never fails for
+ * want of a device (salamander.go:24-40 cannot fail). */
 int sqobfs_pconn_open(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int fd,
                       const sqobfs_pconn_opts *opts, sqobfs_pconn **out);
 /* Graceful stop (net.PacketConn.Close): later writes fail with SQ_ECLOSED;
@@ -578,7 +622,9 @@ void sqobfs_pconn_close(sqobfs_pconn *pc);
 /* WriteTo (salamander.go:57-70 / 81-93, xplus.go:62-75 / 86-98): queue the
  * payload p[0..len) for `to` (socket mode) with `tag`.  Returns SQ_OK, SQ_EINVAL
  * (longer than slot_bytes - S), SQ_ECLOSED, SQ_ETIMEDOUT (write deadline, while
- * every transmit batch is busy), or an earlier datagram's send error (once). */
+ * every transmit batch is busy), or a send error: an inline write's own
+ * (opts.inline_gap_us: the reference's behaviour), else that of an earlier
+ * batched datagram, reported once by the next write. */
 int sqobfs_pconn_write(sqobfs_pconn *pc, const uint8_t *p, uint32_t len, const sqobfs_addr *to,
                        uint64_t tag);
 /* ReadFrom (salamander.go:42-55, xplus.go:46-60) into p[0..cap): *n is what
@@ -623,6 +669,37 @@ int sqobfs_pconn_tx_done(sqobfs_pconn *pc);
 int sqobfs_pconn_stats_get(const sqobfs_pconn *pc, sqobfs_pconn_stats *out);
 /* live sqobfs_host_alloc blocks in the process (leak checks) */
 int64_t sqobfs_debug_host_allocs(void);
+
+/* The engine.  Every pconn of a context (ctx NULL: of the process's host
+ * engine) is served by ONE engine: a fixed pool of worker threads (each with
+ * its own HIP stream) that obfuscate / de-obfuscate and move the batches of
+ * all its pconns, one poller thread that watches their sockets (epoll), and a
+ * pool of batch blocks (page-locked and GPU-mapped with a context) that
+ * pconns take while they fill, transmit or hold unread datagrams and give
+ * back when done.  So opening more pconns -- a port-hopping client re-dials
+ * one per hop, hysteria/hop.go:114 -- adds no threads, and memory follows the
+ * datagrams in flight, not the number of pconns. */
+typedef struct sqobfs_engine_info {
+  uint32_t pconns;       /* open pconns */
+  uint32_t threads;      /* engine threads (workers + poller) */
+  uint32_t workers;
+  uint32_t pool_blocks;  /* batch blocks allocated (in use + free) */
+  uint64_t pool_bytes;
+  uint32_t blocks_in_use;
+  uint32_t gpu_disabled; /* 1 after a failed launch: every batch runs on the CPU */
+} sqobfs_engine_info;
+/* ctx NULL: the host engine.  SQ_OK with zeros when it was never started. */
+int sqobfs_engine_info_get(sqobfs_ctx *ctx, sqobfs_engine_info *out);
+/* Worker threads of the context's engine (0 = 4); only before its first
+ * pconn opens (SQ_EINVAL after). */
+int sqobfs_engine_set_workers(sqobfs_ctx *ctx, uint32_t workers);
+/* Free the pool's unused blocks; returns how many were freed. */
+int sqobfs_engine_trim(sqobfs_ctx *ctx);
+/* Test hook: the next `count` launches of every engine fail -- at submission
+ * (at_completion == 0: nothing ran; the batch is redone on the CPU) or when
+ * waited for (1: as a kernel that faulted; the batch is dropped) -- and the
+ * engines switch to the CPU path, as after a real device failure. */
+void sqobfs_debug_engine_fail(int count, int at_completion);
 
 #ifdef __cplusplus
 }

@@ -2,9 +2,11 @@
 //
 // Contexts (one per GPU), keyrings (the PSK captured by NewSalamanderConn /
 // NewXPlusPacketConn, hysteria2/salamander.go:24-40, hysteria/xplus.go:19-37),
-// device-resident batch launches and the host-staged path.  No hashing or
-// XOR happens on the host: every byte transform runs in sq_kernels.hip, and
-// a missing/failed GPU is reported as an error, never worked around.
+// device-resident batch launches and the host-staged path.  Every device
+// entry point runs its byte transform in sq_kernels.hip and reports a missing
+// or failed GPU as an error.  The one host transform is the explicit CPU
+// path (sqobfs_cpu_run, host keyrings; host/sq_cpu.cpp), which the packet
+// conn engine picks for small batches and when there is no working GPU.
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 #include <string.h>
@@ -20,6 +22,7 @@
 #include <vector>
 
 #include "../../include/sqobfs.h"
+#include "../host/sq_cpu.h"
 #include "sq_internal.h"
 
 struct sqobfs_ctx {
@@ -110,7 +113,7 @@ struct sqobfs_quic_keyring {
 };
 
 struct sqobfs_keyring {
-  sqobfs_ctx *ctx = nullptr;
+  sqobfs_ctx *ctx = nullptr;      // NULL: a host keyring (no device state)
   mutable KeyringUses uses;
   int kind = 0;
   uint32_t count = 0;
@@ -118,6 +121,7 @@ struct sqobfs_keyring {
   sq::PskEntry host0;             // entry 0, passed by value to the kernels
   uint32_t hot_m = 16;            // block-0 message words any entry needs
   uint32_t hot_iv = 0;            // 1: every entry starts from the hash's initial state
+  std::vector<sq::PskEntry> host; // the same state made on the host (sq_cpu.h)
 };
 
 namespace {
@@ -222,6 +226,36 @@ int sq_ctx_stream_wait(sqobfs_ctx *ctx, void *s, uint32_t spin_us) {
   const int st = sq_spin_wait(s, spin_us);
   if (st != 1) return st;
   return hip_status(hipStreamSynchronize((hipStream_t)s));
+}
+
+int sq_host_alloc_mapped(sqobfs_ctx *ctx, size_t bytes, void **out) {
+  const int st = sqobfs_host_alloc(ctx, bytes, out);
+  if (st != SQ_OK) return st;
+  void *dev = nullptr;  // the GPU's view of the block: the same address on ROCm
+  DeviceScope ds_(ctx->device);
+  if (hipHostGetDevicePointer(&dev, *out, 0) != hipSuccess || dev != *out) {
+    (void)hipGetLastError();
+    sqobfs_host_free(ctx, *out);
+    *out = nullptr;
+    return SQ_EDEVICE;
+  }
+  return SQ_OK;
+}
+
+const sq::PskEntry *sq_keyring_host(const sqobfs_keyring *kr, uint32_t *count) {
+  *count = kr->count;
+  return kr->host.data();
+}
+
+sqobfs_ctx *sq_keyring_ctx(const sqobfs_keyring *kr) { return kr->ctx; }
+
+void sq_salt_take(sqobfs_ctx *ctx, uint32_t key[8], uint64_t *seq) {
+  if (!ctx) {
+    sq_host_salt_take(key, seq);
+    return;
+  }
+  memcpy(key, ctx->salt_key, sizeof ctx->salt_key);
+  *seq = ctx->salt_seq.fetch_add(1);
 }
 
 // Default unit (packets per wavefront) of a device batch whose lengths the
@@ -504,6 +538,7 @@ int sqobfs_open(int device, sqobfs_ctx **out) {
 
 void sqobfs_close(sqobfs_ctx *ctx) {
   if (!ctx) return;
+  sq_engine_ctx_closed(ctx);  // its packet conn engine's threads and blocks
   DeviceScope ds_(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   (void)hipStreamSynchronize(ctx->rel);  // keyrings released before the context
@@ -606,19 +641,35 @@ void keyring_hot_words(int kind, uint32_t count, const uint32_t *len, uint32_t &
 
 int sqobfs_keyring_create(sqobfs_ctx *ctx, int kind, uint32_t count, const uint8_t *blob,
                           const uint64_t *off, const uint32_t *len, sqobfs_keyring **out) {
-  if (!ctx || !out || count == 0 || !off || !len) return SQ_EINVAL;
+  if (!out || count == 0 || !off || !len) return SQ_EINVAL;
   if (kind != SQOBFS_SALAMANDER && kind != SQOBFS_XPLUS) return SQ_EINVAL;
   *out = nullptr;
   size_t blob_bytes = 0;
   for (uint32_t k = 0; k < count; k++) blob_bytes = std::max<size_t>(blob_bytes, off[k] + len[k]);
   if (blob_bytes && !blob) return SQ_EINVAL;
-  DeviceScope ds_(ctx->device);
-  if (ds_.status != SQ_OK) return ds_.status;
   sqobfs_keyring *kr = new (std::nothrow) sqobfs_keyring();
   if (!kr) return SQ_ENOMEM;
   kr->ctx = ctx;
   kr->kind = kind;
   kr->count = count;
+  try {
+    kr->host.resize(count);
+  } catch (...) {
+    delete kr;
+    return SQ_ENOMEM;
+  }
+  for (uint32_t k = 0; k < count; k++)
+    sq::cpu::psk_prepare(kind, blob ? blob + off[k] : nullptr, len[k], &kr->host[k]);
+  if (!ctx) {  // a host keyring
+    kr->host0 = kr->host[0];
+    *out = kr;
+    return SQ_OK;
+  }
+  DeviceScope ds_(ctx->device);
+  if (ds_.status != SQ_OK) {
+    delete kr;
+    return ds_.status;
+  }
   keyring_hot_words(kind, count, len, kr->hot_m, kr->hot_iv);
   uint8_t *d_blob = nullptr;
   uint64_t *d_off = nullptr;
@@ -656,6 +707,10 @@ int sqobfs_keyring_create(sqobfs_ctx *ctx, int kind, uint32_t count, const uint8
 
 void sqobfs_keyring_destroy(sqobfs_keyring *kr) {
   if (!kr) return;
+  if (!kr->ctx) {
+    delete kr;
+    return;
+  }
   DeviceScope ds_(kr->ctx->device);
   // launches that used the table may still run: free it after them, in
   // stream order, without blocking (and without a device-wide sync)
@@ -667,9 +722,57 @@ void sqobfs_keyring_destroy(sqobfs_keyring *kr) {
 int sqobfs_keyring_kind(const sqobfs_keyring *kr) { return kr ? kr->kind : SQ_EINVAL; }
 uint32_t sqobfs_keyring_count(const sqobfs_keyring *kr) { return kr ? kr->count : 0; }
 
+int sqobfs_keyring_release_stream(const sqobfs_keyring *kr, void *stream) {
+  if (!kr) return SQ_EINVAL;
+  if (!kr->ctx || !stream) return SQ_OK;  // host keyring / the null stream (never destroyed)
+  DeviceScope ds_(kr->ctx->device);
+  if (ds_.status != SQ_OK) return ds_.status;
+  const int st = hip_status(hipStreamSynchronize((hipStream_t)stream));
+  kr->uses.forget((hipStream_t)stream);
+  return st;
+}
+
+int sqobfs_debug_keyring_check(const sqobfs_keyring *kr) {
+  if (!kr || !kr->ctx) return SQ_EINVAL;
+  DeviceScope ds_(kr->ctx->device);
+  if (ds_.status != SQ_OK) return ds_.status;
+  std::vector<sq::PskEntry> dev(kr->count);
+  hipStream_t s = kr->ctx->stream;
+  int st = hip_status(hipMemcpyAsync(dev.data(), kr->table, sizeof(sq::PskEntry) * kr->count,
+                                     hipMemcpyDeviceToHost, s));
+  if (st == SQ_OK) st = hip_status(hipStreamSynchronize(s));
+  if (st != SQ_OK) return st;
+  int bad = 0;
+  for (uint32_t k = 0; k < kr->count; k++)
+    if (memcmp(&dev[k], &kr->host[k], sizeof(sq::PskEntry)) != 0) bad++;
+  return bad;
+}
+
+int sqobfs_cpu_run(const sqobfs_keyring *kr, int dir, const sqobfs_batch *b) {
+  if (!kr || (dir != SQOBFS_OBFUSCATE && dir != SQOBFS_DEOBFUSCATE)) return SQ_EINVAL;
+  int st = check_batch_shape(b, dir);
+  if (st != SQ_OK || b->n == 0) return st;
+  std::vector<uint8_t> salts;
+  if (b->flags & SQOBFS_FLAG_DEVICE_SALT) {
+    const size_t S = salt_len(kr->kind);
+    uint32_t key[8];
+    uint64_t seq;
+    sq_salt_take(kr->ctx, key, &seq);
+    try {
+      salts.resize((size_t)b->n * S);
+    } catch (...) {
+      return SQ_ENOMEM;
+    }
+    sq::cpu::salt_stream(key, seq, salts.data(), salts.size());
+    if (b->salt_out) memcpy(b->salt_out, salts.data(), salts.size());
+  }
+  return sq::cpu::run_batch(kr->kind, dir, kr->host.data(), kr->count, b,
+                            salts.empty() ? nullptr : salts.data());
+}
+
 int sqobfs_launch(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir, const sqobfs_batch *b,
                   void *stream) {
-  if (!ctx || !kr || kr->ctx != ctx) return SQ_EINVAL;
+  if (!ctx || !kr || kr->ctx != ctx) return SQ_EINVAL;  // (host keyrings: sqobfs_cpu_run)
   if (dir != SQOBFS_OBFUSCATE && dir != SQOBFS_DEOBFUSCATE) return SQ_EINVAL;
   const int st = check_batch_shape(b, dir);
   if (st != SQ_OK || b->n == 0) return st;

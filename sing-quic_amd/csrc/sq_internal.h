@@ -166,6 +166,9 @@ struct QGParams {
 int sq_spin_wait(void *stream, uint32_t us);
 // packets per wavefront of a device batch of n packets (lengths unknown)
 uint32_t sq_unit_packets_default(uint32_t n);
+// ---- the device interface of the host engines (pconn.cpp, udp_batch.cpp).
+// Implemented by sq_api.hip; tests/cpp/sq_devstub.cpp implements the same
+// functions over a CPU "device" for the sanitizer builds (no HIP at all).
 // private streams of host engines (pconn.cpp) on a context's GPU
 struct sqobfs_ctx;
 int sq_ctx_stream_create(sqobfs_ctx *ctx, void **out);
@@ -175,6 +178,21 @@ int sq_ctx_stream_wait(sqobfs_ctx *ctx, void *s, uint32_t spin_us);
 // keyring's release fence (sqobfs_keyring_destroy)
 struct sqobfs_keyring;
 void sq_keyring_forget(const sqobfs_keyring *kr, void *s);
+// page-locked host memory the context's GPU reads and writes at the same
+// address (zero-copy batches); freed with sqobfs_host_free
+int sq_host_alloc_mapped(sqobfs_ctx *ctx, size_t bytes, void **out);
+// the keyring's host copy of its per-PSK state (sq_cpu.h), and its context
+// (NULL for a host keyring)
+const sq::PskEntry *sq_keyring_host(const sqobfs_keyring *kr, uint32_t *count);
+sqobfs_ctx *sq_keyring_ctx(const sqobfs_keyring *kr);
+// one sequence number of the context's salt stream (SQOBFS_FLAG_DEVICE_SALT)
+// and its key, for salts made on the host; ctx NULL: the process's host
+// generator (sq_cpu.cpp)
+void sq_salt_take(sqobfs_ctx *ctx, uint32_t key[8], uint64_t *seq);
+// the process's host salt generator (sq_cpu.cpp): random key, own sequence
+void sq_host_salt_take(uint32_t key[8], uint64_t *seq);
+// sqobfs_close: ends the context's packet conn engine (pconn.cpp)
+void sq_engine_ctx_closed(sqobfs_ctx *ctx);
 
 // launchers implemented in sq_quic_gcm.hip
 extern "C" int sq_launch_quic_gcm(int open, const sq::QGParams *qp, void *stream);

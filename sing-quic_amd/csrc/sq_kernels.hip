@@ -72,11 +72,6 @@ namespace sq {
 #ifndef SQ_ABLATE
 #define SQ_ABLATE 0
 #endif
-// Extra dynamic LDS per block in timing builds (bytes): pins the resident
-// blocks per CU when an ablation changes the register count.
-#ifndef SQ_LDSPAD
-#define SQ_LDSPAD 0
-#endif
 // 1: the first packet of a unit gives the blocks it owns in the 64-byte line
 // its output starts in to the previous unit's wave (which holds it as its
 // look-ahead lane), so no output line is written by two waves.
@@ -89,26 +84,9 @@ namespace sq {
 #ifndef SQ_ALIGN
 #define SQ_ALIGN 3
 #endif
-// 1: a stream step keeps only the LDS address of each block's keystream and
-// reads it when the block is stored (16 fewer VGPRs per U blocks in flight).
-#ifndef SQ_KLATE
-#define SQ_KLATE 0
-#endif
-// 1: the first stream step's loads are issued right after the plan, before
-// the contents (key and images), so they are in flight during the hash
-// (needs SQ_KLATE: the keystreams are read when the blocks are stored).
-#ifndef SQ_EARLY
-#define SQ_EARLY 0
-#endif
-static_assert(!SQ_EARLY || SQ_KLATE, "SQ_EARLY needs SQ_KLATE");
 // Flat blocks a unit's block map covers (its role bytes live in LDS).
 #ifndef SQ_MAPBLK
 #define SQ_MAPBLK 4096
-#endif
-// Timing builds (never shipped): extra kernel instantiations picked at run
-// time by SQOBFS_DEV_* variables, for in-process A/B comparisons.
-#ifndef SQ_DEVVAR
-#define SQ_DEVVAR 0
 #endif
 // 1: deobfuscate reads the salt with the head window (one round trip after
 // the descriptor instead of two); 0: a dependent salt load first (round 2)
@@ -156,7 +134,7 @@ extern "C" const char *sqobfs_build_info(void) {
   return "gfx950 obfs_kernel U=" SQ_STR(SQ_U) " default_ppw=" SQ_STR(SQ_PPW) " NT=" SQ_STR(SQ_NT)
          " minw=" SQ_STR(SQ_MINW) " wpb=2"
          " ablate=" SQ_STR(SQ_ABLATE) " donate=" SQ_STR(SQ_DONATE) " align=" SQ_STR(SQ_ALIGN)
-         " klate=" SQ_STR(SQ_KLATE) " early=" SQ_STR(SQ_EARLY) " map=" SQ_STR(SQ_MAPBLK)
+         " map=" SQ_STR(SQ_MAPBLK)
          " winsafe=" SQ_STR(SQ_WINSAFE) " xcd=" SQ_STR(SQ_XCD);
 }
 
@@ -565,9 +543,6 @@ __device__ __forceinline__ bool tail_from_window(uint64_t rs, uint64_t re) {
 // deobfuscate -0.8 / -1.1 %; Salamander deobfuscate +0.3 / +1.0 / +1.2 %;
 // the multi-PSK obfuscate +5.7 %.  SQ_WINSAFE=1: the two kernels that gain;
 // 2: every kernel; 0: none.
-#ifndef SQ_WINSAFE
-#define SQ_WINSAFE 1
-#endif
 template <int KIND, int DIR, bool MULTI>
 constexpr bool kWinSafe =
     SQ_WINSAFE == 2 || (SQ_WINSAFE == 1 && !MULTI && (KIND == 0) == (DIR == 0));
@@ -998,28 +973,16 @@ __device__ __forceinline__ uint32_t locate(uint32_t cst, uint32_t b0, uint32_t c
 // conditional store makes it fall back to draining).
 constexpr uint32_t kOffNone = 0xFFFFFFF0u;
 // cache-policy bits of the stream's buffer ops (gfx950: sc0 = 1, nt = 2,
-// sc1 = 16); SQ_AUXLD / SQ_AUXST override them in timing builds
-#ifdef SQ_AUXLD
-constexpr int kAuxLd = SQ_AUXLD;
-#else
+// sc1 = 16)
 constexpr int kAuxLd = (SQ_NT & 1) ? 2 : 0;  // nt
-#endif
-#ifdef SQ_AUXST
-constexpr int kAuxSt = SQ_AUXST;
-#else
 constexpr int kAuxSt = (SQ_NT & 2) ? 2 : 0;
-#endif
 
 // One stream step in flight: U blocks per lane with their keystreams (or
 // special values) and output offsets.
 template <int U>
 struct Step {
   u32x4 v[U];
-#if SQ_KLATE
-  uint32_t ka[U];  // byte offset of the block's keystream in the WaveLds
-#else
   u32x4 k[U];
-#endif
   uint32_t doff[U];
 };
 
@@ -1057,12 +1020,7 @@ __device__ __forceinline__ void stream_issue(const WaveLds &L, const WaveBufs &B
       const uint64_t se = *reinterpret_cast<const uint64_t *>(&R.sidx);
       idx[u] = c == (uint32_t)se ? 2u : (c >= (uint32_t)(se >> 32) ? 3u : (c & 1u));
     }
-#if SQ_KLATE
-    S.ka[u] = (uint32_t)(reinterpret_cast<const char *>(&R.tab[idx[u]]) -
-                         reinterpret_cast<const char *>(&L));
-#else
     S.k[u] = R.tab[idx[u]];
-#endif
   }
 #pragma unroll
   for (int u = 0; u < U; u++) {
@@ -1078,17 +1036,10 @@ __device__ __forceinline__ void stream_issue(const WaveLds &L, const WaveBufs &B
 template <int U>
 __device__ __forceinline__ void stream_store(const WaveLds &L, const WaveBufs &B,
                                              const Step<U> &S) {
-#if SQ_KLATE
-  u32x4 k[U];
+  (void)L;
 #pragma unroll
   for (int u = 0; u < U; u++)
-    k[u] = *reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>(&L) + S.ka[u]);
-#else
-  const u32x4(&k)[U] = S.k;
-#endif
-#pragma unroll
-  for (int u = 0; u < U; u++)
-    __builtin_amdgcn_raw_buffer_store_b128(S.v[u] ^ k[u], B.dst, S.doff[u], 0, kAuxSt);
+    __builtin_amdgcn_raw_buffer_store_b128(S.v[u] ^ S.k[u], B.dst, S.doff[u], 0, kAuxSt);
 }
 
 // Double-buffered stream loop.  The caller has issued step 0's loads into
@@ -1181,14 +1132,13 @@ __global__ __launch_bounds__(WPB * kWave) void obfs_kernel(const KParams P) {
   const UnitStream S = plan_unit(J, owner, lane, ppw, first != 0, ob, P.out_lines != 0, L, G);
   SQ_STAMP(2);
   Step<U> cur;
-  if (SQ_EARLY && S.fast && S.map) stream_issue<U, true>(L, S.B, S.cst, S.T, lane, 0, cur);
   const uint32_t pid = MULTI && d.pid < P.n_psk ? d.pid : 0u;
   // 2 + 3b. key and block contents
   fill_unit<KIND, DIR, MULTI>(P, J, salt, do_hash, pid, hot, W, owner, lane, ob, G, L);
   SQ_STAMP(3);
   // 4. the stream
   if (S.fast && S.map) {
-    if (!SQ_EARLY) stream_issue<U, true>(L, S.B, S.cst, S.T, lane, 0, cur);
+    stream_issue<U, true>(L, S.B, S.cst, S.T, lane, 0, cur);
     stream_loop<U, true>(L, S.B, S.cst, S.T, lane, cur);
   } else if (S.fast) {
     stream_issue<U, false>(L, S.B, S.cst, S.T, lane, 0, cur);
@@ -1288,11 +1238,11 @@ template <int KIND, int DIR>
 constexpr int kWavesPerGroup = 2;
 
 template <int KIND, int DIR, bool MULTI, int U, int WPB>
-static int launch_k(const KParams &P, uint32_t pad, hipStream_t s) {
+static int launch_k(const KParams &P, hipStream_t s) {
   const uint64_t units = ((uint64_t)P.n + P.ppw - 1) / P.ppw;
   const uint64_t blocks = (units + WPB - 1) / WPB;
   hipLaunchKernelGGL((obfs_kernel<KIND, DIR, MULTI, U, WPB>), dim3((uint32_t)blocks),
-                     dim3(WPB * kWave), pad, s, P);
+                     dim3(WPB * kWave), 0, s, P);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -1304,42 +1254,7 @@ static int launch_one(const KParams *kp, hipStream_t s) {
   if (P.ppw > kMaxUnitPackets) return -1;
   const uint64_t units = ((uint64_t)P.n + P.ppw - 1) / P.ppw;
   P.xcd = SQ_XCD < 0 ? (units >= kXcdMinUnits ? 1u : 0u) : (uint32_t)SQ_XCD;
-#if SQ_DEVVAR
-  // timing builds only, for in-process A/B: SQOBFS_DEV_WPB = 1 / 2 / 4 waves
-  // per workgroup (any kernel); SQOBFS_DEV_U another stream step size and
-  // SQOBFS_DEV_LDSPAD dynamic LDS per workgroup (caps the resident groups),
-  // both for Salamander obfuscate, single PSK (SQ_U sizes the map's slack)
-  {
-    const char *ew = getenv("SQOBFS_DEV_WPB");
-    const int wpb = ew ? atoi(ew) : 0;
-    const char *lp = getenv("SQOBFS_DEV_LDSPAD");
-    const uint32_t pad = lp ? (uint32_t)atoi(lp) : (uint32_t)SQ_LDSPAD;
-    if (wpb == 1) return launch_k<KIND, DIR, MULTI, U, 1>(P, pad, s);
-    if (wpb == 2) return launch_k<KIND, DIR, MULTI, U, 2>(P, pad, s);
-    if (wpb == 4) return launch_k<KIND, DIR, MULTI, U, 4>(P, pad, s);
-    if (KIND == 0 && DIR == 0 && !MULTI) {
-      const char *e = getenv("SQOBFS_DEV_U");
-      const int u = e ? atoi(e) : U;
-      constexpr int W = kWavesPerGroup<KIND, DIR>;
-#define SQ_DEV_U(UU)                                                          \
-  case UU:                                                                    \
-    if constexpr (UU <= SQ_U) /* the role map's slack covers SQ_U */          \
-      return launch_k<KIND, DIR, MULTI, UU, W>(P, pad, s);                    \
-    break;
-      switch (u) {
-        SQ_DEV_U(2)
-        SQ_DEV_U(3)
-        SQ_DEV_U(5)
-        SQ_DEV_U(6)
-        SQ_DEV_U(8)
-        default: break;
-      }
-#undef SQ_DEV_U
-    }
-    return launch_k<KIND, DIR, MULTI, U, kWavesPerGroup<KIND, DIR>>(P, pad, s);
-  }
-#endif
-  return launch_k<KIND, DIR, MULTI, U, kWavesPerGroup<KIND, DIR>>(P, SQ_LDSPAD, s);
+  return launch_k<KIND, DIR, MULTI, U, kWavesPerGroup<KIND, DIR>>(P, s);
 }
 
 }  // namespace sq

@@ -1,46 +1,69 @@
 // pconn.cpp -- the obfuscating packet conn engine (include/sqobfs.h,
-// "Obfuscating packet conn"): the batching core under the Go decorators
-// go/sqobfs.Conn, written here so that its behaviour (coalescing, deadlines,
-// shutdown, memory) is the same for every host language and is tested
-// natively (tests/cpp/test_pconn.c).
+// "Obfuscating packet conn" and "The engine"): the batching core under the
+// Go decorators go/sqobfs.Conn, written here so that its behaviour
+// (coalescing, deadlines, shutdown, memory, failure handling) is the same for
+// every host language and is tested natively (tests/cpp/test_pconn.c, on the
+// GPU and, over the CPU device of tests/cpp/sq_devstub.cpp, under ASan and
+// TSan).
 //
 // Reference: SalamanderPacketConn / XPlusPacketConn (hysteria2/salamander.go:
 // 19-109, hysteria/xplus.go:39-118) transform one datagram per ReadFrom /
-// WriteTo call on the caller's goroutine.  Here the per-call contract stays
-// (one datagram in or out per call, the reference's return values) and the
-// byte work moves into batches of page-locked, GPU-mapped slots, one kernel
-// launch per batch:
+// WriteTo call on the caller's goroutine, and cannot fail to be constructed.
+// Here the per-call contract stays (one datagram in or out per call, the
+// reference's return values) and the byte work moves into batches:
 //
-//   write()  -> fill batch --(full, or the worker is idle)--> tx worker:
-//               obfuscate in place (device salts) -> sendmmsg | tx_take
-//   recvmmsg | rx_push -> rx batch -> rx worker: deobfuscate in place ->
-//               ready queue -> read() copies one datagram out
+//   write()  -> fill batch --(full, or the engine is idle)--> worker:
+//               obfuscate in place -> sendmmsg | tx_take
+//   epoll -> worker: recvmmsg | rx_push -> rx batch -> deobfuscate in place
+//               -> ready queue -> read() copies one datagram out
 //
-// Natural batching: a worker takes whatever has accumulated as soon as it
-// is idle, so a lone packet (a handshake, an ACK) is launched at once and
-// the datagrams written during a launch form the next batch.  linger_us
-// trades latency for larger batches when asked.
+// ONE engine per context serves every pconn on it: a fixed pool of worker
+// threads (each with its own HIP stream), one poller thread (epoll over the
+// sockets) and a pool of batch blocks (page-locked, GPU-mapped) that pconns
+// take while a batch fills, flies or waits to be read, and give back after.
+// So pconns -- one per hop socket of a port-hopping client, hop.go:114 --
+// cost no threads of their own, and pinned memory follows the datagrams in
+// flight.
+//
+// Where the bytes are transformed, per batch:
+//   * on the GPU, one launch, when the batch's cost (payload bytes + 1 KiB
+//     per datagram) exceeds opts.cpu_max;
+//   * on the CPU (sq_cpu.h) otherwise, and always without a context (no GPU:
+//     the drop-in constructors never fail), and for good after a launch
+//     fails (a batch whose launch was refused is redone on the CPU; one whose
+//     kernel failed after it started is dropped, as a lost datagram);
+//   * inline: a write made while the transmit side is idle (and the previous
+//     write is opts.inline_gap_us old) is obfuscated and sent on the writer's
+//     own thread, and its send error is that call's -- the reference's
+//     behaviour, for handshakes, ACKs and keep-alives.
+// Natural batching: a worker takes whatever has accumulated as soon as it is
+// free, and the datagrams written during a launch form the next batch.
 #include <errno.h>
 #include <fcntl.h>
-#include <hip/hip_runtime.h>
 #include <netinet/in.h>
 #include <netinet/udp.h>
 #include <poll.h>
+#include <stdlib.h>
 #include <string.h>
+#include <sys/epoll.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <time.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
+#include <map>
 #include <mutex>
 #include <new>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
+#include "sq_cpu.h"
 #include "sq_internal.h"
 #include "sq_sockaddr.h"
 #include "sqobfs.h"
@@ -48,6 +71,10 @@
 namespace {
 
 constexpr uint32_t kDefBatch = 256, kDefSlot = 2048, kDefBatches = 3, kDefSpinUs = 200;
+constexpr uint32_t kDefCpuMax = 65536;    // cost: payload bytes + kHashCost per datagram
+constexpr uint32_t kHashCost = 1024;      // one key derivation ~ 1 KiB of XOR on a core
+constexpr uint32_t kDefInlineGapUs = 100;
+constexpr uint32_t kDefWorkers = 4, kMaxWorkers = 64;
 constexpr uint32_t kMaxBatch = 1u << 16;
 constexpr int64_t kDrainNs = 200'000'000;  // shutdown: time given to queued writes
 constexpr uint32_t kMmsg = 256;            // messages per sendmmsg / recvmmsg call
@@ -55,6 +82,10 @@ constexpr uint32_t kGsoMaxSegs = 64;       // UDP_MAX_SEGMENTS of older kernels
 constexpr uint32_t kGsoMaxBytes = 65000;   // one GSO send stays below 64 KiB of IP payload
 constexpr uint32_t kGroBuf = 65536;        // one coalesced receive
 constexpr size_t kCtlWords = (CMSG_SPACE(sizeof(uint16_t)) + 7) / 8;
+
+// sqobfs_debug_engine_fail
+std::atomic<int> g_fail_count{0};
+std::atomic<int> g_fail_at_completion{0};
 
 int64_t unix_ns() {
   timespec ts;
@@ -75,56 +106,78 @@ std::chrono::steady_clock::time_point mono_tp(int64_t ns) {
       std::chrono::duration_cast<std::chrono::steady_clock::duration>(std::chrono::nanoseconds(ns)));
 }
 
-// One batch: its slots and descriptor arrays live in the mapped block (the
-// kernel reads and writes them over PCIe), addresses and tags on the host.
-struct PBatch {
-  uint32_t n = 0;       // datagrams in the batch
-  uint32_t next = 0;    // rx: next datagram read() hands out
-  int64_t first_ns = 0; // monotonic time of the first datagram (linger)
+// One batch's memory, from the engine pool: the slots, then per datagram
+// two u64 and two u32 arrays (the kernel reads and writes them in place).
+struct Block {
+  void *mem = nullptr;
+  size_t bytes = 0;
+  uint32_t B = 0, slot = 0;
   uint8_t *slots = nullptr;
   uint64_t *in_off = nullptr, *out_off = nullptr;
   uint32_t *len = nullptr, *out_len = nullptr;
+};
+
+// One batch of a pconn.  Its block is taken from the pool when the batch
+// starts filling (or receiving) and given back when it is free again.
+struct PBatch {
+  Block *blk = nullptr;
+  uint32_t n = 0;       // datagrams in the batch
+  uint32_t next = 0;    // rx: next datagram read() hands out
+  int64_t first_ns = 0; // monotonic time of the first datagram (linger)
   std::vector<sqobfs_addr> addr;
   std::vector<uint64_t> tag;
   std::vector<uint8_t> head;  // rx: the first 16 wire bytes of each datagram
 };
 
+enum { kTx = 0, kRx = 1 };
+
+struct Engine;
+
 }  // namespace
 
 struct sqobfs_pconn {
+  Engine *eng = nullptr;
   sqobfs_ctx *ctx = nullptr;
   const sqobfs_keyring *kr = nullptr;
+  const sq::PskEntry *psk0 = nullptr;  // the keyring's host entry 0 (inline writes)
   int kind = 0;
   uint32_t S = 0;
-  int fd = -1;    // socket mode: our dup of the caller's socket
-  int wake = -1;  // eventfd, readable after shutdown (wakes poll)
+  uint64_t id = 0;  // the engine's handle (epoll data)
+  int fd = -1;      // socket mode: our dup of the caller's socket
+  int wake = -1;    // eventfd, readable after shutdown (wakes a blocked send)
   sqobfs_pconn_opts o{};
-  void *block = nullptr;
-  void *txs = nullptr, *rxs = nullptr;  // private streams
   std::vector<PBatch> tb, rb;
 
+  // ---- under mu
   std::mutex mu;
-  std::condition_variable cv_txw;   // tx worker: work arrived
   std::condition_variable cv_txs;   // writers: a tx batch freed; shutdown: drained
-  std::condition_variable cv_rxw;   // pump rx worker: work arrived
   std::condition_variable cv_rxr;   // readers: a batch is ready
-  std::condition_variable cv_rxs;   // rx worker / pushers: an rx batch freed
+  std::condition_variable cv_rxs;   // pushers: an rx batch freed
   std::condition_variable cv_take;  // pump taker: an obfuscated batch is ready
   std::deque<uint32_t> tfree, tq, ttaken, rfree, rq, rready;
   int tfill = -1, rfill = -1;
-  bool tx_busy = false;      // tx worker is launching / sending a batch
-  bool rx_busy = false;      // pump rx worker is launching
+  bool tx_busy = false;      // a worker is transforming / sending a tx batch
   bool taken = false;        // pump: the front of ttaken is out with the taker
+  bool inline_busy = false;  // a writer is sending inline
+  bool rx_stall = false;     // socket rx waits for a free batch (read() reschedules)
+  bool rx_dead = false;      // the socket failed for good: no more receives
   bool writes_closed = false;
   bool closed = false;
   int tx_err = 0;            // reported once by the next write
   int rx_err = 0;            // reported once the ready queue is empty
   bool rx_err_sticky = false;
   int64_t rdl = 0, wdl = 0;  // deadlines, unix ns (0 = none)
+  int64_t last_write_ns = 0;
   sqobfs_pconn_stats st{};
-  std::mutex join_mu;
-  std::thread txw, rxw;
-  // sendmmsg / recvmmsg scratch (owned by the tx / rx worker thread)
+  std::vector<uint8_t> ibuf;  // the inline writer's datagram
+
+  // ---- under eng->mu
+  bool sched[2] = {false, false};  // a tx / rx task is queued, timed or running
+  bool timed[2] = {false, false};  // ... waiting for its linger deadline
+  bool again[2] = {false, false};  // work arrived while it ran: run it once more
+  uint32_t tasks = 0;
+
+  // socket I/O scratch, used by the one task of each direction at a time
   std::vector<mmsghdr> tmsg, rmsg;
   std::vector<iovec> tiov, riov;
   std::vector<sockaddr_storage> tss, rss;
@@ -133,10 +186,39 @@ struct sqobfs_pconn {
   bool gso = false, gro = false;     // offloads in effect (socket mode)
 
   bool socket_mode() const { return fd >= 0; }
-  uint8_t *slot(PBatch &b, uint32_t i) { return b.slots + (size_t)i * o.slot_bytes; }
+  uint8_t *slot(PBatch &b, uint32_t i) { return b.blk->slots + (size_t)i * o.slot_bytes; }
 };
 
 namespace {
+
+struct Task {
+  sqobfs_pconn *pc;
+  int dir;  // kTx / kRx
+};
+
+struct Engine {
+  sqobfs_ctx *ctx = nullptr;  // NULL: the host engine (CPU only)
+  uint32_t nworkers = kDefWorkers;
+  std::mutex mu;
+  std::condition_variable cv;       // workers: a task is queued / a timer changed / stop
+  std::condition_variable cv_idle;  // a pconn's last task ended
+  std::deque<Task> runq;
+  std::vector<std::pair<int64_t, Task>> timers;  // linger deadlines (monotonic ns)
+  std::unordered_map<uint64_t, sqobfs_pconn *> byid;
+  uint64_t next_id = 1;
+  uint32_t pconns = 0;
+  bool stop = false;
+  std::vector<std::thread> threads;
+  std::vector<void *> streams;  // one per worker, made by that worker on first launch
+  int epfd = -1, wake = -1;
+  std::atomic<bool> gpu_off{false};
+  std::atomic<uint32_t> launch_us{40};  // recent launch completion time (EWMA)
+
+  std::mutex pool_mu;
+  std::map<std::pair<uint32_t, uint32_t>, std::vector<Block *>> free_blocks;
+  uint32_t blocks = 0, in_use = 0;
+  uint64_t pool_bytes = 0;
+};
 
 // ---- waiting on a condition with a deadline (unix ns, 0 = none): returns
 // false when the deadline has passed
@@ -155,25 +237,286 @@ bool wait_dl(std::unique_lock<std::mutex> &lk, std::condition_variable &cv, cons
   return true;
 }
 
-int launch_wait(sqobfs_pconn *pc, void *stream, int dir, PBatch &b, bool slotted = true) {
+// ---------------------------------------------------------------- registry
+
+std::mutex g_eng_mu;
+std::map<sqobfs_ctx *, Engine *> g_engines;     // ctx NULL: the host engine (never ended)
+std::map<sqobfs_ctx *, uint32_t> g_workers_cfg;  // sqobfs_engine_set_workers
+
+void worker_main(Engine *E, uint32_t w);
+void poller_main(Engine *E);
+
+Engine *engine_get(sqobfs_ctx *ctx, int *status) {
+  std::lock_guard<std::mutex> g(g_eng_mu);
+  auto it = g_engines.find(ctx);
+  if (it != g_engines.end()) return it->second;
+  Engine *E = new (std::nothrow) Engine();
+  if (!E) {
+    *status = SQ_ENOMEM;
+    return nullptr;
+  }
+  E->ctx = ctx;
+  auto c = g_workers_cfg.find(ctx);
+  if (c != g_workers_cfg.end() && c->second) E->nworkers = c->second;
+  E->streams.assign(E->nworkers, nullptr);
+  E->wake = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
+  E->epfd = epoll_create1(EPOLL_CLOEXEC);
+  epoll_event ev{};
+  ev.events = EPOLLIN;
+  ev.data.u64 = 0;  // id 0: the engine's wake fd
+  if (E->wake < 0 || E->epfd < 0 || epoll_ctl(E->epfd, EPOLL_CTL_ADD, E->wake, &ev) != 0) {
+    if (E->wake >= 0) close(E->wake);
+    if (E->epfd >= 0) close(E->epfd);
+    delete E;
+    *status = SQ_ENOMEM;
+    return nullptr;
+  }
+  try {
+    for (uint32_t w = 0; w < E->nworkers; w++) E->threads.emplace_back(worker_main, E, w);
+    E->threads.emplace_back(poller_main, E);
+  } catch (...) {
+    {
+      std::lock_guard<std::mutex> lk(E->mu);
+      E->stop = true;
+    }
+    E->cv.notify_all();
+    const uint64_t one = 1;
+    (void)!write(E->wake, &one, sizeof one);
+    for (auto &t : E->threads) t.join();
+    close(E->wake);
+    close(E->epfd);
+    delete E;
+    *status = SQ_ENOMEM;
+    return nullptr;
+  }
+  g_engines[ctx] = E;
+  return E;
+}
+
+// ---------------------------------------------------------------- block pool
+
+Block *block_take(Engine *E, uint32_t B, uint32_t slot) {
+  std::lock_guard<std::mutex> g(E->pool_mu);
+  auto &fl = E->free_blocks[{B, slot}];
+  if (!fl.empty()) {
+    Block *b = fl.back();
+    fl.pop_back();
+    E->in_use++;
+    return b;
+  }
+  Block *b = new (std::nothrow) Block();
+  if (!b) return nullptr;
+  const size_t slots = (size_t)B * slot, arrays = (size_t)B * (8 + 8 + 4 + 4);
+  b->bytes = slots + arrays;
+  if (E->ctx) {
+    if (sq_host_alloc_mapped(E->ctx, b->bytes, &b->mem) != SQ_OK) b->mem = nullptr;
+  } else {
+    b->mem = aligned_alloc(4096, (b->bytes + 4095) / 4096 * 4096);
+  }
+  if (!b->mem) {
+    delete b;
+    return nullptr;
+  }
+  uint8_t *p = (uint8_t *)b->mem;
+  b->B = B;
+  b->slot = slot;
+  b->slots = p;
+  p += slots;
+  b->in_off = (uint64_t *)p;
+  p += 8ull * B;
+  b->out_off = (uint64_t *)p;
+  p += 8ull * B;
+  b->len = (uint32_t *)p;
+  p += 4ull * B;
+  b->out_len = (uint32_t *)p;
+  E->blocks++;
+  E->in_use++;
+  E->pool_bytes += b->bytes;
+  return b;
+}
+
+void block_free_mem(Engine *E, Block *b) {
+  if (E->ctx) sqobfs_host_free(E->ctx, b->mem);
+  else free(b->mem);
+  delete b;
+}
+
+void block_give(Engine *E, Block *b) {
+  std::lock_guard<std::mutex> g(E->pool_mu);
+  E->in_use--;
+  E->free_blocks[{b->B, b->slot}].push_back(b);
+}
+
+// A batch's block, with the slot offsets of its direction: tx -- payload
+// behind S bytes of headroom, wire = salt || payload in place from the slot
+// start (the vectorised writers' layout, salamander.go:81-93); rx -- wire at
+// the slot start, payload decoded in place behind the salt.
+bool batch_attach(sqobfs_pconn *pc, PBatch &b, bool tx) {
+  if (!b.blk) {
+    b.blk = block_take(pc->eng, pc->o.batch, pc->o.slot_bytes);
+    if (!b.blk) return false;
+  }
+  for (uint32_t i = 0; i < pc->o.batch; i++) {
+    const uint64_t s0 = (uint64_t)i * pc->o.slot_bytes;
+    b.blk->in_off[i] = tx ? s0 + pc->S : s0;
+    b.blk->out_off[i] = tx ? s0 : s0 + pc->S;
+  }
+  return true;
+}
+
+void batch_detach(sqobfs_pconn *pc, PBatch &b) {
+  if (b.blk) block_give(pc->eng, b.blk);
+  b.blk = nullptr;
+  b.n = 0;
+  b.next = 0;
+}
+
+// ---------------------------------------------------------------- scheduling
+
+// Queue the pconn's task of direction d unless one is queued, timed or
+// running; a running one is told to run once more (`again`), so work that
+// arrives while it finishes is never left behind.  Caller holds eng->mu.
+void schedule_locked(Engine *E, sqobfs_pconn *pc, int d) {
+  if (pc->sched[d]) {
+    if (pc->timed[d]) {  // more work than the linger waits for: run now
+      for (size_t k = 0; k < E->timers.size(); k++)
+        if (E->timers[k].second.pc == pc && E->timers[k].second.dir == d) {
+          E->timers.erase(E->timers.begin() + (long)k);
+          break;
+        }
+      pc->timed[d] = false;
+      E->runq.push_back({pc, d});
+      E->cv.notify_one();
+    } else {
+      pc->again[d] = true;
+    }
+    return;
+  }
+  pc->sched[d] = true;
+  pc->tasks++;
+  E->runq.push_back({pc, d});
+  E->cv.notify_one();
+}
+
+// Caller holds pc->mu (lock order: pc->mu, then eng->mu).
+void schedule(sqobfs_pconn *pc, int d) {
+  std::lock_guard<std::mutex> lk(pc->eng->mu);
+  schedule_locked(pc->eng, pc, d);
+}
+
+// The running task of direction d is done with the work it found: requeue
+// (more work), park until `due` (linger), or end.  Caller holds pc->mu.
+void task_end(sqobfs_pconn *pc, int d, bool more, int64_t due = 0) {
+  Engine *E = pc->eng;
+  std::lock_guard<std::mutex> lk(E->mu);
+  if (pc->again[d]) {  // scheduled while running: look at once
+    pc->again[d] = false;
+    more = true;
+    due = 0;
+  }
+  if (more && !pc->closed) {
+    if (due) {
+      pc->timed[d] = true;
+      E->timers.push_back({due, {pc, d}});
+    } else {
+      E->runq.push_back({pc, d});
+    }
+    E->cv.notify_one();
+    return;
+  }
+  pc->sched[d] = false;
+  pc->tasks--;
+  if (pc->tasks == 0) E->cv_idle.notify_all();
+}
+
+// ---------------------------------------------------------------- transform
+
+// The batch's bytes, GPU or CPU (module comment).  Returns SQ_OK, or an
+// error when the batch is lost (a launch that failed after it started);
+// *cpu / *failed report what happened, for the pconn's stats.
+int transform(Engine *E, uint32_t w, sqobfs_pconn *pc, int dir, PBatch &b, bool slotted,
+              bool *cpu, bool *failed) {
+  *cpu = false;
+  *failed = false;
+  Block &k = *b.blk;
   sqobfs_batch d;
   memset(&d, 0, sizeof d);
   d.n = b.n;
-  // slots are multiples of 16 bytes: every output owns its blocks, so the
-  // kernel writes them whole (SQOBFS_FLAG_OUT_BLOCKS); GRO buffers pack the
-  // datagrams back to back (no flag)
-  d.flags = (slotted ? SQOBFS_FLAG_OUT_BLOCKS : 0u) |
-            (dir == SQOBFS_OBFUSCATE ? SQOBFS_FLAG_DEVICE_SALT : 0u);
-  d.in = b.slots;
-  d.in_off = b.in_off;
-  d.in_len = b.len;
-  d.out = b.slots;
-  d.out_off = b.out_off;
-  d.out_len = b.out_len;
-  const int st = sqobfs_launch(pc->ctx, pc->kr, dir, &d, stream);
-  if (st != SQ_OK) return st;
-  return sq_ctx_stream_wait(pc->ctx, stream, pc->o.spin_us);
+  d.in = k.slots;
+  d.in_off = k.in_off;
+  d.in_len = k.len;
+  d.out = k.slots;
+  d.out_off = k.out_off;
+  d.out_len = k.out_len;
+  uint64_t cost = 0;
+  for (uint32_t i = 0; i < b.n; i++) cost += k.len[i] + kHashCost;
+  const uint32_t cmax = pc->o.cpu_max;
+  const bool want_gpu = E->ctx && !E->gpu_off.load(std::memory_order_relaxed) &&
+                        (cmax == SQOBFS_PCONN_NEVER || cost > cmax);
+  if (want_gpu) {
+    // slots are multiples of 16 bytes: every output owns its blocks, so the
+    // kernel writes them whole (SQOBFS_FLAG_OUT_BLOCKS); GRO buffers pack the
+    // datagrams back to back (no flag)
+    d.flags = (slotted ? SQOBFS_FLAG_OUT_BLOCKS : 0u) |
+              (dir == SQOBFS_OBFUSCATE ? SQOBFS_FLAG_DEVICE_SALT : 0u);
+    int st = SQ_OK;
+    if (!E->streams[w]) {  // (only worker w writes its slot; close reads it under mu)
+      void *s = nullptr;
+      st = sq_ctx_stream_create(E->ctx, &s);
+      std::lock_guard<std::mutex> lk(E->mu);
+      E->streams[w] = s;
+    }
+    int inject = 0;
+    for (int c = g_fail_count.load(); c > 0;)
+      if (g_fail_count.compare_exchange_weak(c, c - 1)) {
+        inject = g_fail_at_completion.load() ? 2 : 1;
+        break;
+      }
+    const int64_t t0 = mono_ns();
+    if (st == SQ_OK) st = inject == 1 ? SQ_EDEVICE : sqobfs_launch(E->ctx, pc->kr, dir, &d, E->streams[w]);
+    if (st != SQ_OK) {
+      // refused before anything ran: the batch is intact, redo it on the CPU
+      E->gpu_off.store(true);
+      *failed = true;
+    } else {
+      const uint32_t ew = E->launch_us.load(std::memory_order_relaxed);
+      const uint32_t spin = std::min<uint32_t>(pc->o.spin_us, 2 * ew + 20);
+      st = sq_ctx_stream_wait(E->ctx, E->streams[w], spin);
+      if (inject == 2) st = SQ_EDEVICE;
+      if (st != SQ_OK) {
+        // the kernel ran, in place, and failed: the slots' state is unknown
+        E->gpu_off.store(true);
+        *failed = true;
+        return st;
+      }
+      const uint32_t us = (uint32_t)std::min<int64_t>((mono_ns() - t0) / 1000, 100000);
+      E->launch_us.store((7 * ew + us) / 8, std::memory_order_relaxed);
+      return SQ_OK;
+    }
+  }
+  // the CPU path (sq_cpu.h): salts of the context's stream, as a launch's
+  *cpu = true;
+  uint32_t count = 0;
+  const sq::PskEntry *tab = sq_keyring_host(pc->kr, &count);
+  uint8_t sbuf[64 * 16];
+  std::vector<uint8_t> sv;
+  uint8_t *salts = nullptr;
+  if (dir == SQOBFS_OBFUSCATE) {
+    const size_t bytes = (size_t)b.n * pc->S;
+    salts = sbuf;
+    if (bytes > sizeof sbuf) {
+      sv.resize(bytes);
+      salts = sv.data();
+    }
+    uint32_t key[8];
+    uint64_t seq;
+    sq_salt_take(E->ctx, key, &seq);
+    sq::cpu::salt_stream(key, seq, salts, bytes);
+  }
+  return sq::cpu::run_batch(pc->kind, dir, tab, count, &d, salts);
 }
+
+// ---------------------------------------------------------------- sending
 
 // sendmmsg of a transmitted batch.  With GSO, consecutive datagrams to one
 // address whose lengths are equal (the last of a run may be shorter) go out
@@ -185,24 +528,24 @@ int launch_wait(sqobfs_pconn *pc, void *stream, int dir, PBatch &b, bool slotted
 // its error is reported by the next write.  SQ_ECLOSED when shutdown
 // interrupts a wait for socket space.
 int send_batch(sqobfs_pconn *pc, PBatch &b, uint32_t from, int *first_err, uint64_t *errors) {
-  // messages over datagrams [from, n)
+  const Block &k = *b.blk;
   uint32_t nm = 0;
   for (uint32_t i = from; i < b.n;) {
     uint32_t j = i + 1;
     if (pc->gso) {
-      const uint32_t g = b.out_len[i];
+      const uint32_t g = k.out_len[i];
       uint32_t bytes = g;
-      while (j < b.n && j - i < kGsoMaxSegs && g > 0 && b.out_len[j] <= g && b.out_len[j] > 0 &&
-             bytes + b.out_len[j] <= kGsoMaxBytes &&
+      while (j < b.n && j - i < kGsoMaxSegs && g > 0 && k.out_len[j] <= g && k.out_len[j] > 0 &&
+             bytes + k.out_len[j] <= kGsoMaxBytes &&
              memcmp(&b.addr[j], &b.addr[i], sizeof b.addr[i]) == 0) {
-        bytes += b.out_len[j];
+        bytes += k.out_len[j];
         j++;
-        if (b.out_len[j - 1] < g) break;
+        if (k.out_len[j - 1] < g) break;
       }
     }
-    for (uint32_t k = i; k < j; k++) {
-      pc->tiov[k].iov_base = pc->slot(b, k);
-      pc->tiov[k].iov_len = b.out_len[k];
+    for (uint32_t q = i; q < j; q++) {
+      pc->tiov[q].iov_base = pc->slot(b, q);
+      pc->tiov[q].iov_len = k.out_len[q];
     }
     mmsghdr &h = pc->tmsg[nm];
     memset(&h, 0, sizeof h);
@@ -219,7 +562,7 @@ int send_batch(sqobfs_pconn *pc, PBatch &b, uint32_t from, int *first_err, uint6
       cm->cmsg_level = SOL_UDP;
       cm->cmsg_type = UDP_SEGMENT;
       cm->cmsg_len = CMSG_LEN(sizeof(uint16_t));
-      const uint16_t gs = (uint16_t)b.out_len[i];
+      const uint16_t gs = (uint16_t)k.out_len[i];
       memcpy(CMSG_DATA(cm), &gs, sizeof gs);
     }
     pc->tfirst[nm++] = i;
@@ -227,8 +570,8 @@ int send_batch(sqobfs_pconn *pc, PBatch &b, uint32_t from, int *first_err, uint6
   }
   uint32_t done = 0;
   while (done < nm) {
-    const uint32_t k = std::min(nm - done, kMmsg);
-    const int m = sendmmsg(pc->fd, &pc->tmsg[done], k, MSG_DONTWAIT);
+    const uint32_t c = std::min(nm - done, kMmsg);
+    const int m = sendmmsg(pc->fd, &pc->tmsg[done], c, MSG_DONTWAIT);
     if (m < 0) {
       const int e = errno;
       if (e == EINTR) continue;
@@ -253,235 +596,382 @@ int send_batch(sqobfs_pconn *pc, PBatch &b, uint32_t from, int *first_err, uint6
   return SQ_OK;
 }
 
-// ---- transmit worker: socket mode sends, pump mode hands to the taker
-void tx_worker(sqobfs_pconn *pc) {
-  std::unique_lock<std::mutex> lk(pc->mu);
-  for (;;) {
-    // wait for a queued batch, or promote the filling one (at once, or after
-    // linger_us from its first datagram)
-    for (;;) {
-      if (pc->closed) return;
-      if (!pc->tq.empty()) break;
-      if (pc->tfill >= 0 && pc->tb[pc->tfill].n > 0) {
-        const int64_t due = pc->tb[pc->tfill].first_ns + (int64_t)pc->o.linger_us * 1000;
-        if (pc->o.linger_us == 0 || pc->writes_closed || mono_ns() >= due) {
-          pc->tq.push_back((uint32_t)pc->tfill);
-          pc->tfill = -1;
-          break;
-        }
-        pc->cv_txw.wait_until(lk, mono_tp(due));
-        continue;
-      }
-      pc->cv_txw.wait(lk);
-    }
-    const uint32_t idx = pc->tq.front();
-    pc->tq.pop_front();
-    pc->tx_busy = true;
-    PBatch &b = pc->tb[idx];
-    lk.unlock();
-    int st = launch_wait(pc, pc->txs, SQOBFS_OBFUSCATE, b);
-    int send_err = 0;
-    uint64_t nerr = 0;
-    if (st == SQ_OK && pc->socket_mode()) st = send_batch(pc, b, 0, &send_err, &nerr);
-    lk.lock();
-    pc->tx_busy = false;
-    if (st != SQ_OK && st != SQ_ECLOSED && !pc->tx_err) pc->tx_err = st;
-    if (send_err && !pc->tx_err) pc->tx_err = send_err;
-    pc->st.tx_send_errors += nerr;
-    if (st == SQ_OK) {
-      pc->st.tx_datagrams += b.n;
-      pc->st.tx_batches++;
-      pc->st.tx_max_batch = std::max(pc->st.tx_max_batch, b.n);
-    }
-    if (st == SQ_OK && !pc->socket_mode()) {
-      pc->ttaken.push_back(idx);
-      pc->cv_take.notify_one();
-    } else {
-      b.n = 0;
-      pc->tfree.push_back(idx);
-      pc->cv_txs.notify_all();
-    }
-  }
+// Transform bookkeeping shared by the tasks (under pc->mu).
+void note_transform(sqobfs_pconn *pc, bool cpu, bool failed, int st, uint32_t n) {
+  if (cpu) pc->st.cpu_batches++;
+  if (failed) pc->st.gpu_failures++;
+  if (st != SQ_OK) pc->st.dropped += n;
 }
 
-// ---- receive worker, socket mode: recvmmsg a batch, deobfuscate, publish
-void rx_worker_socket(sqobfs_pconn *pc) {
-  for (;;) {
-    uint32_t idx;
-    {
-      std::unique_lock<std::mutex> lk(pc->mu);
-      pc->cv_rxs.wait(lk, [&] { return pc->closed || !pc->rfree.empty(); });
-      if (pc->closed) return;
-      idx = pc->rfree.front();
-      pc->rfree.pop_front();
+// ---------------------------------------------------------------- tasks
+
+// Transmit: the next queued batch (or the filling one, once its linger is
+// due) -> transform -> sendmmsg (socket mode) or the pump taker.
+void tx_task(Engine *E, uint32_t w, sqobfs_pconn *pc) {
+  std::unique_lock<std::mutex> lk(pc->mu);
+  if (pc->closed) return task_end(pc, kTx, false);
+  if (pc->tq.empty()) {
+    if (pc->tfill >= 0 && pc->tb[pc->tfill].n > 0) {
+      const int64_t due = pc->tb[pc->tfill].first_ns + (int64_t)pc->o.linger_us * 1000;
+      if (pc->o.linger_us && !pc->writes_closed && mono_ns() < due)
+        return task_end(pc, kTx, true, due);
+      pc->tq.push_back((uint32_t)pc->tfill);
+      pc->tfill = -1;
+    } else {
+      return task_end(pc, kTx, false);
     }
-    PBatch &b = pc->rb[idx];
-    int m = 0;
-    // GRO: the batch's slot region as 64 KiB buffers of up to 64 coalesced
-    // datagrams each (so the batch arrays always have room)
-    const uint32_t ngro = pc->gro ? std::max<uint32_t>(1, std::min<uint64_t>(
-                                        (uint64_t)pc->o.batch * pc->o.slot_bytes / kGroBuf,
-                                        pc->o.batch / kGsoMaxSegs))
-                                  : 0;
-    for (;;) {
-      pollfd p[2] = {{pc->fd, POLLIN, 0}, {pc->wake, POLLIN, 0}};
-      const int r = poll(p, 2, -1);
-      if (r < 0 && errno == EINTR) continue;
-      if (p[1].revents & POLLIN) return;  // shutdown
-      const uint32_t want = pc->gro ? ngro : pc->o.batch;
-      for (uint32_t j = 0; j < want; j++) {
-        pc->riov[j].iov_base = pc->gro ? b.slots + (size_t)j * kGroBuf : pc->slot(b, j);
-        pc->riov[j].iov_len = pc->gro ? kGroBuf : pc->o.slot_bytes;
-        memset(&pc->rmsg[j], 0, sizeof pc->rmsg[j]);
-        pc->rmsg[j].msg_hdr.msg_iov = &pc->riov[j];
-        pc->rmsg[j].msg_hdr.msg_iovlen = 1;
-        pc->rmsg[j].msg_hdr.msg_name = &pc->rss[j];
-        pc->rmsg[j].msg_hdr.msg_namelen = sizeof pc->rss[j];
-        if (pc->gro) {
-          pc->rmsg[j].msg_hdr.msg_control = &pc->rctl[8ull * j];
-          pc->rmsg[j].msg_hdr.msg_controllen = 8 * sizeof(uint64_t);
-        }
-      }
-      m = recvmmsg(pc->fd, pc->rmsg.data(), want, MSG_DONTWAIT, nullptr);
-      if (m > 0) break;
-      const int e = m < 0 ? errno : EAGAIN;
-      if (e == EAGAIN || e == EWOULDBLOCK || e == EINTR) continue;
+  }
+  const uint32_t idx = pc->tq.front();
+  pc->tq.pop_front();
+  pc->tx_busy = true;
+  PBatch &b = pc->tb[idx];
+  lk.unlock();
+  bool cpu, failed;
+  int st = transform(E, w, pc, SQOBFS_OBFUSCATE, b, true, &cpu, &failed);
+  int send_err = 0;
+  uint64_t nerr = 0;
+  if (st == SQ_OK && pc->socket_mode()) st = send_batch(pc, b, 0, &send_err, &nerr);
+  lk.lock();
+  pc->tx_busy = false;
+  note_transform(pc, cpu, failed, st == SQ_ECLOSED ? SQ_OK : st, b.n);
+  if (send_err && !pc->tx_err) pc->tx_err = send_err;
+  pc->st.tx_send_errors += nerr;
+  if (st == SQ_OK) {
+    pc->st.tx_datagrams += b.n;
+    pc->st.tx_batches++;
+    pc->st.tx_max_batch = std::max(pc->st.tx_max_batch, b.n);
+  }
+  if (st == SQ_OK && !pc->socket_mode()) {
+    pc->ttaken.push_back(idx);
+    pc->cv_take.notify_one();
+  } else {
+    batch_detach(pc, b);
+    pc->tfree.push_back(idx);
+  }
+  pc->cv_txs.notify_all();
+  const bool more = !pc->tq.empty() || (pc->tfill >= 0 && pc->tb[pc->tfill].n > 0);
+  task_end(pc, kTx, more);
+}
+
+// Receive, pump mode: the batch the caller pushed -> deobfuscate -> ready.
+void rx_pump_task(Engine *E, uint32_t w, sqobfs_pconn *pc) {
+  std::unique_lock<std::mutex> lk(pc->mu);
+  if (pc->closed) return task_end(pc, kRx, false);
+  if (pc->rq.empty()) {
+    if (pc->rfill >= 0 && pc->rb[pc->rfill].n > 0) {
+      const int64_t due = pc->rb[pc->rfill].first_ns + (int64_t)pc->o.linger_us * 1000;
+      if (pc->o.linger_us && mono_ns() < due) return task_end(pc, kRx, true, due);
+      pc->rq.push_back((uint32_t)pc->rfill);
+      pc->rfill = -1;
+    } else {
+      return task_end(pc, kRx, false);
+    }
+  }
+  const uint32_t idx = pc->rq.front();
+  pc->rq.pop_front();
+  PBatch &b = pc->rb[idx];
+  b.next = 0;
+  lk.unlock();
+  bool cpu, failed;
+  const int st = transform(E, w, pc, SQOBFS_DEOBFUSCATE, b, true, &cpu, &failed);
+  lk.lock();
+  note_transform(pc, cpu, failed, st, b.n);
+  if (st != SQ_OK) {  // lost with the failed launch
+    batch_detach(pc, b);
+    pc->rfree.push_back(idx);
+    pc->cv_rxs.notify_all();
+  } else {
+    pc->st.rx_datagrams += b.n;
+    pc->st.rx_batches++;
+    pc->st.rx_max_batch = std::max(pc->st.rx_max_batch, b.n);
+    pc->rready.push_back(idx);
+    pc->cv_rxr.notify_all();
+  }
+  const bool more = !pc->rq.empty() || (pc->rfill >= 0 && pc->rb[pc->rfill].n > 0);
+  task_end(pc, kRx, more);
+}
+
+void rearm(Engine *E, sqobfs_pconn *pc) {
+  epoll_event ev{};
+  ev.events = EPOLLIN | EPOLLONESHOT;
+  ev.data.u64 = pc->id;
+  (void)epoll_ctl(E->epfd, EPOLL_CTL_MOD, pc->fd, &ev);  // (ENOENT after close: fine)
+}
+
+// Receive, socket mode (the poller saw the socket readable): recvmmsg one
+// batch -> deobfuscate -> ready; requeued while the socket has more, the
+// socket re-armed when it is drained.
+void rx_socket_task(Engine *E, uint32_t w, sqobfs_pconn *pc) {
+  std::unique_lock<std::mutex> lk(pc->mu);
+  if (pc->closed || pc->rx_dead) return task_end(pc, kRx, false);
+  if (pc->rfree.empty()) {  // every batch holds unread datagrams: read() restarts us
+    pc->rx_stall = true;
+    return task_end(pc, kRx, false);
+  }
+  const uint32_t idx = pc->rfree.front();
+  pc->rfree.pop_front();
+  PBatch &b = pc->rb[idx];
+  if (!batch_attach(pc, b, false)) {
+    pc->rfree.push_front(idx);
+    pc->rx_stall = true;  // no memory now: the next read() retries
+    return task_end(pc, kRx, false);
+  }
+  lk.unlock();
+  // GRO: the batch's slot region as 64 KiB buffers of up to 64 coalesced
+  // datagrams each (so the batch arrays always have room)
+  const uint32_t ngro = pc->gro ? std::max<uint32_t>(1, std::min<uint64_t>(
+                                      (uint64_t)pc->o.batch * pc->o.slot_bytes / kGroBuf,
+                                      pc->o.batch / kGsoMaxSegs))
+                                : 0;
+  const uint32_t want = pc->gro ? ngro : pc->o.batch;
+  Block &k = *b.blk;
+  for (uint32_t j = 0; j < want; j++) {
+    pc->riov[j].iov_base = pc->gro ? k.slots + (size_t)j * kGroBuf : pc->slot(b, j);
+    pc->riov[j].iov_len = pc->gro ? kGroBuf : pc->o.slot_bytes;
+    memset(&pc->rmsg[j], 0, sizeof pc->rmsg[j]);
+    pc->rmsg[j].msg_hdr.msg_iov = &pc->riov[j];
+    pc->rmsg[j].msg_hdr.msg_iovlen = 1;
+    pc->rmsg[j].msg_hdr.msg_name = &pc->rss[j];
+    pc->rmsg[j].msg_hdr.msg_namelen = sizeof pc->rss[j];
+    if (pc->gro) {
+      pc->rmsg[j].msg_hdr.msg_control = &pc->rctl[8ull * j];
+      pc->rmsg[j].msg_hdr.msg_controllen = 8 * sizeof(uint64_t);
+    }
+  }
+  int m;
+  do {
+    m = recvmmsg(pc->fd, pc->rmsg.data(), want, MSG_DONTWAIT, nullptr);
+  } while (m < 0 && errno == EINTR);
+  if (m <= 0) {
+    const int e = m < 0 ? errno : EAGAIN;
+    lk.lock();
+    batch_detach(pc, b);
+    pc->rfree.push_front(idx);
+    if (e != EAGAIN && e != EWOULDBLOCK) {
       // ICMP-reported errors are per datagram (the next read works);
       // anything else ends the receive side
-      std::lock_guard<std::mutex> lk(pc->mu);
       pc->rx_err = SQOBFS_ERRNO(e);
       const bool transient = e == ECONNREFUSED || e == EHOSTUNREACH || e == ENETUNREACH;
       pc->rx_err_sticky = !transient;
+      pc->rx_dead = !transient;
       pc->cv_rxr.notify_all();
-      if (!transient) return;
     }
-    uint64_t trunc = 0;
-    uint32_t n = 0;
-    if (pc->gro) {
-      // split every coalesced message into its datagrams (cmsg UDP_GRO gives
-      // the segment size; the last may be shorter), decoded in place
-      for (int j = 0; j < m; j++) {
-        const uint32_t total = pc->rmsg[j].msg_len;
-        uint32_t seg = total;
-        for (cmsghdr *cm = CMSG_FIRSTHDR(&pc->rmsg[j].msg_hdr); cm;
-             cm = CMSG_NXTHDR(&pc->rmsg[j].msg_hdr, cm))
-          if (cm->cmsg_level == SOL_UDP && cm->cmsg_type == UDP_GRO) {
-            int v;
-            memcpy(&v, CMSG_DATA(cm), sizeof v);
-            if (v > 0) seg = (uint32_t)v;
-          }
-        if (pc->rmsg[j].msg_hdr.msg_flags & MSG_TRUNC) trunc++;
-        sqobfs_addr from;
-        sq::from_sockaddr(pc->rss[j], &from);
-        const uint64_t base = (uint64_t)j * kGroBuf;
-        for (uint32_t o = 0; (o < total || (total == 0 && o == 0)) && n < pc->o.batch;
-             o += seg ? seg : 1) {
-          const uint32_t l = std::min(seg, total - o);
-          b.in_off[n] = base + o;
-          b.out_off[n] = base + o + pc->S;
-          b.len[n] = l;
-          memcpy(&b.head[16ull * n], b.slots + base + o, std::min<uint32_t>(16, l));
-          b.addr[n] = from;
-          b.tag[n] = 0;
-          n++;
-          if (total == 0) break;
+    if (!pc->rx_dead) rearm(E, pc);
+    return task_end(pc, kRx, false);
+  }
+  uint64_t trunc = 0;
+  uint32_t n = 0;
+  if (pc->gro) {
+    // split every coalesced message into its datagrams (cmsg UDP_GRO gives
+    // the segment size; the last may be shorter), decoded in place
+    for (int j = 0; j < m; j++) {
+      const uint32_t total = pc->rmsg[j].msg_len;
+      uint32_t seg = total;
+      for (cmsghdr *cm = CMSG_FIRSTHDR(&pc->rmsg[j].msg_hdr); cm;
+           cm = CMSG_NXTHDR(&pc->rmsg[j].msg_hdr, cm))
+        if (cm->cmsg_level == SOL_UDP && cm->cmsg_type == UDP_GRO) {
+          int v;
+          memcpy(&v, CMSG_DATA(cm), sizeof v);
+          if (v > 0) seg = (uint32_t)v;
         }
+      if (pc->rmsg[j].msg_hdr.msg_flags & MSG_TRUNC) trunc++;
+      sqobfs_addr from;
+      sq::from_sockaddr(pc->rss[j], &from);
+      const uint64_t base = (uint64_t)j * kGroBuf;
+      for (uint32_t o = 0; (o < total || (total == 0 && o == 0)) && n < pc->o.batch;
+           o += seg ? seg : 1) {
+        const uint32_t l = std::min(seg, total - o);
+        k.in_off[n] = base + o;
+        k.out_off[n] = base + o + pc->S;
+        k.len[n] = l;
+        memcpy(&b.head[16ull * n], k.slots + base + o, std::min<uint32_t>(16, l));
+        b.addr[n] = from;
+        b.tag[n] = 0;
+        n++;
+        if (total == 0) break;
       }
-    } else {
-      for (int j = 0; j < m; j++) {
-        b.len[j] = std::min<uint32_t>(pc->rmsg[j].msg_len, pc->o.slot_bytes);
-        memcpy(&b.head[16ull * j], pc->slot(b, (uint32_t)j), 16);
-        if (pc->rmsg[j].msg_hdr.msg_flags & MSG_TRUNC) trunc++;
-        sq::from_sockaddr(pc->rss[j], &b.addr[j]);
-        b.tag[j] = 0;
-      }
-      n = (uint32_t)m;
     }
-    b.n = n;
-    b.next = 0;
-    const int st = launch_wait(pc, pc->rxs, SQOBFS_DEOBFUSCATE, b, !pc->gro);
-    std::lock_guard<std::mutex> lk(pc->mu);
-    pc->st.rx_truncated += trunc;
-    if (st != SQ_OK) {
-      pc->rx_err = st;
-      pc->rx_err_sticky = true;
-      pc->cv_rxr.notify_all();
-      return;
+  } else {
+    for (int j = 0; j < m; j++) {
+      k.len[j] = std::min<uint32_t>(pc->rmsg[j].msg_len, pc->o.slot_bytes);
+      memcpy(&b.head[16ull * j], pc->slot(b, (uint32_t)j), 16);
+      if (pc->rmsg[j].msg_hdr.msg_flags & MSG_TRUNC) trunc++;
+      sq::from_sockaddr(pc->rss[j], &b.addr[j]);
+      b.tag[j] = 0;
     }
+    n = (uint32_t)m;
+  }
+  b.n = n;
+  b.next = 0;
+  bool cpu, failed;
+  const int st = transform(E, w, pc, SQOBFS_DEOBFUSCATE, b, !pc->gro, &cpu, &failed);
+  lk.lock();
+  pc->st.rx_truncated += trunc;
+  note_transform(pc, cpu, failed, st, b.n);
+  if (st != SQ_OK) {
+    batch_detach(pc, b);
+    pc->rfree.push_back(idx);
+  } else {
     pc->st.rx_datagrams += b.n;
     pc->st.rx_batches++;
     pc->st.rx_max_batch = std::max(pc->st.rx_max_batch, b.n);
     pc->rready.push_back(idx);
     pc->cv_rxr.notify_all();
   }
+  task_end(pc, kRx, true);  // the socket may hold more: look again (EAGAIN re-arms)
 }
 
-// ---- receive worker, pump mode: the caller pushes datagrams; launch
-// batches as the tx worker does
-void rx_worker_pump(sqobfs_pconn *pc) {
-  std::unique_lock<std::mutex> lk(pc->mu);
+void worker_main(Engine *E, uint32_t w) {
+  std::unique_lock<std::mutex> lk(E->mu);
   for (;;) {
-    for (;;) {
-      if (pc->closed) return;
-      if (!pc->rq.empty()) break;
-      if (pc->rfill >= 0 && pc->rb[pc->rfill].n > 0) {
-        const int64_t due = pc->rb[pc->rfill].first_ns + (int64_t)pc->o.linger_us * 1000;
-        if (pc->o.linger_us == 0 || mono_ns() >= due) {
-          pc->rq.push_back((uint32_t)pc->rfill);
-          pc->rfill = -1;
-          break;
+    if (E->stop) return;
+    int64_t next = 0;
+    if (!E->timers.empty()) {
+      const int64_t now = mono_ns();
+      for (size_t k = 0; k < E->timers.size();) {
+        if (E->timers[k].first <= now) {
+          Task t = E->timers[k].second;
+          t.pc->timed[t.dir] = false;
+          E->runq.push_back(t);
+          E->timers.erase(E->timers.begin() + (long)k);
+        } else {
+          next = next ? std::min(next, E->timers[k].first) : E->timers[k].first;
+          k++;
         }
-        pc->cv_rxw.wait_until(lk, mono_tp(due));
-        continue;
       }
-      pc->cv_rxw.wait(lk);
     }
-    const uint32_t idx = pc->rq.front();
-    pc->rq.pop_front();
-    pc->rx_busy = true;
-    PBatch &b = pc->rb[idx];
-    b.next = 0;
+    if (E->runq.empty()) {
+      if (next) E->cv.wait_until(lk, mono_tp(next));
+      else E->cv.wait(lk);
+      continue;
+    }
+    const Task t = E->runq.front();
+    E->runq.pop_front();
     lk.unlock();
-    const int st = launch_wait(pc, pc->rxs, SQOBFS_DEOBFUSCATE, b);
+    if (t.dir == kTx) tx_task(E, w, t.pc);
+    else if (t.pc->socket_mode()) rx_socket_task(E, w, t.pc);
+    else rx_pump_task(E, w, t.pc);
     lk.lock();
-    pc->rx_busy = false;
-    if (st != SQ_OK) {
-      pc->rx_err = st;
-      pc->rx_err_sticky = true;
-      pc->cv_rxr.notify_all();
-      return;
-    }
-    pc->st.rx_datagrams += b.n;
-    pc->st.rx_batches++;
-    pc->st.rx_max_batch = std::max(pc->st.rx_max_batch, b.n);
-    pc->rready.push_back(idx);
-    pc->cv_rxr.notify_all();
   }
 }
 
-void free_pconn(sqobfs_pconn *pc) {
-  if (pc->txs) {
-    sq_ctx_stream_destroy(pc->ctx, pc->txs);  // synchronises first
-    sq_keyring_forget(pc->kr, pc->txs);
+void poller_main(Engine *E) {
+  epoll_event ev[64];
+  for (;;) {
+    const int n = epoll_wait(E->epfd, ev, 64, -1);
+    if (n < 0 && errno != EINTR) return;
+    std::lock_guard<std::mutex> lk(E->mu);
+    if (E->stop) return;
+    for (int i = 0; i < n; i++) {
+      if (ev[i].data.u64 == 0) continue;  // the wake fd (stop)
+      auto it = E->byid.find(ev[i].data.u64);
+      if (it == E->byid.end()) continue;  // closed meanwhile
+      schedule_locked(E, it->second, kRx);
+    }
   }
-  if (pc->rxs) {
-    sq_ctx_stream_destroy(pc->ctx, pc->rxs);
-    sq_keyring_forget(pc->kr, pc->rxs);
+}
+
+void engine_end(Engine *E) {
+  {
+    std::lock_guard<std::mutex> lk(E->mu);
+    E->stop = true;
   }
-  if (pc->block) sqobfs_host_free(pc->ctx, pc->block);
-  if (pc->fd >= 0) close(pc->fd);
-  if (pc->wake >= 0) close(pc->wake);
-  delete pc;
+  E->cv.notify_all();
+  const uint64_t one = 1;
+  (void)!write(E->wake, &one, sizeof one);
+  for (auto &t : E->threads) t.join();
+  for (void *s : E->streams)
+    if (s) sq_ctx_stream_destroy(E->ctx, s);
+  for (auto &kv : E->free_blocks)
+    for (Block *b : kv.second) block_free_mem(E, b);
+  close(E->wake);
+  close(E->epfd);
+  delete E;
 }
 
 }  // namespace
 
+// ---------------------------------------------------------------- engine ABI
+
+void sq_engine_ctx_closed(sqobfs_ctx *ctx) {
+  Engine *E = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_eng_mu);
+    g_workers_cfg.erase(ctx);
+    auto it = g_engines.find(ctx);
+    if (it == g_engines.end()) return;
+    E = it->second;
+    g_engines.erase(it);
+  }
+  engine_end(E);  // (the context outlives its pconns: none is open)
+}
+
 extern "C" {
+
+int sqobfs_engine_info_get(sqobfs_ctx *ctx, sqobfs_engine_info *out) {
+  if (!out) return SQ_EINVAL;
+  memset(out, 0, sizeof *out);
+  std::lock_guard<std::mutex> g(g_eng_mu);
+  auto it = g_engines.find(ctx);
+  if (it == g_engines.end()) return SQ_OK;
+  Engine *E = it->second;
+  {
+    std::lock_guard<std::mutex> lk(E->mu);
+    out->pconns = E->pconns;
+    out->threads = (uint32_t)E->threads.size();
+    out->workers = E->nworkers;
+  }
+  std::lock_guard<std::mutex> pg(E->pool_mu);
+  out->pool_blocks = E->blocks;
+  out->pool_bytes = E->pool_bytes;
+  out->blocks_in_use = E->in_use;
+  out->gpu_disabled = E->gpu_off.load() ? 1u : 0u;
+  return SQ_OK;
+}
+
+int sqobfs_engine_set_workers(sqobfs_ctx *ctx, uint32_t workers) {
+  if (workers > kMaxWorkers) return SQ_EINVAL;
+  std::lock_guard<std::mutex> g(g_eng_mu);
+  if (g_engines.count(ctx)) return SQ_EINVAL;
+  g_workers_cfg[ctx] = workers;
+  return SQ_OK;
+}
+
+int sqobfs_engine_trim(sqobfs_ctx *ctx) {
+  Engine *E;
+  {
+    std::lock_guard<std::mutex> g(g_eng_mu);
+    auto it = g_engines.find(ctx);
+    if (it == g_engines.end()) return 0;
+    E = it->second;
+  }
+  std::vector<Block *> drop;
+  {
+    std::lock_guard<std::mutex> pg(E->pool_mu);
+    for (auto &kv : E->free_blocks) {
+      drop.insert(drop.end(), kv.second.begin(), kv.second.end());
+      kv.second.clear();
+    }
+    for (Block *b : drop) {
+      E->blocks--;
+      E->pool_bytes -= b->bytes;
+    }
+  }
+  for (Block *b : drop) block_free_mem(E, b);
+  return (int)drop.size();
+}
+
+void sqobfs_debug_engine_fail(int count, int at_completion) {
+  g_fail_at_completion.store(at_completion ? 1 : 0);
+  g_fail_count.store(count > 0 ? count : 0);
+}
+
+// ---------------------------------------------------------------- pconn ABI
 
 int sqobfs_pconn_open(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int fd,
                       const sqobfs_pconn_opts *opts, sqobfs_pconn **out) {
   if (out) *out = nullptr;
-  if (!ctx || !kr || !out) return SQ_EINVAL;
+  if (!kr || !out || sq_keyring_ctx(kr) != ctx) return SQ_EINVAL;
   sqobfs_pconn_opts o{};
   if (opts) o = *opts;
   if (o.batch == 0) o.batch = kDefBatch;
@@ -489,98 +979,96 @@ int sqobfs_pconn_open(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int fd,
   if (o.tx_batches == 0) o.tx_batches = kDefBatches;
   if (o.rx_batches == 0) o.rx_batches = kDefBatches;
   if (o.spin_us == 0) o.spin_us = kDefSpinUs;
+  if (o.cpu_max == 0) o.cpu_max = kDefCpuMax;
+  if (o.inline_gap_us == 0) o.inline_gap_us = kDefInlineGapUs;
   const int kind = sqobfs_keyring_kind(kr);
   const uint32_t S = kind == SQOBFS_SALAMANDER ? SQOBFS_SALAMANDER_SALT_LEN : SQOBFS_XPLUS_SALT_LEN;
   if (o.batch > kMaxBatch || o.slot_bytes % 16 || o.slot_bytes <= S ||
       (o.flags & ~(uint32_t)(SQOBFS_UDP_TX_GSO | SQOBFS_UDP_RX_GRO)) || o.tx_batches > 64 ||
       o.rx_batches > 64)
     return SQ_EINVAL;
+  int st = SQ_OK;
+  Engine *E = engine_get(ctx, &st);
+  if (!E) return st;
   sqobfs_pconn *pc = new (std::nothrow) sqobfs_pconn();
   if (!pc) return SQ_ENOMEM;
+  pc->eng = E;
   pc->ctx = ctx;
   pc->kr = kr;
+  uint32_t count = 0;
+  pc->psk0 = sq_keyring_host(kr, &count);
   pc->kind = kind;
   pc->S = S;
   pc->o = o;
+  try {
+    pc->tb.resize(o.tx_batches);
+    pc->rb.resize(o.rx_batches);
+    for (auto *v : {&pc->tb, &pc->rb})
+      for (PBatch &b : *v) {
+        b.addr.resize(o.batch);
+        b.tag.resize(o.batch);
+      }
+    for (PBatch &b : pc->rb) b.head.resize(16ull * o.batch);
+    if (fd >= 0) {
+      pc->tmsg.resize(o.batch);
+      pc->tiov.resize(o.batch);
+      pc->tss.resize(o.batch);
+      pc->tctl.assign(kCtlWords * o.batch, 0);
+      pc->tfirst.resize(o.batch);
+      pc->rmsg.resize(o.batch);
+      pc->riov.resize(o.batch);
+      pc->rss.resize(o.batch);
+      pc->ibuf.resize(o.slot_bytes);
+    }
+  } catch (...) {
+    delete pc;
+    return SQ_ENOMEM;
+  }
+  for (uint32_t k = 0; k < o.tx_batches; k++) pc->tfree.push_back(k);
+  for (uint32_t k = 0; k < o.rx_batches; k++) pc->rfree.push_back(k);
+  pc->wake = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
+  if (pc->wake < 0) {
+    delete pc;
+    return SQ_ENOMEM;
+  }
   if (fd >= 0) {
     pc->fd = fcntl(fd, F_DUPFD_CLOEXEC, 0);
     if (pc->fd < 0) {
       const int e = errno;
+      close(pc->wake);
       delete pc;
       return SQOBFS_ERRNO(e);
     }
-  }
-  pc->wake = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
-  if (pc->wake < 0) {
-    free_pconn(pc);
-    return SQ_ENOMEM;
-  }
-  // one mapped block: all slots, then per batch 2 u64 + 2 u32 arrays
-  const uint32_t nb = o.tx_batches + o.rx_batches, B = o.batch;
-  const size_t slots = (size_t)B * o.slot_bytes, arrays = (size_t)B * (8 + 8 + 4 + 4);
-  int st = sqobfs_host_alloc(ctx, (size_t)nb * (slots + arrays), &pc->block);
-  void *dev = nullptr;  // the GPU's view of the block (the same address on ROCm)
-  if (st == SQ_OK && (hipHostGetDevicePointer(&dev, pc->block, 0) != hipSuccess ||
-                      dev != pc->block)) {
-    (void)hipGetLastError();
-    st = SQ_EDEVICE;
-  }
-  if (st == SQ_OK) st = sq_ctx_stream_create(ctx, &pc->txs);
-  if (st == SQ_OK) st = sq_ctx_stream_create(ctx, &pc->rxs);
-  if (st != SQ_OK) {
-    free_pconn(pc);
-    return st;
-  }
-  uint8_t *p = (uint8_t *)pc->block, *a = p + (size_t)nb * slots;
-  pc->tb.resize(o.tx_batches);
-  pc->rb.resize(o.rx_batches);
-  for (uint32_t k = 0; k < nb; k++) {
-    const bool tx = k < o.tx_batches;
-    PBatch &b = tx ? pc->tb[k] : pc->rb[k - o.tx_batches];
-    b.slots = p + (size_t)k * slots;
-    b.in_off = (uint64_t *)a;   a += 8ull * B;
-    b.out_off = (uint64_t *)a;  a += 8ull * B;
-    b.len = (uint32_t *)a;      a += 4ull * B;
-    b.out_len = (uint32_t *)a;  a += 4ull * B;
-    b.addr.resize(B);
-    b.tag.resize(B);
-    if (!tx) b.head.resize(16ull * B);
-    for (uint32_t i = 0; i < B; i++) {
-      const uint64_t s0 = (uint64_t)i * o.slot_bytes;
-      // tx: payload behind S bytes of headroom, wire = salt || payload in
-      // place from the slot start (the vectorised writers' layout,
-      // salamander.go:81-93); rx: wire at the slot start, payload decoded in
-      // place behind the salt
-      b.in_off[i] = tx ? s0 + S : s0;
-      b.out_off[i] = tx ? s0 : s0 + S;
-    }
-    if (tx) pc->tfree.push_back(k);
-    else pc->rfree.push_back(k - o.tx_batches);
-  }
-  if (pc->socket_mode()) {
-    pc->tmsg.resize(B);
-    pc->tiov.resize(B);
-    pc->tss.resize(B);
-    pc->tctl.assign(kCtlWords * B, 0);
-    pc->tfirst.resize(B);
-    pc->rmsg.resize(B);
-    pc->riov.resize(B);
-    pc->rss.resize(B);
     pc->gso = o.flags & SQOBFS_UDP_TX_GSO;  // probed by the first send
-    if ((o.flags & SQOBFS_UDP_RX_GRO) && B >= kGsoMaxSegs &&
-        (uint64_t)B * o.slot_bytes >= kGroBuf) {
+    if ((o.flags & SQOBFS_UDP_RX_GRO) && o.batch >= kGsoMaxSegs &&
+        (uint64_t)o.batch * o.slot_bytes >= kGroBuf) {
       const int one = 1;
       pc->gro = setsockopt(pc->fd, SOL_UDP, UDP_GRO, &one, sizeof one) == 0;
-      if (pc->gro) pc->rctl.assign(8ull * B, 0);
+      if (pc->gro) pc->rctl.assign(8ull * o.batch, 0);
     }
   }
-  try {
-    pc->txw = std::thread(tx_worker, pc);
-    pc->rxw = pc->socket_mode() ? std::thread(rx_worker_socket, pc) : std::thread(rx_worker_pump, pc);
-  } catch (...) {
-    sqobfs_pconn_shutdown(pc);
-    free_pconn(pc);
-    return SQ_ENOMEM;
+  {
+    std::lock_guard<std::mutex> lk(E->mu);
+    pc->id = E->next_id++;
+    E->byid[pc->id] = pc;
+    E->pconns++;
+  }
+  if (fd >= 0) {
+    epoll_event ev{};
+    ev.events = EPOLLIN | EPOLLONESHOT;
+    ev.data.u64 = pc->id;
+    if (epoll_ctl(E->epfd, EPOLL_CTL_ADD, pc->fd, &ev) != 0) {
+      const int e = errno;
+      {
+        std::lock_guard<std::mutex> lk(E->mu);
+        E->byid.erase(pc->id);
+        E->pconns--;
+      }
+      close(pc->fd);
+      close(pc->wake);
+      delete pc;
+      return SQOBFS_ERRNO(e);
+    }
   }
   *out = pc;
   return SQ_OK;
@@ -588,39 +1076,71 @@ int sqobfs_pconn_open(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int fd,
 
 void sqobfs_pconn_shutdown(sqobfs_pconn *pc) {
   if (!pc) return;
+  Engine *E = pc->eng;
+  bool closer = false;
   {
     std::unique_lock<std::mutex> lk(pc->mu);
     if (!pc->writes_closed) {
+      closer = true;
       pc->writes_closed = true;
-      pc->cv_txw.notify_all();
+      // what was written goes out: the filling batch now (no linger), then
+      // wait (bounded) until the transmit side has drained -- sent, or taken
+      // and done by the pump taker
+      if (pc->tfill >= 0 && pc->tb[pc->tfill].n > 0) {
+        pc->tq.push_back((uint32_t)pc->tfill);
+        pc->tfill = -1;
+      }
+      if (!pc->tq.empty()) schedule(pc, kTx);
       pc->cv_txs.notify_all();
-      // what was written goes out: wait (bounded) until the transmit side
-      // has drained -- sent, or taken and done by the pump taker
       const int64_t until = mono_ns() + kDrainNs;
-      while (!pc->closed && (pc->tx_busy || !pc->tq.empty() || !pc->ttaken.empty() ||
-                             (pc->tfill >= 0 && pc->tb[pc->tfill].n > 0))) {
+      while (pc->tx_busy || pc->inline_busy || !pc->tq.empty() || !pc->ttaken.empty()) {
         if (mono_ns() >= until) break;
         pc->cv_txs.wait_until(lk, mono_tp(std::min(until, mono_ns() + 5'000'000)));
       }
       pc->closed = true;
-      for (auto *cv : {&pc->cv_txw, &pc->cv_txs, &pc->cv_rxw, &pc->cv_rxr, &pc->cv_rxs,
-                       &pc->cv_take})
-        cv->notify_all();
+      for (auto *cv : {&pc->cv_txs, &pc->cv_rxr, &pc->cv_rxs, &pc->cv_take}) cv->notify_all();
     }
   }
-  if (pc->wake >= 0) {
+  if (closer) {
     const uint64_t one = 1;
-    (void)!write(pc->wake, &one, sizeof one);
+    (void)!write(pc->wake, &one, sizeof one);  // a send blocked on socket space
+    if (pc->fd >= 0) (void)epoll_ctl(E->epfd, EPOLL_CTL_DEL, pc->fd, nullptr);
   }
-  std::lock_guard<std::mutex> jl(pc->join_mu);
-  if (pc->txw.joinable()) pc->txw.join();
-  if (pc->rxw.joinable()) pc->rxw.join();
+  // every call (a concurrent second one too) returns once the pconn's tasks
+  // have ended, so sqobfs_pconn_close may free it
+  std::unique_lock<std::mutex> lk(E->mu);
+  E->byid.erase(pc->id);
+  for (size_t k = 0; k < E->timers.size();) {
+    if (E->timers[k].second.pc == pc) {
+      const int d = E->timers[k].second.dir;
+      pc->timed[d] = false;
+      pc->sched[d] = false;
+      pc->tasks--;
+      E->timers.erase(E->timers.begin() + (long)k);
+    } else {
+      k++;
+    }
+  }
+  E->cv_idle.wait(lk, [&] { return pc->tasks == 0; });
 }
 
 void sqobfs_pconn_close(sqobfs_pconn *pc) {
   if (!pc) return;
   sqobfs_pconn_shutdown(pc);
-  free_pconn(pc);
+  Engine *E = pc->eng;
+  // its launches are all complete: the keyring need not fence the engine's
+  // streams for them (sqobfs_keyring_destroy)
+  {
+    std::lock_guard<std::mutex> lk(E->mu);
+    for (void *s : E->streams)
+      if (s) sq_keyring_forget(pc->kr, s);
+    E->pconns--;
+  }
+  for (auto *v : {&pc->tb, &pc->rb})
+    for (PBatch &b : *v) batch_detach(pc, b);
+  if (pc->fd >= 0) close(pc->fd);
+  if (pc->wake >= 0) close(pc->wake);
+  delete pc;
 }
 
 int sqobfs_pconn_set_deadline(sqobfs_pconn *pc, uint32_t which, int64_t unix_ns_) {
@@ -637,6 +1157,48 @@ int sqobfs_pconn_set_deadline(sqobfs_pconn *pc, uint32_t which, int64_t unix_ns_
   return SQ_OK;
 }
 
+namespace {
+
+// The inline write (opts.inline_gap_us): obfuscate on this thread and send,
+// waiting for socket space as a blocking WriteTo does (bounded by the write
+// deadline and by shutdown).  Caller set inline_busy; returns the send's
+// status.
+int write_inline(sqobfs_pconn *pc, const uint8_t *p, uint32_t len, const sqobfs_addr *to) {
+  uint32_t key8[8];
+  uint64_t seq;
+  sq_salt_take(pc->ctx, key8, &seq);
+  uint8_t *w = pc->ibuf.data();
+  sq::cpu::salt_stream(key8, seq, w, pc->S);
+  uint8_t key[32];
+  sq::cpu::derive_key(*pc->psk0, w, key);
+  sq::cpu::xor_stream(w + pc->S, p, len, key);
+  sockaddr_storage ss;
+  socklen_t sl;
+  sq::to_sockaddr(*to, &ss, &sl);
+  for (;;) {
+    const ssize_t r = sendto(pc->fd, w, pc->S + len, MSG_DONTWAIT, (sockaddr *)&ss, sl);
+    if (r >= 0) return SQ_OK;
+    const int e = errno;
+    if (e == EINTR) continue;
+    if (e != EAGAIN && e != EWOULDBLOCK && e != ENOBUFS) return SQOBFS_ERRNO(e);
+    int ms = 100;
+    {
+      std::lock_guard<std::mutex> lk(pc->mu);
+      if (pc->closed) return SQ_ECLOSED;
+      if (pc->wdl) {
+        const int64_t left = pc->wdl - unix_ns();
+        if (left <= 0) return SQ_ETIMEDOUT;
+        ms = (int)std::min<int64_t>(100, left / 1000000 + 1);
+      }
+    }
+    pollfd q[2] = {{pc->fd, POLLOUT, 0}, {pc->wake, POLLIN, 0}};
+    (void)poll(q, 2, ms);
+    if (q[1].revents & POLLIN) return SQ_ECLOSED;
+  }
+}
+
+}  // namespace
+
 int sqobfs_pconn_write(sqobfs_pconn *pc, const uint8_t *p, uint32_t len, const sqobfs_addr *to,
                        uint64_t tag) {
   if (!pc || (len && !p) || (pc->socket_mode() && !to)) return SQ_EINVAL;
@@ -650,6 +1212,29 @@ int sqobfs_pconn_write(sqobfs_pconn *pc, const uint8_t *p, uint32_t len, const s
     pc->tx_err = 0;
     return e;
   }
+  const int64_t now = mono_ns();
+  const int64_t gap = now - pc->last_write_ns;
+  pc->last_write_ns = now;
+  if (pc->socket_mode() && pc->o.inline_gap_us != SQOBFS_PCONN_NEVER && !pc->inline_busy &&
+      pc->tfill < 0 && pc->tq.empty() && !pc->tx_busy &&
+      gap >= (int64_t)pc->o.inline_gap_us * 1000) {
+    bool idle;
+    {
+      std::lock_guard<std::mutex> el(pc->eng->mu);
+      idle = !pc->sched[kTx];
+    }
+    if (idle) {
+      pc->inline_busy = true;
+      lk.unlock();
+      const int st = write_inline(pc, p, len, to);
+      lk.lock();
+      pc->inline_busy = false;
+      pc->st.inline_writes++;
+      if (st == SQ_OK) pc->st.tx_datagrams++;
+      pc->cv_txs.notify_all();
+      return st;
+    }
+  }
   if (pc->tfill < 0) {
     const bool ok = wait_dl(lk, pc->cv_txs, pc->wdl, [&] {
       return pc->writes_closed || pc->tfill >= 0 || !pc->tfree.empty();
@@ -657,25 +1242,27 @@ int sqobfs_pconn_write(sqobfs_pconn *pc, const uint8_t *p, uint32_t len, const s
     if (pc->writes_closed) return SQ_ECLOSED;
     if (!ok) return SQ_ETIMEDOUT;
     if (pc->tfill < 0) {  // (another writer may have opened one meanwhile)
-      pc->tfill = (int)pc->tfree.front();
+      const uint32_t k = pc->tfree.front();
+      if (!batch_attach(pc, pc->tb[k], true)) return SQ_ENOMEM;
       pc->tfree.pop_front();
-      pc->tb[pc->tfill].n = 0;
+      pc->tfill = (int)k;
+      pc->tb[k].n = 0;
     }
   }
   PBatch &b = pc->tb[pc->tfill];
   const uint32_t i = b.n++;
-  if (i == 0) b.first_ns = mono_ns();
+  if (i == 0) b.first_ns = now;
   if (len) memcpy(pc->slot(b, i) + pc->S, p, len);
-  b.len[i] = len;
+  b.blk->len[i] = len;
   if (to) b.addr[i] = *to;
   else memset(&b.addr[i], 0, sizeof b.addr[i]);
   b.tag[i] = tag;
   if (b.n == pc->o.batch) {
     pc->tq.push_back((uint32_t)pc->tfill);
     pc->tfill = -1;
-    pc->cv_txw.notify_one();
-  } else if (i == 0 && !pc->tx_busy) {
-    pc->cv_txw.notify_one();  // an idle worker takes it at once (or lingers)
+    schedule(pc, kTx);
+  } else if (i == 0) {
+    schedule(pc, kTx);  // a free worker takes it at once (or after linger_us)
   }
   return SQ_OK;
 }
@@ -704,10 +1291,11 @@ int sqobfs_pconn_read(sqobfs_pconn *pc, uint8_t *p, uint32_t cap, uint32_t *n,
   }
   const uint32_t idx = pc->rready.front();
   PBatch &b = pc->rb[idx];
+  const Block &k = *b.blk;
   const uint32_t i = b.next++;
   // the reference reads the datagram into p (cut to len(p)) and decodes
   // what it got: m = min(wire, cap)
-  const uint32_t w = b.len[i], m = std::min(w, cap), S = pc->S;
+  const uint32_t w = k.len[i], m = std::min(w, cap), S = pc->S;
   uint32_t r = 0;
   const uint8_t *src = nullptr;
   if (pc->kind == SQOBFS_SALAMANDER && m <= S) {
@@ -717,7 +1305,7 @@ int sqobfs_pconn_read(sqobfs_pconn *pc, uint8_t *p, uint32_t cap, uint32_t *n,
     r = 0;                  // xplus.go:50-52
   } else {
     r = m - S;              // the first m - S payload bytes
-    src = b.slots + b.out_off[i];
+    src = k.slots + k.out_off[i];
   }
   if (r) memcpy(p, src, r);
   *n = r;
@@ -725,9 +1313,13 @@ int sqobfs_pconn_read(sqobfs_pconn *pc, uint8_t *p, uint32_t cap, uint32_t *n,
   if (tag) *tag = b.tag[i];
   if (b.next == b.n) {
     pc->rready.pop_front();
-    b.n = 0;
+    batch_detach(pc, b);
     pc->rfree.push_back(idx);
     pc->cv_rxs.notify_all();
+    if (pc->rx_stall) {  // the socket task waits for a free batch
+      pc->rx_stall = false;
+      schedule(pc, kRx);
+    }
   }
   return SQ_OK;
 }
@@ -740,9 +1332,11 @@ int sqobfs_pconn_rx_push(sqobfs_pconn *pc, const uint8_t *wire, uint32_t n,
     pc->cv_rxs.wait(lk, [&] { return pc->closed || !pc->rfree.empty() || pc->rfill >= 0; });
     if (pc->closed) return SQ_ECLOSED;
     if (pc->rfill < 0) {
-      pc->rfill = (int)pc->rfree.front();
+      const uint32_t k = pc->rfree.front();
+      if (!batch_attach(pc, pc->rb[k], false)) return SQ_ENOMEM;
       pc->rfree.pop_front();
-      pc->rb[pc->rfill].n = 0;
+      pc->rfill = (int)k;
+      pc->rb[k].n = 0;
     }
   }
   if (pc->closed) return SQ_ECLOSED;
@@ -753,16 +1347,16 @@ int sqobfs_pconn_rx_push(sqobfs_pconn *pc, const uint8_t *wire, uint32_t n,
   if (m < n) pc->st.rx_truncated++;
   if (m) memcpy(pc->slot(b, i), wire, m);
   memcpy(&b.head[16ull * i], pc->slot(b, i), 16);
-  b.len[i] = m;
+  b.blk->len[i] = m;
   if (from) b.addr[i] = *from;
   else memset(&b.addr[i], 0, sizeof b.addr[i]);
   b.tag[i] = tag;
   if (b.n == pc->o.batch) {
     pc->rq.push_back((uint32_t)pc->rfill);
     pc->rfill = -1;
-    pc->cv_rxw.notify_one();
-  } else if (i == 0 && !pc->rx_busy) {
-    pc->cv_rxw.notify_one();
+    schedule(pc, kRx);
+  } else if (i == 0) {
+    schedule(pc, kRx);
   }
   return SQ_OK;
 }
@@ -792,9 +1386,9 @@ int sqobfs_pconn_tx_take(sqobfs_pconn *pc, int timeout_ms, sqobfs_pconn_tx *out)
   PBatch &b = pc->tb[pc->ttaken.front()];
   pc->taken = true;
   out->count = b.n;
-  out->base = b.slots;
-  out->off = b.out_off;
-  out->len = b.out_len;
+  out->base = b.blk->slots;
+  out->off = b.blk->out_off;
+  out->len = b.blk->out_len;
   out->to = b.addr.data();
   out->tag = b.tag.data();
   return SQ_OK;
@@ -807,7 +1401,7 @@ int sqobfs_pconn_tx_done(sqobfs_pconn *pc) {
   const uint32_t idx = pc->ttaken.front();
   pc->ttaken.pop_front();
   pc->taken = false;
-  pc->tb[idx].n = 0;
+  batch_detach(pc, pc->tb[idx]);
   pc->tfree.push_back(idx);
   pc->cv_txs.notify_all();
   return SQ_OK;

@@ -1,0 +1,355 @@
+// sq_cpu.cpp -- the product's CPU transform (sq_cpu.h).
+//
+// Per packet it computes what SalamanderPacketConn / XPlusPacketConn compute
+// per call (hysteria2/salamander.go:42-70, hysteria/xplus.go:46-75): a key
+// from psk || salt, then the keystream XOR, with the quirk table of
+// include/sqobfs.h.  Unlike the reference it hashes from the keyring's
+// per-PSK midstate (one compression per packet for PSKs up to 120 / 39 B)
+// and XORs a word at a time.
+#include "sq_cpu.h"
+
+#include <string.h>
+#include <sys/random.h>
+
+#include <atomic>
+#include <mutex>
+
+namespace sq {
+namespace cpu {
+namespace {
+
+inline uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+inline uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+inline uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+
+constexpr uint64_t kB2IV[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL,
+                               0x3c6ef372fe94f82bULL, 0xa54ff53a5f1d36f1ULL,
+                               0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+                               0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+// RFC 7693 section 2.7 (rounds 10 and 11 reuse rows 0 and 1)
+constexpr uint8_t kSigma[12][16] = {
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+    {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+    {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4},
+    {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+    {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13},
+    {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+    {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11},
+    {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+    {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5},
+    {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0},
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+    {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3}};
+
+inline void b2_g(uint64_t *v, int a, int b, int c, int d, uint64_t x, uint64_t y) {
+  v[a] = v[a] + v[b] + x;
+  v[d] = rotr64(v[d] ^ v[a], 32);
+  v[c] = v[c] + v[d];
+  v[b] = rotr64(v[b] ^ v[c], 24);
+  v[a] = v[a] + v[b] + y;
+  v[d] = rotr64(v[d] ^ v[a], 16);
+  v[c] = v[c] + v[d];
+  v[b] = rotr64(v[b] ^ v[c], 63);
+}
+
+constexpr uint32_t kS2K[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4,
+    0xab1c5ed5, 0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe,
+    0x9bdc06a7, 0xc19bf174, 0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f,
+    0x4a7484aa, 0x5cb0a9dc, 0x76f988da, 0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7,
+    0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967, 0x27b70a85, 0x2e1b2138, 0x4d2c6dfc,
+    0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85, 0xa2bfe8a1, 0xa81a664b,
+    0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070, 0x19a4c116,
+    0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7,
+    0xc67178f2};
+
+inline uint64_t ld64le(const uint8_t *p) {
+  uint64_t v;
+  memcpy(&v, p, 8);  // x86-64: little endian
+  return v;
+}
+inline uint32_t ld32be(const uint8_t *p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+void b2_init256(uint64_t h[8]) {
+  for (int i = 0; i < 8; i++) h[i] = kB2IV[i];
+  h[0] ^= 0x01010020ULL;  // digest 32, key 0, fanout 1, depth 1
+}
+
+void s2_init(uint32_t st[8]) {
+  static const uint32_t iv[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                                 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  memcpy(st, iv, sizeof iv);
+}
+
+constexpr uint32_t kBadLen = 0xFFFFFFFEu;   // sq_kernels.hip kBadLen
+constexpr uint64_t kMaxPacket = 1ull << 26;  // sq_kernels.hip kMaxPacket
+
+}  // namespace
+
+void b2_compress(uint64_t h[8], const uint64_t m[16], uint64_t t, bool last) {
+  uint64_t v[16];
+  for (int i = 0; i < 8; i++) {
+    v[i] = h[i];
+    v[i + 8] = kB2IV[i];
+  }
+  v[12] ^= t;
+  if (last) v[14] = ~v[14];
+  for (int r = 0; r < 12; r++) {
+    const uint8_t *s = kSigma[r];
+    b2_g(v, 0, 4, 8, 12, m[s[0]], m[s[1]]);
+    b2_g(v, 1, 5, 9, 13, m[s[2]], m[s[3]]);
+    b2_g(v, 2, 6, 10, 14, m[s[4]], m[s[5]]);
+    b2_g(v, 3, 7, 11, 15, m[s[6]], m[s[7]]);
+    b2_g(v, 0, 5, 10, 15, m[s[8]], m[s[9]]);
+    b2_g(v, 1, 6, 11, 12, m[s[10]], m[s[11]]);
+    b2_g(v, 2, 7, 8, 13, m[s[12]], m[s[13]]);
+    b2_g(v, 3, 4, 9, 14, m[s[14]], m[s[15]]);
+  }
+  for (int i = 0; i < 8; i++) h[i] ^= v[i] ^ v[i + 8];
+}
+
+void s2_compress(uint32_t st[8], const uint32_t m[16]) {
+  uint32_t w[64];
+  for (int i = 0; i < 16; i++) w[i] = m[i];
+  for (int i = 16; i < 64; i++) {
+    const uint32_t s0 = rotr32(w[i - 15], 7) ^ rotr32(w[i - 15], 18) ^ (w[i - 15] >> 3);
+    const uint32_t s1 = rotr32(w[i - 2], 17) ^ rotr32(w[i - 2], 19) ^ (w[i - 2] >> 10);
+    w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+  }
+  uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6],
+           h = st[7];
+  for (int i = 0; i < 64; i++) {
+    const uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
+    const uint32_t t1 = h + S1 + ((e & f) ^ (~e & g)) + kS2K[i] + w[i];
+    const uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
+    const uint32_t t2 = S0 + ((a & b) ^ (a & c) ^ (b & c));
+    h = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + t2;
+  }
+  st[0] += a;
+  st[1] += b;
+  st[2] += c;
+  st[3] += d;
+  st[4] += e;
+  st[5] += f;
+  st[6] += g;
+  st[7] += h;
+}
+
+void chacha20_block(const uint32_t key[8], uint32_t counter, const uint32_t nonce[3],
+                    uint32_t out[16]) {
+  const uint32_t in[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
+                           key[0],      key[1],      key[2],      key[3],
+                           key[4],      key[5],      key[6],      key[7],
+                           counter,     nonce[0],    nonce[1],    nonce[2]};
+  uint32_t x[16];
+  memcpy(x, in, sizeof x);
+  auto qr = [&](int a, int b, int c, int d) {
+    x[a] += x[b]; x[d] = rotl32(x[d] ^ x[a], 16);
+    x[c] += x[d]; x[b] = rotl32(x[b] ^ x[c], 12);
+    x[a] += x[b]; x[d] = rotl32(x[d] ^ x[a], 8);
+    x[c] += x[d]; x[b] = rotl32(x[b] ^ x[c], 7);
+  };
+  for (int r = 0; r < 10; r++) {
+    qr(0, 4, 8, 12);
+    qr(1, 5, 9, 13);
+    qr(2, 6, 10, 14);
+    qr(3, 7, 11, 15);
+    qr(0, 5, 10, 15);
+    qr(1, 6, 11, 12);
+    qr(2, 7, 8, 13);
+    qr(3, 4, 9, 14);
+  }
+  for (int i = 0; i < 16; i++) out[i] = x[i] + in[i];
+}
+
+void psk_prepare(int kind, const uint8_t *psk, uint32_t L, PskEntry *e) {
+  memset(e, 0, sizeof *e);
+  uint8_t tm[256];
+  memset(tm, 0, sizeof tm);
+  e->psk_len = L;
+  e->kind = (uint32_t)kind;
+  if (kind == SQOBFS_SALAMANDER) {
+    // every PSK-only 128-byte block is followed by salt bytes, so it is never
+    // BLAKE2b's final block (RFC 7693 section 3.3)
+    uint64_t h[8];
+    b2_init256(h);
+    const uint32_t nfull = L / 128;
+    for (uint32_t bk = 0; bk < nfull; bk++) {
+      uint64_t m[16];
+      for (int j = 0; j < 16; j++) m[j] = ld64le(psk + 128 * bk + 8 * j);
+      b2_compress(h, m, 128ull * (bk + 1), false);
+    }
+    const uint32_t tail = L - 128 * nfull, tot = tail + kSalamanderSalt;
+    if (tail) memcpy(tm, psk + 128 * nfull, tail);
+    memcpy(e->h, h, sizeof h);
+    for (int j = 0; j < 32; j++) e->m[j] = ld64le(tm + 8 * j);
+    e->nblocks = tot > 128 ? 2 : 1;
+    e->salt_pos = tail;
+    e->t_first = 128ull * nfull + 128;
+    e->t_last = 128ull * nfull + tot;
+  } else {
+    // SHA-256: 0x80 pad and the 64-bit big-endian bit length
+    uint32_t st[8];
+    s2_init(st);
+    const uint32_t nfull = L / 64;
+    for (uint32_t bk = 0; bk < nfull; bk++) {
+      uint32_t m[16];
+      for (int j = 0; j < 16; j++) m[j] = ld32be(psk + 64 * bk + 4 * j);
+      s2_compress(st, m);
+    }
+    const uint32_t tail = L - 64 * nfull, used = tail + kXPlusSalt + 1 + 8;
+    const uint32_t nb = used > 64 ? 2 : 1;
+    if (tail) memcpy(tm, psk + 64 * nfull, tail);
+    tm[tail + kXPlusSalt] = 0x80;
+    const uint64_t bits = ((uint64_t)L + kXPlusSalt) * 8;
+    for (int i = 0; i < 8; i++) tm[64 * nb - 1 - i] = (uint8_t)(bits >> (8 * i));
+    uint32_t *h32 = reinterpret_cast<uint32_t *>(e->h);
+    for (int i = 0; i < 8; i++) h32[i] = st[i];
+    uint32_t *m32 = reinterpret_cast<uint32_t *>(e->m);
+    for (int j = 0; j < 32; j++) m32[j] = ld32be(tm + 4 * j);
+    e->nblocks = nb;
+    e->salt_pos = tail;
+  }
+}
+
+void derive_key(const PskEntry &e, const uint8_t *salt, uint8_t key[32]) {
+  if (e.kind == SQOBFS_SALAMANDER) {
+    // the final block(s): the entry's template (PSK tail, zero padded) with
+    // the salt at salt_pos; on a little-endian host the words are the bytes
+    uint8_t blk[256];
+    memcpy(blk, e.m, sizeof blk);
+    memcpy(blk + e.salt_pos, salt, kSalamanderSalt);
+    uint64_t h[8], m[16];
+    memcpy(h, e.h, sizeof h);
+    for (uint32_t b = 0; b < e.nblocks; b++) {
+      memcpy(m, blk + 128 * b, 128);
+      const bool last = b + 1 == e.nblocks;
+      b2_compress(h, m, last ? e.t_last : e.t_first, last);
+    }
+    memcpy(key, h, 32);
+  } else {
+    // big-endian words: byte i of the block is bits 24 - 8 (i % 4) of word i / 4
+    uint32_t m[32];
+    memcpy(m, e.m, sizeof m);
+    for (uint32_t k = 0; k < (uint32_t)kXPlusSalt; k++) {
+      const uint32_t i = e.salt_pos + k;
+      m[i / 4] |= (uint32_t)salt[k] << (24 - 8 * (i % 4));
+    }
+    uint32_t st[8];
+    memcpy(st, e.h, sizeof st);
+    for (uint32_t b = 0; b < e.nblocks; b++) s2_compress(st, m + 16 * b);
+    for (int i = 0; i < 8; i++) {
+      key[4 * i] = (uint8_t)(st[i] >> 24);
+      key[4 * i + 1] = (uint8_t)(st[i] >> 16);
+      key[4 * i + 2] = (uint8_t)(st[i] >> 8);
+      key[4 * i + 3] = (uint8_t)st[i];
+    }
+  }
+}
+
+// 32 bytes per iteration as four 64-bit words (the compiler widens the loop
+// to vector registers); the key's period is 32, so the key words are fixed.
+void xor_stream(uint8_t *dst, const uint8_t *src, size_t n, const uint8_t key[32]) {
+  uint64_t k[4];
+  memcpy(k, key, 32);
+  size_t j = 0;
+  for (; j + 32 <= n; j += 32) {
+    uint64_t w[4];
+    memcpy(w, src + j, 32);
+    w[0] ^= k[0];
+    w[1] ^= k[1];
+    w[2] ^= k[2];
+    w[3] ^= k[3];
+    memcpy(dst + j, w, 32);
+  }
+  for (; j < n; j++) dst[j] = src[j] ^ key[j & 31];
+}
+
+void salt_stream(const uint32_t key[8], uint64_t seq, uint8_t *out, size_t bytes) {
+  const uint32_t nonce[3] = {0x626f7173u /* "sqob" */, (uint32_t)seq, (uint32_t)(seq >> 32)};
+  uint32_t blk[16];
+  for (size_t o = 0, c = 0; o < bytes; o += 64, c++) {
+    chacha20_block(key, (uint32_t)c, nonce, blk);
+    const size_t k = bytes - o < 64 ? bytes - o : 64;
+    memcpy(out + o, blk, k);  // little-endian words are the keystream bytes
+  }
+}
+
+int run_batch(int kind, int dir, const PskEntry *table, uint32_t count, const sqobfs_batch *b,
+              const uint8_t *salts) {
+  if (!b || !table || count == 0) return SQ_EINVAL;
+  if (b->n == 0) return SQ_OK;
+  if (!b->in || !b->in_off || !b->in_len || !b->out || !b->out_off || !b->out_len)
+    return SQ_EINVAL;
+  const size_t S = kind == SQOBFS_SALAMANDER ? kSalamanderSalt : kXPlusSalt;
+  const bool obfs = dir == SQOBFS_OBFUSCATE;
+  if (obfs && !salts && !b->salt) return SQ_EINVAL;
+  for (uint32_t i = 0; i < b->n; i++) {
+    const uint32_t pid = b->psk_id ? b->psk_id[i] : 0u;
+    const uint64_t len = b->in_len[i];
+    const uint64_t cap = (!obfs && kind == SQOBFS_XPLUS && b->in_cap && b->in_cap[i] > len)
+                             ? b->in_cap[i] : len;
+    if (len > kMaxPacket || cap > kMaxPacket) {
+      b->out_len[i] = kBadLen;
+      continue;
+    }
+    if (pid >= count) {
+      b->out_len[i] = SQOBFS_BAD_PSK;
+      continue;
+    }
+    const uint8_t *in = b->in + b->in_off[i];
+    uint8_t *out = b->out + b->out_off[i];
+    uint8_t key[32];
+    if (obfs) {  // salamander.go:57-70, xplus.go:62-75: salt || payload ^ key
+      const uint8_t *salt = salts ? salts + (size_t)i * S : b->salt + (size_t)i * S;
+      uint8_t s[16];
+      memcpy(s, salt, S);  // (the salt may sit where the output goes)
+      derive_key(table[pid], s, key);
+      xor_stream(out + S, in, len, key);
+      memcpy(out, s, S);
+      b->out_len[i] = (uint32_t)(S + len);
+    } else if (kind == SQOBFS_SALAMANDER && len <= S) {
+      memmove(out, in, len);  // salamander.go:47-49: returned as is
+      b->out_len[i] = (uint32_t)len;
+    } else if (kind == SQOBFS_XPLUS && len < S) {
+      b->out_len[i] = 0;  // xplus.go:50-52
+    } else {  // salamander.go:50-53, xplus.go:54-57 (XPlus to len(p) = cap)
+      derive_key(table[pid], in, key);
+      xor_stream(out, in + S, cap - S, key);
+      b->out_len[i] = (uint32_t)(len - S);
+    }
+  }
+  return SQ_OK;
+}
+
+}  // namespace cpu
+}  // namespace sq
+
+// ---- the process's host salt generator (keyrings without a context):
+// ChaCha20 keyed from getrandom(2) once, one sequence number per use
+void sq_host_salt_take(uint32_t key[8], uint64_t *seq) {
+  static std::once_flag once;
+  static uint32_t k[8];
+  static std::atomic<uint64_t> next{0};
+  std::call_once(once, [] {
+    uint8_t b[32];
+    size_t got = 0;
+    while (got < sizeof b) {
+      const ssize_t r = getrandom(b + got, sizeof b - got, 0);
+      if (r > 0) got += (size_t)r;
+    }
+    memcpy(k, b, sizeof k);
+  });
+  memcpy(key, k, sizeof k);
+  *seq = next.fetch_add(1);
+}

@@ -18,7 +18,6 @@
 // sync).  A socket batch is a few hundred KiB, so one launch + sync costs far
 // less than the staged H2D | kernel | D2H of sqobfs_run_host.
 #include <errno.h>
-#include <hip/hip_runtime.h>
 #include <netinet/in.h>
 #include <netinet/udp.h>
 #include <poll.h>
@@ -421,16 +420,11 @@ int sqobfs_udp_conn_open(sqobfs_ctx *ctx, const sqobfs_keyring *kr, const int *f
   // salts (8 B each) | 2 u16 packet-number offset arrays
   const size_t sb = (size_t)slots * slot_bytes, a64 = 8ull * slots, a32 = 4ull * slots;
   const size_t bytes = 2 * sb + 7 * a64 + 4 * a32 + 8ull * slots + 4ull * slots;
-  if (sqobfs_host_alloc(ctx, bytes, &c->block) != SQ_OK) {
+  // page-locked and mapped: the GPU reads and writes it at the same address
+  const int st = sq_host_alloc_mapped(ctx, bytes, &c->block);
+  if (st != SQ_OK) {
     delete c;
-    return SQ_ENOMEM;
-  }
-  void *dev = nullptr;  // the GPU's view of the block (the same address on ROCm)
-  if (hipHostGetDevicePointer(&dev, c->block, 0) != hipSuccess || dev != c->block) {
-    (void)hipGetLastError();
-    sqobfs_host_free(ctx, c->block);
-    delete c;
-    return SQ_EDEVICE;
+    return st;
   }
   uint8_t *p = (uint8_t *)c->block;
   c->rx = p;                                 p += sb;

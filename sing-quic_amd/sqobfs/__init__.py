@@ -1,8 +1,10 @@
 """ctypes binding of libsqobfs.so (include/sqobfs.h) for tests and bench.py.
 
 The product is the C ABI + gfx950 kernels; this module is plumbing.  It
-loads the in-tree ``sing-quic_amd/libsqobfs.so`` and raises if it is missing
--- there is no CPU fallback anywhere in the product path.
+loads the in-tree ``sing-quic_amd/libsqobfs.so`` and raises if it is missing.
+Device entry points never fall back to the CPU; the product's CPU path is
+explicit (host keyrings, ``cpu_run``, and the packet conn engine's small or
+GPU-less batches, include/sqobfs.h).
 
 Names mirror the reference's obfuscation layer:
   hysteria2/salamander.go  -> SALAMANDER, salt 8, BLAKE2b-256
@@ -222,6 +224,16 @@ def load(path: str) -> ctypes.CDLL:
     L.sqobfs_pconn_tx_take.argtypes = [vp, i32, vp]
     L.sqobfs_pconn_tx_done.argtypes = [vp]
     L.sqobfs_pconn_stats_get.argtypes = [vp, vp]
+    if not hasattr(L, "sqobfs_cpu_run"):
+        return L  # ABI 4
+    L.sqobfs_cpu_run.argtypes = [vp, i32, ctypes.POINTER(Batch)]
+    L.sqobfs_keyring_release_stream.argtypes = [vp, vp]
+    L.sqobfs_debug_keyring_check.argtypes = [vp]
+    L.sqobfs_engine_info_get.argtypes = [vp, vp]
+    L.sqobfs_engine_set_workers.argtypes = [vp, u32]
+    L.sqobfs_engine_trim.argtypes = [vp]
+    L.sqobfs_debug_engine_fail.argtypes = [i32, i32]
+    L.sqobfs_debug_engine_fail.restype = None
     return L
 
 
@@ -330,16 +342,17 @@ class Context:
 class Keyring:
     """Device copy of the PSK(s): the `password` field of
     SalamanderPacketConn (salamander.go:19-22) / `key` of XPlusPacketConn
-    (xplus.go:39-44)."""
+    (xplus.go:39-44).  ctx=None makes a host keyring (no GPU: cpu_run and
+    packet conns opened without a context)."""
 
-    def __init__(self, ctx: Context, kind: int, psks: list[bytes]):
+    def __init__(self, ctx: Context | None, kind: int, psks: list[bytes]):
         blob = np.frombuffer(b"".join(psks) + b"\0", dtype=np.uint8).copy()
         lens = np.array([len(p) for p in psks], dtype=np.uint32)
         offs = np.zeros(len(psks), dtype=np.uint64)
         if len(psks) > 1:
             offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
         h = ctypes.c_void_p()
-        _check(lib().sqobfs_keyring_create(ctx.handle, kind, len(psks), _ptr(blob),
+        _check(lib().sqobfs_keyring_create(ctx.handle if ctx else None, kind, len(psks), _ptr(blob),
                                            _ptr(offs), _ptr(lens), ctypes.byref(h)),
                "sqobfs_keyring_create")
         self.handle = h
@@ -352,11 +365,37 @@ class Keyring:
             lib().sqobfs_keyring_destroy(self.handle)
             self.handle = None
 
+    def device_check(self) -> int:
+        """Entries whose device hash state differs from the host copy."""
+        st = lib().sqobfs_debug_keyring_check(self.handle)
+        if st < 0:
+            raise SqError(st, "sqobfs_debug_keyring_check")
+        return st
+
     def __enter__(self):
         return self
 
     def __exit__(self, *exc):
         self.close()
+
+
+def cpu_run(kr: Keyring, direction: int, batch: Batch) -> None:
+    """The product's CPU path over a host batch (sqobfs_cpu_run)."""
+    _check(lib().sqobfs_cpu_run(kr.handle, direction, ctypes.byref(batch)), "sqobfs_cpu_run")
+
+
+class EngineInfo(ctypes.Structure):
+    _fields_ = [("pconns", ctypes.c_uint32), ("threads", ctypes.c_uint32),
+                ("workers", ctypes.c_uint32), ("pool_blocks", ctypes.c_uint32),
+                ("pool_bytes", ctypes.c_uint64), ("blocks_in_use", ctypes.c_uint32),
+                ("gpu_disabled", ctypes.c_uint32)]
+
+
+def engine_info(ctx: Context | None) -> EngineInfo:
+    info = EngineInfo()
+    _check(lib().sqobfs_engine_info_get(ctx.handle if ctx else None, ctypes.byref(info)),
+           "sqobfs_engine_info_get")
+    return info
 
 
 def make_batch(n, in_, in_off, in_len, out, out_off, out_len, salt=None,

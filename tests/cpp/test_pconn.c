@@ -17,7 +17,20 @@
  *             receive batch full and no reader returns promptly; writes
  *             queued before Close still go out
  *   pump      the generic-PacketConn mode (tx_take / rx_push) with tags
- *   memory    sqobfs_host_alloc blocks balance after every Close
+ *   memory    every batch block is back in the engine's pool after every
+ *             Close, and sqobfs_host_alloc blocks balance once it is trimmed
+ *   syncerr   an inline write returns its own send error (the reference's
+ *             WriteTo); with inline writes off, the next write reports it
+ *   shared    8 pconns on one context: one engine (threads flat), blocks
+ *             taken only while datagrams are in flight, wire == reference
+ *   routing   small batches on the CPU path, bursts on the GPU
+ *   fail      injected launch failures: a refused launch is redone on the
+ *             CPU, a failed kernel's batch is dropped, and every datagram
+ *             after either still reads / writes as the reference's
+ * Modes (argv[1]): "gpu" (default: a context on GPU 0; with the CPU device
+ * of tests/cpp/sq_devstub.cpp in the sanitizer builds) and "nodev" (no
+ * context: host keyrings, every batch on the CPU path -- the drop-in with no
+ * GPU at all).
  * Build and run: tests/test_pconn.py (gcc, -lsqobfs -loracle -lpthread). */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
@@ -57,7 +70,19 @@ static const uint8_t PSK[] = "sing-quic-mi355x-bench-psk";
 #define PL (sizeof PSK - 1)
 #define MAXW 4096
 
-static sqobfs_ctx *g_ctx;
+static sqobfs_ctx *g_ctx; /* NULL: nodev mode */
+static int g_nodev;
+
+/* every block back in the engine's pool; trimmed, the pinned allocations
+ * balance */
+static void check_mem(int64_t a0) {
+  sqobfs_engine_info info;
+  CHECK(sqobfs_engine_info_get(g_ctx, &info));
+  EXPECT(info.blocks_in_use == 0, "%u batch blocks still in use", info.blocks_in_use);
+  sqobfs_engine_trim(g_ctx);
+  EXPECT(sqobfs_debug_host_allocs() == a0, "host allocs %lld -> %lld", (long long)a0,
+         (long long)sqobfs_debug_host_allocs());
+}
 
 static double now_s(void) {
   struct timespec ts;
@@ -218,7 +243,11 @@ static void t_wire(int kind, uint32_t offload) {
     EXPECT(!memcmp(ref, wire[i], (size_t)wlen[i]), "kind %d dgram %d: wire differs", kind, i);
   }
   sqobfs_pconn_stats st;
-  CHECK(sqobfs_pconn_stats_get(pc, &st));
+  for (int k = 0; k < 500; k++) { /* (a batch is counted after its send returns) */
+    CHECK(sqobfs_pconn_stats_get(pc, &st));
+    if (st.tx_datagrams == (uint64_t)N) break;
+    sleep_ms(1);
+  }
   EXPECT(st.tx_datagrams == (uint64_t)N, "tx_datagrams %llu", (unsigned long long)st.tx_datagrams);
   printf("  wire kind %d%s: %d datagrams in %llu batches (max %u), wire == reference\n", kind,
          offload ? " (GSO)" : "", N, (unsigned long long)st.tx_batches, st.tx_max_batch);
@@ -226,8 +255,7 @@ static void t_wire(int kind, uint32_t offload) {
   close(fa);
   close(fp);
   sqobfs_keyring_destroy(kr);
-  EXPECT(sqobfs_debug_host_allocs() == a0, "host allocs %lld -> %lld", (long long)a0,
-         (long long)sqobfs_debug_host_allocs());
+  check_mem(a0);
 }
 
 /* ------------------------------------------------------------ read */
@@ -288,7 +316,7 @@ static void t_read(int kind) {
   close(fa);
   close(fp);
   sqobfs_keyring_destroy(kr);
-  EXPECT(sqobfs_debug_host_allocs() == a0, "host allocs leak");
+  check_mem(a0);
 }
 
 /* ------------------------------------------------------------ roundtrip */
@@ -363,7 +391,7 @@ static void t_roundtrip(int kind, uint32_t offload) {
   close(fa);
   close(fb);
   sqobfs_keyring_destroy(kr);
-  EXPECT(sqobfs_debug_host_allocs() == a0, "host allocs leak");
+  check_mem(a0);
 }
 
 /* ------------------------------------------------------------ deadlines */
@@ -433,7 +461,7 @@ static void t_deadline(void) {
   close(fa);
   close(fp);
   sqobfs_keyring_destroy(kr);
-  EXPECT(sqobfs_debug_host_allocs() == a0, "host allocs leak");
+  check_mem(a0);
 }
 
 /* ------------------------------------------------------------ shutdown */
@@ -497,7 +525,7 @@ static void t_shutdown(void) {
   close(fa);
   close(fp);
   sqobfs_keyring_destroy(kr);
-  EXPECT(sqobfs_debug_host_allocs() == a0, "host allocs leak");
+  check_mem(a0);
 }
 
 /* ------------------------------------------------------------ pump */
@@ -568,7 +596,7 @@ static void t_pump(int kind) {
   sqobfs_pconn_close(pc);
   CHECK(sqobfs_pconn_open(g_ctx, kr, -1, NULL, &pc));
   CHECK(sqobfs_pconn_rx_fail(pc, SQ_EIO, 1)); /* once: one reader sees it, reads go on */
-  uint8_t buf[64], w[40], s8[8] = {5}, p8[32] = {6};
+  uint8_t buf[64], w[40], s8[16] = {5}, p8[32] = {6};
   uint32_t n;
   EXPECT(sqobfs_pconn_read(pc, buf, sizeof buf, &n, NULL, NULL) == SQ_EIO, "rx_fail once");
   ref_write(kind, s8, p8, (size_t)(40 - S), w);
@@ -582,13 +610,285 @@ static void t_pump(int kind) {
   printf("  pump kind %d: %d datagrams taken == reference WriteTo, %d pushed == ReadFrom\n", kind,
          N, N);
   sqobfs_keyring_destroy(kr);
-  EXPECT(sqobfs_debug_host_allocs() == a0, "host allocs leak");
+  check_mem(a0);
+}
+
+/* ------------------------------------------------------------ syncerr */
+static void t_syncerr(int kind) {
+  const int S = salt_len(kind);
+  const int64_t a0 = sqobfs_debug_host_allocs();
+  sqobfs_keyring *kr = keyring(kind);
+  uint16_t pa, pp;
+  int fa = udp_socket(&pa), fp = udp_socket(&pp);
+  const sqobfs_addr to = loop_addr(pp), bad = loop_addr(0); /* UDP to port 0: EINVAL */
+  uint8_t p[100], w[MAXW], ref[MAXW];
+  for (int i = 0; i < 100; i++) p[i] = (uint8_t)rnd();
+  /* 1. inline (the default): the failing write itself returns the error, the
+   *    next one is clean and its datagram is the reference's */
+  sqobfs_pconn *pc = NULL;
+  CHECK(sqobfs_pconn_open(g_ctx, kr, fa, NULL, &pc));
+  sleep_ms(2);
+  int st = sqobfs_pconn_write(pc, p, 100, &bad, 0);
+  EXPECT(st == SQOBFS_ERRNO(EINVAL), "kind %d: inline write to port 0 returned %d", kind, st);
+  sleep_ms(2);
+  CHECK(sqobfs_pconn_write(pc, p, 100, &to, 0));
+  long n = recv_to(fp, w, sizeof w, 2000);
+  EXPECT(n == 100 + S, "kind %d: inline datagram %ld", kind, n);
+  ref_write(kind, w, p, 100, ref);
+  EXPECT(!memcmp(ref, w, (size_t)n), "kind %d: inline wire differs", kind);
+  sqobfs_pconn_stats sa;
+  CHECK(sqobfs_pconn_stats_get(pc, &sa));
+  EXPECT(sa.inline_writes == 2 && sa.tx_datagrams == 1, "inline stats %llu %llu",
+         (unsigned long long)sa.inline_writes, (unsigned long long)sa.tx_datagrams);
+  sqobfs_pconn_close(pc);
+  /* 2. every write batched: the error of a sent batch is reported once, by
+   *    the next write (which then queues nothing), and later writes work */
+  sqobfs_pconn_opts o;
+  memset(&o, 0, sizeof o);
+  o.inline_gap_us = SQOBFS_PCONN_NEVER;
+  CHECK(sqobfs_pconn_open(g_ctx, kr, fa, &o, &pc));
+  CHECK(sqobfs_pconn_write(pc, p, 100, &bad, 0));
+  sleep_ms(50);
+  st = sqobfs_pconn_write(pc, p, 100, &to, 0);
+  EXPECT(st == SQOBFS_ERRNO(EINVAL), "kind %d: batched error reported by %d", kind, st);
+  CHECK(sqobfs_pconn_write(pc, p, 100, &to, 0));
+  n = recv_to(fp, w, sizeof w, 2000);
+  EXPECT(n == 100 + S, "kind %d: batched datagram %ld", kind, n);
+  EXPECT(recv_to(fp, w, sizeof w, 50) < 0, "the reporting write queued nothing");
+  CHECK(sqobfs_pconn_stats_get(pc, &sa));
+  EXPECT(sa.inline_writes == 0 && sa.tx_send_errors == 1, "batched stats");
+  sqobfs_pconn_close(pc);
+  printf("  syncerr kind %d: inline write -> its own EINVAL; batched -> the next write's\n", kind);
+  close(fa);
+  close(fp);
+  sqobfs_keyring_destroy(kr);
+  check_mem(a0);
+}
+
+/* ------------------------------------------------------------ shared */
+typedef struct {
+  sqobfs_pconn *pc;
+  int kind, n, fp, bad, got;
+  uint16_t port;
+} Lane;
+
+static void *lane_run(void *arg) {
+  Lane *l = arg;
+  const int S = salt_len(l->kind);
+  const sqobfs_addr to = loop_addr(l->port);
+  uint8_t p[1400], w[MAXW], ref[MAXW];
+  for (int i = 0; i < l->n; i++) {
+    const uint32_t L = 1 + (uint32_t)(i * 37 % 1399);
+    for (uint32_t j = 0; j < L; j++) p[j] = (uint8_t)(i + j * 7 + l->port);
+    CHECK(sqobfs_pconn_write(l->pc, p, L, &to, 0));
+    const long n = recv_to(l->fp, w, sizeof w, 2000);
+    if (n != (long)L + S) {
+      l->bad++;
+      continue;
+    }
+    ref_write(l->kind, w, p, L, ref);
+    if (memcmp(ref, w, (size_t)n)) l->bad++;
+    l->got++;
+  }
+  return NULL;
+}
+
+static void t_shared(void) {
+  enum { K = 8, N = 300 };
+  const int64_t a0 = sqobfs_debug_host_allocs();
+  sqobfs_keyring *kr[2] = {keyring(0), keyring(1)};
+  sqobfs_pconn *one = NULL;
+  uint16_t p1;
+  int f1 = udp_socket(&p1);
+  CHECK(sqobfs_pconn_open(g_ctx, kr[0], f1, NULL, &one));
+  sqobfs_engine_info i1, i8, iend, peak;
+  CHECK(sqobfs_engine_info_get(g_ctx, &i1));
+  Lane ln[K];
+  int fa[K];
+  pthread_t th[K];
+  for (int k = 0; k < K; k++) {
+    uint16_t pa;
+    fa[k] = udp_socket(&pa);
+    ln[k].fp = udp_socket(&ln[k].port);
+    ln[k].kind = k % 2;
+    ln[k].n = N;
+    ln[k].bad = ln[k].got = 0;
+    sqobfs_pconn_opts o;
+    memset(&o, 0, sizeof o);
+    o.inline_gap_us = SQOBFS_PCONN_NEVER; /* through the engine's workers */
+    CHECK(sqobfs_pconn_open(g_ctx, kr[k % 2], fa[k], &o, &ln[k].pc));
+  }
+  CHECK(sqobfs_engine_info_get(g_ctx, &i8));
+  for (int k = 0; k < K; k++) pthread_create(&th[k], NULL, lane_run, &ln[k]);
+  for (int k = 0; k < K; k++) pthread_join(th[k], NULL);
+  CHECK(sqobfs_engine_info_get(g_ctx, &peak));
+  for (int k = 0; k < K; k++) {
+    EXPECT(ln[k].got == N && ln[k].bad == 0, "shared conn %d: got %d bad %d", k, ln[k].got,
+           ln[k].bad);
+    sqobfs_pconn_close(ln[k].pc);
+    close(fa[k]);
+    close(ln[k].fp);
+  }
+  CHECK(sqobfs_engine_info_get(g_ctx, &iend));
+  EXPECT(i8.pconns == i1.pconns + (uint32_t)K, "pconns %u -> %u", i1.pconns, i8.pconns);
+  EXPECT(i8.threads == i1.threads && i8.threads == i1.workers + 1,
+         "threads %u with 1 conn, %u with 9 (workers %u)", i1.threads, i8.threads, i1.workers);
+  EXPECT(peak.pool_blocks <= 2 * (uint32_t)K + 2, "pool grew to %u blocks for %d conns",
+         peak.pool_blocks, K);
+  EXPECT(iend.blocks_in_use == 0, "blocks in use after close: %u", iend.blocks_in_use);
+  printf("  shared: 9 conns on one engine: %u threads (as with 1), pool %u blocks (%.1f MiB) "
+         "after %d x %d datagrams, wire == reference\n", i8.threads, peak.pool_blocks,
+         peak.pool_bytes / 1048576.0, K, N);
+  sqobfs_pconn_close(one);
+  close(f1);
+  sqobfs_keyring_destroy(kr[0]);
+  sqobfs_keyring_destroy(kr[1]);
+  check_mem(a0);
+}
+
+/* ------------------------------------------------------------ routing */
+static void t_routing(void) {
+  const int64_t a0 = sqobfs_debug_host_allocs();
+  sqobfs_keyring *kr = keyring(SQOBFS_SALAMANDER);
+  uint16_t pa, pp;
+  int fa = udp_socket(&pa), fp = udp_socket(&pp);
+  sqobfs_pconn *pc = NULL;
+  sqobfs_pconn_opts o;
+  memset(&o, 0, sizeof o);
+  o.inline_gap_us = SQOBFS_PCONN_NEVER;
+  CHECK(sqobfs_pconn_open(g_ctx, kr, fa, &o, &pc));
+  const sqobfs_addr to = loop_addr(pp);
+  static uint8_t pay[2000][1400];
+  uint8_t w[MAXW], ref[MAXW];
+  /* lone datagrams: CPU batches */
+  for (int i = 0; i < 5; i++) {
+    for (int j = 0; j < 1350; j++) pay[i][j] = (uint8_t)rnd();
+    CHECK(sqobfs_pconn_write(pc, pay[i], 1350, &to, 0));
+    EXPECT(recv_to(fp, w, sizeof w, 2000) == 1358, "lone datagram");
+    ref_write(0, w, pay[i], 1350, ref);
+    EXPECT(!memcmp(ref, w, 1358), "lone datagram wire");
+  }
+  sqobfs_pconn_stats a;
+  for (int k = 0; k < 200; k++) { /* (the worker counts a batch after its send) */
+    CHECK(sqobfs_pconn_stats_get(pc, &a));
+    if (a.tx_datagrams == 5) break;
+    sleep_ms(1);
+  }
+  EXPECT(a.cpu_batches == 5 && a.tx_batches == 5, "lone datagrams: %llu CPU of %llu batches",
+         (unsigned long long)a.cpu_batches, (unsigned long long)a.tx_batches);
+  /* a burst: batches grow past cpu_max and launch */
+  for (int i = 0; i < 2000; i++) {
+    for (int j = 0; j < 1350; j += 8) pay[i][j] = (uint8_t)rnd();
+    CHECK(sqobfs_pconn_write(pc, pay[i], 1350, &to, 0));
+  }
+  int got = 0, bad = 0;
+  for (int i = 0; i < 2000; i++) {
+    const long n = recv_to(fp, w, sizeof w, 2000);
+    if (n < 0) break;
+    ref_write(0, w, pay[i], 1350, ref);
+    if (n != 1358 || memcmp(ref, w, 1358)) bad++;
+    got++;
+  }
+  sqobfs_pconn_stats b;
+  for (int k = 0; k < 200; k++) {
+    CHECK(sqobfs_pconn_stats_get(pc, &b));
+    if (b.tx_datagrams == 2005) break;
+    sleep_ms(1);
+  }
+  EXPECT(got == 2000 && bad == 0, "burst: got %d bad %d", got, bad);
+  const uint64_t gpu = (b.tx_batches - a.tx_batches) - (b.cpu_batches - a.cpu_batches);
+  EXPECT(gpu > 0, "the burst never launched (%llu batches, max %u)",
+         (unsigned long long)(b.tx_batches - a.tx_batches), b.tx_max_batch);
+  printf("  routing: 5 lone datagrams -> 5 CPU batches; a 2000-datagram burst -> %llu batches "
+         "(%llu on the GPU, max %u)\n", (unsigned long long)(b.tx_batches - a.tx_batches),
+         (unsigned long long)gpu, b.tx_max_batch);
+  sqobfs_pconn_close(pc);
+  close(fa);
+  close(fp);
+  sqobfs_keyring_destroy(kr);
+  check_mem(a0);
+}
+
+/* ------------------------------------------------------------ fail */
+/* On a context of its own (a failure turns its engine to the CPU for good).
+ * at_completion 0: the launch is refused -> the batch is redone on the CPU;
+ * 1: the kernel "faults" after running -> the batch is dropped. */
+static void t_fail(int at_completion) {
+  sqobfs_ctx *ctx = NULL;
+  CHECK(sqobfs_open(0, &ctx));
+  const int64_t a0 = sqobfs_debug_host_allocs();
+  for (int kind = 0; kind < 2; kind++) {
+    const int S = salt_len(kind);
+    uint64_t off = 0;
+    uint32_t plen_psk = PL;
+    sqobfs_keyring *kr = NULL;
+    CHECK(sqobfs_keyring_create(ctx, kind, 1, PSK, &off, &plen_psk, &kr));
+    sqobfs_pconn *pc = NULL;
+    sqobfs_pconn_opts o;
+    memset(&o, 0, sizeof o);
+    o.cpu_max = SQOBFS_PCONN_NEVER; /* every batch launches while the GPU works */
+    CHECK(sqobfs_pconn_open(ctx, kr, -1, &o, &pc));
+    static uint8_t pay[400][2048];
+    static uint32_t plen[400];
+    for (int i = 0; i < 400; i++) {
+      plen[i] = pick_len(i, S, 2048);
+      for (uint32_t j = 0; j < plen[i]; j++) pay[i][j] = (uint8_t)rnd();
+    }
+    /* transmit: 100 before the failure, the failure, 300 after */
+    Taker t = {pc, kind, 0, 0, pay, plen};
+    pthread_t th;
+    pthread_create(&th, NULL, taker, &t);
+    for (int i = 0; i < 100; i++) CHECK(sqobfs_pconn_write(pc, pay[i], plen[i], NULL, (uint64_t)i));
+    sleep_ms(50);
+    if (kind == 0) sqobfs_debug_engine_fail(1, at_completion);
+    for (int i = 100; i < 400; i++) {
+      CHECK(sqobfs_pconn_write(pc, pay[i], plen[i], NULL, (uint64_t)i));
+      if (i % 50 == 0) sleep_ms(2);
+    }
+    sleep_ms(100);
+    sqobfs_pconn_stats st;
+    CHECK(sqobfs_pconn_stats_get(pc, &st));
+    /* receive: pushed datagrams still read back as the reference's ReadFrom
+     * (the engine is on the CPU now) */
+    for (int i = 0; i < 300; i++) {
+      uint8_t salt[16], w[MAXW], got[MAXW], ref[MAXW];
+      for (int b = 0; b < 16; b++) salt[b] = (uint8_t)rnd();
+      ref_write(kind, salt, pay[i], plen[i], w);
+      CHECK(sqobfs_pconn_rx_push(pc, w, plen[i] + (uint32_t)S, NULL, (uint64_t)i));
+      uint32_t n;
+      CHECK(sqobfs_pconn_read(pc, got, MAXW, &n, NULL, NULL));
+      const long want = ref_read(kind, w, plen[i] + (uint32_t)S, MAXW, ref);
+      EXPECT((long)n == want && (!n || !memcmp(got, ref, n)), "after failure: read %d", i);
+    }
+    sqobfs_pconn_shutdown(pc);
+    pthread_join(th, NULL);
+    sqobfs_engine_info info;
+    CHECK(sqobfs_engine_info_get(ctx, &info));
+    EXPECT(t.bad == 0, "fail kind %d: %d taken datagrams differ", kind, t.bad);
+    EXPECT(info.gpu_disabled == 1, "the engine did not switch to the CPU");
+    EXPECT(kind == 1 || st.gpu_failures == 1, "failure not counted");
+    if (at_completion)
+      EXPECT(t.count + (int)st.dropped == 400 && (kind == 1 || st.dropped > 0),
+             "fail kind %d: taken %d + dropped %llu != 400", kind, t.count,
+             (unsigned long long)st.dropped);
+    else
+      EXPECT(t.count == 400 && st.dropped == 0, "fail kind %d: taken %d of 400", kind, t.count);
+    printf("  fail kind %d (%s): %d of 400 datagrams taken == reference (%llu dropped), "
+           "%llu CPU batches; 300 reads after it == reference\n", kind,
+           at_completion ? "kernel failed" : "launch refused", t.count,
+           (unsigned long long)st.dropped, (unsigned long long)st.cpu_batches);
+    sqobfs_pconn_close(pc);
+    sqobfs_keyring_destroy(kr);
+  }
+  sqobfs_engine_trim(ctx);
+  EXPECT(sqobfs_debug_host_allocs() == a0, "fail: host allocs");
+  sqobfs_close(ctx);
 }
 
 int main(int argc, char **argv) {
-  (void)argc;
-  (void)argv;
-  CHECK(sqobfs_open(0, &g_ctx));
+  g_nodev = argc > 1 && !strcmp(argv[1], "nodev");
+  if (!g_nodev) CHECK(sqobfs_open(0, &g_ctx));
+  const int64_t a0 = sqobfs_debug_host_allocs();
   for (int kind = 0; kind < 2; kind++) {
     t_wire(kind, 0);
     t_wire(kind, SQOBFS_UDP_TX_GSO);
@@ -596,10 +896,23 @@ int main(int argc, char **argv) {
     t_roundtrip(kind, 0);
     t_roundtrip(kind, SQOBFS_UDP_TX_GSO | SQOBFS_UDP_RX_GRO);
     t_pump(kind);
+    t_syncerr(kind);
   }
   t_deadline();
   t_shutdown();
-  sqobfs_close(g_ctx);
-  printf("ok: pconn engine (socket + pump modes, deadlines, shutdown, memory)\n");
+  t_shared();
+  if (!g_nodev) {
+    t_routing();
+    t_fail(0);
+    t_fail(1);
+  }
+  sqobfs_engine_info info;
+  CHECK(sqobfs_engine_info_get(g_ctx, &info));
+  EXPECT(info.gpu_disabled == 0, "the shared engine switched to the CPU");
+  if (g_ctx) sqobfs_close(g_ctx);
+  EXPECT(sqobfs_debug_host_allocs() == a0, "host allocs after close");
+  printf("ok: pconn engine [%s] (socket + pump modes, deadlines, shutdown, memory, sync errors, "
+         "shared engine%s)\n", g_nodev ? "no device" : "device",
+         g_nodev ? "" : ", routing, launch failures");
   return 0;
 }

@@ -54,7 +54,7 @@ int main(void){printf("%zu %zu %zu %zu %zu\n", sizeof(sqobfs_batch),
 
 def test_abi_version_and_strerror():
     L = sqobfs.lib()
-    assert L.sqobfs_abi_version() == 4
+    assert L.sqobfs_abi_version() == 5
     for st in (0, -1, -2, -3, -4, -5, -6, -7, -8):
         assert sqobfs.strerror(st) != "unknown status"
 
@@ -71,7 +71,8 @@ def test_null_arguments_rejected_without_gpu():
 
 @pytest.mark.skipif(os.environ.get("SQ_ASSUME_GPU") == "1", reason="GPU box")
 def test_no_gpu_reports_enodev_not_fallback():
-    """Without a GPU the product fails loudly (no CPU fallback)."""
+    """Without a GPU the device entry points fail loudly (never a silent CPU
+    fallback); the CPU path is explicit (host keyrings, tests/test_cpu_path.py)."""
     import torch
     if torch.cuda.is_available():
         pytest.skip("GPU present")
