@@ -61,7 +61,10 @@ def parse():
     ap.add_argument("--inproc", type=int, default=0,
                     help="in-process sharding: one process, K contexts over the visible GPUs "
                          "(context k on GPU k mod count), the config's batch cut by bytes "
-                         "(sqobfs_shard_cuts) and launched with sqobfs_shard_run")
+                         "(sqobfs_shard_cuts) and launched with sqobfs_shard_launch")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="--inproc: shard steps in flight (1 = sqobfs_shard_run, a host round "
+                         "trip per step)")
     ap.add_argument("--unit-packets", type=int, default=0,
                     help="obfuscation kernel unit size, packets per wavefront (0 = sized "
                          "from the batch's bytes by sqobfs_unit_packets_for, as a caller "
@@ -410,8 +413,10 @@ def load_traffic(config: str, kernel_bytes: float):
 
 
 def inproc_bench(args):
-    """sqobfs_shard_run over K contexts in one process (the Go service's
-    multi-GPU path); one JSON line."""
+    """K contexts in one process (the Go service's multi-GPU path), steps of
+    sqobfs_shard_launch kept --inflight deep (each waited through its ticket;
+    --inflight 1: sqobfs_shard_run, a host round trip per step); one JSON
+    line."""
     import torch
     import sqobfs
     ndev = torch.cuda.device_count()
@@ -447,20 +452,28 @@ def inproc_bench(args):
         payload += sh["payload_bytes"]
     for d in set(devs):
         torch.cuda.synchronize(d)
-    for _ in range(args.warmup):
-        sqobfs.shard_run(ctxs, krs, sqobfs.OBFUSCATE, bs)
+    depth = max(1, args.inflight)
+
+    def steps(k):
+        pending = []
+        for _ in range(k):
+            pending.append(sqobfs.shard_launch(ctxs, krs, sqobfs.OBFUSCATE, bs))
+            if len(pending) >= depth:
+                pending.pop(0).wait()
+        for t in pending:
+            t.wait()
+    steps(args.warmup)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        sqobfs.shard_run(ctxs, krs, sqobfs.OBFUSCATE, bs)
+    steps(args.steps)
     el = time.perf_counter() - t0
     out = {"metric": f"GiB/s payload obfuscated, device-resident, {args.config}, "
-                     f"{K} in-process shards (sqobfs_shard_run)",
+                     f"{K} in-process shards (sqobfs_shard_launch, {depth} steps in flight)",
            "value": round(payload * args.steps / el / 2**30, 3), "unit": "GiB/s",
            "n_gpus": len(set(devs)), "contexts": K, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(el * 1e3 / args.steps, 4),
            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
            "data": "synthetic", "shard_packets": [int(cut[k + 1] - cut[k]) for k in range(K)],
-           "config": {"workload": args.config, "inproc": K}}
+           "config": {"workload": args.config, "inproc": K, "inflight": depth}}
     print(json.dumps(out), flush=True)
     for kr in krs:
         kr.close()

@@ -402,9 +402,27 @@ int sqobfs_shard_cuts(uint32_t n, const uint32_t *in_len, uint32_t parts, uint32
 int sqobfs_run_host_sharded(uint32_t nctx, sqobfs_ctx *const *ctxs,
                             const sqobfs_keyring *const *krs, int dir, const sqobfs_batch *hb);
 /* Device-resident shards: bs[k] lives on ctxs[k]'s GPU and is launched there
- * on the context's stream; returns after all shards complete (first error). */
+ * on the context's stream; returns after all shards complete (first error).
+ * = sqobfs_shard_launch + sqobfs_shard_wait. */
 int sqobfs_shard_run(uint32_t nctx, sqobfs_ctx *const *ctxs, const sqobfs_keyring *const *krs,
                      int dir, const sqobfs_batch *bs);
+/* The same without waiting: every shard is queued on its context's stream,
+ * one completion event is recorded per context, and the call returns at
+ * once with a ticket.  A caller keeps several steps in flight (launch step
+ * i + 1, then wait for step i) so no host round trip sits between one
+ * step's kernels and the next's.  Contexts may share a GPU.  On a failed
+ * launch the shards already queued are waited for and the error returned
+ * (no ticket). */
+typedef struct sqobfs_shard_ticket sqobfs_shard_ticket;
+int sqobfs_shard_launch(uint32_t nctx, sqobfs_ctx *const *ctxs, const sqobfs_keyring *const *krs,
+                        int dir, const sqobfs_batch *bs, sqobfs_shard_ticket **out);
+/* 1 when every shard of the ticket is done, 0 while one still runs, or an
+ * error status (the ticket stays valid: wait for it to release it). */
+int sqobfs_shard_query(sqobfs_shard_ticket *t);
+/* Wait for every shard (polling each context's stream for its
+ * sqobfs_set_sync_spin time, then blocking), release the ticket, return the
+ * first error. */
+int sqobfs_shard_wait(sqobfs_shard_ticket *t);
 
 /* Bytes of pinned staging sqobfs_run_host holds (it grows to the largest
  * batch span seen: the input and output byte ranges the batch touches, not

@@ -112,6 +112,15 @@ struct sqobfs_quic_keyring {
   uint32_t grk0[44], ghrk0[44], giv0[3];
 };
 
+// sqobfs_shard_launch: one completion event per context of the step
+struct sqobfs_shard_ticket {
+  struct Part {
+    sqobfs_ctx *ctx;
+    hipEvent_t ev;
+  };
+  std::vector<Part> parts;
+};
+
 struct sqobfs_keyring {
   sqobfs_ctx *ctx = nullptr;      // NULL: a host keyring (no device state)
   mutable KeyringUses uses;
@@ -1479,23 +1488,92 @@ int sqobfs_run_host_sharded(uint32_t nctx, sqobfs_ctx *const *ctxs,
   return SQ_OK;
 }
 
-int sqobfs_shard_run(uint32_t nctx, sqobfs_ctx *const *ctxs, const sqobfs_keyring *const *krs,
-                     int dir, const sqobfs_batch *bs) {
-  if (nctx == 0 || !ctxs || !krs || !bs) return SQ_EINVAL;
+int sqobfs_shard_launch(uint32_t nctx, sqobfs_ctx *const *ctxs, const sqobfs_keyring *const *krs,
+                        int dir, const sqobfs_batch *bs, sqobfs_shard_ticket **out) {
+  if (out) *out = nullptr;
+  if (nctx == 0 || !ctxs || !krs || !bs || !out) return SQ_EINVAL;
   for (uint32_t k = 0; k < nctx; k++)
     if (!ctxs[k] || !krs[k] || krs[k]->ctx != ctxs[k]) return SQ_EINVAL;
-  // launches are asynchronous: one host thread issues every shard on its
-  // context's stream, then waits for all of them
+  sqobfs_shard_ticket *t = new (std::nothrow) sqobfs_shard_ticket();
+  if (!t) return SQ_ENOMEM;
+  // launches are asynchronous: one host thread queues every shard on its
+  // context's stream and records the context's completion event after it
   int st = SQ_OK;
-  uint32_t launched = 0;
-  for (; launched < nctx && st == SQ_OK; launched++)
-    st = sqobfs_launch(ctxs[launched], krs[launched], dir, &bs[launched],
-                       sqobfs_stream(ctxs[launched]));
-  for (uint32_t k = 0; k < launched; k++) {
-    const int s2 = sqobfs_sync(ctxs[k], sqobfs_stream(ctxs[k]));
-    if (st == SQ_OK) st = s2;
+  for (uint32_t k = 0; k < nctx && st == SQ_OK; k++) {
+    st = sqobfs_launch(ctxs[k], krs[k], dir, &bs[k], ctxs[k]->stream);
+    if (st != SQ_OK) break;
+    DeviceScope ds_(ctxs[k]->device);
+    hipEvent_t e = nullptr;
+    st = hip_status(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (st == SQ_OK) {
+      st = hip_status(hipEventRecord(e, ctxs[k]->stream));
+      t->parts.push_back({ctxs[k], e});
+      if (st != SQ_OK) t->parts.back().ev = nullptr, (void)hipEventDestroy(e);
+    }
+    if (st != SQ_OK) {
+      // the shards queued so far: wait for them before reporting
+      for (uint32_t j = 0; j <= k; j++) (void)sqobfs_sync(ctxs[j], ctxs[j]->stream);
+    }
   }
+  if (st != SQ_OK) {
+    (void)sqobfs_shard_wait(t);
+    return st;
+  }
+  *out = t;
+  return SQ_OK;
+}
+
+int sqobfs_shard_query(sqobfs_shard_ticket *t) {
+  if (!t) return SQ_EINVAL;
+  for (auto &p : t->parts) {
+    if (!p.ev) continue;
+    DeviceScope ds_(p.ctx->device);
+    const hipError_t q = hipEventQuery(p.ev);
+    if (q == hipErrorNotReady) return 0;
+    if (q != hipSuccess) return hip_status(q);
+  }
+  return 1;
+}
+
+int sqobfs_shard_wait(sqobfs_shard_ticket *t) {
+  if (!t) return SQ_EINVAL;
+  int st = SQ_OK;
+  for (auto &p : t->parts) {
+    if (!p.ev) continue;
+    DeviceScope ds_(p.ctx->device);
+    // poll (sqobfs_set_sync_spin) before blocking, as sqobfs_sync does
+    const uint32_t spin = p.ctx->spin_us.load(std::memory_order_relaxed);
+    int s2 = 1;
+    if (spin) {
+      const auto t0 = std::chrono::steady_clock::now();
+      for (;;) {
+        const hipError_t q = hipEventQuery(p.ev);
+        if (q == hipSuccess) {
+          s2 = SQ_OK;
+          break;
+        }
+        if (q != hipErrorNotReady) {
+          s2 = hip_status(q);
+          break;
+        }
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin)) break;
+        cpu_relax();
+      }
+    }
+    if (s2 == 1) s2 = hip_status(hipEventSynchronize(p.ev));
+    if (st == SQ_OK) st = s2;
+    (void)hipEventDestroy(p.ev);
+  }
+  delete t;
   return st;
+}
+
+int sqobfs_shard_run(uint32_t nctx, sqobfs_ctx *const *ctxs, const sqobfs_keyring *const *krs,
+                     int dir, const sqobfs_batch *bs) {
+  sqobfs_shard_ticket *t = nullptr;
+  const int st = sqobfs_shard_launch(nctx, ctxs, krs, dir, bs, &t);
+  if (st != SQ_OK) return st;
+  return sqobfs_shard_wait(t);
 }
 
 }  // extern "C"

@@ -110,6 +110,11 @@ namespace sq {
 #ifndef SQ_WINSAFE
 #define SQ_WINSAFE 1  // unconditional window loads (fetch_windows)
 #endif
+// Unconditional window loads: an unneeded block reads the packet's own first
+// input block when it has one (1) instead of the descriptor entry (0).
+#ifndef SQ_WINPKT
+#define SQ_WINPKT 0
+#endif
 // XCD-contiguous units.  Workgroups are dispatched round-robin over the 8
 // XCDs, so block b runs on XCD b % 8 and, unmapped, the XCDs share one
 // moving window of the batch.  Remapped, each XCD walks its own contiguous
@@ -135,7 +140,7 @@ extern "C" const char *sqobfs_build_info(void) {
          " minw=" SQ_STR(SQ_MINW) " wpb=2"
          " ablate=" SQ_STR(SQ_ABLATE) " donate=" SQ_STR(SQ_DONATE) " align=" SQ_STR(SQ_ALIGN)
          " map=" SQ_STR(SQ_MAPBLK)
-         " winsafe=" SQ_STR(SQ_WINSAFE) " xcd=" SQ_STR(SQ_XCD);
+         " winsafe=" SQ_STR(SQ_WINSAFE) " winpkt=" SQ_STR(SQ_WINPKT) " xcd=" SQ_STR(SQ_XCD);
 }
 
 // default unit size (KParams.ppw == 0); any 1 .. kMaxUnitPackets works
@@ -575,6 +580,9 @@ __device__ __forceinline__ void fetch_windows(const PacketJob &J, bool wire_salt
   const uint64_t TB = ta & ~15ull;
   const bool c_t1 = c_t0 && te > TB + 16;
   if (WS) {
+    // (an aligned block holding one readable byte is readable: B holds the
+    // first payload byte whenever the packet needs a window at all)
+    if (SQ_WINPKT && c_h0) safe = B;
     const uint64_t a_s0 = c_s0 ? B - 16 : safe, a_h0 = c_h0 ? B : safe,
                    a_h1 = c_h1 ? B + 16 : safe, a_h2 = c_h2 ? B + 32 : safe,
                    a_t0 = c_t0 ? TB : safe, a_t1 = c_t1 ? TB + 16 : safe;

@@ -234,6 +234,9 @@ def load(path: str) -> ctypes.CDLL:
     L.sqobfs_engine_trim.argtypes = [vp]
     L.sqobfs_debug_engine_fail.argtypes = [i32, i32]
     L.sqobfs_debug_engine_fail.restype = None
+    L.sqobfs_shard_launch.argtypes = [u32, vp, vp, i32, vp, ctypes.POINTER(vp)]
+    L.sqobfs_shard_query.argtypes = [vp]
+    L.sqobfs_shard_wait.argtypes = [vp]
     return L
 
 
@@ -365,6 +368,11 @@ class Keyring:
             lib().sqobfs_keyring_destroy(self.handle)
             self.handle = None
 
+    def release_stream(self, stream: int) -> None:
+        """The caller is about to destroy `stream` (sqobfs_keyring_release_stream)."""
+        _check(lib().sqobfs_keyring_release_stream(self.handle, stream),
+               "sqobfs_keyring_release_stream")
+
     def device_check(self) -> int:
         """Entries whose device hash state differs from the host copy."""
         st = lib().sqobfs_debug_keyring_check(self.handle)
@@ -437,6 +445,34 @@ def shard_run(ctxs: list[Context], krs: list[Keyring], direction: int,
     arr = (Batch * len(batches))(*batches)
     _check(lib().sqobfs_shard_run(len(ctxs), _handles(ctxs), _handles(krs), direction, arr),
            "sqobfs_shard_run")
+
+
+class ShardTicket:
+    """A step of device-resident shards in flight (sqobfs_shard_launch)."""
+
+    def __init__(self, handle):
+        self.handle = handle
+
+    def done(self) -> bool:
+        st = lib().sqobfs_shard_query(self.handle)
+        if st < 0:
+            raise SqError(st, "sqobfs_shard_query")
+        return st == 1
+
+    def wait(self) -> None:
+        if self.handle:
+            h, self.handle = self.handle, None
+            _check(lib().sqobfs_shard_wait(h), "sqobfs_shard_wait")
+
+
+def shard_launch(ctxs: list[Context], krs: list[Keyring], direction: int,
+                 batches: list[Batch]) -> ShardTicket:
+    """Queue shard k on ctxs[k]'s stream; returns at once (wait on the ticket)."""
+    arr = (Batch * len(batches))(*batches)
+    h = ctypes.c_void_p()
+    _check(lib().sqobfs_shard_launch(len(ctxs), _handles(ctxs), _handles(krs), direction, arr,
+                                     ctypes.byref(h)), "sqobfs_shard_launch")
+    return ShardTicket(h)
 
 
 def debug_fail_chunk(chunk: int) -> None:

@@ -134,6 +134,81 @@ void *tput_reader(void *arg) {
   return NULL;
 }
 
+/* per-datagram latency through the packet conn engine (opts o, NULL =
+ * defaults): WriteTo bursts -> arrival at a peer socket; peer bursts ->
+ * ReadFrom */
+static void pconn_lat(sqobfs_ctx *ctx, sqobfs_keyring *kr, const char *label,
+                      const sqobfs_pconn_opts *o) {
+  static double v[MAXN * 400];
+  uint16_t pa, pp;
+  int fa = udp_socket(&pa), fp = udp_socket(&pp);
+  sqobfs_pconn *pc;
+  CHECK(sqobfs_pconn_open(ctx, kr, fa, o, &pc));
+  const sqobfs_addr to = loop_addr(pp);
+  static uint8_t pay[L], buf[4096], wire[MAXN][L + 8];
+  memset(pay, 5, L);
+  static double tw[MAXN];
+  printf("\"pconn_write%s\": {", label);
+  for (int k = 0; k < NS; k++) {
+    const int n = SIZES[k], it = iters_for(n) / 4 + 1;
+    int m = 0;
+    for (int i = 0; i < it + 5; i++) {
+      for (int j = 0; j < n; j++) {
+        tw[j] = now_us();
+        CHECK(sqobfs_pconn_write(pc, pay, L, &to, 0));
+      }
+      for (int j = 0; j < n; j++) {
+        if (recv_to(fp, buf, sizeof buf, 2000) < 0) exit(3);
+        if (i >= 5) v[m++] = now_us() - tw[j];
+      }
+    }
+    char nm[16];
+    snprintf(nm, sizeof nm, "%d", n);
+    print_stat(nm, v, m, k == NS - 1);
+  }
+  printf("}, ");
+  /* receive side: obfuscated datagrams from the peer */
+  for (int j = 0; j < MAXN; j++) {
+    uint8_t salt[8] = {(uint8_t)j, 1, 2, 3, 4, 5, 6, 7};
+    or_salamander_write(PSK, PL, salt, pay, L, wire[j]);
+  }
+  struct sockaddr_in a;
+  memset(&a, 0, sizeof a);
+  a.sin_family = AF_INET;
+  a.sin_port = htons(pa);
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  printf("\"pconn_read%s\": {", label);
+  for (int k = 0; k < NS; k++) {
+    const int n = SIZES[k], it = iters_for(n) / 4 + 1;
+    int m = 0;
+    for (int i = 0; i < it + 5; i++) {
+      const double t0 = now_us();
+      for (int j = 0; j < n; j++)
+        sendto(fp, wire[j], L + 8, 0, (struct sockaddr *)&a, sizeof a);
+      for (int j = 0; j < n; j++) {
+        uint32_t got;
+        CHECK(sqobfs_pconn_read(pc, buf, sizeof buf, &got, NULL, NULL));
+        if (got != L) exit(4);
+        if (i >= 5) v[m++] = now_us() - t0;
+      }
+    }
+    char nm[16];
+    snprintf(nm, sizeof nm, "%d", n);
+    print_stat(nm, v, m, k == NS - 1);
+  }
+  printf("}, ");
+  sqobfs_pconn_stats st;
+  CHECK(sqobfs_pconn_stats_get(pc, &st));
+  printf("\"pconn_stats%s\": {\"tx_datagrams\": %llu, \"tx_batches\": %llu, \"rx_datagrams\": "
+         "%llu, \"rx_batches\": %llu, \"cpu_batches\": %llu, \"inline_writes\": %llu}, ",
+         label, (unsigned long long)st.tx_datagrams, (unsigned long long)st.tx_batches,
+         (unsigned long long)st.rx_datagrams, (unsigned long long)st.rx_batches,
+         (unsigned long long)st.cpu_batches, (unsigned long long)st.inline_writes);
+  sqobfs_pconn_close(pc);
+  close(fa);
+  close(fp);
+}
+
 int main(void) {
   sqobfs_ctx *ctx;
   CHECK(sqobfs_open(0, &ctx));
@@ -275,76 +350,22 @@ int main(void) {
     close(fp);
   }
 
-  /* ---- pconn: WriteTo bursts -> arrival; peer bursts -> ReadFrom */
-  {
-    uint16_t pa, pp;
-    int fa = udp_socket(&pa), fp = udp_socket(&pp);
-    sqobfs_pconn *pc;
-    CHECK(sqobfs_pconn_open(ctx, kr, fa, NULL, &pc));
-    const sqobfs_addr to = loop_addr(pp);
-    static uint8_t pay[L], buf[4096], wire[MAXN][L + 8];
-    memset(pay, 5, L);
-    static double tw[MAXN];
-    printf("\"pconn_write\": {");
-    for (int k = 0; k < NS; k++) {
-      const int n = SIZES[k], it = iters_for(n) / 4 + 1;
-      int m = 0;
-      for (int i = 0; i < it + 5; i++) {
-        for (int j = 0; j < n; j++) {
-          tw[j] = now_us();
-          CHECK(sqobfs_pconn_write(pc, pay, L, &to, 0));
-        }
-        for (int j = 0; j < n; j++) {
-          if (recv_to(fp, buf, sizeof buf, 2000) < 0) exit(3);
-          if (i >= 5) v[m++] = now_us() - tw[j];
-        }
-      }
-      char nm[16];
-      snprintf(nm, sizeof nm, "%d", n);
-      print_stat(nm, v, m, k == NS - 1);
-    }
-    printf("}, ");
-    sqobfs_pconn_stats st0;
-    CHECK(sqobfs_pconn_stats_get(pc, &st0));
-    /* receive side: obfuscated datagrams from the peer */
-    for (int j = 0; j < MAXN; j++) {
-      uint8_t salt[8] = {(uint8_t)j, 1, 2, 3, 4, 5, 6, 7};
-      or_salamander_write(PSK, PL, salt, pay, L, wire[j]);
-    }
-    struct sockaddr_in a;
-    memset(&a, 0, sizeof a);
-    a.sin_family = AF_INET;
-    a.sin_port = htons(pa);
-    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
-    printf("\"pconn_read\": {");
-    for (int k = 0; k < NS; k++) {
-      const int n = SIZES[k], it = iters_for(n) / 4 + 1;
-      int m = 0;
-      for (int i = 0; i < it + 5; i++) {
-        const double t0 = now_us();
-        for (int j = 0; j < n; j++)
-          sendto(fp, wire[j], L + 8, 0, (struct sockaddr *)&a, sizeof a);
-        for (int j = 0; j < n; j++) {
-          uint32_t got;
-          CHECK(sqobfs_pconn_read(pc, buf, sizeof buf, &got, NULL, NULL));
-          if (got != L) exit(4);
-          if (i >= 5) v[m++] = now_us() - t0;
-        }
-      }
-      char nm[16];
-      snprintf(nm, sizeof nm, "%d", n);
-      print_stat(nm, v, m, k == NS - 1);
-    }
-    printf("}, ");
-    sqobfs_pconn_stats st;
-    CHECK(sqobfs_pconn_stats_get(pc, &st));
-    printf("\"pconn_stats\": {\"tx_datagrams\": %llu, \"tx_batches\": %llu, \"rx_datagrams\": %llu, "
-           "\"rx_batches\": %llu}, ",
-           (unsigned long long)st.tx_datagrams, (unsigned long long)st.tx_batches,
-           (unsigned long long)st.rx_datagrams, (unsigned long long)st.rx_batches);
-    sqobfs_pconn_close(pc);
-    close(fa);
-    close(fp);
+  /* ---- pconn: WriteTo bursts -> arrival; peer bursts -> ReadFrom, with the
+   * engine's defaults (inline writes when idle, small batches on the CPU
+   * path) and with every batch launched on the GPU (round 3's engine) */
+  sqobfs_pconn_opts gpu_only;
+  memset(&gpu_only, 0, sizeof gpu_only);
+  gpu_only.cpu_max = SQOBFS_PCONN_NEVER;
+  gpu_only.inline_gap_us = SQOBFS_PCONN_NEVER;
+  pconn_lat(ctx, kr, "", NULL);
+  pconn_lat(ctx, kr, "_gpu_only", &gpu_only);
+  {  /* no GPU at all: a host keyring and the host engine */
+    sqobfs_keyring *hk;
+    uint64_t o0 = 0;
+    uint32_t l0 = PL;
+    CHECK(sqobfs_keyring_create(NULL, SQOBFS_SALAMANDER, 1, PSK, &o0, &l0, &hk));
+    pconn_lat(NULL, hk, "_no_device", NULL);
+    sqobfs_keyring_destroy(hk);
   }
 
   /* ---- pconn throughput: pconn A -> pconn B over loopback, one writer

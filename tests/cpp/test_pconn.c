@@ -465,6 +465,11 @@ static void t_deadline(void) {
 }
 
 /* ------------------------------------------------------------ shutdown */
+static void *shutdown_thread(void *arg) {
+  sqobfs_pconn_shutdown((sqobfs_pconn *)arg);
+  return NULL;
+}
+
 static void t_shutdown(void) {
   const int64_t a0 = sqobfs_debug_host_allocs();
   sqobfs_keyring *kr = keyring(SQOBFS_XPLUS);
@@ -520,8 +525,26 @@ static void t_shutdown(void) {
   int got = 0;
   while (recv_to(fp, buf, sizeof buf, 200) == 1216) got++;
   EXPECT(got == 100, "%d of 100 datagrams written before Close were sent", got);
+  /* 4. two concurrent Close calls: neither cuts the other's drain short
+   *    (the second call used to wake the workers early) */
+  {
+    sqobfs_pconn_opts o2;
+    memset(&o2, 0, sizeof o2);
+    o2.inline_gap_us = SQOBFS_PCONN_NEVER;
+    CHECK(sqobfs_pconn_open(g_ctx, kr, fa, &o2, &pc));
+    for (int i = 0; i < 300; i++) CHECK(sqobfs_pconn_write(pc, p, 1200, &to, 0));
+    pthread_t t1, t2;
+    pthread_create(&t1, NULL, shutdown_thread, pc);
+    pthread_create(&t2, NULL, shutdown_thread, pc);
+    pthread_join(t1, NULL);
+    pthread_join(t2, NULL);
+    sqobfs_pconn_close(pc);
+    got = 0;
+    while (recv_to(fp, buf, sizeof buf, 200) == 1216) got++;
+    EXPECT(got == 300, "%d of 300 datagrams sent with two concurrent closes", got);
+  }
   printf("  shutdown: blocked read -> SQ_ECLOSED; close with full rx batches %.1f ms; "
-         "writes before close sent\n", tc * 1e3);
+         "writes before close sent (also with two concurrent closes)\n", tc * 1e3);
   close(fa);
   close(fp);
   sqobfs_keyring_destroy(kr);

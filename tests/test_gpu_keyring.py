@@ -104,3 +104,32 @@ def test_sync_spin_is_opt_in():
         assert L.sqobfs_set_sync_spin(ctx.handle, 1000) == 0
         ctx.sync(ctx.stream)
         assert L.sqobfs_set_sync_spin(None, 10) == sqobfs.SQ_EINVAL
+
+
+def test_caller_stream_released_before_destroy():
+    """A caller that destroys its own stream first releases it from the
+    keyring (sqobfs_keyring_release_stream): the launch on it completes, and
+    the keyring's later release never touches the destroyed handle (ADVICE
+    round 3: the fence used to record on every stream it had seen)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    with sqobfs.Context(0) as ctx:
+        kr = sqobfs.Keyring(ctx, SALAMANDER, [PSK])
+        st = torch.cuda.Stream(dev)
+        batch, keep = _big_batch(torch, dev, n=1 << 16)
+        torch.cuda.synchronize(dev)
+        sqobfs.launch(ctx, kr, OBFUSCATE, batch, st.cuda_stream)
+        kr.release_stream(st.cuda_stream)  # waits for the launch
+        assert st.query()
+        olen = keep[6]
+        assert int(olen.min().item()) == 1358 and int(olen.max().item()) == 1358
+        del st  # torch destroys (or recycles) the stream
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        kr.close()
+        assert time.perf_counter() - t0 < 0.05
+        # releasing a stream the keyring never saw, or the null stream, is fine
+        kr2 = sqobfs.Keyring(ctx, SALAMANDER, [PSK])
+        kr2.release_stream(0)
+        kr2.release_stream(torch.cuda.Stream(dev).cuda_stream)
+        kr2.close()

@@ -93,3 +93,71 @@ def test_shard_run_device_resident(ctxs, kind):
     hb.out[:] = d_out.cpu().numpy()
     hb.out_len[:] = d_olen.cpu().numpy()
     gh.assert_same(hb, ref, "device shards")
+
+
+@pytest.mark.parametrize("kind", [SALAMANDER, XPLUS])
+def test_shard_launch_steps_in_flight(kind):
+    """sqobfs_shard_launch: several steps queued before any is waited for
+    (tickets), obfuscate then deobfuscate in flight together, each shard on
+    its own context -- on distinct GPUs when the box has more than one, else
+    on device 0 (the same path); both steps equal the oracle."""
+    import torch
+    ndev = torch.cuda.device_count()
+    devs = [0, 1] if ndev > 1 else [0, 0]
+    rng = np.random.Generator(np.random.PCG64(540 + kind))
+    S = sqobfs.SALT_LEN[kind]
+    n = 20000
+    lens = rng.integers(64, 1453, n)
+    hb = gh.make_case(rng, kind, OBFUSCATE, lens, PSKS[:1])
+    ref = gh.run_oracle(kind, OBFUSCATE, PSKS[:1], hb)
+    cut = sqobfs.shard_cuts(hb.in_len, 2).astype(np.int64)
+    ctxs = [sqobfs.Context(d) for d in devs]
+    krs = [sqobfs.Keyring(c, kind, PSKS[:1]) for c in ctxs]
+    try:
+        parts = []
+        for k, (a, b) in enumerate(zip(cut[:-1], cut[1:])):
+            dev = torch.device("cuda", devs[k])
+            t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)  # noqa: E731
+            m = int(b - a)
+            base = int(hb.in_off[a])
+            end = int(hb.in_off[b - 1]) + int(hb.in_len[b - 1])
+            clean = np.zeros(end - base, np.uint8)  # payload bytes only
+            for i in range(int(a), int(b)):
+                o = int(hb.in_off[i]) - base
+                clean[o:o + int(hb.in_len[i])] = hb.data[o + base:o + base + int(hb.in_len[i])]
+            d_in = t(clean)
+            d_ioff = t(hb.in_off[a:b] - base)
+            d_len = t(hb.in_len[a:b])
+            obase = int(hb.out_off[a])
+            oend = int(hb.out_off[b - 1]) + int(hb.in_len[b - 1]) + S
+            d_out = torch.zeros(oend - obase, dtype=torch.uint8, device=dev)
+            d_ooff = t(hb.out_off[a:b] - obase)
+            d_olen = torch.zeros(m, dtype=torch.int32, device=dev)
+            d_back = torch.zeros_like(d_in)
+            d_blen = torch.zeros(m, dtype=torch.int32, device=dev)
+            d_wlen = t((hb.in_len[a:b] + S).astype(np.uint32))
+            obf = sqobfs.make_batch(m, d_in, d_ioff, d_len, d_out, d_ooff, d_olen,
+                                    t(hb.salt[S * a:S * b]))
+            deo = sqobfs.make_batch(m, d_out, d_ooff, d_wlen, d_back, d_ioff, d_blen)
+            parts.append((a, b, obase, d_in, d_out, d_olen, d_back, d_blen, obf, deo))
+            torch.cuda.synchronize(dev)
+        t1 = sqobfs.shard_launch(ctxs, krs, OBFUSCATE, [p[8] for p in parts])
+        t2 = sqobfs.shard_launch(ctxs, krs, DEOBFUSCATE, [p[9] for p in parts])
+        t2.wait()  # (stream order: the decode ran after the encode)
+        assert t1.done()
+        t1.wait()
+        for a, b, obase, d_in, d_out, d_olen, d_back, d_blen, _, _ in parts:
+            got = d_out.cpu().numpy()
+            for i in range(int(a), int(b), 97):
+                o = int(hb.out_off[i]) - obase
+                L = int(hb.in_len[i]) + S
+                assert got[o:o + L].tobytes() == \
+                    ref.out[int(hb.out_off[i]):int(hb.out_off[i]) + L].tobytes()
+            assert np.array_equal(d_olen.cpu().numpy(), ref.out_len[a:b].astype(np.int32))
+            assert torch.equal(d_back, d_in)
+            assert np.array_equal(d_blen.cpu().numpy(), hb.in_len[a:b].astype(np.int32))
+    finally:
+        for k in krs:
+            k.close()
+        for c in ctxs:
+            c.close()
