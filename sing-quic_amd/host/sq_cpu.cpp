@@ -8,6 +8,8 @@
 // and XORs a word at a time.
 #include "sq_cpu.h"
 
+#include <immintrin.h>
+#include <stdlib.h>
 #include <string.h>
 #include <sys/random.h>
 
@@ -89,7 +91,83 @@ constexpr uint64_t kMaxPacket = 1ull << 26;  // sq_kernels.hip kMaxPacket
 
 }  // namespace
 
+namespace {
+
+// BLAKE2b compression with AVX2: the state as four rows of four 64-bit
+// words, G on the four columns at once, then on the diagonals (rows b, c, d
+// rotated by 1, 2, 3 lanes); rotations by 32 / 24 / 16 are byte shuffles,
+// by 63 a shift pair.
+__attribute__((target("avx2"))) void b2_compress_avx2(uint64_t h[8], const uint64_t m[16],
+                                                       uint64_t t, bool last) {
+  const __m256i r24 = _mm256_setr_epi8(3, 4, 5, 6, 7, 0, 1, 2, 11, 12, 13, 14, 15, 8, 9, 10,
+                                       3, 4, 5, 6, 7, 0, 1, 2, 11, 12, 13, 14, 15, 8, 9, 10);
+  const __m256i r16 = _mm256_setr_epi8(2, 3, 4, 5, 6, 7, 0, 1, 10, 11, 12, 13, 14, 15, 8, 9,
+                                       2, 3, 4, 5, 6, 7, 0, 1, 10, 11, 12, 13, 14, 15, 8, 9);
+  const __m256i h0 = _mm256_loadu_si256((const __m256i *)&h[0]);
+  const __m256i h1 = _mm256_loadu_si256((const __m256i *)&h[4]);
+  __m256i a = h0, b = h1;
+  __m256i c = _mm256_loadu_si256((const __m256i *)&kB2IV[0]);
+  __m256i d = _mm256_xor_si256(_mm256_loadu_si256((const __m256i *)&kB2IV[4]),
+                               _mm256_set_epi64x(0, last ? -1ll : 0, 0, (long long)t));
+  // (a macro: a lambda would not inherit the function's target)
+#define SQ_B2G_AVX2(x, y)                                                      \
+  do {                                                                         \
+    a = _mm256_add_epi64(_mm256_add_epi64(a, b), (x));                         \
+    d = _mm256_shuffle_epi32(_mm256_xor_si256(d, a), _MM_SHUFFLE(2, 3, 0, 1)); \
+    c = _mm256_add_epi64(c, d);                                                \
+    b = _mm256_shuffle_epi8(_mm256_xor_si256(b, c), r24);                      \
+    a = _mm256_add_epi64(_mm256_add_epi64(a, b), (y));                         \
+    d = _mm256_shuffle_epi8(_mm256_xor_si256(d, a), r16);                      \
+    c = _mm256_add_epi64(c, d);                                                \
+    const __m256i e_ = _mm256_xor_si256(b, c);                                 \
+    b = _mm256_or_si256(_mm256_srli_epi64(e_, 63), _mm256_add_epi64(e_, e_));  \
+  } while (0)
+  for (int r = 0; r < 12; r++) {
+    const uint8_t *z = kSigma[r];
+    SQ_B2G_AVX2(_mm256_set_epi64x((long long)m[z[6]], (long long)m[z[4]], (long long)m[z[2]],
+                                  (long long)m[z[0]]),
+                _mm256_set_epi64x((long long)m[z[7]], (long long)m[z[5]], (long long)m[z[3]],
+                                  (long long)m[z[1]]));
+    b = _mm256_permute4x64_epi64(b, 0x39);  // diagonals: lane j holds b[j+1], c[j+2], d[j+3]
+    c = _mm256_permute4x64_epi64(c, 0x4E);
+    d = _mm256_permute4x64_epi64(d, 0x93);
+    SQ_B2G_AVX2(_mm256_set_epi64x((long long)m[z[14]], (long long)m[z[12]], (long long)m[z[10]],
+                                  (long long)m[z[8]]),
+                _mm256_set_epi64x((long long)m[z[15]], (long long)m[z[13]], (long long)m[z[11]],
+                                  (long long)m[z[9]]));
+    b = _mm256_permute4x64_epi64(b, 0x93);
+    c = _mm256_permute4x64_epi64(c, 0x4E);
+    d = _mm256_permute4x64_epi64(d, 0x39);
+  }
+  _mm256_storeu_si256((__m256i *)&h[0], _mm256_xor_si256(h0, _mm256_xor_si256(a, c)));
+  _mm256_storeu_si256((__m256i *)&h[4], _mm256_xor_si256(h1, _mm256_xor_si256(b, d)));
+#undef SQ_B2G_AVX2
+}
+
+void b2_compress_portable(uint64_t h[8], const uint64_t m[16], uint64_t t, bool last);
+
+using B2Fn = void (*)(uint64_t *, const uint64_t *, uint64_t, bool);
+// SQOBFS_CPU_PORTABLE=1 (tests): the portable compressions on any CPU
+bool force_portable() {
+  const char *e = getenv("SQOBFS_CPU_PORTABLE");
+  return e && *e == '1';
+}
+
+B2Fn pick_b2() {
+  __builtin_cpu_init();
+  return __builtin_cpu_supports("avx2") && !force_portable() ? b2_compress_avx2
+                                                              : b2_compress_portable;
+}
+
+}  // namespace
+
 void b2_compress(uint64_t h[8], const uint64_t m[16], uint64_t t, bool last) {
+  static const B2Fn fn = pick_b2();
+  fn(h, m, t, last);
+}
+
+namespace {
+void b2_compress_portable(uint64_t h[8], const uint64_t m[16], uint64_t t, bool last) {
   uint64_t v[16];
   for (int i = 0; i < 8; i++) {
     v[i] = h[i];
@@ -110,8 +188,65 @@ void b2_compress(uint64_t h[8], const uint64_t m[16], uint64_t t, bool last) {
   }
   for (int i = 0; i < 8; i++) h[i] ^= v[i] ^ v[i + 8];
 }
+}  // namespace
+
+namespace {
+
+// SHA-256 compression with the x86 SHA extensions (four rounds per
+// sha256rnds2 pair, the schedule by sha256msg1 / sha256msg2); used when the
+// CPU has them (AMD Zen, Intel since Ice Lake), picked once at first use.
+__attribute__((target("sha,sse4.1"))) void s2_compress_shani(uint32_t st[8],
+                                                             const uint32_t m[16]) {
+  __m128i t = _mm_loadu_si128((const __m128i *)&st[0]);  // A B C D
+  __m128i s1 = _mm_loadu_si128((const __m128i *)&st[4]); // E F G H
+  t = _mm_shuffle_epi32(t, 0xB1);
+  s1 = _mm_shuffle_epi32(s1, 0x1B);
+  __m128i s0 = _mm_alignr_epi8(t, s1, 8);     // A B E F (the instruction's order)
+  s1 = _mm_blend_epi16(s1, t, 0xF0);          // C D G H
+  const __m128i abef = s0, cdgh = s1;
+  __m128i w[4];
+  for (int i = 0; i < 16; i++) {
+    __m128i x;
+    if (i < 4) {
+      x = _mm_loadu_si128((const __m128i *)&m[4 * i]);  // (the words, already decoded)
+    } else {
+      x = _mm_sha256msg1_epu32(w[(i - 4) & 3], w[(i - 3) & 3]);
+      x = _mm_add_epi32(x, _mm_alignr_epi8(w[(i - 1) & 3], w[(i - 2) & 3], 4));
+      x = _mm_sha256msg2_epu32(x, w[(i - 1) & 3]);
+    }
+    w[i & 3] = x;
+    __m128i mk = _mm_add_epi32(x, _mm_loadu_si128((const __m128i *)&kS2K[4 * i]));
+    s1 = _mm_sha256rnds2_epu32(s1, s0, mk);
+    mk = _mm_shuffle_epi32(mk, 0x0E);
+    s0 = _mm_sha256rnds2_epu32(s0, s1, mk);
+  }
+  s0 = _mm_add_epi32(s0, abef);
+  s1 = _mm_add_epi32(s1, cdgh);
+  t = _mm_shuffle_epi32(s0, 0x1B);
+  s1 = _mm_shuffle_epi32(s1, 0xB1);
+  _mm_storeu_si128((__m128i *)&st[0], _mm_blend_epi16(t, s1, 0xF0));  // A B C D
+  _mm_storeu_si128((__m128i *)&st[4], _mm_alignr_epi8(s1, t, 8));     // E F G H
+}
+
+void s2_compress_portable(uint32_t st[8], const uint32_t m[16]);
+
+using S2Fn = void (*)(uint32_t *, const uint32_t *);
+S2Fn pick_s2() {
+  __builtin_cpu_init();
+  return __builtin_cpu_supports("sha") && __builtin_cpu_supports("sse4.1") && !force_portable()
+             ? s2_compress_shani
+             : s2_compress_portable;
+}
+
+}  // namespace
 
 void s2_compress(uint32_t st[8], const uint32_t m[16]) {
+  static const S2Fn fn = pick_s2();
+  fn(st, m);
+}
+
+namespace {
+void s2_compress_portable(uint32_t st[8], const uint32_t m[16]) {
   uint32_t w[64];
   for (int i = 0; i < 16; i++) w[i] = m[i];
   for (int i = 16; i < 64; i++) {
@@ -144,6 +279,7 @@ void s2_compress(uint32_t st[8], const uint32_t m[16]) {
   st[6] += g;
   st[7] += h;
 }
+}  // namespace
 
 void chacha20_block(const uint32_t key[8], uint32_t counter, const uint32_t nonce[3],
                     uint32_t out[16]) {
@@ -259,7 +395,9 @@ void derive_key(const PskEntry &e, const uint8_t *salt, uint8_t key[32]) {
 
 // 32 bytes per iteration as four 64-bit words (the compiler widens the loop
 // to vector registers); the key's period is 32, so the key words are fixed.
-void xor_stream(uint8_t *dst, const uint8_t *src, size_t n, const uint8_t key[32]) {
+__attribute__((target_clones("avx2", "default"))) void xor_stream(uint8_t *dst,
+                                                                   const uint8_t *src, size_t n,
+                                                                   const uint8_t key[32]) {
   uint64_t k[4];
   memcpy(k, key, 32);
   size_t j = 0;

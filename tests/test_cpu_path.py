@@ -143,3 +143,17 @@ def test_generated_salts_are_the_wire_salts(kind):
         p = hb.data[int(hb.in_off[i]):int(hb.in_off[i]) + L].tobytes()
         w, _ = write(psks[0], hb.salt_out[i * S:(i + 1) * S].tobytes(), p)
         assert hb.out[o:o + L + S].tobytes() == w
+
+
+def test_portable_compressions_too():
+    """The CPU path picks AVX2 BLAKE2b / SHA-NI SHA-256 where the host has
+    them; the portable compressions (hosts without) pass the same tests
+    (SQOBFS_CPU_PORTABLE=1 forces them)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, SQOBFS_CPU_PORTABLE="1")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider",
+                        os.path.abspath(__file__), "-k", "not portable"],
+                       capture_output=True, text=True, env=env, timeout=600,
+                       cwd=os.path.dirname(os.path.abspath(__file__)))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
