@@ -395,9 +395,12 @@ void derive_key(const PskEntry &e, const uint8_t *salt, uint8_t key[32]) {
 
 // 32 bytes per iteration as four 64-bit words (the compiler widens the loop
 // to vector registers); the key's period is 32, so the key words are fixed.
-__attribute__((target_clones("avx2", "default"))) void xor_stream(uint8_t *dst,
-                                                                   const uint8_t *src, size_t n,
-                                                                   const uint8_t key[32]) {
+// Two builds of the same loop, AVX2 and baseline, picked once (a plain
+// function pointer, not an ifunc: ifunc resolvers run before the sanitizer
+// runtimes are up).
+namespace {
+template <int>
+inline void xor_loop(uint8_t *dst, const uint8_t *src, size_t n, const uint8_t key[32]) {
   uint64_t k[4];
   memcpy(k, key, 32);
   size_t j = 0;
@@ -411,6 +414,24 @@ __attribute__((target_clones("avx2", "default"))) void xor_stream(uint8_t *dst,
     memcpy(dst + j, w, 32);
   }
   for (; j < n; j++) dst[j] = src[j] ^ key[j & 31];
+}
+__attribute__((target("avx2"))) void xor_avx2(uint8_t *dst, const uint8_t *src, size_t n,
+                                              const uint8_t key[32]) {
+  xor_loop<1>(dst, src, n, key);
+}
+void xor_base(uint8_t *dst, const uint8_t *src, size_t n, const uint8_t key[32]) {
+  xor_loop<0>(dst, src, n, key);
+}
+using XorFn = void (*)(uint8_t *, const uint8_t *, size_t, const uint8_t *);
+XorFn pick_xor() {
+  __builtin_cpu_init();
+  return __builtin_cpu_supports("avx2") && !force_portable() ? xor_avx2 : xor_base;
+}
+}  // namespace
+
+void xor_stream(uint8_t *dst, const uint8_t *src, size_t n, const uint8_t key[32]) {
+  static const XorFn fn = pick_xor();
+  fn(dst, src, n, key);
 }
 
 void salt_stream(const uint32_t key[8], uint64_t seq, uint8_t *out, size_t bytes) {
