@@ -346,6 +346,72 @@ def cpu_baseline(seconds: float):
             "cpu_seconds": round(wall * threads + wall1, 2)}
 
 
+def cpu_path_rate(seconds: float = 1.5):
+    """The PRODUCT's CPU path (sqobfs_cpu_run: host/sq_cpu.cpp, AVX2 BLAKE2b,
+    word XOR; what the packet conn engine runs without a GPU and for small
+    batches) on configs[0]'s workload, one contiguous shard per thread (ctypes
+    releases the GIL).  Not the baseline: that is the reference's byte loops
+    (cpu_baseline)."""
+    import threading
+    import numpy as np
+    import sqobfs
+    n, L, S = 65536, 1200, 8
+    threads = cpu_share()
+    rng = np.random.Generator(np.random.PCG64(1))
+    data = rng.integers(0, 256, n * L, dtype=np.uint8)
+    salt = np.random.Generator(np.random.PCG64(2)).integers(0, 256, n * S, dtype=np.uint8)
+    wire = np.ones(n * (L + S), np.uint8)  # (pages touched: no first-write faults timed)
+    back = np.ones(n * L, np.uint8)
+    cut = [n * t // threads for t in range(threads + 1)]
+    kr = sqobfs.Keyring(None, sqobfs.SALAMANDER, [PSK])
+
+    def shard(t, direction):
+        a, b = cut[t], cut[t + 1]
+        m = b - a
+        if direction == sqobfs.OBFUSCATE:
+            hb = sqobfs.HostBatch(data[a * L:b * L], np.arange(m, dtype=np.uint64) * L,
+                                  np.full(m, L, np.uint32), wire[a * (L + S):b * (L + S)],
+                                  np.arange(m, dtype=np.uint64) * (L + S), np.zeros(m, np.uint32),
+                                  salt[a * S:b * S])
+        else:
+            hb = sqobfs.HostBatch(wire[a * (L + S):b * (L + S)],
+                                  np.arange(m, dtype=np.uint64) * (L + S),
+                                  np.full(m, L + S, np.uint32), back[a * L:b * L],
+                                  np.arange(m, dtype=np.uint64) * L, np.zeros(m, np.uint32))
+        return hb.as_batch(), hb
+
+    def run(direction, nthreads):
+        batches = [shard(t, direction) for t in range(nthreads)] if nthreads == threads else \
+            [shard(0, direction)]
+        ths = [threading.Thread(target=sqobfs.cpu_run, args=(kr, direction, b)) for b, _ in batches]
+        t0 = time.perf_counter()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        return time.perf_counter() - t0, sum(int(h.in_len.sum()) if direction == 0 else
+                                             int(h.in_len.sum()) - S * h.n for _, h in batches)
+
+    res = {}
+    run(sqobfs.OBFUSCATE, threads)  # warm
+    for name, direction in (("obfuscate", sqobfs.OBFUSCATE), ("deobfuscate", sqobfs.DEOBFUSCATE)):
+        tot = byt = 0.0
+        t_end = time.perf_counter() + seconds / 2
+        while tot == 0 or time.perf_counter() < t_end:
+            dt, b = run(direction, threads)
+            tot += dt
+            byt += b
+        res[name] = round(byt / tot / 2**30, 3)
+    ok = bool(np.array_equal(back, data))
+    dt1, b1 = run(sqobfs.OBFUSCATE, 1)
+    kr.close()
+    return {"value": res["obfuscate"], "unit": "GiB/s", "threads": threads,
+            "per_direction": res, "per_thread_obfuscate": round(b1 / dt1 / 2**30, 3),
+            "round_trip_identity": ok,
+            "what": "sqobfs_cpu_run (the product CPU path, no GPU) on configs[0]'s 65,536 x "
+                    "1200 B, one shard per thread"}
+
+
 def cgroup_cpu_quota():
     """CPUs the cgroup's CPU quota allows (cgroup v2 cpu.max "quota period",
     v1 cfs_quota_us / cfs_period_us), or None when unlimited / unreadable."""
@@ -752,6 +818,7 @@ def main():
                                    for su in (0, 1) for bt in (256, 1024)]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        out["cpu_path"] = cpu_path_rate()
     if rank == 0:
         out["host"] = host_info(torch, dev)
     if rank == 0:
