@@ -1,7 +1,8 @@
 // packet_conn.cpp -- C++ mirror of the reference's obfuscating PacketConn
-// decorators (see packet_conn.h).  Every transform goes through the C ABI
-// (sqobfs_run_host -> gfx950 kernels); this file only moves bytes between
-// sockets and batches.
+// decorators (see packet_conn.h).  Every transform goes through the C ABI --
+// sqobfs_run_host (gfx950 kernels) for batches worth a launch, sqobfs_cpu_run
+// (the library's CPU path) for single datagrams, small batches and when no
+// GPU can be opened; this file only moves bytes between sockets and batches.
 #include "packet_conn.h"
 
 #include <string.h>
@@ -172,8 +173,9 @@ void crypto_random(uint8_t *b, size_t n) {
 // ---------------------------------------------------------------- Obfuscator
 
 Obfuscator::Obfuscator(int kind, const uint8_t *psk, size_t psk_len, int device) : kind_(kind) {
-  status_ = sqobfs_open(device, &ctx_);
-  if (status_ != SQ_OK) return;
+  // no GPU: a host keyring, every batch on the CPU path (the reference's
+  // constructors cannot fail, salamander.go:24-40, xplus.go:19-37)
+  if (sqobfs_open(device, &ctx_) != SQ_OK) ctx_ = nullptr;
   const uint64_t off = 0;
   const uint32_t len = (uint32_t)psk_len;
   static const uint8_t empty = 0;
@@ -186,8 +188,16 @@ Obfuscator::~Obfuscator() {
 }
 
 int Obfuscator::run(int dir, const sqobfs_batch &b) {
-  if (status_ != SQ_OK) return status_;  // no GPU: fail loudly, no fallback
-  return sqobfs_run_host(ctx_, kr_, dir, &b);
+  if (status_ != SQ_OK) return status_;
+  // a batch worth a launch goes to the GPU (cost as the packet conn engine
+  // counts it: payload bytes + 1 KiB per datagram, above 64 KiB); a single
+  // datagram costs ~1 us on the CPU path against a ~50 us staged round trip
+  uint64_t cost = 0;
+  for (uint32_t i = 0; i < b.n; i++) cost += b.in_len[i] + 1024u;
+  if (!ctx_ || gpu_failed_ || cost <= 65536) return sqobfs_cpu_run(kr_, dir, &b);
+  const int st = sqobfs_run_host(ctx_, kr_, dir, &b);
+  if (st == SQ_EDEVICE || st == SQ_ENODEV) gpu_failed_ = true;  // later batches: the CPU
+  return st;
 }
 
 // ---------------------------------------------------------------- Salamander

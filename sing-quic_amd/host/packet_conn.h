@@ -8,11 +8,14 @@
 //                            VectorisedSalamanderPacketConn
 //   hysteria/xplus.go        NewXPlusPacketConn / XPlusPacketConn /
 //                            VectorisedXPlusConn
-// with every byte transform executed by the gfx950 kernels (no CPU path).
-// The batch methods (ReadBatch / WriteBatch) are the intended use: one GPU
-// launch per batch of datagrams (recvmmsg/sendmmsg style).  The per-packet
-// methods exist so call sites written against the reference compile
-// unchanged; they pay one GPU round trip per datagram.
+// with every byte transform executed through the C ABI: batches worth a
+// launch by the gfx950 kernels, single datagrams and small batches by the
+// library's CPU path (sqobfs_cpu_run), which also serves every call when no
+// GPU can be opened -- so, like the reference's, the constructors never fail
+// for want of a device.  The batch methods (ReadBatch / WriteBatch) are the
+// intended use: one GPU launch per batch of datagrams (recvmmsg/sendmmsg
+// style); the per-packet methods keep call sites written against the
+// reference compiling unchanged.
 #pragma once
 
 #include <stddef.h>
@@ -76,13 +79,16 @@ class Obfuscator {
 
   int kind() const { return kind_; }
   size_t salt_len() const { return kind_ == SQOBFS_SALAMANDER ? 8 : 16; }
-  // host batch through sqobfs_run_host; returns sqobfs status
+  // host batch: sqobfs_run_host when it is worth a launch, else (and with
+  // no GPU, or after a failed launch) sqobfs_cpu_run; returns sqobfs status
   int run(int dir, const sqobfs_batch &b);
   int status() const { return status_; }
+  bool has_gpu() const { return ctx_ != nullptr && !gpu_failed_; }
 
  private:
   int kind_;
   int status_ = SQ_OK;
+  bool gpu_failed_ = false;
   sqobfs_ctx *ctx_ = nullptr;
   sqobfs_keyring *kr_ = nullptr;
 };

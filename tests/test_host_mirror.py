@@ -1,6 +1,8 @@
 """The C++ mirror of the reference's PacketConn decorators
-(sing-quic_amd/host/packet_conn.*): compiles on CPU; behaviour checked
-against the oracle on the GPU (tests/cpp/test_packet_conn.cpp)."""
+(sing-quic_amd/host/packet_conn.*): behaviour checked against the oracle
+(tests/cpp/test_packet_conn.cpp) on the GPU and, with no GPU at all, on the
+library's CPU path (the constructors do not fail without a device, as the
+reference's cannot)."""
 from __future__ import annotations
 
 import os
@@ -29,6 +31,17 @@ def _compile() -> str:
 def test_host_mirror_compiles_and_links():
     assert os.path.exists(os.path.join(REPO, "sing-quic_amd", "libsqobfs.so"))
     _compile()
+
+
+def test_host_mirror_without_a_device():
+    """No GPU in this process's view: every transform on the CPU path."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present (the -m gpu test covers it)")
+    exe = _compile()
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ok" in r.stdout
 
 
 @pytest.mark.gpu
