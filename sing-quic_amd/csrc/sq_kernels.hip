@@ -115,6 +115,10 @@ namespace sq {
 #ifndef SQ_WINPKT
 #define SQ_WINPKT 0
 #endif
+// Window loads through a wave-uniform buffer resource (kWinBuf)
+#ifndef SQ_WINBUF
+#define SQ_WINBUF 0
+#endif
 // XCD-contiguous units.  Workgroups are dispatched round-robin over the 8
 // XCDs, so block b runs on XCD b % 8 and, unmapped, the XCDs share one
 // moving window of the batch.  Remapped, each XCD walks its own contiguous
@@ -140,7 +144,8 @@ extern "C" const char *sqobfs_build_info(void) {
          " minw=" SQ_STR(SQ_MINW) " wpb=2"
          " ablate=" SQ_STR(SQ_ABLATE) " donate=" SQ_STR(SQ_DONATE) " align=" SQ_STR(SQ_ALIGN)
          " map=" SQ_STR(SQ_MAPBLK)
-         " winsafe=" SQ_STR(SQ_WINSAFE) " winpkt=" SQ_STR(SQ_WINPKT) " xcd=" SQ_STR(SQ_XCD);
+         " winsafe=" SQ_STR(SQ_WINSAFE) " winpkt=" SQ_STR(SQ_WINPKT) " winbuf=" SQ_STR(SQ_WINBUF)
+         " xcd=" SQ_STR(SQ_XCD);
 }
 
 // default unit size (KParams.ppw == 0); any 1 .. kMaxUnitPackets works
@@ -551,22 +556,113 @@ __device__ __forceinline__ bool tail_from_window(uint64_t rs, uint64_t re) {
 template <int KIND, int DIR, bool MULTI>
 constexpr bool kWinSafe =
     SQ_WINSAFE == 2 || (SQ_WINSAFE == 1 && !MULTI && (KIND == 0) == (DIR == 0));
+// SQ_WINBUF: the six window loads are raw buffer loads against one
+// wave-uniform resource based at the wave's lowest window block; a block a
+// packet does not need gets an offset past num_records, so it reads zero
+// without a memory access: unconditional loads, no substitute reads, no
+// masks.  A lane whose blocks lie 4 GiB or more past that base (a ragged
+// batch scattered over more than 4 GiB within one unit) loads them again with
+// global loads where the images are built.
+// 1: the kernels kWinSafe leaves on conditional loads; 2: every kernel.
+template <int KIND, int DIR, bool MULTI>
+constexpr bool kWinBuf = SQ_WINBUF == 2 || (SQ_WINBUF == 1 && !kWinSafe<KIND, DIR, MULTI>);
 struct Windows {
   u32x4 h0, h1, h2, t0, t1;
   u32x4 s0;     // deobfuscate: the block before h0 when it holds salt bytes
   uint32_t ok;  // bits: h0 1, h1 2, h2 4, t0 8, t1 16, s0 32 (SQ_WINSAFE)
+  uint32_t rl;  // SQ_WINBUF: the needed blocks out of the resource's range
 };
 constexpr uint32_t kWinH0 = 1, kWinH1 = 2, kWinH2 = 4, kWinT0 = 8, kWinT1 = 16, kWinS0 = 32;
+constexpr uint32_t kWinOffNone = 0xFFFFFFF0u;  // past num_records: reads zero
 
 // Deobfuscate with a key (wire_salt): the salt is the S wire bytes before
 // the payload, [src_pay - S, src_pay); it lies in h0 and, when src_pay % 16 <
 // S, the block before it, loaded here with the head window.
+// The window block addresses of a packet (need bits as Windows::ok).
+struct WinAddr {
+  uint64_t s0, h0, h1, h2, t0, t1;
+  uint32_t need;
+};
+
+template <int DIR, uint32_t S>
+__device__ __forceinline__ WinAddr window_addrs(const PacketJob &J, bool wire_salt) {
+  uint64_t rs, re;
+  bool ne;
+  out_range(J, rs, re, ne);
+  const uint64_t hw = !ne ? 0ull : (J.len < 32 - J.pre ? J.len : 32 - J.pre);
+  const uint64_t B = J.src_pay & ~15ull, e = J.src_pay + hw;
+  const bool c_h0 = hw != 0, c_h1 = c_h0 && e > B + 16, c_h2 = c_h0 && e > B + 32;
+  const bool c_s0 = SQ_SALTWIN && DIR == 1 && c_h0 && wire_salt && (J.src_pay & 15) < S;
+  const bool c_t0 = ne && tail_from_window(rs, re);
+  const uint64_t ta = J.src_pay + ((re & ~15ull) - J.dst_pay), te = J.src_pay + J.len;
+  const uint64_t TB = ta & ~15ull;
+  const bool c_t1 = c_t0 && te > TB + 16;
+  WinAddr A;
+  A.s0 = B - 16;
+  A.h0 = B;
+  A.h1 = B + 16;
+  A.h2 = B + 32;
+  A.t0 = TB;
+  A.t1 = TB + 16;
+  A.need = (c_h0 ? kWinH0 : 0u) | (c_h1 ? kWinH1 : 0u) | (c_h2 ? kWinH2 : 0u) |
+           (c_t0 ? kWinT0 : 0u) | (c_t1 ? kWinT1 : 0u) | (c_s0 ? kWinS0 : 0u);
+  return A;
+}
+
+// SQ_WINBUF loads (see kWinBuf).  Every needed block lies at or after h0 (or
+// s0) of its own packet: a tail block follows its head.
+template <int DIR, uint32_t S>
+__device__ __forceinline__ void fetch_windows_buf(const PacketJob &J, bool wire_salt,
+                                                  Windows &W) {
+  const WinAddr A = window_addrs<DIR, S>(J, wire_salt);
+  const uint64_t first = (A.need & kWinS0) ? A.s0 : A.h0;
+  const uint64_t lo0 = uniform64(wave_min64(A.need ? first : ~0ull));
+  const uint64_t lo = lo0 == ~0ull ? 0ull : lo0;  // (no lane needs a block)
+  const __amdgpu_buffer_rsrc_t R =
+      __builtin_amdgcn_make_buffer_rsrc((void *)lo, 0, (int)kWinOffNone, 0x00020000);
+  uint32_t rl = 0u;
+  auto off = [&](uint64_t a, uint32_t bit) -> uint32_t {
+    if (!(A.need & bit)) return kWinOffNone;
+    const uint64_t o = a - lo;  // a >= lo for every needed block
+    if (o >= kWinOffNone) {
+      rl |= bit;
+      return kWinOffNone;
+    }
+    return (uint32_t)o;
+  };
+  const uint32_t o_s0 = off(A.s0, kWinS0), o_h0 = off(A.h0, kWinH0), o_h1 = off(A.h1, kWinH1),
+                 o_h2 = off(A.h2, kWinH2), o_t0 = off(A.t0, kWinT0), o_t1 = off(A.t1, kWinT1);
+  W.s0 = DIR == 1 ? __builtin_amdgcn_raw_buffer_load_b128(R, o_s0, 0, 0) : u32x4{0u, 0u, 0u, 0u};
+  W.h0 = __builtin_amdgcn_raw_buffer_load_b128(R, o_h0, 0, 0);
+  W.h1 = __builtin_amdgcn_raw_buffer_load_b128(R, o_h1, 0, 0);
+  W.h2 = __builtin_amdgcn_raw_buffer_load_b128(R, o_h2, 0, 0);
+  W.t0 = __builtin_amdgcn_raw_buffer_load_b128(R, o_t0, 0, 0);
+  W.t1 = __builtin_amdgcn_raw_buffer_load_b128(R, o_t1, 0, 0);
+  W.ok = ~0u;  // unneeded blocks read zero
+  W.rl = rl;
+}
+
+// The blocks fetch_windows_buf could not reach (rare: a unit scattered over
+// more than 4 GiB), loaded where the images are built.
+template <int DIR, uint32_t S>
+__device__ __forceinline__ void reload_windows(const PacketJob &J, bool wire_salt, Windows &W) {
+  if (__ballot(W.rl != 0u) == 0) return;
+  const WinAddr A = window_addrs<DIR, S>(J, wire_salt);
+  if (W.rl & kWinS0) W.s0 = gld<u32x4>(A.s0);
+  if (W.rl & kWinH0) W.h0 = gld<u32x4>(A.h0);
+  if (W.rl & kWinH1) W.h1 = gld<u32x4>(A.h1);
+  if (W.rl & kWinH2) W.h2 = gld<u32x4>(A.h2);
+  if (W.rl & kWinT0) W.t0 = gld<u32x4>(A.t0);
+  if (W.rl & kWinT1) W.t1 = gld<u32x4>(A.t1);
+}
+
 template <int DIR, uint32_t S, bool WS>
 __device__ __forceinline__ void fetch_windows(const PacketJob &J, bool wire_salt, uint64_t safe,
                                               Windows &W) {
   const u32x4 z = {0u, 0u, 0u, 0u};
   W.h0 = W.h1 = W.h2 = W.t0 = W.t1 = W.s0 = z;
   W.ok = 0u;
+  W.rl = 0u;
   if (SQ_ABLATE & 8) return;
   uint64_t rs, re;
   bool ne;
@@ -846,7 +942,7 @@ __device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
   // every window register stays allocated until here: a component no image
   // uses would otherwise be handed to the plan while its load is in flight,
   // and overwriting it waits for the load (SQ_WINSAFE)
-  constexpr bool WS = kWinSafe<KIND, DIR, MULTI>;
+  constexpr bool WS = kWinSafe<KIND, DIR, MULTI> || kWinBuf<KIND, DIR, MULTI>;
   if (WS && DIR == 1)
     asm volatile("" ::"v"(W.h0), "v"(W.h1), "v"(W.h2), "v"(W.t0), "v"(W.t1), "v"(W.s0));
   else if (WS)  // (obfuscate loads no salt block)
@@ -1130,8 +1226,12 @@ __global__ __launch_bounds__(WPB * kWave) void obfs_kernel(const KParams P) {
   }
   SQ_STAMP(1);
   Windows W;
-  fetch_windows<DIR, KIND == 0 ? kSalamanderSalt : kXPlusSalt, kWinSafe<KIND, DIR, MULTI>>(
-      J, do_hash, (uint64_t)(P.in_off + p) & ~15ull, W);
+  constexpr uint32_t kSalt = KIND == 0 ? kSalamanderSalt : kXPlusSalt;
+  if constexpr (kWinBuf<KIND, DIR, MULTI>)
+    fetch_windows_buf<DIR, kSalt>(J, do_hash, W);
+  else
+    fetch_windows<DIR, kSalt, kWinSafe<KIND, DIR, MULTI>>(J, do_hash,
+                                                          (uint64_t)(P.in_off + p) & ~15ull, W);
   if (owner) P.out_len[p] = olen;
   // 3a. plan
   Geo G;
@@ -1141,6 +1241,7 @@ __global__ __launch_bounds__(WPB * kWave) void obfs_kernel(const KParams P) {
   SQ_STAMP(2);
   Step<U> cur;
   const uint32_t pid = MULTI && d.pid < P.n_psk ? d.pid : 0u;
+  if constexpr (kWinBuf<KIND, DIR, MULTI>) reload_windows<DIR, kSalt>(J, do_hash, W);
   // 2 + 3b. key and block contents
   fill_unit<KIND, DIR, MULTI>(P, J, salt, do_hash, pid, hot, W, owner, lane, ob, G, L);
   SQ_STAMP(3);

@@ -408,9 +408,14 @@ def engine_info(ctx: Context | None) -> EngineInfo:
 
 def make_batch(n, in_, in_off, in_len, out, out_off, out_len, salt=None,
                psk_id=None, in_cap=None, salt_out=None, flags=0) -> Batch:
-    """Batch from numpy arrays (host) or torch tensors (device)."""
-    return Batch(n, flags, _ptr(in_), _ptr(in_off), _ptr(in_len), _ptr(out), _ptr(out_off),
-                 _ptr(out_len), _ptr(salt), _ptr(psk_id), _ptr(in_cap), _ptr(salt_out))
+    """Batch from numpy arrays (host) or torch tensors (device).  The batch
+    holds references to them: a launch reads them after this returns, so a
+    temporary passed here must not be freed (and its memory reused) before
+    the batch is."""
+    b = Batch(n, flags, _ptr(in_), _ptr(in_off), _ptr(in_len), _ptr(out), _ptr(out_off),
+              _ptr(out_len), _ptr(salt), _ptr(psk_id), _ptr(in_cap), _ptr(salt_out))
+    b._keep = (in_, in_off, in_len, out, out_off, out_len, salt, psk_id, in_cap, salt_out)
+    return b
 
 
 def launch(ctx: Context, kr: Keyring, direction: int, batch: Batch,
@@ -727,8 +732,10 @@ class QuicKeyring:
 
 def quic_batch(n, in_, in_off, in_len, out, out_off, out_len, pn_offset, pn, key_id=None,
                pn_out=None) -> QuicBatch:
-    return QuicBatch(n, 0, _ptr(in_), _ptr(in_off), _ptr(in_len), _ptr(out), _ptr(out_off),
-                     _ptr(out_len), _ptr(pn_offset), _ptr(pn), _ptr(key_id), _ptr(pn_out))
+    b = QuicBatch(n, 0, _ptr(in_), _ptr(in_off), _ptr(in_len), _ptr(out), _ptr(out_off),
+                  _ptr(out_len), _ptr(pn_offset), _ptr(pn), _ptr(key_id), _ptr(pn_out))
+    b._keep = (in_, in_off, in_len, out, out_off, out_len, pn_offset, pn, key_id, pn_out)  # (make_batch)
+    return b
 
 
 def quic_seal(ctx: Context, kr: QuicKeyring, batch: QuicBatch, stream=None) -> None:

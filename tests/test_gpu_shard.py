@@ -136,9 +136,12 @@ def test_shard_launch_steps_in_flight(kind):
             d_back = torch.zeros_like(d_in)
             d_blen = torch.zeros(m, dtype=torch.int32, device=dev)
             d_wlen = t((hb.in_len[a:b] + S).astype(np.uint32))
-            obf = sqobfs.make_batch(m, d_in, d_ioff, d_len, d_out, d_ooff, d_olen,
-                                    t(hb.salt[S * a:S * b]))
+            d_salt = t(hb.salt[S * a:S * b])
+            # (each batch holds its tensors: shard 0's must outlive this loop,
+            # or shard 1's allocations reuse their memory before the launch)
+            obf = sqobfs.make_batch(m, d_in, d_ioff, d_len, d_out, d_ooff, d_olen, d_salt)
             deo = sqobfs.make_batch(m, d_out, d_ooff, d_wlen, d_back, d_ioff, d_blen)
+            assert obf._keep[1] is d_ioff and deo._keep[2] is d_wlen
             parts.append((a, b, obase, d_in, d_out, d_olen, d_back, d_blen, obf, deo))
             torch.cuda.synchronize(dev)
         t1 = sqobfs.shard_launch(ctxs, krs, OBFUSCATE, [p[8] for p in parts])
