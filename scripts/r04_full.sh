@@ -14,3 +14,6 @@ cat $O/smoke.log
 timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err \
   || { echo "bench rc=$?"; tail -20 $O/bench.err; exit 1; }
 cat $O/bench.json
+timeout -k 10 300 sing-quic_amd/bin/lat_bench > $O/lat.json 2> $O/lat.err \
+  || { echo "lat_bench rc=$?"; tail $O/lat.err; exit 1; }
+cat $O/lat.json

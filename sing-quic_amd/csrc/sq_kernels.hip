@@ -107,18 +107,6 @@ namespace sq {
 #define SQ_TIMELINE 0
 #endif
 
-#ifndef SQ_WINSAFE
-#define SQ_WINSAFE 1  // unconditional window loads (fetch_windows)
-#endif
-// Unconditional window loads: an unneeded block reads the packet's own first
-// input block when it has one (1) instead of the descriptor entry (0).
-#ifndef SQ_WINPKT
-#define SQ_WINPKT 0
-#endif
-// Window loads through a wave-uniform buffer resource (kWinBuf)
-#ifndef SQ_WINBUF
-#define SQ_WINBUF 0
-#endif
 // XCD-contiguous units.  Workgroups are dispatched round-robin over the 8
 // XCDs, so block b runs on XCD b % 8 and, unmapped, the XCDs share one
 // moving window of the batch.  Remapped, each XCD walks its own contiguous
@@ -144,8 +132,7 @@ extern "C" const char *sqobfs_build_info(void) {
          " minw=" SQ_STR(SQ_MINW) " wpb=2"
          " ablate=" SQ_STR(SQ_ABLATE) " donate=" SQ_STR(SQ_DONATE) " align=" SQ_STR(SQ_ALIGN)
          " map=" SQ_STR(SQ_MAPBLK)
-         " winsafe=" SQ_STR(SQ_WINSAFE) " winpkt=" SQ_STR(SQ_WINPKT) " winbuf=" SQ_STR(SQ_WINBUF)
-         " xcd=" SQ_STR(SQ_XCD);
+         " windows=buffer xcd=" SQ_STR(SQ_XCD);
 }
 
 // default unit size (KParams.ppw == 0); any 1 .. kMaxUnitPackets works
@@ -537,48 +524,32 @@ __device__ __forceinline__ bool tail_from_window(uint64_t rs, uint64_t re) {
 
 // The input blocks the packet's images need, all loaded together: the head
 // window (payload bytes [0, 32 - pre)) and the tail window (payload bytes of
-// the last partial output block).
+// the last partial output block); deobfuscate also the block before the head
+// when it holds salt bytes.
 //
-// SQ_WINSAFE: every lane issues all six loads unconditionally; a block the
-// packet does not need is read from `safe` (the aligned 16 bytes around its
-// descriptor entry, readable by construction: an aligned block holding one
-// readable byte lies in one page) and masked off at its use (ok bits) in
-// fill_unit.  Conditional loads left phi copies that the compiler resolved
-// with a full `s_waitcnt vmcnt(0)` right after the second head block, so
-// every wave waited for its windows (and, multi-PSK, its keyring entry)
-// before the plan instead of planning while they were in flight.
-// Measured per kernel in one process, three passes on two boxes (DESIGN.md
-// section 5, profiles/r03/ab/winsafe): Salamander obfuscate, one PSK,
-// -1.0 / -2.2 / -3.2 % on configs[1] and -0.5 / -0.6 / -0.9 % ragged; XPlus
-// deobfuscate -0.8 / -1.1 %; Salamander deobfuscate +0.3 / +1.0 / +1.2 %;
-// the multi-PSK obfuscate +5.7 %.  SQ_WINSAFE=1: the two kernels that gain;
-// 2: every kernel; 0: none.
-template <int KIND, int DIR, bool MULTI>
-constexpr bool kWinSafe =
-    SQ_WINSAFE == 2 || (SQ_WINSAFE == 1 && !MULTI && (KIND == 0) == (DIR == 0));
-// SQ_WINBUF: the six window loads are raw buffer loads against one
-// wave-uniform resource based at the wave's lowest window block; a block a
-// packet does not need gets an offset past num_records, so it reads zero
-// without a memory access: unconditional loads, no substitute reads, no
-// masks.  A lane whose blocks lie 4 GiB or more past that base (a ragged
-// batch scattered over more than 4 GiB within one unit) loads them again with
-// global loads where the images are built.
-// 1: the kernels kWinSafe leaves on conditional loads; 2: every kernel.
-template <int KIND, int DIR, bool MULTI>
-constexpr bool kWinBuf = SQ_WINBUF == 2 || (SQ_WINBUF == 1 && !kWinSafe<KIND, DIR, MULTI>);
+// The six loads are raw buffer loads against one wave-uniform resource based
+// at the wave's lowest window block.  A block a packet does not need gets an
+// offset past num_records, so it reads zero without a memory access: every
+// load is unconditional, with no substitute reads and no masks.  (Round 3
+// issued conditional global loads, whose phi copies the compiler resolved
+// with a full `s_waitcnt vmcnt(0)` before the plan, or unconditional loads
+// of a readable substitute block for two of the eight kernels.)  Measured in
+// one process against round 3's loads (DESIGN.md section 5,
+// profiles/r04/ab): ragged deobfuscate -1.2 % dense / -1.7 % in 16-byte
+// slots (both now >= 0.70), configs[1] deobfuscate -1.0 %, the 256-PSK
+// obfuscate -5.2 %, the other kernels -0.1 to -0.5 %.
+// A lane whose blocks lie 4 GiB or more past the base (a ragged batch
+// scattered over more than 4 GiB within one unit) loads those again with
+// 64-bit global loads where the images are built (reload_windows).
 struct Windows {
   u32x4 h0, h1, h2, t0, t1;
   u32x4 s0;     // deobfuscate: the block before h0 when it holds salt bytes
-  uint32_t ok;  // bits: h0 1, h1 2, h2 4, t0 8, t1 16, s0 32 (SQ_WINSAFE)
-  uint32_t rl;  // SQ_WINBUF: the needed blocks out of the resource's range
+  uint32_t rl;  // the needed blocks out of the resource's range
 };
 constexpr uint32_t kWinH0 = 1, kWinH1 = 2, kWinH2 = 4, kWinT0 = 8, kWinT1 = 16, kWinS0 = 32;
 constexpr uint32_t kWinOffNone = 0xFFFFFFF0u;  // past num_records: reads zero
 
-// Deobfuscate with a key (wire_salt): the salt is the S wire bytes before
-// the payload, [src_pay - S, src_pay); it lies in h0 and, when src_pay % 16 <
-// S, the block before it, loaded here with the head window.
-// The window block addresses of a packet (need bits as Windows::ok).
+// The window block addresses of a packet (need: bits kWin*).
 struct WinAddr {
   uint64_t s0, h0, h1, h2, t0, t1;
   uint32_t need;
@@ -609,11 +580,16 @@ __device__ __forceinline__ WinAddr window_addrs(const PacketJob &J, bool wire_sa
   return A;
 }
 
-// SQ_WINBUF loads (see kWinBuf).  Every needed block lies at or after h0 (or
-// s0) of its own packet: a tail block follows its head.
+// Every needed block lies at or after the packet's h0 (s0 when needed): a
+// tail block follows its head.
 template <int DIR, uint32_t S>
-__device__ __forceinline__ void fetch_windows_buf(const PacketJob &J, bool wire_salt,
-                                                  Windows &W) {
+__device__ __forceinline__ void fetch_windows(const PacketJob &J, bool wire_salt, Windows &W) {
+  if (SQ_ABLATE & 8) {
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    W.h0 = W.h1 = W.h2 = W.t0 = W.t1 = W.s0 = z;
+    W.rl = 0u;
+    return;
+  }
   const WinAddr A = window_addrs<DIR, S>(J, wire_salt);
   const uint64_t first = (A.need & kWinS0) ? A.s0 : A.h0;
   const uint64_t lo0 = uniform64(wave_min64(A.need ? first : ~0ull));
@@ -638,12 +614,11 @@ __device__ __forceinline__ void fetch_windows_buf(const PacketJob &J, bool wire_
   W.h2 = __builtin_amdgcn_raw_buffer_load_b128(R, o_h2, 0, 0);
   W.t0 = __builtin_amdgcn_raw_buffer_load_b128(R, o_t0, 0, 0);
   W.t1 = __builtin_amdgcn_raw_buffer_load_b128(R, o_t1, 0, 0);
-  W.ok = ~0u;  // unneeded blocks read zero
   W.rl = rl;
 }
 
-// The blocks fetch_windows_buf could not reach (rare: a unit scattered over
-// more than 4 GiB), loaded where the images are built.
+// The blocks fetch_windows could not reach, loaded where the images are
+// built (wave-uniform test; never taken for units within 4 GiB).
 template <int DIR, uint32_t S>
 __device__ __forceinline__ void reload_windows(const PacketJob &J, bool wire_salt, Windows &W) {
   if (__ballot(W.rl != 0u) == 0) return;
@@ -654,63 +629,6 @@ __device__ __forceinline__ void reload_windows(const PacketJob &J, bool wire_sal
   if (W.rl & kWinH2) W.h2 = gld<u32x4>(A.h2);
   if (W.rl & kWinT0) W.t0 = gld<u32x4>(A.t0);
   if (W.rl & kWinT1) W.t1 = gld<u32x4>(A.t1);
-}
-
-template <int DIR, uint32_t S, bool WS>
-__device__ __forceinline__ void fetch_windows(const PacketJob &J, bool wire_salt, uint64_t safe,
-                                              Windows &W) {
-  const u32x4 z = {0u, 0u, 0u, 0u};
-  W.h0 = W.h1 = W.h2 = W.t0 = W.t1 = W.s0 = z;
-  W.ok = 0u;
-  W.rl = 0u;
-  if (SQ_ABLATE & 8) return;
-  uint64_t rs, re;
-  bool ne;
-  out_range(J, rs, re, ne);
-  const uint64_t hw = !ne ? 0ull : (J.len < 32 - J.pre ? J.len : 32 - J.pre);
-  const uint64_t B = J.src_pay & ~15ull, e = J.src_pay + hw;
-  const bool c_h0 = hw != 0, c_h1 = c_h0 && e > B + 16, c_h2 = c_h0 && e > B + 32;
-  const bool c_s0 = SQ_SALTWIN && DIR == 1 && c_h0 && wire_salt && (J.src_pay & 15) < S;
-  const bool c_t0 = ne && tail_from_window(rs, re);
-  const uint64_t ta = J.src_pay + ((re & ~15ull) - J.dst_pay), te = J.src_pay + J.len;
-  const uint64_t TB = ta & ~15ull;
-  const bool c_t1 = c_t0 && te > TB + 16;
-  if (WS) {
-    // (an aligned block holding one readable byte is readable: B holds the
-    // first payload byte whenever the packet needs a window at all)
-    if (SQ_WINPKT && c_h0) safe = B;
-    const uint64_t a_s0 = c_s0 ? B - 16 : safe, a_h0 = c_h0 ? B : safe,
-                   a_h1 = c_h1 ? B + 16 : safe, a_h2 = c_h2 ? B + 32 : safe,
-                   a_t0 = c_t0 ? TB : safe, a_t1 = c_t1 ? TB + 16 : safe;
-    // every address before the first load: otherwise the scheduler issues a
-    // load and then computes another address into that load's destination
-    // registers, which costs a wait for the load
-    asm volatile("" ::"v"(a_s0), "v"(a_h0), "v"(a_h1), "v"(a_h2), "v"(a_t0), "v"(a_t1)
-                 : "memory");
-    W.s0 = gld<u32x4>(a_s0);
-    W.h0 = gld<u32x4>(a_h0);
-    W.h1 = gld<u32x4>(a_h1);
-    W.h2 = gld<u32x4>(a_h2);
-    W.t0 = gld<u32x4>(a_t0);
-    W.t1 = gld<u32x4>(a_t1);
-    W.ok = (c_h0 ? kWinH0 : 0u) | (c_h1 ? kWinH1 : 0u) | (c_h2 ? kWinH2 : 0u) |
-           (c_t0 ? kWinT0 : 0u) | (c_t1 ? kWinT1 : 0u) | (c_s0 ? kWinS0 : 0u);
-  } else {
-    if (c_s0) W.s0 = gld<u32x4>(B - 16);
-    if (c_h0) W.h0 = gld<u32x4>(B);
-    if (c_h1) W.h1 = gld<u32x4>(B + 16);
-    if (c_h2) W.h2 = gld<u32x4>(B + 32);
-    if (c_t0) W.t0 = gld<u32x4>(TB);
-    if (c_t1) W.t1 = gld<u32x4>(TB + 16);
-    W.ok = ~0u;
-  }
-}
-
-// A window block, zero unless the packet needed it (applied where the
-// images are built, after the plan).
-__device__ __forceinline__ u32x4 win_blk(const Windows &W, const u32x4 &v, uint32_t bit) {
-  const u32x4 z = {0u, 0u, 0u, 0u};
-  return (W.ok & bit) ? v : z;
 }
 
 // LDS record of a packet with blocks in the flat space (96 B), stored at the
@@ -941,16 +859,14 @@ __device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
   uint32_t sl[4] = {salt[0], salt[1], salt[2], salt[3]};
   // every window register stays allocated until here: a component no image
   // uses would otherwise be handed to the plan while its load is in flight,
-  // and overwriting it waits for the load (SQ_WINSAFE)
-  constexpr bool WS = kWinSafe<KIND, DIR, MULTI> || kWinBuf<KIND, DIR, MULTI>;
-  if (WS && DIR == 1)
+  // and overwriting it waits for the load
+  if (DIR == 1)
     asm volatile("" ::"v"(W.h0), "v"(W.h1), "v"(W.h2), "v"(W.t0), "v"(W.t1), "v"(W.s0));
-  else if (WS)  // (obfuscate loads no salt block)
+  else  // (obfuscate loads no salt block)
     asm volatile("" ::"v"(W.h0), "v"(W.h1), "v"(W.h2), "v"(W.t0), "v"(W.t1));
-  const u32x4 wh0 = win_blk(W, W.h0, kWinH0), wh1 = win_blk(W, W.h1, kWinH1),
-              wh2 = win_blk(W, W.h2, kWinH2);
+  const u32x4 wh0 = W.h0, wh1 = W.h1, wh2 = W.h2;
   if (SQ_SALTWIN && DIR == 1) {  // the wire salt, from the head window
-    const u32x4 ws0 = win_blk(W, W.s0, kWinS0);
+    const u32x4 ws0 = W.s0;
     const uint32_t w[12] = {ws0.x, ws0.y, ws0.z, ws0.w, wh0.x, wh0.y,
                             wh0.z, wh0.w, wh1.x, wh1.y, wh1.z, wh1.w};
     win16(w, (uint32_t)(J.src_pay & 15) + 16 - S, sl);
@@ -989,7 +905,7 @@ __device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
   uint32_t ti[4];
   if (tail_from_window(rs, re)) {
     const uint64_t ta = J.src_pay + (BL - J.dst_pay);
-    const u32x4 wt0 = win_blk(W, W.t0, kWinT0), wt1 = win_blk(W, W.t1, kWinT1);
+    const u32x4 wt0 = W.t0, wt1 = W.t1;
     const uint32_t w[12] = {0u, 0u, 0u, 0u, wt0.x, wt0.y, wt0.z, wt0.w,
                             wt1.x, wt1.y, wt1.z, wt1.w};
     uint32_t ks[4];
@@ -1227,11 +1143,7 @@ __global__ __launch_bounds__(WPB * kWave) void obfs_kernel(const KParams P) {
   SQ_STAMP(1);
   Windows W;
   constexpr uint32_t kSalt = KIND == 0 ? kSalamanderSalt : kXPlusSalt;
-  if constexpr (kWinBuf<KIND, DIR, MULTI>)
-    fetch_windows_buf<DIR, kSalt>(J, do_hash, W);
-  else
-    fetch_windows<DIR, kSalt, kWinSafe<KIND, DIR, MULTI>>(J, do_hash,
-                                                          (uint64_t)(P.in_off + p) & ~15ull, W);
+  fetch_windows<DIR, kSalt>(J, do_hash, W);
   if (owner) P.out_len[p] = olen;
   // 3a. plan
   Geo G;
@@ -1241,7 +1153,7 @@ __global__ __launch_bounds__(WPB * kWave) void obfs_kernel(const KParams P) {
   SQ_STAMP(2);
   Step<U> cur;
   const uint32_t pid = MULTI && d.pid < P.n_psk ? d.pid : 0u;
-  if constexpr (kWinBuf<KIND, DIR, MULTI>) reload_windows<DIR, kSalt>(J, do_hash, W);
+  reload_windows<DIR, kSalt>(J, do_hash, W);
   // 2 + 3b. key and block contents
   fill_unit<KIND, DIR, MULTI>(P, J, salt, do_hash, pid, hot, W, owner, lane, ob, G, L);
   SQ_STAMP(3);
