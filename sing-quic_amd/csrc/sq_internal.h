@@ -147,6 +147,9 @@ struct QGParams {
   const uint64_t *pn;
   const uint16_t *key_id;
   uint64_t *pn_out;
+  const uint32_t *perm;  // multi-key: packet indices grouped by key (or null)
+  uint32_t *units;       // grouped: the units the staged kernel left (or null)
+  uint32_t *units_n;     // ... and their count
   const QuicGcmKeyDev *keys;
   const uint32_t *t0;
   uint32_t n;
@@ -196,6 +199,14 @@ void sq_engine_ctx_closed(sqobfs_ctx *ctx);
 
 // launchers implemented in sq_quic_gcm.hip
 extern "C" int sq_launch_quic_gcm(int open, const sq::QGParams *qp, void *stream);
+// Multi-key AES-128-GCM batches: the packet permutation that groups them by
+// key (stable counting sort).  sq_gcm_group_scratch: the device scratch it
+// needs (perm[n] | histograms | deferred-unit count | deferred units), 0 when
+// such a batch is not grouped (too few packets or too many keys).  sq_launch_gcm_group returns 1 when not
+// grouped, 0 on success, < 0 on a launch error.
+extern "C" uint64_t sq_gcm_group_scratch(uint32_t n, uint32_t n_keys);
+extern "C" int sq_launch_gcm_group(const uint16_t *key_id, uint32_t n, uint32_t n_keys,
+                                   void *scratch, void *stream);
 
 // launchers implemented in sq_quic.hip
 extern "C" int sq_launch_quic(int open, const sq::QParams *qp, void *stream);

@@ -42,8 +42,13 @@
 // Payloads above 2,048 B (chunk multipliers past H^128) are walked by their
 // owner lane in phase 3 (plain Horner), so any length works.
 // Single-key launches keep the round keys in the kernarg segment (scalar
-// operands) and the GHASH tables in LDS; multi-key launches read both from
-// the packet's keyring entry in global memory.
+// operands) and the GHASH tables in LDS.  Multi-key launches of a large
+// batch first group the packets by key (a stable counting sort,
+// gcm_group_*: a permutation of the packet indices); each workgroup then
+// stages the key of its current units (round keys and GHASH tables, 40 KiB)
+// in LDS, and a wave whose packets all use that key runs the single-key code
+// on it.  Waves across a key boundary, and small or ungrouped batches, read
+// the packet's keyring entry from global memory.
 #include <hip/hip_runtime.h>
 
 #include "sq_bytes.h"
@@ -83,12 +88,19 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, int n) {
   return __builtin_amdgcn_alignbit(x, x, 32 - n);
 }
 
-// round key r (4 column words): kernarg (single key) or the lane's entry
-template <bool MULTI>
+// Where a launch's keys live (KM): 0 one key (round keys in the kernarg
+// segment, GHASH tables in LDS), 1 per-packet keyring entries in global
+// memory, 2 the workgroup's staged key (round keys and tables in LDS).
+// round key r (4 column words); KM 2 reads them wave-uniform into SGPRs, as
+// the kernarg ones are
+template <int KM>
 __device__ __forceinline__ void round_key(const uint32_t *rk, int r, uint32_t (&k)[4]) {
-  if (MULTI) {
+  if (KM == 1) {
     const u32x4 v = gld<u32x4>((uint64_t)(rk + 4 * r));
     k[0] = v.x; k[1] = v.y; k[2] = v.z; k[3] = v.w;
+  } else if (KM == 2) {
+#pragma unroll
+    for (int c = 0; c < 4; c++) k[c] = __builtin_amdgcn_readfirstlane(rk[4 * r + c]);
   } else {
     k[0] = rk[4 * r]; k[1] = rk[4 * r + 1]; k[2] = rk[4 * r + 2]; k[3] = rk[4 * r + 3];
   }
@@ -114,18 +126,18 @@ __device__ __forceinline__ uint32_t t1at(const uint32_t *tT, uint32_t a) {
 // T1[s_c+3.b3]) ^ rk (T2 = rotl16 T0, T3 = rotl16 T1; ShiftRows folded into
 // the byte picks); the last round takes the S-box byte (T0 byte 1, T1 bytes
 // 2 and 3) instead.
-template <bool MULTI, int NB>
+template <int KM, int NB>
 __device__ __forceinline__ void aes_encrypt_n(const uint32_t *rk, const uint32_t *tT, uint32_t lo,
                                               uint32_t (&s)[NB][4]) {
   uint32_t k[4];
-  round_key<MULTI>(rk, 0, k);
+  round_key<KM>(rk, 0, k);
 #pragma unroll
   for (int q = 0; q < NB; q++)
 #pragma unroll
     for (int c = 0; c < 4; c++) s[q][c] ^= k[c];
 #pragma unroll
   for (int r = 1; r < 10; r++) {
-    round_key<MULTI>(rk, r, k);
+    round_key<KM>(rk, r, k);
     uint32_t t[NB][4];
 #pragma unroll
     for (int q = 0; q < NB; q++)
@@ -142,7 +154,7 @@ __device__ __forceinline__ void aes_encrypt_n(const uint32_t *rk, const uint32_t
 #pragma unroll
       for (int c = 0; c < 4; c++) s[q][c] = t[q][c];
   }
-  round_key<MULTI>(rk, 10, k);
+  round_key<KM>(rk, 10, k);
   uint32_t t[NB][4];
 #pragma unroll
   for (int q = 0; q < NB; q++)
@@ -161,11 +173,11 @@ __device__ __forceinline__ void aes_encrypt_n(const uint32_t *rk, const uint32_t
     for (int c = 0; c < 4; c++) s[q][c] = t[q][c];
 }
 
-template <bool MULTI>
+template <int KM>
 __device__ __forceinline__ void aes_encrypt(const uint32_t *rk, const uint32_t *tT, uint32_t lo,
                                             uint32_t (&s)[4]) {
   uint32_t b[1][4] = {{s[0], s[1], s[2], s[3]}};
-  aes_encrypt_n<MULTI, 1>(rk, tT, lo, b);
+  aes_encrypt_n<KM, 1>(rk, tT, lo, b);
 #pragma unroll
   for (int c = 0; c < 4; c++) s[c] = b[0][c];
 }
@@ -248,13 +260,13 @@ __device__ __forceinline__ void ghash_absorb(uint32_t (&y)[4], const uint32_t (&
 
 // Key material of one packet: round keys, header-protection round keys,
 // IV, and the GHASH tables (table k-1 = H^k).
-template <bool MULTI>
+template <int KM>
 struct GKey {
   const uint32_t *rk, *hrk, *iv, *hpos, *htab;
   __device__ __forceinline__ const uint32_t *pow(uint32_t k) const { return htab + 64 * (k - 1); }
   // x <- x * H^k (k = 1 .. kGcmPow)
   __device__ __forceinline__ void mul_pow(uint32_t (&x)[4], uint32_t k) const {
-    gmul<MULTI>(x, pow(k), (k - 1) & 15u);
+    gmul<KM == 1>(x, pow(k), (k - 1) & 15u);
   }
 };
 
@@ -268,8 +280,8 @@ struct GKey {
 // OB (fused Salamander layer): output (seal) or input (open) bytes are also
 // XORed with the packet's Salamander key; okr = the key rotated to the first
 // byte at src / dst (16-byte block j uses half j & 1).
-template <bool OPEN, bool MULTI, bool OB>
-__device__ __forceinline__ void gcm_run(const GKey<MULTI> &K, const uint32_t *tT, uint32_t tcol,
+template <bool OPEN, int KM, bool OB>
+__device__ __forceinline__ void gcm_run(const GKey<KM> &K, const uint32_t *tT, uint32_t tcol,
                                         const uint32_t (&nonce)[3], uint32_t ctr0, uint64_t src,
                                         uint64_t dst, uint32_t nv, uint32_t (&y)[4],
                                         uint32_t (&first32)[8], const uint32_t (&okr)[8]) {
@@ -296,7 +308,7 @@ __device__ __forceinline__ void gcm_run(const GKey<MULTI> &K, const uint32_t *tT
   auto finish = [&](uint32_t j, const uint32_t (&in)[4], const uint32_t (&c0)[4]) {
     const uint32_t(&g)[4] = OPEN ? in : c0;
     ghash_absorb(y, g);
-    gmul_pos<MULTI>(y, K.hpos);
+    gmul_pos<KM == 1>(y, K.hpos);
 #pragma unroll
     for (int w = 0; w < 4; w++) {
       first32[w] = bsel(j == 0, g[w], first32[w]);
@@ -324,7 +336,7 @@ __device__ __forceinline__ void gcm_run(const GKey<MULTI> &K, const uint32_t *tT
     uint32_t in[4], c[4];
     uint32_t s1[4] = {nonce[0], nonce[1], nonce[2], __builtin_bswap32(ctr0 + j)};
     funnel(A, Bq, ib, in);
-    aes_encrypt<MULTI>(K.rk, tT, tcol, s1);
+    aes_encrypt<KM>(K.rk, tT, tcol, s1);
     const int nb = (int)nv - 16 * (int)j;
 #pragma unroll
     for (int w = 0; w < 4; w++) {
@@ -347,7 +359,7 @@ __device__ __forceinline__ void gcm_run(const GKey<MULTI> &K, const uint32_t *tT
                          {nonce[0], nonce[1], nonce[2], __builtin_bswap32(ctr0 + j + 1)}};
     funnel(A, Bq, ib, in[0]);
     funnel(Bq, C, ib, in[1]);
-    aes_encrypt_n<MULTI, 2>(K.rk, tT, tcol, s2);
+    aes_encrypt_n<KM, 2>(K.rk, tT, tcol, s2);
 #pragma unroll
     for (int q = 0; q < 2; q++) {
       const int nb = (int)nv - 16 * (int)(j + q);  // valid bytes (may be <= 0)
@@ -377,12 +389,12 @@ __device__ __forceinline__ void gcm_run(const GKey<MULTI> &K, const uint32_t *tT
 }
 
 // 5 header-protection mask bytes (RFC 9001 5.4.3): AES-ECB(hp, sample)
-template <bool MULTI>
-__device__ __forceinline__ void gcm_hp_mask(const GKey<MULTI> &K, const uint32_t *tT, uint32_t tcol,
+template <int KM>
+__device__ __forceinline__ void gcm_hp_mask(const GKey<KM> &K, const uint32_t *tT, uint32_t tcol,
                                             const uint32_t (&sample)[4], uint32_t &m0,
                                             uint32_t &m1) {
   uint32_t s[4] = {sample[0], sample[1], sample[2], sample[3]};
-  aes_encrypt<MULTI>(K.hrk, tT, tcol, s);
+  aes_encrypt<KM>(K.hrk, tT, tcol, s);
   m0 = s[0];
   m1 = s[1] & 0xFFu;
 }
@@ -399,14 +411,18 @@ struct alignas(16) GRec {
   uint32_t okr[8];     // fused Salamander layer: key rotated to the payload start
 };
 
-template <bool MULTI>
-__device__ __forceinline__ GKey<MULTI> key_of(const QGParams &Q, uint32_t kid, const uint32_t *tP,
-                                              const uint32_t *tH, const uint32_t *tK) {
-  GKey<MULTI> K;
+// STAGED: the workgroup's staged key (round keys, IV and GHASH tables in LDS)
+template <bool MULTI, bool STAGED>
+__device__ __forceinline__ GKey<MULTI ? 1 : (STAGED ? 2 : 0)> key_of(
+    const QGParams &Q, uint32_t kid, const uint32_t *tP, const uint32_t *tH, const uint32_t *tK) {
+  GKey<MULTI ? 1 : (STAGED ? 2 : 0)> K;
   if (MULTI) {
     const QuicGcmKeyDev *E = Q.keys + kid;
     K.rk = E->rk; K.hrk = E->hrk; K.iv = E->iv;
     K.hpos = &E->hpos[0][0][0]; K.htab = &E->htab[0][0][0];
+  } else if (STAGED) {
+    K.rk = tK; K.hrk = tK + 44; K.iv = tK + 88;
+    K.hpos = tP; K.htab = tH;
   } else {
 #if SQ_GRK_LDS
     K.rk = tK; K.hrk = tK + 44;
@@ -418,14 +434,315 @@ __device__ __forceinline__ GKey<MULTI> key_of(const QGParams &Q, uint32_t kid, c
   return K;
 }
 
-template <bool OPEN, bool MULTI, bool OB>
-__global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
-  __shared__ uint32_t tT[256 * 64];
-  __shared__ __attribute__((aligned(16))) uint32_t tP[MULTI ? 4 : 32 * 64];
-  __shared__ __attribute__((aligned(16))) uint32_t tH[MULTI ? 4 : kGcmPow * 64];
-  __shared__ GRec recs[kGWaves][kGPpw];
-  __shared__ __attribute__((aligned(16))) uint32_t tK[88];  // single key: rk0 || hrk0
-  // stage the T-table image and (single key) the round keys and GHASH tables
+constexpr uint32_t kNoKey = 0xFFFFFFFFu;
+
+// Copy keyring entry E's round keys, IV and GHASH tables into the block's
+// LDS (every thread of the block takes part).
+__device__ __forceinline__ void stage_key(const QuicGcmKeyDev *E, uint32_t *tP, uint32_t *tH,
+                                          uint32_t *tK) {
+  if (threadIdx.x < 91) {
+    const uint32_t i = threadIdx.x;
+    tK[i] = i < 44 ? E->rk[i] : (i < 88 ? E->hrk[i - 44] : E->iv[i - 88]);
+  }
+  const uint32_t *src = &E->hpos[0][0][0];  // hpos then htab, contiguous
+  for (uint32_t i = threadIdx.x; i < (32 + kGcmPow) * 16; i += kGBlock) {
+    const u32x4 v = gld<u32x4>((uint64_t)(src + 4 * i));
+    if (i < 32 * 16) *(u32x4 *)(tP + 4 * i) = v;
+    else *(u32x4 *)(tH + 4 * (i - 32 * 16)) = v;
+  }
+}
+
+// One unit (kGPpw packets) of a wave: the three phases.  recs = the wave's
+// records.  STAGED (with MULTI false): every packet of the unit uses the
+// workgroup's staged key.
+template <bool OPEN, bool MULTI, bool OB, bool STAGED>
+__device__ __forceinline__ void gcm_unit(const QGParams &Q, uint64_t u, uint32_t lane,
+                                         const uint32_t *tT, uint32_t tcol, const uint32_t *tP,
+                                         const uint32_t *tH, const uint32_t *tK, GRec *recs) {
+  constexpr int KM = MULTI ? 1 : (STAGED ? 2 : 0);
+  const uint64_t i64 = u * kGPpw + lane;
+  const bool owner = lane < kGPpw && i64 < Q.n;
+  // grouped batches: the packet at this position of the key order
+  const uint32_t p = owner && Q.perm ? Q.perm[i64] : (uint32_t)i64;
+
+  // ---- 1. owner lanes
+  bool live = owner;
+  uint64_t pn_dec = 0;  // open: decoded packet number (0 if rejected)
+uint32_t status = 0, len = 0, pno = 0, first = 0, pn_len = 0, hdr = 0, pl = 0, kid = 0;
+  uint64_t src = 0, dst = 0;
+  uint32_t nonce[3] = {0u, 0u, 0u}, rtag[4] = {0u, 0u, 0u, 0u}, y[4] = {0u, 0u, 0u, 0u};
+  uint32_t hd[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, pnw = 0;  // packet bytes 0..31; seal: pn bytes
+  // fused Salamander layer (OB): wire = salt8 || QUIC packet ^ okey
+  uint64_t wire = 0;
+  uint32_t okey[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, osalt[4] = {0u, 0u, 0u, 0u};
+  if (live && MULTI) {
+    kid = Q.key_id[p];
+    if (kid >= Q.n_keys) {
+      status = kQEKey;
+      live = false;
+      kid = 0;
+      if (OPEN && Q.pn_out) Q.pn_out[p] = 0;  // rejected: pn_out 0 (as below)
+    }
+  }
+  const GKey<KM> K = key_of<MULTI, STAGED>(Q, kid, tP, tH, tK);
+  if (live) {
+    src = (uint64_t)Q.in + Q.in_off[p];
+    dst = (uint64_t)Q.out + Q.out_off[p];
+    len = Q.in_len[p];
+    pno = Q.pn_offset[p];
+    uint64_t pn = Q.pn[p];
+    uint32_t pnb[4] = {0u, 0u, 0u, 0u};
+    if (OB) {
+      if (!OPEN) {  // wire = salt || protected packet ^ key
+        wire = dst;
+        dst = wire + kSalamanderSalt;
+        const uint32_t *sp = reinterpret_cast<const uint32_t *>(Q.osalt + 8ull * p);
+        osalt[0] = sp[0];
+        osalt[1] = sp[1];
+      } else if (len >= (uint32_t)kSalamanderSalt && len <= kQMaxPacket) {
+        wire = src;  // salt = the first 8 wire bytes (salamander.go:50)
+        load16(src, src + kSalamanderSalt, osalt);
+        src += kSalamanderSalt;
+        len -= kSalamanderSalt;
+      } else {
+        len = 0;  // too short for a salt: rejected below
+      }
+      salamander_key(&Q.opsk, osalt, okey);
+    }
+    // packet byte k (de-obfuscated when the fused layer is on)
+    auto hb = [&](uint32_t k) -> uint32_t {
+      const uint32_t b = head_byte(hd, src, k);
+      return (OB && OPEN && k >= 32) ? b ^ byte32(okey, k & 31) : b;
+    };
+    if (!OPEN) {
+      if (len) load_head32(src, len, hd);
+      first = hd[0] & 0xFFu;
+      pn_len = (first & 3) + 1;
+      hdr = pno + pn_len;
+      if (len == 0 || len > kQMaxPacket || hdr > len || pno + 4 > len) {
+        live = false;
+      } else {
+        pl = len - hdr;
+        for (uint32_t i = 0; i < pn_len; i++) pnw |= hb(pno + i) << (8 * i);
+      }
+    } else if (len < 16 || len > kQMaxPacket || pno + 4 + 16 > len) {
+      live = false;
+    } else {
+      uint32_t sample[4], m0, m1;
+      load16(src + pno + 4, src + len, sample);
+      load16(src + len - 16, src + len, rtag);  // before any in-place write
+      load_head32(src, len, hd);
+      if (OB) {  // de-obfuscate what was read: key byte of QUIC offset k is okey[k % 32]
+        uint32_t k4[4];
+        keywin(okey, (pno + 4) & 31, k4);
+#pragma unroll
+        for (int w = 0; w < 4; w++) sample[w] ^= k4[w];
+        keywin(okey, (len - 16) & 31, k4);
+#pragma unroll
+        for (int w = 0; w < 4; w++) rtag[w] ^= k4[w];
+        keywin(okey, 0, k4);
+#pragma unroll
+        for (int w = 0; w < 4; w++) hd[w] ^= k4[w];
+        keywin(okey, 16, k4);
+#pragma unroll
+        for (int w = 0; w < 4; w++) hd[4 + w] ^= k4[w];
+      }
+      gcm_hp_mask<KM>(K, tT, tcol, sample, m0, m1);
+      const uint32_t pfirst = hd[0] & 0xFFu;
+      first = pfirst ^ (m0 & ((pfirst & 0x80) ? 0x0Fu : 0x1Fu));
+      pn_len = (first & 3) + 1;
+      hdr = pno + pn_len;
+      if (hdr > len - 16) {
+        live = false;
+      } else {
+        uint64_t trunc = 0;
+        for (uint32_t i = 0; i < pn_len; i++) {
+          pnb[i] = hb(pno + i) ^ mask_byte(m0, m1, 1 + i);
+          trunc = (trunc << 8) | pnb[i];
+        }
+        pn = decode_pn(pn, trunc, 8 * pn_len);
+        pn_dec = pn;
+        pl = len - 16 - hdr;
+      }
+    }
+    if (!live) status = kQEShort;
+  // every owner lane writes its pn_out (0 when the packet was rejected)
+  if (OPEN && owner && Q.pn_out) Q.pn_out[p] = pn_dec;
+    if (live) {
+      const uint32_t iv[3] = {K.iv[0], K.iv[1], K.iv[2]};
+      quic_nonce_iv(iv, pn, nonce);
+      // AAD = the unprotected header; seal copies it unchanged (protection
+      // is applied in phase 3), open writes the unprotected header
+      for (uint32_t q = 0; q < hdr; q += 16) {
+        uint32_t w[4];
+        head_block(hd, src, q, hdr, w);
+        if (OB && OPEN && q >= 32) {
+          uint32_t k4[4];
+          keywin(okey, q & 31, k4);
+#pragma unroll
+          for (int j = 0; j < 4; j++) w[j] ^= k4[j] & range_mask(0, (int)(hdr - q), j);
+        }
+        if (OPEN) {
+          if (q == 0) set_byte(w, 0, first);
+          for (uint32_t i = 0; i < pn_len; i++) {
+            const uint32_t pos = pno + i;
+            if (pos >= q && pos < q + 16) set_byte(w, pos - q, pnb[i]);
+          }
+        }
+        ghash_absorb(y, w);
+        gmul_pos<MULTI>(y, K.hpos);
+        if (OB && !OPEN) {  // the wire carries the (still unprotected) header ^ key
+          uint32_t k4[4];
+          keywin(okey, q & 31, k4);
+#pragma unroll
+          for (int j = 0; j < 4; j++) w[j] ^= k4[j];
+        }
+        if (OPEN || OB || dst != src) store16(dst + q, w, hdr - q < 16 ? hdr - q : 16);
+      }
+    }
+  }
+  const bool coop = live && pl <= kGCoopMax;
+  const uint32_t np = (pl + 15) / 16;
+  // the header's GHASH, placed ahead of the payload blocks
+  if (coop && np) K.mul_pow(y, np);
+  const uint32_t nblk = coop ? (pl + 63) / 64 : 0u;
+  uint32_t incl = nblk;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const uint32_t t = __shfl_up(incl, d, kWave);
+    if (lane >= (uint32_t)d) incl += t;
+  }
+  const uint32_t start = incl - nblk, T = __shfl(incl, kWave - 1, kWave);
+  if (lane < kGPpw) {
+    GRec &R = recs[lane];
+    R.src = src + hdr;
+    R.dst = dst + hdr;
+    R.pl = pl;
+    R.start = start;
+    R.np = np;
+    R.kid = kid;
+#pragma unroll
+    for (int i = 0; i < 3; i++) R.nonce[i] = nonce[i];
+#pragma unroll
+    for (int i = 0; i < 4; i++) R.x[i] = coop ? y[i] : 0u;
+#pragma unroll
+    for (int i = 0; i < 8; i++) R.ct32[i] = 0u;
+    if (OB) {
+      uint32_t k4[4];
+      keywin(okey, hdr & 31, k4);
+#pragma unroll
+      for (int i = 0; i < 4; i++) R.okr[i] = k4[i];
+      keywin(okey, (hdr + 16) & 31, k4);
+#pragma unroll
+      for (int i = 0; i < 4; i++) R.okr[4 + i] = k4[i];
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+  // ---- 2. cooperative payload pass over the flat chunk space
+  for (uint32_t base = 0; base < T; base += kWave) {
+    const uint32_t f = base + lane;
+    const uint32_t pp = q_locate(start, base, f < T ? f : T - 1);
+    if (f < T) {
+      GRec &R = recs[pp];
+      const GKey<KM> KB = key_of<MULTI, STAGED>(Q, R.kid, tP, tH, tK);
+      const uint32_t b = f - R.start, off0 = 64 * b;
+      const uint32_t nv = R.pl - off0 < 64 ? R.pl - off0 : 64u;
+      const uint32_t rn[3] = {R.nonce[0], R.nonce[1], R.nonce[2]};
+      uint32_t yb[4] = {0u, 0u, 0u, 0u}, f32[8];
+      uint32_t rokr[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) rokr[i] = OB ? R.okr[i] : 0u;
+      gcm_run<OPEN, KM, OB>(KB, tT, tcol, rn, 2 + 4 * b, R.src + off0, R.dst + off0, nv, yb,
+                               f32, rokr);
+      const uint32_t m = R.np - 4 * b - (nv + 15) / 16;  // payload blocks after this chunk
+      if (m) KB.mul_pow(yb, m);
+#pragma unroll
+      for (int i = 0; i < 4; i++) atomicXor(&R.x[i], yb[i]);
+      if (!OPEN && b == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) R.ct32[i] = f32[i];
+      }
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+  // ---- 3. owner lanes: lengths block, tag, header protection
+  if (!owner) return;
+  if (!live) {
+    Q.out_len[p] = status;
+    return;
+  }
+  uint32_t ct32[8];
+  if (coop) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) y[i] = recs[lane].x[i];
+#pragma unroll
+    for (int i = 0; i < 8; i++) ct32[i] = recs[lane].ct32[i];
+  } else {
+    uint32_t rokr[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) rokr[i] = OB ? recs[lane].okr[i] : 0u;
+    gcm_run<OPEN, KM, OB>(K, tT, tcol, nonce, 2, src + hdr, dst + hdr, pl, y, ct32, rokr);
+  }
+  // lengths block: be64(8 * hdr) || be64(8 * pl)
+  y[1] ^= 8 * hdr;
+  y[2] ^= pl >> 29;
+  y[3] ^= 8 * pl;
+  gmul_pos<MULTI>(y, K.hpos);
+  uint32_t tag[4] = {nonce[0], nonce[1], nonce[2], __builtin_bswap32(1u)};
+  aes_encrypt<KM>(K.rk, tT, tcol, tag);  // E(K, J0)
+#pragma unroll
+  for (int w = 0; w < 4; w++) tag[w] ^= __builtin_bswap32(y[w]);
+  if (OPEN) {
+    const bool ok = ((tag[0] ^ rtag[0]) | (tag[1] ^ rtag[1]) | (tag[2] ^ rtag[2]) |
+                     (tag[3] ^ rtag[3])) == 0;
+    Q.out_len[p] = ok ? len - 16 : kQEAuth;
+    return;
+  }
+  if (OB) {
+    uint32_t k4[4], t4[4];
+    keywin(okey, len & 31, k4);
+#pragma unroll
+    for (int w = 0; w < 4; w++) t4[w] = tag[w] ^ k4[w];
+    store16(dst + len, t4, 16);
+    store16(wire, osalt, kSalamanderSalt);
+  } else {
+    store16(dst + len, tag, 16);
+  }
+  // header protection: sample = (ciphertext || tag)[4 - pn_len ..][0..16)
+  const uint32_t so = 4 - pn_len;
+  uint32_t sample[4];
+  if (pl >= so + 16) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) sample[j] = __builtin_amdgcn_alignbyte(ct32[j + 1], ct32[j], so);
+  } else {  // short payload: the sample reaches into the tag
+    const uint32_t t8[8] = {tag[0], tag[1], tag[2], tag[3], 0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int j = 0; j < 4; j++) sample[j] = 0u;
+    for (uint32_t i = 0; i < 16; i++) {
+      const uint32_t k = so + i;
+      const uint32_t bb = k < pl ? byte32(ct32, k) : byte32(t8, k - pl);
+      sample[i >> 2] |= bb << (8 * (i & 3));
+    }
+  }
+  uint32_t m0, m1;
+  gcm_hp_mask<KM>(K, tT, tcol, sample, m0, m1);
+  const uint32_t kb0 = OB ? okey[0] & 0xFFu : 0u;
+  gst<uint8_t>(dst, (uint8_t)(first ^ kb0 ^ (m0 & ((first & 0x80) ? 0x0Fu : 0x1Fu))));
+  for (uint32_t i = 0; i < pn_len; i++) {
+    const uint32_t bb = (pnw >> (8 * i)) & 0xFFu;
+    const uint32_t kb = OB ? byte32(okey, (pno + i) & 31) : 0u;
+    gst<uint8_t>(dst + pno + i, (uint8_t)(bb ^ kb ^ mask_byte(m0, m1, 1 + i)));
+  }
+  Q.out_len[p] = len + 16 + (OB ? kSalamanderSalt : 0u);
+}
+
+// The T-table image (every launch) and, single key, the key's GHASH tables
+// and round keys, into LDS.
+template <bool MULTI>
+__device__ __forceinline__ void stage_common(const QGParams &Q, uint32_t *tT, uint32_t *tP,
+                                             uint32_t *tH, uint32_t *tK) {
   for (uint32_t i = threadIdx.x; i < 256 * 64; i += kGBlock) {
     const uint32_t v = Q.t0[i >> 6];
     tT[i] = (i & 32) ? rotl(v, 8) : v;
@@ -440,305 +757,210 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
       else *(u32x4 *)(tH + 4 * (i - 32 * 16)) = v;
     }
   }
+}
+
+// One key (MULTI false) or per-packet keys from the keyring in global memory
+// (MULTI true): every unit of the batch, or (Q.units) the units of that list.
+template <bool OPEN, bool MULTI, bool OB>
+__global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
+  __shared__ uint32_t tT[256 * 64];
+  __shared__ __attribute__((aligned(16))) uint32_t tP[MULTI ? 4 : 32 * 64];
+  __shared__ __attribute__((aligned(16))) uint32_t tH[MULTI ? 4 : kGcmPow * 64];
+  __shared__ GRec recs[kGWaves][kGPpw];
+  __shared__ __attribute__((aligned(16))) uint32_t tK[88];  // single key: rk0 || hrk0
+  stage_common<MULTI>(Q, tT, tP, tH, tK);
   __syncthreads();
   const uint32_t lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
   const uint32_t tcol = 4 * (lane & 31);  // this lane's T-table column (byte offset)
+  const uint64_t units = Q.units ? *Q.units_n : ((uint64_t)Q.n + kGPpw - 1) / kGPpw;
+  const uint64_t stride = (uint64_t)gridDim.x * kGWaves;
+  for (uint64_t k = (uint64_t)blockIdx.x * kGWaves + wv; k < units; k += stride) {
+    const uint64_t u = Q.units ? Q.units[k] : k;
+    gcm_unit<OPEN, MULTI, OB, false>(Q, u, lane, tT, tcol, tP, tH, tK, recs[wv]);
+  }
+}
+
+// Grouped multi-key batches (Q.perm): each workgroup stages the key of its
+// first packet in LDS whenever it changes (block-uniform loop: the staging
+// barriers) and runs the single-key code on every unit whose packets all use
+// it; the other units (key boundaries, invalid key ids) are listed in
+// Q.units for quic_gcm_kernel<MULTI> afterwards.
+template <bool OPEN, bool OB>
+__global__ __launch_bounds__(kGBlock) void quic_gcm_staged_kernel(const QGParams Q) {
+  __shared__ uint32_t tT[256 * 64];
+  __shared__ __attribute__((aligned(16))) uint32_t tP[32 * 64];
+  __shared__ __attribute__((aligned(16))) uint32_t tH[kGcmPow * 64];
+  __shared__ GRec recs[kGWaves][kGPpw];
+  __shared__ __attribute__((aligned(16))) uint32_t tK[92];  // rk || hrk || iv
+  stage_common<true>(Q, tT, tP, tH, tK);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+  const uint32_t tcol = 4 * (lane & 31);
   const uint64_t units = ((uint64_t)Q.n + kGPpw - 1) / kGPpw;
   const uint64_t stride = (uint64_t)gridDim.x * kGWaves;
-  for (uint64_t u = (uint64_t)blockIdx.x * kGWaves + wv; u < units; u += stride) {
-    const uint64_t p64 = u * kGPpw + lane;
-    const bool owner = lane < kGPpw && p64 < Q.n;
-    const uint32_t p = (uint32_t)p64;
-
-    // ---- 1. owner lanes
-    bool live = owner;
-    uint64_t pn_dec = 0;  // open: decoded packet number (0 if rejected)
-  uint32_t status = 0, len = 0, pno = 0, first = 0, pn_len = 0, hdr = 0, pl = 0, kid = 0;
-    uint64_t src = 0, dst = 0;
-    uint32_t nonce[3] = {0u, 0u, 0u}, rtag[4] = {0u, 0u, 0u, 0u}, y[4] = {0u, 0u, 0u, 0u};
-    uint32_t hd[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, pnw = 0;  // packet bytes 0..31; seal: pn bytes
-    // fused Salamander layer (OB): wire = salt8 || QUIC packet ^ okey
-    uint64_t wire = 0;
-    uint32_t okey[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, osalt[4] = {0u, 0u, 0u, 0u};
-    if (live && MULTI) {
-      kid = Q.key_id[p];
-      if (kid >= Q.n_keys) {
-        status = kQEKey;
-        live = false;
-        kid = 0;
-        if (OPEN && Q.pn_out) Q.pn_out[p] = 0;  // rejected: pn_out 0 (as below)
-      }
+  uint32_t staged = kNoKey;
+  for (uint64_t ub = (uint64_t)blockIdx.x * kGWaves; ub < units; ub += stride) {
+    const uint32_t k0 = Q.key_id[Q.perm[ub * kGPpw]];
+    if (k0 < Q.n_keys && k0 != staged) {  // (block-uniform)
+      __syncthreads();  // every wave is done with the previous key
+      stage_key(Q.keys + k0, tP, tH, tK);
+      __syncthreads();
+      staged = k0;
     }
-    const GKey<MULTI> K = key_of<MULTI>(Q, kid, tP, tH, tK);
-    if (live) {
-      src = (uint64_t)Q.in + Q.in_off[p];
-      dst = (uint64_t)Q.out + Q.out_off[p];
-      len = Q.in_len[p];
-      pno = Q.pn_offset[p];
-      uint64_t pn = Q.pn[p];
-      uint32_t pnb[4] = {0u, 0u, 0u, 0u};
-      if (OB) {
-        if (!OPEN) {  // wire = salt || protected packet ^ key
-          wire = dst;
-          dst = wire + kSalamanderSalt;
-          const uint32_t *sp = reinterpret_cast<const uint32_t *>(Q.osalt + 8ull * p);
-          osalt[0] = sp[0];
-          osalt[1] = sp[1];
-        } else if (len >= (uint32_t)kSalamanderSalt && len <= kQMaxPacket) {
-          wire = src;  // salt = the first 8 wire bytes (salamander.go:50)
-          load16(src, src + kSalamanderSalt, osalt);
-          src += kSalamanderSalt;
-          len -= kSalamanderSalt;
-        } else {
-          len = 0;  // too short for a salt: rejected below
-        }
-        salamander_key(&Q.opsk, osalt, okey);
-      }
-      // packet byte k (de-obfuscated when the fused layer is on)
-      auto hb = [&](uint32_t k) -> uint32_t {
-        const uint32_t b = head_byte(hd, src, k);
-        return (OB && OPEN && k >= 32) ? b ^ byte32(okey, k & 31) : b;
-      };
-      if (!OPEN) {
-        if (len) load_head32(src, len, hd);
-        first = hd[0] & 0xFFu;
-        pn_len = (first & 3) + 1;
-        hdr = pno + pn_len;
-        if (len == 0 || len > kQMaxPacket || hdr > len || pno + 4 > len) {
-          live = false;
-        } else {
-          pl = len - hdr;
-          for (uint32_t i = 0; i < pn_len; i++) pnw |= hb(pno + i) << (8 * i);
-        }
-      } else if (len < 16 || len > kQMaxPacket || pno + 4 + 16 > len) {
-        live = false;
-      } else {
-        uint32_t sample[4], m0, m1;
-        load16(src + pno + 4, src + len, sample);
-        load16(src + len - 16, src + len, rtag);  // before any in-place write
-        load_head32(src, len, hd);
-        if (OB) {  // de-obfuscate what was read: key byte of QUIC offset k is okey[k % 32]
-          uint32_t k4[4];
-          keywin(okey, (pno + 4) & 31, k4);
-#pragma unroll
-          for (int w = 0; w < 4; w++) sample[w] ^= k4[w];
-          keywin(okey, (len - 16) & 31, k4);
-#pragma unroll
-          for (int w = 0; w < 4; w++) rtag[w] ^= k4[w];
-          keywin(okey, 0, k4);
-#pragma unroll
-          for (int w = 0; w < 4; w++) hd[w] ^= k4[w];
-          keywin(okey, 16, k4);
-#pragma unroll
-          for (int w = 0; w < 4; w++) hd[4 + w] ^= k4[w];
-        }
-        gcm_hp_mask<MULTI>(K, tT, tcol, sample, m0, m1);
-        const uint32_t pfirst = hd[0] & 0xFFu;
-        first = pfirst ^ (m0 & ((pfirst & 0x80) ? 0x0Fu : 0x1Fu));
-        pn_len = (first & 3) + 1;
-        hdr = pno + pn_len;
-        if (hdr > len - 16) {
-          live = false;
-        } else {
-          uint64_t trunc = 0;
-          for (uint32_t i = 0; i < pn_len; i++) {
-            pnb[i] = hb(pno + i) ^ mask_byte(m0, m1, 1 + i);
-            trunc = (trunc << 8) | pnb[i];
-          }
-          pn = decode_pn(pn, trunc, 8 * pn_len);
-          pn_dec = pn;
-          pl = len - 16 - hdr;
-        }
-      }
-      if (!live) status = kQEShort;
-    // every owner lane writes its pn_out (0 when the packet was rejected)
-    if (OPEN && owner && Q.pn_out) Q.pn_out[p] = pn_dec;
-      if (live) {
-        const uint32_t iv[3] = {K.iv[0], K.iv[1], K.iv[2]};
-        quic_nonce_iv(iv, pn, nonce);
-        // AAD = the unprotected header; seal copies it unchanged (protection
-        // is applied in phase 3), open writes the unprotected header
-        for (uint32_t q = 0; q < hdr; q += 16) {
-          uint32_t w[4];
-          head_block(hd, src, q, hdr, w);
-          if (OB && OPEN && q >= 32) {
-            uint32_t k4[4];
-            keywin(okey, q & 31, k4);
-#pragma unroll
-            for (int j = 0; j < 4; j++) w[j] ^= k4[j] & range_mask(0, (int)(hdr - q), j);
-          }
-          if (OPEN) {
-            if (q == 0) set_byte(w, 0, first);
-            for (uint32_t i = 0; i < pn_len; i++) {
-              const uint32_t pos = pno + i;
-              if (pos >= q && pos < q + 16) set_byte(w, pos - q, pnb[i]);
-            }
-          }
-          ghash_absorb(y, w);
-          gmul_pos<MULTI>(y, K.hpos);
-          if (OB && !OPEN) {  // the wire carries the (still unprotected) header ^ key
-            uint32_t k4[4];
-            keywin(okey, q & 31, k4);
-#pragma unroll
-            for (int j = 0; j < 4; j++) w[j] ^= k4[j];
-          }
-          if (OPEN || OB || dst != src) store16(dst + q, w, hdr - q < 16 ? hdr - q : 16);
-        }
-      }
+    const uint64_t u = ub + wv;
+    if (u >= units) continue;
+    const uint64_t i64 = u * kGPpw + lane;
+    bool same = true;
+    if (lane < kGPpw && i64 < Q.n) same = Q.key_id[Q.perm[i64]] == staged;
+    if (staged != kNoKey && __ballot(!same) == 0) {
+      gcm_unit<OPEN, false, OB, true>(Q, u, lane, tT, tcol, tP, tH, tK, recs[wv]);
+    } else if (lane == 0) {
+      const uint32_t at = atomicAdd(Q.units_n, 1u);
+      Q.units[at] = (uint32_t)u;
     }
-    const bool coop = live && pl <= kGCoopMax;
-    const uint32_t np = (pl + 15) / 16;
-    // the header's GHASH, placed ahead of the payload blocks
-    if (coop && np) K.mul_pow(y, np);
-    const uint32_t nblk = coop ? (pl + 63) / 64 : 0u;
-    uint32_t incl = nblk;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-      const uint32_t t = __shfl_up(incl, d, kWave);
-      if (lane >= (uint32_t)d) incl += t;
-    }
-    const uint32_t start = incl - nblk, T = __shfl(incl, kWave - 1, kWave);
-    if (lane < kGPpw) {
-      GRec &R = recs[wv][lane];
-      R.src = src + hdr;
-      R.dst = dst + hdr;
-      R.pl = pl;
-      R.start = start;
-      R.np = np;
-      R.kid = kid;
-#pragma unroll
-      for (int i = 0; i < 3; i++) R.nonce[i] = nonce[i];
-#pragma unroll
-      for (int i = 0; i < 4; i++) R.x[i] = coop ? y[i] : 0u;
-#pragma unroll
-      for (int i = 0; i < 8; i++) R.ct32[i] = 0u;
-      if (OB) {
-        uint32_t k4[4];
-        keywin(okey, hdr & 31, k4);
-#pragma unroll
-        for (int i = 0; i < 4; i++) R.okr[i] = k4[i];
-        keywin(okey, (hdr + 16) & 31, k4);
-#pragma unroll
-        for (int i = 0; i < 4; i++) R.okr[4 + i] = k4[i];
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-
-    // ---- 2. cooperative payload pass over the flat chunk space
-    for (uint32_t base = 0; base < T; base += kWave) {
-      const uint32_t f = base + lane;
-      const uint32_t pp = q_locate(start, base, f < T ? f : T - 1);
-      if (f < T) {
-        GRec &R = recs[wv][pp];
-        const GKey<MULTI> KB = key_of<MULTI>(Q, R.kid, tP, tH, tK);
-        const uint32_t b = f - R.start, off0 = 64 * b;
-        const uint32_t nv = R.pl - off0 < 64 ? R.pl - off0 : 64u;
-        const uint32_t rn[3] = {R.nonce[0], R.nonce[1], R.nonce[2]};
-        uint32_t yb[4] = {0u, 0u, 0u, 0u}, f32[8];
-        uint32_t rokr[8];
-#pragma unroll
-        for (int i = 0; i < 8; i++) rokr[i] = OB ? R.okr[i] : 0u;
-        gcm_run<OPEN, MULTI, OB>(KB, tT, tcol, rn, 2 + 4 * b, R.src + off0, R.dst + off0, nv, yb,
-                                 f32, rokr);
-        const uint32_t m = R.np - 4 * b - (nv + 15) / 16;  // payload blocks after this chunk
-        if (m) KB.mul_pow(yb, m);
-#pragma unroll
-        for (int i = 0; i < 4; i++) atomicXor(&R.x[i], yb[i]);
-        if (!OPEN && b == 0) {
-#pragma unroll
-          for (int i = 0; i < 8; i++) R.ct32[i] = f32[i];
-        }
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-
-    // ---- 3. owner lanes: lengths block, tag, header protection
-    if (!owner) continue;
-    if (!live) {
-      Q.out_len[p] = status;
-      continue;
-    }
-    uint32_t ct32[8];
-    if (coop) {
-#pragma unroll
-      for (int i = 0; i < 4; i++) y[i] = recs[wv][lane].x[i];
-#pragma unroll
-      for (int i = 0; i < 8; i++) ct32[i] = recs[wv][lane].ct32[i];
-    } else {
-      uint32_t rokr[8];
-#pragma unroll
-      for (int i = 0; i < 8; i++) rokr[i] = OB ? recs[wv][lane].okr[i] : 0u;
-      gcm_run<OPEN, MULTI, OB>(K, tT, tcol, nonce, 2, src + hdr, dst + hdr, pl, y, ct32, rokr);
-    }
-    // lengths block: be64(8 * hdr) || be64(8 * pl)
-    y[1] ^= 8 * hdr;
-    y[2] ^= pl >> 29;
-    y[3] ^= 8 * pl;
-    gmul_pos<MULTI>(y, K.hpos);
-    uint32_t tag[4] = {nonce[0], nonce[1], nonce[2], __builtin_bswap32(1u)};
-    aes_encrypt<MULTI>(K.rk, tT, tcol, tag);  // E(K, J0)
-#pragma unroll
-    for (int w = 0; w < 4; w++) tag[w] ^= __builtin_bswap32(y[w]);
-    if (OPEN) {
-      const bool ok = ((tag[0] ^ rtag[0]) | (tag[1] ^ rtag[1]) | (tag[2] ^ rtag[2]) |
-                       (tag[3] ^ rtag[3])) == 0;
-      Q.out_len[p] = ok ? len - 16 : kQEAuth;
-      continue;
-    }
-    if (OB) {
-      uint32_t k4[4], t4[4];
-      keywin(okey, len & 31, k4);
-#pragma unroll
-      for (int w = 0; w < 4; w++) t4[w] = tag[w] ^ k4[w];
-      store16(dst + len, t4, 16);
-      store16(wire, osalt, kSalamanderSalt);
-    } else {
-      store16(dst + len, tag, 16);
-    }
-    // header protection: sample = (ciphertext || tag)[4 - pn_len ..][0..16)
-    const uint32_t so = 4 - pn_len;
-    uint32_t sample[4];
-    if (pl >= so + 16) {
-#pragma unroll
-      for (int j = 0; j < 4; j++) sample[j] = __builtin_amdgcn_alignbyte(ct32[j + 1], ct32[j], so);
-    } else {  // short payload: the sample reaches into the tag
-      const uint32_t t8[8] = {tag[0], tag[1], tag[2], tag[3], 0u, 0u, 0u, 0u};
-#pragma unroll
-      for (int j = 0; j < 4; j++) sample[j] = 0u;
-      for (uint32_t i = 0; i < 16; i++) {
-        const uint32_t k = so + i;
-        const uint32_t bb = k < pl ? byte32(ct32, k) : byte32(t8, k - pl);
-        sample[i >> 2] |= bb << (8 * (i & 3));
-      }
-    }
-    uint32_t m0, m1;
-    gcm_hp_mask<MULTI>(K, tT, tcol, sample, m0, m1);
-    const uint32_t kb0 = OB ? okey[0] & 0xFFu : 0u;
-    gst<uint8_t>(dst, (uint8_t)(first ^ kb0 ^ (m0 & ((first & 0x80) ? 0x0Fu : 0x1Fu))));
-    for (uint32_t i = 0; i < pn_len; i++) {
-      const uint32_t bb = (pnw >> (8 * i)) & 0xFFu;
-      const uint32_t kb = OB ? byte32(okey, (pno + i) & 31) : 0u;
-      gst<uint8_t>(dst + pno + i, (uint8_t)(bb ^ kb ^ mask_byte(m0, m1, 1 + i)));
-    }
-    Q.out_len[p] = len + 16 + (OB ? kSalamanderSalt : 0u);
   }
+}
+
+// ---------------------------------------------------------------- key groups
+
+// Multi-key batches are grouped by key when they have at least kGrpMinN
+// packets and at most kGrpMaxKeys keys.  Counting sort in three launches:
+// per-chunk key histograms (bin n_keys: ids out of range), one exclusive
+// scan over them in key-major order, and a stable scatter by one wave per
+// chunk (ranks among equal keys from ballots over the key bits).
+constexpr uint32_t kGrpMinN = 2048;
+constexpr uint32_t kGrpMaxKeys = 1024;
+constexpr uint32_t kGrpChunk = 4096;  // packets per histogram chunk
+constexpr uint32_t kGrpBits = 11;     // bins <= kGrpMaxKeys + 1 <= 2^11
+
+__global__ __launch_bounds__(256) void gcm_group_hist(const uint16_t *kid, uint32_t n,
+                                                      uint32_t bins, uint32_t nch,
+                                                      uint32_t *hist) {
+  __shared__ uint32_t h[kGrpMaxKeys + 1];
+  for (uint32_t i = threadIdx.x; i < bins; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  const uint64_t c0 = (uint64_t)blockIdx.x * kGrpChunk;
+  for (uint32_t i = threadIdx.x; i < kGrpChunk && c0 + i < n; i += blockDim.x) {
+    const uint32_t k = kid[c0 + i];
+    atomicAdd(&h[k < bins - 1 ? k : bins - 1], 1u);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < bins; i += blockDim.x) hist[(uint64_t)i * nch + blockIdx.x] = h[i];
+}
+
+// exclusive prefix sum of total words, in place, one block of 1024 threads
+__global__ __launch_bounds__(1024) void gcm_group_scan(uint32_t *hist, uint32_t total,
+                                                       uint32_t *units_n) {
+  __shared__ uint32_t s[1024];
+  if (threadIdx.x == 0) *units_n = 0;  // the staged kernel's deferred-unit count
+  const uint32_t t = threadIdx.x, seg = (total + 1023) / 1024;
+  const uint64_t a = (uint64_t)t * seg, b = a + seg < total ? a + seg : total;
+  uint32_t sum = 0;
+  for (uint64_t i = a; i < b; i++) sum += hist[i];
+  s[t] = sum;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {
+    const uint32_t v = t >= d ? s[t - d] : 0u;
+    __syncthreads();
+    s[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = s[t] - sum;
+  for (uint64_t i = a; i < b; i++) {
+    const uint32_t v = hist[i];
+    hist[i] = run;
+    run += v;
+  }
+}
+
+__global__ __launch_bounds__(64) void gcm_group_scatter(const uint16_t *kid, uint32_t n,
+                                                        uint32_t bins, uint32_t nch,
+                                                        const uint32_t *hist, uint32_t *perm) {
+  __shared__ uint32_t base[kGrpMaxKeys + 1];
+  __shared__ uint16_t kk[kGrpChunk];
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t i = lane; i < bins; i += kWave) base[i] = hist[(uint64_t)i * nch + blockIdx.x];
+  const uint64_t c0 = (uint64_t)blockIdx.x * kGrpChunk;
+  const uint32_t m = n - c0 < kGrpChunk ? (uint32_t)(n - c0) : kGrpChunk;
+  for (uint32_t i = lane; i < m; i += kWave) {
+    const uint32_t k = kid[c0 + i];
+    kk[i] = (uint16_t)(k < bins - 1 ? k : bins - 1);
+  }
+  __syncthreads();
+  const uint64_t below = (1ull << lane) - 1ull;
+  for (uint32_t j = 0; j < m; j += kWave) {
+    const uint32_t i = j + lane;
+    const bool valid = i < m;
+    const uint32_t k = valid ? kk[i] : 0u;
+    // lanes holding the same key as this one
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (uint32_t bt = 0; bt < kGrpBits; bt++) {
+      const uint64_t on = __ballot(valid && ((k >> bt) & 1u));
+      peers &= ((k >> bt) & 1u) ? on : ~on;
+    }
+    const uint32_t b0 = valid ? base[k] : 0u;
+    if (valid) perm[b0 + __popcll(peers & below)] = (uint32_t)(c0 + i);
+    // the highest lane of each key advances its base (after every read)
+    __builtin_amdgcn_wave_barrier();
+    if (valid && (peers >> lane) == 1ull) base[k] = b0 + (uint32_t)__popcll(peers);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the base writes land first
+  }
+}
+
+static uint32_t grp_chunks(uint32_t n) { return (n + kGrpChunk - 1) / kGrpChunk; }
+
+}  // namespace sq
+
+extern "C" uint64_t sq_gcm_group_scratch(uint32_t n, uint32_t n_keys) {
+  using namespace sq;
+  if (n < kGrpMinN || n_keys == 0 || n_keys > kGrpMaxKeys) return 0;  // not grouped
+  // perm[n] | hist[bins * chunks] | units_n | units[units]
+  return 4ull * n + 4ull * (n_keys + 1) * grp_chunks(n) + 4ull + 4ull * ((n + kGPpw - 1) / kGPpw);
+}
+
+extern "C" int sq_launch_gcm_group(const uint16_t *key_id, uint32_t n, uint32_t n_keys,
+                                   void *scratch, void *stream) {
+  using namespace sq;
+  if (n < kGrpMinN || n_keys == 0 || n_keys > kGrpMaxKeys) return 1;
+  hipStream_t s = (hipStream_t)stream;
+  const uint32_t nch = grp_chunks(n), bins = n_keys + 1;
+  uint32_t *perm = (uint32_t *)scratch;
+  uint32_t *hist = perm + n;
+  uint32_t *units_n = hist + (uint64_t)bins * nch;
+  hipLaunchKernelGGL(gcm_group_hist, dim3(nch), dim3(256), 0, s, key_id, n, bins, nch, hist);
+  hipLaunchKernelGGL(gcm_group_scan, dim3(1), dim3(1024), 0, s, hist, bins * nch, units_n);
+  hipLaunchKernelGGL(gcm_group_scatter, dim3(nch), dim3(kWave), 0, s, key_id, n, bins, nch,
+                     (const uint32_t *)hist, perm);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+namespace sq {
+
+// resident workgroups of a kernel on the device (the persistent grid)
+static uint64_t resident_blocks(const void *fn) {
+  int dev = 0, per_cu = 0, cus = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kGBlock, 0);
+  return (uint64_t)(per_cu < 1 ? 1 : per_cu) * (uint64_t)(cus < 1 ? 1 : cus);
 }
 
 template <bool OPEN, bool MULTI, bool OB>
 static int launch_gcm(const QGParams *qp, hipStream_t s) {
-  // resident blocks on the device, queried once (thread-safe static init)
-  static const uint64_t cap = [] {
-    int dev = 0, per_cu = 0, cus = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, quic_gcm_kernel<OPEN, MULTI, OB>,
-                                                       kGBlock, 0);
-    return (uint64_t)(per_cu < 1 ? 1 : per_cu) * (uint64_t)(cus < 1 ? 1 : cus);
-  }();
+  // queried once (thread-safe static init)
+  static const uint64_t cap = resident_blocks((const void *)quic_gcm_kernel<OPEN, MULTI, OB>);
+  static const uint64_t cap_st =
+      resident_blocks((const void *)quic_gcm_staged_kernel<OPEN, OB>);
   const uint64_t waves = ((uint64_t)qp->n + kGPpw - 1) / kGPpw;
   const uint64_t want = (waves + kGWaves - 1) / kGWaves;
-  const dim3 grid((uint32_t)(want < cap ? want : cap));
-  hipLaunchKernelGGL((quic_gcm_kernel<OPEN, MULTI, OB>), grid, dim3(kGBlock), 0, s, *qp);
+  if (MULTI && qp->perm) {
+    hipLaunchKernelGGL((quic_gcm_staged_kernel<OPEN, OB>), dim3((uint32_t)(want < cap_st ? want : cap_st)),
+                       dim3(kGBlock), 0, s, *qp);
+    if (hipGetLastError() != hipSuccess) return -3;
+  }
+  hipLaunchKernelGGL((quic_gcm_kernel<OPEN, MULTI, OB>), dim3((uint32_t)(want < cap ? want : cap)),
+                     dim3(kGBlock), 0, s, *qp);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -142,3 +142,41 @@ def test_open_rejects_tampering_and_bad_input(ctx):  # noqa: F811
     _, _, ol_, _, _ = run(ctx, keys, True, [b"\x40\x01\x02", b"\x43" + bytes(40)], [1, 1], [1, 2],
                           key_ids=[0, 5], suite=GCM)
     assert ol_[0] == sqobfs.QUIC_ESHORT and ol_[1] == sqobfs.QUIC_EKEY
+
+
+@pytest.mark.parametrize("nkeys,n,inplace", [(300, 6000, False), (16, 4096, True), (2, 2047, False),
+                                             (1100, 3000, False)])
+def test_key_grouped_batches(ctx, nkeys, n, inplace):  # noqa: F811
+    """Multi-key batches of >= 2,048 packets and <= 1,024 keys are grouped by
+    key (sq_launch_gcm_group) and run on staged keys, units across a key
+    boundary or with a bad key id on the per-packet path; 2,047 packets and
+    1,100 keys stay ungrouped.  Random key order, 1 % invalid key ids; seal
+    then open against the oracle."""
+    rng = np.random.Generator(np.random.PCG64(900 + nkeys + n))
+    kb, keys = _keys(rng, nkeys)
+    pkts, pnos, pns = _random_packets(rng, n)
+    kid = rng.integers(0, nkeys, n)
+    bad = rng.random(n) < 0.01
+    kid[bad] = nkeys + rng.integers(0, 5, int(bad.sum()))
+    out, oo, ol_, _, buf = run(ctx, keys, True, pkts, pnos, pns, key_ids=kid, inplace=inplace,
+                               suite=GCM)
+    prot = []
+    for i, p in enumerate(pkts):
+        if bad[i]:
+            assert ol_[i] == sqobfs.QUIC_EKEY, i
+            prot.append(p + bytes(16))
+            continue
+        want, r = ol.quic_seal(*kb[kid[i]], pns[i], p, pnos[i], suite=ol.AES128GCM)
+        assert ol_[i] == r == len(p) + 16, i
+        got = out[int(oo[i]):int(oo[i]) + r].tobytes()
+        assert got == want, i
+        prot.append(got)
+    largest = [max(0, pn - int(rng.integers(1, 100))) for pn in pns]
+    out2, oo2, ol2, pno2, _ = run(ctx, keys, False, prot, pnos, largest, key_ids=kid,
+                                  inplace=inplace, suite=GCM)
+    for i, p in enumerate(pkts):
+        if bad[i]:
+            assert ol2[i] == sqobfs.QUIC_EKEY and pno2[i] == 0, i
+            continue
+        assert ol2[i] == len(p) and pno2[i] == pns[i], i
+        assert out2[int(oo2[i]):int(oo2[i]) + ol2[i]].tobytes() == p, i
