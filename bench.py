@@ -528,7 +528,12 @@ def inproc_bench(args):
                 pending.pop(0).wait()
         for t in pending:
             t.wait()
-    steps(args.warmup)
+    # warm-up as the queued mode's: at least --warmup steps and --warmup-s of
+    # wall time (a fresh process's first ~25 launches run up to 10 % slower)
+    warm, wt0 = 0, time.perf_counter()
+    while warm < args.warmup or time.perf_counter() - wt0 < args.warmup_s:
+        steps(1)
+        warm += 1
     t0 = time.perf_counter()
     steps(args.steps)
     el = time.perf_counter() - t0
@@ -536,7 +541,8 @@ def inproc_bench(args):
                      f"{K} in-process shards (sqobfs_shard_launch, {depth} steps in flight)",
            "value": round(payload * args.steps / el / 2**30, 3), "unit": "GiB/s",
            "n_gpus": len(set(devs)), "contexts": K, "steps": args.steps,
-           "warmup": args.warmup, "ms_per_step": round(el * 1e3 / args.steps, 4),
+           "warmup": args.warmup, "warmup_steps": warm,
+           "ms_per_step": round(el * 1e3 / args.steps, 4),
            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
            "data": "synthetic", "shard_packets": [int(cut[k + 1] - cut[k]) for k in range(K)],
            "config": {"workload": args.config, "inproc": K, "inflight": depth}}

@@ -768,11 +768,12 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
   __shared__ __attribute__((aligned(16))) uint32_t tH[MULTI ? 4 : kGcmPow * 64];
   __shared__ GRec recs[kGWaves][kGPpw];
   __shared__ __attribute__((aligned(16))) uint32_t tK[88];  // single key: rk0 || hrk0
+  const uint64_t units = Q.units ? *Q.units_n : ((uint64_t)Q.n + kGPpw - 1) / kGPpw;
+  if ((uint64_t)blockIdx.x * kGWaves >= units) return;  // (a short list: idle blocks)
   stage_common<MULTI>(Q, tT, tP, tH, tK);
   __syncthreads();
   const uint32_t lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
   const uint32_t tcol = 4 * (lane & 31);  // this lane's T-table column (byte offset)
-  const uint64_t units = Q.units ? *Q.units_n : ((uint64_t)Q.n + kGPpw - 1) / kGPpw;
   const uint64_t stride = (uint64_t)gridDim.x * kGWaves;
   for (uint64_t k = (uint64_t)blockIdx.x * kGWaves + wv; k < units; k += stride) {
     const uint64_t u = Q.units ? Q.units[k] : k;
@@ -780,11 +781,14 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
   }
 }
 
-// Grouped multi-key batches (Q.perm): each workgroup stages the key of its
-// first packet in LDS whenever it changes (block-uniform loop: the staging
-// barriers) and runs the single-key code on every unit whose packets all use
-// it; the other units (key boundaries, invalid key ids) are listed in
-// Q.units for quic_gcm_kernel<MULTI> afterwards.
+// Grouped multi-key batches (Q.perm): the workgroups stride over the units
+// kGWaves at a time and stage the key of the first packet of each step in
+// LDS when it changes (block-uniform: the staging barriers); a wave runs the
+// single-key code on its unit when every packet of it uses that key.  The
+// other units (key boundaries, invalid key ids) are listed in Q.units for
+// quic_gcm_kernel<MULTI> afterwards.  (Each block walking its own contiguous
+// range instead, so that it restages only at a key boundary: 16-key seal /
+// open 3,794 / 3,847 us against 3,637 / 3,746 striding.)
 template <bool OPEN, bool OB>
 __global__ __launch_bounds__(kGBlock) void quic_gcm_staged_kernel(const QGParams Q) {
   __shared__ uint32_t tT[256 * 64];
