@@ -1103,15 +1103,13 @@ static int quic_launch(int open, sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr,
     const uint64_t gbytes = b->key_id ? sq_gcm_group_scratch(b->n, kr->count) : 0;
     if (gbytes && hipMallocAsync(&scratch, gbytes, s) != hipSuccess) scratch = nullptr;
     if (scratch) {
-      const int gs = sq_launch_gcm_group(b->key_id, b->n, kr->count, scratch, s);
+      const int gs = sq_launch_gcm_group(b->key_id, b->n, kr->count, open, b->out_len,
+                                         open ? b->pn_out : nullptr, scratch, &g.gmeta, s);
       if (gs < 0) {
         (void)hipFreeAsync(scratch, s);
         return gs;
       }
       g.perm = (const uint32_t *)scratch;
-      const uint32_t nch = (b->n + 4095) / 4096;  // (sq_quic_gcm.hip kGrpChunk)
-      g.units_n = (uint32_t *)scratch + b->n + (uint64_t)(kr->count + 1) * nch;
-      g.units = g.units_n + 1;
     }
     const int st = sq_launch_quic_gcm(open, &g, s);
     if (scratch) (void)hipFreeAsync(scratch, s);

@@ -148,8 +148,7 @@ struct QGParams {
   const uint16_t *key_id;
   uint64_t *pn_out;
   const uint32_t *perm;  // multi-key: packet indices grouped by key (or null)
-  uint32_t *units;       // grouped: the units the staged kernel left (or null)
-  uint32_t *units_n;     // ... and their count
+  const uint32_t *gmeta; // grouped: per key start | count | first step, steps
   const QuicGcmKeyDev *keys;
   const uint32_t *t0;
   uint32_t n;
@@ -200,13 +199,17 @@ void sq_engine_ctx_closed(sqobfs_ctx *ctx);
 // launchers implemented in sq_quic_gcm.hip
 extern "C" int sq_launch_quic_gcm(int open, const sq::QGParams *qp, void *stream);
 // Multi-key AES-128-GCM batches: the packet permutation that groups them by
-// key (stable counting sort).  sq_gcm_group_scratch: the device scratch it
-// needs (perm[n] | histograms | deferred-unit count | deferred units), 0 when
-// such a batch is not grouped (too few packets or too many keys).  sq_launch_gcm_group returns 1 when not
-// grouped, 0 on success, < 0 on a launch error.
+// key (stable counting sort) and the per-key step table of the staged
+// kernel; packets with an out-of-range key id are rejected there (out_len,
+// pn_out) and take no step.  sq_gcm_group_scratch: the device scratch it
+// needs (perm[n] | histograms | meta), 0 when such a batch is not grouped
+// (too few packets per key, or too many keys).  sq_launch_gcm_group returns
+// 1 when not grouped, 0 on success, < 0 on a launch error; *meta = the
+// step table inside scratch.
 extern "C" uint64_t sq_gcm_group_scratch(uint32_t n, uint32_t n_keys);
 extern "C" int sq_launch_gcm_group(const uint16_t *key_id, uint32_t n, uint32_t n_keys,
-                                   void *scratch, void *stream);
+                                   int open, uint32_t *out_len, uint64_t *pn_out,
+                                   void *scratch, const uint32_t **meta, void *stream);
 
 // launchers implemented in sq_quic.hip
 extern "C" int sq_launch_quic(int open, const sq::QParams *qp, void *stream);

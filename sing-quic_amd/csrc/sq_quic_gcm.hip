@@ -44,11 +44,12 @@
 // Single-key launches keep the round keys in the kernarg segment (scalar
 // operands) and the GHASH tables in LDS.  Multi-key launches of a large
 // batch first group the packets by key (a stable counting sort,
-// gcm_group_*: a permutation of the packet indices); each workgroup then
-// stages the key of its current units (round keys and GHASH tables, 40 KiB)
-// in LDS, and a wave whose packets all use that key runs the single-key code
-// on it.  Waves across a key boundary, and small or ungrouped batches, read
-// the packet's keyring entry from global memory.
+// gcm_group_*: a permutation of the packet indices and a table of steps of
+// up to 12 units of one key); each workgroup then stages the key of its
+// current step (IV and GHASH tables, 40 KiB) in LDS and runs the single-key
+// code on it, its round keys read as scalars from the keyring entry.  Batches that are not grouped (few packets per key,
+// more than 1,023 keys) read each packet's keyring entry from global
+// memory.
 #include <hip/hip_runtime.h>
 
 #include "sq_bytes.h"
@@ -88,9 +89,15 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, int n) {
   return __builtin_amdgcn_alignbit(x, x, 32 - n);
 }
 
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t x) {
+  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
+         __builtin_amdgcn_readfirstlane((uint32_t)x);
+}
+
 // Where a launch's keys live (KM): 0 one key (round keys in the kernarg
 // segment, GHASH tables in LDS), 1 per-packet keyring entries in global
-// memory, 2 the workgroup's staged key (round keys and tables in LDS).
+// memory, 2 the workgroup's staged key (GHASH tables and IV in LDS, round
+// keys read wave-uniform from its keyring entry).
 // round key r (4 column words); KM 2 reads them wave-uniform into SGPRs, as
 // the kernarg ones are
 template <int KM>
@@ -99,8 +106,12 @@ __device__ __forceinline__ void round_key(const uint32_t *rk, int r, uint32_t (&
     const u32x4 v = gld<u32x4>((uint64_t)(rk + 4 * r));
     k[0] = v.x; k[1] = v.y; k[2] = v.z; k[3] = v.w;
   } else if (KM == 2) {
-#pragma unroll
-    for (int c = 0; c < 4; c++) k[c] = __builtin_amdgcn_readfirstlane(rk[4 * r + c]);
+    // the staged key's entry in global memory, through the constant address
+    // space at a wave-uniform address: scalar loads into SGPRs (read from
+    // LDS they held VGPRs and made these kernels spill)
+    typedef const __attribute__((address_space(4))) uint32_t *cptr;
+    const cptr c = (cptr)(uintptr_t)uniform_u64((uint64_t)(uintptr_t)(rk + 4 * r));
+    k[0] = c[0]; k[1] = c[1]; k[2] = c[2]; k[3] = c[3];
   } else {
     k[0] = rk[4 * r]; k[1] = rk[4 * r + 1]; k[2] = rk[4 * r + 2]; k[3] = rk[4 * r + 3];
   }
@@ -420,8 +431,8 @@ __device__ __forceinline__ GKey<MULTI ? 1 : (STAGED ? 2 : 0)> key_of(
     const QuicGcmKeyDev *E = Q.keys + kid;
     K.rk = E->rk; K.hrk = E->hrk; K.iv = E->iv;
     K.hpos = &E->hpos[0][0][0]; K.htab = &E->htab[0][0][0];
-  } else if (STAGED) {
-    K.rk = tK; K.hrk = tK + 44; K.iv = tK + 88;
+  } else if (STAGED) {  // kid: the staged key
+    K.rk = Q.keys[kid].rk; K.hrk = Q.keys[kid].hrk; K.iv = tK + 88;
     K.hpos = tP; K.htab = tH;
   } else {
 #if SQ_GRK_LDS
@@ -436,14 +447,11 @@ __device__ __forceinline__ GKey<MULTI ? 1 : (STAGED ? 2 : 0)> key_of(
 
 constexpr uint32_t kNoKey = 0xFFFFFFFFu;
 
-// Copy keyring entry E's round keys, IV and GHASH tables into the block's
-// LDS (every thread of the block takes part).
+// Copy keyring entry E's IV and GHASH tables into the block's LDS (every
+// thread of the block takes part).
 __device__ __forceinline__ void stage_key(const QuicGcmKeyDev *E, uint32_t *tP, uint32_t *tH,
                                           uint32_t *tK) {
-  if (threadIdx.x < 91) {
-    const uint32_t i = threadIdx.x;
-    tK[i] = i < 44 ? E->rk[i] : (i < 88 ? E->hrk[i - 44] : E->iv[i - 88]);
-  }
+  if (threadIdx.x < 3) tK[88 + threadIdx.x] = E->iv[threadIdx.x];  // (round keys: scalar loads)
   const uint32_t *src = &E->hpos[0][0][0];  // hpos then htab, contiguous
   for (uint32_t i = threadIdx.x; i < (32 + kGcmPow) * 16; i += kGBlock) {
     const u32x4 v = gld<u32x4>((uint64_t)(src + 4 * i));
@@ -452,23 +460,26 @@ __device__ __forceinline__ void stage_key(const QuicGcmKeyDev *E, uint32_t *tP, 
   }
 }
 
-// One unit (kGPpw packets) of a wave: the three phases.  recs = the wave's
-// records.  STAGED (with MULTI false): every packet of the unit uses the
-// workgroup's staged key.
+// One unit (up to kGPpw packets) of a wave: the three phases.  recs = the
+// wave's records.  STAGED (with MULTI false): every packet of the unit uses
+// the workgroup's staged key.
 template <bool OPEN, bool MULTI, bool OB, bool STAGED>
-__device__ __forceinline__ void gcm_unit(const QGParams &Q, uint64_t u, uint32_t lane,
+__device__ __forceinline__ void gcm_unit(const QGParams &Q, uint64_t base, uint32_t cnt,
+                                         uint32_t skid, uint32_t lane,
                                          const uint32_t *tT, uint32_t tcol, const uint32_t *tP,
                                          const uint32_t *tH, const uint32_t *tK, GRec *recs) {
   constexpr int KM = MULTI ? 1 : (STAGED ? 2 : 0);
-  const uint64_t i64 = u * kGPpw + lane;
-  const bool owner = lane < kGPpw && i64 < Q.n;
-  // grouped batches: the packet at this position of the key order
+  // the unit's packets: positions [base, base + cnt) (grouped batches: of
+  // the key order)
+  const uint64_t i64 = base + lane;
+  const bool owner = lane < kGPpw && lane < cnt;
   const uint32_t p = owner && Q.perm ? Q.perm[i64] : (uint32_t)i64;
 
   // ---- 1. owner lanes
   bool live = owner;
   uint64_t pn_dec = 0;  // open: decoded packet number (0 if rejected)
-uint32_t status = 0, len = 0, pno = 0, first = 0, pn_len = 0, hdr = 0, pl = 0, kid = 0;
+  uint32_t status = 0, len = 0, pno = 0, first = 0, pn_len = 0, hdr = 0, pl = 0,
+           kid = STAGED ? skid : 0u;
   uint64_t src = 0, dst = 0;
   uint32_t nonce[3] = {0u, 0u, 0u}, rtag[4] = {0u, 0u, 0u, 0u}, y[4] = {0u, 0u, 0u, 0u};
   uint32_t hd[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, pnw = 0;  // packet bytes 0..31; seal: pn bytes
@@ -760,7 +771,7 @@ __device__ __forceinline__ void stage_common(const QGParams &Q, uint32_t *tT, ui
 }
 
 // One key (MULTI false) or per-packet keys from the keyring in global memory
-// (MULTI true): every unit of the batch, or (Q.units) the units of that list.
+// (MULTI true, batches that are not grouped).
 template <bool OPEN, bool MULTI, bool OB>
 __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
   __shared__ uint32_t tT[256 * 64];
@@ -768,27 +779,30 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
   __shared__ __attribute__((aligned(16))) uint32_t tH[MULTI ? 4 : kGcmPow * 64];
   __shared__ GRec recs[kGWaves][kGPpw];
   __shared__ __attribute__((aligned(16))) uint32_t tK[88];  // single key: rk0 || hrk0
-  const uint64_t units = Q.units ? *Q.units_n : ((uint64_t)Q.n + kGPpw - 1) / kGPpw;
-  if ((uint64_t)blockIdx.x * kGWaves >= units) return;  // (a short list: idle blocks)
+  const uint64_t units = ((uint64_t)Q.n + kGPpw - 1) / kGPpw;
   stage_common<MULTI>(Q, tT, tP, tH, tK);
   __syncthreads();
   const uint32_t lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
   const uint32_t tcol = 4 * (lane & 31);  // this lane's T-table column (byte offset)
   const uint64_t stride = (uint64_t)gridDim.x * kGWaves;
-  for (uint64_t k = (uint64_t)blockIdx.x * kGWaves + wv; k < units; k += stride) {
-    const uint64_t u = Q.units ? Q.units[k] : k;
-    gcm_unit<OPEN, MULTI, OB, false>(Q, u, lane, tT, tcol, tP, tH, tK, recs[wv]);
+  for (uint64_t u = (uint64_t)blockIdx.x * kGWaves + wv; u < units; u += stride) {
+    const uint64_t base = u * kGPpw;
+    const uint32_t cnt = Q.n - base < kGPpw ? (uint32_t)(Q.n - base) : kGPpw;
+    gcm_unit<OPEN, MULTI, OB, false>(Q, base, cnt, 0u, lane, tT, tcol, tP, tH, tK, recs[wv]);
   }
 }
 
-// Grouped multi-key batches (Q.perm): the workgroups stride over the units
-// kGWaves at a time and stage the key of the first packet of each step in
-// LDS when it changes (block-uniform: the staging barriers); a wave runs the
-// single-key code on its unit when every packet of it uses that key.  The
-// other units (key boundaries, invalid key ids) are listed in Q.units for
-// quic_gcm_kernel<MULTI> afterwards.  (Each block walking its own contiguous
-// range instead, so that it restages only at a key boundary: 16-key seal /
-// open 3,794 / 3,847 us against 3,637 / 3,746 striding.)
+// Grouped multi-key batches (Q.perm, Q.gmeta): the work is a list of steps,
+// each up to kGWaves units of ONE key (a key's units in order, kGWaves per
+// step; its last step partly idle).  The workgroups stride over the steps
+// and stage a step's key in LDS (IV, GHASH tables) when it
+// changes (block-uniform: the staging barriers); every wave then runs the
+// single-key code on its unit.  Invalid key ids were rejected by the
+// grouping and take no step.  (Round-4 measurements, 1M packets, 16 keys,
+// one process: steps that could straddle a key boundary, with the straddling
+// units deferred to a per-packet launch, ran that launch's one unit-time,
+// 350-390 us, serially after the rest; each workgroup walking a contiguous
+// range of units measured slower than striding.)
 template <bool OPEN, bool OB>
 __global__ __launch_bounds__(kGBlock) void quic_gcm_staged_kernel(const QGParams Q) {
   __shared__ uint32_t tT[256 * 64];
@@ -800,40 +814,52 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_staged_kernel(const QGParams
   __syncthreads();
   const uint32_t lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
   const uint32_t tcol = 4 * (lane & 31);
-  const uint64_t units = ((uint64_t)Q.n + kGPpw - 1) / kGPpw;
-  const uint64_t stride = (uint64_t)gridDim.x * kGWaves;
+  // step table (gcm_group_scan): kstart[bins] | kcount[bins] | sfirst[bins],
+  // sfirst[n_keys] = the number of steps
+  const uint32_t bins = Q.n_keys + 1;
+  const uint32_t *kstart = Q.gmeta, *kcount = Q.gmeta + bins, *sfirst = Q.gmeta + 2 * bins;
+  const uint32_t nsteps = __builtin_amdgcn_readfirstlane(sfirst[Q.n_keys]);
   uint32_t staged = kNoKey;
-  for (uint64_t ub = (uint64_t)blockIdx.x * kGWaves; ub < units; ub += stride) {
-    const uint32_t k0 = Q.key_id[Q.perm[ub * kGPpw]];
-    if (k0 < Q.n_keys && k0 != staged) {  // (block-uniform)
+  for (uint32_t st = blockIdx.x; st < nsteps; st += gridDim.x) {
+    // the step's key: the last k with sfirst[k] <= st (keys without packets
+    // share their successor's sfirst)
+    uint32_t lo = 0, hi = Q.n_keys;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) / 2;
+      if (__builtin_amdgcn_readfirstlane(sfirst[mid]) <= st) lo = mid;
+      else hi = mid;
+    }
+    const uint32_t k = lo;
+    if (k != staged) {  // (block-uniform)
       __syncthreads();  // every wave is done with the previous key
-      stage_key(Q.keys + k0, tP, tH, tK);
+      stage_key(Q.keys + k, tP, tH, tK);
       __syncthreads();
-      staged = k0;
+      staged = k;
     }
-    const uint64_t u = ub + wv;
-    if (u >= units) continue;
-    const uint64_t i64 = u * kGPpw + lane;
-    bool same = true;
-    if (lane < kGPpw && i64 < Q.n) same = Q.key_id[Q.perm[i64]] == staged;
-    if (staged != kNoKey && __ballot(!same) == 0) {
-      gcm_unit<OPEN, false, OB, true>(Q, u, lane, tT, tcol, tP, tH, tK, recs[wv]);
-    } else if (lane == 0) {
-      const uint32_t at = atomicAdd(Q.units_n, 1u);
-      Q.units[at] = (uint32_t)u;
-    }
+    const uint32_t j = st - __builtin_amdgcn_readfirstlane(sfirst[k]);
+    const uint32_t cnt_k = __builtin_amdgcn_readfirstlane(kcount[k]);
+    const uint64_t first = ((uint64_t)j * kGWaves + wv) * kGPpw;  // within the key
+    if (first >= cnt_k) continue;
+    const uint32_t cnt = cnt_k - first < kGPpw ? (uint32_t)(cnt_k - first) : kGPpw;
+    gcm_unit<OPEN, false, OB, true>(Q, __builtin_amdgcn_readfirstlane(kstart[k]) + first, cnt, k,
+                                    lane, tT, tcol, tP, tH, tK, recs[wv]);
   }
 }
 
 // ---------------------------------------------------------------- key groups
 
 // Multi-key batches are grouped by key when they have at least kGrpMinN
-// packets and at most kGrpMaxKeys keys.  Counting sort in three launches:
-// per-chunk key histograms (bin n_keys: ids out of range), one exclusive
-// scan over them in key-major order, and a stable scatter by one wave per
-// chunk (ranks among equal keys from ballots over the key bits).
+// packets, at most kGrpMaxKeys keys and at least kGrpPerKey packets per key
+// on average (a key's last step is partly idle: ~6 of 12 units, so sparser
+// keys waste more than the staging saves).  Counting sort in three
+// launches: per-chunk key histograms (bin n_keys: ids out of range), one
+// exclusive scan over them in key-major order that also builds the step
+// table, and a stable scatter by one wave per chunk (ranks among equal keys
+// from ballots over the key bits) that rejects the out-of-range ids.
 constexpr uint32_t kGrpMinN = 2048;
-constexpr uint32_t kGrpMaxKeys = 1024;
+constexpr uint32_t kGrpMaxKeys = 1023;  // bins = keys + 1 <= 1024 (one scan block)
+constexpr uint32_t kGrpPerKey = 1024;
+constexpr uint32_t kStepPackets = kGWaves * kGPpw;  // a step: 12 units of 32
 constexpr uint32_t kGrpChunk = 4096;  // packets per histogram chunk
 constexpr uint32_t kGrpBits = 11;     // bins <= kGrpMaxKeys + 1 <= 2^11
 
@@ -852,11 +878,13 @@ __global__ __launch_bounds__(256) void gcm_group_hist(const uint16_t *kid, uint3
   for (uint32_t i = threadIdx.x; i < bins; i += blockDim.x) hist[(uint64_t)i * nch + blockIdx.x] = h[i];
 }
 
-// exclusive prefix sum of total words, in place, one block of 1024 threads
+// exclusive prefix sum of the histograms (total words, in place), then the
+// step table meta = kstart[bins] | kcount[bins] | sfirst[bins]; one block of
+// 1024 threads
 __global__ __launch_bounds__(1024) void gcm_group_scan(uint32_t *hist, uint32_t total,
-                                                       uint32_t *units_n) {
+                                                       uint32_t n, uint32_t bins, uint32_t nch,
+                                                       uint32_t *meta) {
   __shared__ uint32_t s[1024];
-  if (threadIdx.x == 0) *units_n = 0;  // the staged kernel's deferred-unit count
   const uint32_t t = threadIdx.x, seg = (total + 1023) / 1024;
   const uint64_t a = (uint64_t)t * seg, b = a + seg < total ? a + seg : total;
   uint32_t sum = 0;
@@ -875,11 +903,35 @@ __global__ __launch_bounds__(1024) void gcm_group_scan(uint32_t *hist, uint32_t 
     hist[i] = run;
     run += v;
   }
+  __syncthreads();  // (the block's global writes, visible to the block)
+  // per key: start, count, steps; the steps' exclusive prefix (bin bins-1,
+  // the invalid ids, takes none: its sfirst is the total)
+  uint32_t kst = 0, kc = 0, steps = 0;
+  if (t < bins) {
+    kst = hist[(uint64_t)t * nch];
+    kc = (t + 1 < bins ? hist[(uint64_t)(t + 1) * nch] : n) - kst;
+    steps = t + 1 < bins ? (kc + kStepPackets - 1) / kStepPackets : 0u;
+  }
+  __syncthreads();
+  s[t] = steps;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {
+    const uint32_t v = t >= d ? s[t - d] : 0u;
+    __syncthreads();
+    s[t] += v;
+    __syncthreads();
+  }
+  if (t < bins) {
+    meta[t] = kst;
+    meta[bins + t] = kc;
+    meta[2 * bins + t] = s[t] - steps;
+  }
 }
 
 __global__ __launch_bounds__(64) void gcm_group_scatter(const uint16_t *kid, uint32_t n,
                                                         uint32_t bins, uint32_t nch,
-                                                        const uint32_t *hist, uint32_t *perm) {
+                                                        const uint32_t *hist, uint32_t *perm,
+                                                        uint32_t *out_len, uint64_t *pn_out) {
   __shared__ uint32_t base[kGrpMaxKeys + 1];
   __shared__ uint16_t kk[kGrpChunk];
   const uint32_t lane = threadIdx.x;
@@ -889,6 +941,10 @@ __global__ __launch_bounds__(64) void gcm_group_scatter(const uint16_t *kid, uin
   for (uint32_t i = lane; i < m; i += kWave) {
     const uint32_t k = kid[c0 + i];
     kk[i] = (uint16_t)(k < bins - 1 ? k : bins - 1);
+    if (k >= bins - 1) {  // an id past the keyring: rejected, as the kernels do
+      out_len[c0 + i] = kQEKey;
+      if (pn_out) pn_out[c0 + i] = 0;
+    }
   }
   __syncthreads();
   const uint64_t below = (1ull << lane) - 1ull;
@@ -918,24 +974,27 @@ static uint32_t grp_chunks(uint32_t n) { return (n + kGrpChunk - 1) / kGrpChunk;
 
 extern "C" uint64_t sq_gcm_group_scratch(uint32_t n, uint32_t n_keys) {
   using namespace sq;
-  if (n < kGrpMinN || n_keys == 0 || n_keys > kGrpMaxKeys) return 0;  // not grouped
-  // perm[n] | hist[bins * chunks] | units_n | units[units]
-  return 4ull * n + 4ull * (n_keys + 1) * grp_chunks(n) + 4ull + 4ull * ((n + kGPpw - 1) / kGPpw);
+  if (n < kGrpMinN || n_keys == 0 || n_keys > kGrpMaxKeys || n / n_keys < kGrpPerKey)
+    return 0;  // not grouped
+  // perm[n] | hist[bins * chunks] | meta[3 * bins]
+  return 4ull * n + 4ull * (n_keys + 1) * grp_chunks(n) + 12ull * (n_keys + 1);
 }
 
 extern "C" int sq_launch_gcm_group(const uint16_t *key_id, uint32_t n, uint32_t n_keys,
-                                   void *scratch, void *stream) {
+                                   int open, uint32_t *out_len, uint64_t *pn_out,
+                                   void *scratch, const uint32_t **meta, void *stream) {
   using namespace sq;
-  if (n < kGrpMinN || n_keys == 0 || n_keys > kGrpMaxKeys) return 1;
+  if (sq_gcm_group_scratch(n, n_keys) == 0) return 1;
   hipStream_t s = (hipStream_t)stream;
   const uint32_t nch = grp_chunks(n), bins = n_keys + 1;
   uint32_t *perm = (uint32_t *)scratch;
   uint32_t *hist = perm + n;
-  uint32_t *units_n = hist + (uint64_t)bins * nch;
+  uint32_t *mt = hist + (uint64_t)bins * nch;
+  *meta = mt;
   hipLaunchKernelGGL(gcm_group_hist, dim3(nch), dim3(256), 0, s, key_id, n, bins, nch, hist);
-  hipLaunchKernelGGL(gcm_group_scan, dim3(1), dim3(1024), 0, s, hist, bins * nch, units_n);
+  hipLaunchKernelGGL(gcm_group_scan, dim3(1), dim3(1024), 0, s, hist, bins * nch, n, bins, nch, mt);
   hipLaunchKernelGGL(gcm_group_scatter, dim3(nch), dim3(kWave), 0, s, key_id, n, bins, nch,
-                     (const uint32_t *)hist, perm);
+                     (const uint32_t *)hist, perm, out_len, open ? pn_out : nullptr);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -958,10 +1017,10 @@ static int launch_gcm(const QGParams *qp, hipStream_t s) {
       resident_blocks((const void *)quic_gcm_staged_kernel<OPEN, OB>);
   const uint64_t waves = ((uint64_t)qp->n + kGPpw - 1) / kGPpw;
   const uint64_t want = (waves + kGWaves - 1) / kGWaves;
-  if (MULTI && qp->perm) {
+  if (MULTI && qp->perm) {  // grouped: every valid packet is in a step
     hipLaunchKernelGGL((quic_gcm_staged_kernel<OPEN, OB>), dim3((uint32_t)(want < cap_st ? want : cap_st)),
                        dim3(kGBlock), 0, s, *qp);
-    if (hipGetLastError() != hipSuccess) return -3;
+    return hipGetLastError() == hipSuccess ? 0 : -3;
   }
   hipLaunchKernelGGL((quic_gcm_kernel<OPEN, MULTI, OB>), dim3((uint32_t)(want < cap ? want : cap)),
                      dim3(kGBlock), 0, s, *qp);

@@ -367,6 +367,13 @@ int main(void) {
     pconn_lat(NULL, hk, "_no_device", NULL);
     sqobfs_keyring_destroy(hk);
   }
+  /* the GPU context's engine with every batch on the CPU path, and the
+   * defaults again (after the no-device run: order effects) */
+  sqobfs_pconn_opts cpu_only;
+  memset(&cpu_only, 0, sizeof cpu_only);
+  cpu_only.cpu_max = 1u << 30;
+  pconn_lat(ctx, kr, "_cpu_only", &cpu_only);
+  pconn_lat(ctx, kr, "_defaults_again", NULL);
 
   /* ---- pconn throughput: pconn A -> pconn B over loopback, one writer
    * thread (the Go Conn's WriteTo callers), one reader thread; without and

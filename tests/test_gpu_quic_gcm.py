@@ -144,14 +144,16 @@ def test_open_rejects_tampering_and_bad_input(ctx):  # noqa: F811
     assert ol_[0] == sqobfs.QUIC_ESHORT and ol_[1] == sqobfs.QUIC_EKEY
 
 
-@pytest.mark.parametrize("nkeys,n,inplace", [(300, 6000, False), (16, 4096, True), (2, 2047, False),
+@pytest.mark.parametrize("nkeys,n,inplace", [(16, 20000, False), (4, 8192, True), (1, 4096, False),
+                                             (300, 6000, False), (2, 2047, False),
                                              (1100, 3000, False)])
 def test_key_grouped_batches(ctx, nkeys, n, inplace):  # noqa: F811
-    """Multi-key batches of >= 2,048 packets and <= 1,024 keys are grouped by
-    key (sq_launch_gcm_group) and run on staged keys, units across a key
-    boundary or with a bad key id on the per-packet path; 2,047 packets and
-    1,100 keys stay ungrouped.  Random key order, 1 % invalid key ids; seal
-    then open against the oracle."""
+    """Multi-key batches of >= 2,048 packets, <= 1,023 keys and >= 1,024
+    packets per key are grouped by key (sq_launch_gcm_group: steps of one
+    key each, run on staged keys; invalid ids rejected by the grouping); 300
+    keys over 6,000 packets, 2,047 packets and 1,100 keys stay on the
+    per-packet kernel.  Random key order, 1 % invalid key ids; seal then open
+    against the oracle."""
     rng = np.random.Generator(np.random.PCG64(900 + nkeys + n))
     kb, keys = _keys(rng, nkeys)
     pkts, pnos, pns = _random_packets(rng, n)

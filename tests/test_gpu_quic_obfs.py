@@ -110,7 +110,7 @@ def test_seal_open_ragged_vs_oracle(ctx, nkeys, inplace, suite):  # noqa: F811
     rng = np.random.Generator(np.random.PCG64(500 + nkeys + inplace + 10 * suite))
     kb, keys = _keys(rng, nkeys, suite)
     # (multi-key AES-GCM batches of >= 2,048 packets are grouped by key)
-    pkts, pnos, pns = _random_packets(rng, 2600 if nkeys > 1 else 2000)
+    pkts, pnos, pns = _random_packets(rng, 3200 if nkeys > 1 else 2000)
     salts = [rng.integers(0, 256, 8, dtype=np.uint8).tobytes() for _ in pkts]
     kid = rng.integers(0, nkeys, len(pkts)) if nkeys > 1 else np.zeros(len(pkts), np.int64)
     kid_arg = kid if nkeys > 1 else None
