@@ -89,9 +89,13 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, int n) {
   return __builtin_amdgcn_alignbit(x, x, 32 - n);
 }
 
+// readfirstlane of 32-bit values (the builtin returns int: without the
+// cast a word >= 2^31 sign-extends when widened)
+__device__ __forceinline__ uint32_t rfl32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+}
 __device__ __forceinline__ uint64_t uniform_u64(uint64_t x) {
-  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
-         __builtin_amdgcn_readfirstlane((uint32_t)x);
+  return ((uint64_t)rfl32((uint32_t)(x >> 32)) << 32) | (uint64_t)rfl32((uint32_t)x);
 }
 
 // Where a launch's keys live (KM): 0 one key (round keys in the kernarg
@@ -818,7 +822,7 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_staged_kernel(const QGParams
   // sfirst[n_keys] = the number of steps
   const uint32_t bins = Q.n_keys + 1;
   const uint32_t *kstart = Q.gmeta, *kcount = Q.gmeta + bins, *sfirst = Q.gmeta + 2 * bins;
-  const uint32_t nsteps = __builtin_amdgcn_readfirstlane(sfirst[Q.n_keys]);
+  const uint32_t nsteps = rfl32(sfirst[Q.n_keys]);
   uint32_t staged = kNoKey;
   for (uint32_t st = blockIdx.x; st < nsteps; st += gridDim.x) {
     // the step's key: the last k with sfirst[k] <= st (keys without packets
@@ -826,7 +830,7 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_staged_kernel(const QGParams
     uint32_t lo = 0, hi = Q.n_keys;
     while (hi - lo > 1) {
       const uint32_t mid = (lo + hi) / 2;
-      if (__builtin_amdgcn_readfirstlane(sfirst[mid]) <= st) lo = mid;
+      if (rfl32(sfirst[mid]) <= st) lo = mid;
       else hi = mid;
     }
     const uint32_t k = lo;
@@ -836,12 +840,12 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_staged_kernel(const QGParams
       __syncthreads();
       staged = k;
     }
-    const uint32_t j = st - __builtin_amdgcn_readfirstlane(sfirst[k]);
-    const uint32_t cnt_k = __builtin_amdgcn_readfirstlane(kcount[k]);
+    const uint32_t j = st - rfl32(sfirst[k]);
+    const uint32_t cnt_k = rfl32(kcount[k]);
     const uint64_t first = ((uint64_t)j * kGWaves + wv) * kGPpw;  // within the key
     if (first >= cnt_k) continue;
     const uint32_t cnt = cnt_k - first < kGPpw ? (uint32_t)(cnt_k - first) : kGPpw;
-    gcm_unit<OPEN, false, OB, true>(Q, __builtin_amdgcn_readfirstlane(kstart[k]) + first, cnt, k,
+    gcm_unit<OPEN, false, OB, true>(Q, (uint64_t)rfl32(kstart[k]) + first, cnt, k,
                                     lane, tT, tcol, tP, tH, tK, recs[wv]);
   }
 }
