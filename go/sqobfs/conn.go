@@ -30,7 +30,8 @@ type Options struct {
 	Pump      bool          // move datagrams through the wrapped conn even when it is a *net.UDPConn
 	NoOffload bool          // socket mode: no UDP GSO on send / GRO on receive
 	// CPUMax: batches costing at most this (payload bytes + 1 KiB per
-	// datagram) run on the CPU path, not a launch (0: 64 KiB; < 0: always launch)
+	// datagram) run on the CPU path, not a launch (0: the engine's measured
+	// break-even, launch round trip x CPU-path rate; < 0: always launch)
 	CPUMax int
 	// InlineGap: a WriteTo made while the engine is idle, at least this long
 	// after the previous one, is obfuscated and sent on the calling goroutine

@@ -600,9 +600,12 @@ typedef struct sqobfs_pconn_opts {
                           the batch) */
   uint32_t cpu_max;    /* batches whose cost (payload bytes + 1024 per
                           datagram, a key derivation's worth) is at most this
-                          run on the CPU path instead of a launch (0 = 65536;
-                          SQOBFS_PCONN_NEVER = always launch while the GPU
-                          works) */
+                          run on the CPU path instead of a launch (0 = the
+                          engine's measured break-even: its recent launch
+                          round trip x its recent CPU-path rate, within
+                          16 KiB .. 4 MiB, ~80 KiB before any measurement,
+                          sqobfs_engine_info.route_bytes; SQOBFS_PCONN_NEVER =
+                          always launch while the GPU works) */
   uint32_t inline_gap_us; /* socket mode: a write made when the transmit side
                           is idle and the previous write is at least this old
                           is obfuscated on the CPU and sent on the writer's own
@@ -705,6 +708,10 @@ typedef struct sqobfs_engine_info {
   uint64_t pool_bytes;
   uint32_t blocks_in_use;
   uint32_t gpu_disabled; /* 1 after a failed launch: every batch runs on the CPU */
+  uint64_t route_bytes;  /* pconns with cpu_max 0: batches costing more go to
+                            the GPU (0 without a context) */
+  uint32_t launch_us;    /* recent launch round trip (EWMA) */
+  uint32_t cpu_ns_per_kib; /* recent CPU-path time per KiB of cost (EWMA) */
 } sqobfs_engine_info;
 /* ctx NULL: the host engine.  SQ_OK with zeros when it was never started. */
 int sqobfs_engine_info_get(sqobfs_ctx *ctx, sqobfs_engine_info *out);

@@ -27,7 +27,10 @@
 //
 // Where the bytes are transformed, per batch:
 //   * on the GPU, one launch, when the batch's cost (payload bytes + 1 KiB
-//     per datagram) exceeds opts.cpu_max;
+//     per datagram) exceeds opts.cpu_max -- by default a measured
+//     break-even: the engine's recent launch round trip times its recent
+//     CPU-path rate (route_bytes), so a batch goes to the GPU when the CPU
+//     would take longer than a launch;
 //   * on the CPU (sq_cpu.h) otherwise, and always without a context (no GPU:
 //     the drop-in constructors never fail), and for good after a launch
 //     fails (a batch whose launch was refused is redone on the CPU; one whose
@@ -71,7 +74,11 @@
 namespace {
 
 constexpr uint32_t kDefBatch = 256, kDefSlot = 2048, kDefBatches = 3, kDefSpinUs = 200;
-constexpr uint32_t kDefCpuMax = 65536;    // cost: payload bytes + kHashCost per datagram
+// routing (opts.cpu_max 0): the CPU path's cost estimate before it is
+// measured, and the bounds of the measured break-even
+constexpr uint32_t kDefCpuNsPerKiB = 500;
+constexpr uint64_t kRouteMin = 16u << 10, kRouteMax = 4u << 20;
+constexpr uint64_t kRouteSample = 8u << 10;  // CPU batches at least this costly update the rate
 constexpr uint32_t kHashCost = 1024;      // one key derivation ~ 1 KiB of XOR on a core
 constexpr uint32_t kDefInlineGapUs = 100;
 constexpr uint32_t kDefWorkers = 4, kMaxWorkers = 64;
@@ -213,6 +220,7 @@ struct Engine {
   int epfd = -1, wake = -1;
   std::atomic<bool> gpu_off{false};
   std::atomic<uint32_t> launch_us{40};  // recent launch completion time (EWMA)
+  std::atomic<uint32_t> cpu_ns_kib{kDefCpuNsPerKiB};  // recent CPU-path ns per KiB of cost (EWMA)
 
   std::mutex pool_mu;
   std::map<std::pair<uint32_t, uint32_t>, std::vector<Block *>> free_blocks;
@@ -434,6 +442,14 @@ void task_end(sqobfs_pconn *pc, int d, bool more, int64_t due = 0) {
 // The batch's bytes, GPU or CPU (module comment).  Returns SQ_OK, or an
 // error when the batch is lost (a launch that failed after it started);
 // *cpu / *failed report what happened, for the pconn's stats.
+// The measured break-even cost: the CPU path would take a launch's round
+// trip on a batch of this cost.
+uint64_t route_bytes(const Engine *E) {
+  const uint64_t l = E->launch_us.load(std::memory_order_relaxed);
+  const uint64_t c = std::max<uint32_t>(1u, E->cpu_ns_kib.load(std::memory_order_relaxed));
+  return std::min(kRouteMax, std::max(kRouteMin, l * 1000u * 1024u / c));
+}
+
 int transform(Engine *E, uint32_t w, sqobfs_pconn *pc, int dir, PBatch &b, bool slotted,
               bool *cpu, bool *failed) {
   *cpu = false;
@@ -452,7 +468,8 @@ int transform(Engine *E, uint32_t w, sqobfs_pconn *pc, int dir, PBatch &b, bool 
   for (uint32_t i = 0; i < b.n; i++) cost += k.len[i] + kHashCost;
   const uint32_t cmax = pc->o.cpu_max;
   const bool want_gpu = E->ctx && !E->gpu_off.load(std::memory_order_relaxed) &&
-                        (cmax == SQOBFS_PCONN_NEVER || cost > cmax);
+                        (cmax == SQOBFS_PCONN_NEVER ||
+                         cost > (cmax == 0 ? route_bytes(E) : (uint64_t)cmax));
   if (want_gpu) {
     // slots are multiples of 16 bytes: every output owns its blocks, so the
     // kernel writes them whole (SQOBFS_FLAG_OUT_BLOCKS); GRO buffers pack the
@@ -513,7 +530,15 @@ int transform(Engine *E, uint32_t w, sqobfs_pconn *pc, int dir, PBatch &b, bool 
     sq_salt_take(E->ctx, key, &seq);
     sq::cpu::salt_stream(key, seq, salts, bytes);
   }
-  return sq::cpu::run_batch(pc->kind, dir, tab, count, &d, salts);
+  const int64_t t0 = mono_ns();
+  const int st = sq::cpu::run_batch(pc->kind, dir, tab, count, &d, salts);
+  if (cost >= kRouteSample) {  // (smaller batches: timer noise)
+    const uint64_t ns = (uint64_t)std::max<int64_t>(0, mono_ns() - t0);
+    const uint32_t now = (uint32_t)std::min<uint64_t>(1u << 20, ns * 1024u / cost);
+    const uint32_t ew = E->cpu_ns_kib.load(std::memory_order_relaxed);
+    E->cpu_ns_kib.store((7 * ew + now) / 8, std::memory_order_relaxed);
+  }
+  return st;
 }
 
 // ---------------------------------------------------------------- sending
@@ -926,6 +951,9 @@ int sqobfs_engine_info_get(sqobfs_ctx *ctx, sqobfs_engine_info *out) {
   out->pool_bytes = E->pool_bytes;
   out->blocks_in_use = E->in_use;
   out->gpu_disabled = E->gpu_off.load() ? 1u : 0u;
+  out->route_bytes = E->ctx ? route_bytes(E) : 0u;
+  out->launch_us = E->launch_us.load();
+  out->cpu_ns_per_kib = E->cpu_ns_kib.load();
   return SQ_OK;
 }
 
@@ -979,7 +1007,7 @@ int sqobfs_pconn_open(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int fd,
   if (o.tx_batches == 0) o.tx_batches = kDefBatches;
   if (o.rx_batches == 0) o.rx_batches = kDefBatches;
   if (o.spin_us == 0) o.spin_us = kDefSpinUs;
-  if (o.cpu_max == 0) o.cpu_max = kDefCpuMax;
+  // (cpu_max 0 stays 0: the measured break-even, route_bytes)
   if (o.inline_gap_us == 0) o.inline_gap_us = kDefInlineGapUs;
   const int kind = sqobfs_keyring_kind(kr);
   const uint32_t S = kind == SQOBFS_SALAMANDER ? SQOBFS_SALAMANDER_SALT_LEN : SQOBFS_XPLUS_SALT_LEN;

@@ -779,6 +779,7 @@ static void t_routing(void) {
   sqobfs_pconn_opts o;
   memset(&o, 0, sizeof o);
   o.inline_gap_us = SQOBFS_PCONN_NEVER;
+  o.cpu_max = 65536; /* a fixed threshold here; the measured default below */
   CHECK(sqobfs_pconn_open(g_ctx, kr, fa, &o, &pc));
   const sqobfs_addr to = loop_addr(pp);
   static uint8_t pay[2000][1400];
@@ -825,6 +826,16 @@ static void t_routing(void) {
   printf("  routing: 5 lone datagrams -> 5 CPU batches; a 2000-datagram burst -> %llu batches "
          "(%llu on the GPU, max %u)\n", (unsigned long long)(b.tx_batches - a.tx_batches),
          (unsigned long long)gpu, b.tx_max_batch);
+  /* the measured break-even (cpu_max 0): within its bounds, from the
+   * engine's launch round trip and CPU-path rate */
+  sqobfs_engine_info ei;
+  CHECK(sqobfs_engine_info_get(g_ctx, &ei));
+  EXPECT(ei.route_bytes >= (16u << 10) && ei.route_bytes <= (4u << 20) && ei.launch_us > 0 &&
+             ei.cpu_ns_per_kib > 0,
+         "route %llu B (launch %u us, cpu %u ns/KiB)", (unsigned long long)ei.route_bytes,
+         ei.launch_us, ei.cpu_ns_per_kib);
+  printf("  measured break-even: %llu B (launch %u us, CPU path %u ns per KiB of cost)\n",
+         (unsigned long long)ei.route_bytes, ei.launch_us, ei.cpu_ns_per_kib);
   sqobfs_pconn_close(pc);
   close(fa);
   close(fp);
