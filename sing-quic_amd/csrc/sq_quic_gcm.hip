@@ -813,7 +813,7 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_staged_kernel(const QGParams
   __shared__ __attribute__((aligned(16))) uint32_t tP[32 * 64];
   __shared__ __attribute__((aligned(16))) uint32_t tH[kGcmPow * 64];
   __shared__ GRec recs[kGWaves][kGPpw];
-  __shared__ __attribute__((aligned(16))) uint32_t tK[92];  // rk || hrk || iv
+  __shared__ __attribute__((aligned(16))) uint32_t tK[92];  // [88..90]: the staged key's IV
   stage_common<true>(Q, tT, tP, tH, tK);
   __syncthreads();
   const uint32_t lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
