@@ -106,6 +106,17 @@ namespace sq {
 #ifndef SQ_TIMELINE
 #define SQ_TIMELINE 0
 #endif
+// 1: the plan's and the windows' wave-wide 64-bit min / max by DPP row
+// moves and four readlanes (no LDS round trips) instead of a shuffle
+// butterfly
+#ifndef SQ_DPPRED
+#define SQ_DPPRED 0
+#endif
+// 1: device salts (SQOBFS_FLAG_DEVICE_SALT) are computed while the
+// descriptor loads are in flight (fetch_desc) instead of after they land
+#ifndef SQ_EARLYSALT
+#define SQ_EARLYSALT 0
+#endif
 
 // XCD-contiguous units.  Workgroups are dispatched round-robin over the 8
 // XCDs, so block b runs on XCD b % 8 and, unmapped, the XCDs share one
@@ -132,7 +143,8 @@ extern "C" const char *sqobfs_build_info(void) {
          " minw=" SQ_STR(SQ_MINW) " wpb=2"
          " ablate=" SQ_STR(SQ_ABLATE) " donate=" SQ_STR(SQ_DONATE) " align=" SQ_STR(SQ_ALIGN)
          " map=" SQ_STR(SQ_MAPBLK)
-         " windows=buffer xcd=" SQ_STR(SQ_XCD);
+         " windows=buffer earlysalt=" SQ_STR(SQ_EARLYSALT) " dppred=" SQ_STR(SQ_DPPRED)
+         " xcd=" SQ_STR(SQ_XCD);
 }
 
 // default unit size (KParams.ppw == 0); any 1 .. kMaxUnitPackets works
@@ -222,6 +234,31 @@ __device__ __forceinline__ uint64_t wave_max64(uint64_t x) {
   }
   return x;
 }
+// Wave-uniform 64-bit min / max (SQ_DPPRED): within each row of 16 lanes by
+// DPP moves (quad swaps, half-row mirror, row mirror: every lane then holds
+// its row's result), then the four rows' results by readlane.  Every lane
+// must be active.
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp64(uint64_t x) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, CTRL, 0xF, 0xF, false);
+  const uint32_t hi =
+      (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), CTRL, 0xF, 0xF, false);
+  return ((uint64_t)hi << 32) | lo;
+}
+template <bool MAX>
+__device__ __forceinline__ uint64_t wave_ext64_dpp(uint64_t x) {
+  auto pick = [](uint64_t a, uint64_t b) { return MAX ? (a > b ? a : b) : (a < b ? a : b); };
+  x = pick(x, dpp64<0xB1>(x));   // quad_perm [1,0,3,2]
+  x = pick(x, dpp64<0x4E>(x));   // quad_perm [2,3,0,1]
+  x = pick(x, dpp64<0x141>(x));  // row_half_mirror
+  x = pick(x, dpp64<0x140>(x));  // row_mirror
+  uint64_t r[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    r[k] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), 16 * k) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, 16 * k);
+  return pick(pick(r[0], r[1]), pick(r[2], r[3]));
+}
 __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
   return b2_pack(__builtin_amdgcn_readfirstlane((uint32_t)x),
                  __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)));
@@ -241,7 +278,8 @@ __device__ __forceinline__ uint32_t shfl32(uint32_t x, uint32_t src) {
 // keystream's first n*S bytes.  Each lane computes its own packet's block
 // (lanes sharing a block compute it redundantly: same instruction stream).
 template <uint32_t S>
-__device__ __forceinline__ void device_salt(const KParams &P, uint32_t p, uint32_t (&salt)[4]) {
+__device__ __forceinline__ void device_salt_words(const KParams &P, uint32_t p,
+                                                  uint32_t (&salt)[4]) {
   constexpr uint32_t per_block = 64 / S;  // 8 Salamander, 4 XPlus
   uint32_t blk[16];
   chacha20_block(P.salt_key, p / per_block, P.salt_nonce, blk);
@@ -258,6 +296,12 @@ __device__ __forceinline__ void device_salt(const KParams &P, uint32_t p, uint32
   }
 #pragma unroll
   for (uint32_t k = 0; k < S / 4; k++) salt[k] = y[k];
+}
+
+// ... and its copy to salt_out (SQOBFS_FLAG_DEVICE_SALT with salt_out)
+template <uint32_t S>
+__device__ __forceinline__ void device_salt_out(const KParams &P, uint32_t p,
+                                                const uint32_t (&salt)[4]) {
   if (P.salt_out) {
     uint32_t *so = reinterpret_cast<uint32_t *>(P.salt_out + (uint64_t)p * S);
 #pragma unroll
@@ -296,6 +340,8 @@ __device__ __forceinline__ void fetch_desc(const KParams &P, uint32_t p, bool va
 #pragma unroll
     for (uint32_t k = 0; k < S / 4; k++) d.salt[k] = sp[k];
   }
+  // device salts depend on p alone: computed while the loads above fly
+  if (DIR == 0 && SQ_EARLYSALT && P.device_salt) device_salt_words<S>(P, p, d.salt);
 }
 
 template <int KIND, int DIR, bool MULTI>
@@ -328,7 +374,13 @@ __device__ __forceinline__ void finalize_desc(const KParams &P, uint32_t p, bool
     olen = kBadPsk;
   } else if (DIR == 0) {  // obfuscate: wire = salt || payload ^ key
     if (P.device_salt) {
-      device_salt<S>(P, p, salt);
+      if (SQ_EARLYSALT) {
+#pragma unroll
+        for (uint32_t k = 0; k < S / 4; k++) salt[k] = d.salt[k];
+      } else {
+        device_salt_words<S>(P, p, salt);
+      }
+      device_salt_out<S>(P, p, salt);
     } else {
 #pragma unroll
       for (uint32_t k = 0; k < S / 4; k++) salt[k] = d.salt[k];
@@ -592,7 +644,8 @@ __device__ __forceinline__ void fetch_windows(const PacketJob &J, bool wire_salt
   }
   const WinAddr A = window_addrs<DIR, S>(J, wire_salt);
   const uint64_t first = (A.need & kWinS0) ? A.s0 : A.h0;
-  const uint64_t lo0 = uniform64(wave_min64(A.need ? first : ~0ull));
+  const uint64_t lo0 = SQ_DPPRED ? wave_ext64_dpp<false>(A.need ? first : ~0ull)
+                                 : uniform64(wave_min64(A.need ? first : ~0ull));
   const uint64_t lo = lo0 == ~0ull ? 0ull : lo0;  // (no lane needs a block)
   const __amdgpu_buffer_rsrc_t R =
       __builtin_amdgcn_make_buffer_rsrc((void *)lo, 0, (int)kWinOffNone, 0x00020000);
@@ -784,10 +837,14 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
   const uint64_t sabs = B0 + (J.src_pay - J.dst_pay);  // input of block B0
   const uint64_t s_first = sabs + 16ull * i_lo, s_end = sabs + 16ull * i_hi;
   // spans: output of every flat block, input of every interior block
-  const uint64_t d_lo = uniform64(wave_min64(F ? B0 : ~0ull));
-  const uint64_t d_hi = uniform64(wave_max64(F ? B0 + 16ull * F : 0ull));
-  const uint64_t s_lo = uniform64(wave_min64(has_int ? s_first : ~0ull));
-  const uint64_t s_hi = uniform64(wave_max64(has_int ? s_end : 0ull));
+  const uint64_t d_lo = SQ_DPPRED ? wave_ext64_dpp<false>(F ? B0 : ~0ull)
+                                  : uniform64(wave_min64(F ? B0 : ~0ull));
+  const uint64_t d_hi = SQ_DPPRED ? wave_ext64_dpp<true>(F ? B0 + 16ull * F : 0ull)
+                                  : uniform64(wave_max64(F ? B0 + 16ull * F : 0ull));
+  const uint64_t s_lo = SQ_DPPRED ? wave_ext64_dpp<false>(has_int ? s_first : ~0ull)
+                                  : uniform64(wave_min64(has_int ? s_first : ~0ull));
+  const uint64_t s_hi = SQ_DPPRED ? wave_ext64_dpp<true>(has_int ? s_end : 0ull)
+                                  : uniform64(wave_max64(has_int ? s_end : 0ull));
   const bool mis = has_int && (sabs & 3);
   const bool sok = s_hi <= s_lo || s_hi - s_lo <= kMaxSpan;
   U.fast = T0 != 0 && __ballot(mis) == 0 && d_hi - d_lo <= kMaxSpan && sok;
