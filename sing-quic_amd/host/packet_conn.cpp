@@ -190,13 +190,32 @@ Obfuscator::~Obfuscator() {
 int Obfuscator::run(int dir, const sqobfs_batch &b) {
   if (status_ != SQ_OK) return status_;
   // a batch worth a launch goes to the GPU (cost as the packet conn engine
-  // counts it: payload bytes + 1 KiB per datagram, above 64 KiB); a single
-  // datagram costs ~1 us on the CPU path against a ~50 us staged round trip
+  // counts it: payload bytes + 1 KiB per datagram): above the measured
+  // break-even -- the recent staged round trip (sqobfs_run_host) times the
+  // recent CPU-path rate, as the engine's route_bytes; a single datagram
+  // costs ~1 us on the CPU path against a ~50 us staged round trip
   uint64_t cost = 0;
   for (uint32_t i = 0; i < b.n; i++) cost += b.in_len[i] + 1024u;
-  if (!ctx_ || gpu_failed_ || cost <= 65536) return sqobfs_cpu_run(kr_, dir, &b);
+  const uint64_t g = gpu_us_.load(std::memory_order_relaxed);
+  const uint64_t c = std::max<uint32_t>(1u, cpu_ns_kib_.load(std::memory_order_relaxed));
+  const uint64_t route = std::min<uint64_t>(16u << 20, std::max<uint64_t>(16u << 10, g * 1024000u / c));
+  const auto t0 = std::chrono::steady_clock::now();
+  auto ewma = [&](std::atomic<uint32_t> &a, uint64_t v) {
+    const uint32_t o = a.load(std::memory_order_relaxed);
+    a.store((uint32_t)((7ull * o + std::min<uint64_t>(v, 1u << 30)) / 8), std::memory_order_relaxed);
+  };
+  if (!ctx_ || gpu_failed_ || cost <= route) {
+    const int st = sqobfs_cpu_run(kr_, dir, &b);
+    if (cost >= (8u << 10))  // (smaller batches: timer noise)
+      ewma(cpu_ns_kib_, (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                            std::chrono::steady_clock::now() - t0).count() * 1024u / cost);
+    return st;
+  }
   const int st = sqobfs_run_host(ctx_, kr_, dir, &b);
   if (st == SQ_EDEVICE || st == SQ_ENODEV) gpu_failed_ = true;  // later batches: the CPU
+  if (st == SQ_OK)
+    ewma(gpu_us_, (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(
+                      std::chrono::steady_clock::now() - t0).count());
   return st;
 }
 

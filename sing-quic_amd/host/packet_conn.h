@@ -21,6 +21,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <memory>
 #include <mutex>
 #include <random>
@@ -89,6 +90,10 @@ class Obfuscator {
   int kind_;
   int status_ = SQ_OK;
   bool gpu_failed_ = false;
+  // routing (run): recent staged round trip (us) and CPU-path ns per KiB of
+  // cost, EWMAs; ~120 KiB break-even before either is measured
+  std::atomic<uint32_t> gpu_us_{60};
+  std::atomic<uint32_t> cpu_ns_kib_{500};
   sqobfs_ctx *ctx_ = nullptr;
   sqobfs_keyring *kr_ = nullptr;
 };
