@@ -106,17 +106,7 @@ namespace sq {
 #ifndef SQ_TIMELINE
 #define SQ_TIMELINE 0
 #endif
-// 1: the plan's and the windows' wave-wide 64-bit min / max by DPP row
-// moves and four readlanes (no LDS round trips) instead of a shuffle
-// butterfly
-#ifndef SQ_DPPRED
-#define SQ_DPPRED 0
-#endif
-// 1: device salts (SQOBFS_FLAG_DEVICE_SALT) are computed while the
-// descriptor loads are in flight (fetch_desc) instead of after they land
-#ifndef SQ_EARLYSALT
-#define SQ_EARLYSALT 0
-#endif
+
 
 // XCD-contiguous units.  Workgroups are dispatched round-robin over the 8
 // XCDs, so block b runs on XCD b % 8 and, unmapped, the XCDs share one
@@ -143,8 +133,7 @@ extern "C" const char *sqobfs_build_info(void) {
          " minw=" SQ_STR(SQ_MINW) " wpb=2"
          " ablate=" SQ_STR(SQ_ABLATE) " donate=" SQ_STR(SQ_DONATE) " align=" SQ_STR(SQ_ALIGN)
          " map=" SQ_STR(SQ_MAPBLK)
-         " windows=buffer earlysalt=" SQ_STR(SQ_EARLYSALT) " dppred=" SQ_STR(SQ_DPPRED)
-         " xcd=" SQ_STR(SQ_XCD);
+         " windows=buffer earlysalt=1 dppred=1 xcd=" SQ_STR(SQ_XCD);
 }
 
 // default unit size (KParams.ppw == 0); any 1 .. kMaxUnitPackets works
@@ -217,27 +206,12 @@ struct PacketJob {
 
 // ------------------------------------------------------------ wave helpers
 
-// 64-bit wave min / max (butterfly), result wave-uniform.
-__device__ __forceinline__ uint64_t wave_min64(uint64_t x) {
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    const uint64_t y = __shfl_xor((unsigned long long)x, d, kWave);
-    x = y < x ? y : x;
-  }
-  return x;
-}
-__device__ __forceinline__ uint64_t wave_max64(uint64_t x) {
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    const uint64_t y = __shfl_xor((unsigned long long)x, d, kWave);
-    x = y > x ? y : x;
-  }
-  return x;
-}
-// Wave-uniform 64-bit min / max (SQ_DPPRED): within each row of 16 lanes by
-// DPP moves (quad swaps, half-row mirror, row mirror: every lane then holds
-// its row's result), then the four rows' results by readlane.  Every lane
-// must be active.
+// Wave-uniform 64-bit min / max: within each row of 16 lanes by DPP moves
+// (quad swaps, half-row mirror, row mirror: every lane then holds its row's
+// result), then the four rows' results by readlane -- no LDS round trips.
+// Every lane must be active.  Measured in one process against a shuffle
+// (ds_bpermute) butterfly (round 4, profiles/r04/ab2): -0.15 to -0.6 % on
+// every kernel, -2 % with device salts on the ragged batch.
 template <int CTRL>
 __device__ __forceinline__ uint64_t dpp64(uint64_t x) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, CTRL, 0xF, 0xF, false);
@@ -258,10 +232,6 @@ __device__ __forceinline__ uint64_t wave_ext64_dpp(uint64_t x) {
     r[k] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), 16 * k) << 32) |
            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, 16 * k);
   return pick(pick(r[0], r[1]), pick(r[2], r[3]));
-}
-__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
-  return b2_pack(__builtin_amdgcn_readfirstlane((uint32_t)x),
-                 __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)));
 }
 __device__ __forceinline__ uint64_t shfl64(uint64_t x, uint32_t src) {
   return b2_pack((uint32_t)__shfl((int)(uint32_t)x, (int)src, kWave),
@@ -341,7 +311,9 @@ __device__ __forceinline__ void fetch_desc(const KParams &P, uint32_t p, bool va
     for (uint32_t k = 0; k < S / 4; k++) d.salt[k] = sp[k];
   }
   // device salts depend on p alone: computed while the loads above fly
-  if (DIR == 0 && SQ_EARLYSALT && P.device_salt) device_salt_words<S>(P, p, d.salt);
+  // (round 4, profiles/r04/ab2: configs[1] with device salts -2.6 %, XPlus
+  // -0.8 %, against computing them after the loads land)
+  if (DIR == 0 && P.device_salt) device_salt_words<S>(P, p, d.salt);
 }
 
 template <int KIND, int DIR, bool MULTI>
@@ -373,13 +345,9 @@ __device__ __forceinline__ void finalize_desc(const KParams &P, uint32_t p, bool
   } else if (bad) {
     olen = kBadPsk;
   } else if (DIR == 0) {  // obfuscate: wire = salt || payload ^ key
-    if (P.device_salt) {
-      if (SQ_EARLYSALT) {
+    if (P.device_salt) {  // (computed by fetch_desc)
 #pragma unroll
-        for (uint32_t k = 0; k < S / 4; k++) salt[k] = d.salt[k];
-      } else {
-        device_salt_words<S>(P, p, salt);
-      }
+      for (uint32_t k = 0; k < S / 4; k++) salt[k] = d.salt[k];
       device_salt_out<S>(P, p, salt);
     } else {
 #pragma unroll
@@ -644,8 +612,7 @@ __device__ __forceinline__ void fetch_windows(const PacketJob &J, bool wire_salt
   }
   const WinAddr A = window_addrs<DIR, S>(J, wire_salt);
   const uint64_t first = (A.need & kWinS0) ? A.s0 : A.h0;
-  const uint64_t lo0 = SQ_DPPRED ? wave_ext64_dpp<false>(A.need ? first : ~0ull)
-                                 : uniform64(wave_min64(A.need ? first : ~0ull));
+  const uint64_t lo0 = wave_ext64_dpp<false>(A.need ? first : ~0ull);
   const uint64_t lo = lo0 == ~0ull ? 0ull : lo0;  // (no lane needs a block)
   const __amdgpu_buffer_rsrc_t R =
       __builtin_amdgcn_make_buffer_rsrc((void *)lo, 0, (int)kWinOffNone, 0x00020000);
@@ -837,14 +804,10 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
   const uint64_t sabs = B0 + (J.src_pay - J.dst_pay);  // input of block B0
   const uint64_t s_first = sabs + 16ull * i_lo, s_end = sabs + 16ull * i_hi;
   // spans: output of every flat block, input of every interior block
-  const uint64_t d_lo = SQ_DPPRED ? wave_ext64_dpp<false>(F ? B0 : ~0ull)
-                                  : uniform64(wave_min64(F ? B0 : ~0ull));
-  const uint64_t d_hi = SQ_DPPRED ? wave_ext64_dpp<true>(F ? B0 + 16ull * F : 0ull)
-                                  : uniform64(wave_max64(F ? B0 + 16ull * F : 0ull));
-  const uint64_t s_lo = SQ_DPPRED ? wave_ext64_dpp<false>(has_int ? s_first : ~0ull)
-                                  : uniform64(wave_min64(has_int ? s_first : ~0ull));
-  const uint64_t s_hi = SQ_DPPRED ? wave_ext64_dpp<true>(has_int ? s_end : 0ull)
-                                  : uniform64(wave_max64(has_int ? s_end : 0ull));
+  const uint64_t d_lo = wave_ext64_dpp<false>(F ? B0 : ~0ull);
+  const uint64_t d_hi = wave_ext64_dpp<true>(F ? B0 + 16ull * F : 0ull);
+  const uint64_t s_lo = wave_ext64_dpp<false>(has_int ? s_first : ~0ull);
+  const uint64_t s_hi = wave_ext64_dpp<true>(has_int ? s_end : 0ull);
   const bool mis = has_int && (sabs & 3);
   const bool sok = s_hi <= s_lo || s_hi - s_lo <= kMaxSpan;
   U.fast = T0 != 0 && __ballot(mis) == 0 && d_hi - d_lo <= kMaxSpan && sok;
