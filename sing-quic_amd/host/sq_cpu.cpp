@@ -393,6 +393,130 @@ void derive_key(const PskEntry &e, const uint8_t *salt, uint8_t key[32]) {
   }
 }
 
+
+// ---- multi-buffer BLAKE2b: L one-block messages at once, one per 64-bit
+// vector lane (every packet's key is one compression for PSKs up to 120 B),
+// so a batch's keys cost ~1/L of a compression each instead of one.
+// L = 8 with AVX-512 (rotations are vprorq), 4 with AVX2.  SoA in and out:
+// h[i][l] = chaining word i of message l, m[j][l] = its message word j,
+// t[l] = its byte counter; key[i][l] = word i of its 32-byte digest.
+namespace {
+template <int L>
+struct B2Lanes {
+  uint64_t h[8][L], m[16][L], t[L];
+  uint64_t key[4][L];
+};
+
+#define SQ_B2MB_ROR(x, n) (((x) >> (n)) | ((x) << (64 - (n))))
+#define SQ_B2MB_G(a, b, c, d, x, y)                  \
+  do {                                               \
+    v[a] = v[a] + v[b] + (x);                        \
+    v[d] = SQ_B2MB_ROR(v[d] ^ v[a], 32);             \
+    v[c] = v[c] + v[d];                              \
+    v[b] = SQ_B2MB_ROR(v[b] ^ v[c], 24);             \
+    v[a] = v[a] + v[b] + (y);                        \
+    v[d] = SQ_B2MB_ROR(v[d] ^ v[a], 16);             \
+    v[c] = v[c] + v[d];                              \
+    v[b] = SQ_B2MB_ROR(v[b] ^ v[c], 63);             \
+  } while (0)
+#define SQ_B2MB_BODY(V)                                                         \
+  V v[16], mm[16];                                                             \
+  for (int i = 0; i < 8; i++) {                                                \
+    memcpy(&v[i], J.h[i], sizeof(V));                                          \
+    v[i + 8] = (V){} + kB2IV[i];                                               \
+  }                                                                            \
+  V tt;                                                                        \
+  memcpy(&tt, J.t, sizeof(V));                                                 \
+  v[12] ^= tt;                                                                 \
+  v[14] = ~v[14]; /* every message here is its own final block */              \
+  for (int j = 0; j < 16; j++) memcpy(&mm[j], J.m[j], sizeof(V));              \
+  /* (macros: a lambda would not inherit the function's target) */           \
+  for (int r = 0; r < 12; r++) {                                               \
+    const uint8_t *z = kSigma[r];                                              \
+    SQ_B2MB_G(0, 4, 8, 12, mm[z[0]], mm[z[1]]);                                \
+    SQ_B2MB_G(1, 5, 9, 13, mm[z[2]], mm[z[3]]);                                \
+    SQ_B2MB_G(2, 6, 10, 14, mm[z[4]], mm[z[5]]);                               \
+    SQ_B2MB_G(3, 7, 11, 15, mm[z[6]], mm[z[7]]);                               \
+    SQ_B2MB_G(0, 5, 10, 15, mm[z[8]], mm[z[9]]);                               \
+    SQ_B2MB_G(1, 6, 11, 12, mm[z[10]], mm[z[11]]);                             \
+    SQ_B2MB_G(2, 7, 8, 13, mm[z[12]], mm[z[13]]);                              \
+    SQ_B2MB_G(3, 4, 9, 14, mm[z[14]], mm[z[15]]);                              \
+  }                                                                            \
+  for (int i = 0; i < 4; i++) {                                                \
+    V hi;                                                                      \
+    memcpy(&hi, J.h[i], sizeof(V));                                            \
+    const V k = hi ^ v[i] ^ v[i + 8];                                          \
+    memcpy(J.key[i], &k, sizeof(V));                                           \
+  }
+
+typedef uint64_t u64x8 __attribute__((vector_size(64)));
+typedef uint64_t u64x4 __attribute__((vector_size(32)));
+__attribute__((target("avx512f"))) void b2_mb8_avx512(B2Lanes<8> &J) { SQ_B2MB_BODY(u64x8) }
+__attribute__((target("avx2"))) void b2_mb4_avx2(B2Lanes<4> &J) { SQ_B2MB_BODY(u64x4) }
+#undef SQ_B2MB_BODY
+#undef SQ_B2MB_G
+#undef SQ_B2MB_ROR
+
+// lanes per multi-buffer call on this CPU (0: none, per-message compressions)
+int pick_b2_lanes() {
+  __builtin_cpu_init();
+  if (force_portable()) return 0;
+  if (__builtin_cpu_supports("avx512f")) return 8;
+  return __builtin_cpu_supports("avx2") ? 4 : 0;
+}
+int b2_lanes() {
+  static const int l = pick_b2_lanes();
+  return l;
+}
+
+// The keys of n <= 8 packets whose entries are one-block (nblocks == 1):
+// salts[k] = packet k's salt (8 bytes), keys[k] = its key.
+template <int L>
+void b2_keys_mb(const PskEntry *const *es, const uint8_t (*salts)[16], uint32_t n,
+                uint8_t (*keys)[32], void (*fn)(B2Lanes<L> &)) {
+  for (uint32_t k0 = 0; k0 < n; k0 += L) {
+    B2Lanes<L> J;
+    for (int l = 0; l < L; l++) {
+      const uint32_t k = k0 + l < n ? k0 + l : n - 1;  // (a short group repeats its last)
+      const PskEntry &e = *es[k];
+      uint8_t blk[128];
+      memcpy(blk, e.m, sizeof blk);
+      memcpy(blk + e.salt_pos, salts[k], kSalamanderSalt);
+      for (int i = 0; i < 8; i++) J.h[i][l] = e.h[i];
+      for (int j = 0; j < 16; j++) J.m[j][l] = ld64le(blk + 8 * j);
+      J.t[l] = e.t_last;
+    }
+    fn(J);
+    for (int l = 0; l < L && k0 + l < n; l++)
+      for (int i = 0; i < 4; i++) memcpy(keys[k0 + l] + 8 * i, &J.key[i][l], 8);
+  }
+}
+}  // namespace
+
+void derive_keys(const PskEntry *const *es, const uint8_t (*salts)[16], uint32_t n,
+                 uint8_t (*keys)[32]) {
+  // one-block Salamander entries through the multi-buffer compression,
+  // everything else (XPlus, two-block PSKs) one at a time
+  const PskEntry *one[kKeyBatch];
+  uint8_t osalt[kKeyBatch][16];
+  uint32_t idx[kKeyBatch], m = 0;
+  const int lanes = b2_lanes();
+  for (uint32_t k = 0; k < n; k++) {
+    if (lanes && es[k]->kind == SQOBFS_SALAMANDER && es[k]->nblocks == 1) {
+      one[m] = es[k];
+      memcpy(osalt[m], salts[k], 16);
+      idx[m++] = k;
+    } else {
+      derive_key(*es[k], salts[k], keys[k]);
+    }
+  }
+  if (!m) return;
+  uint8_t ok[kKeyBatch][32];
+  if (lanes == 8) b2_keys_mb<8>(one, osalt, m, ok, b2_mb8_avx512);
+  else b2_keys_mb<4>(one, osalt, m, ok, b2_mb4_avx2);
+  for (uint32_t q = 0; q < m; q++) memcpy(keys[idx[q]], ok[q], 32);
+}
+
 // 32 bytes per iteration as four 64-bit words (the compiler widens the loop
 // to vector registers); the key's period is 32, so the key words are fixed.
 // Two builds of the same loop, AVX2 and baseline, picked once (a plain
@@ -453,39 +577,78 @@ int run_batch(int kind, int dir, const PskEntry *table, uint32_t count, const sq
   const size_t S = kind == SQOBFS_SALAMANDER ? kSalamanderSalt : kXPlusSalt;
   const bool obfs = dir == SQOBFS_OBFUSCATE;
   if (obfs && !salts && !b->salt) return SQ_EINVAL;
-  for (uint32_t i = 0; i < b->n; i++) {
-    const uint32_t pid = b->psk_id ? b->psk_id[i] : 0u;
-    const uint64_t len = b->in_len[i];
-    const uint64_t cap = (!obfs && kind == SQOBFS_XPLUS && b->in_cap && b->in_cap[i] > len)
-                             ? b->in_cap[i] : len;
-    if (len > kMaxPacket || cap > kMaxPacket) {
-      b->out_len[i] = kBadLen;
-      continue;
+  // kKeyBatch packets at a time: first every key of the group (the salts
+  // copied first: an in-place salt may sit where the output goes), then the
+  // XORs.  Packets' buffers do not overlap one another's.
+  enum : uint8_t { kDone, kObfs, kCopy, kDeobfs };
+  for (uint32_t i0 = 0; i0 < b->n; i0 += kKeyBatch) {
+    const uint32_t i1 = b->n - i0 < kKeyBatch ? b->n : i0 + kKeyBatch;
+    uint8_t what[kKeyBatch];
+    uint64_t caps[kKeyBatch];
+    uint8_t sl[kKeyBatch][16];
+    uint8_t keys[kKeyBatch][32];
+    const PskEntry *es[kKeyBatch];
+    uint8_t ks[kKeyBatch][16];
+    uint32_t kidx[kKeyBatch], nk = 0;
+    for (uint32_t i = i0; i < i1; i++) {
+      const uint32_t q = i - i0;
+      what[q] = kDone;
+      const uint32_t pid = b->psk_id ? b->psk_id[i] : 0u;
+      const uint64_t len = b->in_len[i];
+      const uint64_t cap = (!obfs && kind == SQOBFS_XPLUS && b->in_cap && b->in_cap[i] > len)
+                               ? b->in_cap[i] : len;
+      caps[q] = cap;
+      if (len > kMaxPacket || cap > kMaxPacket) {
+        b->out_len[i] = kBadLen;
+        continue;
+      }
+      if (pid >= count) {
+        b->out_len[i] = SQOBFS_BAD_PSK;
+        continue;
+      }
+      const uint8_t *in = b->in + b->in_off[i];
+      if (obfs) {  // salamander.go:57-70, xplus.go:62-75: salt || payload ^ key
+        memcpy(sl[q], salts ? salts + (size_t)i * S : b->salt + (size_t)i * S, S);
+        what[q] = kObfs;
+      } else if (kind == SQOBFS_SALAMANDER && len <= S) {
+        what[q] = kCopy;  // salamander.go:47-49: returned as is
+        continue;
+      } else if (kind == SQOBFS_XPLUS && len < S) {
+        b->out_len[i] = 0;  // xplus.go:50-52
+        continue;
+      } else {  // salamander.go:50-53, xplus.go:54-57: the salt is the wire's head
+        memcpy(sl[q], in, S);
+        what[q] = kDeobfs;
+      }
+      es[nk] = &table[pid];
+      memcpy(ks[nk], sl[q], 16);
+      kidx[nk++] = q;
     }
-    if (pid >= count) {
-      b->out_len[i] = SQOBFS_BAD_PSK;
-      continue;
-    }
-    const uint8_t *in = b->in + b->in_off[i];
-    uint8_t *out = b->out + b->out_off[i];
-    uint8_t key[32];
-    if (obfs) {  // salamander.go:57-70, xplus.go:62-75: salt || payload ^ key
-      const uint8_t *salt = salts ? salts + (size_t)i * S : b->salt + (size_t)i * S;
-      uint8_t s[16];
-      memcpy(s, salt, S);  // (the salt may sit where the output goes)
-      derive_key(table[pid], s, key);
-      xor_stream(out + S, in, len, key);
-      memcpy(out, s, S);
-      b->out_len[i] = (uint32_t)(S + len);
-    } else if (kind == SQOBFS_SALAMANDER && len <= S) {
-      memmove(out, in, len);  // salamander.go:47-49: returned as is
-      b->out_len[i] = (uint32_t)len;
-    } else if (kind == SQOBFS_XPLUS && len < S) {
-      b->out_len[i] = 0;  // xplus.go:50-52
-    } else {  // salamander.go:50-53, xplus.go:54-57 (XPlus to len(p) = cap)
-      derive_key(table[pid], in, key);
-      xor_stream(out, in + S, cap - S, key);
-      b->out_len[i] = (uint32_t)(len - S);
+    uint8_t kk[kKeyBatch][32];
+    derive_keys(es, ks, nk, kk);
+    for (uint32_t k = 0; k < nk; k++) memcpy(keys[kidx[k]], kk[k], 32);
+    for (uint32_t i = i0; i < i1; i++) {
+      const uint32_t q = i - i0;
+      const uint64_t len = b->in_len[i];
+      const uint8_t *in = b->in + b->in_off[i];
+      uint8_t *out = b->out + b->out_off[i];
+      switch (what[q]) {
+        case kObfs:
+          xor_stream(out + S, in, len, keys[q]);
+          memcpy(out, sl[q], S);
+          b->out_len[i] = (uint32_t)(S + len);
+          break;
+        case kCopy:
+          memmove(out, in, len);
+          b->out_len[i] = (uint32_t)len;
+          break;
+        case kDeobfs:  // (XPlus XORs to len(p) = cap)
+          xor_stream(out, in + S, caps[q] - S, keys[q]);
+          b->out_len[i] = (uint32_t)(len - S);
+          break;
+        default:
+          break;
+      }
     }
   }
   return SQ_OK;
