@@ -493,16 +493,89 @@ void b2_keys_mb(const PskEntry *const *es, const uint8_t (*salts)[16], uint32_t 
 }
 }  // namespace
 
+// ---- multi-buffer SHA-256 for XPlus: L one-block messages at once, one
+// per 32-bit lane (every key is one compression for PSKs up to 39 B); L = 16
+// with AVX-512, 8 with AVX2.  SoA: st[i][l], m[j][l] (big-endian words).
+namespace {
+template <int L>
+struct S2Lanes {
+  uint32_t st[8][L], m[16][L];
+};
+
+#define SQ_S2MB_ROR(x, n) (((x) >> (n)) | ((x) << (32 - (n))))
+#define SQ_S2MB_BODY(V)                                                            \
+  V w[16], a, b, c, d, e, f, g, h, st0[8];                                        \
+  for (int i = 0; i < 8; i++) memcpy(&st0[i], J.st[i], sizeof(V));                \
+  for (int j = 0; j < 16; j++) memcpy(&w[j], J.m[j], sizeof(V));                  \
+  a = st0[0]; b = st0[1]; c = st0[2]; d = st0[3];                                 \
+  e = st0[4]; f = st0[5]; g = st0[6]; h = st0[7];                                 \
+  for (int i = 0; i < 64; i++) {                                                  \
+    if (i >= 16) {                                                                \
+      const V x15 = w[(i - 15) & 15], x2 = w[(i - 2) & 15];                       \
+      const V s0 = SQ_S2MB_ROR(x15, 7) ^ SQ_S2MB_ROR(x15, 18) ^ (x15 >> 3);       \
+      const V s1 = SQ_S2MB_ROR(x2, 17) ^ SQ_S2MB_ROR(x2, 19) ^ (x2 >> 10);        \
+      w[i & 15] = w[i & 15] + s0 + w[(i - 7) & 15] + s1;                          \
+    }                                                                             \
+    const V S1 = SQ_S2MB_ROR(e, 6) ^ SQ_S2MB_ROR(e, 11) ^ SQ_S2MB_ROR(e, 25);     \
+    const V t1 = h + S1 + ((e & f) ^ (~e & g)) + kS2K[i] + w[i & 15];             \
+    const V S0 = SQ_S2MB_ROR(a, 2) ^ SQ_S2MB_ROR(a, 13) ^ SQ_S2MB_ROR(a, 22);     \
+    const V t2 = S0 + ((a & b) ^ (a & c) ^ (b & c));                              \
+    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;            \
+  }                                                                               \
+  const V out[8] = {a + st0[0], b + st0[1], c + st0[2], d + st0[3],               \
+                    e + st0[4], f + st0[5], g + st0[6], h + st0[7]};              \
+  for (int i = 0; i < 8; i++) memcpy(J.st[i], &out[i], sizeof(V));
+
+typedef uint32_t u32x16 __attribute__((vector_size(64)));
+typedef uint32_t u32x8 __attribute__((vector_size(32)));
+__attribute__((target("avx512f"))) void s2_mb16_avx512(S2Lanes<16> &J) { SQ_S2MB_BODY(u32x16) }
+__attribute__((target("avx2"))) void s2_mb8_avx2(S2Lanes<8> &J) { SQ_S2MB_BODY(u32x8) }
+#undef SQ_S2MB_BODY
+#undef SQ_S2MB_ROR
+
+// The keys of n one-block XPlus packets (salts[k]: 16 bytes)
+template <int L>
+void s2_keys_mb(const PskEntry *const *es, const uint8_t (*salts)[16], uint32_t n,
+                uint8_t (*keys)[32], void (*fn)(S2Lanes<L> &)) {
+  for (uint32_t k0 = 0; k0 < n; k0 += L) {
+    S2Lanes<L> J;
+    for (int l = 0; l < L; l++) {
+      const uint32_t k = k0 + l < n ? k0 + l : n - 1;  // (a short group repeats its last)
+      const PskEntry &e = *es[k];
+      uint32_t m[16];
+      memcpy(m, e.m, sizeof m);
+      for (uint32_t q = 0; q < (uint32_t)kXPlusSalt; q++) {
+        const uint32_t i = e.salt_pos + q;
+        m[i / 4] |= (uint32_t)salts[k][q] << (24 - 8 * (i % 4));
+      }
+      const uint32_t *h32 = reinterpret_cast<const uint32_t *>(e.h);
+      for (int i = 0; i < 8; i++) J.st[i][l] = h32[i];
+      for (int j = 0; j < 16; j++) J.m[j][l] = m[j];
+    }
+    fn(J);
+    for (int l = 0; l < L && k0 + l < n; l++)
+      for (int i = 0; i < 8; i++) {
+        const uint32_t x = J.st[i][l];
+        keys[k0 + l][4 * i] = (uint8_t)(x >> 24);
+        keys[k0 + l][4 * i + 1] = (uint8_t)(x >> 16);
+        keys[k0 + l][4 * i + 2] = (uint8_t)(x >> 8);
+        keys[k0 + l][4 * i + 3] = (uint8_t)x;
+      }
+  }
+}
+}  // namespace
+
 void derive_keys(const PskEntry *const *es, const uint8_t (*salts)[16], uint32_t n,
                  uint8_t (*keys)[32]) {
-  // one-block Salamander entries through the multi-buffer compression,
-  // everything else (XPlus, two-block PSKs) one at a time
+  // one-block entries through the multi-buffer compressions (BLAKE2b
+  // Salamander, SHA-256 XPlus), two-block PSKs one at a time
   const PskEntry *one[kKeyBatch];
   uint8_t osalt[kKeyBatch][16];
   uint32_t idx[kKeyBatch], m = 0;
-  const int lanes = b2_lanes();
+  const int lanes = b2_lanes();  // (8: AVX-512, 4: AVX2, 0: neither)
+  const int kind = n ? (int)es[0]->kind : 0;  // (one keyring: one kind)
   for (uint32_t k = 0; k < n; k++) {
-    if (lanes && es[k]->kind == SQOBFS_SALAMANDER && es[k]->nblocks == 1) {
+    if (lanes && es[k]->nblocks == 1) {
       one[m] = es[k];
       memcpy(osalt[m], salts[k], 16);
       idx[m++] = k;
@@ -512,8 +585,13 @@ void derive_keys(const PskEntry *const *es, const uint8_t (*salts)[16], uint32_t
   }
   if (!m) return;
   uint8_t ok[kKeyBatch][32];
-  if (lanes == 8) b2_keys_mb<8>(one, osalt, m, ok, b2_mb8_avx512);
-  else b2_keys_mb<4>(one, osalt, m, ok, b2_mb4_avx2);
+  if (kind == SQOBFS_SALAMANDER) {
+    if (lanes == 8) b2_keys_mb<8>(one, osalt, m, ok, b2_mb8_avx512);
+    else b2_keys_mb<4>(one, osalt, m, ok, b2_mb4_avx2);
+  } else {
+    if (lanes == 8) s2_keys_mb<16>(one, osalt, m, ok, s2_mb16_avx512);
+    else s2_keys_mb<8>(one, osalt, m, ok, s2_mb8_avx2);
+  }
   for (uint32_t q = 0; q < m; q++) memcpy(keys[idx[q]], ok[q], 32);
 }
 

@@ -44,8 +44,9 @@ void psk_prepare(int kind, const uint8_t *psk, uint32_t len, PskEntry *e);
 // SHA-256(psk || salt16) (xplus.go:54,70), from the entry's midstate.
 void derive_key(const PskEntry &e, const uint8_t *salt, uint8_t key[32]);
 // The keys of n <= kKeyBatch packets (es[k]'s PSK, salts[k] its salt, S
-// bytes of 16); one-block Salamander entries by the multi-buffer BLAKE2b
-// (AVX-512: 8 at once, AVX2: 4).
+// bytes of 16); one-block entries by the multi-buffer compressions
+// (BLAKE2b: 8 at once with AVX-512, 4 with AVX2; SHA-256: 16 / 8).  All
+// entries of one call are of one kind (one keyring).
 constexpr uint32_t kKeyBatch = 64;
 void derive_keys(const PskEntry *const *es, const uint8_t (*salts)[16], uint32_t n,
                  uint8_t (*keys)[32]);
