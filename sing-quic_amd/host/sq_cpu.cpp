@@ -458,10 +458,13 @@ __attribute__((target("avx2"))) void b2_mb4_avx2(B2Lanes<4> &J) { SQ_B2MB_BODY(u
 #undef SQ_B2MB_ROR
 
 // lanes per multi-buffer call on this CPU (0: none, per-message compressions)
+// SQOBFS_CPU_MB=avx2 (tests): the AVX2 multi-buffer width on an AVX-512 host
 int pick_b2_lanes() {
   __builtin_cpu_init();
   if (force_portable()) return 0;
-  if (__builtin_cpu_supports("avx512f")) return 8;
+  const char *e = getenv("SQOBFS_CPU_MB");
+  const bool avx2_only = e && strcmp(e, "avx2") == 0;
+  if (__builtin_cpu_supports("avx512f") && !avx2_only) return 8;
   return __builtin_cpu_supports("avx2") ? 4 : 0;
 }
 int b2_lanes() {

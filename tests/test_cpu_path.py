@@ -145,13 +145,16 @@ def test_generated_salts_are_the_wire_salts(kind):
         assert hb.out[o:o + L + S].tobytes() == w
 
 
-def test_portable_compressions_too():
-    """The CPU path picks AVX2 BLAKE2b / SHA-NI SHA-256 where the host has
-    them; the portable compressions (hosts without) pass the same tests
-    (SQOBFS_CPU_PORTABLE=1 forces them)."""
+@pytest.mark.parametrize("force", ["portable", "avx2"])
+def test_portable_compressions_too(force):
+    """The CPU path picks AVX2 BLAKE2b / SHA-NI SHA-256 and the AVX-512
+    multi-buffer key groups where the host has them; the portable
+    compressions (hosts without: SQOBFS_CPU_PORTABLE=1 forces them) and the
+    AVX2 multi-buffer width (SQOBFS_CPU_MB=avx2) pass the same tests."""
     import subprocess
     import sys
-    env = dict(os.environ, SQOBFS_CPU_PORTABLE="1")
+    env = dict(os.environ, **({"SQOBFS_CPU_PORTABLE": "1"} if force == "portable"
+                              else {"SQOBFS_CPU_MB": "avx2"}))
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider",
                         os.path.abspath(__file__), "-k", "not portable"],
                        capture_output=True, text=True, env=env, timeout=600,
