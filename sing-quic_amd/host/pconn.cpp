@@ -426,10 +426,14 @@ void task_end(sqobfs_pconn *pc, int d, bool more, int64_t due = 0) {
     if (due) {
       pc->timed[d] = true;
       E->timers.push_back({due, {pc, d}});
+      E->cv.notify_one();  // (a sleeping worker's deadline may be later)
     } else {
+      // no wake-up: the calling worker goes back to the run queue next and
+      // takes it itself.  Waking another worker for it made every batch a
+      // hand-off between two threads (a futex wake and a context switch per
+      // batch), which kept batches small at high rates.
       E->runq.push_back({pc, d});
     }
-    E->cv.notify_one();
     return;
   }
   pc->sched[d] = false;

@@ -377,55 +377,81 @@ int main(void) {
 
   /* ---- pconn throughput: pconn A -> pconn B over loopback, one writer
    * thread (the Go Conn's WriteTo callers), one reader thread; without and
-   * with UDP GSO (A) / GRO (B) */
-  for (int off = 0; off < 2; off++) {
-    uint16_t pa, pb;
-    int fa = udp_socket(&pa), fb = udp_socket(&pb);
-    sqobfs_pconn *A, *B;
-    sqobfs_pconn_opts oa, ob;
-    memset(&oa, 0, sizeof oa);
-    memset(&ob, 0, sizeof ob);
-    oa.flags = off ? SQOBFS_UDP_TX_GSO : 0u;
-    ob.flags = off ? SQOBFS_UDP_RX_GRO : 0u;
-    CHECK(sqobfs_pconn_open(ctx, kr, fa, &oa, &A));
-    CHECK(sqobfs_pconn_open(ctx, kr, fb, &ob, &B));
-    const sqobfs_addr to = loop_addr(pb);
-    static uint8_t pay[L];
-    memset(pay, 9, L);
-    struct rd {
-      sqobfs_pconn *pc;
-      long got;
-      double last_us;
-    } r = {B, 0, 0};
-    pthread_t th;
-    extern void *tput_reader(void *);
-    pthread_create(&th, NULL, tput_reader, &r);
-    const long N = 200000;
-    const double t0 = now_us();
-    for (long i = 0; i < N; i++) {
-      CHECK(sqobfs_pconn_write(A, pay, L, &to, 0));
-      if ((i & 1023) == 1023) {
-        /* stay inside the loopback socket buffers (UDP drops, the test
-         * counts what arrives) */
-        struct timespec ts = {0, 200000};
-        nanosleep(&ts, NULL);
+   * with UDP GSO (A) / GRO (B); with the engine's routing (defaults), every
+   * batch launched (_gpu_only), every batch on the CPU path (_cpu_only) and
+   * on the host engine (_no_device); the defaults again last (order
+   * effects) */
+  {
+    sqobfs_keyring *hk;
+    uint64_t o0 = 0;
+    uint32_t l0 = PL;
+    CHECK(sqobfs_keyring_create(NULL, SQOBFS_SALAMANDER, 1, PSK, &o0, &l0, &hk));
+    static const char *const modes[] = {"", "_gpu_only", "_cpu_only", "_no_device",
+                                        "_defaults_again"};
+    for (int m = 0; m < 5; m++)
+      for (int off = 0; off < 2; off++) {
+        sqobfs_ctx *const c = m == 3 ? NULL : ctx;
+        sqobfs_keyring *const k = m == 3 ? hk : kr;
+        uint16_t pa, pb;
+        int fa = udp_socket(&pa), fb = udp_socket(&pb);
+        sqobfs_pconn *A, *B;
+        sqobfs_pconn_opts oa, ob;
+        memset(&oa, 0, sizeof oa);
+        memset(&ob, 0, sizeof ob);
+        oa.flags = off ? SQOBFS_UDP_TX_GSO : 0u;
+        ob.flags = off ? SQOBFS_UDP_RX_GRO : 0u;
+        if (m == 1) oa.cpu_max = ob.cpu_max = oa.inline_gap_us = ob.inline_gap_us = SQOBFS_PCONN_NEVER;
+        if (m == 2) oa.cpu_max = ob.cpu_max = 1u << 30;
+        CHECK(sqobfs_pconn_open(c, k, fa, &oa, &A));
+        CHECK(sqobfs_pconn_open(c, k, fb, &ob, &B));
+        const sqobfs_addr to = loop_addr(pb);
+        static uint8_t pay[L];
+        memset(pay, 9, L);
+        struct rd {
+          sqobfs_pconn *pc;
+          long got;
+          double last_us;
+        } r = {B, 0, 0};
+        pthread_t th;
+        extern void *tput_reader(void *);
+        pthread_create(&th, NULL, tput_reader, &r);
+        const long N = 200000;
+        const double t0 = now_us();
+        for (long i = 0; i < N; i++) {
+          CHECK(sqobfs_pconn_write(A, pay, L, &to, 0));
+          if ((i & 1023) == 1023) {
+            /* stay inside the loopback socket buffers (UDP drops, the test
+             * counts what arrives) */
+            struct timespec ts = {0, 200000};
+            nanosleep(&ts, NULL);
+          }
+        }
+        const double tw = now_us();
+        CHECK(sqobfs_pconn_set_deadline(B, SQOBFS_PCONN_READ, 0));
+        pthread_join(th, NULL);
+        const double dt = (r.last_us - t0) * 1e-6;  /* to the last datagram's arrival */
+        sqobfs_pconn_stats sa, sb;
+        CHECK(sqobfs_pconn_stats_get(A, &sa));
+        CHECK(sqobfs_pconn_stats_get(B, &sb));
+        sqobfs_engine_info ei;
+        CHECK(sqobfs_engine_info_get(c, &ei));
+        printf("\"pconn_throughput%s%s\": {\"datagrams\": %ld, \"received\": %ld, \"seconds\": %.3f, "
+               "\"write_seconds\": %.3f, \"datagrams_per_s\": %.0f, \"payload_gib_s\": %.3f, "
+               "\"tx_batches\": %llu, \"rx_batches\": %llu, \"tx_cpu_batches\": %llu, "
+               "\"rx_cpu_batches\": %llu, \"inline_writes\": %llu, \"route_bytes\": %llu, "
+               "\"launch_us\": %u, \"cpu_ns_per_kib\": %u}, ",
+               modes[m], off ? "_gso_gro" : "", N, r.got, dt, (tw - t0) * 1e-6, r.got / dt,
+               r.got * (double)L / dt / (1 << 30), (unsigned long long)sa.tx_batches,
+               (unsigned long long)sb.rx_batches, (unsigned long long)sa.cpu_batches,
+               (unsigned long long)sb.cpu_batches, (unsigned long long)sa.inline_writes,
+               (unsigned long long)ei.route_bytes, ei.launch_us, ei.cpu_ns_per_kib);
+        fflush(stdout);
+        sqobfs_pconn_close(A);
+        sqobfs_pconn_close(B);
+        close(fa);
+        close(fb);
       }
-    }
-    CHECK(sqobfs_pconn_set_deadline(B, SQOBFS_PCONN_READ, 0));
-    pthread_join(th, NULL);
-    const double dt = (r.last_us - t0) * 1e-6;  /* to the last datagram's arrival */
-    sqobfs_pconn_stats sa, sb;
-    CHECK(sqobfs_pconn_stats_get(A, &sa));
-    CHECK(sqobfs_pconn_stats_get(B, &sb));
-    printf("\"pconn_throughput%s\": {\"datagrams\": %ld, \"received\": %ld, \"seconds\": %.3f, "
-           "\"datagrams_per_s\": %.0f, \"payload_gib_s\": %.3f, \"tx_batches\": %llu, "
-           "\"rx_batches\": %llu}, ",
-           off ? "_gso_gro" : "", N, r.got, dt, r.got / dt, r.got * (double)L / dt / (1 << 30),
-           (unsigned long long)sa.tx_batches, (unsigned long long)sb.rx_batches);
-    sqobfs_pconn_close(A);
-    sqobfs_pconn_close(B);
-    close(fa);
-    close(fb);
+    sqobfs_keyring_destroy(hk);
   }
 
   /* ---- the reference's per-datagram work, one core (oracle byte loops) */
