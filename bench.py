@@ -691,20 +691,33 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
+    # The timed region holds the launches only: one HIP event pair on the
+    # launch stream spans it, so the kernel average is the span / steps
+    # (back-to-back kernels, their dispatch gaps included).  An event pair
+    # around every launch put two marker packets between kernels and cost
+    # 7-9 us per step (scripts/dev/timing_probe.py).
+    e_beg, e_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    for e0, e1 in ev:
-        e0.record(stream)
+    e_beg.record(stream)
+    for _ in range(args.steps):
         sqobfs.launch(ctx, kr, direction, b, s)
-        e1.record(stream)
+    e_end.record(stream)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kern_ms = sorted(e0.elapsed_time(e1) for e0, e1 in ev)
-    kern_avg_ms = sum(kern_ms) / len(kern_ms)
+    kern_avg_ms = e_beg.elapsed_time(e_end) / args.steps
+    # per-launch spread, after the timed region (not in `value`): each
+    # kernel's own dispatch records its event pair
+    n_each = min(args.steps, 20)
+    dev_ev = sqobfs.DispatchEvents(n_each)
+    for i in range(n_each):
+        dev_ev.arm(i)
+        sqobfs.launch(ctx, kr, direction, b, s)
+    torch.cuda.synchronize(dev)
+    kern_ms = sorted(dev_ev.elapsed_ms(i) for i in range(n_each))
+    dev_ev.close()
 
     tdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     if dist:
@@ -720,7 +733,7 @@ def main():
         salts = np.frombuffer(ol.device_salts(SALT_KEY, last, n, S), np.uint8)
         sh["salt"] = torch.from_numpy(salts.copy()).to(dev)
     if direction == sqobfs.OBFUSCATE:
-        parity = spot_check(torch, sh, kind, n, sh["out"], saved, warm + args.steps)
+        parity = spot_check(torch, sh, kind, n, sh["out"], saved, warm + args.steps + n_each)
     else:
         lens = sh["lens"].cpu().numpy()
         offs = sh["in_off"].cpu().numpy()
@@ -794,8 +807,12 @@ def main():
             "kernel": kernel_name(kind, direction, n_psk > 1, ctx.unit_packets),
             "build": sqobfs.build_info(),
             "kernel_avg_us": round(kern_avg_ms * 1e3, 2),
+            "kernel_avg_rule": "HIP events spanning the timed region's back-to-back "
+                               "launches / steps (dispatch gaps included)",
             "kernel_min_us": round(kern_ms[0] * 1e3, 2),
             "kernel_median_us": round(kern_ms[len(kern_ms) // 2] * 1e3, 2),
+            "kernel_each_rule": f"{n_each} launches after the timed region, each timed by "
+                                "its own dispatch (sqobfs_debug_time_next_launch)",
             "algorithmic_bytes_per_launch": alg_bytes,
             "bytes_rule": "obfuscate 2L+2S per packet (2L+S with device salts), "
                           "deobfuscate 2L+S (SURVEY.md 8(d))",

@@ -431,6 +431,12 @@ size_t sqobfs_host_staging_bytes(const sqobfs_ctx *ctx);
 /* Test hook: the next sqobfs_run_host whose pipeline reaches chunk `chunk`
  * fails there with SQ_EDEVICE, as a failed launch would (-1 = off). */
 void sqobfs_debug_fail_chunk(int chunk);
+/* Measurement hook (bench.py): the calling thread's next obfuscation launch
+ * (sqobfs_launch / sqobfs_run_host chunk) records start_event / stop_event
+ * (hipEvent_t, created with timing) with its own kernel dispatch
+ * (hipExtLaunchKernel), so per-kernel times cost no marker packets between
+ * kernels.  Either may be NULL; cleared by that launch. */
+void sqobfs_debug_time_next_launch(void *start_event, void *stop_event);
 
 /* ------------------------------------------------------------------------
  * Batched UDP socket I/O (Linux) -- the host side of the path.

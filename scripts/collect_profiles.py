@@ -22,17 +22,23 @@ for d in sorted(glob.glob(os.path.join(src, "*"))):
         shutil.copy(st[0], os.path.join(dst, f"kernel_stats_{cfg}.csv"))
     tr = glob.glob(os.path.join(d, "kt", "**", "*kernel_trace.csv"), recursive=True)
     if tr:
-        # the timed launches are the last `steps` obfs_kernel dispatches (the
-        # kernel-stats average also holds the cold first launches of warm-up)
+        # the timed launches are the `steps` obfs_kernel dispatches before the
+        # bench's per-launch pass (min(steps, 20) more, when its line has
+        # kernel_each_rule), or the last `steps` (earlier bench lines); the
+        # kernel-stats average also holds the cold first launches of warm-up
         import csv
         rows = [r for r in csv.DictReader(open(tr[0])) if "obfs_kernel" in r["Kernel_Name"]]
         rows.sort(key=lambda r: int(r["Start_Timestamp"]))
         kt = json.loads(open(os.path.join(d, "kt.json")).read().strip().splitlines()[-1])
-        last = rows[-kt["steps"]:]
+        k = kt["steps"]
+        each = min(k, 20) if "kernel_each_rule" in kt["roofline"] else 0
+        last = rows[len(rows) - each - k:len(rows) - each]
         us = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in last]
+        span = (int(last[-1]["End_Timestamp"]) - int(last[0]["Start_Timestamp"])) / 1e3 / k
         json.dump({"kernel": last[-1]["Kernel_Name"], "dispatches": len(rows),
                    "timed_dispatches": len(us), "timed_avg_us": round(sum(us) / len(us), 2),
                    "timed_min_us": round(min(us), 2), "timed_max_us": round(max(us), 2),
+                   "timed_span_per_dispatch_us": round(span, 2),
                    "bench_kernel_avg_us_same_run": kt["roofline"]["kernel_avg_us"],
                    "lds_bytes": last[-1]["LDS_Block_Size"],
                    "grid": last[-1]["Grid_Size_X"], "workgroup": last[-1]["Workgroup_Size_X"],

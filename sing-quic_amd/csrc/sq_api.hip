@@ -1177,6 +1177,10 @@ size_t sqobfs_host_staging_bytes(const sqobfs_ctx *ctx) { return ctx ? ctx->pinn
 
 void sqobfs_debug_fail_chunk(int chunk) { g_fail_chunk.store(chunk); }
 
+void sqobfs_debug_time_next_launch(void *start_event, void *stop_event) {
+  sq_time_next_launch(start_event, stop_event);
+}
+
 int sqobfs_host_alloc(sqobfs_ctx *ctx, size_t bytes, void **out) {
   if (!ctx || !out) return SQ_EINVAL;
   *out = nullptr;

@@ -215,6 +215,9 @@ extern "C" int sq_launch_gcm_group(const uint16_t *key_id, uint32_t n, uint32_t 
 extern "C" int sq_launch_quic(int open, const sq::QParams *qp, void *stream);
 
 // launchers implemented in sq_kernels.hip
+// the calling thread's next obfuscation launch records these events with its
+// dispatch (sqobfs_debug_time_next_launch)
+extern "C" void sq_time_next_launch(void *start, void *stop);
 extern "C" int sq_launch_obfs(int kind, int dir, const sq::KParams *kp,
                               void *stream);
 extern "C" int sq_launch_psk_prepare(int kind, const uint8_t *blob,

@@ -42,6 +42,7 @@
 // costs 7-12 % (holes) to 30 % (holes filled early) of the HBM rate, and
 // splitting wave instructions into 256-byte pieces (16 lanes per packet)
 // costs 40 %.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
@@ -1278,12 +1279,23 @@ __global__ void psk_prepare_kernel(int kind, const uint8_t *blob, const uint64_t
 template <int KIND, int DIR>
 constexpr int kWavesPerGroup = 2;
 
+// sqobfs_debug_time_next_launch: events the calling thread's next launch
+// records with its own dispatch (no marker packets between kernels)
+thread_local hipEvent_t t_time_ev[2] = {nullptr, nullptr};
+
 template <int KIND, int DIR, bool MULTI, int U, int WPB>
 static int launch_k(const KParams &P, hipStream_t s) {
   const uint64_t units = ((uint64_t)P.n + P.ppw - 1) / P.ppw;
   const uint64_t blocks = (units + WPB - 1) / WPB;
-  hipLaunchKernelGGL((obfs_kernel<KIND, DIR, MULTI, U, WPB>), dim3((uint32_t)blocks),
-                     dim3(WPB * kWave), 0, s, P);
+  if (t_time_ev[0] || t_time_ev[1]) {
+    hipEvent_t e0 = t_time_ev[0], e1 = t_time_ev[1];
+    t_time_ev[0] = t_time_ev[1] = nullptr;
+    hipExtLaunchKernelGGL((obfs_kernel<KIND, DIR, MULTI, U, WPB>), dim3((uint32_t)blocks),
+                          dim3(WPB * kWave), 0, s, e0, e1, 0u, P);
+  } else {
+    hipLaunchKernelGGL((obfs_kernel<KIND, DIR, MULTI, U, WPB>), dim3((uint32_t)blocks),
+                       dim3(WPB * kWave), 0, s, P);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -1292,7 +1304,10 @@ static int launch_one(const KParams *kp, hipStream_t s) {
   constexpr int U = SQ_U;
   KParams P = *kp;
   if (P.ppw == 0) P.ppw = kPktPerWave;
-  if (P.ppw > kMaxUnitPackets) return -1;
+  if (P.ppw > kMaxUnitPackets) {
+    t_time_ev[0] = t_time_ev[1] = nullptr;
+    return -1;
+  }
   const uint64_t units = ((uint64_t)P.n + P.ppw - 1) / P.ppw;
   P.xcd = SQ_XCD < 0 ? (units >= kXcdMinUnits ? 1u : 0u) : (uint32_t)SQ_XCD;
   return launch_k<KIND, DIR, MULTI, U, kWavesPerGroup<KIND, DIR>>(P, s);
@@ -1300,9 +1315,17 @@ static int launch_one(const KParams *kp, hipStream_t s) {
 
 }  // namespace sq
 
+extern "C" void sq_time_next_launch(void *start, void *stop) {
+  sq::t_time_ev[0] = (hipEvent_t)start;
+  sq::t_time_ev[1] = (hipEvent_t)stop;
+}
+
 extern "C" int sq_launch_obfs(int kind, int dir, const sq::KParams *kp, void *stream) {
   using namespace sq;
-  if (kp->n == 0) return 0;
+  if (kp->n == 0) {
+    t_time_ev[0] = t_time_ev[1] = nullptr;
+    return 0;
+  }
   hipStream_t s = (hipStream_t)stream;
   const bool multi = kp->psk_id != nullptr;
   const int sel = (kind << 2) | (dir << 1) | (multi ? 1 : 0);

@@ -170,6 +170,8 @@ def load(path: str) -> ctypes.CDLL:
     L.sqobfs_host_staging_bytes.restype = ctypes.c_size_t
     L.sqobfs_debug_fail_chunk.argtypes = [i32]
     L.sqobfs_debug_fail_chunk.restype = None
+    L.sqobfs_debug_time_next_launch.argtypes = [vp, vp]
+    L.sqobfs_debug_time_next_launch.restype = None
     L.sqobfs_shard_cuts.argtypes = [u32, vp, u32, vp]
     L.sqobfs_run_host_sharded.argtypes = [u32, vp, vp, i32, ctypes.POINTER(Batch)]
     L.sqobfs_shard_run.argtypes = [u32, vp, vp, i32, vp]
@@ -484,6 +486,43 @@ def shard_launch(ctxs: list[Context], krs: list[Keyring], direction: int,
 def debug_fail_chunk(chunk: int) -> None:
     """Test hook: the next run_host fails (SQ_EDEVICE) at that pipeline chunk."""
     lib().sqobfs_debug_fail_chunk(chunk)
+
+
+class DispatchEvents:
+    """`count` pairs of HIP timing events, each pair recorded by one launch's
+    own kernel dispatch (sqobfs_debug_time_next_launch): per-kernel times
+    with no marker packets queued between the kernels, as a pair of
+    hipEventRecord calls around each launch would.  Used by bench.py."""
+
+    def __init__(self, count: int):
+        self._hip = ctypes.CDLL("libamdhip64.so")
+        self._hip.hipEventCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+        self._hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float),
+                                                  ctypes.c_void_p, ctypes.c_void_p]
+        self._hip.hipEventDestroy.argtypes = [ctypes.c_void_p]
+        self.ev = []
+        for _ in range(2 * count):
+            e = ctypes.c_void_p()
+            if self._hip.hipEventCreate(ctypes.byref(e)) != 0:
+                self.close()
+                raise SqError(-5, "hipEventCreate")
+            self.ev.append(e)
+
+    def arm(self, i: int) -> None:
+        """The calling thread's next launch records pair i."""
+        lib().sqobfs_debug_time_next_launch(self.ev[2 * i], self.ev[2 * i + 1])
+
+    def elapsed_ms(self, i: int) -> float:
+        ms = ctypes.c_float()
+        st = self._hip.hipEventElapsedTime(ctypes.byref(ms), self.ev[2 * i], self.ev[2 * i + 1])
+        if st != 0:
+            raise SqError(-5, f"hipEventElapsedTime: {st}")
+        return ms.value
+
+    def close(self) -> None:
+        for e in self.ev:
+            self._hip.hipEventDestroy(e)
+        self.ev = []
 
 
 def run_host(ctx: Context, kr: Keyring, direction: int, batch: Batch) -> None:
