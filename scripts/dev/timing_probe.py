@@ -6,6 +6,9 @@ set, one process; interleaved rounds of STEPS launches each, timed three ways:
   ext     the pair recorded by the launch's own dispatch
           (sqobfs.DispatchEvents / sqobfs_debug_time_next_launch)
   none    launches only
+  two     launches only, alternating between two streams (each with its own
+          output buffers), so a launch's head may overlap the previous
+          one's tail
 Prints per mode the wall time per step (sync-bracketed) and the kernel
 average where events exist.  usage: timing_probe.py [ROUNDS] [STEPS]"""
 import os
@@ -37,8 +40,13 @@ lens = torch.full((n,), ln, device=dev, dtype=torch.int32)
 out = torch.empty(n * (ln + 8), device=dev, dtype=torch.uint8)
 out_len = torch.zeros(n, device=dev, dtype=torch.int32)
 b = sqobfs.make_batch(n, data, in_off, lens, out, out_off, out_len, salt)
+out2 = torch.empty_like(out)
+out_len2 = torch.zeros_like(out_len)
+b2 = sqobfs.make_batch(n, data, in_off, lens, out2, out_off, out_len2, salt)
 stream = torch.cuda.current_stream(dev)
 s = stream.cuda_stream
+side = torch.cuda.Stream(dev)
+s2 = side.cuda_stream
 ctx.unit_packets = sqobfs.unit_packets_for(n * ln, n)
 
 tev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
@@ -56,6 +64,8 @@ def run(mode):
         elif mode == "ext":
             dev_ev.arm(i)
             sqobfs.launch(ctx, kr, sqobfs.OBFUSCATE, b, s)
+        elif mode == "two" and i % 2:
+            sqobfs.launch(ctx, kr, sqobfs.OBFUSCATE, b2, s2)
         else:
             sqobfs.launch(ctx, kr, sqobfs.OBFUSCATE, b, s)
     torch.cuda.synchronize(dev)
@@ -72,7 +82,7 @@ def run(mode):
 for _ in range(80):
     sqobfs.launch(ctx, kr, sqobfs.OBFUSCATE, b, s)
 torch.cuda.synchronize(dev)
-modes = ["torch2", "ext", "none"]
+modes = ["torch2", "ext", "none", "two"]
 res = {m: [] for m in modes}
 for r in range(R):
     for m in (modes if r % 2 == 0 else modes[::-1]):
