@@ -435,7 +435,8 @@ void sqobfs_debug_fail_chunk(int chunk);
  * (sqobfs_launch / sqobfs_run_host chunk) records start_event / stop_event
  * (hipEvent_t, created with timing) with its own kernel dispatch
  * (hipExtLaunchKernel), so per-kernel times cost no marker packets between
- * kernels.  Either may be NULL; cleared by that launch. */
+ * kernels.  Either may be NULL; spent by the next sqobfs_launch call even
+ * when it launches nothing (an empty or refused batch). */
 void sqobfs_debug_time_next_launch(void *start_event, void *stop_event);
 
 /* ------------------------------------------------------------------------

@@ -781,12 +781,17 @@ int sqobfs_cpu_run(const sqobfs_keyring *kr, int dir, const sqobfs_batch *b) {
 
 int sqobfs_launch(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir, const sqobfs_batch *b,
                   void *stream) {
-  if (!ctx || !kr || kr->ctx != ctx) return SQ_EINVAL;  // (host keyrings: sqobfs_cpu_run)
-  if (dir != SQOBFS_OBFUSCATE && dir != SQOBFS_DEOBFUSCATE) return SQ_EINVAL;
+  // a launch that returns before its kernel still spends the timing hook
+  const auto unarmed = [](int r) {
+    sq_time_next_launch(nullptr, nullptr);
+    return r;
+  };
+  if (!ctx || !kr || kr->ctx != ctx) return unarmed(SQ_EINVAL);  // (host keyrings: sqobfs_cpu_run)
+  if (dir != SQOBFS_OBFUSCATE && dir != SQOBFS_DEOBFUSCATE) return unarmed(SQ_EINVAL);
   const int st = check_batch_shape(b, dir);
-  if (st != SQ_OK || b->n == 0) return st;
+  if (st != SQ_OK || b->n == 0) return unarmed(st);
   DeviceScope ds_(ctx->device);
-  if (ds_.status != SQ_OK) return ds_.status;
+  if (ds_.status != SQ_OK) return unarmed(ds_.status);
   sq::KParams kp = make_params(ctx, kr, b);
   if (kp.ppw == 0) kp.ppw = sq_unit_packets_default(b->n);
   hipStream_t s = pick_stream(ctx, stream);
