@@ -1287,6 +1287,10 @@ template <int KIND, int DIR, bool MULTI, int U, int WPB>
 static int launch_k(const KParams &P, hipStream_t s) {
   const uint64_t units = ((uint64_t)P.n + P.ppw - 1) / P.ppw;
   const uint64_t blocks = (units + WPB - 1) / WPB;
+  // HIP keeps a failed call's error until it is read: clear one left by an
+  // earlier call on this thread (the caller's), or it would be taken for
+  // this launch's and the launch reported as refused although it ran
+  (void)hipGetLastError();
   if (t_time_ev[0] || t_time_ev[1]) {
     hipEvent_t e0 = t_time_ev[0], e1 = t_time_ev[1];
     t_time_ev[0] = t_time_ev[1] = nullptr;
@@ -1357,6 +1361,7 @@ extern "C" int sq_launch_psk_prepare(int kind, const uint8_t *blob, const uint64
                                      void *stream) {
   if (count == 0) return 0;
   const uint32_t threads = 64;
+  (void)hipGetLastError();  // (a stale error is not this launch's: launch_k)
   hipLaunchKernelGGL(sq::psk_prepare_kernel, dim3((count + threads - 1) / threads),
                      dim3(threads), 0, (hipStream_t)stream, kind, blob, off, len, count, out);
   return hipGetLastError() == hipSuccess ? 0 : -3;

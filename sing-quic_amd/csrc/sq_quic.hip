@@ -1005,6 +1005,7 @@ extern "C" int sq_launch_quic(int open, const sq::QParams *qp, void *stream) {
   hipStream_t s = (hipStream_t)stream;
   const bool multi = qp->key_id != nullptr;
 #define SQ_QL(O, M, B) hipLaunchKernelGGL((quic_kernel<O, M, B>), grid, dim3(kQBlock), 0, s, *qp)
+  (void)hipGetLastError();  // (a stale error is not this launch's: sq_kernels.hip launch_k)
   if (qp->obfs) {
     if (open) { if (multi) SQ_QL(true, true, true); else SQ_QL(true, false, true); }
     else { if (multi) SQ_QL(false, true, true); else SQ_QL(false, false, true); }

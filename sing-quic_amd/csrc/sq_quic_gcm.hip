@@ -995,6 +995,7 @@ extern "C" int sq_launch_gcm_group(const uint16_t *key_id, uint32_t n, uint32_t 
   uint32_t *hist = perm + n;
   uint32_t *mt = hist + (uint64_t)bins * nch;
   *meta = mt;
+  (void)hipGetLastError();  // (a stale error is not these launches': sq_kernels.hip launch_k)
   hipLaunchKernelGGL(gcm_group_hist, dim3(nch), dim3(256), 0, s, key_id, n, bins, nch, hist);
   hipLaunchKernelGGL(gcm_group_scan, dim3(1), dim3(1024), 0, s, hist, bins * nch, n, bins, nch, mt);
   hipLaunchKernelGGL(gcm_group_scatter, dim3(nch), dim3(kWave), 0, s, key_id, n, bins, nch,
@@ -1021,6 +1022,7 @@ static int launch_gcm(const QGParams *qp, hipStream_t s) {
       resident_blocks((const void *)quic_gcm_staged_kernel<OPEN, OB>);
   const uint64_t waves = ((uint64_t)qp->n + kGPpw - 1) / kGPpw;
   const uint64_t want = (waves + kGWaves - 1) / kGWaves;
+  (void)hipGetLastError();  // (a stale error is not this launch's: sq_kernels.hip launch_k)
   if (MULTI && qp->perm) {  // grouped: every valid packet is in a step
     hipLaunchKernelGGL((quic_gcm_staged_kernel<OPEN, OB>), dim3((uint32_t)(want < cap_st ? want : cap_st)),
                        dim3(kGBlock), 0, s, *qp);

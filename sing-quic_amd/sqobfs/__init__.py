@@ -516,6 +516,7 @@ class DispatchEvents:
         ms = ctypes.c_float()
         st = self._hip.hipEventElapsedTime(ctypes.byref(ms), self.ev[2 * i], self.ev[2 * i + 1])
         if st != 0:
+            self._hip.hipGetLastError()  # (HIP keeps the error until read)
             raise SqError(-5, f"hipEventElapsedTime: {st}")
         return ms.value
 

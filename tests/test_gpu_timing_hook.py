@@ -65,3 +65,32 @@ def test_empty_batch_spends_the_hook(ctx):
                 ev.elapsed_ms(0)
     finally:
         ev.close()
+
+
+def test_stale_hip_error_is_not_the_launch_s(ctx):
+    """A failed HIP call of the caller's, left unread on this thread, is not
+    taken for the next keyring build's or launch's error."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipEventCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+    hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p,
+                                        ctypes.c_void_p]
+    hip.hipEventDestroy.argtypes = [ctypes.c_void_p]
+    a, b = ctypes.c_void_p(), ctypes.c_void_p()
+    assert hip.hipEventCreate(ctypes.byref(a)) == 0 and hip.hipEventCreate(ctypes.byref(b)) == 0
+    ms = ctypes.c_float()
+    try:
+        for kind in (SALAMANDER, XPLUS):
+            # never recorded: fails, and the error stays unread
+            assert hip.hipEventElapsedTime(ctypes.byref(ms), a, b) != 0
+            rng = np.random.Generator(np.random.PCG64(4420 + kind))
+            hb = gh.make_case(rng, kind, OBFUSCATE, rng.integers(0, 1500, 3000), PSK)
+            ref = gh.run_oracle(kind, OBFUSCATE, PSK, hb)
+            with sqobfs.Keyring(ctx, kind, PSK) as kr:
+                assert hip.hipEventElapsedTime(ctypes.byref(ms), a, b) != 0
+                gh.run_device(ctx, kr, OBFUSCATE, hb)
+            gh.assert_same(hb, ref, f"after a stale error kind={kind}")
+    finally:
+        hip.hipGetLastError()
+        hip.hipEventDestroy(a)
+        hip.hipEventDestroy(b)
