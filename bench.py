@@ -67,7 +67,7 @@ def parse():
                          "trip per step)")
     ap.add_argument("--unit-packets", type=int, default=0,
                     help="obfuscation kernel unit size, packets per wavefront (0 = sized "
-                         "from the batch's bytes by sqobfs_unit_packets_for, as a caller "
+                         "from the batch's bytes by sqobfs_unit_packets_for_kind, as a caller "
                          "that built the batch does)")
     ap.add_argument("--warmup-s", type=float, default=0.15,
                     help="keep warming up (untimed) until this much wall time has passed "
@@ -507,7 +507,7 @@ def inproc_bench(args):
         # blocking wake-up (~80 us) after every step
         c.set_sync_spin(4000)
         c.unit_packets = args.unit_packets or sqobfs.unit_packets_for(
-            sh["payload_bytes"], n_k, n_psk > 1)
+            sh["payload_bytes"], n_k, n_psk > 1, kind)
         kr = sqobfs.Keyring(c, kind, sh["psks"])
         ctxs.append(c)
         krs.append(kr)
@@ -634,7 +634,7 @@ def main():
     ctx = sqobfs.Context(gpu)
     kr = sqobfs.Keyring(ctx, kind, sh["psks"])
     ctx.unit_packets = args.unit_packets or sqobfs.unit_packets_for(
-        sh["payload_bytes"], n, n_psk > 1)
+        sh["payload_bytes"], n, n_psk > 1, kind)
     stream = torch.cuda.current_stream(dev)
     s = stream.cuda_stream
 
@@ -793,8 +793,9 @@ def main():
             "unit_order": ("XCD-contiguous" if -(-n // ctx.unit_packets) >= 1 << 18
                            else "dispatch order"),
             "unit_rule": ("--unit-packets" if args.unit_packets else
-                          "sqobfs_unit_packets_for(payload bytes, n): ~21.7 KB per wavefront "
-                          "(31.5 KB with a multi-PSK keyring; at least 2,048 wavefronts)"),
+                          "sqobfs_unit_packets_for_kind(kind, payload bytes, n): ~21.7 KB per "
+                          "wavefront (XPlus 19.5 KB; 31.5 KB with a multi-PSK keyring; at least "
+                          "2,048 wavefronts)"),
             "parallelism": f"shard{world} (independent packets, no collective)",
         },
         "roofline": {

@@ -203,6 +203,10 @@ uint32_t sqobfs_unit_packets(const sqobfs_ctx *ctx);
  * select keyring entries (psk_id != NULL), at least 2,048 wavefronts for
  * small batches, clamped to 1 .. 62. */
 uint32_t sqobfs_unit_packets_for(uint64_t bytes, uint32_t n, int multi_psk);
+/* The same for the keyring kind's kernel: XPlus with one PSK streams best at
+ * ~19.5 KB per wavefront (16 packets of 1,200 B); Salamander as above
+ * (sqobfs_unit_packets_for is this with SQOBFS_SALAMANDER). */
+uint32_t sqobfs_unit_packets_for_kind(int kind, uint64_t bytes, uint32_t n, int multi_psk);
 
 /* Upload `count` pre-shared keys (host memory: psk k = blob[off[k] .. +len[k]])
  * and derive each one's per-PSK hash state on the GPU.  kind selects the

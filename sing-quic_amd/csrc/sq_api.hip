@@ -578,8 +578,14 @@ int sqobfs_set_unit_packets(sqobfs_ctx *ctx, uint32_t packets) {
 }
 
 uint32_t sqobfs_unit_packets_for(uint64_t bytes, uint32_t n, int multi_psk) {
+  return sqobfs_unit_packets_for_kind(SQOBFS_SALAMANDER, bytes, n, multi_psk);
+}
+
+uint32_t sqobfs_unit_packets_for_kind(int kind, uint64_t bytes, uint32_t n, int multi_psk) {
   if (n == 0) return sq::kDefaultUnitPackets;
-  const uint64_t target = multi_psk ? sq::kUnitBytesMultiPsk : sq::kUnitBytes;
+  const uint64_t target = multi_psk ? sq::kUnitBytesMultiPsk
+                          : kind == SQOBFS_XPLUS ? sq::kUnitBytesXPlus
+                                                 : sq::kUnitBytes;
   const uint64_t u = bytes ? target * n / bytes : sq::kMaxUnitPackets;  // floor(target / mean)
   // and at least kMinUnits wavefronts for small batches
   const uint64_t spread = ((uint64_t)n + sq::kMinUnits - 1) / sq::kMinUnits;
@@ -1399,7 +1405,7 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
       if (kp.ppw == 0) {  // lengths are on the host: size the units by bytes
         uint64_t bytes = 0;
         for (uint32_t i = ri.p0; i < ri.p1; i++) bytes += hb->in_len[i];
-        kp.ppw = sqobfs_unit_packets_for(bytes, db.n, hb->psk_id != nullptr);
+        kp.ppw = sqobfs_unit_packets_for_kind(kr->kind, bytes, db.n, hb->psk_id != nullptr);
       }
       int fc = (int)c;
       st = g_fail_chunk.compare_exchange_strong(fc, -1) ? SQ_EDEVICE

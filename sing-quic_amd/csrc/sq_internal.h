@@ -24,6 +24,9 @@ constexpr uint32_t kMaxUnitPackets = 62;
 // in both directions; 24 -- ~32 KB, consecutive waves' spans close to a
 // power of two apart -- the slowest point on two of the three boxes.)
 constexpr uint64_t kUnitBytes = 21700, kUnitBytesMultiPsk = 31500;
+// XPlus with one PSK: 16 packets of 1,200 B beat 18 by 0.7-1.7 % in both
+// directions on three boxes (unit size)
+constexpr uint64_t kUnitBytesXPlus = 19500;
 // ... but at least this many wavefronts per launch when the batch is small
 // (latency: a socket batch of 256 datagrams runs as 256 one-packet waves)
 constexpr uint32_t kMinUnits = 2048;

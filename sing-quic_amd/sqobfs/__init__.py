@@ -208,6 +208,9 @@ def load(path: str) -> ctypes.CDLL:
     L.sqobfs_unit_packets.restype = ctypes.c_uint32
     L.sqobfs_unit_packets_for.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int]
     L.sqobfs_unit_packets_for.restype = ctypes.c_uint32
+    L.sqobfs_unit_packets_for_kind.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32,
+                                               ctypes.c_int]
+    L.sqobfs_unit_packets_for_kind.restype = ctypes.c_uint32
     if not hasattr(L, "sqobfs_pconn_open"):
         return L  # an older build (dev A/B against earlier rounds' libraries)
     L.sqobfs_set_sync_spin.argtypes = [vp, u32]
@@ -242,10 +245,11 @@ def load(path: str) -> ctypes.CDLL:
     return L
 
 
-def unit_packets_for(total_bytes: int, n: int, multi_psk: bool = False) -> int:
+def unit_packets_for(total_bytes: int, n: int, multi_psk: bool = False,
+                     kind: int = SALAMANDER) -> int:
     """Unit size (packets per wavefront) for a batch of n packets holding
-    total_bytes bytes: sqobfs_unit_packets_for."""
-    return lib().sqobfs_unit_packets_for(total_bytes, n, int(multi_psk))
+    total_bytes bytes, for the kind's kernel: sqobfs_unit_packets_for_kind."""
+    return lib().sqobfs_unit_packets_for_kind(kind, total_bytes, n, int(multi_psk))
 
 
 def build_info() -> str:

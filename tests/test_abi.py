@@ -107,7 +107,9 @@ def test_unit_packets_for_sizes_units_by_bytes():
     (DESIGN.md section 5)."""
     f = sqobfs.unit_packets_for
     assert f(1350 << 20, 1 << 20) == 16          # configs[1]
-    assert f(1200 << 20, 1 << 20) == 18          # configs[2]
+    assert f(1200 << 20, 1 << 20) == 18          # (Salamander rule at 1,200 B)
+    assert f(1200 << 20, 1 << 20, kind=sqobfs.XPLUS) == 16  # configs[2]
+    assert f(1200 << 20, 1 << 20, True, sqobfs.XPLUS) == 26  # multi-PSK XPlus: 31.5 KB
     assert f(758 * (4 << 20), 4 << 20) == 28     # configs[3] (mean of U[64, 1452])
     assert f(1350 * (16 << 20), 16 << 20, True) == 23  # configs[4]
     assert f(64 * 100_000, 100_000) == 49 and f(0, 1 << 20) == 62

@@ -69,7 +69,7 @@ def _full_parity(config: str, layout: str = "dense", n=None, L="config", rank=0,
     h_ids = _host(sh["psk_id"])
     h_ids = None if h_ids is None else h_ids.view(np.uint16)
     with sqobfs.Context(0) as ctx, sqobfs.Keyring(ctx, kind, sh["psks"]) as kr:
-        ctx.unit_packets = sqobfs.unit_packets_for(sh["payload_bytes"], n, n_psk > 1)
+        ctx.unit_packets = sqobfs.unit_packets_for(sh["payload_bytes"], n, n_psk > 1, kind)
         # -------- obfuscate: every datagram vs the restatement
         b = sqobfs.make_batch(n, sh["data"], sh["in_off"], lens, sh["out"], sh["out_off"],
                               sh["out_len"], sh["salt"], sh["psk_id"], flags=flags)
