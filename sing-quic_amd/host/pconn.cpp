@@ -431,7 +431,12 @@ void task_end(sqobfs_pconn *pc, int d, bool more, int64_t due = 0) {
       // no wake-up: the calling worker goes back to the run queue next and
       // takes it itself.  Waking another worker for it made every batch a
       // hand-off between two threads (a futex wake and a context switch per
-      // batch), which kept batches small at high rates.
+      // batch), which kept batches small at high rates (waking
+      // one only when other tasks wait ahead brought that back: the tx and
+      // rx tasks of a busy pair of conns are queued together most of the
+      // time).  No task starves: a sleeping worker means the queue was empty
+      // when it slept, and every task queued since came with a wake-up or,
+      // like this one, with the worker that queued it.
       E->runq.push_back({pc, d});
     }
     return;
