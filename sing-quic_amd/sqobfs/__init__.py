@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 import re
 from dataclasses import dataclass
 
@@ -138,6 +139,15 @@ def lib() -> ctypes.CDLL:
 def load(path: str) -> ctypes.CDLL:
     """A libsqobfs build at `path` with its prototypes declared (lib() loads
     the in-tree one; dev A/B scripts load timing variants side by side)."""
+    # torch (the device-memory plumbing of the tests and the bench) first,
+    # where it is installed: its wheel carries its own HIP runtime, which the
+    # library then shares; loaded after the library, torch would bring a
+    # second runtime that finds no GPU (INTEGRATION.md)
+    if "torch" not in sys.modules:
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     L = ctypes.CDLL(path)
     vp, u32, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
     L.sqobfs_abi_version.restype = i32
