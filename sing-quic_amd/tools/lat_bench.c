@@ -379,16 +379,16 @@ int main(void) {
    * thread (the Go Conn's WriteTo callers), one reader thread; without and
    * with UDP GSO (A) / GRO (B); with the engine's routing (defaults), every
    * batch launched (_gpu_only), every batch on the CPU path (_cpu_only) and
-   * on the host engine (_no_device); the defaults again last (order
-   * effects) */
+   * on the host engine (_no_device), with batches held up to 20 us for more
+   * datagrams (_linger20); the defaults again last (order effects) */
   {
     sqobfs_keyring *hk;
     uint64_t o0 = 0;
     uint32_t l0 = PL;
     CHECK(sqobfs_keyring_create(NULL, SQOBFS_SALAMANDER, 1, PSK, &o0, &l0, &hk));
     static const char *const modes[] = {"", "_gpu_only", "_cpu_only", "_no_device",
-                                        "_defaults_again"};
-    for (int m = 0; m < 5; m++)
+                                        "_linger20", "_defaults_again"};
+    for (int m = 0; m < 6; m++)
       for (int off = 0; off < 2; off++) {
         sqobfs_ctx *const c = m == 3 ? NULL : ctx;
         sqobfs_keyring *const k = m == 3 ? hk : kr;
@@ -402,6 +402,7 @@ int main(void) {
         ob.flags = off ? SQOBFS_UDP_RX_GRO : 0u;
         if (m == 1) oa.cpu_max = ob.cpu_max = oa.inline_gap_us = ob.inline_gap_us = SQOBFS_PCONN_NEVER;
         if (m == 2) oa.cpu_max = ob.cpu_max = 1u << 30;
+        if (m == 4) oa.linger_us = ob.linger_us = 20;
         CHECK(sqobfs_pconn_open(c, k, fa, &oa, &A));
         CHECK(sqobfs_pconn_open(c, k, fb, &ob, &B));
         const sqobfs_addr to = loop_addr(pb);
