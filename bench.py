@@ -596,19 +596,99 @@ def quic_valu_roofline(suite_name: str, op: str, kernel_us: float):
     return None
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` (N > 1) run as a bare command: start the N rank
+    processes here, one per GPU, as children of this one, each with the
+    torch.distributed.run environment (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR 127.0.0.1 / MASTER_PORT).  This process never touches the GPU
+    (torch.cuda.device_count() does not initialise HIP on this image) and
+    never re-execs: it waits for the ranks, relays rank 0's one JSON line to
+    stdout and every rank's stderr to stderr, and exits non-zero when any rank
+    fails (the others are stopped, so a rank stuck in a barrier cannot hang
+    the job).  The torchrun form (WORLD_SIZE set) does not come here."""
+    import signal
+    import subprocess
+    import tempfile
+    import torch
+    ndev = torch.cuda.device_count()
+    if args.gpus > ndev and args.dist_backend != "gloo":
+        print(f"bench.py: --gpus {args.gpus} but {ndev} GPU(s) visible; one rank per GPU "
+              f"(--dist-backend gloo lets ranks share a GPU, tests only)", file=sys.stderr)
+        return 2
+    port = free_port()
+    procs, outs = [], []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        out = tempfile.TemporaryFile(mode="w+")
+        outs.append(out)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env, stdout=out, start_new_session=True))
+    failed = None
+    try:
+        while any(p.poll() is None for p in procs):
+            bad = [i for i, p in enumerate(procs) if p.returncode not in (None, 0)]
+            if bad:
+                failed = bad[0]
+                break
+            time.sleep(0.05)
+    finally:
+        if failed is not None or any(p.poll() is None for p in procs):
+            # a failed rank leaves the others in a collective: give them a
+            # moment, then stop their process groups
+            deadline = time.time() + 15
+            while time.time() < deadline and any(p.poll() is None for p in procs):
+                time.sleep(0.1)
+            for p in procs:
+                if p.poll() is None:
+                    os.killpg(p.pid, signal.SIGTERM)
+            for p in procs:
+                try:
+                    p.wait(timeout=10)
+                except subprocess.TimeoutExpired:
+                    os.killpg(p.pid, signal.SIGKILL)
+                    p.wait()
+    rcs = [p.returncode for p in procs]
+    for r, out in enumerate(outs):
+        out.seek(0)
+        text = out.read()
+        if r == 0:
+            for line in text.splitlines():
+                if line.startswith("{"):
+                    print(line, flush=True)
+                else:
+                    print(line, file=sys.stderr)
+        elif text.strip():
+            print(f"[rank {r} stdout]\n{text}", file=sys.stderr)
+    if any(rc != 0 for rc in rcs):
+        print(f"bench.py: rank exit codes {rcs}", file=sys.stderr)
+        rc = next(rc for rc in rcs if rc != 0)
+        return rc if rc > 0 else 1  # a rank killed by a signal
+    return 0
+
+
 def main():
     args = parse()
     if args.inproc:
         return inproc_bench(args)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}")
     import torch
     import sqobfs
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
     dist = None
     ndev = torch.cuda.device_count()
     assert ndev > 0, "bench.py needs a GPU"
@@ -1359,4 +1439,4 @@ def udp_rate(sqobfs, ctx, kr, kind, L, seconds=3.0, batch=256, nsock=4, offload=
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

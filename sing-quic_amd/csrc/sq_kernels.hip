@@ -63,15 +63,9 @@ namespace sq {
 #ifndef SQ_U
 #define SQ_U 4
 #endif
-// Minimum waves per SIMD the register allocation must allow (0 = no bound).
-#ifndef SQ_MINW
-#define SQ_MINW 0
-#endif
-// Timing-only ablation builds (never the shipped .so): bit 0 skips the key
-// derivation, bit 1 skips the byte-exact stores, bit 3 skips the image
-// windows' loads.
-#ifndef SQ_ABLATE
-#define SQ_ABLATE 0
+// Wavefronts per workgroup (see kWavesPerGroup).
+#ifndef SQ_WPB
+#define SQ_WPB 2
 #endif
 // 1: the first packet of a unit gives the blocks it owns in the 64-byte line
 // its output starts in to the previous unit's wave (which holds it as its
@@ -88,11 +82,6 @@ namespace sq {
 // Flat blocks a unit's block map covers (its role bytes live in LDS).
 #ifndef SQ_MAPBLK
 #define SQ_MAPBLK 4096
-#endif
-// 1: deobfuscate reads the salt with the head window (one round trip after
-// the descriptor instead of two); 0: a dependent salt load first (round 2)
-#ifndef SQ_SALTWIN
-#define SQ_SALTWIN 1
 #endif
 // 1: multi-PSK kernels load each lane's keyring entry (chaining value and
 // first message block) right after the descriptor, so the gather overlaps
@@ -131,8 +120,8 @@ constexpr uint64_t kXcdMinUnits = 1u << 18;
 #define SQ_STR(x) SQ_STR2(x)
 extern "C" const char *sqobfs_build_info(void) {
   return "gfx950 obfs_kernel U=" SQ_STR(SQ_U) " default_ppw=" SQ_STR(SQ_PPW) " NT=" SQ_STR(SQ_NT)
-         " minw=" SQ_STR(SQ_MINW) " wpb=2"
-         " ablate=" SQ_STR(SQ_ABLATE) " donate=" SQ_STR(SQ_DONATE) " align=" SQ_STR(SQ_ALIGN)
+         " wpb=" SQ_STR(SQ_WPB)
+         " donate=" SQ_STR(SQ_DONATE) " align=" SQ_STR(SQ_ALIGN)
          " map=" SQ_STR(SQ_MAPBLK)
          " windows=buffer earlysalt=1 dppred=1 xcd=" SQ_STR(SQ_XCD);
 }
@@ -364,13 +353,8 @@ __device__ __forceinline__ void finalize_desc(const KParams &P, uint32_t p, bool
   } else if (KIND == 1 && len < S) {
     olen = 0;  // xplus.go:50-52: dropped as empty
   } else {  // deobfuscate: salt = first S wire bytes
-#if !SQ_SALTWIN
-    uint32_t w[4];
-    load_window(in_base, in_base + S, in_base, w);
-#pragma unroll
-    for (uint32_t k = 0; k < S / 4; k++) salt[k] = w[k];
-#endif
-    // (SQ_SALTWIN: the salt comes with the head window, fetch_windows)
+    // (read with the head window, fetch_windows: one round trip after the
+    // descriptor instead of two)
     J = {in_base + S, out_base, (uint64_t)cap - S, 0};
     olen = len - S;
     do_hash = true;
@@ -494,11 +478,6 @@ __device__ __forceinline__ void derive_key(bool do_hash, const PskEntry *E, cons
                                            const uint32_t (&salt)[4], uint32_t (&key)[8]) {
 #pragma unroll
   for (int i = 0; i < 8; i++) key[i] = 0u;
-  if (SQ_ABLATE & 1) {
-    key[0] = salt[0];
-    key[1] = salt[1];
-    do_hash = false;
-  }
   if (do_hash) {
     if (HOT) {
       if (KIND == 0) salamander_key_hot(H, E, salt, key);
@@ -584,7 +563,7 @@ __device__ __forceinline__ WinAddr window_addrs(const PacketJob &J, bool wire_sa
   const uint64_t hw = !ne ? 0ull : (J.len < 32 - J.pre ? J.len : 32 - J.pre);
   const uint64_t B = J.src_pay & ~15ull, e = J.src_pay + hw;
   const bool c_h0 = hw != 0, c_h1 = c_h0 && e > B + 16, c_h2 = c_h0 && e > B + 32;
-  const bool c_s0 = SQ_SALTWIN && DIR == 1 && c_h0 && wire_salt && (J.src_pay & 15) < S;
+  const bool c_s0 = DIR == 1 && c_h0 && wire_salt && (J.src_pay & 15) < S;
   const bool c_t0 = ne && tail_from_window(rs, re);
   const uint64_t ta = J.src_pay + ((re & ~15ull) - J.dst_pay), te = J.src_pay + J.len;
   const uint64_t TB = ta & ~15ull;
@@ -605,12 +584,6 @@ __device__ __forceinline__ WinAddr window_addrs(const PacketJob &J, bool wire_sa
 // tail block follows its head.
 template <int DIR, uint32_t S>
 __device__ __forceinline__ void fetch_windows(const PacketJob &J, bool wire_salt, Windows &W) {
-  if (SQ_ABLATE & 8) {
-    const u32x4 z = {0u, 0u, 0u, 0u};
-    W.h0 = W.h1 = W.h2 = W.t0 = W.t1 = W.s0 = z;
-    W.rl = 0u;
-    return;
-  }
   const WinAddr A = window_addrs<DIR, S>(J, wire_salt);
   const uint64_t first = (A.need & kWinS0) ? A.s0 : A.h0;
   const uint64_t lo0 = wave_ext64_dpp<false>(A.need ? first : ~0ull);
@@ -886,7 +859,7 @@ __device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
   else  // (obfuscate loads no salt block)
     asm volatile("" ::"v"(W.h0), "v"(W.h1), "v"(W.h2), "v"(W.t0), "v"(W.t1));
   const u32x4 wh0 = W.h0, wh1 = W.h1, wh2 = W.h2;
-  if (SQ_SALTWIN && DIR == 1) {  // the wire salt, from the head window
+  if (DIR == 1) {  // the wire salt, from the head window
     const u32x4 ws0 = W.s0;
     const uint32_t w[12] = {ws0.x, ws0.y, ws0.z, ws0.w, wh0.x, wh0.y,
                             wh0.z, wh0.w, wh1.x, wh1.y, wh1.z, wh1.w};
@@ -946,7 +919,7 @@ __device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
   for (int j = 0; j < 4; j++) hn[j] = shfl32(hi[j], nl);
 
   // byte-exact stores of the bytes no datagram pair covers whole
-  if (!(SQ_ABLATE & 2) && owner && G.ne) {
+  if (owner && G.ne) {
     if ((rs & 15) && !G.pfull && !G.obh) {
       const uint64_t lend = re < G.B0 ? re : G.B0;
       const uint32_t v[4] = {hi[0], hi[1], hi[2], hi[3]};
@@ -1128,11 +1101,7 @@ __device__ __noinline__ void stream_generic(const WaveLds &L, uint32_t cst, uint
 
 // WPB: wavefronts per workgroup (independent units; they share nothing).
 template <int KIND, int DIR, bool MULTI, int U, int WPB>
-#if SQ_MINW
-__global__ __launch_bounds__(WPB * kWave, SQ_MINW) void obfs_kernel(const KParams P) {
-#else
 __global__ __launch_bounds__(WPB * kWave) void obfs_kernel(const KParams P) {
-#endif
   __shared__ WaveLds lds[WPB];
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wv = threadIdx.x / kWave;
@@ -1277,7 +1246,7 @@ __global__ void psk_prepare_kernel(int kind, const uint8_t *blob, const uint64_t
 // 1.5 % of it for every kernel and direction (Salamander obfuscate 2.6 %
 // faster than 4-wave groups, XPlus obfuscate 3.4 % faster than 1-wave ones).
 template <int KIND, int DIR>
-constexpr int kWavesPerGroup = 2;
+constexpr int kWavesPerGroup = SQ_WPB;
 
 // sqobfs_debug_time_next_launch: events the calling thread's next launch
 // records with its own dispatch (no marker packets between kernels)

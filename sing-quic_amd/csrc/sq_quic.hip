@@ -22,7 +22,7 @@
 //   3. owner lane: the partials combined with powers of r, the tag, and
 //      (seal) the header-protection mask from the ciphertext sample.
 // The owner phases' ChaCha20 blocks are shared by lanes l and l + 32
-// (SQ_QSPLIT).  Payloads past the cooperative range are walked by their
+// (lane pairs).  Payloads past the cooperative range are walked by their
 // owner lane with a streaming realigner (payload_pass): aligned 16-byte
 // loads one step ahead, realigned in registers, aligned 16-byte stores.
 #include <hip/hip_runtime.h>
@@ -35,12 +35,6 @@
 
 namespace sq {
 
-#ifndef SQ_QABLATE
-#define SQ_QABLATE 0  // timing builds only (never the shipped .so)
-#endif
-#ifndef SQ_QPREFETCH
-#define SQ_QPREFETCH 0  // 1: load the next cooperative step's input one step ahead (measured 2 % slower)
-#endif
 // Threads per workgroup.  Its waves share nothing, and a workgroup's slots
 // free only when all of its waves have ended: 1-wave groups measured 1.3 %
 // (seal) and 1.0 % (open) faster than 4-wave ones, 3 interleaved passes.
@@ -71,21 +65,13 @@ constexpr uint32_t kQPpw = SQ_QPPW;
 #endif
 constexpr uint32_t kQCoopMax = SQ_QCOOPMAX;  // payloads up to this size take the cooperative pass
 constexpr uint32_t kQMaxBlk = kQPpw * (kQCoopMax / 64);
-// Pairs (SQ_QPAIR): every packet's flat blocks start at an even index, and
-// the even lane of each pair of lanes folds its neighbour's partial MAC into
-// its own (P_b r^k + P_b+1, k = the chunks of block b+1), so LDS holds one
-// partial per two blocks: 13 KB per wave instead of 20 KB, 12 waves per CU
-// instead of 8.
-#ifndef SQ_QPAIR
-#define SQ_QPAIR 1
-#endif
+// Pairs: every packet's flat blocks start at an even index, and the even
+// lane of each pair of lanes folds its neighbour's partial MAC into its own
+// (P_b r^k + P_b+1, k = the chunks of block b+1), so LDS holds one partial
+// per two blocks: 13 KB per wave instead of 20 KB, 12 waves per CU instead of
+// 8.
 static_assert((kQCoopMax / 64) % 2 == 0, "pairs: a packet's padded block count stays in range");
-static_assert(!(SQ_QPAIR && SQ_QPREFETCH), "the prefetching loop is not paired");
-// Junction stores (coop_block; the paired loop only)
-#ifndef SQ_QJUNC
-#define SQ_QJUNC 1
-#endif
-constexpr uint32_t kQParts = SQ_QPAIR ? kQMaxBlk / 2 : kQMaxBlk;
+constexpr uint32_t kQParts = kQMaxBlk / 2;
 
 // ---------------------------------------------------------------- Poly1305
 
@@ -140,12 +126,6 @@ __device__ __forceinline__ void poly_block(Poly &P, const uint32_t (&m)[4]) {
   poly_mul(P);
 }
 
-// multiplier := h of X (a power of r), with its 5x terms
-__device__ __forceinline__ void poly_set_r(Poly &P, const Poly &X) {
-  P.r0 = X.h0; P.r1 = X.h1; P.r2 = X.h2; P.r3 = X.h3; P.r4 = X.h4;
-  P.s1 = P.r1 * 5; P.s2 = P.r2 * 5; P.s3 = P.r3 * 5; P.s4 = P.r4 * 5;
-}
-
 // tag = (h mod p) + s mod 2^128, s = otk[16..32)
 __device__ __forceinline__ void poly_finish(Poly &P, const uint32_t (&otk)[16],
                                             uint32_t (&tag)[4]) {
@@ -184,22 +164,11 @@ __device__ __forceinline__ void quic_nonce(const QuicKeyDev &K, uint64_t pn, uin
   quic_nonce_iv(K.iv, pn, n);
 }
 
-// 5 mask bytes (RFC 9001 5.4.4): ChaCha20(hp, counter = sample[0..4),
-// nonce = sample[4..16)) of zeros; returned as words (bytes 0..3, byte 4)
-__device__ __forceinline__ void hp_mask(const QuicKeyDev &K, const uint32_t (&sample)[4],
-                                        uint32_t &m0, uint32_t &m1) {
-  const uint32_t nonce[3] = {sample[1], sample[2], sample[3]};
-  uint32_t blk[16];
-  chacha20_block(K.hp, sample[0], nonce, blk);
-  m0 = blk[0];
-  m1 = blk[1] & 0xFFu;
-}
-
 // ------------------------------------------------- lane-pair ChaCha20 blocks
 // The owner phases run one ChaCha20 block per packet at a time (the Poly1305
 // key block; the header-protection mask block) on the 32 owner lanes while
 // lanes 32-63 idle, and a wave instruction costs the same whatever its exec
-// mask.  Lane pairs (SQ_QSPLIT): owner lane l and lane l + 32 share the
+// mask.  Lane pairs: owner lane l and lane l + 32 share the
 // block.  The low lane holds state columns 0-1, the high lane columns 2-3
 // (4 x 4 state, words x0..x15 row-major, RFC 8439 2.3).  The column round
 // is local; the diagonal round runs on the pair's diagonals after a swap of
@@ -207,10 +176,7 @@ __device__ __forceinline__ void hp_mask(const QuicKeyDev &K, const uint32_t (&sa
 // c = (c0', c1'), d = (d1', d0), where ' is the partner's) and swaps 4 back
 // after it.  Per lane 40 quarter rounds and 80 word swaps instead of 80
 // quarter rounds.
-#ifndef SQ_QSPLIT
-#define SQ_QSPLIT 1
-#endif
-static_assert(!SQ_QSPLIT || kQPpw == kWave / 2, "lane pairs are lanes l and l + 32");
+static_assert(kQPpw == kWave / 2, "lane pairs are lanes l and l + 32");
 
 // the partner lane's x (lane l <-> lane l + 32); every lane must be active
 __device__ __forceinline__ uint32_t xhalf(uint32_t x, bool hi) {
@@ -276,16 +242,13 @@ template <bool MULTI>
 __device__ __forceinline__ void hp_mask_lanes(const QuicKeyDev *K, const uint32_t (&sample)[4],
                                               bool live, uint32_t lane, uint32_t &m0,
                                               uint32_t &m1) {
-#if SQ_QSPLIT
+  (void)live;
   const bool hi = lane >= kWave / 2;
   const QuicKeyDev *KP = MULTI ? xlow_ptr(K, hi) : K;
   uint32_t o[8];
   chacha20_pair(KP->hp, sample[0], sample[1], sample[2], sample[3], hi, o);
   m0 = o[0];
   m1 = o[1] & 0xFFu;
-#else
-  if (live) hp_mask(*K, sample, m0, m1);
-#endif
 }
 
 // The Poly1305 one-time key, otk[0..8) = ChaCha20(key, 0, nonce) words 0-7,
@@ -293,7 +256,7 @@ __device__ __forceinline__ void hp_mask_lanes(const QuicKeyDev *K, const uint32_
 template <bool MULTI>
 __device__ __forceinline__ void otk_lanes(const QuicKeyDev *K, const uint32_t (&nonce)[3],
                                           bool live, uint32_t lane, uint32_t (&otk)[16]) {
-#if SQ_QSPLIT
+  (void)live;
   const bool hi = lane >= kWave / 2;
   const QuicKeyDev *KP = MULTI ? xlow_ptr(K, hi) : K;
   uint32_t o[8];
@@ -306,9 +269,6 @@ __device__ __forceinline__ void otk_lanes(const QuicKeyDev *K, const uint32_t (&
   otk[5] = o[3];
   otk[6] = xhalf(o[2], hi);
   otk[7] = xhalf(o[3], hi);
-#else
-  if (live) chacha20_block(K->key, 0, nonce, otk);
-#endif
 }
 
 // Payload pass shared by seal (MAC over the output) and open (MAC over the
@@ -337,11 +297,7 @@ __device__ __forceinline__ void payload_pass(const QuicKeyDev &K, const uint32_t
   // address is clamped so the load is unconditional (no branch, exact waits)
   auto load_blk = [&](uint32_t i, uint32_t (&v)[4]) {
     const uint64_t A = S0 + 16ull * i;
-#if SQ_QABLATE  // timing-only: no payload loads
-    const u32x4 x = {(uint32_t)A, 1u, 2u, 3u};
-#else
     const u32x4 x = gld<u32x4>(A < last ? A : last);
-#endif
     const bool ok = A <= last;
     v[0] = ok ? x.x : 0u; v[1] = ok ? x.y : 0u; v[2] = ok ? x.z : 0u; v[3] = ok ? x.w : 0u;
   };
@@ -388,12 +344,8 @@ __device__ __forceinline__ void payload_pass(const QuicKeyDev &K, const uint32_t
         funnel(prev_c, c, 16 - oa, blk);
         const uint32_t lo = j == 0 ? oa : 0u;
         const uint32_t hi = oa + len - 16 * j < 16 ? oa + len - 16 * j : 16u;
-#if SQ_QABLATE  // timing-only: keep the values, store only the last
-        if (j + 1 == nchunk) store_partial(D0 + 16ull * j, blk, lo, hi);
-#else
         if (lo == 0 && hi == 16) gst<u32x4>(D0 + 16ull * j, u32x4{blk[0], blk[1], blk[2], blk[3]});
         else store_partial(D0 + 16ull * j, blk, lo, hi);
-#endif
 #pragma unroll
         for (int w = 0; w < 4; w++) prev_c[w] = c[w];
       }
@@ -467,7 +419,7 @@ __device__ __forceinline__ void coop_load(const QRec &R, uint32_t b, uint32_t (&
   }
 }
 
-// Junctions (SQ_QJUNC): the aligned output block a lane shares with the lane
+// Junctions: the aligned output block a lane shares with the lane
 // holding the packet's next keystream block is written whole, once, by the
 // later lane (its head bytes OR the earlier lane's tail bytes, over a lane
 // shuffle) instead of as two byte-exact partial stores.  merge_head: this
@@ -717,7 +669,7 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
   const uint32_t nblk = coop ? (pl + 63) / 64 : 0u;
   // chunks of the last block (1..4) and, for pairs, r^2..r^4
   const uint32_t klast = nblk ? ((pl - 64 * (nblk - 1)) + 15) / 16 : 1u;
-  const uint32_t nflat = SQ_QPAIR ? (nblk + 1) & ~1u : nblk;
+  const uint32_t nflat = (nblk + 1) & ~1u;
   uint32_t incl = nflat;
 #pragma unroll
   for (int d = 1; d < kWave; d <<= 1) {
@@ -736,7 +688,7 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
 #pragma unroll
     for (int i = 0; i < 3; i++) R.nonce[i] = nonce[i];
     R.r[0] = P.r0; R.r[1] = P.r1; R.r[2] = P.r2; R.r[3] = P.r3; R.r[4] = P.r4;
-    if (SQ_QPAIR && nblk) {
+    if (nblk) {
       // X.h = r^k for k = 2, 3, 4 (X.r = r)
       Poly X = P;
       X.h0 = P.r0; X.h1 = P.r1; X.h2 = P.r2; X.h3 = P.r3; X.h4 = P.r4;
@@ -764,33 +716,6 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
   // ---- 2. cooperative payload pass over the flat block space
-#if SQ_QPREFETCH
-  // the next step's input is loaded while this step's ChaCha20 block runs
-  uint32_t f = lane, pp = T ? q_locate(start, 0, f < T ? f : T - 1) : 0u, blk[5][4];
-  if (f < T) coop_load(recs[wv][pp], f - recs[wv][pp].start, blk);
-  for (uint32_t base = 0; base < T; base += kWave) {
-    const uint32_t fn = base + kWave + lane;
-    uint32_t ppn = 0, nblk5[5][4];
-    if (base + kWave < T) {
-      ppn = q_locate(start, base + kWave, fn < T ? fn : T - 1);
-      if (fn < T) coop_load(recs[wv][ppn], fn - recs[wv][ppn].start, nblk5);
-    }
-    if (f < T) {
-      QRec &R = recs[wv][pp];
-      const QuicKeyDev &KB = MULTI ? Q.keys[R.kid] : Q.key0;
-      uint32_t c5[5], h4[4], t4[4];
-      coop_block<OPEN, OB>(KB, R, f - R.start, blk, c5, false, false, h4, t4);
-#pragma unroll
-      for (int i = 0; i < 5; i++) parts[wv][f][i] = c5[i];
-    }
-    f = fn;
-    pp = ppn;
-#pragma unroll
-    for (int i = 0; i < 5; i++)
-#pragma unroll
-      for (int w = 0; w < 4; w++) blk[i][w] = nblk5[i][w];
-  }
-#elif SQ_QPAIR
   for (uint32_t base = 0; base < T; base += kWave) {
     const uint32_t f = base + lane;
     const uint32_t pp = q_locate(start, base, f < T ? f : T - 1);
@@ -807,22 +732,20 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
       // end inside it: the tag or another packet's bytes follow)
       const uint32_t oa = (uint32_t)(R.dst & 15);
       const uint32_t rem = R.pl - 64 * b, rem1 = rem > 64 ? rem - 64 : 0u;
-      mh = SQ_QJUNC && b > 0 && lane > 0 && oa + (rem < 64 ? rem : 64u) >= 16;
-      const bool gt = SQ_QJUNC && b + 1 < R.nblk && lane + 1 < kWave &&
+      mh = b > 0 && lane > 0 && oa + (rem < 64 ? rem : 64u) >= 16;
+      const bool gt = b + 1 < R.nblk && lane + 1 < kWave &&
                       oa + (rem1 < 64 ? rem1 : 64u) >= 16;
       jaddr = R.dst + 64ull * b - oa;
       uint32_t blk[5][4];
       coop_load(R, b, blk);
       coop_block<OPEN, OB>(KB, R, b, blk, c5, mh, gt, h4, t4);
     }
-#if SQ_QJUNC
     {  // the junction: this lane's head bytes | the previous lane's tail bytes
       uint32_t pt[4];
 #pragma unroll
       for (int w = 0; w < 4; w++) pt[w] = __shfl_up(t4[w], 1, kWave);
       if (mh) gst<u32x4>(jaddr, u32x4{h4[0] | pt[0], h4[1] | pt[1], h4[2] | pt[2], h4[3] | pt[3]});
     }
-#endif
     // the odd neighbour's partial (the same packet: pairs start even)
     uint32_t n5[5];
 #pragma unroll
@@ -843,34 +766,17 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
       for (int i = 0; i < 5; i++) parts[wv][f >> 1][i] = c5[i];
     }
   }
-#else
-  for (uint32_t base = 0; base < T; base += kWave) {
-    const uint32_t f = base + lane;
-    const uint32_t pp = q_locate(start, base, f < T ? f : T - 1);
-    if (f < T) {
-      QRec &R = recs[wv][pp];
-      const QuicKeyDev &KB = MULTI ? Q.keys[R.kid] : Q.key0;
-      uint32_t c5[5], blk[5][4], h4[4], t4[4];
-      coop_load(R, f - R.start, blk);
-      coop_block<OPEN, OB>(KB, R, f - R.start, blk, c5, false, false, h4, t4);
-#pragma unroll
-      for (int i = 0; i < 5; i++) parts[wv][f][i] = c5[i];
-    }
-  }
-#endif
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
   // ---- 3. owner lanes: combine, tag, header protection (seal with lane
   // pairs: every lane stays for the mask block)
   const bool fin = owner && live;
   if (owner && !live) Q.out_len[p] = status;
-  if (OPEN || !SQ_QSPLIT) {
-    if (!fin) return;
-  }
+  if (OPEN && !fin) return;
   uint32_t ct32[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
   uint32_t tag[4] = {0u, 0u, 0u, 0u}, sample[4] = {0u, 0u, 0u, 0u};
   if (fin) {
-    if (coop && SQ_QPAIR) {
+    if (coop) {
       // pairs: h = h r^c + E_j, c = 8 chunks for a whole pair, r^klast for a
       // last pair of one block, r^(4 + klast) for one of two
       const QRec &Rq = recs[wv][lane];
@@ -907,40 +813,6 @@ __global__ __launch_bounds__(kQBlock) void quic_kernel
       P.s1 = R1.s1; P.s2 = R1.s2; P.s3 = R1.s3; P.s4 = R1.s4;
 #pragma unroll
       for (int i = 0; i < 8; i++) ct32[i] = Rq.ct32[i];
-    } else if (coop) {
-      // r^1..r^4 as multipliers
-      Poly X = P, R1, R2, R3, R4;
-      X.h0 = P.r0; X.h1 = P.r1; X.h2 = P.r2; X.h3 = P.r3; X.h4 = P.r4;
-      poly_set_r(R1, X);
-      poly_mul(X);
-      poly_set_r(R2, X);
-      poly_mul(X);
-      poly_set_r(R3, X);
-      poly_mul(X);
-      poly_set_r(R4, X);
-      // the last block's multiplier r^klast, selected limb by limb
-      const uint32_t L0 = klast == 4 ? R4.r0 : klast == 3 ? R3.r0 : klast == 2 ? R2.r0 : R1.r0;
-      const uint32_t L1 = klast == 4 ? R4.r1 : klast == 3 ? R3.r1 : klast == 2 ? R2.r1 : R1.r1;
-      const uint32_t L2 = klast == 4 ? R4.r2 : klast == 3 ? R3.r2 : klast == 2 ? R2.r2 : R1.r2;
-      const uint32_t L3 = klast == 4 ? R4.r3 : klast == 3 ? R3.r3 : klast == 2 ? R2.r3 : R1.r3;
-      const uint32_t L4 = klast == 4 ? R4.r4 : klast == 3 ? R3.r4 : klast == 2 ? R2.r4 : R1.r4;
-      for (uint32_t b = 0; b < nblk; b++) {
-        const bool lastb = b + 1 == nblk;
-        P.r0 = lastb ? L0 : R4.r0;
-        P.r1 = lastb ? L1 : R4.r1;
-        P.r2 = lastb ? L2 : R4.r2;
-        P.r3 = lastb ? L3 : R4.r3;
-        P.r4 = lastb ? L4 : R4.r4;
-        P.s1 = P.r1 * 5; P.s2 = P.r2 * 5; P.s3 = P.r3 * 5; P.s4 = P.r4 * 5;
-        poly_mul(P);
-        const uint32_t *c5 = parts[wv][start + b];
-        P.h0 += c5[0]; P.h1 += c5[1]; P.h2 += c5[2]; P.h3 += c5[3]; P.h4 += c5[4];
-      }
-      // restore r for the lengths block
-      P.r0 = R1.r0; P.r1 = R1.r1; P.r2 = R1.r2; P.r3 = R1.r3; P.r4 = R1.r4;
-      P.s1 = R1.s1; P.s2 = R1.s2; P.s3 = R1.s3; P.s4 = R1.s4;
-#pragma unroll
-      for (int i = 0; i < 8; i++) ct32[i] = recs[wv][lane].ct32[i];
     } else {
       uint32_t okr[8];
 #pragma unroll

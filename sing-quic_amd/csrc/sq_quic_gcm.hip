@@ -62,15 +62,6 @@ namespace sq {
 #ifndef SQ_GBLOCK
 #define SQ_GBLOCK 768
 #endif
-#ifndef SQ_GNB
-#define SQ_GNB 2
-#endif
-// 1: single-key round keys staged in LDS (broadcast reads) instead of the
-// kernarg segment (SGPRs, which spill to VGPR lanes at 88 words); measured
-// 17 % slower at 16-wave blocks (the keys then occupy VGPRs), so off
-#ifndef SQ_GRK_LDS
-#define SQ_GRK_LDS 0
-#endif
 constexpr uint32_t kGBlock = SQ_GBLOCK;  // 12 waves: one block per CU (156 KB of LDS)
 constexpr uint32_t kGWaves = kGBlock / kWave;
 // Packets per wave (owner lanes).  32 with 12-wave workgroups (the LDS
@@ -344,27 +335,6 @@ __device__ __forceinline__ void gcm_run(const GKey<KM> &K, const uint32_t *tT, u
 #pragma unroll
     for (int w = 0; w < 4; w++) prev_c[w] = c[w];
   };
-#if SQ_GNB == 1
-  for (uint32_t j = 0; j < nchunk; j++) {
-    uint32_t D[4];
-    load_blk(j + 3, D);
-    uint32_t in[4], c[4];
-    uint32_t s1[4] = {nonce[0], nonce[1], nonce[2], __builtin_bswap32(ctr0 + j)};
-    funnel(A, Bq, ib, in);
-    aes_encrypt<KM>(K.rk, tT, tcol, s1);
-    const int nb = (int)nv - 16 * (int)j;
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-      in[w] &= range_mask(0, nb, w);
-      if (OB && OPEN) in[w] ^= bsel(j & 1, okr[4 + w], okr[w]) & range_mask(0, nb, w);
-      c[w] = (in[w] ^ s1[w]) & range_mask(0, nb, w);
-      A[w] = Bq[w];
-      Bq[w] = C[w];
-      C[w] = D[w];
-    }
-    finish(j, in, c);
-  }
-#else
   for (uint32_t j = 0; j < nchunk; j += 2) {
     uint32_t D[4], E[4];
     load_blk(j + 3, D);  // in flight during this pair's AES and GHASH
@@ -394,7 +364,6 @@ __device__ __forceinline__ void gcm_run(const GKey<KM> &K, const uint32_t *tT, u
     finish(j, in[0], c[0]);
     if (j + 1 < nchunk) finish(j + 1, in[1], c[1]);
   }
-#endif
   if (oa + nv > 16 * nchunk) {  // the last block's tail spills into one more output block
     const uint32_t zero[4] = {0u, 0u, 0u, 0u};
     uint32_t blk[4];
@@ -439,11 +408,7 @@ __device__ __forceinline__ GKey<MULTI ? 1 : (STAGED ? 2 : 0)> key_of(
     K.rk = Q.keys[kid].rk; K.hrk = Q.keys[kid].hrk; K.iv = tK + 88;
     K.hpos = tP; K.htab = tH;
   } else {
-#if SQ_GRK_LDS
-    K.rk = tK; K.hrk = tK + 44;
-#else
-    K.rk = Q.rk0; K.hrk = Q.hrk0;
-#endif
+    K.rk = Q.rk0; K.hrk = Q.hrk0;  // (kernarg: scalar loads)
     K.iv = Q.iv0; K.hpos = tP; K.htab = tH;
   }
   return K;
@@ -753,8 +718,9 @@ __device__ __forceinline__ void gcm_unit(const QGParams &Q, uint64_t base, uint3
   Q.out_len[p] = len + 16 + (OB ? kSalamanderSalt : 0u);
 }
 
-// The T-table image (every launch) and, single key, the key's GHASH tables
-// and round keys, into LDS.
+// The T-table image (every launch) and, single key, the key's GHASH tables,
+// into LDS (single-key round keys stay in the kernarg segment: staged in LDS
+// they measured 17 % slower, the keys then occupying VGPRs).
 template <bool MULTI>
 __device__ __forceinline__ void stage_common(const QGParams &Q, uint32_t *tT, uint32_t *tP,
                                              uint32_t *tH, uint32_t *tK) {
@@ -762,8 +728,6 @@ __device__ __forceinline__ void stage_common(const QGParams &Q, uint32_t *tT, ui
     const uint32_t v = Q.t0[i >> 6];
     tT[i] = (i & 32) ? rotl(v, 8) : v;
   }
-  if (!MULTI && threadIdx.x < 88) tK[threadIdx.x] = threadIdx.x < 44 ? Q.rk0[threadIdx.x]
-                                                                     : Q.hrk0[threadIdx.x - 44];
   if (!MULTI) {
     const uint32_t *src = &Q.keys[0].hpos[0][0][0];  // hpos then htab, contiguous
     for (uint32_t i = threadIdx.x; i < (32 + kGcmPow) * 16; i += kGBlock) {
@@ -782,7 +746,7 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
   __shared__ __attribute__((aligned(16))) uint32_t tP[MULTI ? 4 : 32 * 64];
   __shared__ __attribute__((aligned(16))) uint32_t tH[MULTI ? 4 : kGcmPow * 64];
   __shared__ GRec recs[kGWaves][kGPpw];
-  __shared__ __attribute__((aligned(16))) uint32_t tK[88];  // single key: rk0 || hrk0
+  __shared__ __attribute__((aligned(16))) uint32_t tK[4];  // (staged launches only)
   const uint64_t units = ((uint64_t)Q.n + kGPpw - 1) / kGPpw;
   stage_common<MULTI>(Q, tT, tP, tH, tK);
   __syncthreads();

@@ -80,3 +80,18 @@ def test_sharded_equals_single_gloo_world2():
         assert p.exitcode == 0
     assert np.frombuffer(got, dtype=np.uint64).tolist() == single.tolist()
     assert tmax == 2.0  # max over ranks, as bench.py reports time
+
+
+def test_bench_bare_launch_refuses_more_ranks_than_gpus():
+    """`bench.py --gpus 2` without torchrun starts its own ranks, one per GPU:
+    with fewer GPUs visible (none here) and no gloo opt-in it refuses before
+    starting any rank, with a non-zero exit and no JSON line."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2"],
+                       cwd=repo, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2, r.stderr[-2000:]
+    assert "GPU(s) visible" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

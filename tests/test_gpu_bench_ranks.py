@@ -26,12 +26,17 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("config,packets,scaling", [("salamander-1m", 65536, "weak"),
-                                                    ("salamander-16m-256psk", 131072, "strong")])
-def test_bench_two_ranks(config, packets, scaling):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
-           os.path.join(REPO, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+@pytest.mark.parametrize("config,packets,scaling,launcher", [
+    ("salamander-1m", 65536, "weak", "torchrun"),
+    ("salamander-16m-256psk", 131072, "strong", "torchrun"),
+    # the bare command: bench.py starts its own ranks (the driver's SCALE form)
+    ("salamander-1m", 65536, "weak", "bare"),
+    ("salamander-16m-256psk", 131072, "strong", "bare")])
+def test_bench_two_ranks(config, packets, scaling, launcher):
+    pre = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port())] \
+        if launcher == "torchrun" else [sys.executable]
+    cmd = pre + [os.path.join(REPO, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
            "--steps", "3", "--warmup", "1", "--warmup-s", "0", "--no-cpu-baseline",
            "--config", config, "--packets", str(packets)]
     env = dict(os.environ, OMP_NUM_THREADS="4")
@@ -49,3 +54,14 @@ def test_bench_two_ranks(config, packets, scaling):
     assert abs(d["value"] - total / (d["ms_per_step"] * d["steps"] * 1e-3) / 2**30) \
         <= 0.01 * d["value"]  # ms_per_step is rounded to 0.1 us
     assert d["config"]["packets_per_gpu"] == per_rank
+
+
+def test_bare_launch_stops_ranks_on_failure():
+    """A rank that fails makes the bare command exit non-zero, promptly, with
+    no JSON line (the other rank is stopped, not left in its barrier)."""
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dist-backend",
+           "gloo", "--steps", "1", "--warmup", "1", "--warmup-s", "0", "--no-cpu-baseline",
+           "--packets", "1024", "--layout", "inplace", "--direction", "deobfuscate"]
+    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=110)
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

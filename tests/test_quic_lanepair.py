@@ -1,5 +1,5 @@
 """The lane-pair ChaCha20 block of the QUIC kernel's owner phases
-(sing-quic_amd/csrc/sq_quic.hip chacha20_pair, SQ_QSPLIT), emulated on the
+(sing-quic_amd/csrc/sq_quic.hip chacha20_pair, lane pairs), emulated on the
 CPU: lane l holds state columns 0-1, lane l + 32 columns 2-3, and the
 diagonal round exchanges 4 words each way (v_permlane32_swap).  The two
 halves' outputs must put together the RFC 8439 2.3 block, checked against
