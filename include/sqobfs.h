@@ -435,6 +435,16 @@ size_t sqobfs_host_staging_bytes(const sqobfs_ctx *ctx);
 /* Test hook: the next sqobfs_run_host whose pipeline reaches chunk `chunk`
  * fails there with SQ_EDEVICE, as a failed launch would (-1 = off). */
 void sqobfs_debug_fail_chunk(int chunk);
+/* Test hook: on != 0 makes multi-key AES-128-GCM launches skip the grouping
+ * by key (the path taken when the grouping scratch cannot be allocated). */
+void sqobfs_debug_gcm_ungrouped(int on);
+/* Test hook: keyring tables (obfuscation and QUIC) and the AES-GCM grouping
+ * scratch created from now on are carved from the caller's device region
+ * [base, base + bytes) instead of the device allocator (base NULL: the
+ * allocator again; blocks carved earlier stay valid and are never freed).
+ * Returns the bytes carved from the previous region.  For placement tests
+ * (tables at addresses whose low 32-bit word has bit 31 set). */
+uint64_t sqobfs_debug_device_pool(void *base, uint64_t bytes);
 /* Measurement hook (bench.py): the calling thread's next obfuscation launch
  * (sqobfs_launch / sqobfs_run_host chunk) records start_event / stop_event
  * (hipEvent_t, created with timing) with its own kernel dispatch
@@ -736,6 +746,10 @@ int sqobfs_engine_trim(sqobfs_ctx *ctx);
  * waited for (1: as a kernel that faulted; the batch is dropped) -- and the
  * engines switch to the CPU path, as after a real device failure. */
 void sqobfs_debug_engine_fail(int count, int at_completion);
+/* Test hook: the next `count` batch-block allocations of every engine fail
+ * (as a failed page-locked allocation); a socket pconn's receive side
+ * retries on a timer and recovers. */
+void sqobfs_debug_pool_fail(int count);
 
 #ifdef __cplusplus
 }

@@ -19,6 +19,7 @@
 #include <mutex>
 #include <new>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/sqobfs.h"
@@ -44,6 +45,12 @@ struct sqobfs_ctx {
   std::atomic<uint64_t> salt_seq{0};
   // obfuscation kernel unit size (packets per wavefront); 0 = built-in default
   std::atomic<uint32_t> unit_packets{0};
+  // multi-key AES-GCM grouping scratch, cached per library-owned stream (the
+  // context's own and the engine's; grown as needed, freed with the stream or
+  // the context).  gcm_mu is held while a grouped launch is enqueued, so
+  // two threads on one stream cannot interleave their group / kernel pairs.
+  std::mutex gcm_mu;
+  std::unordered_map<hipStream_t, std::pair<void *, uint64_t>> gcm_scratch;
 };
 
 namespace {
@@ -54,6 +61,45 @@ constexpr uint32_t kHostChunks = SQ_HOSTCHUNKS;  // sqobfs_run_host pipeline dep
 // test hook (sqobfs_debug_fail_chunk): the launch of that pipeline chunk
 // fails as a device error would, once
 std::atomic<int> g_fail_chunk{-1};
+// test hook (sqobfs_debug_gcm_ungrouped): multi-key AES-GCM launches skip the
+// grouping (as when its scratch cannot be allocated)
+std::atomic<int> g_gcm_ungrouped{0};
+// test hook (sqobfs_debug_device_pool): keyring tables and grouping scratch
+// carved from a caller's device region (deterministic placement, e.g. at
+// addresses whose low 32-bit word has bit 31 set) instead of the allocator.
+// [lo, hi) stays known after the pool is turned off, so frees of carved
+// blocks stay no-ops.
+struct DebugPool {
+  std::mutex mu;
+  bool on = false;
+  uint8_t *lo = nullptr, *hi = nullptr;
+  uint64_t used = 0;
+};
+DebugPool g_dpool;
+bool in_dpool(const void *p) {
+  std::lock_guard<std::mutex> g(g_dpool.mu);
+  return p && (const uint8_t *)p >= g_dpool.lo && (const uint8_t *)p < g_dpool.hi;
+}
+// Stream-ordered device allocation of the library's tables and scratch.
+hipError_t tab_alloc(void **p, size_t bytes, hipStream_t s) {
+  {
+    std::lock_guard<std::mutex> g(g_dpool.mu);
+    if (g_dpool.on) {
+      const uint64_t off = (g_dpool.used + 255) & ~255ull;
+      if (g_dpool.lo + off + bytes > g_dpool.hi) return hipErrorOutOfMemory;
+      *p = g_dpool.lo + off;
+      g_dpool.used = off + bytes;
+      return hipSuccess;
+    }
+  }
+  return hipMallocAsync(p, bytes, s);
+}
+void tab_free_async(void *p, hipStream_t s) {
+  if (p && !in_dpool(p)) (void)hipFreeAsync(p, s);
+}
+void tab_free(void *p) {
+  if (p && !in_dpool(p)) (void)hipFree(p);
+}
 // live sqobfs_host_alloc blocks (sqobfs_debug_host_allocs: leak checks)
 std::atomic<int64_t> g_host_allocs{0};
 constexpr uint32_t kEvents = 16;
@@ -211,7 +257,11 @@ int sq_ctx_stream_create(sqobfs_ctx *ctx, void **out) {
   if (ds_.status != SQ_OK) return ds_.status;
   hipStream_t s = nullptr;
   const int st = hip_status(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  if (st == SQ_OK) *out = (void *)s;
+  if (st == SQ_OK) {
+    *out = (void *)s;
+    std::lock_guard<std::mutex> g(ctx->gcm_mu);
+    ctx->gcm_scratch[s] = {nullptr, 0};  // library-owned: its scratch may be cached
+  }
   return st;
 }
 
@@ -219,6 +269,14 @@ void sq_ctx_stream_destroy(sqobfs_ctx *ctx, void *s) {
   if (!s) return;
   DeviceScope ds_(ctx->device);
   (void)hipStreamSynchronize((hipStream_t)s);
+  {
+    std::lock_guard<std::mutex> g(ctx->gcm_mu);
+    auto it = ctx->gcm_scratch.find((hipStream_t)s);
+    if (it != ctx->gcm_scratch.end()) {
+      tab_free(it->second.first);  // (the stream is idle)
+      ctx->gcm_scratch.erase(it);
+    }
+  }
   (void)hipStreamDestroy((hipStream_t)s);
 }
 
@@ -551,6 +609,8 @@ void sqobfs_close(sqobfs_ctx *ctx) {
   DeviceScope ds_(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   (void)hipStreamSynchronize(ctx->rel);  // keyrings released before the context
+  for (auto &kv : ctx->gcm_scratch)
+    tab_free(kv.second.first);
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   if (ctx->dev) (void)hipFree(ctx->dev);
   (void)hipStreamDestroy(ctx->stream);
@@ -689,7 +749,7 @@ int sqobfs_keyring_create(sqobfs_ctx *ctx, int kind, uint32_t count, const uint8
   uint8_t *d_blob = nullptr;
   uint64_t *d_off = nullptr;
   uint32_t *d_len = nullptr;
-  hipError_t e = hipMallocAsync((void **)&kr->table, sizeof(sq::PskEntry) * count, ctx->stream);
+  hipError_t e = tab_alloc((void **)&kr->table, sizeof(sq::PskEntry) * count, ctx->stream);
   if (e == hipSuccess) e = hipMalloc(&d_blob, blob_bytes ? blob_bytes : 1);
   if (e == hipSuccess) e = hipMalloc(&d_off, sizeof(uint64_t) * count);
   if (e == hipSuccess) e = hipMalloc(&d_len, sizeof(uint32_t) * count);
@@ -711,7 +771,7 @@ int sqobfs_keyring_create(sqobfs_ctx *ctx, int kind, uint32_t count, const uint8
   if (d_len) (void)hipFree(d_len);
   if (st != SQ_OK) {
     (void)hipStreamSynchronize(ctx->stream);
-    if (kr->table) (void)hipFreeAsync(kr->table, ctx->stream);
+    tab_free_async(kr->table, ctx->stream);
     (void)hipStreamSynchronize(ctx->stream);
     delete kr;
     return st;
@@ -730,7 +790,7 @@ void sqobfs_keyring_destroy(sqobfs_keyring *kr) {
   // launches that used the table may still run: free it after them, in
   // stream order, without blocking (and without a device-wide sync)
   kr->uses.fence(kr->ctx->rel);
-  if (kr->table) (void)hipFreeAsync(kr->table, kr->ctx->rel);
+  tab_free_async(kr->table, kr->ctx->rel);
   delete kr;
 }
 
@@ -1021,7 +1081,7 @@ int sqobfs_quic_keyring_create_suite(sqobfs_ctx *ctx, uint32_t suite, uint32_t c
       for (int i = 0; i < 8; i++) h[k].hp[i] = le32(keys[k].hp + 4 * i);
     }
     kr->host0 = h[0];
-    e = hipMallocAsync((void **)&kr->table, sizeof(sq::QuicKeyDev) * count, ctx->stream);
+    e = tab_alloc((void **)&kr->table, sizeof(sq::QuicKeyDev) * count, ctx->stream);
     if (e == hipSuccess)
       e = hipMemcpyAsync(kr->table, h.data(), sizeof(sq::QuicKeyDev) * count,
                          hipMemcpyHostToDevice, ctx->stream);
@@ -1032,11 +1092,11 @@ int sqobfs_quic_keyring_create_suite(sqobfs_ctx *ctx, uint32_t suite, uint32_t c
     memcpy(kr->grk0, h[0].rk, sizeof kr->grk0);
     memcpy(kr->ghrk0, h[0].hrk, sizeof kr->ghrk0);
     memcpy(kr->giv0, h[0].iv, sizeof kr->giv0);
-    e = hipMallocAsync((void **)&kr->gtable, sizeof(sq::QuicGcmKeyDev) * count, ctx->stream);
+    e = tab_alloc((void **)&kr->gtable, sizeof(sq::QuicGcmKeyDev) * count, ctx->stream);
     if (e == hipSuccess)
       e = hipMemcpyAsync(kr->gtable, h.data(), sizeof(sq::QuicGcmKeyDev) * count,
                          hipMemcpyHostToDevice, ctx->stream);
-    if (e == hipSuccess) e = hipMallocAsync((void **)&kr->t0, sizeof(uint32_t) * 256, ctx->stream);
+    if (e == hipSuccess) e = tab_alloc((void **)&kr->t0, sizeof(uint32_t) * 256, ctx->stream);
     if (e == hipSuccess)
       e = hipMemcpyAsync(kr->t0, aes_tables().t0, sizeof(uint32_t) * 256, hipMemcpyHostToDevice,
                          ctx->stream);
@@ -1044,9 +1104,9 @@ int sqobfs_quic_keyring_create_suite(sqobfs_ctx *ctx, uint32_t suite, uint32_t c
   }
   if (e != hipSuccess) {
     (void)hipStreamSynchronize(ctx->stream);
-    if (kr->table) (void)hipFreeAsync(kr->table, ctx->stream);
-    if (kr->gtable) (void)hipFreeAsync(kr->gtable, ctx->stream);
-    if (kr->t0) (void)hipFreeAsync(kr->t0, ctx->stream);
+    tab_free_async(kr->table, ctx->stream);
+    tab_free_async(kr->gtable, ctx->stream);
+    tab_free_async(kr->t0, ctx->stream);
     (void)hipStreamSynchronize(ctx->stream);
     delete kr;
     return hip_status(e);
@@ -1064,9 +1124,9 @@ void sqobfs_quic_keyring_destroy(sqobfs_quic_keyring *kr) {
   if (!kr) return;
   DeviceScope ds_(kr->ctx->device);
   kr->uses.fence(kr->ctx->rel);  // as sqobfs_keyring_destroy: stream-ordered, no wait
-  if (kr->table) (void)hipFreeAsync(kr->table, kr->ctx->rel);
-  if (kr->gtable) (void)hipFreeAsync(kr->gtable, kr->ctx->rel);
-  if (kr->t0) (void)hipFreeAsync(kr->t0, kr->ctx->rel);
+  tab_free_async(kr->table, kr->ctx->rel);
+  tab_free_async(kr->gtable, kr->ctx->rel);
+  tab_free_async(kr->t0, kr->ctx->rel);
   delete kr;
 }
 
@@ -1109,21 +1169,45 @@ static int quic_launch(int open, sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr,
     }
     hipStream_t s = pick_stream(ctx, stream);
     // multi-key: group the packets by key first (the kernel then runs each
-    // workgroup's units on one staged key); scratch is stream-ordered
+    // workgroup's units on one staged key).  The scratch is stream-ordered:
+    // cached per library-owned stream, else allocated for this launch; none
+    // (allocation failed, or the test hook) runs the ungrouped kernel
     void *scratch = nullptr;
-    const uint64_t gbytes = b->key_id ? sq_gcm_group_scratch(b->n, kr->count) : 0;
-    if (gbytes && hipMallocAsync(&scratch, gbytes, s) != hipSuccess) scratch = nullptr;
+    bool cached = false;
+    const uint64_t gbytes =
+        b->key_id && !g_gcm_ungrouped.load() ? sq_gcm_group_scratch(b->n, kr->count) : 0;
+    std::unique_lock<std::mutex> glk(ctx->gcm_mu, std::defer_lock);
+    if (gbytes) {
+      glk.lock();
+      if (s == ctx->stream && !ctx->gcm_scratch.count(s)) ctx->gcm_scratch[s] = {nullptr, 0};
+      auto it = ctx->gcm_scratch.find(s);
+      if (it != ctx->gcm_scratch.end()) {
+        auto &e = it->second;
+        if (e.second < gbytes) {  // grow (the old block is freed in stream order)
+          const uint64_t want = std::max<uint64_t>(gbytes, 2 * e.second);
+          tab_free_async(e.first, s);
+          e = {nullptr, 0};
+          if (tab_alloc(&e.first, want, s) == hipSuccess) e.second = want;
+          else e.first = nullptr;
+        }
+        scratch = e.first;
+        cached = true;
+      } else {
+        glk.unlock();  // (a caller's stream: this launch's own scratch)
+        if (tab_alloc(&scratch, gbytes, s) != hipSuccess) scratch = nullptr;
+      }
+    }
     if (scratch) {
       const int gs = sq_launch_gcm_group(b->key_id, b->n, kr->count, open, b->out_len,
                                          open ? b->pn_out : nullptr, scratch, &g.gmeta, s);
       if (gs < 0) {
-        (void)hipFreeAsync(scratch, s);
+        if (!cached) tab_free_async(scratch, s);
         return gs;
       }
       g.perm = (const uint32_t *)scratch;
     }
     const int st = sq_launch_quic_gcm(open, &g, s);
-    if (scratch) (void)hipFreeAsync(scratch, s);
+    if (scratch && !cached) tab_free_async(scratch, s);
     if (st == SQ_OK) {
       kr->uses.note(s);
       if (okr) okr->uses.note(s);
@@ -1187,6 +1271,20 @@ int sqobfs_quic_open(sqobfs_ctx *ctx, const sqobfs_quic_keyring *kr, const sqobf
 size_t sqobfs_host_staging_bytes(const sqobfs_ctx *ctx) { return ctx ? ctx->pinned_cap : 0; }
 
 void sqobfs_debug_fail_chunk(int chunk) { g_fail_chunk.store(chunk); }
+
+void sqobfs_debug_gcm_ungrouped(int on) { g_gcm_ungrouped.store(on ? 1 : 0); }
+
+uint64_t sqobfs_debug_device_pool(void *base, uint64_t bytes) {
+  std::lock_guard<std::mutex> g(g_dpool.mu);
+  const uint64_t used = g_dpool.used;
+  g_dpool.used = 0;
+  g_dpool.on = base != nullptr && bytes != 0;
+  if (g_dpool.on) {
+    g_dpool.lo = (uint8_t *)base;
+    g_dpool.hi = (uint8_t *)base + bytes;
+  }
+  return used;
+}
 
 void sqobfs_debug_time_next_launch(void *start_event, void *stop_event) {
   sq_time_next_launch(start_event, stop_event);

@@ -91,6 +91,18 @@ namespace sq {
 #ifndef SQ_PSKPRE
 #define SQ_PSKPRE 1
 #endif
+// 1: the stream loads special blocks too when every special block of the
+// wave has its input in a 16-byte-aligned block holding a payload byte (so
+// it is mapped); the loaded value is discarded (no read holes)
+#ifndef SQ_LDSPECIAL
+#define SQ_LDSPECIAL 0
+#endif
+// 1: device salts by quads (each quad of lanes computes one ChaCha20 block,
+// one state column per lane, DPP rotations for the diagonal rounds; the
+// wave's blocks staged in LDS); 0: one whole block per lane
+#ifndef SQ_QSALT
+#define SQ_QSALT 0
+#endif
 // Timeline builds (scripts/dev/timeline.py, never shipped): lane 0 of every
 // wave records the constant-rate clock at its phase boundaries.
 #ifndef SQ_TIMELINE
@@ -258,6 +270,79 @@ __device__ __forceinline__ void device_salt_words(const KParams &P, uint32_t p,
   for (uint32_t k = 0; k < S / 4; k++) salt[k] = y[k];
 }
 
+// Quad ChaCha20 (RFC 8439 2.3): the 4 lanes of a quad hold one block's state
+// column by column (lane i: words i, 4 + i, 8 + i, 12 + i).  The column
+// round is one quarter round per lane; the diagonal round rotates rows 1-3
+// across the quad by 1, 2, 3 lanes (DPP quad_perm), runs one quarter round
+// and rotates them back.  Per lane 80 quarter rounds -> 20, plus 60 DPP
+// moves.  Every lane of the wave must call it.
+template <int CTRL>
+__device__ __forceinline__ uint32_t qperm(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, false);
+}
+#define SQ_QQR(a, b, c, d)                                              \
+  a += b; d ^= a; d = __builtin_amdgcn_alignbit(d, d, 16);            \
+  c += d; b ^= c; b = __builtin_amdgcn_alignbit(b, b, 20);            \
+  a += b; d ^= a; d = __builtin_amdgcn_alignbit(d, d, 24);            \
+  c += d; b ^= c; b = __builtin_amdgcn_alignbit(b, b, 25);
+__device__ __forceinline__ void chacha20_quad(const uint32_t (&key)[8], uint32_t counter,
+                                              const uint32_t (&nonce)[3], uint32_t col,
+                                              uint32_t (&o)[4]) {
+  const uint32_t sigma = col == 0 ? 0x61707865u : col == 1 ? 0x3320646eu
+                         : col == 2 ? 0x79622d32u : 0x6b206574u;
+  const uint32_t kb = col == 0 ? key[0] : col == 1 ? key[1] : col == 2 ? key[2] : key[3];
+  const uint32_t kc = col == 0 ? key[4] : col == 1 ? key[5] : col == 2 ? key[6] : key[7];
+  const uint32_t kd = col == 0 ? counter : col == 1 ? nonce[0] : col == 2 ? nonce[1] : nonce[2];
+  uint32_t a = sigma, b = kb, c = kc, d = kd;
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    SQ_QQR(a, b, c, d)
+    // lane i: b of lane i + 1, c of i + 2, d of i + 3 (quad_perm)
+    b = qperm<0x39>(b);
+    c = qperm<0x4E>(c);
+    d = qperm<0x93>(d);
+    SQ_QQR(a, b, c, d)
+    b = qperm<0x93>(b);
+    c = qperm<0x4E>(c);
+    d = qperm<0x39>(d);
+  }
+  o[0] = a + sigma;
+  o[1] = b + kb;
+  o[2] = c + kc;
+  o[3] = d + kd;
+}
+#undef SQ_QQR
+
+// The device salts of a wave's packets (lanes 0 .. ppw + 1: the unit and
+// its two neighbours) by quads: quad q computes keystream block b0 + q (16
+// blocks per pass; a unit of up to 62 packets needs one pass, XPlus units
+// over 58 packets two), the blocks are staged in the wave's LDS scratch
+// (1 KiB), and every lane reads its S bytes.  Every lane must call it.
+template <uint32_t S>
+__device__ __forceinline__ void device_salts_wave(const KParams &P, uint64_t first, uint32_t ppw,
+                                                  uint32_t lane, uint32_t p, bool valid,
+                                                  uint32_t *scratch, uint32_t (&salt)[4]) {
+  constexpr uint32_t per_block = 64 / S;  // 8 Salamander, 4 XPlus
+  const uint64_t lo = first ? first - 1 : 0;
+  const uint64_t hi0 = first + ppw, hi = hi0 < P.n ? hi0 : P.n - 1;
+  const uint32_t b0 = (uint32_t)(lo / per_block);
+  const uint32_t nb = (uint32_t)(hi / per_block) - b0 + 1;  // wave-uniform
+  const uint32_t q = lane >> 2, col = lane & 3;
+  const uint32_t mb = p / per_block - b0;  // this lane's block, relative
+  const uint32_t w0 = (p % per_block) * (S / 4);
+  for (uint32_t pass = 0; pass * 16 < nb; pass++) {
+    uint32_t x[4];
+    chacha20_quad(P.salt_key, b0 + 16 * pass + q, P.salt_nonce, col, x);
+#pragma unroll
+    for (int r = 0; r < 4; r++) scratch[16 * q + 4 * r + col] = x[r];
+    const uint32_t rb = mb - 16 * pass;
+    if (valid && rb < 16) {
+#pragma unroll
+      for (uint32_t k = 0; k < S / 4; k++) salt[k] = scratch[16 * rb + w0 + k];
+    }
+  }
+}
+
 // ... and its copy to salt_out (SQOBFS_FLAG_DEVICE_SALT with salt_out)
 template <uint32_t S>
 __device__ __forceinline__ void device_salt_out(const KParams &P, uint32_t p,
@@ -303,7 +388,7 @@ __device__ __forceinline__ void fetch_desc(const KParams &P, uint32_t p, bool va
   // device salts depend on p alone: computed while the loads above fly
   // (round 4, profiles/r04/ab2: configs[1] with device salts -2.6 %, XPlus
   // -0.8 %, against computing them after the loads land)
-  if (DIR == 0 && P.device_salt) device_salt_words<S>(P, p, d.salt);
+  if (DIR == 0 && P.device_salt && !SQ_QSALT) device_salt_words<S>(P, p, d.salt);
 }
 
 template <int KIND, int DIR, bool MULTI>
@@ -664,6 +749,7 @@ struct UnitStream {
   uint32_t cst;    // lane: flat start of the packet of rank `lane` (~0 past the last)
   uint32_t T;      // wave-uniform: blocks in the flat space
   bool fast;       // wave-uniform: buffer-resource streaming possible
+  bool ldsp;       // wave-uniform: special blocks' inputs loaded too (SQ_LDSPECIAL)
   bool map;        // wave-uniform: the bit map covers the flat space
   WaveBufs B;
 };
@@ -773,9 +859,19 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
   const uint32_t T0 = __builtin_amdgcn_readfirstlane(__shfl(incl, kWave - 1, kWave));
   U.map = T0 + (1u << SQ_ALIGN) <= kMapBlocks;
   // interior blocks [i_lo, i_hi): the only ones loaded
-  const uint32_t i_lo = G.hf ? 1u : 0u, i_hi = G.hl ? nblk - 1 : nblk;
-  const bool has_int = i_hi > i_lo;
+  const uint32_t i_lo0 = G.hf ? 1u : 0u, i_hi0 = G.hl ? nblk - 1 : nblk;
   const uint64_t sabs = B0 + (J.src_pay - J.dst_pay);  // input of block B0
+  // special blocks loadable: every input block of the packet's flat blocks
+  // is 16-byte aligned and its special ones hold a payload byte (mapped)
+  const uint64_t pe = J.src_pay + J.len;
+  const bool sp_ok = !F || ((sabs & 15) == 0 && npad == 0 &&
+                            (!G.hf || (J.len && J.src_pay < sabs + 16 && pe > sabs)) &&
+                            (!(G.hl && G.lfull) ||
+                             (J.len && pe > sabs + 16ull * (nblk - 1) &&
+                              J.src_pay < sabs + 16ull * nblk)));
+  U.ldsp = SQ_LDSPECIAL && !ol && __ballot(!sp_ok) == 0;
+  const uint32_t i_lo = U.ldsp ? 0u : i_lo0, i_hi = U.ldsp ? F : i_hi0;
+  const bool has_int = i_hi > i_lo;
   const uint64_t s_first = sabs + 16ull * i_lo, s_end = sabs + 16ull * i_hi;
   // spans: output of every flat block, input of every interior block
   const uint64_t d_lo = wave_ext64_dpp<false>(F ? B0 : ~0ull);
@@ -1006,7 +1102,7 @@ struct Step {
 // "keystream" is its precomputed value.
 template <int U, bool MAP>
 __device__ __forceinline__ void stream_issue(const WaveLds &L, const WaveBufs &B, uint32_t cst,
-                                             uint32_t T, uint32_t lane, uint32_t base,
+                                             uint32_t T, uint32_t lane, uint32_t base, bool ldsp,
                                              Step<U> &S) {
   uint32_t pp[U], off[U], rl[U];
   // every LDS read of the step first, then the arithmetic, then the loads
@@ -1041,7 +1137,7 @@ __device__ __forceinline__ void stream_issue(const WaveLds &L, const WaveBufs &B
     const uint32_t c = base + u * kWave + lane;
     const bool in = c < T;
     S.doff[u] = in ? (uint32_t)(sd[u] >> 32) + 16u * c : kOffNone;
-    off[u] = in && idx[u] < 2u ? (uint32_t)sd[u] + 16u * c : kOffNone;
+    off[u] = in && (ldsp || idx[u] < 2u) ? (uint32_t)sd[u] + 16u * c : kOffNone;
   }
 #pragma unroll
   for (int u = 0; u < U; u++) S.v[u] = __builtin_amdgcn_raw_buffer_load_b128(B.src, off[u], 0, kAuxLd);
@@ -1061,15 +1157,15 @@ __device__ __forceinline__ void stream_store(const WaveLds &L, const WaveBufs &B
 // stored, so a wave keeps U..2U KiB of reads outstanding.
 template <int U, bool MAP>
 __device__ __forceinline__ void stream_loop(const WaveLds &L, const WaveBufs &B, uint32_t cst,
-                                            uint32_t T, uint32_t lane, Step<U> &cur) {
+                                            uint32_t T, uint32_t lane, bool ldsp, Step<U> &cur) {
   constexpr uint32_t STEP = kWave * U;
   // unrolled by two with two named steps, so no register copies between them
   Step<U> nxt;
   for (uint32_t base = 0;; base += 2 * STEP) {
-    stream_issue<U, MAP>(L, B, cst, T, lane, base + STEP, nxt);
+    stream_issue<U, MAP>(L, B, cst, T, lane, base + STEP, ldsp, nxt);
     stream_store<U>(L, B, cur);
     if (base + STEP >= T) break;
-    stream_issue<U, MAP>(L, B, cst, T, lane, base + 2 * STEP, cur);
+    stream_issue<U, MAP>(L, B, cst, T, lane, base + 2 * STEP, ldsp, cur);
     stream_store<U>(L, B, nxt);
     if (base + 2 * STEP >= T) break;
   }
@@ -1120,6 +1216,10 @@ __global__ __launch_bounds__(WPB * kWave) void obfs_kernel(const KParams P) {
   // 1. descriptor (deobfuscate: the salt load) and the image windows: loads
   RawDesc d;
   fetch_desc<KIND, DIR, MULTI>(P, p, valid, d);
+  constexpr uint32_t kSalt = KIND == 0 ? kSalamanderSalt : kXPlusSalt;
+  if (SQ_QSALT && DIR == 0 && P.device_salt)  // (while the descriptor loads fly)
+    device_salts_wave<kSalt>(P, first, ppw, lane, p, valid,
+                             reinterpret_cast<uint32_t *>(lds[wv].role), d.salt);
   PacketJob J;
   uint32_t salt[4];
   bool do_hash;
@@ -1132,7 +1232,6 @@ __global__ __launch_bounds__(WPB * kWave) void obfs_kernel(const KParams P) {
   }
   SQ_STAMP(1);
   Windows W;
-  constexpr uint32_t kSalt = KIND == 0 ? kSalamanderSalt : kXPlusSalt;
   fetch_windows<DIR, kSalt>(J, do_hash, W);
   if (owner) P.out_len[p] = olen;
   // 3a. plan
@@ -1149,11 +1248,11 @@ __global__ __launch_bounds__(WPB * kWave) void obfs_kernel(const KParams P) {
   SQ_STAMP(3);
   // 4. the stream
   if (S.fast && S.map) {
-    stream_issue<U, true>(L, S.B, S.cst, S.T, lane, 0, cur);
-    stream_loop<U, true>(L, S.B, S.cst, S.T, lane, cur);
+    stream_issue<U, true>(L, S.B, S.cst, S.T, lane, 0, S.ldsp, cur);
+    stream_loop<U, true>(L, S.B, S.cst, S.T, lane, S.ldsp, cur);
   } else if (S.fast) {
-    stream_issue<U, false>(L, S.B, S.cst, S.T, lane, 0, cur);
-    stream_loop<U, false>(L, S.B, S.cst, S.T, lane, cur);
+    stream_issue<U, false>(L, S.B, S.cst, S.T, lane, 0, S.ldsp, cur);
+    stream_loop<U, false>(L, S.B, S.cst, S.T, lane, S.ldsp, cur);
   } else if (S.T != 0) {
     stream_generic(L, S.cst, S.T, lane);
   }

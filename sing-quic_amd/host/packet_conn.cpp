@@ -204,7 +204,7 @@ int Obfuscator::run(int dir, const sqobfs_batch &b) {
     const uint32_t o = a.load(std::memory_order_relaxed);
     a.store((uint32_t)((7ull * o + std::min<uint64_t>(v, 1u << 30)) / 8), std::memory_order_relaxed);
   };
-  if (!ctx_ || gpu_failed_ || cost <= route) {
+  if (!ctx_ || gpu_failed_.load(std::memory_order_relaxed) || cost <= route) {
     const int st = sqobfs_cpu_run(kr_, dir, &b);
     if (cost >= (8u << 10))  // (smaller batches: timer noise)
       ewma(cpu_ns_kib_, (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
@@ -212,7 +212,8 @@ int Obfuscator::run(int dir, const sqobfs_batch &b) {
     return st;
   }
   const int st = sqobfs_run_host(ctx_, kr_, dir, &b);
-  if (st == SQ_EDEVICE || st == SQ_ENODEV) gpu_failed_ = true;  // later batches: the CPU
+  if (st == SQ_EDEVICE || st == SQ_ENODEV)
+    gpu_failed_.store(true, std::memory_order_relaxed);  // later batches: the CPU
   if (st == SQ_OK)
     ewma(gpu_us_, (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(
                       std::chrono::steady_clock::now() - t0).count());

@@ -84,12 +84,12 @@ class Obfuscator {
   // no GPU, or after a failed launch) sqobfs_cpu_run; returns sqobfs status
   int run(int dir, const sqobfs_batch &b);
   int status() const { return status_; }
-  bool has_gpu() const { return ctx_ != nullptr && !gpu_failed_; }
+  bool has_gpu() const { return ctx_ != nullptr && !gpu_failed_.load(std::memory_order_relaxed); }
 
  private:
   int kind_;
   int status_ = SQ_OK;
-  bool gpu_failed_ = false;
+  std::atomic<bool> gpu_failed_{false};  // (run() from concurrent ReadFrom / WriteTo)
   // routing (run): recent staged round trip (us) and CPU-path ns per KiB of
   // cost, EWMAs; ~120 KiB break-even before either is measured
   std::atomic<uint32_t> gpu_us_{60};

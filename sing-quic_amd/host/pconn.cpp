@@ -84,15 +84,24 @@ constexpr uint32_t kDefInlineGapUs = 100;
 constexpr uint32_t kDefWorkers = 4, kMaxWorkers = 64;
 constexpr uint32_t kMaxBatch = 1u << 16;
 constexpr int64_t kDrainNs = 200'000'000;  // shutdown: time given to queued writes
+constexpr int64_t kAttachRetryNs = 1'000'000;  // socket rx: retry a failed block allocation
 constexpr uint32_t kMmsg = 256;            // messages per sendmmsg / recvmmsg call
 constexpr uint32_t kGsoMaxSegs = 64;       // UDP_MAX_SEGMENTS of older kernels
 constexpr uint32_t kGsoMaxBytes = 65000;   // one GSO send stays below 64 KiB of IP payload
 constexpr uint32_t kGroBuf = 65536;        // one coalesced receive
 constexpr size_t kCtlWords = (CMSG_SPACE(sizeof(uint16_t)) + 7) / 8;
 
-// sqobfs_debug_engine_fail
+// sqobfs_debug_engine_fail, sqobfs_debug_pool_fail
 std::atomic<int> g_fail_count{0};
 std::atomic<int> g_fail_at_completion{0};
+std::atomic<int> g_pool_fail{0};
+
+// take one unit of a test hook's countdown
+bool take_one(std::atomic<int> &c) {
+  for (int v = c.load(); v > 0;)
+    if (c.compare_exchange_weak(v, v - 1)) return true;
+  return false;
+}
 
 int64_t unix_ns() {
   timespec ts;
@@ -304,6 +313,7 @@ Engine *engine_get(sqobfs_ctx *ctx, int *status) {
 // ---------------------------------------------------------------- block pool
 
 Block *block_take(Engine *E, uint32_t B, uint32_t slot) {
+  if (take_one(g_pool_fail)) return nullptr;  // (test hook: an allocation failure)
   std::lock_guard<std::mutex> g(E->pool_mu);
   auto &fl = E->free_blocks[{B, slot}];
   if (!fl.empty()) {
@@ -492,17 +502,15 @@ int transform(Engine *E, uint32_t w, sqobfs_pconn *pc, int dir, PBatch &b, bool 
       std::lock_guard<std::mutex> lk(E->mu);
       E->streams[w] = s;
     }
-    int inject = 0;
-    for (int c = g_fail_count.load(); c > 0;)
-      if (g_fail_count.compare_exchange_weak(c, c - 1)) {
-        inject = g_fail_at_completion.load() ? 2 : 1;
-        break;
-      }
+    const int inject = take_one(g_fail_count) ? (g_fail_at_completion.load() ? 2 : 1) : 0;
     const int64_t t0 = mono_ns();
     if (st == SQ_OK) st = inject == 1 ? SQ_EDEVICE : sqobfs_launch(E->ctx, pc->kr, dir, &d, E->streams[w]);
     if (st != SQ_OK) {
-      // refused before anything ran: the batch is intact, redo it on the CPU
-      E->gpu_off.store(true);
+      // refused before anything ran: the batch is intact, redo it on the CPU.
+      // Only a device failure turns the GPU off for the engine; a refusal of
+      // this batch or this moment (no memory for a stream or staging) leaves
+      // the next batch free to launch
+      if (st == SQ_EDEVICE || st == SQ_ENODEV) E->gpu_off.store(true);
       *failed = true;
     } else {
       const uint32_t ew = E->launch_us.load(std::memory_order_relaxed);
@@ -747,8 +755,13 @@ void rx_socket_task(Engine *E, uint32_t w, sqobfs_pconn *pc) {
   PBatch &b = pc->rb[idx];
   if (!batch_attach(pc, b, false)) {
     pc->rfree.push_front(idx);
-    pc->rx_stall = true;  // no memory now: the next read() retries
-    return task_end(pc, kRx, false);
+    if (!pc->rready.empty()) {
+      pc->rx_stall = true;  // no memory now: the read() that frees a batch retries
+      return task_end(pc, kRx, false);
+    }
+    // nothing to read, so no read() will come back here: retry on a timer
+    // (the socket stays un-armed meanwhile; its datagrams wait in the kernel)
+    return task_end(pc, kRx, true, mono_ns() + kAttachRetryNs);
   }
   lk.unlock();
   // GRO: the batch's slot region as 64 KiB buffers of up to 64 coalesced
@@ -975,13 +988,12 @@ int sqobfs_engine_set_workers(sqobfs_ctx *ctx, uint32_t workers) {
 }
 
 int sqobfs_engine_trim(sqobfs_ctx *ctx) {
-  Engine *E;
-  {
-    std::lock_guard<std::mutex> g(g_eng_mu);
-    auto it = g_engines.find(ctx);
-    if (it == g_engines.end()) return 0;
-    E = it->second;
-  }
+  // g_eng_mu held throughout: a concurrent sqobfs_close ends (deletes) the
+  // engine under it, so E stays valid while the blocks are freed
+  std::lock_guard<std::mutex> g(g_eng_mu);
+  auto it = g_engines.find(ctx);
+  if (it == g_engines.end()) return 0;
+  Engine *E = it->second;
   std::vector<Block *> drop;
   {
     std::lock_guard<std::mutex> pg(E->pool_mu);
@@ -1002,6 +1014,8 @@ void sqobfs_debug_engine_fail(int count, int at_completion) {
   g_fail_at_completion.store(at_completion ? 1 : 0);
   g_fail_count.store(count > 0 ? count : 0);
 }
+
+void sqobfs_debug_pool_fail(int count) { g_pool_fail.store(count > 0 ? count : 0); }
 
 // ---------------------------------------------------------------- pconn ABI
 

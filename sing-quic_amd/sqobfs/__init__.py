@@ -252,6 +252,14 @@ def load(path: str) -> ctypes.CDLL:
     L.sqobfs_shard_launch.argtypes = [u32, vp, vp, i32, vp, ctypes.POINTER(vp)]
     L.sqobfs_shard_query.argtypes = [vp]
     L.sqobfs_shard_wait.argtypes = [vp]
+    if not hasattr(L, "sqobfs_debug_pool_fail"):
+        return L  # ABI before round 5
+    L.sqobfs_debug_pool_fail.argtypes = [i32]
+    L.sqobfs_debug_pool_fail.restype = None
+    L.sqobfs_debug_gcm_ungrouped.argtypes = [i32]
+    L.sqobfs_debug_gcm_ungrouped.restype = None
+    L.sqobfs_debug_device_pool.argtypes = [vp, ctypes.c_uint64]
+    L.sqobfs_debug_device_pool.restype = ctypes.c_uint64
     return L
 
 
@@ -495,6 +503,24 @@ def shard_launch(ctxs: list[Context], krs: list[Keyring], direction: int,
     _check(lib().sqobfs_shard_launch(len(ctxs), _handles(ctxs), _handles(krs), direction, arr,
                                      ctypes.byref(h)), "sqobfs_shard_launch")
     return ShardTicket(h)
+
+
+def debug_gcm_ungrouped(on: bool) -> None:
+    """Multi-key AES-128-GCM launches skip the grouping by key while on (the
+    path taken when its scratch cannot be allocated)."""
+    lib().sqobfs_debug_gcm_ungrouped(1 if on else 0)
+
+
+def debug_device_pool(base: int | None, nbytes: int = 0) -> int:
+    """Carve keyring tables and grouping scratch from [base, base + nbytes)
+    (device memory the caller owns) until called with None; returns the bytes
+    carved from the previous region."""
+    return int(lib().sqobfs_debug_device_pool(base, nbytes))
+
+
+def debug_pool_fail(count: int) -> None:
+    """The next `count` packet conn engine batch-block allocations fail."""
+    lib().sqobfs_debug_pool_fail(count)
 
 
 def debug_fail_chunk(chunk: int) -> None:

@@ -27,6 +27,9 @@
  *   fail      injected launch failures: a refused launch is redone on the
  *             CPU, a failed kernel's batch is dropped, and every datagram
  *             after either still reads / writes as the reference's
+ *   poolfail  a receive batch block that cannot be allocated (with nothing
+ *             unread to restart the socket task) is retried: the datagram
+ *             still reads, within its deadline
  * Modes (argv[1]): "gpu" (default: a context on GPU 0; with the CPU device
  * of tests/cpp/sq_devstub.cpp in the sanitizer builds) and "nodev" (no
  * context: host keyrings, every batch on the CPU path -- the drop-in with no
@@ -843,6 +846,44 @@ static void t_routing(void) {
   check_mem(a0);
 }
 
+/* ------------------------------------------------------------ poolfail */
+static void t_poolfail(int kind) {
+  const int S = salt_len(kind);
+  const int64_t a0 = sqobfs_debug_host_allocs();
+  sqobfs_keyring *kr = keyring(kind);
+  uint16_t pa, pp;
+  int fa = udp_socket(&pa), fp = udp_socket(&pp);
+  sqobfs_pconn *pc = NULL;
+  CHECK(sqobfs_pconn_open(g_ctx, kr, fa, NULL, &pc));
+  for (int round = 0; round < 3; round++) {
+    /* round 0: the first allocation fails; 1: the next 5 do; 2: none */
+    sqobfs_debug_pool_fail(round == 0 ? 1 : round == 1 ? 5 : 0);
+    uint8_t salt[16], pay[1400], w[MAXW], got[MAXW], ref[MAXW];
+    for (int b = 0; b < 16; b++) salt[b] = (uint8_t)rnd();
+    const uint32_t L = 100 + 600 * (uint32_t)round;
+    for (uint32_t b = 0; b < L; b++) pay[b] = (uint8_t)rnd();
+    ref_write(kind, salt, pay, L, w);
+    send_to(fp, pa, w, L + (uint32_t)S);
+    CHECK(sqobfs_pconn_set_deadline(pc, SQOBFS_PCONN_READ, unix_ns() + 3000000000ll));
+    uint32_t n = 0;
+    const double t0 = now_s();
+    const int st = sqobfs_pconn_read(pc, got, MAXW, &n, NULL, NULL);
+    EXPECT(st == SQ_OK, "poolfail kind %d round %d: read -> %d after %.2f s (the receive side "
+           "did not recover from the failed allocation)", kind, round, st, now_s() - t0);
+    const long want = ref_read(kind, w, L + (uint32_t)S, MAXW, ref);
+    EXPECT((long)n == want && !memcmp(got, ref, n), "poolfail kind %d round %d: payload", kind,
+           round);
+  }
+  sqobfs_debug_pool_fail(0);
+  CHECK(sqobfs_pconn_set_deadline(pc, SQOBFS_PCONN_READ, 0));
+  printf("  poolfail kind %d: reads recover from failed batch-block allocations\n", kind);
+  sqobfs_pconn_close(pc);
+  close(fa);
+  close(fp);
+  sqobfs_keyring_destroy(kr);
+  check_mem(a0);
+}
+
 /* ------------------------------------------------------------ fail */
 /* On a context of its own (a failure turns its engine to the CPU for good).
  * at_completion 0: the launch is refused -> the batch is redone on the CPU;
@@ -931,6 +972,7 @@ int main(int argc, char **argv) {
     t_roundtrip(kind, SQOBFS_UDP_TX_GSO | SQOBFS_UDP_RX_GRO);
     t_pump(kind);
     t_syncerr(kind);
+    t_poolfail(kind);
   }
   t_deadline();
   t_shutdown();
@@ -946,6 +988,7 @@ int main(int argc, char **argv) {
   if (g_ctx) sqobfs_close(g_ctx);
   EXPECT(sqobfs_debug_host_allocs() == a0, "host allocs after close");
   printf("ok: pconn engine [%s] (socket + pump modes, deadlines, shutdown, memory, sync errors, "
+         "allocation failures, "
          "shared engine%s)\n", g_nodev ? "no device" : "device",
          g_nodev ? "" : ", routing, launch failures");
   return 0;

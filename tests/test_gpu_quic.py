@@ -35,8 +35,10 @@ def _place(sizes, align, gap):
 
 
 def run(ctx, keys, seal, pkts, pn_offsets, pns, key_ids=None, align=1, inplace=False,
-        suite=0, pn_out_fill=0):
-    """One device batch; returns (out buffer, out offsets, out_len, pn_out)."""
+        suite=0, pn_out_fill=0, ctx_stream=False):
+    """One device batch; returns (out buffer, out offsets, out_len, pn_out).
+    ctx_stream: launched on the context's own stream (stream NULL) instead of
+    torch's current one."""
     import torch
     dev = torch.device("cuda", 0)
     n = len(pkts)
@@ -62,8 +64,10 @@ def run(ctx, keys, seal, pkts, pn_offsets, pns, key_ids=None, align=1, inplace=F
     b = sqobfs.quic_batch(n, d_data, d["in_off"], d["in_len"], d_out, d["out_off"], d["out_len"],
                           d["pno"], d["pn"], d["kid"], d["pn_out"])
     with sqobfs.QuicKeyring(ctx, keys, suite) as kr:
-        s = torch.cuda.current_stream(dev).cuda_stream
+        s = None if ctx_stream else torch.cuda.current_stream(dev).cuda_stream
         (sqobfs.quic_seal if seal else sqobfs.quic_open)(ctx, kr, b, s)
+        if ctx_stream:
+            ctx.sync()
         torch.cuda.synchronize(dev)
     return (d_out.cpu().numpy(), out_off, d["out_len"].cpu().numpy(), d["pn_out"].cpu().numpy(),
             out)

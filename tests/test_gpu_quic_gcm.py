@@ -182,3 +182,40 @@ def test_key_grouped_batches(ctx, nkeys, n, inplace):  # noqa: F811
             continue
         assert ol2[i] == len(p) and pno2[i] == pns[i], i
         assert out2[int(oo2[i]):int(oo2[i]) + ol2[i]].tobytes() == p, i
+
+
+@pytest.mark.parametrize("ctx_stream", [False, True])
+def test_ungrouped_fallback_matches_grouped(ctx, ctx_stream):  # noqa: F811
+    """The kernel a multi-key batch falls back to when its grouping scratch
+    cannot be allocated (forced by sqobfs_debug_gcm_ungrouped) gives the same
+    bytes, lengths and packet numbers as the grouped launch.  On the context's
+    own stream the grouping scratch is cached and grows: a smaller batch
+    first, then a larger one, then the smaller again."""
+    rng = np.random.Generator(np.random.PCG64(77))
+    kb, keys = _keys(rng, 16)
+    for n in (4096, 20000, 4096):
+        pkts, pnos, pns = _random_packets(rng, n)
+        kid = rng.integers(0, 16, n)
+        kid[rng.random(n) < 0.01] = 16  # invalid ids: rejected either way
+        res = []
+        for ungrouped in (False, True):
+            sqobfs.debug_gcm_ungrouped(ungrouped)
+            try:
+                out, oo, ol_, _, _ = run(ctx, keys, True, pkts, pnos, pns, key_ids=kid,
+                                         suite=GCM, ctx_stream=ctx_stream)
+                prot = [out[int(oo[i]):int(oo[i]) + int(ol_[i])].tobytes()
+                        if ol_[i] == len(p) + 16 else p + bytes(16) for i, p in enumerate(pkts)]
+                out2, oo2, ol2, pno2, _ = run(ctx, keys, False, prot, pnos, pns, key_ids=kid,
+                                              suite=GCM, ctx_stream=ctx_stream)
+            finally:
+                sqobfs.debug_gcm_ungrouped(False)
+            res.append((prot, ol_.copy(), [out2[int(oo2[i]):int(oo2[i]) + max(0, int(ol2[i]))
+                                               ].tobytes() if ol2[i] < 1 << 31 else b""
+                                           for i in range(n)], ol2.copy(), pno2.copy()))
+        g, u = res
+        assert g[0] == u[0] and np.array_equal(g[1], u[1]), n
+        assert np.array_equal(g[3], u[3]) and np.array_equal(g[4], u[4]), n
+        assert g[2] == u[2], n
+        i = int(np.flatnonzero(kid < 16)[0])
+        want, r = ol.quic_seal(*kb[kid[i]], pns[i], pkts[i], pnos[i], suite=ol.AES128GCM)
+        assert g[0][i] == want and r == len(pkts[i]) + 16
