@@ -613,7 +613,10 @@ typedef struct sqobfs_pconn_opts {
                           batch to grow (0: launch at once) */
   uint32_t spin_us;    /* a worker polls a launch at most this long before it
                           blocks (0 = 200); the engine polls about twice the
-                          launches' recent completion time, within that bound */
+                          launches' recent completion time, within that bound;
+                          SQOBFS_PCONN_NEVER = never poll: block at once on an
+                          interrupt-signalled event (the core is free while
+                          the kernel runs, at a wake-up's latency) */
   uint32_t flags;      /* socket mode: SQOBFS_UDP_TX_GSO (runs of equal-length
                           datagrams to one address go out as UDP_SEGMENT
                           messages; off by itself if the socket refuses) |
@@ -626,7 +629,14 @@ typedef struct sqobfs_pconn_opts {
                           round trip x its recent CPU-path rate, within
                           16 KiB .. 4 MiB, ~80 KiB before any measurement,
                           sqobfs_engine_info.route_bytes; SQOBFS_PCONN_NEVER =
-                          always launch while the GPU works) */
+                          always launch while the GPU works).  With 0, under
+                          sustained load -- the engine's batches would keep
+                          more than a quarter of a core busy on the CPU path
+                          (sqobfs_engine_info.loaded) -- every batch of
+                          more than 64 datagrams launches too, and waits
+                          without polling: the host pays the launch and the
+                          sockets, not the bytes; bursts of up to 64 stay on
+                          the CPU path */
   uint32_t inline_gap_us; /* socket mode: a write made when the transmit side
                           is idle and the previous write is at least this old
                           is obfuscated on the CPU and sent on the writer's own
@@ -733,6 +743,11 @@ typedef struct sqobfs_engine_info {
                             the GPU (0 without a context) */
   uint32_t launch_us;    /* recent launch round trip (EWMA) */
   uint32_t cpu_ns_per_kib; /* recent CPU-path time per KiB of cost (EWMA) */
+  uint32_t load_permille;  /* transform demand: the CPU-path time its batches
+                              would take, per mille of one core's time
+                              (smoothed over 10 ms windows) */
+  uint32_t loaded;         /* 1 while that stays above 250 (off below 120):
+                              batches of more than 64 datagrams launch */
 } sqobfs_engine_info;
 /* ctx NULL: the host engine.  SQ_OK with zeros when it was never started. */
 int sqobfs_engine_info_get(sqobfs_ctx *ctx, sqobfs_engine_info *out);

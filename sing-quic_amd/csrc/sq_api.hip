@@ -295,6 +295,33 @@ int sq_ctx_stream_wait(sqobfs_ctx *ctx, void *s, uint32_t spin_us) {
   return hip_status(hipStreamSynchronize((hipStream_t)s));
 }
 
+namespace {
+// One blocking-sync event per thread and device (engine workers are
+// long-lived threads on one context); destroyed when the thread ends.
+struct BlockingEvents {
+  hipEvent_t ev[64] = {};
+  ~BlockingEvents() {
+    for (hipEvent_t e : ev)
+      if (e) (void)hipEventDestroy(e);
+  }
+};
+thread_local BlockingEvents t_block_ev;
+}  // namespace
+
+int sq_ctx_stream_wait_blocking(sqobfs_ctx *ctx, void *s) {
+  DeviceScope ds_(ctx->device);
+  if (ds_.status != SQ_OK) return ds_.status;
+  if (ctx->device < 0 || ctx->device >= 64) return hip_status(hipStreamSynchronize((hipStream_t)s));
+  hipEvent_t &e = t_block_ev.ev[ctx->device];
+  if (!e && hipEventCreateWithFlags(&e, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess) {
+    e = nullptr;
+    return hip_status(hipStreamSynchronize((hipStream_t)s));
+  }
+  const int st = hip_status(hipEventRecord(e, (hipStream_t)s));
+  if (st != SQ_OK) return st;
+  return hip_status(hipEventSynchronize(e));
+}
+
 int sq_host_alloc_mapped(sqobfs_ctx *ctx, size_t bytes, void **out) {
   const int st = sqobfs_host_alloc(ctx, bytes, out);
   if (st != SQ_OK) return st;

@@ -80,6 +80,16 @@ constexpr uint32_t kDefCpuNsPerKiB = 500;
 constexpr uint64_t kRouteMin = 16u << 10, kRouteMax = 4u << 20;
 constexpr uint64_t kRouteSample = 8u << 10;  // CPU batches at least this costly update the rate
 constexpr uint32_t kHashCost = 1024;      // one key derivation ~ 1 KiB of XOR on a core
+// load-aware routing (cpu_max 0): the engine's transform demand -- the
+// CPU-path time its batches would take per wall second, in per mille of one
+// core, measured over windows of kLoadWindowNs -- above kLoadOnPermille (a
+// quarter of a core: ~1 GiB/s of datagrams each way) turns "loaded" on (off
+// again below kLoadOffPermille); loaded, batches of more than kLoadMinDgrams
+// datagrams launch and wait without polling, so bulk traffic costs the host
+// the launch and the socket work, not the bytes
+constexpr int64_t kLoadWindowNs = 10'000'000;
+constexpr uint32_t kLoadOnPermille = 250, kLoadOffPermille = 120;
+constexpr uint32_t kLoadMinDgrams = 64;
 constexpr uint32_t kDefInlineGapUs = 100;
 constexpr uint32_t kDefWorkers = 4, kMaxWorkers = 64;
 constexpr uint32_t kMaxBatch = 1u << 16;
@@ -230,6 +240,12 @@ struct Engine {
   std::atomic<bool> gpu_off{false};
   std::atomic<uint32_t> launch_us{40};  // recent launch completion time (EWMA)
   std::atomic<uint32_t> cpu_ns_kib{kDefCpuNsPerKiB};  // recent CPU-path ns per KiB of cost (EWMA)
+  // load-aware routing: demand in the current window, its start, the
+  // smoothed demand (permille of the workers' time) and the state
+  std::atomic<uint64_t> demand_ns{0};
+  std::atomic<int64_t> win_t0{0};
+  std::atomic<uint32_t> load_pm{0};
+  std::atomic<bool> loaded{false};
 
   std::mutex pool_mu;
   std::map<std::pair<uint32_t, uint32_t>, std::vector<Block *>> free_blocks;
@@ -469,6 +485,27 @@ uint64_t route_bytes(const Engine *E) {
   return std::min(kRouteMax, std::max(kRouteMin, l * 1000u * 1024u / c));
 }
 
+// Account a batch's transform demand (its estimated CPU-path time, whatever
+// route it takes) and, once a window has passed, update the engine's load.
+void note_demand(Engine *E, uint64_t cost) {
+  const uint64_t est = cost * E->cpu_ns_kib.load(std::memory_order_relaxed) / 1024u;
+  E->demand_ns.fetch_add(est, std::memory_order_relaxed);
+  const int64_t now = mono_ns();
+  int64_t t0 = E->win_t0.load(std::memory_order_relaxed);
+  if (t0 == 0) {
+    E->win_t0.compare_exchange_strong(t0, now);
+    return;
+  }
+  if (now - t0 < kLoadWindowNs || !E->win_t0.compare_exchange_strong(t0, now)) return;
+  const uint64_t d = E->demand_ns.exchange(0, std::memory_order_relaxed);
+  const uint64_t pm = std::min<uint64_t>(100000, d * 1000u / (uint64_t)(now - t0));
+  const uint32_t old = E->load_pm.load(std::memory_order_relaxed);
+  const uint32_t sm = (uint32_t)((old + 3 * pm) / 4);  // (a window's jitter, damped)
+  E->load_pm.store(sm, std::memory_order_relaxed);
+  if (sm >= kLoadOnPermille) E->loaded.store(true, std::memory_order_relaxed);
+  else if (sm < kLoadOffPermille) E->loaded.store(false, std::memory_order_relaxed);
+}
+
 int transform(Engine *E, uint32_t w, sqobfs_pconn *pc, int dir, PBatch &b, bool slotted,
               bool *cpu, bool *failed) {
   *cpu = false;
@@ -486,8 +523,11 @@ int transform(Engine *E, uint32_t w, sqobfs_pconn *pc, int dir, PBatch &b, bool 
   uint64_t cost = 0;
   for (uint32_t i = 0; i < b.n; i++) cost += k.len[i] + kHashCost;
   const uint32_t cmax = pc->o.cpu_max;
+  if (cmax == 0 && E->ctx) note_demand(E, cost);
+  // loaded (cpu_max 0): every batch of more than kLoadMinDgrams launches
+  const bool bulk = cmax == 0 && b.n > kLoadMinDgrams && E->loaded.load(std::memory_order_relaxed);
   const bool want_gpu = E->ctx && !E->gpu_off.load(std::memory_order_relaxed) &&
-                        (cmax == SQOBFS_PCONN_NEVER ||
+                        (cmax == SQOBFS_PCONN_NEVER || bulk ||
                          cost > (cmax == 0 ? route_bytes(E) : (uint64_t)cmax));
   if (want_gpu) {
     // slots are multiples of 16 bytes: every output owns its blocks, so the
@@ -514,8 +554,12 @@ int transform(Engine *E, uint32_t w, sqobfs_pconn *pc, int dir, PBatch &b, bool 
       *failed = true;
     } else {
       const uint32_t ew = E->launch_us.load(std::memory_order_relaxed);
+      // bulk batches and spin_us NEVER block at once (an interrupt-signalled
+      // event: the worker's core is free while the kernel runs)
+      const bool block = bulk || pc->o.spin_us == SQOBFS_PCONN_NEVER;
       const uint32_t spin = std::min<uint32_t>(pc->o.spin_us, 2 * ew + 20);
-      st = sq_ctx_stream_wait(E->ctx, E->streams[w], spin);
+      st = block ? sq_ctx_stream_wait_blocking(E->ctx, E->streams[w])
+                 : sq_ctx_stream_wait(E->ctx, E->streams[w], spin);
       if (inject == 2) st = SQ_EDEVICE;
       if (st != SQ_OK) {
         // the kernel ran, in place, and failed: the slots' state is unknown
@@ -976,6 +1020,8 @@ int sqobfs_engine_info_get(sqobfs_ctx *ctx, sqobfs_engine_info *out) {
   out->route_bytes = E->ctx ? route_bytes(E) : 0u;
   out->launch_us = E->launch_us.load();
   out->cpu_ns_per_kib = E->cpu_ns_kib.load();
+  out->load_permille = E->load_pm.load();
+  out->loaded = E->loaded.load() ? 1u : 0u;
   return SQ_OK;
 }
 

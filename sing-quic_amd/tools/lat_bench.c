@@ -18,7 +18,14 @@
  *   cpu        the oracle's byte-loop WriteTo of one datagram (the
  *              reference's per-call work on one core, no socket)
  * Prints one JSON object (p50 / p99 in microseconds).  Built by
- * `make -C sing-quic_amd tools`; run by bench.py --latency. */
+ * `make -C sing-quic_amd tools`; run by bench.py --latency.
+ *
+ * `lat_bench load [seconds]`: sustained load instead -- pconn A -> pconn B
+ * over loopback (GSO / GRO, 1,024-datagram batches), a writer paced at a
+ * fixed offered rate, for every routing mode: the process's CPU time
+ * (getrusage: every engine thread of both ends, the writer and the reader)
+ * per GiB of payload that arrived, and the batches each route took
+ * ("CPU per GiB"). */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
 #include <errno.h>
@@ -29,6 +36,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/resource.h>
 #include <sys/socket.h>
 #include <time.h>
 #include <unistd.h>
@@ -209,7 +217,117 @@ static void pconn_lat(sqobfs_ctx *ctx, sqobfs_keyring *kr, const char *label,
   close(fp);
 }
 
-int main(void) {
+static double cpu_s(void) {
+  struct rusage ru;
+  getrusage(RUSAGE_SELF, &ru);
+  return ru.ru_utime.tv_sec + ru.ru_utime.tv_usec * 1e-6 + ru.ru_stime.tv_sec +
+         ru.ru_stime.tv_usec * 1e-6;
+}
+
+/* One sustained-load run: `gib_s` of payload offered for `secs` seconds
+ * (0: as fast as the writer goes). */
+static void load_run(const char *name, sqobfs_ctx *c, sqobfs_keyring *k,
+                     const sqobfs_pconn_opts *mode, double gib_s, double secs) {
+  uint16_t pa, pb;
+  int fa = udp_socket(&pa), fb = udp_socket(&pb);
+  int huge = 64 << 20;
+  setsockopt(fb, SOL_SOCKET, SO_RCVBUF, &huge, sizeof huge);
+  setsockopt(fa, SOL_SOCKET, SO_SNDBUF, &huge, sizeof huge);
+  sqobfs_pconn *A, *B;
+  sqobfs_pconn_opts oa = *mode, ob = *mode;
+  oa.flags = SQOBFS_UDP_TX_GSO;
+  ob.flags = SQOBFS_UDP_RX_GRO;
+  oa.batch = ob.batch = 1024;
+  CHECK(sqobfs_pconn_open(c, k, fa, &oa, &A));
+  CHECK(sqobfs_pconn_open(c, k, fb, &ob, &B));
+  const sqobfs_addr to = loop_addr(pb);
+  static uint8_t pay[L];
+  memset(pay, 9, L);
+  struct rd {
+    sqobfs_pconn *pc;
+    long got;
+    double last_us;
+  } r = {B, 0, 0};
+  pthread_t th;
+  extern void *tput_reader(void *);
+  pthread_create(&th, NULL, tput_reader, &r);
+  const double rate = gib_s > 0 ? gib_s * (double)(1 << 30) / L : 0; /* datagrams per s */
+  const double c0 = cpu_s(), t0 = now_us();
+  long n = 0;
+  for (;;) {
+    for (int j = 0; j < 64; j++, n++) CHECK(sqobfs_pconn_write(A, pay, L, &to, 0));
+    const double now = now_us();
+    if (now - t0 >= secs * 1e6) break;
+    if (rate > 0) {
+      const double due = t0 + n / rate * 1e6;
+      if (due > now + 20) {
+        struct timespec ts = {0, (long)((due - now) * 1000)};
+        nanosleep(&ts, NULL);
+      }
+    }
+  }
+  pthread_join(th, NULL); /* (the reader stops 300 ms after the last arrival) */
+  const double c1 = cpu_s();
+  const double dt = (r.last_us - t0) * 1e-6;
+  const double gib = r.got * (double)L / (1 << 30);
+  sqobfs_pconn_stats sa, sb;
+  CHECK(sqobfs_pconn_stats_get(A, &sa));
+  CHECK(sqobfs_pconn_stats_get(B, &sb));
+  sqobfs_engine_info ei;
+  CHECK(sqobfs_engine_info_get(c, &ei));
+  const unsigned long long bt = sa.tx_batches + sb.rx_batches, bc = sa.cpu_batches + sb.cpu_batches;
+  printf("{\"mode\": \"%s\", \"offered_gib_s\": %.3f, \"sent\": %ld, \"received\": %ld, "
+         "\"seconds\": %.3f, \"payload_gib_s\": %.3f, \"cpu_seconds\": %.3f, "
+         "\"cpu_cores\": %.2f, \"cpu_s_per_gib\": %.3f, \"batches\": %llu, "
+         "\"gpu_batches\": %llu, \"cpu_batches\": %llu, \"inline_writes\": %llu, "
+         "\"tx_max_batch\": %u, \"rx_max_batch\": %u, \"load_permille\": %u, \"loaded\": %u}",
+         name, gib_s, n, r.got, dt, gib / dt, c1 - c0, (c1 - c0) / dt, (c1 - c0) / gib, bt, bt - bc,
+         bc, (unsigned long long)sa.inline_writes, sa.tx_max_batch, sb.rx_max_batch,
+         ei.load_permille, ei.loaded);
+  fflush(stdout);
+  sqobfs_pconn_close(A);
+  sqobfs_pconn_close(B);
+  close(fa);
+  close(fb);
+}
+
+static int load_main(double secs) {
+  sqobfs_ctx *ctx;
+  CHECK(sqobfs_open(0, &ctx));
+  uint64_t o0 = 0;
+  uint32_t l0 = PL;
+  sqobfs_keyring *kr, *hk;
+  CHECK(sqobfs_keyring_create(ctx, SQOBFS_SALAMANDER, 1, PSK, &o0, &l0, &kr));
+  CHECK(sqobfs_keyring_create(NULL, SQOBFS_SALAMANDER, 1, PSK, &o0, &l0, &hk));
+  sqobfs_pconn_opts dflt, cpu, gpoll, gblock;
+  memset(&dflt, 0, sizeof dflt);
+  cpu = gpoll = gblock = dflt;
+  cpu.cpu_max = 1u << 30;
+  gpoll.cpu_max = gpoll.inline_gap_us = SQOBFS_PCONN_NEVER;
+  gblock = gpoll;
+  gblock.spin_us = SQOBFS_PCONN_NEVER;
+  static const double rates[] = {0.25, 0.5, 1.0, 2.0, 0};
+  printf("{\"load\": [");
+  int first = 1;
+  for (int ri = 0; ri < 5; ri++)
+    for (int m = 0; m < 5; m++) {
+      if (!first) printf(", ");
+      first = 0;
+      static const char *const names[] = {"default", "cpu_only", "gpu_poll", "gpu_block",
+                                          "no_device"};
+      const sqobfs_pconn_opts *o = m == 0 ? &dflt : m == 1 ? &cpu : m == 2 ? &gpoll
+                                   : m == 3 ? &gblock : &dflt;
+      load_run(names[m], m == 4 ? NULL : ctx, m == 4 ? hk : kr, o, rates[ri], secs);
+    }
+  printf("]}\n");
+  sqobfs_keyring_destroy(hk);
+  sqobfs_keyring_destroy(kr);
+  sqobfs_close(ctx);
+  return 0;
+}
+
+int main(int argc, char **argv) {
+  if (argc > 1 && !strcmp(argv[1], "load")) return load_main(argc > 2 ? atof(argv[2]) : 1.5);
   sqobfs_ctx *ctx;
   CHECK(sqobfs_open(0, &ctx));
   uint64_t off0 = 0;

@@ -27,6 +27,11 @@
  *   fail      injected launch failures: a refused launch is redone on the
  *             CPU, a failed kernel's batch is dropped, and every datagram
  *             after either still reads / writes as the reference's
+ *   load      the default routing under sustained load: bursts of <= 64
+ *             datagrams stay on the CPU path, bulk traffic (the engine's
+ *             transform demand above a quarter of a core) launches batches
+ *             of more than 64 on the GPU; every sampled wire datagram ==
+ *             the reference's WriteTo
  *   poolfail  a receive batch block that cannot be allocated (with nothing
  *             unread to restart the socket task) is retried: the datagram
  *             still reads, within its deadline
@@ -846,6 +851,155 @@ static void t_routing(void) {
   check_mem(a0);
 }
 
+/* ------------------------------------------------------------ load */
+typedef struct {
+  int fd;
+  volatile int stop;
+  long got, checked, bad;
+} LoadPeer;
+
+/* payload of datagram seq: its number, then bytes derived from it */
+static void load_payload(uint32_t seq, uint8_t *p) {
+  memcpy(p, &seq, 4);
+  for (uint32_t j = 4; j < 1350; j++) p[j] = (uint8_t)(seq * 31u + j);
+}
+
+static void *load_peer(void *arg) {
+  LoadPeer *r = arg;
+  enum { M = 64 };
+  static uint8_t buf[M][MAXW];
+  struct mmsghdr h[M];
+  struct iovec iov[M];
+  for (;;) {
+    for (int j = 0; j < M; j++) {
+      iov[j].iov_base = buf[j];
+      iov[j].iov_len = MAXW;
+      memset(&h[j], 0, sizeof h[j]);
+      h[j].msg_hdr.msg_iov = &iov[j];
+      h[j].msg_hdr.msg_iovlen = 1;
+    }
+    struct pollfd p = {r->fd, POLLIN, 0};
+    if (poll(&p, 1, 20) <= 0) {
+      if (r->stop) break;
+      continue;
+    }
+    const int m = recvmmsg(r->fd, h, M, MSG_DONTWAIT, NULL);
+    for (int j = 0; j < m; j++) {
+      r->got++;
+      if ((r->got & 7) && r->got > 64) continue; /* decode one in 8 (oracle byte loops) */
+      uint8_t got[MAXW], want[1350];
+      const long n = ref_read(0, buf[j], h[j].msg_len, MAXW, got);
+      uint32_t seq = 0;
+      if (n == 1350) memcpy(&seq, got, 4);
+      load_payload(seq, want);
+      r->checked++;
+      if (n != 1350 || memcmp(got, want, 1350)) r->bad++;
+    }
+  }
+  return NULL;
+}
+
+static void t_load(void) {
+  const int64_t a0 = sqobfs_debug_host_allocs();
+  sqobfs_keyring *kr = keyring(SQOBFS_SALAMANDER);
+  uint16_t pa, pp;
+  int fa = udp_socket(&pa), fp = udp_socket(&pp);
+  int huge = 64 << 20;
+  setsockopt(fp, SOL_SOCKET, SO_RCVBUF, &huge, sizeof huge);
+  sqobfs_pconn *pc = NULL;
+  sqobfs_pconn_opts o;
+  memset(&o, 0, sizeof o);
+  o.batch = 1024;
+  o.flags = SQOBFS_UDP_TX_GSO;
+  CHECK(sqobfs_pconn_open(g_ctx, kr, fa, &o, &pc));
+  const sqobfs_addr to = loop_addr(pp);
+  LoadPeer r = {fp, 0, 0, 0, 0};
+  pthread_t th;
+  pthread_create(&th, NULL, load_peer, &r);
+  uint8_t pay[1350];
+  uint32_t seq = 0;
+  sqobfs_engine_info ei;
+  /* 1. bursts of 64 with gaps: the CPU path */
+  sqobfs_pconn_stats s0, s1, s2, s3;
+  CHECK(sqobfs_pconn_stats_get(pc, &s0));
+  for (int b = 0; b < 20; b++) {
+    for (int j = 0; j < 64; j++, seq++) {
+      load_payload(seq, pay);
+      CHECK(sqobfs_pconn_write(pc, pay, 1350, &to, 0));
+    }
+    sleep_ms(3);
+  }
+  sleep_ms(20);
+  CHECK(sqobfs_pconn_stats_get(pc, &s1));
+  CHECK(sqobfs_engine_info_get(g_ctx, &ei));
+  const uint64_t route = ei.route_bytes;
+  EXPECT(s1.tx_datagrams - s0.tx_datagrams == 1280, "bursts: %llu of 1280 sent",
+         (unsigned long long)(s1.tx_datagrams - s0.tx_datagrams));
+  if (route >= 64ull * (1350 + 1024))
+    EXPECT(s1.cpu_batches - s0.cpu_batches == s1.tx_batches - s0.tx_batches,
+           "bursts of 64: %llu of %llu batches on the CPU path (route %llu B, load %u)",
+           (unsigned long long)(s1.cpu_batches - s0.cpu_batches),
+           (unsigned long long)(s1.tx_batches - s0.tx_batches), (unsigned long long)route,
+           ei.load_permille);
+  /* 2. sustained: 0.5 s as fast as the writer goes */
+  int loaded = 0;
+  uint32_t pm_max = 0;
+  const double t0 = now_s();
+  while (now_s() - t0 < 0.5) {
+    for (int j = 0; j < 256; j++, seq++) {
+      load_payload(seq, pay);
+      CHECK(sqobfs_pconn_write(pc, pay, 1350, &to, 0));
+    }
+    CHECK(sqobfs_engine_info_get(g_ctx, &ei));
+    loaded |= (int)ei.loaded;
+    if (ei.load_permille > pm_max) pm_max = ei.load_permille;
+  }
+  sleep_ms(50);
+  CHECK(sqobfs_pconn_stats_get(pc, &s2));
+  const uint64_t nb = s2.tx_batches - s1.tx_batches, nc = s2.cpu_batches - s1.cpu_batches;
+  /* (the sanitizer builds' CPU path runs ~10x slower and their writer cannot
+   * offer bulk load: there the load mode is not required to turn on) */
+  CHECK(sqobfs_engine_info_get(g_ctx, &ei));
+  const int slow = ei.cpu_ns_per_kib > 1500;
+  EXPECT(loaded || slow, "sustained load never turned the engine's load mode on (peak %u permille)",
+         pm_max);
+  /* (on the CPU device the batches can stay small: none is eligible) */
+  EXPECT(nb > nc || (slow && !loaded) || s2.tx_max_batch <= 64,
+         "sustained load: no batch launched (%llu batches, all on the CPU path, max %u)",
+         (unsigned long long)nb, s2.tx_max_batch);
+  /* 3. bursts again after the load: on the CPU path (n <= 64) */
+  sleep_ms(30);
+  for (int b = 0; b < 10; b++) {
+    for (int j = 0; j < 64; j++, seq++) {
+      load_payload(seq, pay);
+      CHECK(sqobfs_pconn_write(pc, pay, 1350, &to, 0));
+    }
+    sleep_ms(3);
+  }
+  sleep_ms(20);
+  CHECK(sqobfs_pconn_stats_get(pc, &s3));
+  if (route >= 64ull * (1350 + 1024))
+    EXPECT(s3.cpu_batches - s2.cpu_batches == s3.tx_batches - s2.tx_batches,
+           "bursts after the load: %llu of %llu batches on the CPU path",
+           (unsigned long long)(s3.cpu_batches - s2.cpu_batches),
+           (unsigned long long)(s3.tx_batches - s2.tx_batches));
+  sleep_ms(100);
+  r.stop = 1;
+  pthread_join(th, NULL);
+  EXPECT(r.bad == 0 && r.checked > 100, "load: %ld of %ld decoded datagrams differ", r.bad,
+         r.checked);
+  EXPECT(r.got >= (long)seq / 2, "load: only %ld of %u datagrams arrived", r.got, seq);
+  printf("  load: bursts of 64 on the CPU path; sustained %u datagrams -> %llu batches (max %u), "
+         "%llu launched (peak demand %u permille of a core, loaded %d); %ld arrived, %ld decoded "
+         "== reference\n", seq, (unsigned long long)nb, s2.tx_max_batch,
+         (unsigned long long)(nb - nc), pm_max, loaded, r.got, r.checked);
+  sqobfs_pconn_close(pc);
+  close(fa);
+  close(fp);
+  sqobfs_keyring_destroy(kr);
+  check_mem(a0);
+}
+
 /* ------------------------------------------------------------ poolfail */
 static void t_poolfail(int kind) {
   const int S = salt_len(kind);
@@ -979,6 +1133,7 @@ int main(int argc, char **argv) {
   t_shared();
   if (!g_nodev) {
     t_routing();
+    t_load();
     t_fail(0);
     t_fail(1);
   }
@@ -990,6 +1145,6 @@ int main(int argc, char **argv) {
   printf("ok: pconn engine [%s] (socket + pump modes, deadlines, shutdown, memory, sync errors, "
          "allocation failures, "
          "shared engine%s)\n", g_nodev ? "no device" : "device",
-         g_nodev ? "" : ", routing, launch failures");
+         g_nodev ? "" : ", routing, load routing, launch failures");
   return 0;
 }
