@@ -31,7 +31,10 @@ type Options struct {
 	NoOffload bool          // socket mode: no UDP GSO on send / GRO on receive
 	// CPUMax: batches costing at most this (payload bytes + 1 KiB per
 	// datagram) run on the CPU path, not a launch (0: the engine's measured
-	// break-even, launch round trip x CPU-path rate; < 0: always launch)
+	// break-even, launch round trip x CPU-path rate -- and, while the
+	// engine's traffic would keep more than a quarter of a core busy on the
+	// CPU path, every batch of more than 64 datagrams launches, waiting
+	// without polling; < 0: always launch)
 	CPUMax int
 	// InlineGap: a WriteTo made while the engine is idle, at least this long
 	// after the previous one, is obfuscated and sent on the calling goroutine
@@ -52,7 +55,8 @@ type Options struct {
 //     A WriteTo made while the engine is idle (a handshake, an ACK) is
 //     instead obfuscated on the CPU and sent by the calling goroutine, and
 //     returns its own send error, as the reference's (Options.InlineGap).
-//   - Small batches run on the CPU path (Options.CPUMax); with no usable GPU
+//   - Small batches run on the CPU path (Options.CPUMax), bulk traffic on the
+//     GPU (the engine's load mode, sqobfs_engine_info.loaded); with no usable GPU
 //     every batch does, so NewConn does not fail for want of a device, and a
 //     failed launch moves the engine to the CPU instead of failing the Conn.
 //   - ReadFrom (salamander.go:42-55, xplus.go:46-60) returns the next datagram

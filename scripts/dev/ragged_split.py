@@ -5,14 +5,17 @@ Cases (dense wire layout, Salamander, one PSK, as bench.py builds them):
   F16   configs[1]: 1M x 1350 B at its default unit (16 packets per wave)
   R<u>  configs[3]: 4M x U[64,1452] (mean 758) at its default unit (28)
   C<u>  4M x 758 B constant (same mean) at the ragged default unit
-  R16   the ragged lengths at 16 packets per wave
-  C16   the constant 758 B at 16 packets per wave
+  FB16  2,372,000 x 1350 B at 16: configs[1]'s packets with configs[3]'s
+        footprint (the same input and output bytes)
+  P<u>  1M x 758 B at the ragged unit: configs[3]'s packets per byte with a
+        footprint near configs[1]'s
   B<u>  the ragged lengths reordered inside every run of 4096 packets as
         shortest, longest, 2nd shortest, 2nd longest, ...: the same lengths
         and packets per byte, but every unit holds nearly the same bytes
         (R's unit bytes vary ~10 %)
 R vs C separates length variance from the per-packet fixed cost (same
-packets per byte); R16 / C16 vs F16 separates the packets per wave.
+packets per byte); FB16 and P vs F16 separate the footprint (address
+translation) from the packets per byte.
 usage: ragged_split.py DIRECTION ROUNDS lib1.so [lib2.so ...]
 Prints per lib and case the median kernel time, ns per KiB of algorithmic
 bytes and frac of 8 TB/s; every lib's output of a case is compared with the
@@ -74,10 +77,12 @@ srt = ragged.view(-1, 4096).sort(dim=1).values
 bal = torch.stack([srt[:, :2048], srt[:, 2048:].flip(1)], dim=2).reshape(-1)
 const = torch.full((n4,), 758, device=dev, dtype=torch.int64)
 fixed = torch.full((1 << 20,), 1350, device=dev, dtype=torch.int64)
+fbig = torch.full((2372000,), 1350, device=dev, dtype=torch.int64)
+p758 = torch.full((1 << 20,), 758, device=dev, dtype=torch.int64)
 sqobfs._lib = sqobfs.load(paths[0])
 u_r = sqobfs.unit_packets_for(int(ragged.sum().item()), n4)
 cases = [("F16", fixed, 0), (f"R{u_r}", ragged, u_r), (f"C{u_r}", const, u_r),
-         ("R16", ragged, 16), ("C16", const, 16), (f"B{u_r}", bal, u_r)]
+         ("FB16", fbig, 16), (f"P{u_r}", p758, u_r), (f"B{u_r}", bal, u_r)]
 bufs = {}
 for name, lens, u in cases:
     key = id(lens)

@@ -25,7 +25,13 @@
  * fixed offered rate, for every routing mode: the process's CPU time
  * (getrusage: every engine thread of both ends, the writer and the reader)
  * per GiB of payload that arrived, and the batches each route took
- * ("CPU per GiB"). */
+ * ("CPU per GiB").
+ *
+ * `lat_bench tput [runs]`: the default-routing GSO / GRO throughput run
+ * (200,000 datagrams A -> B) repeated, each with its process CPU time,
+ * involuntary context switches and the cgroup's CPU-quota throttling
+ * (cpu.stat nr_throttled / throttled_usec) over the run: whether a slow run
+ * was a throttled one ("the small-batch regime"). */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
 #include <errno.h>
@@ -217,6 +223,20 @@ static void pconn_lat(sqobfs_ctx *ctx, sqobfs_keyring *kr, const char *label,
   close(fp);
 }
 
+/* the cgroup's CPU throttling counters (v2 cpu.stat; zeros when absent) */
+static void cg_throttle(long long *nr, long long *usec) {
+  *nr = *usec = 0;
+  FILE *f = fopen("/sys/fs/cgroup/cpu.stat", "r");
+  if (!f) return;
+  char k[64];
+  long long v;
+  while (fscanf(f, "%63s %lld", k, &v) == 2) {
+    if (!strcmp(k, "nr_throttled")) *nr = v;
+    if (!strcmp(k, "throttled_usec")) *usec = v;
+  }
+  fclose(f);
+}
+
 static double cpu_s(void) {
   struct rusage ru;
   getrusage(RUSAGE_SELF, &ru);
@@ -326,8 +346,89 @@ static int load_main(double secs) {
   return 0;
 }
 
+/* One default-routing throughput run (the main table's pconn_throughput
+ * _gso_gro line) with its CPU, context-switch and throttling counters. */
+static void tput_run(sqobfs_ctx *ctx, sqobfs_keyring *kr, int run, int last) {
+  uint16_t pa, pb;
+  int fa = udp_socket(&pa), fb = udp_socket(&pb);
+  sqobfs_pconn *A, *B;
+  sqobfs_pconn_opts oa, ob;
+  memset(&oa, 0, sizeof oa);
+  memset(&ob, 0, sizeof ob);
+  oa.flags = SQOBFS_UDP_TX_GSO;
+  ob.flags = SQOBFS_UDP_RX_GRO;
+  CHECK(sqobfs_pconn_open(ctx, kr, fa, &oa, &A));
+  CHECK(sqobfs_pconn_open(ctx, kr, fb, &ob, &B));
+  const sqobfs_addr to = loop_addr(pb);
+  static uint8_t pay[L];
+  memset(pay, 9, L);
+  struct rd {
+    sqobfs_pconn *pc;
+    long got;
+    double last_us;
+  } r = {B, 0, 0};
+  pthread_t th;
+  extern void *tput_reader(void *);
+  pthread_create(&th, NULL, tput_reader, &r);
+  struct rusage u0, u1, w0, w1;
+  long long nr0, us0, nr1, us1;
+  cg_throttle(&nr0, &us0);
+  getrusage(RUSAGE_SELF, &u0);
+  getrusage(RUSAGE_THREAD, &w0);
+  const long N = 200000;
+  const double t0 = now_us();
+  for (long i = 0; i < N; i++) {
+    CHECK(sqobfs_pconn_write(A, pay, L, &to, 0));
+    if ((i & 1023) == 1023) {
+      struct timespec ts = {0, 200000};
+      nanosleep(&ts, NULL);
+    }
+  }
+  getrusage(RUSAGE_THREAD, &w1);
+  pthread_join(th, NULL);
+  getrusage(RUSAGE_SELF, &u1);
+  cg_throttle(&nr1, &us1);
+  const double dt = (r.last_us - t0) * 1e-6;
+  sqobfs_pconn_stats sa, sb;
+  CHECK(sqobfs_pconn_stats_get(A, &sa));
+  CHECK(sqobfs_pconn_stats_get(B, &sb));
+#define TV(a) ((a).tv_sec + (a).tv_usec * 1e-6)
+  printf("{\"run\": %d, \"received\": %ld, \"seconds\": %.3f, \"datagrams_per_s\": %.0f, "
+         "\"tx_batches\": %llu, \"rx_batches\": %llu, \"cpu_s\": %.3f, \"writer_cpu_s\": %.3f, "
+         "\"nivcsw\": %ld, \"nvcsw\": %ld, \"writer_nivcsw\": %ld, \"throttled_periods\": %lld, "
+         "\"throttled_ms\": %.1f}%s\n",
+         run, r.got, dt, r.got / dt, (unsigned long long)sa.tx_batches,
+         (unsigned long long)sb.rx_batches,
+         TV(u1.ru_utime) + TV(u1.ru_stime) - TV(u0.ru_utime) - TV(u0.ru_stime),
+         TV(w1.ru_utime) + TV(w1.ru_stime) - TV(w0.ru_utime) - TV(w0.ru_stime),
+         u1.ru_nivcsw - u0.ru_nivcsw, u1.ru_nvcsw - u0.ru_nvcsw, w1.ru_nivcsw - w0.ru_nivcsw,
+         nr1 - nr0, (us1 - us0) * 1e-3, last ? "" : ",");
+#undef TV
+  fflush(stdout);
+  sqobfs_pconn_close(A);
+  sqobfs_pconn_close(B);
+  close(fa);
+  close(fb);
+}
+
+static int tput_main(int runs) {
+  sqobfs_ctx *ctx;
+  CHECK(sqobfs_open(0, &ctx));
+  uint64_t o0 = 0;
+  uint32_t l0 = PL;
+  sqobfs_keyring *kr;
+  CHECK(sqobfs_keyring_create(ctx, SQOBFS_SALAMANDER, 1, PSK, &o0, &l0, &kr));
+  printf("{\"tput_gso_gro\": [\n");
+  for (int i = 0; i < runs; i++) tput_run(ctx, kr, i, i == runs - 1);
+  printf("]}\n");
+  sqobfs_keyring_destroy(kr);
+  sqobfs_close(ctx);
+  return 0;
+}
+
 int main(int argc, char **argv) {
   if (argc > 1 && !strcmp(argv[1], "load")) return load_main(argc > 2 ? atof(argv[2]) : 1.5);
+  if (argc > 1 && !strcmp(argv[1], "tput")) return tput_main(argc > 2 ? atoi(argv[2]) : 45);
   sqobfs_ctx *ctx;
   CHECK(sqobfs_open(0, &ctx));
   uint64_t off0 = 0;
