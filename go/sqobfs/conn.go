@@ -32,9 +32,9 @@ type Options struct {
 	// CPUMax: batches costing at most this (payload bytes + 1 KiB per
 	// datagram) run on the CPU path, not a launch (0: the engine's measured
 	// break-even, launch round trip x CPU-path rate -- and, while the
-	// engine's traffic would keep more than a quarter of a core busy on the
-	// CPU path, every batch of more than 64 datagrams launches, waiting
-	// without polling; < 0: always launch)
+	// engine's traffic would keep more than a tenth of a core busy on the
+	// CPU path, a batch of more than 64 datagrams launches, waiting without
+	// polling, when that costs the host less CPU; < 0: always launch)
 	CPUMax int
 	// InlineGap: a WriteTo made while the engine is idle, at least this long
 	// after the previous one, is obfuscated and sent on the calling goroutine

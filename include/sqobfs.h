@@ -631,12 +631,14 @@ typedef struct sqobfs_pconn_opts {
                           sqobfs_engine_info.route_bytes; SQOBFS_PCONN_NEVER =
                           always launch while the GPU works).  With 0, under
                           sustained load -- the engine's batches would keep
-                          more than a quarter of a core busy on the CPU path
-                          (sqobfs_engine_info.loaded) -- every batch of
-                          more than 64 datagrams launches too, and waits
-                          without polling: the host pays the launch and the
-                          sockets, not the bytes; bursts of up to 64 stay on
-                          the CPU path */
+                          more than a tenth of a core busy on the CPU path
+                          (sqobfs_engine_info.loaded) -- a batch of more than
+                          64 datagrams also launches, waiting without
+                          polling, when its CPU-path time exceeds the host
+                          CPU time a launched batch costs (measured,
+                          sqobfs_engine_info.gpu_host_ns): the host pays the
+                          launch and the sockets, not the bytes; bursts of up
+                          to 64 stay on the CPU path */
   uint32_t inline_gap_us; /* socket mode: a write made when the transmit side
                           is idle and the previous write is at least this old
                           is obfuscated on the CPU and sent on the writer's own
@@ -746,8 +748,10 @@ typedef struct sqobfs_engine_info {
   uint32_t load_permille;  /* transform demand: the CPU-path time its batches
                               would take, per mille of one core's time
                               (smoothed over 10 ms windows) */
-  uint32_t loaded;         /* 1 while that stays above 250 (off below 120):
-                              batches of more than 64 datagrams launch */
+  uint32_t loaded;         /* 1 while that stays above 100 (off below 50):
+                              batches of more than 64 datagrams may launch */
+  uint32_t gpu_host_ns;    /* host CPU time of a launched batch with a
+                              blocking wait (launch call + wait; EWMA) */
 } sqobfs_engine_info;
 /* ctx NULL: the host engine.  SQ_OK with zeros when it was never started. */
 int sqobfs_engine_info_get(sqobfs_ctx *ctx, sqobfs_engine_info *out);

@@ -82,14 +82,18 @@ constexpr uint64_t kRouteSample = 8u << 10;  // CPU batches at least this costly
 constexpr uint32_t kHashCost = 1024;      // one key derivation ~ 1 KiB of XOR on a core
 // load-aware routing (cpu_max 0): the engine's transform demand -- the
 // CPU-path time its batches would take per wall second, in per mille of one
-// core, measured over windows of kLoadWindowNs -- above kLoadOnPermille (a
-// quarter of a core: ~1 GiB/s of datagrams each way) turns "loaded" on (off
-// again below kLoadOffPermille); loaded, batches of more than kLoadMinDgrams
-// datagrams launch and wait without polling, so bulk traffic costs the host
-// the launch and the socket work, not the bytes
+// core, measured over windows of kLoadWindowNs -- above kLoadOnPermille turns
+// "loaded" on (off again below kLoadOffPermille).  Loaded, the host's CPU
+// time is what the routing saves, not a batch's latency: a batch of more
+// than kLoadMinDgrams datagrams launches (and waits without polling) when
+// its CPU-path time is more than a launch costs the host -- the worker
+// thread's own CPU time per launched batch, launch call and blocking wait,
+// measured (gpu_host_ns) -- so bulk traffic costs the host the launch and
+// the socket work, not the bytes
 constexpr int64_t kLoadWindowNs = 10'000'000;
-constexpr uint32_t kLoadOnPermille = 250, kLoadOffPermille = 120;
+constexpr uint32_t kLoadOnPermille = 100, kLoadOffPermille = 50;
 constexpr uint32_t kLoadMinDgrams = 64;
+constexpr uint32_t kDefGpuHostNs = 20'000;  // before the first launch is measured
 constexpr uint32_t kDefInlineGapUs = 100;
 constexpr uint32_t kDefWorkers = 4, kMaxWorkers = 64;
 constexpr uint32_t kMaxBatch = 1u << 16;
@@ -116,6 +120,11 @@ bool take_one(std::atomic<int> &c) {
 int64_t unix_ns() {
   timespec ts;
   clock_gettime(CLOCK_REALTIME, &ts);
+  return (int64_t)ts.tv_sec * 1000000000 + ts.tv_nsec;
+}
+int64_t thread_cpu_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
   return (int64_t)ts.tv_sec * 1000000000 + ts.tv_nsec;
 }
 int64_t mono_ns() {
@@ -246,6 +255,7 @@ struct Engine {
   std::atomic<int64_t> win_t0{0};
   std::atomic<uint32_t> load_pm{0};
   std::atomic<bool> loaded{false};
+  std::atomic<uint32_t> gpu_host_ns{kDefGpuHostNs};  // host CPU per launched batch (EWMA)
 
   std::mutex pool_mu;
   std::map<std::pair<uint32_t, uint32_t>, std::vector<Block *>> free_blocks;
@@ -524,8 +534,12 @@ int transform(Engine *E, uint32_t w, sqobfs_pconn *pc, int dir, PBatch &b, bool 
   for (uint32_t i = 0; i < b.n; i++) cost += k.len[i] + kHashCost;
   const uint32_t cmax = pc->o.cpu_max;
   if (cmax == 0 && E->ctx) note_demand(E, cost);
-  // loaded (cpu_max 0): every batch of more than kLoadMinDgrams launches
-  const bool bulk = cmax == 0 && b.n > kLoadMinDgrams && E->loaded.load(std::memory_order_relaxed);
+  // loaded (cpu_max 0): a batch of more than kLoadMinDgrams launches when
+  // the CPU path would cost the host more than a launch does
+  const bool bulk = cmax == 0 && b.n > kLoadMinDgrams &&
+                    E->loaded.load(std::memory_order_relaxed) &&
+                    cost * E->cpu_ns_kib.load(std::memory_order_relaxed) / 1024u >
+                        E->gpu_host_ns.load(std::memory_order_relaxed);
   const bool want_gpu = E->ctx && !E->gpu_off.load(std::memory_order_relaxed) &&
                         (cmax == SQOBFS_PCONN_NEVER || bulk ||
                          cost > (cmax == 0 ? route_bytes(E) : (uint64_t)cmax));
@@ -543,7 +557,7 @@ int transform(Engine *E, uint32_t w, sqobfs_pconn *pc, int dir, PBatch &b, bool 
       E->streams[w] = s;
     }
     const int inject = take_one(g_fail_count) ? (g_fail_at_completion.load() ? 2 : 1) : 0;
-    const int64_t t0 = mono_ns();
+    const int64_t t0 = mono_ns(), c0 = thread_cpu_ns();
     if (st == SQ_OK) st = inject == 1 ? SQ_EDEVICE : sqobfs_launch(E->ctx, pc->kr, dir, &d, E->streams[w]);
     if (st != SQ_OK) {
       // refused before anything ran: the batch is intact, redo it on the CPU.
@@ -569,6 +583,11 @@ int transform(Engine *E, uint32_t w, sqobfs_pconn *pc, int dir, PBatch &b, bool 
       }
       const uint32_t us = (uint32_t)std::min<int64_t>((mono_ns() - t0) / 1000, 100000);
       E->launch_us.store((7 * ew + us) / 8, std::memory_order_relaxed);
+      if (block) {  // the host's cost of a launched batch (polled waits would count their spin)
+        const uint32_t hn = (uint32_t)std::min<int64_t>(thread_cpu_ns() - c0, 10'000'000);
+        const uint32_t eh = E->gpu_host_ns.load(std::memory_order_relaxed);
+        E->gpu_host_ns.store((7 * eh + hn) / 8, std::memory_order_relaxed);
+      }
       return SQ_OK;
     }
   }
@@ -1022,6 +1041,7 @@ int sqobfs_engine_info_get(sqobfs_ctx *ctx, sqobfs_engine_info *out) {
   out->cpu_ns_per_kib = E->cpu_ns_kib.load();
   out->load_permille = E->load_pm.load();
   out->loaded = E->loaded.load() ? 1u : 0u;
+  out->gpu_host_ns = E->gpu_host_ns.load();
   return SQ_OK;
 }
 

@@ -422,7 +422,8 @@ class EngineInfo(ctypes.Structure):
                 ("pool_bytes", ctypes.c_uint64), ("blocks_in_use", ctypes.c_uint32),
                 ("gpu_disabled", ctypes.c_uint32), ("route_bytes", ctypes.c_uint64),
                 ("launch_us", ctypes.c_uint32), ("cpu_ns_per_kib", ctypes.c_uint32),
-                ("load_permille", ctypes.c_uint32), ("loaded", ctypes.c_uint32)]
+                ("load_permille", ctypes.c_uint32), ("loaded", ctypes.c_uint32),
+                ("gpu_host_ns", ctypes.c_uint32)]
 
 
 def engine_info(ctx: Context | None) -> EngineInfo:

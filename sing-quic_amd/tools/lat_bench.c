@@ -300,10 +300,11 @@ static void load_run(const char *name, sqobfs_ctx *c, sqobfs_keyring *k,
          "\"seconds\": %.3f, \"payload_gib_s\": %.3f, \"cpu_seconds\": %.3f, "
          "\"cpu_cores\": %.2f, \"cpu_s_per_gib\": %.3f, \"batches\": %llu, "
          "\"gpu_batches\": %llu, \"cpu_batches\": %llu, \"inline_writes\": %llu, "
-         "\"tx_max_batch\": %u, \"rx_max_batch\": %u, \"load_permille\": %u, \"loaded\": %u}",
+         "\"tx_max_batch\": %u, \"rx_max_batch\": %u, \"load_permille\": %u, \"loaded\": %u, "
+         "\"gpu_host_ns\": %u, \"cpu_ns_per_kib\": %u, \"launch_us\": %u}",
          name, gib_s, n, r.got, dt, gib / dt, c1 - c0, (c1 - c0) / dt, (c1 - c0) / gib, bt, bt - bc,
          bc, (unsigned long long)sa.inline_writes, sa.tx_max_batch, sb.rx_max_batch,
-         ei.load_permille, ei.loaded);
+         ei.load_permille, ei.loaded, ei.gpu_host_ns, ei.cpu_ns_per_kib, ei.launch_us);
   fflush(stdout);
   sqobfs_pconn_close(A);
   sqobfs_pconn_close(B);

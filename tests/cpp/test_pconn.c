@@ -29,7 +29,7 @@
  *             after either still reads / writes as the reference's
  *   load      the default routing under sustained load: bursts of <= 64
  *             datagrams stay on the CPU path, bulk traffic (the engine's
- *             transform demand above a quarter of a core) launches batches
+ *             transform demand above a tenth of a core) launches batches
  *             of more than 64 on the GPU; every sampled wire datagram ==
  *             the reference's WriteTo
  *   poolfail  a receive batch block that cannot be allocated (with nothing
