@@ -864,7 +864,7 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
   // special blocks loadable: every input block of the packet's flat blocks
   // is 16-byte aligned and its special ones hold a payload byte (mapped)
   const uint64_t pe = J.src_pay + J.len;
-  const bool sp_ok = !F || ((sabs & 15) == 0 && npad == 0 &&
+  const bool sp_ok = !F || ((sabs & 15) == 0 && npad == 0 && !ovl &&
                             (!G.hf || (J.len && J.src_pay < sabs + 16 && pe > sabs)) &&
                             (!(G.hl && G.lfull) ||
                              (J.len && pe > sabs + 16ull * (nblk - 1) &&
@@ -942,7 +942,7 @@ __device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
                                           const uint32_t (&salt)[4], bool do_hash, uint32_t pid,
                                           const PskHot &hot,
                                           const Windows &W, bool owner, uint32_t lane,
-                                          bool ob, const Geo &G, WaveLds &L) {
+                                          bool ob, bool ldsp, const Geo &G, WaveLds &L) {
   constexpr uint32_t S = KIND == 0 ? kSalamanderSalt : kXPlusSalt;
   constexpr uint32_t PW = DIR == 0 ? S / 4 : 0;  // salt words in front of the payload
   uint32_t key[8];
@@ -1036,6 +1036,19 @@ __device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
     win16(w, 16 - t, sh);
 #pragma unroll
     for (int j = 0; j < 4; j++) vl[j] = (ti[j] & range_mask(0, (int)t, j)) | (ob ? 0u : sh[j]);
+  }
+  if (ldsp) {
+    // the stream loads the special blocks too (SQ_LDSPECIAL) and XORs what
+    // it loads: their "keystream" is their value ^ their input block, which
+    // a window holds (input and output 16-byte phases agree: plan_unit)
+    if (G.hf) {
+      vf[0] ^= wh0.x; vf[1] ^= wh0.y; vf[2] ^= wh0.z; vf[3] ^= wh0.w;
+    }
+    if (G.lfull) {
+      const uint32_t kb = (uint32_t)((BL - (J.dst_pay & ~15ull)) >> 4);
+      const u32x4 ti4 = tail_from_window(rs, re) ? W.t0 : (kb == 0 ? wh0 : (kb == 1 ? wh1 : wh2));
+      vl[0] ^= ti4.x; vl[1] ^= ti4.y; vl[2] ^= ti4.z; vl[3] ^= ti4.w;
+    }
   }
   uint32_t k0[4], k1[4];
   const uint32_t ph = (uint32_t)(G.B0 - J.dst_pay) & 31u;
@@ -1244,7 +1257,7 @@ __global__ __launch_bounds__(WPB * kWave) void obfs_kernel(const KParams P) {
   const uint32_t pid = MULTI && d.pid < P.n_psk ? d.pid : 0u;
   reload_windows<DIR, kSalt>(J, do_hash, W);
   // 2 + 3b. key and block contents
-  fill_unit<KIND, DIR, MULTI>(P, J, salt, do_hash, pid, hot, W, owner, lane, ob, G, L);
+  fill_unit<KIND, DIR, MULTI>(P, J, salt, do_hash, pid, hot, W, owner, lane, ob, S.ldsp, G, L);
   SQ_STAMP(3);
   // 4. the stream
   if (S.fast && S.map) {

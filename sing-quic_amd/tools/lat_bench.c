@@ -31,7 +31,11 @@
  * (200,000 datagrams A -> B) repeated, each with its process CPU time,
  * involuntary context switches and the cgroup's CPU-quota throttling
  * (cpu.stat nr_throttled / throttled_usec) over the run: whether a slow run
- * was a throttled one ("the small-batch regime"). */
+ * was a throttled one, and how many L3 domains (CCDs) the process's threads
+ * last ran on ("the small-batch regime").
+ * `lat_bench tput [runs] pin`: the process (and so every engine thread it
+ * starts) restricted to the CPUs that share the L3 of the CPU it starts
+ * on, within its affinity. */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
 #include <errno.h>
@@ -42,6 +46,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <dirent.h>
+#include <sched.h>
 #include <sys/resource.h>
 #include <sys/socket.h>
 #include <time.h>
@@ -237,6 +243,69 @@ static void cg_throttle(long long *nr, long long *usec) {
   fclose(f);
 }
 
+/* L3 (CCD) id of a CPU, -1 when unknown */
+static int l3_of(int cpu) {
+  char path[128];
+  snprintf(path, sizeof path, "/sys/devices/system/cpu/cpu%d/cache/index3/id", cpu);
+  FILE *f = fopen(path, "r");
+  if (!f) return -1;
+  int id = -1;
+  if (fscanf(f, "%d", &id) != 1) id = -1;
+  fclose(f);
+  return id;
+}
+
+/* distinct L3 domains the process's threads last ran on, and the threads */
+static int l3_spread(int *threads) {
+  int ids[64], nid = 0;
+  *threads = 0;
+  DIR *d = opendir("/proc/self/task");
+  if (!d) return -1;
+  struct dirent *e;
+  while ((e = readdir(d))) {
+    if (e->d_name[0] == '.') continue;
+    char path[300], buf[1024];
+    snprintf(path, sizeof path, "/proc/self/task/%s/stat", e->d_name);
+    FILE *f = fopen(path, "r");
+    if (!f) continue;
+    const size_t n = fread(buf, 1, sizeof buf - 1, f);
+    fclose(f);
+    buf[n] = 0;
+    const char *p = strrchr(buf, ')'); /* fields after the command name */
+    if (!p) continue;
+    int field = 2, cpu = -1;
+    for (const char *q = p + 1; *q; q++)
+      if (*q == ' ' && ++field == 39) {
+        cpu = atoi(q + 1);
+        break;
+      }
+    if (cpu < 0) continue;
+    (*threads)++;
+    const int id = l3_of(cpu);
+    int seen = 0;
+    for (int i = 0; i < nid; i++) seen |= ids[i] == id;
+    if (!seen && nid < 64) ids[nid++] = id;
+  }
+  closedir(d);
+  return nid;
+}
+
+/* restrict the process to the allowed CPUs sharing this CPU's L3 */
+static int pin_to_l3(void) {
+  cpu_set_t cur, want;
+  if (sched_getaffinity(0, sizeof cur, &cur)) return 0;
+  const int me = sched_getcpu(), l3 = l3_of(me);
+  CPU_ZERO(&want);
+  int n = 0;
+  for (int c = 0; c < CPU_SETSIZE; c++)
+    if (CPU_ISSET(c, &cur) && l3_of(c) == l3) {
+      CPU_SET(c, &want);
+      n++;
+    }
+  if (n && sched_setaffinity(0, sizeof want, &want)) return 0;
+  return n;
+}
+
 static double cpu_s(void) {
   struct rusage ru;
   getrusage(RUSAGE_SELF, &ru);
@@ -389,6 +458,8 @@ static void tput_run(sqobfs_ctx *ctx, sqobfs_keyring *kr, int run, int last) {
   pthread_join(th, NULL);
   getrusage(RUSAGE_SELF, &u1);
   cg_throttle(&nr1, &us1);
+  int nthr;
+  const int l3 = l3_spread(&nthr);
   const double dt = (r.last_us - t0) * 1e-6;
   sqobfs_pconn_stats sa, sb;
   CHECK(sqobfs_pconn_stats_get(A, &sa));
@@ -397,13 +468,13 @@ static void tput_run(sqobfs_ctx *ctx, sqobfs_keyring *kr, int run, int last) {
   printf("{\"run\": %d, \"received\": %ld, \"seconds\": %.3f, \"datagrams_per_s\": %.0f, "
          "\"tx_batches\": %llu, \"rx_batches\": %llu, \"cpu_s\": %.3f, \"writer_cpu_s\": %.3f, "
          "\"nivcsw\": %ld, \"nvcsw\": %ld, \"writer_nivcsw\": %ld, \"throttled_periods\": %lld, "
-         "\"throttled_ms\": %.1f}%s\n",
+         "\"throttled_ms\": %.1f, \"l3_domains\": %d, \"threads\": %d}%s\n",
          run, r.got, dt, r.got / dt, (unsigned long long)sa.tx_batches,
          (unsigned long long)sb.rx_batches,
          TV(u1.ru_utime) + TV(u1.ru_stime) - TV(u0.ru_utime) - TV(u0.ru_stime),
          TV(w1.ru_utime) + TV(w1.ru_stime) - TV(w0.ru_utime) - TV(w0.ru_stime),
          u1.ru_nivcsw - u0.ru_nivcsw, u1.ru_nvcsw - u0.ru_nvcsw, w1.ru_nivcsw - w0.ru_nivcsw,
-         nr1 - nr0, (us1 - us0) * 1e-3, last ? "" : ",");
+         nr1 - nr0, (us1 - us0) * 1e-3, l3, nthr, last ? "" : ",");
 #undef TV
   fflush(stdout);
   sqobfs_pconn_close(A);
@@ -412,14 +483,20 @@ static void tput_run(sqobfs_ctx *ctx, sqobfs_keyring *kr, int run, int last) {
   close(fb);
 }
 
-static int tput_main(int runs) {
+static int tput_main(int runs, int pin) {
+  const int pinned = pin ? pin_to_l3() : 0;
+  long long nr, us;
+  FILE *cs = fopen("/sys/fs/cgroup/cpu.stat", "r");
+  if (cs) fclose(cs);
+  cg_throttle(&nr, &us);
   sqobfs_ctx *ctx;
   CHECK(sqobfs_open(0, &ctx));
   uint64_t o0 = 0;
   uint32_t l0 = PL;
   sqobfs_keyring *kr;
   CHECK(sqobfs_keyring_create(ctx, SQOBFS_SALAMANDER, 1, PSK, &o0, &l0, &kr));
-  printf("{\"tput_gso_gro\": [\n");
+  printf("{\"pinned_cpus\": %d, \"cgroup_cpu_stat\": %s, \"tput_gso_gro\": [\n", pinned,
+         cs ? "true" : "false");
   for (int i = 0; i < runs; i++) tput_run(ctx, kr, i, i == runs - 1);
   printf("]}\n");
   sqobfs_keyring_destroy(kr);
@@ -429,7 +506,8 @@ static int tput_main(int runs) {
 
 int main(int argc, char **argv) {
   if (argc > 1 && !strcmp(argv[1], "load")) return load_main(argc > 2 ? atof(argv[2]) : 1.5);
-  if (argc > 1 && !strcmp(argv[1], "tput")) return tput_main(argc > 2 ? atoi(argv[2]) : 45);
+  if (argc > 1 && !strcmp(argv[1], "tput"))
+    return tput_main(argc > 2 ? atoi(argv[2]) : 45, argc > 3 && !strcmp(argv[3], "pin"));
   sqobfs_ctx *ctx;
   CHECK(sqobfs_open(0, &ctx));
   uint64_t off0 = 0;
