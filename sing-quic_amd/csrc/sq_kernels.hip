@@ -881,6 +881,7 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
   const bool mis = has_int && (sabs & 3);
   const bool sok = s_hi <= s_lo || s_hi - s_lo <= kMaxSpan;
   U.fast = T0 != 0 && __ballot(mis) == 0 && d_hi - d_lo <= kMaxSpan && sok;
+  U.ldsp = U.ldsp && U.fast;  // (the generic path never loads special blocks)
   // map path (buffer streaming only: the generic path walks [0, T) by
   // `locate`): shift the flat space so that slot c sits at d_lo's line phase
   const uint32_t phase = U.map && U.fast && SQ_ALIGN
