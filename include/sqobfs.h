@@ -752,12 +752,24 @@ typedef struct sqobfs_engine_info {
                               batches of more than 64 datagrams may launch */
   uint32_t gpu_host_ns;    /* host CPU time of a launched batch with a
                               blocking wait (launch call + wait; EWMA) */
+  uint32_t cpus;           /* CPUs the engine's threads are kept on (the L3
+                              domain of the thread that started it; 0 = not
+                              restricted: sqobfs_engine_set_affinity) */
 } sqobfs_engine_info;
 /* ctx NULL: the host engine.  SQ_OK with zeros when it was never started. */
 int sqobfs_engine_info_get(sqobfs_ctx *ctx, sqobfs_engine_info *out);
 /* Worker threads of the context's engine (0 = 4); only before its first
  * pconn opens (SQ_EINVAL after). */
 int sqobfs_engine_set_workers(sqobfs_ctx *ctx, uint32_t workers);
+/* Where the engine's threads run: SQOBFS_ENGINE_AFFINITY_L3 (the default)
+ * keeps the workers and the poller on the CPUs of the process's affinity that
+ * share the L3 cache (the CCD) of the thread that starts the engine -- the
+ * first pconn open -- so its hand-offs stay in one cache; _NONE leaves them
+ * to the scheduler.  Only before the context's first pconn opens (SQ_EINVAL
+ * after). */
+#define SQOBFS_ENGINE_AFFINITY_NONE 0
+#define SQOBFS_ENGINE_AFFINITY_L3 1
+int sqobfs_engine_set_affinity(sqobfs_ctx *ctx, int mode);
 /* Free the pool's unused blocks; returns how many were freed. */
 int sqobfs_engine_trim(sqobfs_ctx *ctx);
 /* Test hook: the next `count` launches of every engine fail -- at submission

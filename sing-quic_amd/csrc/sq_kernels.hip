@@ -91,18 +91,6 @@ namespace sq {
 #ifndef SQ_PSKPRE
 #define SQ_PSKPRE 1
 #endif
-// 1: the stream loads special blocks too when every special block of the
-// wave has its input in a 16-byte-aligned block holding a payload byte (so
-// it is mapped); the loaded value is discarded (no read holes)
-#ifndef SQ_LDSPECIAL
-#define SQ_LDSPECIAL 0
-#endif
-// 1: device salts by quads (each quad of lanes computes one ChaCha20 block,
-// one state column per lane, DPP rotations for the diagonal rounds; the
-// wave's blocks staged in LDS); 0: one whole block per lane
-#ifndef SQ_QSALT
-#define SQ_QSALT 0
-#endif
 // Timeline builds (scripts/dev/timeline.py, never shipped): lane 0 of every
 // wave records the constant-rate clock at its phase boundaries.
 #ifndef SQ_TIMELINE
@@ -245,31 +233,10 @@ __device__ __forceinline__ uint32_t shfl32(uint32_t x, uint32_t src) {
 
 // ------------------------------------------------------------ per-packet steps
 
-// Device salt of packet p (SQOBFS_FLAG_DEVICE_SALT): bytes [(p % (64/S))*S,
-// +S) of ChaCha20 keystream block p / (64/S), so the batch's salts are the
-// keystream's first n*S bytes.  Each lane computes its own packet's block
-// (lanes sharing a block compute it redundantly: same instruction stream).
-template <uint32_t S>
-__device__ __forceinline__ void device_salt_words(const KParams &P, uint32_t p,
-                                                  uint32_t (&salt)[4]) {
-  constexpr uint32_t per_block = 64 / S;  // 8 Salamander, 4 XPlus
-  uint32_t blk[16];
-  chacha20_block(P.salt_key, p / per_block, P.salt_nonce, blk);
-  // word offset (p % per_block) * S/4: barrel-select S/4 words
-  const uint32_t q = (p % per_block) * (S / 4);
-  uint32_t y[16];
-#pragma unroll
-  for (int j = 0; j < 16; j++) y[j] = blk[j];
-#pragma unroll
-  for (int sh = 8; sh >= 1; sh >>= 1) {
-    const bool b = q & sh;
-#pragma unroll
-    for (int j = 0; j + sh < 16; j++) y[j] = bsel(b, y[j + sh], y[j]);
-  }
-#pragma unroll
-  for (uint32_t k = 0; k < S / 4; k++) salt[k] = y[k];
-}
-
+// Device salts (SQOBFS_FLAG_DEVICE_SALT): the salt of packet p is bytes
+// [(p % (64/S))*S, +S) of ChaCha20 keystream block p / (64/S), so a batch's
+// salts are the keystream's first n*S bytes.
+//
 // Quad ChaCha20 (RFC 8439 2.3): the 4 lanes of a quad hold one block's state
 // column by column (lane i: words i, 4 + i, 8 + i, 12 + i).  The column
 // round is one quarter round per lane; the diagonal round rotates rows 1-3
@@ -385,10 +352,7 @@ __device__ __forceinline__ void fetch_desc(const KParams &P, uint32_t p, bool va
 #pragma unroll
     for (uint32_t k = 0; k < S / 4; k++) d.salt[k] = sp[k];
   }
-  // device salts depend on p alone: computed while the loads above fly
-  // (round 4, profiles/r04/ab2: configs[1] with device salts -2.6 %, XPlus
-  // -0.8 %, against computing them after the loads land)
-  if (DIR == 0 && P.device_salt && !SQ_QSALT) device_salt_words<S>(P, p, d.salt);
+  // (device salts: device_salts_wave, while these loads fly)
 }
 
 template <int KIND, int DIR, bool MULTI>
@@ -749,7 +713,6 @@ struct UnitStream {
   uint32_t cst;    // lane: flat start of the packet of rank `lane` (~0 past the last)
   uint32_t T;      // wave-uniform: blocks in the flat space
   bool fast;       // wave-uniform: buffer-resource streaming possible
-  bool ldsp;       // wave-uniform: special blocks' inputs loaded too (SQ_LDSPECIAL)
   bool map;        // wave-uniform: the bit map covers the flat space
   WaveBufs B;
 };
@@ -859,19 +822,9 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
   const uint32_t T0 = __builtin_amdgcn_readfirstlane(__shfl(incl, kWave - 1, kWave));
   U.map = T0 + (1u << SQ_ALIGN) <= kMapBlocks;
   // interior blocks [i_lo, i_hi): the only ones loaded
-  const uint32_t i_lo0 = G.hf ? 1u : 0u, i_hi0 = G.hl ? nblk - 1 : nblk;
-  const uint64_t sabs = B0 + (J.src_pay - J.dst_pay);  // input of block B0
-  // special blocks loadable: every input block of the packet's flat blocks
-  // is 16-byte aligned and its special ones hold a payload byte (mapped)
-  const uint64_t pe = J.src_pay + J.len;
-  const bool sp_ok = !F || ((sabs & 15) == 0 && npad == 0 && !ovl &&
-                            (!G.hf || (J.len && J.src_pay < sabs + 16 && pe > sabs)) &&
-                            (!(G.hl && G.lfull) ||
-                             (J.len && pe > sabs + 16ull * (nblk - 1) &&
-                              J.src_pay < sabs + 16ull * nblk)));
-  U.ldsp = SQ_LDSPECIAL && !ol && __ballot(!sp_ok) == 0;
-  const uint32_t i_lo = U.ldsp ? 0u : i_lo0, i_hi = U.ldsp ? F : i_hi0;
+  const uint32_t i_lo = G.hf ? 1u : 0u, i_hi = G.hl ? nblk - 1 : nblk;
   const bool has_int = i_hi > i_lo;
+  const uint64_t sabs = B0 + (J.src_pay - J.dst_pay);  // input of block B0
   const uint64_t s_first = sabs + 16ull * i_lo, s_end = sabs + 16ull * i_hi;
   // spans: output of every flat block, input of every interior block
   const uint64_t d_lo = wave_ext64_dpp<false>(F ? B0 : ~0ull);
@@ -881,7 +834,6 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
   const bool mis = has_int && (sabs & 3);
   const bool sok = s_hi <= s_lo || s_hi - s_lo <= kMaxSpan;
   U.fast = T0 != 0 && __ballot(mis) == 0 && d_hi - d_lo <= kMaxSpan && sok;
-  U.ldsp = U.ldsp && U.fast;  // (the generic path never loads special blocks)
   // map path (buffer streaming only: the generic path walks [0, T) by
   // `locate`): shift the flat space so that slot c sits at d_lo's line phase
   const uint32_t phase = U.map && U.fast && SQ_ALIGN
@@ -943,7 +895,7 @@ __device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
                                           const uint32_t (&salt)[4], bool do_hash, uint32_t pid,
                                           const PskHot &hot,
                                           const Windows &W, bool owner, uint32_t lane,
-                                          bool ob, bool ldsp, const Geo &G, WaveLds &L) {
+                                          bool ob, const Geo &G, WaveLds &L) {
   constexpr uint32_t S = KIND == 0 ? kSalamanderSalt : kXPlusSalt;
   constexpr uint32_t PW = DIR == 0 ? S / 4 : 0;  // salt words in front of the payload
   uint32_t key[8];
@@ -1038,19 +990,6 @@ __device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
 #pragma unroll
     for (int j = 0; j < 4; j++) vl[j] = (ti[j] & range_mask(0, (int)t, j)) | (ob ? 0u : sh[j]);
   }
-  if (ldsp) {
-    // the stream loads the special blocks too (SQ_LDSPECIAL) and XORs what
-    // it loads: their "keystream" is their value ^ their input block, which
-    // a window holds (input and output 16-byte phases agree: plan_unit)
-    if (G.hf) {
-      vf[0] ^= wh0.x; vf[1] ^= wh0.y; vf[2] ^= wh0.z; vf[3] ^= wh0.w;
-    }
-    if (G.lfull) {
-      const uint32_t kb = (uint32_t)((BL - (J.dst_pay & ~15ull)) >> 4);
-      const u32x4 ti4 = tail_from_window(rs, re) ? W.t0 : (kb == 0 ? wh0 : (kb == 1 ? wh1 : wh2));
-      vl[0] ^= ti4.x; vl[1] ^= ti4.y; vl[2] ^= ti4.z; vl[3] ^= ti4.w;
-    }
-  }
   uint32_t k0[4], k1[4];
   const uint32_t ph = (uint32_t)(G.B0 - J.dst_pay) & 31u;
   keywin(key, ph, k0);
@@ -1116,7 +1055,7 @@ struct Step {
 // "keystream" is its precomputed value.
 template <int U, bool MAP>
 __device__ __forceinline__ void stream_issue(const WaveLds &L, const WaveBufs &B, uint32_t cst,
-                                             uint32_t T, uint32_t lane, uint32_t base, bool ldsp,
+                                             uint32_t T, uint32_t lane, uint32_t base,
                                              Step<U> &S) {
   uint32_t pp[U], off[U], rl[U];
   // every LDS read of the step first, then the arithmetic, then the loads
@@ -1151,7 +1090,7 @@ __device__ __forceinline__ void stream_issue(const WaveLds &L, const WaveBufs &B
     const uint32_t c = base + u * kWave + lane;
     const bool in = c < T;
     S.doff[u] = in ? (uint32_t)(sd[u] >> 32) + 16u * c : kOffNone;
-    off[u] = in && (ldsp || idx[u] < 2u) ? (uint32_t)sd[u] + 16u * c : kOffNone;
+    off[u] = in && idx[u] < 2u ? (uint32_t)sd[u] + 16u * c : kOffNone;
   }
 #pragma unroll
   for (int u = 0; u < U; u++) S.v[u] = __builtin_amdgcn_raw_buffer_load_b128(B.src, off[u], 0, kAuxLd);
@@ -1171,15 +1110,15 @@ __device__ __forceinline__ void stream_store(const WaveLds &L, const WaveBufs &B
 // stored, so a wave keeps U..2U KiB of reads outstanding.
 template <int U, bool MAP>
 __device__ __forceinline__ void stream_loop(const WaveLds &L, const WaveBufs &B, uint32_t cst,
-                                            uint32_t T, uint32_t lane, bool ldsp, Step<U> &cur) {
+                                            uint32_t T, uint32_t lane, Step<U> &cur) {
   constexpr uint32_t STEP = kWave * U;
   // unrolled by two with two named steps, so no register copies between them
   Step<U> nxt;
   for (uint32_t base = 0;; base += 2 * STEP) {
-    stream_issue<U, MAP>(L, B, cst, T, lane, base + STEP, ldsp, nxt);
+    stream_issue<U, MAP>(L, B, cst, T, lane, base + STEP, nxt);
     stream_store<U>(L, B, cur);
     if (base + STEP >= T) break;
-    stream_issue<U, MAP>(L, B, cst, T, lane, base + 2 * STEP, ldsp, cur);
+    stream_issue<U, MAP>(L, B, cst, T, lane, base + 2 * STEP, cur);
     stream_store<U>(L, B, nxt);
     if (base + 2 * STEP >= T) break;
   }
@@ -1231,7 +1170,11 @@ __global__ __launch_bounds__(WPB * kWave) void obfs_kernel(const KParams P) {
   RawDesc d;
   fetch_desc<KIND, DIR, MULTI>(P, p, valid, d);
   constexpr uint32_t kSalt = KIND == 0 ? kSalamanderSalt : kXPlusSalt;
-  if (SQ_QSALT && DIR == 0 && P.device_salt)  // (while the descriptor loads fly)
+  // device salts depend on p alone: computed while the descriptor loads fly
+  // (round 4: -2.6 % on configs[1] against computing them after the loads
+  // land), by quads (round 5: -0.8 % configs[1], -1.9 % ragged against one
+  // whole block per lane)
+  if (DIR == 0 && P.device_salt)
     device_salts_wave<kSalt>(P, first, ppw, lane, p, valid,
                              reinterpret_cast<uint32_t *>(lds[wv].role), d.salt);
   PacketJob J;
@@ -1258,15 +1201,15 @@ __global__ __launch_bounds__(WPB * kWave) void obfs_kernel(const KParams P) {
   const uint32_t pid = MULTI && d.pid < P.n_psk ? d.pid : 0u;
   reload_windows<DIR, kSalt>(J, do_hash, W);
   // 2 + 3b. key and block contents
-  fill_unit<KIND, DIR, MULTI>(P, J, salt, do_hash, pid, hot, W, owner, lane, ob, S.ldsp, G, L);
+  fill_unit<KIND, DIR, MULTI>(P, J, salt, do_hash, pid, hot, W, owner, lane, ob, G, L);
   SQ_STAMP(3);
   // 4. the stream
   if (S.fast && S.map) {
-    stream_issue<U, true>(L, S.B, S.cst, S.T, lane, 0, S.ldsp, cur);
-    stream_loop<U, true>(L, S.B, S.cst, S.T, lane, S.ldsp, cur);
+    stream_issue<U, true>(L, S.B, S.cst, S.T, lane, 0, cur);
+    stream_loop<U, true>(L, S.B, S.cst, S.T, lane, cur);
   } else if (S.fast) {
-    stream_issue<U, false>(L, S.B, S.cst, S.T, lane, 0, S.ldsp, cur);
-    stream_loop<U, false>(L, S.B, S.cst, S.T, lane, S.ldsp, cur);
+    stream_issue<U, false>(L, S.B, S.cst, S.T, lane, 0, cur);
+    stream_loop<U, false>(L, S.B, S.cst, S.T, lane, cur);
   } else if (S.T != 0) {
     stream_generic(L, S.cst, S.T, lane);
   }

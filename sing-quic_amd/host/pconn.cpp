@@ -46,6 +46,9 @@
 #include <netinet/in.h>
 #include <netinet/udp.h>
 #include <poll.h>
+#include <pthread.h>
+#include <sched.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/epoll.h>
@@ -257,6 +260,11 @@ struct Engine {
   std::atomic<bool> loaded{false};
   std::atomic<uint32_t> gpu_host_ns{kDefGpuHostNs};  // host CPU per launched batch (EWMA)
 
+  // the CPUs the engine's threads run on (sqobfs_engine_set_affinity);
+  // ncpus 0: not restricted
+  cpu_set_t cpus;
+  uint32_t ncpus = 0;
+
   std::mutex pool_mu;
   std::map<std::pair<uint32_t, uint32_t>, std::vector<Block *>> free_blocks;
   uint32_t blocks = 0, in_use = 0;
@@ -285,6 +293,43 @@ bool wait_dl(std::unique_lock<std::mutex> &lk, std::condition_variable &cv, cons
 std::mutex g_eng_mu;
 std::map<sqobfs_ctx *, Engine *> g_engines;     // ctx NULL: the host engine (never ended)
 std::map<sqobfs_ctx *, uint32_t> g_workers_cfg;  // sqobfs_engine_set_workers
+std::map<sqobfs_ctx *, int> g_affinity_cfg;      // sqobfs_engine_set_affinity
+
+// L3 (CCD) id of a CPU from sysfs; -1 when unknown
+int l3_of(int cpu) {
+  char path[96];
+  snprintf(path, sizeof path, "/sys/devices/system/cpu/cpu%d/cache/index3/id", cpu);
+  FILE *f = fopen(path, "r");
+  if (!f) return -1;
+  int id = -1;
+  if (fscanf(f, "%d", &id) != 1) id = -1;
+  fclose(f);
+  return id;
+}
+
+// The CPUs of the process's affinity that share the calling thread's L3:
+// the engine's threads stay together, next to the thread that started it.
+// Measured ("the small-batch regime"): threads spread over
+// 2-4 CCDs of the GPU box ran 5 of 45 loopback throughput runs at 0.9-1.3
+// M datagrams/s; kept on one L3, 0 of 45, and +26 % at the median.
+uint32_t l3_cpus(cpu_set_t *out) {
+  CPU_ZERO(out);
+  cpu_set_t cur;
+  if (sched_getaffinity(0, sizeof cur, &cur)) return 0;
+  const int me = sched_getcpu(), l3 = me >= 0 ? l3_of(me) : -1;
+  if (l3 < 0) return 0;
+  uint32_t n = 0;
+  for (int c = 0; c < CPU_SETSIZE; c++)
+    if (CPU_ISSET(c, &cur) && l3_of(c) == l3) {
+      CPU_SET(c, out);
+      n++;
+    }
+  return n >= 2 ? n : 0;  // (one CPU: leave the threads free)
+}
+
+void engine_thread_pin(const Engine *E) {
+  if (E->ncpus) (void)pthread_setaffinity_np(pthread_self(), sizeof E->cpus, &E->cpus);
+}
 
 void worker_main(Engine *E, uint32_t w);
 void poller_main(Engine *E);
@@ -301,6 +346,9 @@ Engine *engine_get(sqobfs_ctx *ctx, int *status) {
   E->ctx = ctx;
   auto c = g_workers_cfg.find(ctx);
   if (c != g_workers_cfg.end() && c->second) E->nworkers = c->second;
+  auto a = g_affinity_cfg.find(ctx);
+  const int aff = a != g_affinity_cfg.end() ? a->second : SQOBFS_ENGINE_AFFINITY_L3;
+  if (aff == SQOBFS_ENGINE_AFFINITY_L3) E->ncpus = l3_cpus(&E->cpus);
   E->streams.assign(E->nworkers, nullptr);
   E->wake = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
   E->epfd = epoll_create1(EPOLL_CLOEXEC);
@@ -932,6 +980,7 @@ void rx_socket_task(Engine *E, uint32_t w, sqobfs_pconn *pc) {
 }
 
 void worker_main(Engine *E, uint32_t w) {
+  engine_thread_pin(E);
   std::unique_lock<std::mutex> lk(E->mu);
   for (;;) {
     if (E->stop) return;
@@ -966,6 +1015,7 @@ void worker_main(Engine *E, uint32_t w) {
 }
 
 void poller_main(Engine *E) {
+  engine_thread_pin(E);
   epoll_event ev[64];
   for (;;) {
     const int n = epoll_wait(E->epfd, ev, 64, -1);
@@ -1008,6 +1058,7 @@ void sq_engine_ctx_closed(sqobfs_ctx *ctx) {
   {
     std::lock_guard<std::mutex> g(g_eng_mu);
     g_workers_cfg.erase(ctx);
+    g_affinity_cfg.erase(ctx);
     auto it = g_engines.find(ctx);
     if (it == g_engines.end()) return;
     E = it->second;
@@ -1042,6 +1093,7 @@ int sqobfs_engine_info_get(sqobfs_ctx *ctx, sqobfs_engine_info *out) {
   out->load_permille = E->load_pm.load();
   out->loaded = E->loaded.load() ? 1u : 0u;
   out->gpu_host_ns = E->gpu_host_ns.load();
+  out->cpus = E->ncpus;
   return SQ_OK;
 }
 
@@ -1050,6 +1102,14 @@ int sqobfs_engine_set_workers(sqobfs_ctx *ctx, uint32_t workers) {
   std::lock_guard<std::mutex> g(g_eng_mu);
   if (g_engines.count(ctx)) return SQ_EINVAL;
   g_workers_cfg[ctx] = workers;
+  return SQ_OK;
+}
+
+int sqobfs_engine_set_affinity(sqobfs_ctx *ctx, int mode) {
+  if (mode != SQOBFS_ENGINE_AFFINITY_NONE && mode != SQOBFS_ENGINE_AFFINITY_L3) return SQ_EINVAL;
+  std::lock_guard<std::mutex> g(g_eng_mu);
+  if (g_engines.count(ctx)) return SQ_EINVAL;
+  g_affinity_cfg[ctx] = mode;
   return SQ_OK;
 }
 

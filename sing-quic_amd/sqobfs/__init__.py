@@ -258,6 +258,7 @@ def load(path: str) -> ctypes.CDLL:
     L.sqobfs_debug_pool_fail.restype = None
     L.sqobfs_debug_gcm_ungrouped.argtypes = [i32]
     L.sqobfs_debug_gcm_ungrouped.restype = None
+    L.sqobfs_engine_set_affinity.argtypes = [vp, i32]
     L.sqobfs_debug_device_pool.argtypes = [vp, ctypes.c_uint64]
     L.sqobfs_debug_device_pool.restype = ctypes.c_uint64
     return L
@@ -423,7 +424,7 @@ class EngineInfo(ctypes.Structure):
                 ("gpu_disabled", ctypes.c_uint32), ("route_bytes", ctypes.c_uint64),
                 ("launch_us", ctypes.c_uint32), ("cpu_ns_per_kib", ctypes.c_uint32),
                 ("load_permille", ctypes.c_uint32), ("loaded", ctypes.c_uint32),
-                ("gpu_host_ns", ctypes.c_uint32)]
+                ("gpu_host_ns", ctypes.c_uint32), ("cpus", ctypes.c_uint32)]
 
 
 def engine_info(ctx: Context | None) -> EngineInfo:

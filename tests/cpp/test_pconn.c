@@ -1045,6 +1045,9 @@ static void t_poolfail(int kind) {
 static void t_fail(int at_completion) {
   sqobfs_ctx *ctx = NULL;
   CHECK(sqobfs_open(0, &ctx));
+  /* (this context's engine threads left to the scheduler; after its first
+   * pconn the setting is refused) */
+  CHECK(sqobfs_engine_set_affinity(ctx, SQOBFS_ENGINE_AFFINITY_NONE));
   const int64_t a0 = sqobfs_debug_host_allocs();
   for (int kind = 0; kind < 2; kind++) {
     const int S = salt_len(kind);
@@ -1057,6 +1060,11 @@ static void t_fail(int at_completion) {
     memset(&o, 0, sizeof o);
     o.cpu_max = SQOBFS_PCONN_NEVER; /* every batch launches while the GPU works */
     CHECK(sqobfs_pconn_open(ctx, kr, -1, &o, &pc));
+    EXPECT(sqobfs_engine_set_affinity(ctx, SQOBFS_ENGINE_AFFINITY_L3) == SQ_EINVAL,
+           "affinity changed after the engine started");
+    sqobfs_engine_info ai;
+    CHECK(sqobfs_engine_info_get(ctx, &ai));
+    EXPECT(ai.cpus == 0, "AFFINITY_NONE engine restricted to %u CPUs", ai.cpus);
     static uint8_t pay[400][2048];
     static uint32_t plen[400];
     for (int i = 0; i < 400; i++) {
@@ -1140,6 +1148,9 @@ int main(int argc, char **argv) {
   sqobfs_engine_info info;
   CHECK(sqobfs_engine_info_get(g_ctx, &info));
   EXPECT(info.gpu_disabled == 0, "the shared engine switched to the CPU");
+  EXPECT(info.cpus == 0 || info.cpus >= 2, "engine kept on %u CPU", info.cpus);
+  printf("  engine threads kept on %u CPUs (the L3 domain of the thread that started it; 0 = "
+         "free)\n", info.cpus);
   if (g_ctx) sqobfs_close(g_ctx);
   EXPECT(sqobfs_debug_host_allocs() == a0, "host allocs after close");
   printf("ok: pconn engine [%s] (socket + pump modes, deadlines, shutdown, memory, sync errors, "
