@@ -83,6 +83,16 @@ sqobfs._lib = sqobfs.load(paths[0])
 u_r = sqobfs.unit_packets_for(int(ragged.sum().item()), n4)
 cases = [("F16", fixed, 0), (f"R{u_r}", ragged, u_r), (f"C{u_r}", const, u_r),
          ("FB16", fbig, 16), (f"P{u_r}", p758, u_r), (f"B{u_r}", bal, u_r)]
+if os.environ.get("SPLIT_CASES") == "ladder":
+    # the per-byte rate against the batch's packet count, for both lengths
+    # (a size ladder: 1M, 2M / 2.37M, 4M packets)
+    del ragged, srt, bal, const, fbig
+    cases = [("F1M", fixed, 16),
+             ("F2.4M", torch.full((2372000,), 1350, device=dev, dtype=torch.int64), 16),
+             ("F4M", torch.full((n4,), 1350, device=dev, dtype=torch.int64), 16),
+             ("P1M", p758, u_r),
+             ("P2M", torch.full((1 << 21,), 758, device=dev, dtype=torch.int64), u_r),
+             ("P4M", torch.full((n4,), 758, device=dev, dtype=torch.int64), u_r)]
 bufs = {}
 for name, lens, u in cases:
     key = id(lens)
