@@ -65,12 +65,24 @@ def pin(ctx, hb, keep, phase=0):
 @pytest.mark.parametrize("direction", [OBFUSCATE, DEOBFUSCATE])
 @pytest.mark.parametrize("flags", ["none", "blocks", "lines", "lines+uninit"])
 def test_slot_staging(kind, direction, flags):
-    rng = np.random.Generator(np.random.PCG64(8100 + 10 * kind + direction +
+    _slot_staging(kind, direction, flags, 2048)
+
+
+@pytest.mark.parametrize("kind", [SALAMANDER, XPLUS])
+@pytest.mark.parametrize("direction", [OBFUSCATE, DEOBFUSCATE])
+def test_slot_staging_1536_lines(kind, direction):
+    """1,536-byte slots (12 whole 128-byte lines: wire <= 1,468 B for both
+    schemes), the stride DESIGN.md section 5 compared with 2,048."""
+    _slot_staging(kind, direction, "lines+uninit", 1536)
+
+
+def _slot_staging(kind, direction, flags, slot):
+    rng = np.random.Generator(np.random.PCG64(8100 + 10 * kind + direction + slot +
                                               100 * ["none", "blocks", "lines",
                                                      "lines+uninit"].index(flags)))
-    n, slot = 9000, 2048  # several pipeline chunks
+    n = 9000  # several pipeline chunks
     hb = slotted(rng, kind, direction, n, slot, lead=0 if flags != "none" else 5,
-                 cap_extra=kind == XPLUS and direction == DEOBFUSCATE)
+                 cap_extra=kind == XPLUS and direction == DEOBFUSCATE and slot >= 2048)
     ref = gh.run_oracle(kind, direction, PSKS, hb)
     hb.flags = {"none": 0, "blocks": sqobfs.FLAG_OUT_BLOCKS, "lines": sqobfs.FLAG_OUT_LINES,
                 "lines+uninit": sqobfs.FLAG_OUT_LINES | sqobfs.FLAG_OUT_UNINIT}[flags]
