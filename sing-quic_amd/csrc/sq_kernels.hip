@@ -114,14 +114,7 @@ namespace sq {
 #ifndef SQ_XCD
 #define SQ_XCD -1
 #endif
-// Runs (KParams.xcd == 2): XCD x runs logical blocks in runs of SQ_XCDRUN
-// consecutive ones, windows of 8 runs, so a unit and its neighbours run on
-// one XCD (its L2) at nearly the same time -- the descriptor lines two
-// units share (units of 28 packets split 128-byte lines of the 8-byte
-// arrays) are then fetched once.
-#ifndef SQ_XCDRUN
-#define SQ_XCDRUN 4
-#endif
+
 constexpr uint64_t kXcdMinUnits = 1u << 18;
 
 #define SQ_STR2(x) #x
@@ -1163,14 +1156,7 @@ __global__ __launch_bounds__(WPB * kWave) void obfs_kernel(const KParams P) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wv = threadIdx.x / kWave;
   uint32_t lb = blockIdx.x;
-  if (P.xcd == 2) {  // runs (a bijection: full windows remapped, the tail as is)
-    constexpr uint32_t R = SQ_XCDRUN;
-    const uint32_t full = gridDim.x / (8 * R) * (8 * R);
-    if (lb < full) {
-      const uint32_t xcd = lb % 8, k = lb / 8;
-      lb = (k / R) * (8 * R) + xcd * R + k % R;
-    }
-  } else if (P.xcd) {  // eighths (a bijection of [0, gridDim.x) for any grid size)
+  if (P.xcd) {  // eighths (a bijection of [0, gridDim.x) for any grid size)
     const uint32_t ng = gridDim.x, q = ng / 8, r = ng % 8, xcd = lb % 8, ix = lb / 8;
     lb = xcd < r ? xcd * (q + 1) + ix : r * (q + 1) + (xcd - r) * q + ix;
   }

@@ -92,8 +92,10 @@ def _slot_staging(kind, direction, flags, slot):
             pin(ctx, hb, keep)
             with sqobfs.Keyring(ctx, kind, PSKS) as kr:
                 gh.run_host(ctx, kr, direction, hb)
-                # packed: well under the two 2,048-byte-slot spans
-                assert ctx.staging_bytes < 2 * n * slot * 7 // 8, ctx.staging_bytes
+                # packed: well under the two 2,048-byte-slot spans (1,536-byte
+                # slots of whole lines hold rows of 1,536: nothing to pack)
+                if slot == 2048:
+                    assert ctx.staging_bytes < 2 * n * slot * 7 // 8, ctx.staging_bytes
             assert np.array_equal(hb.out_len, ref.out_len)
             out = hb.out.copy()
         finally:
