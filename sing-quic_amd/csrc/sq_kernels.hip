@@ -258,9 +258,18 @@ __device__ __forceinline__ void chacha20_quad(const uint32_t (&key)[8], uint32_t
                                               uint32_t (&o)[4]) {
   const uint32_t sigma = col == 0 ? 0x61707865u : col == 1 ? 0x3320646eu
                          : col == 2 ? 0x79622d32u : 0x6b206574u;
-  const uint32_t kb = col == 0 ? key[0] : col == 1 ? key[1] : col == 2 ? key[2] : key[3];
-  const uint32_t kc = col == 0 ? key[4] : col == 1 ? key[5] : col == 2 ? key[6] : key[7];
-  const uint32_t kd = col == 0 ? counter : col == 1 ? nonce[0] : col == 2 ? nonce[1] : nonce[2];
+  // the key and nonce words are wave-uniform: read them as scalars and
+  // select per lane (a per-lane index into the kernarg array became a
+  // vector load from it, whose wait drained the descriptor loads too)
+  uint32_t kw[8], nw[3];
+#pragma unroll
+  for (int i = 0; i < 8; i++) kw[i] = (uint32_t)__builtin_amdgcn_readfirstlane((int)key[i]);
+#pragma unroll
+  for (int i = 0; i < 3; i++) nw[i] = (uint32_t)__builtin_amdgcn_readfirstlane((int)nonce[i]);
+  const bool c1 = col == 1, c2 = col == 2, c3 = col == 3;
+  const uint32_t kb = c3 ? kw[3] : c2 ? kw[2] : c1 ? kw[1] : kw[0];
+  const uint32_t kc = c3 ? kw[7] : c2 ? kw[6] : c1 ? kw[5] : kw[4];
+  const uint32_t kd = c3 ? nw[2] : c2 ? nw[1] : c1 ? nw[0] : counter;
   uint32_t a = sigma, b = kb, c = kc, d = kd;
 #pragma unroll
   for (int r = 0; r < 10; r++) {
@@ -338,20 +347,26 @@ struct RawDesc {
 template <int KIND, int DIR, bool MULTI>
 __device__ __forceinline__ void fetch_desc(const KParams &P, uint32_t p, bool valid, RawDesc &d) {
   constexpr uint32_t S = KIND == 0 ? kSalamanderSalt : kXPlusSalt;
-  d.ioff = d.ooff = 0;
-  d.len = d.cap = d.pid = 0;
+  // Unconditional loads (a lane without a packet reads entry 0, which every
+  // batch has, and drops it): loads under a divergent branch made the
+  // compiler wait for all of them (s_waitcnt vmcnt(0)) where the branches
+  // join, before the device salts below could run under them.
+  const uint32_t q = valid ? p : 0u;
+  const uint64_t ioff = P.in_off[q], ooff = P.out_off[q];
+  const uint32_t len = P.in_len[q];
+  const uint32_t pid = MULTI ? (uint32_t)P.psk_id[q] : 0u;
+  const uint32_t cap = (KIND == 1 && DIR == 1 && P.in_cap) ? P.in_cap[q] : 0u;
+  d.ioff = valid ? ioff : 0;
+  d.ooff = valid ? ooff : 0;
+  d.len = valid ? len : 0u;
+  d.pid = valid ? pid : 0u;
+  d.cap = valid ? cap : 0u;
 #pragma unroll
   for (int k = 0; k < 4; k++) d.salt[k] = 0u;
-  if (!valid) return;
-  d.ioff = P.in_off[p];
-  d.ooff = P.out_off[p];
-  d.len = P.in_len[p];
-  if (MULTI) d.pid = P.psk_id[p];
-  if (KIND == 1 && DIR == 1 && P.in_cap) d.cap = P.in_cap[p];
   if (DIR == 0 && !P.device_salt) {
-    const uint32_t *sp = reinterpret_cast<const uint32_t *>(P.salt + (uint64_t)p * S);
+    const uint32_t *sp = reinterpret_cast<const uint32_t *>(P.salt + (uint64_t)q * S);
 #pragma unroll
-    for (uint32_t k = 0; k < S / 4; k++) d.salt[k] = sp[k];
+    for (uint32_t k = 0; k < S / 4; k++) d.salt[k] = valid ? sp[k] : 0u;
   }
   // (device salts: device_salts_wave, while these loads fly)
 }
