@@ -345,13 +345,15 @@ struct RawDesc {
 };
 
 template <int KIND, int DIR, bool MULTI>
-__device__ __forceinline__ void fetch_desc(const KParams &P, uint32_t p, bool valid, RawDesc &d) {
+__device__ __forceinline__ void fetch_desc(const KParams &P, uint32_t p, bool valid, uint32_t p0,
+                                           RawDesc &d) {
   constexpr uint32_t S = KIND == 0 ? kSalamanderSalt : kXPlusSalt;
-  // Unconditional loads (a lane without a packet reads entry 0, which every
-  // batch has, and drops it): loads under a divergent branch made the
-  // compiler wait for all of them (s_waitcnt vmcnt(0)) where the branches
-  // join, before the device salts below could run under them.
-  const uint32_t q = valid ? p : 0u;
+  // Unconditional loads (a lane without a packet reads the unit's first
+  // entry, p0, in the lines the wave reads anyway, and drops it): loads
+  // under a divergent branch made the compiler wait for all of them
+  // (s_waitcnt vmcnt(0)) where the branches join, before the device salts
+  // could run under them.
+  const uint32_t q = valid ? p : p0;
   const uint64_t ioff = P.in_off[q], ooff = P.out_off[q];
   const uint32_t len = P.in_len[q];
   const uint32_t pid = MULTI ? (uint32_t)P.psk_id[q] : 0u;
@@ -1184,7 +1186,7 @@ __global__ __launch_bounds__(WPB * kWave) void obfs_kernel(const KParams P) {
   const uint32_t p = lane_packet(first, ppw, lane, P.n, valid, owner);
   // 1. descriptor (deobfuscate: the salt load) and the image windows: loads
   RawDesc d;
-  fetch_desc<KIND, DIR, MULTI>(P, p, valid, d);
+  fetch_desc<KIND, DIR, MULTI>(P, p, valid, (uint32_t)first, d);
   constexpr uint32_t kSalt = KIND == 0 ? kSalamanderSalt : kXPlusSalt;
   // device salts depend on p alone: computed while the descriptor loads fly
   // (round 4: -2.6 % on configs[1] against computing them after the loads
