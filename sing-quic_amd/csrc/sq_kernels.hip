@@ -353,6 +353,20 @@ __device__ __forceinline__ void fetch_desc(const KParams &P, uint32_t p, bool va
   // under a divergent branch made the compiler wait for all of them
   // (s_waitcnt vmcnt(0)) where the branches join, before the device salts
   // could run under them.
+  if (DIR == 1) {  // (deobfuscate: no device salts to overlap; the branch
+                   // measured 0.3-0.9 % faster, profiles/r05/ab/desc_*)
+    d.ioff = d.ooff = 0;
+    d.len = d.cap = d.pid = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) d.salt[k] = 0u;
+    if (!valid) return;
+    d.ioff = P.in_off[p];
+    d.ooff = P.out_off[p];
+    d.len = P.in_len[p];
+    if (MULTI) d.pid = P.psk_id[p];
+    if (KIND == 1 && P.in_cap) d.cap = P.in_cap[p];
+    return;
+  }
   const uint32_t q = valid ? p : p0;
   const uint64_t ioff = P.in_off[q], ooff = P.out_off[q];
   const uint32_t len = P.in_len[q];
