@@ -932,6 +932,13 @@ __device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
   constexpr uint32_t PW = DIR == 0 ? S / 4 : 0;  // salt words in front of the payload
   uint32_t key[8];
   uint32_t sl[4] = {salt[0], salt[1], salt[2], salt[3]};
+  // every window register stays allocated until here: a component no image
+  // uses would otherwise be handed to the plan while its load is in flight,
+  // and overwriting it waits for the load
+  if (DIR == 1)
+    asm volatile("" ::"v"(W.h0), "v"(W.h1), "v"(W.h2), "v"(W.t0), "v"(W.t1), "v"(W.s0));
+  else  // (obfuscate loads no salt block)
+    asm volatile("" ::"v"(W.h0), "v"(W.h1), "v"(W.h2), "v"(W.t0), "v"(W.t1));
   const u32x4 wh0 = W.h0, wh1 = W.h1, wh2 = W.h2;
   if (DIR == 1) {  // the wire salt, from the head window
     const u32x4 ws0 = W.s0;
@@ -942,17 +949,6 @@ __device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
   // single PSK: the kernarg copy (scalar loads); several: the device table
   derive_key<KIND, MULTI && SQ_PSKPRE>(do_hash, MULTI ? P.psk_table + pid : &P.psk0, hot, sl,
                                         key);
-  // every window register stays allocated until here: a component no image
-  // uses would otherwise be handed to the plan or the hash while its load
-  // is in flight, and overwriting it waits for the load.  After the hash,
-  // not before it: an asm input must have landed, so the keep-alive waits
-  // for every window (s_waitcnt vmcnt(0)); placed before the hash (rounds
-  // 3-4) it put the windows' whole latency in front of the hash instead of
-  // under it.
-  if (DIR == 1)
-    asm volatile("" ::"v"(W.h0), "v"(W.h1), "v"(W.h2), "v"(W.t0), "v"(W.t1), "v"(W.s0));
-  else  // (obfuscate loads no salt block)
-    asm volatile("" ::"v"(W.h0), "v"(W.h1), "v"(W.h2), "v"(W.t0), "v"(W.t1));
   const uint64_t rs = G.rs, re = G.re;
   // head image: output bytes [rs, rs + 32) = salt || payload ^ key
   uint32_t hi[8];
