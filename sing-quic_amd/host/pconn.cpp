@@ -52,6 +52,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/epoll.h>
+#include <sys/prctl.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <time.h>
@@ -329,6 +330,9 @@ uint32_t l3_cpus(cpu_set_t *out) {
 
 void engine_thread_pin(const Engine *E) {
   if (E->ncpus) (void)pthread_setaffinity_np(pthread_self(), sizeof E->cpus, &E->cpus);
+  // the sleeps of non-polling launch waits wake within ~1 us, not the
+  // default 50 us of timer slack
+  (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
 }
 
 void worker_main(Engine *E, uint32_t w);
@@ -620,7 +624,7 @@ int transform(Engine *E, uint32_t w, sqobfs_pconn *pc, int dir, PBatch &b, bool 
       // event: the worker's core is free while the kernel runs)
       const bool block = bulk || pc->o.spin_us == SQOBFS_PCONN_NEVER;
       const uint32_t spin = std::min<uint32_t>(pc->o.spin_us, 2 * ew + 20);
-      st = block ? sq_ctx_stream_wait_blocking(E->ctx, E->streams[w])
+      st = block ? sq_ctx_stream_wait_blocking(E->ctx, E->streams[w], ew)
                  : sq_ctx_stream_wait(E->ctx, E->streams[w], spin);
       if (inject == 2) st = SQ_EDEVICE;
       if (st != SQ_OK) {

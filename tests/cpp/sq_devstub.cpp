@@ -99,7 +99,9 @@ int sq_ctx_stream_wait(sqobfs_ctx *, void *s, uint32_t) {
   if (s) static_cast<Stream *>(s)->drain();
   return SQ_OK;
 }
-int sq_ctx_stream_wait_blocking(sqobfs_ctx *ctx, void *s) { return sq_ctx_stream_wait(ctx, s, 0); }
+int sq_ctx_stream_wait_blocking(sqobfs_ctx *ctx, void *s, uint32_t) {
+  return sq_ctx_stream_wait(ctx, s, 0);
+}
 void sq_keyring_forget(const sqobfs_keyring *, void *) {}
 int sq_host_alloc_mapped(sqobfs_ctx *ctx, size_t bytes, void **out) {
   return sqobfs_host_alloc(ctx, bytes, out);
