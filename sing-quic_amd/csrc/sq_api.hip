@@ -309,19 +309,20 @@ struct BlockingEvents {
 thread_local BlockingEvents t_block_ev;
 }  // namespace
 
-int sq_ctx_stream_wait_blocking(sqobfs_ctx *ctx, void *s, uint32_t expect_us) {
+int sq_ctx_stream_wait_blocking(sqobfs_ctx *ctx, void *s, uint32_t nap_us) {
   DeviceScope ds_(ctx->device);
   if (ds_.status != SQ_OK) return ds_.status;
   hipStream_t hs = (hipStream_t)s;
-  // Sleep through most of the expected time, then poll with short sleeps:
-  // the thread holds no core meanwhile.  (An event with hipEventBlockingSync
-  // measured ~33 us of host CPU per ~35 us launch: the runtime spins before
-  // it sleeps.)  Past ~2 ms of polls, the blocking event.
+  // Sleep nap_us (the caller's estimate of most of the kernel's time), then
+  // poll with short sleeps: the thread holds no core meanwhile.  (An event
+  // with hipEventBlockingSync measured ~33 us of host CPU per ~35 us launch:
+  // the runtime spins before it sleeps.)  Past ~2 ms of polls, the blocking
+  // event.
   auto nap = [](uint32_t us) {
     timespec ts = {0, (long)us * 1000};
     nanosleep(&ts, nullptr);
   };
-  if (expect_us > 8) nap(expect_us - 6);
+  if (nap_us) nap(nap_us);
   for (int i = 0; i < 400; i++) {
     const hipError_t q = hipStreamQuery(hs);
     if (q == hipSuccess) return SQ_OK;

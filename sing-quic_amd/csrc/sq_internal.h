@@ -179,9 +179,9 @@ struct sqobfs_ctx;
 int sq_ctx_stream_create(sqobfs_ctx *ctx, void **out);
 void sq_ctx_stream_destroy(sqobfs_ctx *ctx, void *s);
 int sq_ctx_stream_wait(sqobfs_ctx *ctx, void *s, uint32_t spin_us);
-// wait without holding a core: sleep through most of expect_us, then poll
-// with short sleeps (an event with hipEventBlockingSync after ~2 ms)
-int sq_ctx_stream_wait_blocking(sqobfs_ctx *ctx, void *s, uint32_t expect_us);
+// wait without holding a core: sleep nap_us, then poll with short sleeps
+// (an event with hipEventBlockingSync after ~2 ms)
+int sq_ctx_stream_wait_blocking(sqobfs_ctx *ctx, void *s, uint32_t nap_us);
 // a synchronised library stream about to be destroyed: drop it from the
 // keyring's release fence (sqobfs_keyring_destroy)
 struct sqobfs_keyring;

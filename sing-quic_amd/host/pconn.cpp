@@ -260,6 +260,10 @@ struct Engine {
   std::atomic<uint32_t> load_pm{0};
   std::atomic<bool> loaded{false};
   std::atomic<uint32_t> gpu_host_ns{kDefGpuHostNs};  // host CPU per launched batch (EWMA)
+  // non-polling waits: the time from launch to the completion the wait saw
+  // (EWMA, us); the wait sleeps 3/4 of it, then polls, so the estimate
+  // tracks the kernel and not the wait's own sleep
+  std::atomic<uint32_t> kern_us{30};
 
   // the CPUs the engine's threads run on (sqobfs_engine_set_affinity);
   // ncpus 0: not restricted
@@ -624,7 +628,8 @@ int transform(Engine *E, uint32_t w, sqobfs_pconn *pc, int dir, PBatch &b, bool 
       // event: the worker's core is free while the kernel runs)
       const bool block = bulk || pc->o.spin_us == SQOBFS_PCONN_NEVER;
       const uint32_t spin = std::min<uint32_t>(pc->o.spin_us, 2 * ew + 20);
-      st = block ? sq_ctx_stream_wait_blocking(E->ctx, E->streams[w], ew)
+      const uint32_t ek = E->kern_us.load(std::memory_order_relaxed);
+      st = block ? sq_ctx_stream_wait_blocking(E->ctx, E->streams[w], ek * 3 / 4)
                  : sq_ctx_stream_wait(E->ctx, E->streams[w], spin);
       if (inject == 2) st = SQ_EDEVICE;
       if (st != SQ_OK) {
@@ -636,6 +641,8 @@ int transform(Engine *E, uint32_t w, sqobfs_pconn *pc, int dir, PBatch &b, bool 
       const uint32_t us = (uint32_t)std::min<int64_t>((mono_ns() - t0) / 1000, 100000);
       E->launch_us.store((7 * ew + us) / 8, std::memory_order_relaxed);
       if (block) {  // the host's cost of a launched batch (polled waits would count their spin)
+        E->kern_us.store((7 * E->kern_us.load(std::memory_order_relaxed) + us) / 8,
+                         std::memory_order_relaxed);
         const uint32_t hn = (uint32_t)std::min<int64_t>(thread_cpu_ns() - c0, 10'000'000);
         const uint32_t eh = E->gpu_host_ns.load(std::memory_order_relaxed);
         E->gpu_host_ns.store((7 * eh + hn) / 8, std::memory_order_relaxed);
