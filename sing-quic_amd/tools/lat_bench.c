@@ -20,7 +20,7 @@
  * Prints one JSON object (p50 / p99 in microseconds).  Built by
  * `make -C sing-quic_amd tools`; run by bench.py --latency.
  *
- * `lat_bench load [seconds]`: sustained load instead -- pconn A -> pconn B
+ * `lat_bench load [seconds [reps]]`: sustained load instead -- pconn A -> pconn B
  * over loopback (GSO / GRO, 1,024-datagram batches), a writer paced at a
  * fixed offered rate, for every routing mode: the process's CPU time
  * (getrusage: every engine thread of both ends, the writer and the reader)
@@ -381,7 +381,7 @@ static void load_run(const char *name, sqobfs_ctx *c, sqobfs_keyring *k,
   close(fb);
 }
 
-static int load_main(double secs) {
+static int load_main(double secs, int reps) {
   sqobfs_ctx *ctx;
   CHECK(sqobfs_open(0, &ctx));
   uint64_t o0 = 0;
@@ -396,11 +396,18 @@ static int load_main(double secs) {
   gpoll.cpu_max = gpoll.inline_gap_us = SQOBFS_PCONN_NEVER;
   gblock = gpoll;
   gblock.spin_us = SQOBFS_PCONN_NEVER;
-  static const double rates[] = {0.25, 0.5, 1.0, 2.0, 0};
+  static const double rates_all[] = {0.25, 0.5, 1.0, 2.0, 0};
+  static const double rates_bulk[] = {1.0, 2.0, 0};
+  /* reps > 1: the bulk rates only, every mode but the polling one, the
+   * (rate, mode) runs interleaved reps times (box noise between runs) */
+  const double *rates = reps > 1 ? rates_bulk : rates_all;
+  const int nr = reps > 1 ? 3 : 5;
   printf("{\"load\": [");
   int first = 1;
-  for (int ri = 0; ri < 5; ri++)
+  for (int ri = 0; ri < nr; ri++)
+    for (int rp = 0; rp < (reps > 1 ? reps : 1); rp++)
     for (int m = 0; m < 5; m++) {
+      if (reps > 1 && m == 2) continue;
       if (!first) printf(", ");
       first = 0;
       static const char *const names[] = {"default", "cpu_only", "gpu_poll", "gpu_block",
@@ -505,7 +512,8 @@ static int tput_main(int runs, int pin) {
 }
 
 int main(int argc, char **argv) {
-  if (argc > 1 && !strcmp(argv[1], "load")) return load_main(argc > 2 ? atof(argv[2]) : 1.5);
+  if (argc > 1 && !strcmp(argv[1], "load"))
+    return load_main(argc > 2 ? atof(argv[2]) : 1.5, argc > 3 ? atoi(argv[3]) : 1);
   if (argc > 1 && !strcmp(argv[1], "tput"))
     return tput_main(argc > 2 ? atoi(argv[2]) : 45, argc > 3 && !strcmp(argv[3], "pin"));
   sqobfs_ctx *ctx;
