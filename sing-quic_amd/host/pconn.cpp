@@ -90,7 +90,8 @@ constexpr uint32_t kHashCost = 1024;      // one key derivation ~ 1 KiB of XOR o
 // "loaded" on (off again below kLoadOffPermille).  Loaded, the host's CPU
 // time is what the routing saves, not a batch's latency: a batch of more
 // than kLoadMinDgrams datagrams launches (and waits without polling) when
-// its CPU-path time is more than a launch costs the host -- the worker
+// its CPU-path time is more than twice what a launch costs the host (the
+// margin: a launched batch also waits ~3x longer) -- the worker
 // thread's own CPU time per launched batch, launch call and blocking wait,
 // measured (gpu_host_ns) -- so bulk traffic costs the host the launch and
 // the socket work, not the bytes
@@ -595,7 +596,7 @@ int transform(Engine *E, uint32_t w, sqobfs_pconn *pc, int dir, PBatch &b, bool 
   const bool bulk = cmax == 0 && b.n > kLoadMinDgrams &&
                     E->loaded.load(std::memory_order_relaxed) &&
                     cost * E->cpu_ns_kib.load(std::memory_order_relaxed) / 1024u >
-                        E->gpu_host_ns.load(std::memory_order_relaxed);
+                        2ull * E->gpu_host_ns.load(std::memory_order_relaxed);
   const bool want_gpu = E->ctx && !E->gpu_off.load(std::memory_order_relaxed) &&
                         (cmax == SQOBFS_PCONN_NEVER || bulk ||
                          cost > (cmax == 0 ? route_bytes(E) : (uint64_t)cmax));
