@@ -614,9 +614,10 @@ typedef struct sqobfs_pconn_opts {
   uint32_t spin_us;    /* a worker polls a launch at most this long before it
                           blocks (0 = 200); the engine polls about twice the
                           launches' recent completion time, within that bound;
-                          SQOBFS_PCONN_NEVER = never poll: block at once on an
-                          interrupt-signalled event (the core is free while
-                          the kernel runs, at a wake-up's latency) */
+                          SQOBFS_PCONN_NEVER = never poll: sleep through most
+                          of the kernel's expected time, then poll with short
+                          sleeps (the core is free while the kernel runs, at
+                          ~50 us more latency) */
   uint32_t flags;      /* socket mode: SQOBFS_UDP_TX_GSO (runs of equal-length
                           datagrams to one address go out as UDP_SEGMENT
                           messages; off by itself if the socket refuses) |
@@ -634,8 +635,8 @@ typedef struct sqobfs_pconn_opts {
                           more than a tenth of a core busy on the CPU path
                           (sqobfs_engine_info.loaded) -- a batch of more than
                           64 datagrams also launches, waiting without
-                          polling, when its CPU-path time exceeds the host
-                          CPU time a launched batch costs (measured,
+                          polling, when its CPU-path time exceeds twice the
+                          host CPU time a launched batch costs (measured,
                           sqobfs_engine_info.gpu_host_ns): the host pays the
                           launch and the sockets, not the bytes; bursts of up
                           to 64 stay on the CPU path */
@@ -751,7 +752,7 @@ typedef struct sqobfs_engine_info {
   uint32_t loaded;         /* 1 while that stays above 100 (off below 50):
                               batches of more than 64 datagrams may launch */
   uint32_t gpu_host_ns;    /* host CPU time of a launched batch with a
-                              blocking wait (launch call + wait; EWMA) */
+                              non-polling wait (launch call + wait; EWMA) */
   uint32_t cpus;           /* CPUs the engine's threads are kept on (the L3
                               domain of the thread that started it; 0 = not
                               restricted: sqobfs_engine_set_affinity) */
