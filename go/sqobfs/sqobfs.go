@@ -123,6 +123,24 @@ func Shared(device int) (*Context, error) {
 	return x, nil
 }
 
+// SetEngineAffinity chooses where the context's packet conn engine runs its
+// threads (sqobfs_engine_set_affinity): l3 true (the default) keeps them on
+// the CPUs sharing the L3 cache of the goroutine's OS thread that opens the
+// first Conn, false leaves them to the scheduler.  Only before that first
+// Conn; an error after.
+func (x *Context) SetEngineAffinity(l3 bool) error {
+	x.mu.Lock()
+	defer x.mu.Unlock()
+	if x.c == nil {
+		return ErrClosed
+	}
+	mode := C.int(C.SQOBFS_ENGINE_AFFINITY_NONE)
+	if l3 {
+		mode = C.SQOBFS_ENGINE_AFFINITY_L3
+	}
+	return check(C.sqobfs_engine_set_affinity(x.c, mode))
+}
+
 // ref takes a reference; false once the context is gone.
 func (x *Context) ref() bool {
 	x.mu.Lock()
