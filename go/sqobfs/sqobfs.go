@@ -141,6 +141,22 @@ func (x *Context) SetEngineAffinity(l3 bool) error {
 	return check(C.sqobfs_engine_set_affinity(x.c, mode))
 }
 
+// SetEngineGroup bounds the coalesced launches of the context's engine
+// (sqobfs_engine_set_group): the queued batches of Conns over generic
+// PacketConns -- a hop client's conns -- join one launch, at most maxBatches
+// of them (0 = 8, 1 = every batch its own launch).  Any time.
+func (x *Context) SetEngineGroup(maxBatches int) error {
+	x.mu.Lock()
+	defer x.mu.Unlock()
+	if x.c == nil {
+		return ErrClosed
+	}
+	if maxBatches < 0 {
+		return check(C.SQ_EINVAL)
+	}
+	return check(C.sqobfs_engine_set_group(x.c, C.uint32_t(maxBatches)))
+}
+
 // ref takes a reference; false once the context is gone.
 func (x *Context) ref() bool {
 	x.mu.Lock()

@@ -756,6 +756,11 @@ typedef struct sqobfs_engine_info {
   uint32_t cpus;           /* CPUs the engine's threads are kept on (the L3
                               domain of the thread that started it; 0 = not
                               restricted: sqobfs_engine_set_affinity) */
+  uint32_t group_max;      /* the most batches one launch takes
+                              (sqobfs_engine_set_group) */
+  uint64_t launches;       /* kernel launches of the engine */
+  uint64_t group_launches; /* ... that carried the batches of several pconns */
+  uint64_t group_batches;  /* batches carried by those */
 } sqobfs_engine_info;
 /* ctx NULL: the host engine.  SQ_OK with zeros when it was never started. */
 int sqobfs_engine_info_get(sqobfs_ctx *ctx, sqobfs_engine_info *out);
@@ -771,6 +776,22 @@ int sqobfs_engine_set_workers(sqobfs_ctx *ctx, uint32_t workers);
 #define SQOBFS_ENGINE_AFFINITY_NONE 0
 #define SQOBFS_ENGINE_AFFINITY_L3 1
 int sqobfs_engine_set_affinity(sqobfs_ctx *ctx, int mode);
+/* Coalesced launches.  A Hysteria2 server wraps one socket
+ * (hysteria2/service.go:117-120) but a port-hopping client one conn per hop
+ * (hysteria/hop.go:40-63) over a generic PacketConn (client.go:184-186:
+ * pump mode here), and a process may serve many: when a worker launches the
+ * batch of a pump-mode pconn that leaves the routing to the engine (cpu_max
+ * 0 or SQOBFS_PCONN_NEVER), the batches other such pconns of the same scheme
+ * have queued in the same direction join that launch -- at most max_batches
+ * of them (0 = 8; 1 = every batch its own launch) and 16,384 datagrams -- so
+ * one kernel, one wait and one launch's host cost carry them all; under load
+ * (sqobfs_engine_info.loaded) they are gathered even when none would launch
+ * alone, and launch when together they pass the load rule (cpu_max).  Their
+ * PSKs may differ: the launch then reads per-datagram PSK ids into a keyring
+ * the engine merges from the pconns' keyrings.  Socket-mode pconns are not
+ * gathered (their batches' steps are socket calls that the workers keep
+ * making in parallel).  Any time. */
+int sqobfs_engine_set_group(sqobfs_ctx *ctx, uint32_t max_batches);
 /* Free the pool's unused blocks; returns how many were freed. */
 int sqobfs_engine_trim(sqobfs_ctx *ctx);
 /* Test hook: the next `count` launches of every engine fail -- at submission
@@ -782,6 +803,10 @@ void sqobfs_debug_engine_fail(int count, int at_completion);
  * (as a failed page-locked allocation); a socket pconn's receive side
  * retries on a timer and recovers. */
 void sqobfs_debug_pool_fail(int count);
+/* Test hook: while on, the engines' workers start no task (queued tasks
+ * wait; a running one finishes), so a test can queue the batches of several
+ * pconns and see them coalesced when it turns the hold off. */
+void sqobfs_debug_engine_hold(int on);
 
 #ifdef __cplusplus
 }

@@ -361,6 +361,51 @@ const sq::PskEntry *sq_keyring_host(const sqobfs_keyring *kr, uint32_t *count) {
 
 sqobfs_ctx *sq_keyring_ctx(const sqobfs_keyring *kr) { return kr->ctx; }
 
+void sq_keyring_hot(const sqobfs_keyring *kr, uint32_t *hot_m, uint32_t *hot_iv) {
+  *hot_m = kr->hot_m;
+  *hot_iv = kr->hot_iv;
+}
+
+int sq_keyring_from_entries(sqobfs_ctx *ctx, int kind, const sq::PskEntry *e, uint32_t count,
+                            uint32_t hot_m, uint32_t hot_iv, sqobfs_keyring **out) {
+  *out = nullptr;
+  if (!ctx || !e || count == 0) return SQ_EINVAL;
+  sqobfs_keyring *kr = new (std::nothrow) sqobfs_keyring();
+  if (!kr) return SQ_ENOMEM;
+  kr->ctx = ctx;
+  kr->kind = kind;
+  kr->count = count;
+  kr->hot_m = hot_m;
+  kr->hot_iv = hot_iv;
+  try {
+    kr->host.assign(e, e + count);
+  } catch (...) {
+    delete kr;
+    return SQ_ENOMEM;
+  }
+  kr->host0 = kr->host[0];
+  DeviceScope ds_(ctx->device);
+  int st = ds_.status;
+  // (the host entries are the device layout: sqobfs_debug_keyring_check)
+  if (st == SQ_OK)
+    st = hip_status(tab_alloc((void **)&kr->table, sizeof(sq::PskEntry) * count, ctx->stream));
+  if (st == SQ_OK)
+    st = hip_status(hipMemcpyAsync(kr->table, kr->host.data(), sizeof(sq::PskEntry) * count,
+                                   hipMemcpyHostToDevice, ctx->stream));
+  if (st == SQ_OK) st = hip_status(hipStreamSynchronize(ctx->stream));
+  if (st != SQ_OK) {
+    if (kr->table) {
+      (void)hipStreamSynchronize(ctx->stream);
+      tab_free_async(kr->table, ctx->stream);
+      (void)hipStreamSynchronize(ctx->stream);
+    }
+    delete kr;
+    return st;
+  }
+  *out = kr;
+  return SQ_OK;
+}
+
 void sq_salt_take(sqobfs_ctx *ctx, uint32_t key[8], uint64_t *seq) {
   if (!ctx) {
     sq_host_salt_take(key, seq);

@@ -193,6 +193,13 @@ int sq_host_alloc_mapped(sqobfs_ctx *ctx, size_t bytes, void **out);
 // (NULL for a host keyring)
 const sq::PskEntry *sq_keyring_host(const sqobfs_keyring *kr, uint32_t *count);
 sqobfs_ctx *sq_keyring_ctx(const sqobfs_keyring *kr);
+// the keyring's multi-PSK gather words (sq_api.hip keyring_hot_words)
+void sq_keyring_hot(const sqobfs_keyring *kr, uint32_t *hot_m, uint32_t *hot_iv);
+// a device keyring whose entries are copies of host entries (sq_keyring_host
+// of other keyrings; hot_m / hot_iv: the max / min of theirs): the engine's
+// merged keyrings, one launch over several pconns' batches (pconn.cpp)
+int sq_keyring_from_entries(sqobfs_ctx *ctx, int kind, const sq::PskEntry *e, uint32_t count,
+                            uint32_t hot_m, uint32_t hot_iv, sqobfs_keyring **out);
 // one sequence number of the context's salt stream (SQOBFS_FLAG_DEVICE_SALT)
 // and its key, for salts made on the host; ctx NULL: the process's host
 // generator (sq_cpu.cpp)

@@ -30,7 +30,9 @@
 //     per datagram) exceeds opts.cpu_max -- by default a measured
 //     break-even: the engine's recent launch round trip times its recent
 //     CPU-path rate (route_bytes), so a batch goes to the GPU when the CPU
-//     would take longer than a launch;
+//     would take longer than a launch -- or, under sustained load, when the
+//     CPU path would cost the host more than a launch does; the batches
+//     other pconns have queued then join that launch (run_task);
 //   * on the CPU (sq_cpu.h) otherwise, and always without a context (no GPU:
 //     the drop-in constructors never fail), and for good after a launch
 //     fails (a batch whose launch was refused is redone on the CPU; one whose
@@ -64,6 +66,7 @@
 #include <condition_variable>
 #include <deque>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <thread>
@@ -109,11 +112,16 @@ constexpr uint32_t kGsoMaxSegs = 64;       // UDP_MAX_SEGMENTS of older kernels
 constexpr uint32_t kGsoMaxBytes = 65000;   // one GSO send stays below 64 KiB of IP payload
 constexpr uint32_t kGroBuf = 65536;        // one coalesced receive
 constexpr size_t kCtlWords = (CMSG_SPACE(sizeof(uint16_t)) + 7) / 8;
+// one launch over several pconns' batches (run_task): at most group_max
+// batches (sqobfs_engine_set_group) and kGroupDgrams datagrams; a merged
+// keyring is made anew past kMergedMax PSKs
+constexpr uint32_t kDefGroup = 8, kMaxGroup = 64, kGroupDgrams = 16384, kMergedMax = 256;
 
-// sqobfs_debug_engine_fail, sqobfs_debug_pool_fail
+// sqobfs_debug_engine_fail, sqobfs_debug_pool_fail, sqobfs_debug_engine_hold
 std::atomic<int> g_fail_count{0};
 std::atomic<int> g_fail_at_completion{0};
 std::atomic<int> g_pool_fail{0};
+std::atomic<bool> g_hold{false};
 
 // take one unit of a test hook's countdown
 bool take_one(std::atomic<int> &c) {
@@ -236,6 +244,20 @@ struct Task {
   int dir;  // kTx / kRx
 };
 
+// A keyring the engine made for coalesced launches over pconns with
+// different keyrings: copies of their entry 0 (merged_keyring).
+struct MergedKeyring {
+  sqobfs_keyring *kr = nullptr;
+  std::vector<sq::PskEntry> e;
+  uint32_t hot_m = 0, hot_iv = 1;
+  MergedKeyring() = default;
+  MergedKeyring(const MergedKeyring &) = delete;
+  MergedKeyring &operator=(const MergedKeyring &) = delete;
+  ~MergedKeyring() {
+    if (kr) sqobfs_keyring_destroy(kr);  // (stream-ordered after its launches)
+  }
+};
+
 struct Engine {
   sqobfs_ctx *ctx = nullptr;  // NULL: the host engine (CPU only)
   uint32_t nworkers = kDefWorkers;
@@ -265,6 +287,12 @@ struct Engine {
   // (EWMA, us); the wait sleeps 3/4 of it, then polls, so the estimate
   // tracks the kernel and not the wait's own sleep
   std::atomic<uint32_t> kern_us{30};
+  // coalesced launches (run_task): the most batches one takes, the merged
+  // keyrings of each scheme, and counts
+  std::atomic<uint32_t> group_max{kDefGroup};
+  std::mutex mkr_mu;
+  std::shared_ptr<MergedKeyring> mkr[2];
+  std::atomic<uint64_t> launches{0}, group_launches{0}, group_batches{0};
 
   // the CPUs the engine's threads run on (sqobfs_engine_set_affinity);
   // ncpus 0: not restricted
@@ -300,6 +328,7 @@ std::mutex g_eng_mu;
 std::map<sqobfs_ctx *, Engine *> g_engines;     // ctx NULL: the host engine (never ended)
 std::map<sqobfs_ctx *, uint32_t> g_workers_cfg;  // sqobfs_engine_set_workers
 std::map<sqobfs_ctx *, int> g_affinity_cfg;      // sqobfs_engine_set_affinity
+std::map<sqobfs_ctx *, uint32_t> g_group_cfg;    // sqobfs_engine_set_group
 
 // L3 (CCD) id of a CPU from sysfs; -1 when unknown
 int l3_of(int cpu) {
@@ -358,6 +387,8 @@ Engine *engine_get(sqobfs_ctx *ctx, int *status) {
   auto a = g_affinity_cfg.find(ctx);
   const int aff = a != g_affinity_cfg.end() ? a->second : SQOBFS_ENGINE_AFFINITY_L3;
   if (aff == SQOBFS_ENGINE_AFFINITY_L3) E->ncpus = l3_cpus(&E->cpus);
+  auto gc = g_group_cfg.find(ctx);
+  if (gc != g_group_cfg.end()) E->group_max = gc->second;
   E->streams.assign(E->nworkers, nullptr);
   E->wake = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
   E->epfd = epoll_create1(EPOLL_CLOEXEC);
@@ -541,9 +572,23 @@ void task_end(sqobfs_pconn *pc, int d, bool more, int64_t due = 0) {
 
 // ---------------------------------------------------------------- transform
 
-// The batch's bytes, GPU or CPU (module comment).  Returns SQ_OK, or an
-// error when the batch is lost (a launch that failed after it started);
-// *cpu / *failed report what happened, for the pconn's stats.
+// One task's batch between the task's prepare and finish steps, so that one
+// worker can transform the batches of several tasks with one launch.
+struct Job {
+  sqobfs_pconn *pc = nullptr;
+  int dir = kTx;        // the task's direction: kTx obfuscates, kRx deobfuscates
+  uint32_t idx = 0;     // its batch: pc->tb[idx] / pc->rb[idx]
+  bool slotted = true;  // datagrams in slots (not packed in GRO buffers)
+  uint64_t trunc = 0;   // socket receive: truncated datagrams
+  uint64_t cost = 0;    // payload bytes + kHashCost per datagram
+  int st = SQ_OK;
+  bool cpu = false, failed = false;
+  PBatch &batch() const { return dir == kTx ? pc->tb[idx] : pc->rb[idx]; }
+  int op() const { return dir == kTx ? SQOBFS_OBFUSCATE : SQOBFS_DEOBFUSCATE; }
+};
+
+constexpr int kRefused = 1;  // gpu_run: nothing ran
+
 // The measured break-even cost: the CPU path would take a launch's round
 // trip on a batch of this cost.
 uint64_t route_bytes(const Engine *E) {
@@ -573,12 +618,30 @@ void note_demand(Engine *E, uint64_t cost) {
   else if (sm < kLoadOffPermille) E->loaded.store(false, std::memory_order_relaxed);
 }
 
-int transform(Engine *E, uint32_t w, sqobfs_pconn *pc, int dir, PBatch &b, bool slotted,
-              bool *cpu, bool *failed) {
-  *cpu = false;
-  *failed = false;
-  Block &k = *b.blk;
-  sqobfs_batch d;
+// Where a job's batch is transformed (module comment): true for the GPU.
+// Sets j.cost and *bulk (launched because of load: its wait does not poll).
+bool route_gpu(Engine *E, Job &j, bool *bulk) {
+  const PBatch &b = j.batch();
+  const Block &k = *b.blk;
+  uint64_t cost = 0;
+  for (uint32_t i = 0; i < b.n; i++) cost += k.len[i] + kHashCost;
+  j.cost = cost;
+  const uint32_t cmax = j.pc->o.cpu_max;
+  if (cmax == 0 && E->ctx) note_demand(E, cost);
+  // loaded (cpu_max 0): a batch of more than kLoadMinDgrams launches when
+  // the CPU path would cost the host more than a launch does
+  *bulk = cmax == 0 && b.n > kLoadMinDgrams && E->loaded.load(std::memory_order_relaxed) &&
+          cost * E->cpu_ns_kib.load(std::memory_order_relaxed) / 1024u >
+              2ull * E->gpu_host_ns.load(std::memory_order_relaxed);
+  return E->ctx && !E->gpu_off.load(std::memory_order_relaxed) &&
+         (cmax == SQOBFS_PCONN_NEVER || *bulk ||
+          cost > (cmax == 0 ? route_bytes(E) : (uint64_t)cmax));
+}
+
+// A job's batch as a descriptor over its own block.
+void block_batch(const Job &j, sqobfs_batch &d) {
+  const PBatch &b = j.batch();
+  const Block &k = *b.blk;
   memset(&d, 0, sizeof d);
   d.n = b.n;
   d.in = k.slots;
@@ -587,78 +650,200 @@ int transform(Engine *E, uint32_t w, sqobfs_pconn *pc, int dir, PBatch &b, bool 
   d.out = k.slots;
   d.out_off = k.out_off;
   d.out_len = k.out_len;
-  uint64_t cost = 0;
-  for (uint32_t i = 0; i < b.n; i++) cost += k.len[i] + kHashCost;
-  const uint32_t cmax = pc->o.cpu_max;
-  if (cmax == 0 && E->ctx) note_demand(E, cost);
-  // loaded (cpu_max 0): a batch of more than kLoadMinDgrams launches when
-  // the CPU path would cost the host more than a launch does
-  const bool bulk = cmax == 0 && b.n > kLoadMinDgrams &&
-                    E->loaded.load(std::memory_order_relaxed) &&
-                    cost * E->cpu_ns_kib.load(std::memory_order_relaxed) / 1024u >
-                        2ull * E->gpu_host_ns.load(std::memory_order_relaxed);
-  const bool want_gpu = E->ctx && !E->gpu_off.load(std::memory_order_relaxed) &&
-                        (cmax == SQOBFS_PCONN_NEVER || bulk ||
-                         cost > (cmax == 0 ? route_bytes(E) : (uint64_t)cmax));
-  if (want_gpu) {
-    // slots are multiples of 16 bytes: every output owns its blocks, so the
-    // kernel writes them whole (SQOBFS_FLAG_OUT_BLOCKS); GRO buffers pack the
-    // datagrams back to back (no flag)
-    d.flags = (slotted ? SQOBFS_FLAG_OUT_BLOCKS : 0u) |
-              (dir == SQOBFS_OBFUSCATE ? SQOBFS_FLAG_DEVICE_SALT : 0u);
-    int st = SQ_OK;
-    if (!E->streams[w]) {  // (only worker w writes its slot; close reads it under mu)
-      void *s = nullptr;
-      st = sq_ctx_stream_create(E->ctx, &s);
-      std::lock_guard<std::mutex> lk(E->mu);
-      E->streams[w] = s;
-    }
-    const int inject = take_one(g_fail_count) ? (g_fail_at_completion.load() ? 2 : 1) : 0;
-    const int64_t t0 = mono_ns(), c0 = thread_cpu_ns();
-    if (st == SQ_OK) st = inject == 1 ? SQ_EDEVICE : sqobfs_launch(E->ctx, pc->kr, dir, &d, E->streams[w]);
-    if (st != SQ_OK) {
-      // refused before anything ran: the batch is intact, redo it on the CPU.
-      // Only a device failure turns the GPU off for the engine; a refusal of
-      // this batch or this moment (no memory for a stream or staging) leaves
-      // the next batch free to launch
-      if (st == SQ_EDEVICE || st == SQ_ENODEV) E->gpu_off.store(true);
-      *failed = true;
-    } else {
-      const uint32_t ew = E->launch_us.load(std::memory_order_relaxed);
-      // bulk batches and spin_us NEVER block at once (an interrupt-signalled
-      // event: the worker's core is free while the kernel runs)
-      const bool block = bulk || pc->o.spin_us == SQOBFS_PCONN_NEVER;
-      const uint32_t spin = std::min<uint32_t>(pc->o.spin_us, 2 * ew + 20);
-      const uint32_t ek = E->kern_us.load(std::memory_order_relaxed);
-      st = block ? sq_ctx_stream_wait_blocking(E->ctx, E->streams[w], ek * 3 / 4)
-                 : sq_ctx_stream_wait(E->ctx, E->streams[w], spin);
-      if (inject == 2) st = SQ_EDEVICE;
-      if (st != SQ_OK) {
-        // the kernel ran, in place, and failed: the slots' state is unknown
-        E->gpu_off.store(true);
-        *failed = true;
-        return st;
-      }
-      const uint32_t us = (uint32_t)std::min<int64_t>((mono_ns() - t0) / 1000, 100000);
-      E->launch_us.store((7 * ew + us) / 8, std::memory_order_relaxed);
-      if (block) {  // the host's cost of a launched batch (polled waits would count their spin)
-        E->kern_us.store((7 * E->kern_us.load(std::memory_order_relaxed) + us) / 8,
-                         std::memory_order_relaxed);
-        const uint32_t hn = (uint32_t)std::min<int64_t>(thread_cpu_ns() - c0, 10'000'000);
-        const uint32_t eh = E->gpu_host_ns.load(std::memory_order_relaxed);
-        E->gpu_host_ns.store((7 * eh + hn) / 8, std::memory_order_relaxed);
-      }
-      return SQ_OK;
-    }
+}
+
+// The engine's keyring for one launch over the jobs' batches when their
+// pconns hold different keyrings: one entry per distinct PSK state (the
+// pconns' keyring entry 0, compared by content, so a keyring freed and
+// another made at its address cannot alias), kept and extended while it has
+// room, made anew past kMergedMax entries.  pid[j] = job j's entry.  NULL,
+// with *st, when it cannot be made.
+std::shared_ptr<MergedKeyring> merged_keyring(Engine *E, const Job *jobs, uint32_t nj,
+                                              uint16_t *pid, int *st) {
+  const int kind = jobs[0].pc->kind;
+  const int ki = kind == SQOBFS_SALAMANDER ? 0 : 1;
+  auto find = [](const MergedKeyring *m, const sq::PskEntry *x) -> int {
+    if (m)
+      for (size_t i = 0; i < m->e.size(); i++)
+        if (!memcmp(&m->e[i], x, sizeof *x)) return (int)i;
+    return -1;
+  };
+  std::lock_guard<std::mutex> g(E->mkr_mu);
+  std::shared_ptr<MergedKeyring> cur = E->mkr[ki];
+  uint32_t j = 0;
+  for (; j < nj; j++) {
+    const int i = find(cur.get(), jobs[j].pc->psk0);
+    if (i < 0) break;
+    pid[j] = (uint16_t)i;
   }
-  // the CPU path (sq_cpu.h): salts of the context's stream, as a launch's
-  *cpu = true;
+  if (j == nj) return cur;
+  std::shared_ptr<MergedKeyring> m;
+  try {
+    m = std::make_shared<MergedKeyring>();
+    if (cur && cur->e.size() + nj <= kMergedMax) {
+      m->e = cur->e;
+      m->hot_m = cur->hot_m;
+      m->hot_iv = cur->hot_iv;
+    }
+    for (j = 0; j < nj; j++) {
+      int i = find(m.get(), jobs[j].pc->psk0);
+      if (i < 0) {
+        m->e.push_back(*jobs[j].pc->psk0);
+        i = (int)m->e.size() - 1;
+        uint32_t hm, hi;
+        sq_keyring_hot(jobs[j].pc->kr, &hm, &hi);
+        m->hot_m = std::max(m->hot_m, hm);
+        m->hot_iv = std::min(m->hot_iv, hi);
+      }
+      pid[j] = (uint16_t)i;
+    }
+  } catch (...) {
+    *st = SQ_ENOMEM;
+    return nullptr;
+  }
+  *st = sq_keyring_from_entries(E->ctx, kind, m->e.data(), (uint32_t)m->e.size(), m->hot_m,
+                                m->hot_iv, &m->kr);
+  if (*st != SQ_OK) return nullptr;
+  E->mkr[ki] = m;  // (the old one is destroyed when its last launch lets go)
+  return m;
+}
+
+// Launches the jobs' batches on worker w's stream and waits.  One batch:
+// over its own block.  Several (coalesced, run_task): over one descriptor
+// built in a block of the pool, every datagram addressed from the lowest of
+// their blocks (blocks are mapped at their host addresses, so one base
+// reaches them all), with per-datagram PSK ids into a merged keyring when
+// the pconns' keyrings differ; out_len is copied back into each block.
+// Returns SQ_OK; kRefused when nothing ran (the batches are intact, for the
+// CPU path); or the error of a kernel that failed (the batches, transformed
+// in place, are lost).  A device failure turns the GPU off for the engine;
+// a refusal of this batch or this moment (no memory for a stream, a block
+// or a keyring) leaves the next batch free to launch.
+int gpu_run(Engine *E, uint32_t w, Job *jobs, uint32_t nj, bool block) {
+  auto refused = [E](int st) {
+    if (st == SQ_EDEVICE || st == SQ_ENODEV) E->gpu_off.store(true);
+    return kRefused;
+  };
+  int st = SQ_OK;
+  if (!E->streams[w]) {  // (only worker w writes its slot; close reads it under mu)
+    void *s = nullptr;
+    st = sq_ctx_stream_create(E->ctx, &s);
+    std::lock_guard<std::mutex> lk(E->mu);
+    E->streams[w] = s;
+  }
+  if (st != SQ_OK) return refused(st);
+  const int op = jobs[0].op();
+  const sqobfs_keyring *kr = jobs[0].pc->kr;
+  std::shared_ptr<MergedKeyring> mk;
+  Block *gb = nullptr;
+  sqobfs_batch d;
+  bool slotted = jobs[0].slotted;
+  if (nj == 1) {
+    block_batch(jobs[0], d);
+  } else {
+    gb = block_take(E, kGroupDgrams, 16);  // (psk ids in its slot region)
+    if (!gb) return kRefused;
+    bool same = true;
+    for (uint32_t j = 1; j < nj; j++) same = same && jobs[j].pc->kr == kr;
+    uint16_t pid[kMaxGroup] = {};
+    if (!same) {
+      mk = merged_keyring(E, jobs, nj, pid, &st);
+      if (!mk) {
+        block_give(E, gb);
+        return refused(st);
+      }
+      kr = mk->kr;
+    }
+    uint8_t *base = jobs[0].batch().blk->slots;
+    for (uint32_t j = 1; j < nj; j++) base = std::min(base, jobs[j].batch().blk->slots);
+    uint16_t *ids = (uint16_t *)gb->slots;
+    uint32_t n = 0;
+    for (uint32_t j = 0; j < nj; j++) {
+      const PBatch &b = jobs[j].batch();
+      const Block &k = *b.blk;
+      const uint64_t delta = (uint64_t)(k.slots - base);
+      for (uint32_t i = 0; i < b.n; i++, n++) {
+        gb->in_off[n] = delta + k.in_off[i];
+        gb->out_off[n] = delta + k.out_off[i];
+        gb->len[n] = k.len[i];
+        ids[n] = pid[j];
+      }
+      slotted = slotted && jobs[j].slotted;
+    }
+    memset(&d, 0, sizeof d);
+    d.n = n;
+    d.in = base;
+    d.in_off = gb->in_off;
+    d.in_len = gb->len;
+    d.out = base;
+    d.out_off = gb->out_off;
+    d.out_len = gb->out_len;
+    d.psk_id = same ? nullptr : ids;
+  }
+  // slots are multiples of 16 bytes: every output owns its blocks, so the
+  // kernel writes them whole (SQOBFS_FLAG_OUT_BLOCKS); GRO buffers pack the
+  // datagrams back to back (no flag)
+  d.flags = (slotted ? SQOBFS_FLAG_OUT_BLOCKS : 0u) |
+            (op == SQOBFS_OBFUSCATE ? SQOBFS_FLAG_DEVICE_SALT : 0u);
+  const int inject = take_one(g_fail_count) ? (g_fail_at_completion.load() ? 2 : 1) : 0;
+  const int64_t t0 = mono_ns(), c0 = thread_cpu_ns();
+  st = inject == 1 ? SQ_EDEVICE : sqobfs_launch(E->ctx, kr, op, &d, E->streams[w]);
+  if (st != SQ_OK) {
+    if (gb) block_give(E, gb);
+    return refused(st);
+  }
+  E->launches.fetch_add(1, std::memory_order_relaxed);
+  if (nj > 1) {
+    E->group_launches.fetch_add(1, std::memory_order_relaxed);
+    E->group_batches.fetch_add(nj, std::memory_order_relaxed);
+  }
+  const uint32_t ew = E->launch_us.load(std::memory_order_relaxed);
+  // bulk batches and spin_us NEVER block at once (the worker's core is free
+  // while the kernel runs)
+  const uint32_t spin = std::min<uint32_t>(jobs[0].pc->o.spin_us, 2 * ew + 20);
+  const uint32_t ek = E->kern_us.load(std::memory_order_relaxed);
+  st = block ? sq_ctx_stream_wait_blocking(E->ctx, E->streams[w], ek * 3 / 4)
+             : sq_ctx_stream_wait(E->ctx, E->streams[w], spin);
+  if (inject == 2) st = SQ_EDEVICE;
+  if (st != SQ_OK) {
+    // the kernel ran, in place, and failed: the slots' state is unknown
+    if (gb) block_give(E, gb);
+    E->gpu_off.store(true);
+    return st;
+  }
+  const uint32_t us = (uint32_t)std::min<int64_t>((mono_ns() - t0) / 1000, 100000);
+  E->launch_us.store((7 * ew + us) / 8, std::memory_order_relaxed);
+  if (block) {  // the host's cost of a launched batch (polled waits would count their spin)
+    E->kern_us.store((7 * E->kern_us.load(std::memory_order_relaxed) + us) / 8,
+                     std::memory_order_relaxed);
+    const uint32_t hn = (uint32_t)std::min<int64_t>(thread_cpu_ns() - c0, 10'000'000);
+    const uint32_t eh = E->gpu_host_ns.load(std::memory_order_relaxed);
+    E->gpu_host_ns.store((7 * eh + hn) / 8, std::memory_order_relaxed);
+  }
+  if (gb) {
+    uint32_t n = 0;
+    for (uint32_t j = 0; j < nj; j++) {
+      const PBatch &b = jobs[j].batch();
+      for (uint32_t i = 0; i < b.n; i++) b.blk->out_len[i] = gb->out_len[n++];
+    }
+    block_give(E, gb);
+  }
+  return SQ_OK;
+}
+
+// The CPU path (sq_cpu.h) of a job's batch: salts of the context's stream,
+// as a launch's.
+int cpu_run(Engine *E, const Job &j) {
+  sqobfs_pconn *pc = j.pc;
+  const PBatch &b = j.batch();
+  sqobfs_batch d;
+  block_batch(j, d);
   uint32_t count = 0;
   const sq::PskEntry *tab = sq_keyring_host(pc->kr, &count);
   uint8_t sbuf[64 * 16];
   std::vector<uint8_t> sv;
   uint8_t *salts = nullptr;
-  if (dir == SQOBFS_OBFUSCATE) {
+  if (j.dir == kTx) {
     const size_t bytes = (size_t)b.n * pc->S;
     salts = sbuf;
     if (bytes > sizeof sbuf) {
@@ -671,10 +856,10 @@ int transform(Engine *E, uint32_t w, sqobfs_pconn *pc, int dir, PBatch &b, bool 
     sq::cpu::salt_stream(key, seq, salts, bytes);
   }
   const int64_t t0 = mono_ns();
-  const int st = sq::cpu::run_batch(pc->kind, dir, tab, count, &d, salts);
-  if (cost >= kRouteSample) {  // (smaller batches: timer noise)
+  const int st = sq::cpu::run_batch(pc->kind, j.op(), tab, count, &d, salts);
+  if (j.cost >= kRouteSample) {  // (smaller batches: timer noise)
     const uint64_t ns = (uint64_t)std::max<int64_t>(0, mono_ns() - t0);
-    const uint32_t now = (uint32_t)std::min<uint64_t>(1u << 20, ns * 1024u / cost);
+    const uint32_t now = (uint32_t)std::min<uint64_t>(1u << 20, ns * 1024u / j.cost);
     const uint32_t ew = E->cpu_ns_kib.load(std::memory_order_relaxed);
     E->cpu_ns_kib.store((7 * ew + now) / 8, std::memory_order_relaxed);
   }
@@ -762,56 +947,72 @@ int send_batch(sqobfs_pconn *pc, PBatch &b, uint32_t from, int *first_err, uint6
 }
 
 // Transform bookkeeping shared by the tasks (under pc->mu).
-void note_transform(sqobfs_pconn *pc, bool cpu, bool failed, int st, uint32_t n) {
-  if (cpu) pc->st.cpu_batches++;
-  if (failed) pc->st.gpu_failures++;
-  if (st != SQ_OK) pc->st.dropped += n;
+void note_transform(sqobfs_pconn *pc, const Job &j) {
+  if (j.cpu) pc->st.cpu_batches++;
+  if (j.failed) pc->st.gpu_failures++;
+  if (j.st != SQ_OK && j.st != SQ_ECLOSED) pc->st.dropped += j.batch().n;
 }
 
 // ---------------------------------------------------------------- tasks
+//
+// A task runs in two steps around the transform of its batch: prepare (take
+// the batch; false when the task ended without one) and finish (send or
+// queue it, end or requeue the task).  run_task joins them, so that the
+// batches of several tasks can share one launch.
 
 // Transmit: the next queued batch (or the filling one, once its linger is
 // due) -> transform -> sendmmsg (socket mode) or the pump taker.
-void tx_task(Engine *E, uint32_t w, sqobfs_pconn *pc) {
+bool tx_prepare(sqobfs_pconn *pc, Job &j) {
   std::unique_lock<std::mutex> lk(pc->mu);
-  if (pc->closed) return task_end(pc, kTx, false);
+  if (pc->closed) {
+    task_end(pc, kTx, false);
+    return false;
+  }
   if (pc->tq.empty()) {
     if (pc->tfill >= 0 && pc->tb[pc->tfill].n > 0) {
       const int64_t due = pc->tb[pc->tfill].first_ns + (int64_t)pc->o.linger_us * 1000;
-      if (pc->o.linger_us && !pc->writes_closed && mono_ns() < due)
-        return task_end(pc, kTx, true, due);
+      if (pc->o.linger_us && !pc->writes_closed && mono_ns() < due) {
+        task_end(pc, kTx, true, due);
+        return false;
+      }
       pc->tq.push_back((uint32_t)pc->tfill);
       pc->tfill = -1;
     } else {
-      return task_end(pc, kTx, false);
+      task_end(pc, kTx, false);
+      return false;
     }
   }
-  const uint32_t idx = pc->tq.front();
+  j.pc = pc;
+  j.dir = kTx;
+  j.idx = pc->tq.front();
+  j.slotted = true;
   pc->tq.pop_front();
   pc->tx_busy = true;
-  PBatch &b = pc->tb[idx];
-  lk.unlock();
-  bool cpu, failed;
-  int st = transform(E, w, pc, SQOBFS_OBFUSCATE, b, true, &cpu, &failed);
+  return true;
+}
+
+void tx_finish(Job &j) {
+  sqobfs_pconn *pc = j.pc;
+  PBatch &b = j.batch();
   int send_err = 0;
   uint64_t nerr = 0;
-  if (st == SQ_OK && pc->socket_mode()) st = send_batch(pc, b, 0, &send_err, &nerr);
-  lk.lock();
+  if (j.st == SQ_OK && pc->socket_mode()) j.st = send_batch(pc, b, 0, &send_err, &nerr);
+  std::unique_lock<std::mutex> lk(pc->mu);
   pc->tx_busy = false;
-  note_transform(pc, cpu, failed, st == SQ_ECLOSED ? SQ_OK : st, b.n);
+  note_transform(pc, j);
   if (send_err && !pc->tx_err) pc->tx_err = send_err;
   pc->st.tx_send_errors += nerr;
-  if (st == SQ_OK) {
+  if (j.st == SQ_OK) {
     pc->st.tx_datagrams += b.n;
     pc->st.tx_batches++;
     pc->st.tx_max_batch = std::max(pc->st.tx_max_batch, b.n);
   }
-  if (st == SQ_OK && !pc->socket_mode()) {
-    pc->ttaken.push_back(idx);
+  if (j.st == SQ_OK && !pc->socket_mode()) {
+    pc->ttaken.push_back(j.idx);
     pc->cv_take.notify_one();
   } else {
     batch_detach(pc, b);
-    pc->tfree.push_back(idx);
+    pc->tfree.push_back(j.idx);
   }
   pc->cv_txs.notify_all();
   const bool more = !pc->tq.empty() || (pc->tfill >= 0 && pc->tb[pc->tfill].n > 0);
@@ -819,39 +1020,57 @@ void tx_task(Engine *E, uint32_t w, sqobfs_pconn *pc) {
 }
 
 // Receive, pump mode: the batch the caller pushed -> deobfuscate -> ready.
-void rx_pump_task(Engine *E, uint32_t w, sqobfs_pconn *pc) {
+bool rx_pump_prepare(sqobfs_pconn *pc, Job &j) {
   std::unique_lock<std::mutex> lk(pc->mu);
-  if (pc->closed) return task_end(pc, kRx, false);
+  if (pc->closed) {
+    task_end(pc, kRx, false);
+    return false;
+  }
   if (pc->rq.empty()) {
     if (pc->rfill >= 0 && pc->rb[pc->rfill].n > 0) {
       const int64_t due = pc->rb[pc->rfill].first_ns + (int64_t)pc->o.linger_us * 1000;
-      if (pc->o.linger_us && mono_ns() < due) return task_end(pc, kRx, true, due);
+      if (pc->o.linger_us && mono_ns() < due) {
+        task_end(pc, kRx, true, due);
+        return false;
+      }
       pc->rq.push_back((uint32_t)pc->rfill);
       pc->rfill = -1;
     } else {
-      return task_end(pc, kRx, false);
+      task_end(pc, kRx, false);
+      return false;
     }
   }
-  const uint32_t idx = pc->rq.front();
+  j.pc = pc;
+  j.dir = kRx;
+  j.idx = pc->rq.front();
+  j.slotted = true;
   pc->rq.pop_front();
-  PBatch &b = pc->rb[idx];
-  b.next = 0;
-  lk.unlock();
-  bool cpu, failed;
-  const int st = transform(E, w, pc, SQOBFS_DEOBFUSCATE, b, true, &cpu, &failed);
-  lk.lock();
-  note_transform(pc, cpu, failed, st, b.n);
-  if (st != SQ_OK) {  // lost with the failed launch
+  pc->rb[j.idx].next = 0;
+  return true;
+}
+
+// (pump and socket receive) the batch is ready to read, or lost with a
+// failed launch.  Caller holds pc->mu.
+void rx_done(sqobfs_pconn *pc, Job &j) {
+  PBatch &b = j.batch();
+  note_transform(pc, j);
+  if (j.st != SQ_OK) {
     batch_detach(pc, b);
-    pc->rfree.push_back(idx);
+    pc->rfree.push_back(j.idx);
     pc->cv_rxs.notify_all();
   } else {
     pc->st.rx_datagrams += b.n;
     pc->st.rx_batches++;
     pc->st.rx_max_batch = std::max(pc->st.rx_max_batch, b.n);
-    pc->rready.push_back(idx);
+    pc->rready.push_back(j.idx);
     pc->cv_rxr.notify_all();
   }
+}
+
+void rx_pump_finish(Job &j) {
+  sqobfs_pconn *pc = j.pc;
+  std::unique_lock<std::mutex> lk(pc->mu);
+  rx_done(pc, j);
   const bool more = !pc->rq.empty() || (pc->rfill >= 0 && pc->rb[pc->rfill].n > 0);
   task_end(pc, kRx, more);
 }
@@ -866,12 +1085,16 @@ void rearm(Engine *E, sqobfs_pconn *pc) {
 // Receive, socket mode (the poller saw the socket readable): recvmmsg one
 // batch -> deobfuscate -> ready; requeued while the socket has more, the
 // socket re-armed when it is drained.
-void rx_socket_task(Engine *E, uint32_t w, sqobfs_pconn *pc) {
+bool rx_socket_prepare(Engine *E, sqobfs_pconn *pc, Job &j) {
   std::unique_lock<std::mutex> lk(pc->mu);
-  if (pc->closed || pc->rx_dead) return task_end(pc, kRx, false);
+  if (pc->closed || pc->rx_dead) {
+    task_end(pc, kRx, false);
+    return false;
+  }
   if (pc->rfree.empty()) {  // every batch holds unread datagrams: read() restarts us
     pc->rx_stall = true;
-    return task_end(pc, kRx, false);
+    task_end(pc, kRx, false);
+    return false;
   }
   const uint32_t idx = pc->rfree.front();
   pc->rfree.pop_front();
@@ -880,11 +1103,13 @@ void rx_socket_task(Engine *E, uint32_t w, sqobfs_pconn *pc) {
     pc->rfree.push_front(idx);
     if (!pc->rready.empty()) {
       pc->rx_stall = true;  // no memory now: the read() that frees a batch retries
-      return task_end(pc, kRx, false);
+      task_end(pc, kRx, false);
+      return false;
     }
     // nothing to read, so no read() will come back here: retry on a timer
     // (the socket stays un-armed meanwhile; its datagrams wait in the kernel)
-    return task_end(pc, kRx, true, mono_ns() + kAttachRetryNs);
+    task_end(pc, kRx, true, mono_ns() + kAttachRetryNs);
+    return false;
   }
   lk.unlock();
   // GRO: the batch's slot region as 64 KiB buffers of up to 64 coalesced
@@ -895,17 +1120,17 @@ void rx_socket_task(Engine *E, uint32_t w, sqobfs_pconn *pc) {
                                 : 0;
   const uint32_t want = pc->gro ? ngro : pc->o.batch;
   Block &k = *b.blk;
-  for (uint32_t j = 0; j < want; j++) {
-    pc->riov[j].iov_base = pc->gro ? k.slots + (size_t)j * kGroBuf : pc->slot(b, j);
-    pc->riov[j].iov_len = pc->gro ? kGroBuf : pc->o.slot_bytes;
-    memset(&pc->rmsg[j], 0, sizeof pc->rmsg[j]);
-    pc->rmsg[j].msg_hdr.msg_iov = &pc->riov[j];
-    pc->rmsg[j].msg_hdr.msg_iovlen = 1;
-    pc->rmsg[j].msg_hdr.msg_name = &pc->rss[j];
-    pc->rmsg[j].msg_hdr.msg_namelen = sizeof pc->rss[j];
+  for (uint32_t q = 0; q < want; q++) {
+    pc->riov[q].iov_base = pc->gro ? k.slots + (size_t)q * kGroBuf : pc->slot(b, q);
+    pc->riov[q].iov_len = pc->gro ? kGroBuf : pc->o.slot_bytes;
+    memset(&pc->rmsg[q], 0, sizeof pc->rmsg[q]);
+    pc->rmsg[q].msg_hdr.msg_iov = &pc->riov[q];
+    pc->rmsg[q].msg_hdr.msg_iovlen = 1;
+    pc->rmsg[q].msg_hdr.msg_name = &pc->rss[q];
+    pc->rmsg[q].msg_hdr.msg_namelen = sizeof pc->rss[q];
     if (pc->gro) {
-      pc->rmsg[j].msg_hdr.msg_control = &pc->rctl[8ull * j];
-      pc->rmsg[j].msg_hdr.msg_controllen = 8 * sizeof(uint64_t);
+      pc->rmsg[q].msg_hdr.msg_control = &pc->rctl[8ull * q];
+      pc->rmsg[q].msg_hdr.msg_controllen = 8 * sizeof(uint64_t);
     }
   }
   int m;
@@ -927,27 +1152,28 @@ void rx_socket_task(Engine *E, uint32_t w, sqobfs_pconn *pc) {
       pc->cv_rxr.notify_all();
     }
     if (!pc->rx_dead) rearm(E, pc);
-    return task_end(pc, kRx, false);
+    task_end(pc, kRx, false);
+    return false;
   }
   uint64_t trunc = 0;
   uint32_t n = 0;
   if (pc->gro) {
     // split every coalesced message into its datagrams (cmsg UDP_GRO gives
     // the segment size; the last may be shorter), decoded in place
-    for (int j = 0; j < m; j++) {
-      const uint32_t total = pc->rmsg[j].msg_len;
+    for (int q = 0; q < m; q++) {
+      const uint32_t total = pc->rmsg[q].msg_len;
       uint32_t seg = total;
-      for (cmsghdr *cm = CMSG_FIRSTHDR(&pc->rmsg[j].msg_hdr); cm;
-           cm = CMSG_NXTHDR(&pc->rmsg[j].msg_hdr, cm))
+      for (cmsghdr *cm = CMSG_FIRSTHDR(&pc->rmsg[q].msg_hdr); cm;
+           cm = CMSG_NXTHDR(&pc->rmsg[q].msg_hdr, cm))
         if (cm->cmsg_level == SOL_UDP && cm->cmsg_type == UDP_GRO) {
           int v;
           memcpy(&v, CMSG_DATA(cm), sizeof v);
           if (v > 0) seg = (uint32_t)v;
         }
-      if (pc->rmsg[j].msg_hdr.msg_flags & MSG_TRUNC) trunc++;
+      if (pc->rmsg[q].msg_hdr.msg_flags & MSG_TRUNC) trunc++;
       sqobfs_addr from;
-      sq::from_sockaddr(pc->rss[j], &from);
-      const uint64_t base = (uint64_t)j * kGroBuf;
+      sq::from_sockaddr(pc->rss[q], &from);
+      const uint64_t base = (uint64_t)q * kGroBuf;
       for (uint32_t o = 0; (o < total || (total == 0 && o == 0)) && n < pc->o.batch;
            o += seg ? seg : 1) {
         const uint32_t l = std::min(seg, total - o);
@@ -962,33 +1188,133 @@ void rx_socket_task(Engine *E, uint32_t w, sqobfs_pconn *pc) {
       }
     }
   } else {
-    for (int j = 0; j < m; j++) {
-      k.len[j] = std::min<uint32_t>(pc->rmsg[j].msg_len, pc->o.slot_bytes);
-      memcpy(&b.head[16ull * j], pc->slot(b, (uint32_t)j), 16);
-      if (pc->rmsg[j].msg_hdr.msg_flags & MSG_TRUNC) trunc++;
-      sq::from_sockaddr(pc->rss[j], &b.addr[j]);
-      b.tag[j] = 0;
+    for (int q = 0; q < m; q++) {
+      k.len[q] = std::min<uint32_t>(pc->rmsg[q].msg_len, pc->o.slot_bytes);
+      memcpy(&b.head[16ull * q], pc->slot(b, (uint32_t)q), 16);
+      if (pc->rmsg[q].msg_hdr.msg_flags & MSG_TRUNC) trunc++;
+      sq::from_sockaddr(pc->rss[q], &b.addr[q]);
+      b.tag[q] = 0;
     }
     n = (uint32_t)m;
   }
   b.n = n;
   b.next = 0;
-  bool cpu, failed;
-  const int st = transform(E, w, pc, SQOBFS_DEOBFUSCATE, b, !pc->gro, &cpu, &failed);
-  lk.lock();
-  pc->st.rx_truncated += trunc;
-  note_transform(pc, cpu, failed, st, b.n);
-  if (st != SQ_OK) {
-    batch_detach(pc, b);
-    pc->rfree.push_back(idx);
-  } else {
-    pc->st.rx_datagrams += b.n;
-    pc->st.rx_batches++;
-    pc->st.rx_max_batch = std::max(pc->st.rx_max_batch, b.n);
-    pc->rready.push_back(idx);
-    pc->cv_rxr.notify_all();
-  }
+  j.pc = pc;
+  j.dir = kRx;
+  j.idx = idx;
+  j.slotted = !pc->gro;
+  j.trunc = trunc;
+  return true;
+}
+
+void rx_socket_finish(Job &j) {
+  sqobfs_pconn *pc = j.pc;
+  std::unique_lock<std::mutex> lk(pc->mu);
+  pc->st.rx_truncated += j.trunc;
+  rx_done(pc, j);
   task_end(pc, kRx, true);  // the socket may hold more: look again (EAGAIN re-arms)
+}
+
+bool task_prepare(Engine *E, const Task &t, Job &j) {
+  if (t.dir == kTx) return tx_prepare(t.pc, j);
+  if (t.pc->socket_mode()) return rx_socket_prepare(E, t.pc, j);
+  return rx_pump_prepare(t.pc, j);
+}
+
+void task_finish(Job &j) {
+  if (j.dir == kTx) tx_finish(j);
+  else if (j.pc->socket_mode()) rx_socket_finish(j);
+  else rx_pump_finish(j);
+}
+
+// A pconn whose batches may join another's launch: pump mode -- its tasks'
+// prepare and finish steps are queue operations, so one worker runs several
+// at no cost to the others -- and it leaves the routing to the engine
+// (cpu_max 0 or SQOBFS_PCONN_NEVER).  Socket-mode tasks are not gathered:
+// their steps are the recvmmsg / sendmmsg calls, which the workers must keep
+// making in parallel (measured, lat_bench hops over 8 socket pairs: gathering
+// them halved the unpaced rate, 9-10.7 -> 4.4-4.7 GiB/s, for no CPU saved).
+bool groupable(const sqobfs_pconn *pc) {
+  return !pc->socket_mode() && (pc->o.cpu_max == 0 || pc->o.cpu_max == SQOBFS_PCONN_NEVER);
+}
+
+// Takes off the run queue up to `max` queued tasks of direction dir of
+// groupable pconns of this kind whose batches (at most o.batch datagrams
+// each) fit in `room` datagrams; the calling worker runs them.
+uint32_t grab_tasks(Engine *E, int dir, int kind, uint32_t room, Task *out, uint32_t max) {
+  std::lock_guard<std::mutex> lk(E->mu);
+  uint32_t n = 0;
+  for (auto it = E->runq.begin(); it != E->runq.end() && n < max;) {
+    const sqobfs_pconn *pc = it->pc;
+    if (it->dir == dir && pc->kind == kind && groupable(pc) && pc->o.batch <= room) {
+      room -= pc->o.batch;
+      out[n++] = *it;
+      it = E->runq.erase(it);
+    } else {
+      ++it;
+    }
+  }
+  return n;
+}
+
+// One task.  When its batch launches, the batches other pconns have queued
+// for the same scheme and direction join the launch (up to group_max
+// batches, kGroupDgrams datagrams), and under load they are gathered even
+// when it would not launch alone: the launch goes ahead when, together, they
+// pass the load rule (more than kLoadMinDgrams datagrams whose CPU-path time
+// exceeds twice a launch's host cost).  So bulk traffic spread over several
+// pconns -- the hop conns of a port-hopping client, a server's conns on one
+// context -- in batches each too small to launch costs the host one launch
+// and one wait per group instead of the CPU path's bytes.  A batch that would
+// not have launched on its own rides along: the launch is paid for.  Under
+// load, a gathered group that does not pass runs on the CPU path here (its
+// tasks were queued behind busy workers anyway).
+void run_task(Engine *E, uint32_t w, const Task &t) {
+  Job jobs[kMaxGroup];
+  if (!task_prepare(E, t, jobs[0])) return;
+  bool bulk = false;
+  bool gpu = route_gpu(E, jobs[0], &bulk);
+  uint32_t nj = 1;
+  const uint32_t gmax = std::min(kMaxGroup, E->group_max.load(std::memory_order_relaxed));
+  const uint32_t n0 = jobs[0].batch().n;
+  const bool gather = gpu || (E->ctx && t.pc->o.cpu_max == 0 &&
+                              E->loaded.load(std::memory_order_relaxed) &&
+                              !E->gpu_off.load(std::memory_order_relaxed));
+  if (gather && gmax > 1 && groupable(t.pc) && n0 < kGroupDgrams) {
+    Task more[kMaxGroup];
+    const uint32_t m = grab_tasks(E, t.dir, t.pc->kind, kGroupDgrams - n0, more, gmax - 1);
+    bool any = false;
+    for (uint32_t k = 0; k < m; k++)
+      if (task_prepare(E, more[k], jobs[nj])) {
+        bool b2;
+        any = route_gpu(E, jobs[nj], &b2) || any;  // (and its cost, the engine's demand)
+        nj++;
+      }
+    if (!gpu && nj > 1) {
+      uint64_t n = 0, cost = 0;
+      for (uint32_t k = 0; k < nj; k++) {
+        n += jobs[k].batch().n;
+        cost += jobs[k].cost;
+      }
+      bulk = n > kLoadMinDgrams && cost * E->cpu_ns_kib.load(std::memory_order_relaxed) / 1024u >
+                                       2ull * E->gpu_host_ns.load(std::memory_order_relaxed);
+      gpu = bulk || any;
+    }
+  }
+  const int st = gpu ? gpu_run(E, w, jobs, nj, bulk || t.pc->o.spin_us == SQOBFS_PCONN_NEVER)
+                     : kRefused;
+  for (uint32_t k = 0; k < nj; k++) {
+    Job &j = jobs[k];
+    if (st == kRefused) {  // (refused: redone on the CPU)
+      j.failed = gpu;
+      j.cpu = true;
+      j.st = cpu_run(E, j);
+    } else {
+      j.failed = st != SQ_OK;
+      j.st = st;
+    }
+  }
+  for (uint32_t k = 0; k < nj; k++) task_finish(jobs[k]);
 }
 
 void worker_main(Engine *E, uint32_t w) {
@@ -1011,7 +1337,7 @@ void worker_main(Engine *E, uint32_t w) {
         }
       }
     }
-    if (E->runq.empty()) {
+    if (E->runq.empty() || g_hold.load(std::memory_order_relaxed)) {
       if (next) E->cv.wait_until(lk, mono_tp(next));
       else E->cv.wait(lk);
       continue;
@@ -1019,9 +1345,7 @@ void worker_main(Engine *E, uint32_t w) {
     const Task t = E->runq.front();
     E->runq.pop_front();
     lk.unlock();
-    if (t.dir == kTx) tx_task(E, w, t.pc);
-    else if (t.pc->socket_mode()) rx_socket_task(E, w, t.pc);
-    else rx_pump_task(E, w, t.pc);
+    run_task(E, w, t);
     lk.lock();
   }
 }
@@ -1052,6 +1376,7 @@ void engine_end(Engine *E) {
   const uint64_t one = 1;
   (void)!write(E->wake, &one, sizeof one);
   for (auto &t : E->threads) t.join();
+  for (auto &m : E->mkr) m.reset();  // (fenced on the streams: before they go)
   for (void *s : E->streams)
     if (s) sq_ctx_stream_destroy(E->ctx, s);
   for (auto &kv : E->free_blocks)
@@ -1071,6 +1396,7 @@ void sq_engine_ctx_closed(sqobfs_ctx *ctx) {
     std::lock_guard<std::mutex> g(g_eng_mu);
     g_workers_cfg.erase(ctx);
     g_affinity_cfg.erase(ctx);
+    g_group_cfg.erase(ctx);
     auto it = g_engines.find(ctx);
     if (it == g_engines.end()) return;
     E = it->second;
@@ -1106,6 +1432,10 @@ int sqobfs_engine_info_get(sqobfs_ctx *ctx, sqobfs_engine_info *out) {
   out->loaded = E->loaded.load() ? 1u : 0u;
   out->gpu_host_ns = E->gpu_host_ns.load();
   out->cpus = E->ncpus;
+  out->group_max = E->group_max.load();
+  out->launches = E->launches.load();
+  out->group_launches = E->group_launches.load();
+  out->group_batches = E->group_batches.load();
   return SQ_OK;
 }
 
@@ -1122,6 +1452,16 @@ int sqobfs_engine_set_affinity(sqobfs_ctx *ctx, int mode) {
   std::lock_guard<std::mutex> g(g_eng_mu);
   if (g_engines.count(ctx)) return SQ_EINVAL;
   g_affinity_cfg[ctx] = mode;
+  return SQ_OK;
+}
+
+int sqobfs_engine_set_group(sqobfs_ctx *ctx, uint32_t max_batches) {
+  if (max_batches > kMaxGroup) return SQ_EINVAL;
+  const uint32_t v = max_batches ? max_batches : kDefGroup;
+  std::lock_guard<std::mutex> g(g_eng_mu);
+  g_group_cfg[ctx] = v;
+  auto it = g_engines.find(ctx);
+  if (it != g_engines.end()) it->second->group_max.store(v);
   return SQ_OK;
 }
 
@@ -1154,6 +1494,17 @@ void sqobfs_debug_engine_fail(int count, int at_completion) {
 }
 
 void sqobfs_debug_pool_fail(int count) { g_pool_fail.store(count > 0 ? count : 0); }
+
+void sqobfs_debug_engine_hold(int on) {
+  g_hold.store(on != 0);
+  if (on) return;
+  std::lock_guard<std::mutex> g(g_eng_mu);
+  for (auto &kv : g_engines) {
+    Engine *E = kv.second;
+    { std::lock_guard<std::mutex> lk(E->mu); }  // (a worker between its check and its wait)
+    E->cv.notify_all();
+  }
+}
 
 // ---------------------------------------------------------------- pconn ABI
 

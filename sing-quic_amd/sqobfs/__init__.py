@@ -261,6 +261,9 @@ def load(path: str) -> ctypes.CDLL:
     L.sqobfs_engine_set_affinity.argtypes = [vp, i32]
     L.sqobfs_debug_device_pool.argtypes = [vp, ctypes.c_uint64]
     L.sqobfs_debug_device_pool.restype = ctypes.c_uint64
+    L.sqobfs_engine_set_group.argtypes = [vp, u32]
+    L.sqobfs_debug_engine_hold.argtypes = [i32]
+    L.sqobfs_debug_engine_hold.restype = None
     return L
 
 
@@ -424,7 +427,16 @@ class EngineInfo(ctypes.Structure):
                 ("gpu_disabled", ctypes.c_uint32), ("route_bytes", ctypes.c_uint64),
                 ("launch_us", ctypes.c_uint32), ("cpu_ns_per_kib", ctypes.c_uint32),
                 ("load_permille", ctypes.c_uint32), ("loaded", ctypes.c_uint32),
-                ("gpu_host_ns", ctypes.c_uint32), ("cpus", ctypes.c_uint32)]
+                ("gpu_host_ns", ctypes.c_uint32), ("cpus", ctypes.c_uint32),
+                ("group_max", ctypes.c_uint32), ("launches", ctypes.c_uint64),
+                ("group_launches", ctypes.c_uint64), ("group_batches", ctypes.c_uint64)]
+
+
+def engine_set_group(ctx: Context | None, max_batches: int) -> None:
+    """Most batches of several pconns one engine launch takes (0 = 8, 1 = no
+    coalescing; sqobfs_engine_set_group)."""
+    _check(lib().sqobfs_engine_set_group(ctx.handle if ctx else None, max_batches),
+           "sqobfs_engine_set_group")
 
 
 def engine_info(ctx: Context | None) -> EngineInfo:

@@ -27,6 +27,13 @@
  * per GiB of payload that arrived, and the batches each route took
  * ("CPU per GiB").
  *
+ * `lat_bench hops [K [seconds [reps]]]`: K pump-mode pconns on one context
+ * (a port-hopping client's conns over generic PacketConns; default options,
+ * a keyring per conn as the Go adapters make), K writers together offering
+ * 0.5, 1, 2 GiB/s and unpaced, K takers; the defaults (coalesced launches),
+ * coalescing off (sqobfs_engine_set_group 1) and every batch on the CPU
+ * path: CPU seconds per GiB, launches and batches per launch.
+ *
  * `lat_bench tput [runs]`: the default-routing GSO / GRO throughput run
  * (200,000 datagrams A -> B) repeated, each with its process CPU time,
  * involuntary context switches and the cgroup's CPU-quota throttling
@@ -511,7 +518,144 @@ static int tput_main(int runs, int pin) {
   return 0;
 }
 
+/* ---- hops: several pump-mode pconns on one context, coalesced launches */
+typedef struct {
+  sqobfs_pconn *pc;
+  double rate, secs, t0; /* datagrams per s (0: unpaced) */
+  long n, got;
+  double last_us;
+} Hop;
+
+static void *hop_writer(void *arg) {
+  Hop *h = arg;
+  static const uint8_t pay[L] = {9};
+  for (;;) {
+    for (int j = 0; j < 64; j++, h->n++) CHECK(sqobfs_pconn_write(h->pc, pay, L, NULL, 0));
+    const double now = now_us();
+    if (now - h->t0 >= h->secs * 1e6) break;
+    if (h->rate > 0) {
+      const double due = h->t0 + h->n / h->rate * 1e6;
+      if (due > now + 20) {
+        struct timespec ts = {0, (long)((due - now) * 1000)};
+        nanosleep(&ts, NULL);
+      }
+    }
+  }
+  return NULL;
+}
+
+/* the wrapped conn's side of pump mode: take each obfuscated batch (here:
+ * count it) and hand it back, until 300 ms pass without one */
+static void *hop_taker(void *arg) {
+  Hop *h = arg;
+  for (;;) {
+    sqobfs_pconn_tx v;
+    if (sqobfs_pconn_tx_take(h->pc, 300, &v) != SQ_OK) break;
+    h->got += v.count;
+    h->last_us = now_us();
+    CHECK(sqobfs_pconn_tx_done(h->pc));
+  }
+  return NULL;
+}
+
+/* K pump-mode pconns (the Go adapter over a generic PacketConn: a hop
+ * client's bufio.NewUnbindPacketConn, hysteria/client.go:184-186), each on a
+ * keyring of its own with the same PSK (as the adapters make one per conn),
+ * K writers together offering gib_s of payload (0: unpaced) for secs
+ * seconds, K takers.  cpu_max: the conns' option (0: the default routing). */
+static void hops_run(sqobfs_ctx *c, const char *name, int K, uint32_t group, uint32_t cpu_max,
+                     double gib_s, double secs) {
+  enum { KMAX = 32 };
+  CHECK(sqobfs_engine_set_group(c, group));
+  Hop h[KMAX];
+  sqobfs_keyring *kr[KMAX];
+  pthread_t tw[KMAX], tt[KMAX];
+  uint64_t o0 = 0;
+  uint32_t l0 = PL;
+  for (int k = 0; k < K; k++) {
+    CHECK(sqobfs_keyring_create(c, SQOBFS_SALAMANDER, 1, PSK, &o0, &l0, &kr[k]));
+    sqobfs_pconn_opts o;
+    memset(&o, 0, sizeof o);
+    o.cpu_max = cpu_max;
+    memset(&h[k], 0, sizeof h[k]);
+    CHECK(sqobfs_pconn_open(c, kr[k], -1, &o, &h[k].pc));
+    h[k].rate = gib_s > 0 ? gib_s * (double)(1 << 30) / L / K : 0;
+    h[k].secs = secs;
+  }
+  sqobfs_engine_info e0, e1;
+  CHECK(sqobfs_engine_info_get(c, &e0));
+  const double c0 = cpu_s(), t0 = now_us();
+  for (int k = 0; k < K; k++) {
+    h[k].t0 = t0;
+    pthread_create(&tt[k], NULL, hop_taker, &h[k]);
+    pthread_create(&tw[k], NULL, hop_writer, &h[k]);
+  }
+  long sent = 0, got = 0;
+  double last = t0;
+  for (int k = 0; k < K; k++) {
+    pthread_join(tw[k], NULL);
+    pthread_join(tt[k], NULL);
+    sent += h[k].n;
+    got += h[k].got;
+    if (h[k].last_us > last) last = h[k].last_us;
+  }
+  const double c1 = cpu_s();
+  CHECK(sqobfs_engine_info_get(c, &e1));
+  unsigned long long bt = 0, bc = 0;
+  uint32_t maxb = 0;
+  for (int k = 0; k < K; k++) {
+    sqobfs_pconn_stats s;
+    CHECK(sqobfs_pconn_stats_get(h[k].pc, &s));
+    bt += s.tx_batches;
+    bc += s.cpu_batches;
+    if (s.tx_max_batch > maxb) maxb = s.tx_max_batch;
+  }
+  const double dt = (last - t0) * 1e-6, gib = got * (double)L / (1 << 30);
+  const unsigned long long nl = e1.launches - e0.launches;
+  const unsigned long long gl = e1.group_launches - e0.group_launches;
+  const unsigned long long gb = e1.group_batches - e0.group_batches;
+  printf("{\"mode\": \"%s\", \"conns\": %d, \"group\": %u, \"offered_gib_s\": %.3f, "
+         "\"sent\": %ld, \"taken\": %ld, \"seconds\": %.3f, \"payload_gib_s\": %.3f, "
+         "\"cpu_seconds\": %.3f, \"cpu_s_per_gib\": %.3f, \"batches\": %llu, "
+         "\"max_batch\": %u, \"cpu_batches\": %llu, \"launches\": %llu, "
+         "\"coalesced_launches\": %llu, \"coalesced_batches\": %llu, "
+         "\"batches_per_launch\": %.2f, \"loaded\": %u, \"gpu_host_ns\": %u, "
+         "\"cpu_ns_per_kib\": %u}",
+         name, K, e1.group_max, gib_s, sent, got, dt, gib / dt, c1 - c0, (c1 - c0) / gib, bt,
+         maxb, bc, nl, gl, gb, nl ? (double)(bt - bc) / nl : 0.0, e1.loaded, e1.gpu_host_ns,
+         e1.cpu_ns_per_kib);
+  fflush(stdout);
+  for (int k = 0; k < K; k++) {
+    sqobfs_pconn_close(h[k].pc);
+    sqobfs_keyring_destroy(kr[k]);
+  }
+}
+
+static int hops_main(int K, double secs, int reps) {
+  if (K < 1 || K > 32) K = 8;
+  sqobfs_ctx *ctx;
+  CHECK(sqobfs_open(0, &ctx));
+  static const double rates[] = {0.5, 1.0, 2.0, 0};
+  printf("{\"hops\": [");
+  int first = 1;
+  for (int ri = 0; ri < 4; ri++)
+    for (int rp = 0; rp < reps; rp++)
+      for (int m = 0; m < 3; m++) {
+        if (!first) printf(", ");
+        first = 0;
+        /* the defaults; coalescing off; every batch on the CPU path */
+        static const char *const names[] = {"default", "group_off", "cpu_only"};
+        hops_run(ctx, names[m], K, m == 1 ? 1u : 0u, m == 2 ? 1u << 30 : 0u, rates[ri], secs);
+      }
+  printf("]}\n");
+  sqobfs_close(ctx);
+  return 0;
+}
+
 int main(int argc, char **argv) {
+  if (argc > 1 && !strcmp(argv[1], "hops"))
+    return hops_main(argc > 2 ? atoi(argv[2]) : 8, argc > 3 ? atof(argv[3]) : 1.5,
+                     argc > 4 ? atoi(argv[4]) : 1);
   if (argc > 1 && !strcmp(argv[1], "load"))
     return load_main(argc > 2 ? atof(argv[2]) : 1.5, argc > 3 ? atoi(argv[3]) : 1);
   if (argc > 1 && !strcmp(argv[1], "tput"))

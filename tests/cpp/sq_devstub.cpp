@@ -111,6 +111,23 @@ const sq::PskEntry *sq_keyring_host(const sqobfs_keyring *kr, uint32_t *count) {
   return kr->host.data();
 }
 sqobfs_ctx *sq_keyring_ctx(const sqobfs_keyring *kr) { return kr->ctx; }
+void sq_keyring_hot(const sqobfs_keyring *, uint32_t *hot_m, uint32_t *hot_iv) {
+  *hot_m = 16;
+  *hot_iv = 0;
+}
+int sq_keyring_from_entries(sqobfs_ctx *ctx, int kind, const sq::PskEntry *e, uint32_t count,
+                            uint32_t, uint32_t, sqobfs_keyring **out) {
+  *out = nullptr;
+  if (!ctx || !e || !count) return SQ_EINVAL;
+  sqobfs_keyring *kr = new (std::nothrow) sqobfs_keyring();
+  if (!kr) return SQ_ENOMEM;
+  kr->ctx = ctx;
+  kr->kind = kind;
+  kr->count = count;
+  kr->host.assign(e, e + count);
+  *out = kr;
+  return SQ_OK;
+}
 void sq_salt_take(sqobfs_ctx *ctx, uint32_t key[8], uint64_t *seq) {
   if (!ctx) return sq_host_salt_take(key, seq);
   memcpy(key, ctx->key, sizeof ctx->key);
