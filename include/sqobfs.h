@@ -784,9 +784,8 @@ int sqobfs_engine_set_affinity(sqobfs_ctx *ctx, int mode);
  * 0 or SQOBFS_PCONN_NEVER), the batches other such pconns of the same scheme
  * have queued in the same direction join that launch -- at most max_batches
  * of them (0 = 8; 1 = every batch its own launch) and 16,384 datagrams -- so
- * one kernel, one wait and one launch's host cost carry them all; under load
- * (sqobfs_engine_info.loaded) they are gathered even when none would launch
- * alone, and launch when together they pass the load rule (cpu_max).  Their
+ * one kernel, one wait and one launch's host cost carry them all (batches
+ * are not gathered to make a launch none of them would make alone).  Their
  * PSKs may differ: the launch then reads per-datagram PSK ids into a keyring
  * the engine merges from the pconns' keyrings.  Socket-mode pconns are not
  * gathered (their batches' steps are socket calls that the workers keep

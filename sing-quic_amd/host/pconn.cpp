@@ -1259,47 +1259,31 @@ uint32_t grab_tasks(Engine *E, int dir, int kind, uint32_t room, Task *out, uint
 
 // One task.  When its batch launches, the batches other pconns have queued
 // for the same scheme and direction join the launch (up to group_max
-// batches, kGroupDgrams datagrams), and under load they are gathered even
-// when it would not launch alone: the launch goes ahead when, together, they
-// pass the load rule (more than kLoadMinDgrams datagrams whose CPU-path time
-// exceeds twice a launch's host cost).  So bulk traffic spread over several
-// pconns -- the hop conns of a port-hopping client, a server's conns on one
-// context -- in batches each too small to launch costs the host one launch
-// and one wait per group instead of the CPU path's bytes.  A batch that would
-// not have launched on its own rides along: the launch is paid for.  Under
-// load, a gathered group that does not pass runs on the CPU path here (its
-// tasks were queued behind busy workers anyway).
+// batches, kGroupDgrams datagrams): bulk traffic over several pconns -- the
+// hop conns of a port-hopping client, a server's conns on one context --
+// costs one launch and one wait per group (measured, lat_bench hops, 8 pump
+// conns unpaced: ~4 batches per launch, a quarter of the launches).  A batch
+// that would not have launched on its own rides along: the launch is paid
+// for.  Batches are not gathered to make a launch that none of them would
+// make alone: gathered groups of small batches under paced load launched
+// 4-13K times in 3 s for no CPU saved ("Coalesced launches").
 void run_task(Engine *E, uint32_t w, const Task &t) {
   Job jobs[kMaxGroup];
   if (!task_prepare(E, t, jobs[0])) return;
   bool bulk = false;
-  bool gpu = route_gpu(E, jobs[0], &bulk);
+  const bool gpu = route_gpu(E, jobs[0], &bulk);
   uint32_t nj = 1;
   const uint32_t gmax = std::min(kMaxGroup, E->group_max.load(std::memory_order_relaxed));
   const uint32_t n0 = jobs[0].batch().n;
-  const bool gather = gpu || (E->ctx && t.pc->o.cpu_max == 0 &&
-                              E->loaded.load(std::memory_order_relaxed) &&
-                              !E->gpu_off.load(std::memory_order_relaxed));
-  if (gather && gmax > 1 && groupable(t.pc) && n0 < kGroupDgrams) {
+  if (gpu && gmax > 1 && groupable(t.pc) && n0 < kGroupDgrams) {
     Task more[kMaxGroup];
     const uint32_t m = grab_tasks(E, t.dir, t.pc->kind, kGroupDgrams - n0, more, gmax - 1);
-    bool any = false;
     for (uint32_t k = 0; k < m; k++)
       if (task_prepare(E, more[k], jobs[nj])) {
         bool b2;
-        any = route_gpu(E, jobs[nj], &b2) || any;  // (and its cost, the engine's demand)
+        (void)route_gpu(E, jobs[nj], &b2);  // (its cost, and the engine's demand)
         nj++;
       }
-    if (!gpu && nj > 1) {
-      uint64_t n = 0, cost = 0;
-      for (uint32_t k = 0; k < nj; k++) {
-        n += jobs[k].batch().n;
-        cost += jobs[k].cost;
-      }
-      bulk = n > kLoadMinDgrams && cost * E->cpu_ns_kib.load(std::memory_order_relaxed) / 1024u >
-                                       2ull * E->gpu_host_ns.load(std::memory_order_relaxed);
-      gpu = bulk || any;
-    }
   }
   const int st = gpu ? gpu_run(E, w, jobs, nj, bulk || t.pc->o.spin_us == SQOBFS_PCONN_NEVER)
                      : kRefused;
