@@ -52,6 +52,29 @@ int main(void){printf("%zu %zu %zu %zu %zu\n", sizeof(sqobfs_batch),
                    B.in_cap.offset]
 
 
+def test_engine_info_layout_matches_header():
+    """ctypes mirror of sqobfs_engine_info has the C layout (round 5 grew it:
+    load routing, affinity and the coalesced-launch counters)."""
+    fields = ["pool_bytes", "route_bytes", "cpus", "group_max", "launches", "group_launches",
+              "group_batches"]
+    prog = ('#include <stdio.h>\n#include <stddef.h>\n#include "sqobfs.h"\n'
+            'int main(void){printf("%zu' + ' %zu' * len(fields) + '\\n", sizeof(sqobfs_engine_info)'
+            + "".join(f", offsetof(sqobfs_engine_info,{f})" for f in fields) + ");return 0;}")
+    exe = "/tmp/sq_engine_info_probe"
+    subprocess.run(["gcc", "-x", "c", "-", "-I", os.path.join(REPO, "include"), "-o", exe],
+                   input=prog, text=True, check=True)
+    got = [int(x) for x in subprocess.run([exe], capture_output=True, text=True).stdout.split()]
+    E = sqobfs.EngineInfo
+    assert got == [ctypes.sizeof(E)] + [getattr(E, f).offset for f in fields]
+
+
+def test_engine_set_group_bounds():
+    """sqobfs_engine_set_group (host logic): 0..64 batches per launch."""
+    L = sqobfs.lib()
+    assert L.sqobfs_engine_set_group(None, 65) == sqobfs.SQ_EINVAL
+    sqobfs.engine_set_group(None, 0)  # (the host engine: no launches to coalesce)
+
+
 def test_abi_version_and_strerror():
     L = sqobfs.lib()
     assert L.sqobfs_abi_version() == 5
