@@ -30,7 +30,11 @@ def main():
     cfg = sys.argv[1] if len(sys.argv) > 1 else "salamander-1m"
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    kind, n, L, n_psk = bench.CONFIGS[cfg]
+    if cfg.startswith("const:"):  # const:N:L -- N Salamander packets of L bytes
+        _, n_s, l_s = cfg.split(":")
+        kind, n, L, n_psk = 0, int(n_s), int(l_s), 1
+    else:
+        kind, n, L, n_psk = bench.CONFIGS[cfg]
     sh = bench.build_shard(torch, dev, kind, n, L, n_psk, 0, 1, cfg, "dense", 0)
     ctx = sqobfs.Context(0)
     kr = sqobfs.Keyring(ctx, kind, sh["psks"])
