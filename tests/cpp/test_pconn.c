@@ -1080,8 +1080,10 @@ static long ref_read_psk(int kind, const uint8_t *psk, size_t pl, const uint8_t 
  * (per-datagram PSK ids into the engine's merged keyring), and every
  * datagram is the reference's WriteTo / ReadFrom under its own conn's PSK.
  * Then with coalescing off (group 1) the same traffic takes a launch per
- * batch. */
-static void t_group(int kind) {
+ * batch.  short_psks: the fifth conn's PSK is 12 B instead of 130, so every
+ * PSK of the merged keyring fits the first compressed block (the multi-PSK
+ * kernels then skip loading the chaining values: hot_iv). */
+static void t_group(int kind, int short_psks) {
   enum { K = 6, N = 40 };
   const int S = salt_len(kind);
   sqobfs_ctx *ctx = NULL;
@@ -1092,7 +1094,7 @@ static void t_group(int kind) {
   for (int i = 0; i < 130; i++) long_psk[i] = (uint8_t)(i * 29 + 3);
   static const uint8_t psk_b[] = "hop-b";
   const uint8_t *psk[K] = {PSK, PSK, PSK, psk_b, long_psk, NULL};
-  const uint32_t pl[K] = {PL, PL, PL, 5, 130, 0};
+  const uint32_t pl[K] = {PL, PL, PL, 5, short_psks ? 12u : 130u, 0};
   sqobfs_keyring *kr[K];
   for (int k = 0; k < K; k++) {
     if (k == 1 || k == 2) {
@@ -1185,9 +1187,9 @@ static void t_group(int kind) {
       EXPECT(gl == 0 && nl == 2 * K && i1.group_max == 1,
              "group off kind %d: %llu launches, %llu coalesced", kind, (unsigned long long)nl,
              (unsigned long long)gl);
-    printf("  group kind %d (%s): %d conns x %d datagrams each way (4 PSKs) in %llu launches, "
-           "wire == reference WriteTo / ReadFrom\n", kind, round ? "off" : "on", K, N,
-           (unsigned long long)nl);
+    printf("  group kind %d (%s, PSKs of %u/5/%u/0 B): %d conns x %d datagrams each way in %llu "
+           "launches, wire == reference WriteTo / ReadFrom\n", kind, round ? "off" : "on",
+           (unsigned)PL, pl[4], K, N, (unsigned long long)nl);
   }
   for (int k = 0; k < K; k++) sqobfs_pconn_close(pc[k]);
   for (int k = 0; k < K; k++)
@@ -1297,8 +1299,10 @@ int main(int argc, char **argv) {
   if (!g_nodev) {
     t_routing();
     t_load();
-    t_group(SQOBFS_SALAMANDER);
-    t_group(SQOBFS_XPLUS);
+    t_group(SQOBFS_SALAMANDER, 0);
+    t_group(SQOBFS_XPLUS, 0);
+    t_group(SQOBFS_SALAMANDER, 1);
+    t_group(SQOBFS_XPLUS, 1);
     t_fail(0);
     t_fail(1);
   }
