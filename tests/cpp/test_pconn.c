@@ -36,7 +36,8 @@
  *   group     coalesced launches: the queued batches of six pconns with four
  *             PSKs go out in one launch per direction, every datagram the
  *             reference's under its own conn's PSK; with coalescing off, one
- *             launch per batch
+ *             launch per batch; and eight conns with writer, taker, pusher
+ *             and reader threads on four workers (stress)
  *   poolfail  a receive batch block that cannot be allocated (with nothing
  *             unread to restart the socket task) is retried: the datagram
  *             still reads, within its deadline
@@ -1199,6 +1200,131 @@ static void t_group(int kind, int short_psks) {
   sqobfs_close(ctx);
 }
 
+/* Coalesced launches under concurrency: eight pump pconns (three PSKs, a
+ * keyring each, as the Go adapters make them) on the default four workers,
+ * each with a writer, a taker, a pusher and a reader thread; every batch
+ * launches (cpu_max NEVER), so the workers grab each other's queued tasks
+ * while all of them run.  Every datagram taken or read is the reference's
+ * under its conn's PSK, none is lost.  (Under TSan: the grab against the
+ * tasks' own scheduling.) */
+enum { GS_K = 8, GS_N = 1500 };
+static const uint8_t *gs_psk(int k, uint32_t *len) {
+  static const uint8_t a[] = "hop-alpha", b[] = "a-longer-hop-psk-for-the-second-keyring-0123";
+  switch (k % 3) {
+    case 0: *len = PL; return PSK;
+    case 1: *len = sizeof a - 1; return a;
+    default: *len = sizeof b - 1; return b;
+  }
+}
+static uint32_t gs_pay(int k, int i, uint8_t *p) {
+  const uint32_t L = 1 + (uint32_t)(k * 131 + i * 37) % 1300;
+  for (uint32_t j = 0; j < L; j++) p[j] = (uint8_t)(k * 7 + i * 13 + (int)j);
+  return L;
+}
+typedef struct {
+  sqobfs_pconn *pc;
+  int kind, k, got, bad;
+} GsArg;
+static void *gs_writer(void *arg) {
+  GsArg *g = arg;
+  uint8_t p[1400];
+  for (int i = 0; i < GS_N; i++) {
+    const uint32_t L = gs_pay(g->k, i, p);
+    CHECK(sqobfs_pconn_write(g->pc, p, L, NULL, (uint64_t)i));
+  }
+  return NULL;
+}
+static void *gs_taker(void *arg) {
+  GsArg *g = arg;
+  uint32_t pl;
+  const uint8_t *psk = gs_psk(g->k, &pl);
+  while (g->got < GS_N) {
+    sqobfs_pconn_tx v;
+    const int st = sqobfs_pconn_tx_take(g->pc, 5000, &v);
+    if (st != SQ_OK) break;
+    for (uint32_t i = 0; i < v.count; i++, g->got++) {
+      uint8_t p[1400], ref[MAXW];
+      const uint32_t L = gs_pay(g->k, (int)v.tag[i], p);
+      const uint8_t *w = v.base + v.off[i];
+      ref_write_psk(g->kind, psk, pl, w, p, L, ref);
+      if (v.len[i] != L + (uint32_t)salt_len(g->kind) || memcmp(ref, w, v.len[i])) g->bad++;
+    }
+    CHECK(sqobfs_pconn_tx_done(g->pc));
+  }
+  return NULL;
+}
+static void *gs_pusher(void *arg) {
+  GsArg *g = arg;
+  uint32_t pl;
+  const uint8_t *psk = gs_psk(g->k, &pl);
+  for (int i = 0; i < GS_N; i++) {
+    uint8_t p[1400], salt[16], w[MAXW];
+    const uint32_t L = gs_pay(g->k, i, p);
+    for (int b = 0; b < 16; b++) salt[b] = (uint8_t)(i * 31 + b + g->k);
+    ref_write_psk(g->kind, psk, pl, salt, p, L, w);
+    CHECK(sqobfs_pconn_rx_push(g->pc, w, L + (uint32_t)salt_len(g->kind), NULL, (uint64_t)i));
+  }
+  return NULL;
+}
+static void *gs_reader(void *arg) {
+  GsArg *g = arg;
+  for (; g->got < GS_N; g->got++) {
+    uint8_t got[MAXW], p[1400];
+    uint32_t n;
+    uint64_t tag;
+    const int st = sqobfs_pconn_read(g->pc, got, MAXW, &n, NULL, &tag);
+    if (st != SQ_OK) break;
+    const uint32_t L = gs_pay(g->k, (int)tag, p);
+    if (n != L || memcmp(got, p, L) || tag != (uint64_t)g->got) g->bad++;
+  }
+  return NULL;
+}
+static void t_group_stress(int kind) {
+  sqobfs_ctx *ctx = NULL;
+  CHECK(sqobfs_open(0, &ctx));
+  const int64_t a0 = sqobfs_debug_host_allocs();
+  sqobfs_keyring *kr[GS_K];
+  sqobfs_pconn *pc[GS_K];
+  sqobfs_pconn_opts o;
+  memset(&o, 0, sizeof o);
+  o.cpu_max = SQOBFS_PCONN_NEVER;
+  o.batch = 64;
+  for (int k = 0; k < GS_K; k++) {
+    uint64_t off = 0;
+    uint32_t len;
+    const uint8_t *psk = gs_psk(k, &len);
+    CHECK(sqobfs_keyring_create(ctx, kind, 1, psk, &off, &len, &kr[k]));
+    CHECK(sqobfs_pconn_open(ctx, kr[k], -1, &o, &pc[k]));
+  }
+  GsArg ga[4][GS_K];
+  pthread_t th[4][GS_K];
+  void *(*fn[4])(void *) = {gs_writer, gs_taker, gs_pusher, gs_reader};
+  for (int r = 0; r < 4; r++)
+    for (int k = 0; k < GS_K; k++) {
+      ga[r][k] = (GsArg){pc[k], kind, k, 0, 0};
+      pthread_create(&th[r][k], NULL, fn[r], &ga[r][k]);
+    }
+  for (int r = 0; r < 4; r++)
+    for (int k = 0; k < GS_K; k++) pthread_join(th[r][k], NULL);
+  sqobfs_engine_info ei;
+  CHECK(sqobfs_engine_info_get(ctx, &ei));
+  for (int k = 0; k < GS_K; k++) {
+    EXPECT(ga[1][k].got == GS_N && ga[1][k].bad == 0, "group stress kind %d conn %d: taken %d, %d "
+           "differ", kind, k, ga[1][k].got, ga[1][k].bad);
+    EXPECT(ga[3][k].got == GS_N && ga[3][k].bad == 0, "group stress kind %d conn %d: read %d, %d "
+           "differ", kind, k, ga[3][k].got, ga[3][k].bad);
+    sqobfs_pconn_close(pc[k]);
+    sqobfs_keyring_destroy(kr[k]);
+  }
+  printf("  group stress kind %d: %d conns x %d datagrams each way on 4 workers == reference; "
+         "%llu launches, %llu coalesced (%llu batches)\n", kind, GS_K, GS_N,
+         (unsigned long long)ei.launches, (unsigned long long)ei.group_launches,
+         (unsigned long long)ei.group_batches);
+  sqobfs_engine_trim(ctx);
+  EXPECT(sqobfs_debug_host_allocs() == a0, "group stress: host allocs");
+  sqobfs_close(ctx);
+}
+
 static void t_fail(int at_completion) {
   sqobfs_ctx *ctx = NULL;
   CHECK(sqobfs_open(0, &ctx));
@@ -1303,6 +1429,8 @@ int main(int argc, char **argv) {
     t_group(SQOBFS_XPLUS, 0);
     t_group(SQOBFS_SALAMANDER, 1);
     t_group(SQOBFS_XPLUS, 1);
+    t_group_stress(SQOBFS_SALAMANDER);
+    t_group_stress(SQOBFS_XPLUS);
     t_fail(0);
     t_fail(1);
   }
