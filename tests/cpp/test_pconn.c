@@ -1268,6 +1268,8 @@ static void *gs_pusher(void *arg) {
 }
 static void *gs_reader(void *arg) {
   GsArg *g = arg;
+  /* (a lost datagram fails the count, within the deadline, not by a hang) */
+  CHECK(sqobfs_pconn_set_deadline(g->pc, SQOBFS_PCONN_READ, unix_ns() + 120 * 1000000000ll));
   for (; g->got < GS_N; g->got++) {
     uint8_t got[MAXW], p[1400];
     uint32_t n;
