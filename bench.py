@@ -108,7 +108,11 @@ def parse():
                          "run_host, a mapped launch, the UDP endpoint and the packet conn "
                          "engine at batches of 1/16/64/256, and the engine's loopback rate")
     ap.add_argument("--e2e", action="store_true",
-                    help="also time the host-staged path (pinned H2D + kernel + D2H)")
+                    help="also time every mode of the host-staged path on rank 0 (pageable, "
+                         "pinned, OUT_UNINIT, 2,048-B slots: e2e.modes)")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the all-ranks host-staged batch after the timed region "
+                         "(e2e.aggregate_gib_s / e2e.per_rank)")
     return ap.parse_args()
 
 
@@ -904,8 +908,13 @@ def main():
         out["roofline"]["traffic_source"] = pmc.get("source")
     if args.latency and rank == 0:
         out["latency"] = latency_bench()
+    if not args.no_e2e:
+        # every rank at once, behind a barrier, after the timed region (not in
+        # `value`): the host-staged rate of the whole job
+        out["e2e"] = e2e_all_ranks(torch, sqobfs, ctx, kr, kind, dist, tdev, world)
     if args.e2e and rank == 0:
-        out["e2e"] = e2e_rate(torch, sqobfs, ctx, kr, kind, min(n, 1 << 18), L or 758)
+        out.setdefault("e2e", {})["modes"] = e2e_rate(torch, sqobfs, ctx, kr, kind,
+                                                      min(n, 1 << 18), L or 758)
     if args.quic and rank == 0:
         out["quic"] = {
             "chacha20_poly1305": quic_rate(torch, sqobfs, ctx, dev, max(5, args.steps), suite=0),
@@ -944,6 +953,60 @@ def latency_bench():
     if r.returncode != 0:
         return {"error": r.stderr[-500:]}
     return json.loads(r.stdout)
+
+
+def e2e_all_ranks(torch, sqobfs, ctx, kr, kind, dist, tdev, world, n=1 << 18, L=1350, reps=3):
+    """The host-staged batch on every rank at once: each
+    rank runs sqobfs_run_host -- chunked H2D | kernel | D2H on its own GPU and
+    PCIe link -- over n x L page-locked caller slots with
+    SQOBFS_FLAG_OUT_UNINIT, `reps` times, all ranks released by one barrier.
+    aggregate_gib_s = the payload of every rank / the max-over-ranks wall
+    time; per_rank = each rank's own rate.  Bounded (~0.4 GB per rank).
+    One packet per rank is checked against the device path's contract (its
+    out_len); the bytes' parity is tests/test_gpu_*'s."""
+    import numpy as np
+    S = 8 if kind == 0 else 16
+    rng = np.random.Generator(np.random.PCG64(11 + (dist.get_rank() if dist else 0)))
+    nin, nout = n * slot(L), n * slot(L + S)
+    pd, po = sqobfs.PinnedArray(ctx, nin), sqobfs.PinnedArray(ctx, nout)
+    try:
+        pd.array[:] = np.frombuffer(rng.bytes(nin), np.uint8)
+        in_off = np.arange(n, dtype=np.uint64) * slot(L)
+        out_off = np.arange(n, dtype=np.uint64) * slot(L + S)
+        salt = np.frombuffer(rng.bytes(n * S), np.uint8).copy()
+        out_len = np.zeros(n, np.uint32)
+        hb = sqobfs.HostBatch(pd.array, in_off, np.full(n, L, np.uint32), po.array, out_off,
+                              out_len, salt, flags=sqobfs.FLAG_OUT_UNINIT)
+        b = hb.as_batch()
+        sqobfs.run_host(ctx, kr, sqobfs.OBFUSCATE, b)  # (warm: staging buffers, clocks)
+        ok = bool(hb.out_len[0] == L + S and hb.out_len[-1] == L + S)
+        if dist:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            sqobfs.run_host(ctx, kr, sqobfs.OBFUSCATE, b)
+        dt = time.perf_counter() - t0
+    finally:
+        pd.free()
+        po.free()
+    own = n * L * reps / dt / 2**30
+    if dist:
+        t = torch.tensor([own, dt, 1.0 if ok else 0.0], dtype=torch.float64, device=tdev)
+        g = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(g, t)
+        rates = [float(x[0]) for x in g]
+        wall = max(float(x[1]) for x in g)
+        ok = all(float(x[2]) > 0 for x in g)
+    else:
+        rates, wall = [own], dt
+    return {"aggregate_gib_s": round(n * L * reps * world / wall / 2**30, 3),
+            "per_rank": [round(r, 3) for r in rates],
+            "wall_s": round(wall, 5), "packets_per_rank": n, "payload_bytes": L, "reps": reps,
+            "out_len_ok": ok,
+            "rule": "sum over ranks of n x L x reps / max-over-ranks wall; all ranks released "
+                    "by one barrier after the timed region (not part of `value`)",
+            "path": "sqobfs_run_host, page-locked caller slots, SQOBFS_FLAG_OUT_UNINIT, "
+                    "host salts"}
 
 
 def e2e_rate(torch, sqobfs, ctx, kr, kind, n, L):

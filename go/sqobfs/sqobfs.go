@@ -144,7 +144,7 @@ func (x *Context) SetEngineAffinity(l3 bool) error {
 // SetEngineGroup bounds the coalesced launches of the context's engine
 // (sqobfs_engine_set_group): the queued batches of Conns over generic
 // PacketConns -- a hop client's conns -- join one launch, at most maxBatches
-// of them (0 = 8, 1 = every batch its own launch).  Any time.
+// of them (0 = 32, 1 = every batch its own launch).  Any time.
 func (x *Context) SetEngineGroup(maxBatches int) error {
 	x.mu.Lock()
 	defer x.mu.Unlock()

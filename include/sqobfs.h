@@ -64,7 +64,7 @@
 extern "C" {
 #endif
 
-#define SQOBFS_ABI_VERSION 5
+#define SQOBFS_ABI_VERSION 6
 
 #define SQOBFS_SALAMANDER_SALT_LEN 8 /* hysteria2/salamander.go:15 */
 #define SQOBFS_XPLUS_SALT_LEN 16     /* hysteria/xplus.go:17 */
@@ -607,17 +607,23 @@ typedef struct sqobfs_pconn_opts {
   uint32_t slot_bytes; /* per-datagram slot, multiple of 16 (0 = 2048, hop.go:19);
                           longer received datagrams are cut to it, as a
                           ReadFrom into a buffer of that size cuts them */
-  uint32_t tx_batches; /* transmit batches (0 = 3) */
-  uint32_t rx_batches; /* receive batches (0 = 3) */
+  uint32_t tx_batches; /* transmit batches (0 = 8: while a launch flies, the
+                          writers fill the next ones, and they all join the
+                          following launch; a batch holds a pool block only
+                          while it fills, flies or waits to be taken) */
+  uint32_t rx_batches; /* receive batches (0 = 8; a block only while a batch
+                          fills, flies or holds unread datagrams) */
   uint32_t linger_us;  /* an idle worker waits this long for a partly filled
                           batch to grow (0: launch at once) */
   uint32_t spin_us;    /* a worker polls a launch at most this long before it
                           blocks (0 = 200); the engine polls about twice the
                           launches' recent completion time, within that bound;
-                          SQOBFS_PCONN_NEVER = never poll: sleep through most
-                          of the kernel's expected time, then poll with short
-                          sleeps (the core is free while the kernel runs, at
-                          ~50 us more latency) */
+                          SQOBFS_PCONN_NEVER = never poll: the engine's
+                          completer thread sleeps through most of the
+                          kernel's expected time, then polls with short
+                          sleeps, and the worker goes on with other batches
+                          meanwhile (no core is held while the kernel runs,
+                          at ~50 us more latency) */
   uint32_t flags;      /* socket mode: SQOBFS_UDP_TX_GSO (runs of equal-length
                           datagrams to one address go out as UDP_SEGMENT
                           messages; off by itself if the socket refuses) |
@@ -657,8 +663,13 @@ typedef struct sqobfs_pconn_stats {
   uint32_t tx_max_batch, rx_max_batch;
   uint64_t cpu_batches;   /* batches (tx + rx) transformed on the CPU path */
   uint64_t inline_writes; /* datagrams sent on the writer's thread (inline_gap_us) */
-  uint64_t gpu_failures;  /* launches that failed; the engine then stays on the CPU */
+  uint64_t gpu_failures;  /* batches whose launch failed (the device); the engine
+                             then stays on the CPU path */
   uint64_t dropped;       /* datagrams lost with a launch that failed after it started */
+  uint64_t gpu_refused;   /* batches whose launch was refused for the moment (no
+                             memory for a stream, a descriptor block or a merged
+                             keyring): redone on the CPU path, the GPU stays on
+                             (ABI 6) */
 } sqobfs_pconn_stats;
 
 /* kr's kind picks Salamander or XPlus.  ctx and kr must outlive the pconn.
@@ -726,9 +737,13 @@ int sqobfs_pconn_stats_get(const sqobfs_pconn *pc, sqobfs_pconn_stats *out);
 int64_t sqobfs_debug_host_allocs(void);
 
 /* The engine.  Every pconn of a context (ctx NULL: of the process's host
- * engine) is served by ONE engine: a fixed pool of worker threads (each with
- * its own HIP stream) that obfuscate / de-obfuscate and move the batches of
- * all its pconns, one poller thread that watches their sockets (epoll), and a
+ * engine) is served by ONE engine: a fixed pool of worker threads that
+ * obfuscate / de-obfuscate and move the batches of all its pconns, one poller
+ * thread that watches their sockets (epoll), with a context one completer
+ * thread that waits for the launches that do not poll (bulk batches; spin_us
+ * SQOBFS_PCONN_NEVER) and finishes their batches, so the launching worker is
+ * free at once (launches in flight: at most 32, each on a HIP stream of the
+ * engine's), and a
  * pool of batch blocks (page-locked and GPU-mapped with a context) that
  * pconns take while they fill, transmit or hold unread datagrams and give
  * back when done.  So opening more pconns -- a port-hopping client re-dials
@@ -736,7 +751,8 @@ int64_t sqobfs_debug_host_allocs(void);
  * datagrams in flight, not the number of pconns. */
 typedef struct sqobfs_engine_info {
   uint32_t pconns;       /* open pconns */
-  uint32_t threads;      /* engine threads (workers + poller) */
+  uint32_t threads;      /* engine threads (workers + poller, + completer with a
+                            context) */
   uint32_t workers;
   uint32_t pool_blocks;  /* batch blocks allocated (in use + free) */
   uint64_t pool_bytes;
@@ -761,6 +777,10 @@ typedef struct sqobfs_engine_info {
   uint64_t launches;       /* kernel launches of the engine */
   uint64_t group_launches; /* ... that carried the batches of several pconns */
   uint64_t group_batches;  /* batches carried by those */
+  uint64_t async_launches; /* launches completed by the completer thread (ABI 6) */
+  uint32_t streams;        /* launch streams made: the most launches that were in
+                              flight at once (at most 32) */
+  uint32_t reserved;
 } sqobfs_engine_info;
 /* ctx NULL: the host engine.  SQ_OK with zeros when it was never started. */
 int sqobfs_engine_info_get(sqobfs_ctx *ctx, sqobfs_engine_info *out);
@@ -779,16 +799,20 @@ int sqobfs_engine_set_affinity(sqobfs_ctx *ctx, int mode);
 /* Coalesced launches.  A Hysteria2 server wraps one socket
  * (hysteria2/service.go:117-120) but a port-hopping client one conn per hop
  * (hysteria/hop.go:40-63) over a generic PacketConn (client.go:184-186:
- * pump mode here), and a process may serve many: when a worker launches the
- * batch of a pump-mode pconn that leaves the routing to the engine (cpu_max
- * 0 or SQOBFS_PCONN_NEVER), the batches other such pconns of the same scheme
- * have queued in the same direction join that launch -- at most max_batches
- * of them (0 = 8; 1 = every batch its own launch) and 16,384 datagrams -- so
- * one kernel, one wait and one launch's host cost carry them all (batches
- * are not gathered to make a launch none of them would make alone).  Their
- * PSKs may differ: the launch then reads per-datagram PSK ids into a keyring
- * the engine merges from the pconns' keyrings.  Socket-mode pconns are not
- * gathered (their batches' steps are socket calls that the workers keep
+ * pump mode here), and a process may serve many: when a worker launches a
+ * pconn's batch, the pconn's other full batches queued in that direction
+ * join the launch, and when the pconn is in pump mode and leaves the
+ * routing to the engine (cpu_max 0 or SQOBFS_PCONN_NEVER), so do the batches
+ * other such pconns of the same scheme have queued in the same direction --
+ * at most max_batches batches (0 = 32; 1 = every batch its own launch) and
+ * 16,384 datagrams -- so one kernel, one wait and one launch's host cost
+ * carry them all (batches are not gathered to make a launch none of them
+ * would make alone).  Batches routed to a non-polling launch while one is
+ * still in flight wait for it, and its completion launches them together
+ * (the engine's natural batching under load).  Their PSKs may differ: the
+ * launch then reads per-datagram PSK ids into a keyring the engine merges
+ * from the pconns' keyrings.  Socket-mode pconns' tasks are not gathered by
+ * another pconn's worker (their steps are socket calls that the workers keep
  * making in parallel).  Any time. */
 int sqobfs_engine_set_group(sqobfs_ctx *ctx, uint32_t max_batches);
 /* Free the pool's unused blocks; returns how many were freed. */

@@ -367,7 +367,8 @@ void sq_keyring_hot(const sqobfs_keyring *kr, uint32_t *hot_m, uint32_t *hot_iv)
 }
 
 int sq_keyring_from_entries(sqobfs_ctx *ctx, int kind, const sq::PskEntry *e, uint32_t count,
-                            uint32_t hot_m, uint32_t hot_iv, sqobfs_keyring **out) {
+                            uint32_t hot_m, uint32_t hot_iv, void *stream,
+                            sqobfs_keyring **out) {
   *out = nullptr;
   if (!ctx || !e || count == 0) return SQ_EINVAL;
   sqobfs_keyring *kr = new (std::nothrow) sqobfs_keyring();
@@ -386,18 +387,21 @@ int sq_keyring_from_entries(sqobfs_ctx *ctx, int kind, const sq::PskEntry *e, ui
   kr->host0 = kr->host[0];
   DeviceScope ds_(ctx->device);
   int st = ds_.status;
+  // the table is made on the caller's stream (the engine's launch stream),
+  // so the wait does not queue behind the context stream's own work
+  hipStream_t hs = stream ? (hipStream_t)stream : ctx->stream;
   // (the host entries are the device layout: sqobfs_debug_keyring_check)
   if (st == SQ_OK)
-    st = hip_status(tab_alloc((void **)&kr->table, sizeof(sq::PskEntry) * count, ctx->stream));
+    st = hip_status(tab_alloc((void **)&kr->table, sizeof(sq::PskEntry) * count, hs));
   if (st == SQ_OK)
     st = hip_status(hipMemcpyAsync(kr->table, kr->host.data(), sizeof(sq::PskEntry) * count,
-                                   hipMemcpyHostToDevice, ctx->stream));
-  if (st == SQ_OK) st = hip_status(hipStreamSynchronize(ctx->stream));
+                                   hipMemcpyHostToDevice, hs));
+  if (st == SQ_OK) st = hip_status(hipStreamSynchronize(hs));
   if (st != SQ_OK) {
     if (kr->table) {
-      (void)hipStreamSynchronize(ctx->stream);
-      tab_free_async(kr->table, ctx->stream);
-      (void)hipStreamSynchronize(ctx->stream);
+      (void)hipStreamSynchronize(hs);
+      tab_free_async(kr->table, hs);
+      (void)hipStreamSynchronize(hs);
     }
     delete kr;
     return st;
@@ -1104,6 +1108,12 @@ void gcm_key(const sqobfs_quic_key &k, sq::QuicGcmKeyDev &d) {
   const uint8_t zero[16] = {0};
   uint8_t hb[16];
   aes128_block(d.rk, zero, hb);
+  // rounds 1-9 stored rotated by 16 bits: the kernel folds the round key
+  // under its rotl16 (sq_quic_gcm.hip aes_encrypt_n)
+  for (int i = 4; i < 40; i++) {
+    d.rk[i] = (d.rk[i] >> 16) | (d.rk[i] << 16);
+    d.hrk[i] = (d.hrk[i] >> 16) | (d.hrk[i] << 16);
+  }
   const G128 h = g_load(hb);
   G128 p = h;
   for (uint32_t pw = 0; pw < sq::kGcmPow; pw++) {

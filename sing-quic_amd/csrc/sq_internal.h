@@ -129,8 +129,8 @@ struct QParams {
 // big-endian words).
 constexpr uint32_t kGcmPow = 128;
 struct QuicGcmKeyDev {
-  uint32_t rk[44];
-  uint32_t hrk[44];
+  uint32_t rk[44];   // AES-128 key schedule, words 4..39 (rounds 1-9) rotated
+  uint32_t hrk[44];  // by 16 bits (sq_quic_gcm.hip aes_encrypt_n); hrk: the HP key's
   uint32_t iv[3];
   uint32_t pad;
   uint32_t hpos[32][16][4];
@@ -197,9 +197,11 @@ sqobfs_ctx *sq_keyring_ctx(const sqobfs_keyring *kr);
 void sq_keyring_hot(const sqobfs_keyring *kr, uint32_t *hot_m, uint32_t *hot_iv);
 // a device keyring whose entries are copies of host entries (sq_keyring_host
 // of other keyrings; hot_m / hot_iv: the max / min of theirs): the engine's
-// merged keyrings, one launch over several pconns' batches (pconn.cpp)
+// merged keyrings, one launch over several pconns' batches (pconn.cpp); the
+// table is copied and waited for on `stream` (NULL: the context's stream)
 int sq_keyring_from_entries(sqobfs_ctx *ctx, int kind, const sq::PskEntry *e, uint32_t count,
-                            uint32_t hot_m, uint32_t hot_iv, sqobfs_keyring **out);
+                            uint32_t hot_m, uint32_t hot_iv, void *stream,
+                            sqobfs_keyring **out);
 // one sequence number of the context's salt stream (SQOBFS_FLAG_DEVICE_SALT)
 // and its key, for salts made on the host; ctx NULL: the process's host
 // generator (sq_cpu.cpp)

@@ -127,11 +127,19 @@ __device__ __forceinline__ uint32_t t1at(const uint32_t *tT, uint32_t a) {
   return *(const uint32_t *)((const char *)tT + a + 128);
 }
 
+// three-input XOR in one VALU op (gfx950 v_bitop3_b32, truth table 0x96):
+// the compiler emits two v_xor_b32 for a ^ b ^ c
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
 // FIPS-197 cipher on one block held as 4 little-endian column words.
 // Round: column c = T0[s_c.b0] ^ T1[s_c+1.b1] ^ rotl16(T0[s_c+2.b2] ^
 // T1[s_c+3.b3]) ^ rk (T2 = rotl16 T0, T3 = rotl16 T1; ShiftRows folded into
-// the byte picks); the last round takes the S-box byte (T0 byte 1, T1 bytes
-// 2 and 3) instead.
+// the byte picks), computed as xor3(a0, a1, rotl16(xor3(a2, a3, rotr16 rk)))
+// -- 3 VALU ops per column besides the 4 v_perm addresses; the key schedule
+// holds rounds 1-9 already rotated (sq_api.hip gcm_key).  The last round
+// takes the S-box byte (T0 byte 1, T1 bytes 2 and 3) instead.
 template <int KM, int NB>
 __device__ __forceinline__ void aes_encrypt_n(const uint32_t *rk, const uint32_t *tT, uint32_t lo,
                                               uint32_t (&s)[NB][4]) {
@@ -143,7 +151,8 @@ __device__ __forceinline__ void aes_encrypt_n(const uint32_t *rk, const uint32_t
     for (int c = 0; c < 4; c++) s[q][c] ^= k[c];
 #pragma unroll
   for (int r = 1; r < 10; r++) {
-    round_key<KM>(rk, r, k);
+    uint32_t kr[4];  // (rotated by 16 in the key schedule)
+    round_key<KM>(rk, r, kr);
     uint32_t t[NB][4];
 #pragma unroll
     for (int q = 0; q < NB; q++)
@@ -153,7 +162,7 @@ __device__ __forceinline__ void aes_encrypt_n(const uint32_t *rk, const uint32_t
         const uint32_t a1 = t1at(tT, trow(s[q][(c + 1) & 3], lo, 1));
         const uint32_t a2 = t0at(tT, trow(s[q][(c + 2) & 3], lo, 2));
         const uint32_t a3 = t1at(tT, trow(s[q][(c + 3) & 3], lo, 3));
-        t[q][c] = a0 ^ a1 ^ rotl(a2 ^ a3, 16) ^ k[c];
+        t[q][c] = xor3(a0, a1, rotl(xor3(a2, a3, kr[c]), 16));
       }
 #pragma unroll
     for (int q = 0; q < NB; q++)
@@ -194,33 +203,53 @@ __device__ __forceinline__ void aes_encrypt(const uint32_t *rk, const uint32_t *
 // (x[0] = bytes 0..3).  tab = the 16-entry 4-bit table of H^k; nibbles are
 // consumed from the low end of the 128-bit integer, each step multiplying
 // the accumulator by x^4 (shift right 4, fold the 4 bits shifted out back
-// with the reduction polynomial: rem * 0x1C20 carry-less, at bits 112..127).
-// Entry n of table k-1 is stored in slot n ^ sw, sw = (k-1) & 15: lanes
-// multiplying by different powers then read different 16-byte slots of the
-// bank row for the same nibble (no ds_read_b128 bank conflicts).
+// with the reduction polynomial).  Entry n of table k-1 is stored in slot
+// n ^ sw, sw = (k-1) & 15: lanes multiplying by different powers then read
+// different 16-byte slots of the bank row for the same nibble (no
+// ds_read_b128 bank conflicts).
+// One word (8 nibbles) at a time: its table reads depend only on x, so they
+// are issued back to back (4 in flight); the shifts then run with the
+// fold deferred to the end of the word -- the bits shifted out collect in z4
+// (fold bits enter z0 at bit 21 or above and cannot reach z3's low nibble
+// within 8 shifts), and fold(u) = u ^ u>>1 ^ u>>2 ^ u>>7 over z0:z1, the
+// 4-bit fold (rem<<28 ^ rem<<27 ^ rem<<26 ^ rem<<21) applied to 32 bits at
+// once.
 template <bool GLOBAL>
 __device__ __forceinline__ void gmul(uint32_t (&x)[4], const uint32_t *tab, uint32_t sw) {
   uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
   uint32_t w = x[3], w2 = x[2], w1 = x[1], w0 = x[0];
-  // one word (8 nibbles) per iteration, kept rolled: unrolled, the compiler
-  // hoists all 32 table reads and holds 128 VGPRs of entries
+  const char *t = (const char *)tab;
+  const uint32_t sw16 = sw << 4;
+  // one word per iteration, kept rolled (unrolled, the compiler hoists every
+  // word's reads and spills)
 #pragma unroll 1
   for (int i = 0; i < 4; i++) {
+    const uint32_t w4 = w << 4;
+    uint32_t z4 = 0;
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-      const uint32_t nib = (w >> (4 * j)) & 0xFu;
-      if (i | j) {
-        const uint32_t rem = z3 & 0xFu;
-        z3 = __builtin_amdgcn_alignbit(z2, z3, 4);
-        z2 = __builtin_amdgcn_alignbit(z1, z2, 4);
-        z1 = __builtin_amdgcn_alignbit(z0, z1, 4);
-        z0 = (z0 >> 4) ^ (rem << 28) ^ (rem << 27) ^ (rem << 26) ^ (rem << 21);
+    for (int h = 0; h < 8; h += 4) {  // (4 reads in flight: 8 made the kernels spill)
+      u32x4 e[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int jj = h + j;
+        const uint32_t off = ((((jj & 1) ? w : w4) >> (8 * (jj >> 1))) & 0xF0u) ^ sw16;
+        if (GLOBAL) e[j] = gld<u32x4>((uint64_t)(t + off));
+        else e[j] = *(const u32x4 *)(t + off);
       }
-      u32x4 e;
-      if (GLOBAL) e = gld<u32x4>((uint64_t)(tab + 4 * (nib ^ sw)));
-      else e = *(const u32x4 *)(tab + 4 * (nib ^ sw));
-      z0 ^= e.x; z1 ^= e.y; z2 ^= e.z; z3 ^= e.w;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        if (i | h | j) {
+          z4 = __builtin_amdgcn_alignbit(z3, z4, 4);
+          z3 = __builtin_amdgcn_alignbit(z2, z3, 4);
+          z2 = __builtin_amdgcn_alignbit(z1, z2, 4);
+          z1 = __builtin_amdgcn_alignbit(z0, z1, 4);
+          z0 >>= 4;
+        }
+        z0 ^= e[j].x; z1 ^= e[j].y; z2 ^= e[j].z; z3 ^= e[j].w;
+      }
     }
+    z0 = xor3(z0, xor3(z4, z4 >> 1, z4 >> 2), z4 >> 7);
+    z1 ^= xor3(z4 << 31, z4 << 30, z4 << 25);
     w = w2;
     w2 = w1;
     w1 = w0;
@@ -228,27 +257,43 @@ __device__ __forceinline__ void gmul(uint32_t (&x)[4], const uint32_t *tab, uint
   x[0] = z0; x[1] = z1; x[2] = z2; x[3] = z3;
 }
 
-// x <- x * H with the position tables of H: XOR of pos[j][nibble j of x]
-// over the 32 nibbles (from the low end of the 128-bit integer).  No
-// dependency between the lookups; one word's 8 lookups at a time (the
-// scheduling barrier keeps the compiler from hoisting all 32 entries into
-// 128 VGPRs).
+// x <- x * H with the position tables of H (pos: 32 nibble positions x 16
+// entries x 16 B, one 256-byte bank row per position): the XOR of
+// pos[j][nibble j of x] over the 32 nibbles (from the low end of the 128-bit
+// integer) -- no shifts, no reduction steps.  The lookups do not depend on
+// each other: they are issued 4 at a time back to back (16 VGPRs; 8 at a
+// time made the kernels spill), then folded with three-input XORs; with pos at LDS address 0 an
+// address is the nibble times 16 plus the word's base, and the position an
+// immediate offset.  (Round 5's loop issued one read at a time and waited
+// for it: 32 LDS round trips in a row per multiply.)
 template <bool GLOBAL>
 __device__ __forceinline__ void gmul_pos(uint32_t (&x)[4], const uint32_t *pos) {
   uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
   uint32_t w = x[3], w2 = x[2], w1 = x[1], w0 = x[0];
   const char *base = (const char *)pos;
-  // one word (8 lookups) per iteration, kept rolled: unrolled, the compiler
-  // hoists all 32 entries into 128 VGPRs
+  // one word per iteration, kept rolled (unrolled, the compiler hoists every
+  // word's reads and spills)
 #pragma unroll 1
   for (int i = 0; i < 4; i++) {
+    const uint32_t w4 = w << 4;
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-      const uint32_t off = (((w >> (4 * j)) & 0xFu) << 4) + 256u * j;
-      u32x4 e;
-      if (GLOBAL) e = gld<u32x4>((uint64_t)(base + off));
-      else e = *(const u32x4 *)(base + off);
-      z0 ^= e.x; z1 ^= e.y; z2 ^= e.z; z3 ^= e.w;
+    for (int h = 0; h < 8; h += 4) {
+      u32x4 e[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int jj = h + j;
+        const uint32_t off = (((jj & 1) ? w : w4) >> (8 * (jj >> 1))) & 0xF0u;
+        const char *p = base + 256 * jj + off;
+        if (GLOBAL) e[j] = gld<u32x4>((uint64_t)p);
+        else e[j] = *(const u32x4 *)p;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j += 2) {
+        z0 = xor3(z0, e[j].x, e[j + 1].x);
+        z1 = xor3(z1, e[j].y, e[j + 1].y);
+        z2 = xor3(z2, e[j].z, e[j + 1].z);
+        z3 = xor3(z3, e[j].w, e[j + 1].w);
+      }
     }
     base += 8 * 256;
     w = w2;
@@ -718,6 +763,26 @@ __device__ __forceinline__ void gcm_unit(const QGParams &Q, uint64_t base, uint3
   Q.out_len[p] = len + 16 + (OB ? kSalamanderSalt : 0u);
 }
 
+// The kernels' LDS, one image laid out by hand (the compiler's placement of
+// separate arrays put the position tables past 64 KiB): the GHASH position
+// tables of H at address 0 (8 KiB; a lookup's position is its immediate
+// offset), the AES T-table image (64 KiB; a lookup's row and column come
+// from one v_perm, the image's base is the immediate), the power tables
+// (32 KiB), the staged key words (TK), then the waves' records.  TABLES
+// false (per-packet keys from global memory): no position or power tables.
+template <bool TABLES, uint32_t TK>
+constexpr uint32_t kLdsWords = (TABLES ? 32 * 64 + kGcmPow * 64 : 0u) + 256 * 64 +
+                               (TK + 3) / 4 * 4 + (uint32_t)sizeof(GRec) * kGWaves * kGPpw / 4;
+template <bool TABLES, uint32_t TK>
+__device__ __forceinline__ void gcm_lds(uint32_t *lds, uint32_t *&tP, uint32_t *&tT, uint32_t *&tH,
+                                        uint32_t *&tK, GRec (*&recs)[kGPpw]) {
+  tP = lds;
+  tT = lds + (TABLES ? 32 * 64 : 0);
+  tH = tT + 256 * 64;
+  tK = tH + (TABLES ? kGcmPow * 64 : 0);
+  recs = reinterpret_cast<GRec(*)[kGPpw]>(tK + (TK + 3) / 4 * 4);
+}
+
 // The T-table image (every launch) and, single key, the key's GHASH tables,
 // into LDS (single-key round keys stay in the kernarg segment: staged in LDS
 // they measured 17 % slower, the keys then occupying VGPRs).
@@ -742,11 +807,12 @@ __device__ __forceinline__ void stage_common(const QGParams &Q, uint32_t *tT, ui
 // (MULTI true, batches that are not grouped).
 template <bool OPEN, bool MULTI, bool OB>
 __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
-  __shared__ uint32_t tT[256 * 64];
-  __shared__ __attribute__((aligned(16))) uint32_t tP[MULTI ? 4 : 32 * 64];
-  __shared__ __attribute__((aligned(16))) uint32_t tH[MULTI ? 4 : kGcmPow * 64];
-  __shared__ GRec recs[kGWaves][kGPpw];
-  __shared__ __attribute__((aligned(16))) uint32_t tK[4];  // (staged launches only)
+  // one LDS image laid out by hand (gcm_lds): the GHASH position tables at
+  // address 0, so a lookup's position is its immediate offset (< 64 KiB)
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords<!MULTI, 4>];
+  uint32_t *tP, *tT, *tH, *tK;
+  GRec(*recs)[kGPpw];
+  gcm_lds<!MULTI, 4>(lds, tP, tT, tH, tK, recs);
   const uint64_t units = ((uint64_t)Q.n + kGPpw - 1) / kGPpw;
   stage_common<MULTI>(Q, tT, tP, tH, tK);
   __syncthreads();
@@ -773,11 +839,10 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
 // range of units measured slower than striding.)
 template <bool OPEN, bool OB>
 __global__ __launch_bounds__(kGBlock) void quic_gcm_staged_kernel(const QGParams Q) {
-  __shared__ uint32_t tT[256 * 64];
-  __shared__ __attribute__((aligned(16))) uint32_t tP[32 * 64];
-  __shared__ __attribute__((aligned(16))) uint32_t tH[kGcmPow * 64];
-  __shared__ GRec recs[kGWaves][kGPpw];
-  __shared__ __attribute__((aligned(16))) uint32_t tK[92];  // [88..90]: the staged key's IV
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords<true, 92>];
+  uint32_t *tP, *tT, *tH, *tK;  // tK[88..90]: the staged key's IV
+  GRec(*recs)[kGPpw];
+  gcm_lds<true, 92>(lds, tP, tT, tH, tK, recs);
   stage_common<true>(Q, tT, tP, tH, tK);
   __syncthreads();
   const uint32_t lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;

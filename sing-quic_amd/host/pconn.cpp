@@ -80,7 +80,7 @@
 
 namespace {
 
-constexpr uint32_t kDefBatch = 256, kDefSlot = 2048, kDefBatches = 3, kDefSpinUs = 200;
+constexpr uint32_t kDefBatch = 256, kDefSlot = 2048, kDefBatches = 8, kDefSpinUs = 200;
 // routing (opts.cpu_max 0): the CPU path's cost estimate before it is
 // measured, and the bounds of the measured break-even
 constexpr uint32_t kDefCpuNsPerKiB = 500;
@@ -115,7 +115,14 @@ constexpr size_t kCtlWords = (CMSG_SPACE(sizeof(uint16_t)) + 7) / 8;
 // one launch over several pconns' batches (run_task): at most group_max
 // batches (sqobfs_engine_set_group) and kGroupDgrams datagrams; a merged
 // keyring is made anew past kMergedMax PSKs
-constexpr uint32_t kDefGroup = 8, kMaxGroup = 64, kGroupDgrams = 16384, kMergedMax = 256;
+constexpr uint32_t kDefGroup = 32, kMaxGroup = 64, kGroupDgrams = 16384, kMergedMax = 256;
+// launches in flight at once per engine (one stream each); a worker that
+// would start one more waits for a stream
+constexpr uint32_t kMaxFlights = 32;
+// non-polling launches in flight at once (run_task): past it, the batches
+// routed to the GPU wait, prepared, and the next completion launches all of
+// them together -- the natural batching of the GPU route
+constexpr uint32_t kDefFlightCap = 1;
 
 // sqobfs_debug_engine_fail, sqobfs_debug_pool_fail, sqobfs_debug_engine_hold
 std::atomic<int> g_fail_count{0};
@@ -239,9 +246,14 @@ struct sqobfs_pconn {
 
 namespace {
 
+struct Job;
+struct Flight;
+
 struct Task {
   sqobfs_pconn *pc;
-  int dir;  // kTx / kRx
+  int dir;               // kTx / kRx
+  Flight *fin = nullptr;  // set: finish these landed socket-mode batches of the
+                          // pconn, in order (completer_main)
 };
 
 // A keyring the engine made for coalesced launches over pconns with
@@ -271,8 +283,20 @@ struct Engine {
   uint32_t pconns = 0;
   bool stop = false;
   std::vector<std::thread> threads;
-  std::vector<void *> streams;  // one per worker, made by that worker on first launch
   int epfd = -1, wake = -1;
+  // launches in flight (under cmu): the streams (made on demand, at most
+  // kMaxFlights, each carrying one launch at a time) and the launches the
+  // completer thread waits for, in launch order
+  std::mutex cmu;
+  std::condition_variable cv_flight;  // the completer: a launch was queued / stop
+  std::condition_variable cv_stream;  // a worker: a stream was given back
+  std::vector<void *> streams, sfree;
+  std::deque<Flight *> flights;
+  std::vector<Job> pending;  // routed to the GPU while flight_cap launches fly
+  uint32_t nflight = 0;     // non-polling launches started and not yet landed
+  uint32_t flight_cap = kDefFlightCap;
+  bool cstop = false;
+  std::atomic<uint64_t> async_launches{0};
   std::atomic<bool> gpu_off{false};
   std::atomic<uint32_t> launch_us{40};  // recent launch completion time (EWMA)
   std::atomic<uint32_t> cpu_ns_kib{kDefCpuNsPerKiB};  // recent CPU-path ns per KiB of cost (EWMA)
@@ -369,8 +393,9 @@ void engine_thread_pin(const Engine *E) {
   (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
 }
 
-void worker_main(Engine *E, uint32_t w);
+void worker_main(Engine *E);
 void poller_main(Engine *E);
+void completer_main(Engine *E);
 
 Engine *engine_get(sqobfs_ctx *ctx, int *status) {
   std::lock_guard<std::mutex> g(g_eng_mu);
@@ -389,7 +414,8 @@ Engine *engine_get(sqobfs_ctx *ctx, int *status) {
   if (aff == SQOBFS_ENGINE_AFFINITY_L3) E->ncpus = l3_cpus(&E->cpus);
   auto gc = g_group_cfg.find(ctx);
   if (gc != g_group_cfg.end()) E->group_max = gc->second;
-  E->streams.assign(E->nworkers, nullptr);
+  if (const char *fc = getenv("SQ_ENGINE_FLIGHTS"))  // (dev: the cap sweep)
+    E->flight_cap = std::max(1, std::min(atoi(fc), (int)kMaxFlights));
   E->wake = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
   E->epfd = epoll_create1(EPOLL_CLOEXEC);
   epoll_event ev{};
@@ -403,14 +429,22 @@ Engine *engine_get(sqobfs_ctx *ctx, int *status) {
     return nullptr;
   }
   try {
-    for (uint32_t w = 0; w < E->nworkers; w++) E->threads.emplace_back(worker_main, E, w);
+    E->streams.reserve(kMaxFlights);
+    E->sfree.reserve(kMaxFlights);
+    for (uint32_t w = 0; w < E->nworkers; w++) E->threads.emplace_back(worker_main, E);
     E->threads.emplace_back(poller_main, E);
+    if (ctx) E->threads.emplace_back(completer_main, E);
   } catch (...) {
     {
       std::lock_guard<std::mutex> lk(E->mu);
       E->stop = true;
     }
+    {
+      std::lock_guard<std::mutex> lk(E->cmu);
+      E->cstop = true;
+    }
     E->cv.notify_all();
+    E->cv_flight.notify_all();
     const uint64_t one = 1;
     (void)!write(E->wake, &one, sizeof one);
     for (auto &t : E->threads) t.join();
@@ -536,6 +570,11 @@ void schedule(sqobfs_pconn *pc, int d) {
   schedule_locked(pc->eng, pc, d);
 }
 
+// The calling thread is one of the engine's workers (worker_main), and the
+// tasks it has requeued without a wake-up since the count was last reset.
+thread_local bool t_worker = false;
+thread_local uint32_t t_requeued = 0;
+
 // The running task of direction d is done with the work it found: requeue
 // (more work), park until `due` (linger), or end.  Caller holds pc->mu.
 void task_end(sqobfs_pconn *pc, int d, bool more, int64_t due = 0) {
@@ -560,8 +599,13 @@ void task_end(sqobfs_pconn *pc, int d, bool more, int64_t due = 0) {
       // rx tasks of a busy pair of conns are queued together most of the
       // time).  No task starves: a sleeping worker means the queue was empty
       // when it slept, and every task queued since came with a wake-up or,
-      // like this one, with the worker that queued it.
+      // like this one, with the worker that queued it.  (Off a worker -- the
+      // completer finishing a launch -- there is no such worker: wake one.
+      // A worker that requeues several, after a coalesced launch, wakes
+      // others for the rest: run_task.)
       E->runq.push_back({pc, d});
+      if (t_worker) t_requeued++;
+      else E->cv.notify_one();
     }
     return;
   }
@@ -582,7 +626,13 @@ struct Job {
   uint64_t trunc = 0;   // socket receive: truncated datagrams
   uint64_t cost = 0;    // payload bytes + kHashCost per datagram
   int st = SQ_OK;
-  bool cpu = false, failed = false;
+  // cpu: transformed on the CPU path; failed: its launch failed and the
+  // engine stays on the CPU; refused: its launch was refused for the moment
+  // (redone on the CPU path, the GPU still on)
+  bool cpu = false, failed = false, refused = false;
+  // the last of its task's batches in this transform: its finish ends or
+  // requeues the task (a launch may carry several batches of one task)
+  bool end_task = true;
   PBatch &batch() const { return dir == kTx ? pc->tb[idx] : pc->rb[idx]; }
   int op() const { return dir == kTx ? SQOBFS_OBFUSCATE : SQOBFS_DEOBFUSCATE; }
 };
@@ -659,7 +709,7 @@ void block_batch(const Job &j, sqobfs_batch &d) {
 // room, made anew past kMergedMax entries.  pid[j] = job j's entry.  NULL,
 // with *st, when it cannot be made.
 std::shared_ptr<MergedKeyring> merged_keyring(Engine *E, const Job *jobs, uint32_t nj,
-                                              uint16_t *pid, int *st) {
+                                              uint16_t *pid, void *stream, int *st) {
   const int kind = jobs[0].pc->kind;
   const int ki = kind == SQOBFS_SALAMANDER ? 0 : 1;
   auto find = [](const MergedKeyring *m, const sq::PskEntry *x) -> int {
@@ -702,60 +752,109 @@ std::shared_ptr<MergedKeyring> merged_keyring(Engine *E, const Job *jobs, uint32
     return nullptr;
   }
   *st = sq_keyring_from_entries(E->ctx, kind, m->e.data(), (uint32_t)m->e.size(), m->hot_m,
-                                m->hot_iv, &m->kr);
+                                m->hot_iv, stream, &m->kr);
   if (*st != SQ_OK) return nullptr;
   E->mkr[ki] = m;  // (the old one is destroyed when its last launch lets go)
   return m;
 }
 
-// Launches the jobs' batches on worker w's stream and waits.  One batch:
+// A launch from its start to its completion (gpu_launch .. gpu_land).  A
+// launch whose wait does not poll -- bulk under load, or spin_us NEVER -- is
+// completed by the engine's completer thread (completer_main), so the worker
+// that made it goes back to the run queue at once (other pconns' batches,
+// socket calls, hand-offs) instead of sleeping through the kernel and its
+// round trip (~85 us); a polled launch (the latency route) is waited for by
+// its own worker, which spins on it anyway.
+struct Flight {
+  Job jobs[kMaxGroup];
+  uint32_t nj = 0;
+  Block *gb = nullptr;                // a coalesced launch's descriptor block
+  std::shared_ptr<MergedKeyring> mk;  // ... and its merged keyring
+  void *stream = nullptr;
+  int64_t t0 = 0;          // launch time (monotonic ns)
+  int64_t launch_cpu = 0;  // the launching thread's CPU time in the launch call
+  bool block = false;      // its wait does not poll
+  int inject = 0;          // sqobfs_debug_engine_fail: 2 = the kernel "fails"
+};
+
+// A stream for one launch: a free one, a new one (at most kMaxFlights), or
+// the next one given back.  NULL, with *st, when none can be made.
+void *stream_take(Engine *E, int *st) {
+  std::unique_lock<std::mutex> lk(E->cmu);
+  for (;;) {
+    if (E->cstop) {
+      *st = SQ_ECLOSED;
+      return nullptr;
+    }
+    if (!E->sfree.empty()) {
+      void *s = E->sfree.back();
+      E->sfree.pop_back();
+      return s;
+    }
+    if (E->streams.size() < kMaxFlights) {  // (capacity reserved: no reallocation)
+      void *s = nullptr;
+      *st = sq_ctx_stream_create(E->ctx, &s);
+      if (*st != SQ_OK) return nullptr;
+      E->streams.push_back(s);
+      return s;
+    }
+    E->cv_stream.wait(lk);
+  }
+}
+
+void stream_give(Engine *E, void *s) {
+  {
+    std::lock_guard<std::mutex> lk(E->cmu);
+    E->sfree.push_back(s);  // (capacity reserved)
+  }
+  E->cv_stream.notify_one();
+}
+
+// Starts the launch of f's jobs' batches on a stream of its own.  One batch:
 // over its own block.  Several (coalesced, run_task): over one descriptor
 // built in a block of the pool, every datagram addressed from the lowest of
 // their blocks (blocks are mapped at their host addresses, so one base
 // reaches them all), with per-datagram PSK ids into a merged keyring when
-// the pconns' keyrings differ; out_len is copied back into each block.
-// Returns SQ_OK; kRefused when nothing ran (the batches are intact, for the
-// CPU path); or the error of a kernel that failed (the batches, transformed
-// in place, are lost).  A device failure turns the GPU off for the engine;
-// a refusal of this batch or this moment (no memory for a stream, a block
-// or a keyring) leaves the next batch free to launch.
-int gpu_run(Engine *E, uint32_t w, Job *jobs, uint32_t nj, bool block) {
-  auto refused = [E](int st) {
+// the pconns' keyrings differ.  Returns SQ_OK (in flight: gpu_land completes
+// it) or kRefused (nothing ran: the batches are intact, for the CPU path).
+// A device failure turns the GPU off for the engine; a refusal of this batch
+// or this moment (no memory for a stream, a block or a keyring) leaves the
+// next batch free to launch.
+int gpu_launch(Engine *E, Flight &f) {
+  auto refused = [E, &f](int st) {
     if (st == SQ_EDEVICE || st == SQ_ENODEV) E->gpu_off.store(true);
+    if (f.gb) block_give(E, f.gb);
+    f.gb = nullptr;
+    f.mk.reset();
+    if (f.stream) stream_give(E, f.stream);
+    f.stream = nullptr;
     return kRefused;
   };
+  const Job *jobs = f.jobs;
+  const uint32_t nj = f.nj;
   int st = SQ_OK;
-  if (!E->streams[w]) {  // (only worker w writes its slot; close reads it under mu)
-    void *s = nullptr;
-    st = sq_ctx_stream_create(E->ctx, &s);
-    std::lock_guard<std::mutex> lk(E->mu);
-    E->streams[w] = s;
-  }
-  if (st != SQ_OK) return refused(st);
+  f.stream = stream_take(E, &st);
+  if (!f.stream) return refused(st);
   const int op = jobs[0].op();
   const sqobfs_keyring *kr = jobs[0].pc->kr;
-  std::shared_ptr<MergedKeyring> mk;
-  Block *gb = nullptr;
   sqobfs_batch d;
   bool slotted = jobs[0].slotted;
   if (nj == 1) {
     block_batch(jobs[0], d);
   } else {
-    gb = block_take(E, kGroupDgrams, 16);  // (psk ids in its slot region)
-    if (!gb) return kRefused;
+    f.gb = block_take(E, kGroupDgrams, 16);  // (psk ids in its slot region)
+    if (!f.gb) return refused(SQ_ENOMEM);
     bool same = true;
     for (uint32_t j = 1; j < nj; j++) same = same && jobs[j].pc->kr == kr;
     uint16_t pid[kMaxGroup] = {};
     if (!same) {
-      mk = merged_keyring(E, jobs, nj, pid, &st);
-      if (!mk) {
-        block_give(E, gb);
-        return refused(st);
-      }
-      kr = mk->kr;
+      f.mk = merged_keyring(E, jobs, nj, pid, f.stream, &st);
+      if (!f.mk) return refused(st);
+      kr = f.mk->kr;
     }
     uint8_t *base = jobs[0].batch().blk->slots;
     for (uint32_t j = 1; j < nj; j++) base = std::min(base, jobs[j].batch().blk->slots);
+    Block *gb = f.gb;
     uint16_t *ids = (uint16_t *)gb->slots;
     uint32_t n = 0;
     for (uint32_t j = 0; j < nj; j++) {
@@ -785,50 +884,86 @@ int gpu_run(Engine *E, uint32_t w, Job *jobs, uint32_t nj, bool block) {
   // datagrams back to back (no flag)
   d.flags = (slotted ? SQOBFS_FLAG_OUT_BLOCKS : 0u) |
             (op == SQOBFS_OBFUSCATE ? SQOBFS_FLAG_DEVICE_SALT : 0u);
-  const int inject = take_one(g_fail_count) ? (g_fail_at_completion.load() ? 2 : 1) : 0;
-  const int64_t t0 = mono_ns(), c0 = thread_cpu_ns();
-  st = inject == 1 ? SQ_EDEVICE : sqobfs_launch(E->ctx, kr, op, &d, E->streams[w]);
-  if (st != SQ_OK) {
-    if (gb) block_give(E, gb);
-    return refused(st);
-  }
+  f.inject = take_one(g_fail_count) ? (g_fail_at_completion.load() ? 2 : 1) : 0;
+  f.t0 = mono_ns();
+  const int64_t c0 = thread_cpu_ns();
+  st = f.inject == 1 ? SQ_EDEVICE : sqobfs_launch(E->ctx, kr, op, &d, f.stream);
+  f.launch_cpu = thread_cpu_ns() - c0;
+  if (st != SQ_OK) return refused(st);
   E->launches.fetch_add(1, std::memory_order_relaxed);
   if (nj > 1) {
     E->group_launches.fetch_add(1, std::memory_order_relaxed);
     E->group_batches.fetch_add(nj, std::memory_order_relaxed);
   }
-  const uint32_t ew = E->launch_us.load(std::memory_order_relaxed);
-  // bulk batches and spin_us NEVER block at once (the worker's core is free
-  // while the kernel runs)
-  const uint32_t spin = std::min<uint32_t>(jobs[0].pc->o.spin_us, 2 * ew + 20);
-  const uint32_t ek = E->kern_us.load(std::memory_order_relaxed);
-  st = block ? sq_ctx_stream_wait_blocking(E->ctx, E->streams[w], ek * 3 / 4)
-             : sq_ctx_stream_wait(E->ctx, E->streams[w], spin);
-  if (inject == 2) st = SQ_EDEVICE;
-  if (st != SQ_OK) {
-    // the kernel ran, in place, and failed: the slots' state is unknown
-    if (gb) block_give(E, gb);
-    E->gpu_off.store(true);
-    return st;
-  }
-  const uint32_t us = (uint32_t)std::min<int64_t>((mono_ns() - t0) / 1000, 100000);
-  E->launch_us.store((7 * ew + us) / 8, std::memory_order_relaxed);
-  if (block) {  // the host's cost of a launched batch (polled waits would count their spin)
-    E->kern_us.store((7 * E->kern_us.load(std::memory_order_relaxed) + us) / 8,
-                     std::memory_order_relaxed);
-    const uint32_t hn = (uint32_t)std::min<int64_t>(thread_cpu_ns() - c0, 10'000'000);
-    const uint32_t eh = E->gpu_host_ns.load(std::memory_order_relaxed);
-    E->gpu_host_ns.store((7 * eh + hn) / 8, std::memory_order_relaxed);
-  }
-  if (gb) {
-    uint32_t n = 0;
-    for (uint32_t j = 0; j < nj; j++) {
-      const PBatch &b = jobs[j].batch();
-      for (uint32_t i = 0; i < b.n; i++) b.blk->out_len[i] = gb->out_len[n++];
-    }
-    block_give(E, gb);
-  }
   return SQ_OK;
+}
+
+// Waits for f's launch -- polling up to twice the recent round trip (at most
+// spin_us), or, for a non-polling one, asleep through 3/4 of the kernel's
+// expected time from its start, then polling with short sleeps -- and
+// completes it: the engine's estimates, out_len back into each block of a
+// coalesced launch, the descriptor block and the stream given back.
+// Returns SQ_OK, or the error of a kernel that failed (the batches,
+// transformed in place, are lost; the GPU is off for the engine).
+int gpu_land(Engine *E, Flight &f) {
+  const int64_t c0 = thread_cpu_ns();
+  const uint32_t ew = E->launch_us.load(std::memory_order_relaxed);
+  int st;
+  if (f.block) {
+    const int64_t due = f.t0 + (int64_t)E->kern_us.load(std::memory_order_relaxed) * 750;
+    const int64_t now = mono_ns();
+    st = sq_ctx_stream_wait_blocking(E->ctx, f.stream,
+                                     due > now ? (uint32_t)((due - now) / 1000) : 0u);
+  } else {
+    const uint32_t spin = std::min<uint32_t>(f.jobs[0].pc->o.spin_us, 2 * ew + 20);
+    st = sq_ctx_stream_wait(E->ctx, f.stream, spin);
+  }
+  if (f.inject == 2) st = SQ_EDEVICE;
+  if (st == SQ_OK) {
+    const uint32_t us = (uint32_t)std::min<int64_t>((mono_ns() - f.t0) / 1000, 100000);
+    E->launch_us.store((7 * ew + us) / 8, std::memory_order_relaxed);
+    if (f.block) {  // the host's cost of a launched batch (polled waits would count their spin)
+      E->kern_us.store((7 * E->kern_us.load(std::memory_order_relaxed) + us) / 8,
+                       std::memory_order_relaxed);
+      const uint32_t hn =
+          (uint32_t)std::min<int64_t>(f.launch_cpu + thread_cpu_ns() - c0, 10'000'000);
+      const uint32_t eh = E->gpu_host_ns.load(std::memory_order_relaxed);
+      E->gpu_host_ns.store((7 * eh + hn) / 8, std::memory_order_relaxed);
+    }
+    if (f.gb) {
+      uint32_t n = 0;
+      for (uint32_t j = 0; j < f.nj; j++) {
+        const PBatch &b = f.jobs[j].batch();
+        for (uint32_t i = 0; i < b.n; i++) b.blk->out_len[i] = f.gb->out_len[n++];
+      }
+    }
+  } else {
+    // the kernel ran, in place, and failed: the slots' state is unknown
+    E->gpu_off.store(true);
+  }
+  if (f.gb) block_give(E, f.gb);
+  f.gb = nullptr;
+  f.mk.reset();
+  stream_give(E, f.stream);
+  f.stream = nullptr;
+  return st;
+}
+
+// Queues a started non-polling launch for the completer; false when it
+// cannot (the engine is stopping, or no memory): its worker lands it.
+bool flight_queue(Engine *E, Flight *f) {
+  {
+    std::lock_guard<std::mutex> lk(E->cmu);
+    if (E->cstop) return false;
+    try {
+      E->flights.push_back(f);
+    } catch (...) {
+      return false;
+    }
+  }
+  E->async_launches.fetch_add(1, std::memory_order_relaxed);
+  E->cv_flight.notify_one();
+  return true;
 }
 
 // The CPU path (sq_cpu.h) of a job's batch: salts of the context's stream,
@@ -950,6 +1085,7 @@ int send_batch(sqobfs_pconn *pc, PBatch &b, uint32_t from, int *first_err, uint6
 void note_transform(sqobfs_pconn *pc, const Job &j) {
   if (j.cpu) pc->st.cpu_batches++;
   if (j.failed) pc->st.gpu_failures++;
+  if (j.refused) pc->st.gpu_refused++;
   if (j.st != SQ_OK && j.st != SQ_ECLOSED) pc->st.dropped += j.batch().n;
 }
 
@@ -998,7 +1134,6 @@ void tx_finish(Job &j) {
   uint64_t nerr = 0;
   if (j.st == SQ_OK && pc->socket_mode()) j.st = send_batch(pc, b, 0, &send_err, &nerr);
   std::unique_lock<std::mutex> lk(pc->mu);
-  pc->tx_busy = false;
   note_transform(pc, j);
   if (send_err && !pc->tx_err) pc->tx_err = send_err;
   pc->st.tx_send_errors += nerr;
@@ -1015,6 +1150,8 @@ void tx_finish(Job &j) {
     pc->tfree.push_back(j.idx);
   }
   pc->cv_txs.notify_all();
+  if (!j.end_task) return;  // (the task's last batch ends it)
+  pc->tx_busy = false;
   const bool more = !pc->tq.empty() || (pc->tfill >= 0 && pc->tb[pc->tfill].n > 0);
   task_end(pc, kTx, more);
 }
@@ -1071,6 +1208,7 @@ void rx_pump_finish(Job &j) {
   sqobfs_pconn *pc = j.pc;
   std::unique_lock<std::mutex> lk(pc->mu);
   rx_done(pc, j);
+  if (!j.end_task) return;  // (the task's last batch ends it)
   const bool more = !pc->rq.empty() || (pc->rfill >= 0 && pc->rb[pc->rfill].n > 0);
   task_end(pc, kRx, more);
 }
@@ -1221,6 +1359,27 @@ bool task_prepare(Engine *E, const Task &t, Job &j) {
   return rx_pump_prepare(t.pc, j);
 }
 
+// The next queued batch of a task whose first batch run_task prepared and
+// launches: a transmit task's next full batch, a pump receive task's next
+// pushed one, when it has at most `room` datagrams; false when there is
+// none (socket receive: one recvmmsg per task run).
+bool task_prepare_next(const Task &t, uint32_t room, Job &j) {
+  sqobfs_pconn *pc = t.pc;
+  if (t.dir == kRx && pc->socket_mode()) return false;
+  std::lock_guard<std::mutex> lk(pc->mu);
+  std::deque<uint32_t> &q = t.dir == kTx ? pc->tq : pc->rq;
+  if (pc->closed || q.empty()) return false;
+  std::vector<PBatch> &bs = t.dir == kTx ? pc->tb : pc->rb;
+  if (bs[q.front()].n > room) return false;
+  j.pc = pc;
+  j.dir = t.dir;
+  j.idx = q.front();
+  j.slotted = true;
+  q.pop_front();
+  if (t.dir == kRx) bs[j.idx].next = 0;
+  return true;
+}
+
 void task_finish(Job &j) {
   if (j.dir == kTx) tx_finish(j);
   else if (j.pc->socket_mode()) rx_socket_finish(j);
@@ -1246,7 +1405,7 @@ uint32_t grab_tasks(Engine *E, int dir, int kind, uint32_t room, Task *out, uint
   uint32_t n = 0;
   for (auto it = E->runq.begin(); it != E->runq.end() && n < max;) {
     const sqobfs_pconn *pc = it->pc;
-    if (it->dir == dir && pc->kind == kind && groupable(pc) && pc->o.batch <= room) {
+    if (!it->fin && it->dir == dir && pc->kind == kind && groupable(pc) && pc->o.batch <= room) {
       room -= pc->o.batch;
       out[n++] = *it;
       it = E->runq.erase(it);
@@ -1267,30 +1426,17 @@ uint32_t grab_tasks(Engine *E, int dir, int kind, uint32_t room, Task *out, uint
 // for.  Batches are not gathered to make a launch that none of them would
 // make alone: gathered groups of small batches under paced load launched
 // 4-13K times in 3 s for no CPU saved ("Coalesced launches").
-void run_task(Engine *E, uint32_t w, const Task &t) {
-  Job jobs[kMaxGroup];
-  if (!task_prepare(E, t, jobs[0])) return;
-  bool bulk = false;
-  const bool gpu = route_gpu(E, jobs[0], &bulk);
-  uint32_t nj = 1;
-  const uint32_t gmax = std::min(kMaxGroup, E->group_max.load(std::memory_order_relaxed));
-  const uint32_t n0 = jobs[0].batch().n;
-  if (gpu && gmax > 1 && groupable(t.pc) && n0 < kGroupDgrams) {
-    Task more[kMaxGroup];
-    const uint32_t m = grab_tasks(E, t.dir, t.pc->kind, kGroupDgrams - n0, more, gmax - 1);
-    for (uint32_t k = 0; k < m; k++)
-      if (task_prepare(E, more[k], jobs[nj])) {
-        bool b2;
-        (void)route_gpu(E, jobs[nj], &b2);  // (its cost, and the engine's demand)
-        nj++;
-      }
-  }
-  const int st = gpu ? gpu_run(E, w, jobs, nj, bulk || t.pc->o.spin_us == SQOBFS_PCONN_NEVER)
-                     : kRefused;
+// Sets the outcome of the jobs' transform -- st: SQ_OK, a failed kernel's
+// error, or kRefused (nothing ran: redone on the CPU path; gpu: a launch was
+// tried) -- and runs their finish steps.
+void jobs_finish(Engine *E, Job *jobs, uint32_t nj, int st, bool gpu) {
   for (uint32_t k = 0; k < nj; k++) {
     Job &j = jobs[k];
-    if (st == kRefused) {  // (refused: redone on the CPU)
-      j.failed = gpu;
+    if (st == kRefused) {
+      // a refusal that turned the GPU off counts as a failure; one of the
+      // moment (no stream, block or keyring memory) as a refusal
+      j.failed = gpu && E->gpu_off.load(std::memory_order_relaxed);
+      j.refused = gpu && !j.failed;
       j.cpu = true;
       j.st = cpu_run(E, j);
     } else {
@@ -1298,11 +1444,108 @@ void run_task(Engine *E, uint32_t w, const Task &t) {
       j.st = st;
     }
   }
+  t_requeued = 0;
   for (uint32_t k = 0; k < nj; k++) task_finish(jobs[k]);
+  // a worker that requeued several tasks after a coalesced launch takes one
+  // of them itself and wakes a worker for each of the others, which would
+  // otherwise run one after another here (their batches may go to the CPU
+  // path, where nothing regroups them)
+  if (t_worker)
+    for (uint32_t k = 1; k < t_requeued; k++) E->cv.notify_one();
+  t_requeued = 0;
 }
 
-void worker_main(Engine *E, uint32_t w) {
+// One task.  When its batch launches, the batches other pconns have queued
+// for the same scheme and direction join the launch (up to group_max
+// batches, kGroupDgrams datagrams): bulk traffic over several pconns -- the
+// hop conns of a port-hopping client, a server's conns on one context --
+// costs one launch and one wait per group (measured, lat_bench hops, 8 pump
+// conns unpaced: ~4 batches per launch, a quarter of the launches).  A batch
+// that would not have launched on its own rides along: the launch is paid
+// for.  Batches are not gathered to make a launch that none of them would
+// make alone: gathered groups of small batches under paced load launched
+// 4-13K times in 3 s for no CPU saved ("Coalesced launches").
+// A launch that waits without polling goes to the completer (Flight), and
+// the worker returns to the run queue; the completed launch's batches are
+// finished there, or back on a worker (t.fin: a socket-mode batch).
+void run_task(Engine *E, const Task &t) {
+  if (t.fin) {  // (their status set by the completer)
+    Flight *f = t.fin;
+    jobs_finish(E, f->jobs, f->nj, f->jobs[0].st, true);
+    delete f;
+    return;
+  }
+  Flight f;
+  Job *jobs = f.jobs;
+  if (!task_prepare(E, t, jobs[0])) return;
+  bool bulk = false;
+  const bool gpu = route_gpu(E, jobs[0], &bulk);
+  uint32_t nj = 1, nd = jobs[0].batch().n;
+  // a launched task takes its other queued batches along (finished in
+  // order, the last one ending the task): a conn whose writer filled
+  // several batches during the previous launch sends them all in this one
+  const uint32_t gmax = std::min(kMaxGroup, E->group_max.load(std::memory_order_relaxed));
+  auto take_queued = [&](const Task &tk) {
+    while (nj < gmax && nd < kGroupDgrams && task_prepare_next(tk, kGroupDgrams - nd, jobs[nj])) {
+      bool b2;
+      (void)route_gpu(E, jobs[nj], &b2);  // (its cost, and the engine's demand)
+      jobs[nj - 1].end_task = false;
+      nd += jobs[nj].batch().n;
+      nj++;
+    }
+  };
+  if (gpu) take_queued(t);
+  if (gpu && nj < gmax && groupable(t.pc) && nd < kGroupDgrams) {
+    Task more[kMaxGroup];
+    const uint32_t m = grab_tasks(E, t.dir, t.pc->kind, kGroupDgrams - nd, more, gmax - nj);
+    for (uint32_t k = 0; k < m; k++)
+      if (task_prepare(E, more[k], jobs[nj])) {
+        bool b2;
+        (void)route_gpu(E, jobs[nj], &b2);  // (its cost, and the engine's demand)
+        nd += jobs[nj].batch().n;
+        nj++;
+        take_queued(more[k]);
+      }
+  }
+  f.nj = nj;
+  int st = kRefused;
+  if (gpu) {
+    f.block = bulk || t.pc->o.spin_us == SQOBFS_PCONN_NEVER;
+    if (f.block) {
+      // at most flight_cap non-polling launches fly; past it the batches
+      // wait, prepared, and the completion that frees a slot launches every
+      // one of them at once (completer_main)
+      std::lock_guard<std::mutex> lk(E->cmu);
+      if (!E->cstop && E->nflight >= E->flight_cap) {
+        try {
+          E->pending.insert(E->pending.end(), jobs, jobs + nj);
+          return;
+        } catch (...) {  // (no memory: launch it now, over the cap)
+        }
+      }
+      E->nflight++;
+    }
+    st = gpu_launch(E, f);
+    if (st == SQ_OK && f.block) {
+      Flight *h = new (std::nothrow) Flight(std::move(f));
+      if (h) {
+        if (flight_queue(E, h)) return;
+        f = std::move(*h);
+        delete h;
+      }
+    }
+    if (st == SQ_OK) st = gpu_land(E, f);
+    if (f.block) {
+      std::lock_guard<std::mutex> lk(E->cmu);
+      E->nflight--;
+    }
+  }
+  jobs_finish(E, jobs, nj, st, gpu);
+}
+
+void worker_main(Engine *E) {
   engine_thread_pin(E);
+  t_worker = true;
   std::unique_lock<std::mutex> lk(E->mu);
   for (;;) {
     if (E->stop) return;
@@ -1321,7 +1564,8 @@ void worker_main(Engine *E, uint32_t w) {
         }
       }
     }
-    if (E->runq.empty() || g_hold.load(std::memory_order_relaxed)) {
+    // (held: no new task starts; a completed launch's finish still runs)
+    if (E->runq.empty() || (g_hold.load(std::memory_order_relaxed) && !E->runq.front().fin)) {
       if (next) E->cv.wait_until(lk, mono_tp(next));
       else E->cv.wait(lk);
       continue;
@@ -1329,9 +1573,130 @@ void worker_main(Engine *E, uint32_t w) {
     const Task t = E->runq.front();
     E->runq.pop_front();
     lk.unlock();
-    run_task(E, w, t);
+    run_task(E, t);
     lk.lock();
   }
+}
+
+// Starts one launch over pending batches, the first pending batch's scheme
+// and direction and every other pending batch that may join it (up to
+// kMaxGroup batches and kGroupDgrams datagrams).  Caller holds cmu, with a
+// slot counted in nflight for it; returns with cmu held.  The new flight is
+// queued for the completer; a refused launch's batches run on the CPU path
+// here, and its slot is given back.
+void launch_pending(Engine *E, std::unique_lock<std::mutex> &lk) {
+  Flight *f = new (std::nothrow) Flight();
+  if (!f) {
+    E->nflight--;  // (the batches stay pending for the next completion)
+    return;
+  }
+  const int kind = E->pending[0].pc->kind, dir = E->pending[0].dir;
+  uint32_t nd = 0;
+  // whole tasks only (a task's batches are consecutive, its last one ends
+  // it): a task split over two launches could finish out of order
+  std::vector<Job> &P = E->pending;
+  size_t w = 0;
+  for (size_t i = 0; i < P.size();) {
+    size_t e = i + 1;
+    while (e < P.size() && !P[e - 1].end_task) e++;
+    uint32_t n = 0;
+    for (size_t q = i; q < e; q++) n += P[q].batch().n;
+    if (P[i].pc->kind == kind && P[i].dir == dir && f->nj + (e - i) <= kMaxGroup &&
+        (f->nj == 0 || nd + n <= kGroupDgrams)) {
+      for (size_t q = i; q < e; q++) f->jobs[f->nj++] = P[q];
+      nd += n;
+    } else {
+      for (size_t q = i; q < e; q++) P[w++] = P[q];
+    }
+    i = e;
+  }
+  P.resize(w);
+  f->block = true;
+  lk.unlock();
+  int st = gpu_launch(E, *f);
+  lk.lock();
+  if (st == SQ_OK) {
+    try {
+      E->flights.push_back(f);
+      E->async_launches.fetch_add(1, std::memory_order_relaxed);
+      return;
+    } catch (...) {
+    }
+    lk.unlock();
+    st = gpu_land(E, *f);
+    lk.lock();
+  }
+  E->nflight--;
+  lk.unlock();
+  jobs_finish(E, f->jobs, f->nj, st, true);
+  delete f;
+  lk.lock();
+}
+
+// The completer (engines of a context): takes the launches queued by
+// run_task and launch_pending in launch order and lands each (gpu_land:
+// asleep through most of the kernel, then short polls), then finishes its
+// batches -- pump-mode ones here (queue hand-offs: the batch to the taker
+// or the readers, the task requeued with a wake-up), socket-mode ones on a
+// worker (the sendmmsg, or the next recvmmsg), queued at the front of the
+// run queue -- and launches the batches that waited for the slot.  On stop
+// it lands what is in flight and runs what is pending on the CPU path.
+void completer_main(Engine *E) {
+  engine_thread_pin(E);
+  std::unique_lock<std::mutex> lk(E->cmu);
+  for (;;) {
+    E->cv_flight.wait(lk, [E] { return E->cstop || !E->flights.empty(); });
+    if (E->flights.empty()) break;
+    Flight *f = E->flights.front();
+    E->flights.pop_front();
+    lk.unlock();
+    const int st = gpu_land(E, *f);
+    // a socket-mode pconn's batches (consecutive: one task's) go back to a
+    // worker together, in order, as one finish (their sends use the pconn's
+    // scratch, one batch after another)
+    uint32_t keep = 0;  // pump-mode jobs, finished here
+    for (uint32_t k = 0; k < f->nj;) {
+      uint32_t e = k + 1;
+      while (e < f->nj && f->jobs[e].pc == f->jobs[k].pc && f->jobs[e].dir == f->jobs[k].dir) e++;
+      for (uint32_t q = k; q < e; q++) {
+        f->jobs[q].failed = st != SQ_OK;
+        f->jobs[q].st = st;
+      }
+      Flight *h = f->jobs[k].pc->socket_mode() ? new (std::nothrow) Flight() : nullptr;
+      bool queued = false;
+      if (h) {
+        for (uint32_t q = k; q < e; q++) h->jobs[h->nj++] = f->jobs[q];
+        std::lock_guard<std::mutex> g(E->mu);
+        if (!E->stop) {
+          try {
+            E->runq.push_front(Task{h->jobs[0].pc, h->jobs[0].dir, h});
+            queued = true;
+          } catch (...) {
+          }
+        }
+      }
+      if (queued) {
+        E->cv.notify_one();
+      } else {
+        delete h;
+        for (uint32_t q = k; q < e; q++) f->jobs[keep++] = f->jobs[q];
+      }
+      k = e;
+    }
+    jobs_finish(E, f->jobs, keep, st, true);
+    delete f;
+    lk.lock();
+    E->nflight--;
+    while (!E->pending.empty() && E->nflight < E->flight_cap && !E->cstop) {
+      E->nflight++;
+      launch_pending(E, lk);
+    }
+  }
+  // stopped: what still waits for a slot runs on the CPU path
+  std::vector<Job> rest;
+  rest.swap(E->pending);
+  lk.unlock();
+  for (Job &j : rest) jobs_finish(E, &j, 1, kRefused, false);
 }
 
 void poller_main(Engine *E) {
@@ -1356,13 +1721,18 @@ void engine_end(Engine *E) {
     std::lock_guard<std::mutex> lk(E->mu);
     E->stop = true;
   }
+  {
+    std::lock_guard<std::mutex> lk(E->cmu);
+    E->cstop = true;
+  }
   E->cv.notify_all();
+  E->cv_flight.notify_all();
+  E->cv_stream.notify_all();
   const uint64_t one = 1;
   (void)!write(E->wake, &one, sizeof one);
   for (auto &t : E->threads) t.join();
   for (auto &m : E->mkr) m.reset();  // (fenced on the streams: before they go)
-  for (void *s : E->streams)
-    if (s) sq_ctx_stream_destroy(E->ctx, s);
+  for (void *s : E->streams) sq_ctx_stream_destroy(E->ctx, s);
   for (auto &kv : E->free_blocks)
     for (Block *b : kv.second) block_free_mem(E, b);
   close(E->wake);
@@ -1420,6 +1790,11 @@ int sqobfs_engine_info_get(sqobfs_ctx *ctx, sqobfs_engine_info *out) {
   out->launches = E->launches.load();
   out->group_launches = E->group_launches.load();
   out->group_batches = E->group_batches.load();
+  out->async_launches = E->async_launches.load();
+  {
+    std::lock_guard<std::mutex> cl(E->cmu);
+    out->streams = (uint32_t)E->streams.size();
+  }
   return SQ_OK;
 }
 
@@ -1655,9 +2030,11 @@ void sqobfs_pconn_close(sqobfs_pconn *pc) {
   // its launches are all complete: the keyring need not fence the engine's
   // streams for them (sqobfs_keyring_destroy)
   {
+    std::lock_guard<std::mutex> lk(E->cmu);
+    for (void *s : E->streams) sq_keyring_forget(pc->kr, s);
+  }
+  {
     std::lock_guard<std::mutex> lk(E->mu);
-    for (void *s : E->streams)
-      if (s) sq_keyring_forget(pc->kr, s);
     E->pconns--;
   }
   for (auto *v : {&pc->tb, &pc->rb})

@@ -429,11 +429,13 @@ class EngineInfo(ctypes.Structure):
                 ("load_permille", ctypes.c_uint32), ("loaded", ctypes.c_uint32),
                 ("gpu_host_ns", ctypes.c_uint32), ("cpus", ctypes.c_uint32),
                 ("group_max", ctypes.c_uint32), ("launches", ctypes.c_uint64),
-                ("group_launches", ctypes.c_uint64), ("group_batches", ctypes.c_uint64)]
+                ("group_launches", ctypes.c_uint64), ("group_batches", ctypes.c_uint64),
+                ("async_launches", ctypes.c_uint64), ("streams", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
 
 
 def engine_set_group(ctx: Context | None, max_batches: int) -> None:
-    """Most batches of several pconns one engine launch takes (0 = 8, 1 = no
+    """Most batches of several pconns one engine launch takes (0 = 32, 1 = no
     coalescing; sqobfs_engine_set_group)."""
     _check(lib().sqobfs_engine_set_group(ctx.handle if ctx else None, max_batches),
            "sqobfs_engine_set_group")

@@ -32,7 +32,8 @@
  * a keyring per conn as the Go adapters make), K writers together offering
  * 0.5, 1, 2 GiB/s and unpaced, K takers; the defaults (coalesced launches),
  * coalescing off (sqobfs_engine_set_group 1) and every batch on the CPU
- * path: CPU seconds per GiB, launches and batches per launch.
+ * path: CPU seconds per GiB, launches and batches per launch
+ * (`lat_bench hops K secs reps unpaced`: the unpaced rate only).
  *
  * `lat_bench tput [runs]`: the default-routing GSO / GRO throughput run
  * (200,000 datagrams A -> B) repeated, each with its process CPU time,
@@ -577,6 +578,8 @@ static void hops_run(sqobfs_ctx *c, const char *name, int K, uint32_t group, uin
     sqobfs_pconn_opts o;
     memset(&o, 0, sizeof o);
     o.cpu_max = cpu_max;
+    /* (dev sweep: transmit batches per conn) */
+    if (getenv("HOPS_TXB")) o.tx_batches = (uint32_t)atoi(getenv("HOPS_TXB"));
     memset(&h[k], 0, sizeof h[k]);
     CHECK(sqobfs_pconn_open(c, kr[k], -1, &o, &h[k].pc));
     h[k].rate = gib_s > 0 ? gib_s * (double)(1 << 30) / L / K : 0;
@@ -631,14 +634,14 @@ static void hops_run(sqobfs_ctx *c, const char *name, int K, uint32_t group, uin
   }
 }
 
-static int hops_main(int K, double secs, int reps) {
+static int hops_main(int K, double secs, int reps, int unpaced_only) {
   if (K < 1 || K > 32) K = 8;
   sqobfs_ctx *ctx;
   CHECK(sqobfs_open(0, &ctx));
   static const double rates[] = {0.5, 1.0, 2.0, 0};
   printf("{\"hops\": [");
   int first = 1;
-  for (int ri = 0; ri < 4; ri++)
+  for (int ri = unpaced_only ? 3 : 0; ri < 4; ri++)
     for (int rp = 0; rp < reps; rp++)
       for (int m = 0; m < 3; m++) {
         if (!first) printf(", ");
@@ -655,7 +658,7 @@ static int hops_main(int K, double secs, int reps) {
 int main(int argc, char **argv) {
   if (argc > 1 && !strcmp(argv[1], "hops"))
     return hops_main(argc > 2 ? atoi(argv[2]) : 8, argc > 3 ? atof(argv[3]) : 1.5,
-                     argc > 4 ? atoi(argv[4]) : 1);
+                     argc > 4 ? atoi(argv[4]) : 1, argc > 5 && !strcmp(argv[5], "unpaced"));
   if (argc > 1 && !strcmp(argv[1], "load"))
     return load_main(argc > 2 ? atof(argv[2]) : 1.5, argc > 3 ? atoi(argv[3]) : 1);
   if (argc > 1 && !strcmp(argv[1], "tput"))

@@ -116,7 +116,7 @@ void sq_keyring_hot(const sqobfs_keyring *, uint32_t *hot_m, uint32_t *hot_iv) {
   *hot_iv = 0;
 }
 int sq_keyring_from_entries(sqobfs_ctx *ctx, int kind, const sq::PskEntry *e, uint32_t count,
-                            uint32_t, uint32_t, sqobfs_keyring **out) {
+                            uint32_t, uint32_t, void *, sqobfs_keyring **out) {
   *out = nullptr;
   if (!ctx || !e || !count) return SQ_EINVAL;
   sqobfs_keyring *kr = new (std::nothrow) sqobfs_keyring();

@@ -54,9 +54,10 @@ int main(void){printf("%zu %zu %zu %zu %zu\n", sizeof(sqobfs_batch),
 
 def test_engine_info_layout_matches_header():
     """ctypes mirror of sqobfs_engine_info has the C layout (round 5 grew it:
-    load routing, affinity and the coalesced-launch counters)."""
+    load routing, affinity and the coalesced-launch counters; round 6, ABI 6:
+    the completer's counters)."""
     fields = ["pool_bytes", "route_bytes", "cpus", "group_max", "launches", "group_launches",
-              "group_batches"]
+              "group_batches", "async_launches", "streams"]
     prog = ('#include <stdio.h>\n#include <stddef.h>\n#include "sqobfs.h"\n'
             'int main(void){printf("%zu' + ' %zu' * len(fields) + '\\n", sizeof(sqobfs_engine_info)'
             + "".join(f", offsetof(sqobfs_engine_info,{f})" for f in fields) + ");return 0;}")
@@ -77,7 +78,7 @@ def test_engine_set_group_bounds():
 
 def test_abi_version_and_strerror():
     L = sqobfs.lib()
-    assert L.sqobfs_abi_version() == 5
+    assert L.sqobfs_abi_version() == 6
     for st in (0, -1, -2, -3, -4, -5, -6, -7, -8):
         assert sqobfs.strerror(st) != "unknown status"
 

@@ -54,6 +54,29 @@ def test_bench_two_ranks(config, packets, scaling, launcher):
     assert abs(d["value"] - total / (d["ms_per_step"] * d["steps"] * 1e-3) / 2**30) \
         <= 0.01 * d["value"]  # ms_per_step is rounded to 0.1 us
     assert d["config"]["packets_per_gpu"] == per_rank
+    # the host-staged batch on both ranks at once, after the timed region
+    e = d["e2e"]
+    assert len(e["per_rank"]) == 2 and all(r > 0 for r in e["per_rank"]) and e["out_len_ok"]
+    payload = 2 * e["packets_per_rank"] * e["payload_bytes"] * e["reps"]
+    assert abs(e["aggregate_gib_s"] - payload / e["wall_s"] / 2**30) <= 0.01 * e["aggregate_gib_s"]
+    # the max-over-ranks wall: the aggregate is at most the ranks' own rates summed
+    assert e["aggregate_gib_s"] <= sum(e["per_rank"]) * 1.01
+
+
+def test_bench_one_rank_carries_e2e_and_no_e2e_skips_it():
+    """The default N = 1 line carries the host-staged e2e key (one rank);
+    --no-e2e leaves it out."""
+    base = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "3", "--warmup", "1",
+            "--warmup-s", "0", "--no-cpu-baseline", "--packets", "65536"]
+    for extra, want in (([], True), (["--no-e2e"], False)):
+        r = subprocess.run(base + extra, cwd=REPO, capture_output=True, text=True, timeout=110)
+        assert r.returncode == 0, r.stderr[-3000:]
+        d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+        assert ("e2e" in d) == want
+        if want:
+            e = d["e2e"]
+            assert len(e["per_rank"]) == 1 and e["out_len_ok"]
+            assert abs(e["aggregate_gib_s"] - e["per_rank"][0]) <= 0.01 * e["aggregate_gib_s"]
 
 
 def test_bare_launch_stops_ranks_on_failure():
