@@ -1,0 +1,39 @@
+"""Dev (container): ablation builds of the AES-128-GCM kernel -- each drops
+one piece of the cooperative payload pass (the output is wrong; only the
+time matters), so the GPU run of scripts/dev/gcm_ablate_run.sh attributes the
+kernel's time: the Shoup multiply by H^m per chunk, the GHASH multiply per
+block, the AES keystream per block pair.  Builds
+build/ablate/<name>/libsqobfs.so from the in-tree objects plus a modified
+copy of sq_quic_gcm.hip (nothing here ships; SQOBFS_LIB selects a build).
+usage: python3 scripts/dev/gcm_ablate.py"""
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+PKG = os.path.join(REPO, "sing-quic_amd")
+SRC = os.path.join(PKG, "csrc", "sq_quic_gcm.hip")
+VARIANTS = {
+    "base": [],
+    "no_shoup": [("      if (m) KB.mul_pow(yb, m);", "")],
+    "no_ghash": [("      ghash_absorb(y, g);\n      gmul_pos<KM == 1>(y, K.hpos);", "      ghash_absorb(y, g);")],
+    "no_aes": [("    aes_encrypt_n<KM, 2>(K.rk, tT, tcol, s2);", "")],
+}
+objs = [os.path.join(PKG, "build", "obj", f + ".o")
+        for f in ("sq_kernels", "sq_quic", "sq_api", "packet_conn", "udp_batch", "pconn", "sq_cpu")]
+src = open(SRC).read()
+for name, subs in VARIANTS.items():
+    d = os.path.join(REPO, "build", "ablate", name)
+    os.makedirs(d, exist_ok=True)
+    s = src
+    for a, b in subs:
+        assert a in s, (name, a)
+        s = s.replace(a, b)
+    p = os.path.join(d, "sq_quic_gcm.hip")
+    open(p, "w").write(s)
+    flags = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-I" + os.path.join(REPO, "include"),
+             "-I" + os.path.join(PKG, "csrc"), "-I" + os.path.join(PKG, "host")]
+    subprocess.run(["/opt/rocm/bin/hipcc"] + flags + ["-c", "-o", os.path.join(d, "gcm.o"), p], check=True)
+    subprocess.run(["/opt/rocm/bin/hipcc"] + flags + ["-shared", "-o", os.path.join(d, "libsqobfs.so"),
+                    os.path.join(d, "gcm.o")] + objs + ["-lpthread"], check=True)
+    print(name, "built", flush=True)

@@ -14,6 +14,11 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 // dword-aligned 16-byte access: still one global_load_dwordx4 on gfx950
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+// byte-aligned 16-byte access: one global_load / global_store_dwordx4 as
+// well (the HSA runtime runs gfx950 in unaligned mode); only for bytes that
+// are all inside the buffer (a read past its end may cross into an
+// unmapped page)
+typedef uint32_t u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
 
 // Global-address-space accessors.  Packet addresses are computed as integers;
 // a plain cast would give FLAT pointers, whose loads/stores count in both

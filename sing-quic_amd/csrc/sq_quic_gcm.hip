@@ -262,12 +262,14 @@ __device__ __forceinline__ void gmul(uint32_t (&x)[4], const uint32_t *tab, uint
 // pos[j][nibble j of x] over the 32 nibbles (from the low end of the 128-bit
 // integer) -- no shifts, no reduction steps.  The lookups do not depend on
 // each other: they are issued 4 at a time back to back (16 VGPRs; 8 at a
-// time made the kernels spill), then folded with three-input XORs; with pos at LDS address 0 an
-// address is the nibble times 16 plus the word's base, and the position an
-// immediate offset.  (Round 5's loop issued one read at a time and waited
-// for it: 32 LDS round trips in a row per multiply.)
+// time made the kernels spill), then folded with three-input XORs.  In LDS
+// (pos at a compile-time address below 56 KiB) the loop is unrolled: an
+// address is the nibble times 16, the position an immediate offset; the
+// rolled form (global tables) adds the word's base to every address.
+// (Round 5's loop issued one read at a time and waited for it: 32 LDS round
+// trips in a row per multiply.)
 template <bool GLOBAL>
-__device__ __forceinline__ void gmul_pos(uint32_t (&x)[4], const uint32_t *pos) {
+__device__ __forceinline__ void gmul_pos_rolled(uint32_t (&x)[4], const uint32_t *pos) {
   uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
   uint32_t w = x[3], w2 = x[2], w1 = x[1], w0 = x[0];
   const char *base = (const char *)pos;
@@ -303,6 +305,43 @@ __device__ __forceinline__ void gmul_pos(uint32_t (&x)[4], const uint32_t *pos) 
   x[0] = z0; x[1] = z1; x[2] = z2; x[3] = z3;
 }
 
+template <bool GLOBAL>
+__device__ __forceinline__ void gmul_pos(uint32_t (&x)[4], const uint32_t *pos) {
+  if (GLOBAL) {  // (per-packet keys: the tables in global memory, 64-bit addresses)
+    gmul_pos_rolled<true>(x, pos);
+    return;
+  }
+  uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
+  const char *base = (const char *)pos;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    uint32_t w = x[3 - i];
+#pragma unroll
+    for (int h = 0; h < 8; h += 4) {
+      // (an empty asm the next reads' addresses depend on, after the last
+      // XORs: keeps the unrolled reads from being hoisted into 128 VGPRs)
+      asm volatile("" : "+v"(w), "+v"(z0), "+v"(z1), "+v"(z2), "+v"(z3));
+      const uint32_t w4 = w << 4;
+      u32x4 e[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int jj = h + j;
+        const uint32_t off = (((jj & 1) ? w : w4) >> (8 * (jj >> 1))) & 0xF0u;
+        const char *p = base + 256 * (8 * i + jj) + off;
+        e[j] = *(const u32x4 *)p;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j += 2) {
+        z0 = xor3(z0, e[j].x, e[j + 1].x);
+        z1 = xor3(z1, e[j].y, e[j + 1].y);
+        z2 = xor3(z2, e[j].z, e[j + 1].z);
+        z3 = xor3(z3, e[j].w, e[j + 1].w);
+      }
+    }
+  }
+  x[0] = z0; x[1] = z1; x[2] = z2; x[3] = z3;
+}
+
 // y ^= 16 bytes held as little-endian words
 __device__ __forceinline__ void ghash_absorb(uint32_t (&y)[4], const uint32_t (&m)[4]) {
 #pragma unroll
@@ -324,13 +363,20 @@ struct GKey {
 // ---------------------------------------------------------------- payload
 
 // Payload bytes [0, nv) at src -> dst: CTR blocks ctr0, ctr0 + 1, ...; y
-// absorbs every ciphertext block (y = (y ^ C) * H).  Streaming realigner
-// (one aligned 16-byte load and store per block whatever the alignments,
-// one block of read-ahead), as payload_pass in sq_quic.hip.  In place
-// (src == dst) works.  first32 = ciphertext bytes 0..31 (zero past nv).
-// OB (fused Salamander layer): output (seal) or input (open) bytes are also
-// XORed with the packet's Salamander key; okr = the key rotated to the first
-// byte at src / dst (16-byte block j uses half j & 1).
+// absorbs every ciphertext block (y = (y ^ C) * H).  Full blocks move with
+// one unaligned 16-byte load and store each (global accesses work at any
+// byte address on gfx950 under the HSA runtime's unaligned mode: one
+// global_load / global_store_dwordx4, no realignment funnels -- round 5's
+// aligned loads and two barrel shifts per block cost ~45 VALU ops of the
+// ~200 outside AES and GHASH); the last, partial block reads only the
+// aligned blocks that hold valid bytes (load16: an unaligned read past the
+// payload could cross into an unmapped page) and writes exactly its bytes
+// (store16).  Blocks are loaded one pair ahead of the stores, so in place,
+// or with the output a few bytes after the input (the fused layer's salt),
+// a store never overwrites unread input.  first32 = ciphertext bytes 0..31
+// (zero past nv).  OB (fused Salamander layer): output (seal) or input
+// (open) bytes are also XORed with the packet's Salamander key; okr = the
+// key rotated to the first byte at src / dst (block j uses half j & 1).
 template <bool OPEN, int KM, bool OB>
 __device__ __forceinline__ void gcm_run(const GKey<KM> &K, const uint32_t *tT, uint32_t tcol,
                                         const uint32_t (&nonce)[3], uint32_t ctr0, uint64_t src,
@@ -339,81 +385,62 @@ __device__ __forceinline__ void gcm_run(const GKey<KM> &K, const uint32_t *tT, u
 #pragma unroll
   for (int j = 0; j < 8; j++) first32[j] = 0u;
   if (nv == 0) return;
-  const uint32_t ib = (uint32_t)(src & 15), oa = (uint32_t)(dst & 15);
-  const uint64_t S0 = src - ib, D0 = dst - oa;
-  const uint64_t last = (src + nv - 1) & ~15ull;
   auto load_blk = [&](uint32_t i, uint32_t (&v)[4]) {
-    const uint64_t A = S0 + 16ull * i;
-    const u32x4 x = gld<u32x4>(A < last ? A : last);
-    const bool ok = A <= last;
-    v[0] = ok ? x.x : 0u; v[1] = ok ? x.y : 0u; v[2] = ok ? x.z : 0u; v[3] = ok ? x.w : 0u;
+    const uint32_t o = 16 * i;
+    if (o + 16 <= nv) {
+      const u32x4 x = gld<u32x4_a1>(src + o);
+      v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+    } else if (o < nv) {
+      load16(src + o, src + nv, v);
+    } else {
+#pragma unroll
+      for (int w = 0; w < 4; w++) v[w] = 0u;
+    }
   };
+  const uint32_t nchunk = (nv + 15) / 16;
+  uint32_t in[2][4];
+  load_blk(0, in[0]);
+  load_blk(1, in[1]);
   // two counter blocks per iteration: their AES rounds interleave, so each
   // round has 32 independent T-table reads in flight instead of 16
-  uint32_t A[4], Bq[4], C[4], prev_c[4] = {0u, 0u, 0u, 0u};
-  load_blk(0, A);
-  load_blk(1, Bq);
-  load_blk(2, C);
-  const uint32_t nchunk = (nv + 15) / 16;
-  // one output block: GHASH, header-protection sample, realigned store
-  auto finish = [&](uint32_t j, const uint32_t (&in)[4], const uint32_t (&c0)[4]) {
-    const uint32_t(&g)[4] = OPEN ? in : c0;
-    ghash_absorb(y, g);
-    gmul_pos<KM == 1>(y, K.hpos);
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-      first32[w] = bsel(j == 0, g[w], first32[w]);
-      first32[4 + w] = bsel(j == 1, g[w], first32[4 + w]);
-    }
-    uint32_t c[4];  // what goes on the wire
-    const int nbj = (int)nv - 16 * (int)j;
-#pragma unroll
-    for (int w = 0; w < 4; w++)
-      c[w] = (OB && !OPEN) ? c0[w] ^ (bsel(j & 1, okr[4 + w], okr[w]) & range_mask(0, nbj, w))
-                           : c0[w];
-    uint32_t blk[4];
-    funnel(prev_c, c, 16 - oa, blk);
-    const uint32_t lo = j == 0 ? oa : 0u;
-    const uint32_t hi = oa + nv - 16 * j < 16 ? oa + nv - 16 * j : 16u;
-    if (lo == 0 && hi == 16) gst<u32x4>(D0 + 16ull * j, u32x4{blk[0], blk[1], blk[2], blk[3]});
-    else store_partial(D0 + 16ull * j, blk, lo, hi);
-#pragma unroll
-    for (int w = 0; w < 4; w++) prev_c[w] = c[w];
-  };
   for (uint32_t j = 0; j < nchunk; j += 2) {
-    uint32_t D[4], E[4];
-    load_blk(j + 3, D);  // in flight during this pair's AES and GHASH
-    load_blk(j + 4, E);
-    uint32_t in[2][4], c[2][4];
+    uint32_t nx[2][4];
+    load_blk(j + 2, nx[0]);  // (in flight during this pair's AES and GHASH)
+    load_blk(j + 3, nx[1]);
     uint32_t s2[2][4] = {{nonce[0], nonce[1], nonce[2], __builtin_bswap32(ctr0 + j)},
                          {nonce[0], nonce[1], nonce[2], __builtin_bswap32(ctr0 + j + 1)}};
-    funnel(A, Bq, ib, in[0]);
-    funnel(Bq, C, ib, in[1]);
     aes_encrypt_n<KM, 2>(K.rk, tT, tcol, s2);
 #pragma unroll
     for (int q = 0; q < 2; q++) {
-      const int nb = (int)nv - 16 * (int)(j + q);  // valid bytes (may be <= 0)
+      if (q == 1 && j + 1 >= nchunk) break;
+      const int nb = (int)nv - 16 * (int)(j + q);  // valid bytes, >= 1
+      uint32_t x[4], c[4], m[4];
 #pragma unroll
       for (int w = 0; w < 4; w++) {
-        in[q][w] &= range_mask(0, nb, w);
-        if (OB && OPEN) in[q][w] ^= okr[4 * q + w] & range_mask(0, nb, w);  // j is even
-        c[q][w] = (in[q][w] ^ s2[q][w]) & range_mask(0, nb, w);
+        m[w] = nb >= 16 ? 0xFFFFFFFFu : range_mask(0, nb, w);
+        x[w] = in[q][w];
+        if (OB && OPEN) x[w] ^= okr[4 * q + w] & m[w];  // (j is even)
+        c[w] = (x[w] ^ s2[q][w]) & m[w];
       }
+      const uint32_t(&g)[4] = OPEN ? x : c;
+      ghash_absorb(y, g);
+      gmul_pos<KM == 1>(y, K.hpos);
+      if (j == 0) {
+#pragma unroll
+        for (int w = 0; w < 4; w++) first32[4 * q + w] = g[w];
+      }
+      uint32_t o[4];  // what goes to dst
+#pragma unroll
+      for (int w = 0; w < 4; w++) o[w] = (OB && !OPEN) ? c[w] ^ (okr[4 * q + w] & m[w]) : c[w];
+      const uint64_t D = dst + 16ull * (j + q);
+      if (nb >= 16) gst<u32x4_a1>(D, u32x4_a1{o[0], o[1], o[2], o[3]});
+      else store16(D, o, (uint32_t)nb);
     }
 #pragma unroll
     for (int w = 0; w < 4; w++) {
-      A[w] = C[w];
-      Bq[w] = D[w];
-      C[w] = E[w];
+      in[0][w] = nx[0][w];
+      in[1][w] = nx[1][w];
     }
-    finish(j, in[0], c[0]);
-    if (j + 1 < nchunk) finish(j + 1, in[1], c[1]);
-  }
-  if (oa + nv > 16 * nchunk) {  // the last block's tail spills into one more output block
-    const uint32_t zero[4] = {0u, 0u, 0u, 0u};
-    uint32_t blk[4];
-    funnel(prev_c, zero, 16 - oa, blk);
-    store_partial(D0 + 16ull * nchunk, blk, 0, oa + nv - 16 * nchunk);
   }
 }
 
