@@ -123,6 +123,9 @@ constexpr uint32_t kMaxFlights = 32;
 // routed to the GPU wait, prepared, and the next completion launches all of
 // them together -- the natural batching of the GPU route
 constexpr uint32_t kDefFlightCap = 1;
+// datagrams waiting for the launch slot past which a bulk batch overflows to
+// the CPU path (gpu_saturated)
+constexpr uint32_t kDefPendMax = 2048;
 
 // sqobfs_debug_engine_fail, sqobfs_debug_pool_fail, sqobfs_debug_engine_hold
 std::atomic<int> g_fail_count{0};
@@ -293,6 +296,8 @@ struct Engine {
   std::vector<void *> streams, sfree;
   std::deque<Flight *> flights;
   std::vector<Job> pending;  // routed to the GPU while flight_cap launches fly
+  uint32_t pending_dgrams = 0;
+  uint32_t pend_max = kDefPendMax;  // past it, bulk batches overflow to the CPU path
   uint32_t nflight = 0;     // non-polling launches started and not yet landed
   uint32_t flight_cap = kDefFlightCap;
   bool cstop = false;
@@ -416,6 +421,8 @@ Engine *engine_get(sqobfs_ctx *ctx, int *status) {
   if (gc != g_group_cfg.end()) E->group_max = gc->second;
   if (const char *fc = getenv("SQ_ENGINE_FLIGHTS"))  // (dev: the cap sweep)
     E->flight_cap = std::max(1, std::min(atoi(fc), (int)kMaxFlights));
+  if (const char *pm = getenv("SQ_ENGINE_PENDMAX"))  // (dev: the overflow sweep; 0 = none)
+    E->pend_max = (uint32_t)atoi(pm);
   E->wake = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
   E->epfd = epoll_create1(EPOLL_CLOEXEC);
   epoll_event ev{};
@@ -1426,6 +1433,13 @@ uint32_t grab_tasks(Engine *E, int dir, int kind, uint32_t room, Task *out, uint
 // for.  Batches are not gathered to make a launch that none of them would
 // make alone: gathered groups of small batches under paced load launched
 // 4-13K times in 3 s for no CPU saved ("Coalesced launches").
+// The non-polling GPU route is saturated: every launch slot flies and
+// batches of pend_max datagrams or more already wait for the next one.
+bool gpu_saturated(Engine *E) {
+  std::lock_guard<std::mutex> lk(E->cmu);
+  return E->pend_max && E->nflight >= E->flight_cap && E->pending_dgrams >= E->pend_max;
+}
+
 // Sets the outcome of the jobs' transform -- st: SQ_OK, a failed kernel's
 // error, or kRefused (nothing ran: redone on the CPU path; gpu: a launch was
 // tried) -- and runs their finish steps.
@@ -1479,7 +1493,11 @@ void run_task(Engine *E, const Task &t) {
   Job *jobs = f.jobs;
   if (!task_prepare(E, t, jobs[0])) return;
   bool bulk = false;
-  const bool gpu = route_gpu(E, jobs[0], &bulk);
+  bool gpu = route_gpu(E, jobs[0], &bulk);
+  // the GPU route saturated -- a launch in flight and a full launch's worth
+  // of batches already waiting for it -- a bulk batch runs on the CPU path
+  // instead of waiting: the host's cores add to the GPU's rate
+  if (gpu && bulk && gpu_saturated(E)) gpu = false;
   uint32_t nj = 1, nd = jobs[0].batch().n;
   // a launched task takes its other queued batches along (finished in
   // order, the last one ending the task): a conn whose writer filled
@@ -1519,6 +1537,7 @@ void run_task(Engine *E, const Task &t) {
       if (!E->cstop && E->nflight >= E->flight_cap) {
         try {
           E->pending.insert(E->pending.end(), jobs, jobs + nj);
+          E->pending_dgrams += nd;
           return;
         } catch (...) {  // (no memory: launch it now, over the cap)
         }
@@ -1611,6 +1630,7 @@ void launch_pending(Engine *E, std::unique_lock<std::mutex> &lk) {
     i = e;
   }
   P.resize(w);
+  E->pending_dgrams -= std::min(E->pending_dgrams, nd);
   f->block = true;
   lk.unlock();
   int st = gpu_launch(E, *f);
@@ -1651,6 +1671,15 @@ void completer_main(Engine *E) {
     E->flights.pop_front();
     lk.unlock();
     const int st = gpu_land(E, *f);
+    // the batches that waited for the slot launch first, so the GPU works
+    // on them while this thread finishes the landed ones
+    lk.lock();
+    E->nflight--;
+    while (!E->pending.empty() && E->nflight < E->flight_cap && !E->cstop) {
+      E->nflight++;
+      launch_pending(E, lk);
+    }
+    lk.unlock();
     // a socket-mode pconn's batches (consecutive: one task's) go back to a
     // worker together, in order, as one finish (their sends use the pconn's
     // scratch, one batch after another)
@@ -1686,7 +1715,8 @@ void completer_main(Engine *E) {
     jobs_finish(E, f->jobs, keep, st, true);
     delete f;
     lk.lock();
-    E->nflight--;
+    // (batches that became pending while this thread finished: the next
+    // completion launches them, or now if the slot is free)
     while (!E->pending.empty() && E->nflight < E->flight_cap && !E->cstop) {
       E->nflight++;
       launch_pending(E, lk);
@@ -1695,6 +1725,7 @@ void completer_main(Engine *E) {
   // stopped: what still waits for a slot runs on the CPU path
   std::vector<Job> rest;
   rest.swap(E->pending);
+  E->pending_dgrams = 0;
   lk.unlock();
   for (Job &j : rest) jobs_finish(E, &j, 1, kRefused, false);
 }
