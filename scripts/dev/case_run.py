@@ -3,7 +3,8 @@ launched a few times in a process of its own, so that a `rocprofv3 --pmc`
 pass counts that case alone (per-dispatch counters of one batch shape).
 usage: case_run.py CASE [LAUNCHES]
 CASE: F16 (1M x 1350 B), F4M (4M x 1350), FB16 (2,372,000 x 1350),
-      P28 (1M x 758), C28 (4M x 758), R28 (configs[3]: 4M x U[64,1452])."""
+      P28 (1M x 758), C28 (4M x 758), R28 (configs[3]: 4M x U[64,1452]),
+      F16M (configs[4] on one GPU: 16M x 1350, one PSK)."""
 import os
 import sys
 
@@ -17,7 +18,8 @@ import sqobfs  # noqa: E402
 import bench  # noqa: E402
 
 CASES = {"F16": (1 << 20, 1350), "F4M": (1 << 22, 1350), "FB16": (2372000, 1350),
-         "P28": (1 << 20, 758), "C28": (1 << 22, 758), "R28": (1 << 22, None)}
+         "P28": (1 << 20, 758), "C28": (1 << 22, 758), "R28": (1 << 22, None),
+         "F16M": (1 << 24, 1350)}
 case = sys.argv[1]
 launches = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 n, L = CASES[case]

@@ -17,7 +17,8 @@ REPO = os.path.dirname(os.path.dirname(HERE))
 import torch  # noqa: E402
 
 CASES = {"F16": (1 << 20, 1358), "F4M": (1 << 22, 1358), "FB16": (2372000, 1358),
-         "P28": (1 << 20, 766), "C28": (1 << 22, 766), "R28": (1 << 22, 766)}
+         "P28": (1 << 20, 766), "C28": (1 << 22, 766), "R28": (1 << 22, 766),
+         "F16M": (1 << 24, 1358)}
 case = sys.argv[1]
 launches = int(sys.argv[2]) if len(sys.argv) > 2 else 12
 pat = int(sys.argv[3]) if len(sys.argv) > 3 else 1

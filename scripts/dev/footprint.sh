@@ -32,9 +32,11 @@ import csv, glob, statistics, sys
 o = sys.argv[1]
 # algorithmic bytes per launch (payload in + salt + payload out); R28: mean
 B = {"F16": (1 << 20) * 2716, "F4M": (1 << 22) * 2716, "FB16": 2372000 * 2716,
-     "P28": (1 << 20) * 1532, "C28": (1 << 22) * 1532, "R28": (1 << 22) * 1532}
+     "P28": (1 << 20) * 1532, "C28": (1 << 22) * 1532, "R28": (1 << 22) * 1532,
+     "F16M": (1 << 24) * 2716}
 CB = {"F16": (1 << 20) * 1358, "F4M": (1 << 22) * 1358, "FB16": 2372000 * 1358,
-      "P28": (1 << 20) * 766, "C28": (1 << 22) * 766, "R28": (1 << 22) * 766}
+      "P28": (1 << 20) * 766, "C28": (1 << 22) * 766, "R28": (1 << 22) * 766,
+      "F16M": (1 << 24) * 1358}
 def med(d, key):
     f = glob.glob(f"{o}/{d}/**/*kernel_trace.csv", recursive=True)[0]
     x = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3

@@ -40,7 +40,7 @@ struct sqobfs_ctx {
   size_t pinned_cap = 0;
   uint8_t *dev = nullptr;
   size_t dev_cap = 0;
-  hipEvent_t ev[16] = {};  // pipeline events of sqobfs_run_host
+  hipEvent_t ev[32] = {};  // pipeline events of sqobfs_run_host (kEvents)
   // SQOBFS_FLAG_DEVICE_SALT: ChaCha20 key and the next launch sequence number
   uint32_t salt_key[8] = {};
   std::atomic<uint64_t> salt_seq{0};
@@ -55,10 +55,7 @@ struct sqobfs_ctx {
 };
 
 namespace {
-#ifndef SQ_HOSTCHUNKS
-#define SQ_HOSTCHUNKS 8
-#endif
-constexpr uint32_t kHostChunks = SQ_HOSTCHUNKS;  // sqobfs_run_host pipeline depth
+constexpr uint32_t kHostChunks = 8;  // sqobfs_run_host pipeline depth
 // test hook (sqobfs_debug_fail_chunk): the launch of that pipeline chunk
 // fails as a device error would, once
 std::atomic<int> g_fail_chunk{-1};
@@ -103,7 +100,8 @@ void tab_free(void *p) {
 }
 // live sqobfs_host_alloc blocks (sqobfs_debug_host_allocs: leak checks)
 std::atomic<int64_t> g_host_allocs{0};
-constexpr uint32_t kEvents = 16;
+constexpr uint32_t kEvents = 32;
+static_assert(sizeof(((sqobfs_ctx *)nullptr)->ev) / sizeof(hipEvent_t) == kEvents, "event ring");
 }
 
 // The streams a keyring's table was read on.  Destroying the keyring records
@@ -1424,7 +1422,14 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
   if (hb->psk_id)
     for (uint32_t i = 0; i < n; i++)
       if (hb->psk_id[i] >= kr->count) return SQ_EPSK;
-  const uint32_t nchunk = n < 4096 ? 1u : std::min<uint32_t>(kHostChunks, (n + 4095) / 4096);
+  // caller memory that is already pinned (sqobfs_host_alloc, hipHostMalloc)
+  // is copied by DMA directly; pageable memory goes through pinned staging.
+  // With both pinned there are no host-side staging copies, and twice the
+  // chunks halve the pipeline's fill and drain (the
+  // duplex ceiling)
+  const bool in_pinned = is_pinned(hb->in), out_pinned = is_pinned(hb->out);
+  const uint32_t maxc = in_pinned && out_pinned ? 2 * kHostChunks : kHostChunks;
+  const uint32_t nchunk = n < 4096 ? 1u : std::min<uint32_t>(maxc, (n + 4095) / 4096);
   std::vector<Range> rin(nchunk), rout(nchunk);
   for (uint32_t c = 0; c < nchunk; c++) {
     const uint32_t p0 = (uint32_t)((uint64_t)n * c / nchunk);
@@ -1455,9 +1460,6 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
   }
   if (in_lo > in_hi) in_lo = in_hi = 0;
   if (out_lo > out_hi) out_lo = out_hi = 0;
-  // caller memory that is already pinned (sqobfs_host_alloc, hipHostMalloc)
-  // is copied by DMA directly; pageable memory goes through pinned staging
-  const bool in_pinned = is_pinned(hb->in), out_pinned = is_pinned(hb->out);
   const bool preserve = !(hb->flags & SQOBFS_FLAG_OUT_UNINIT);
 
   // staging layout (device mirror of the host ranges; pinned copies only

@@ -25,26 +25,13 @@ typedef uint32_t u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
 // vmcnt and lgkmcnt and force the compiler to drain every outstanding store
 // before each LDS read (one full HBM round trip per loop iteration).
 #define SQ_GLOBAL __attribute__((address_space(1)))
-// SQ_EDGE_NT (timing builds): 1 = these stores nontemporal, 2 = these loads,
-// 3 = both (they carry the edge bytes of the obfuscation kernel).
-#ifndef SQ_EDGE_NT
-#define SQ_EDGE_NT 0
-#endif
 template <typename T>
 __device__ __forceinline__ T gld(uint64_t a) {
-#if SQ_EDGE_NT & 2
-  return __builtin_nontemporal_load((const SQ_GLOBAL T *)a);
-#else
   return *(const SQ_GLOBAL T *)a;
-#endif
 }
 template <typename T>
 __device__ __forceinline__ void gst(uint64_t a, T v) {
-#if SQ_EDGE_NT & 1
-  __builtin_nontemporal_store(v, (SQ_GLOBAL T *)a);
-#else
   *(SQ_GLOBAL T *)a = v;
-#endif
 }
 
 // ------------------------------------------------------------ byte helpers

@@ -11,10 +11,8 @@ constexpr int kXPlusSalt = 16;      // hysteria/xplus.go:17
 constexpr int kWave = 64;           // CDNA wavefront
 // Obfuscation kernel unit: packets per wavefront (sqobfs_set_unit_packets);
 // two more lanes hold the unit's neighbour packets.
-#ifndef SQ_PPW
-#define SQ_PPW 26
-#endif
-constexpr uint32_t kDefaultUnitPackets = SQ_PPW;
+
+constexpr uint32_t kDefaultUnitPackets = 26;
 constexpr uint32_t kMaxUnitPackets = 62;
 // Sized by bytes when the batch's lengths are known (sqobfs_unit_packets_for):
 // about this many payload bytes per wavefront (~21.7 KB

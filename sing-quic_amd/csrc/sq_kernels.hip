@@ -53,44 +53,32 @@
 
 namespace sq {
 
-// Streaming policy of the bulk loads / stores (SQ_NT bit 0: loads, bit 1:
+// Streaming policy of the bulk loads / stores (bit 0: loads, bit 1:
 // stores).  Payload bytes are touched exactly once, so nontemporal (`nt`)
 // accesses keep them from displacing useful L2 lines.
-#ifndef SQ_NT
-#define SQ_NT 3
-#endif
+constexpr int kNt = 3;
 // Blocks per lane per step (double-buffered: U..2U KiB of loads in flight).
-#ifndef SQ_U
-#define SQ_U 4
-#endif
+constexpr int kU = 4;
 // Wavefronts per workgroup (see kWavesPerGroup).
-#ifndef SQ_WPB
-#define SQ_WPB 2
-#endif
-// 1: the first packet of a unit gives the blocks it owns in the 64-byte line
+constexpr int kWpb = 2;
+// The first packet of a unit gives the blocks it owns in the 64-byte line
 // its output starts in to the previous unit's wave (which holds it as its
 // look-ahead lane), so no output line is written by two waves.
-#ifndef SQ_DONATE
-#define SQ_DONATE 1
-#endif
-// Stream alignment (map path): the flat space starts (d_lo / 16) mod 2^SQ_ALIGN
-// slots in, so for back-to-back outputs every 1 KiB wave instruction covers
-// whole 2^(SQ_ALIGN+4)-byte lines (0: off; 3: 128-byte L2 lines).
-#ifndef SQ_ALIGN
-#define SQ_ALIGN 3
-#endif
+constexpr bool kDonate = true;
+// Stream alignment (map path): the flat space starts (d_lo / 16) mod
+// 2^kAlign slots in, so for back-to-back outputs every 1 KiB wave
+// instruction covers whole 2^(kAlign+4)-byte lines (3: 128-byte L2 lines).
+constexpr int kAlign = 3;
 // Flat blocks a unit's block map covers (its role bytes live in LDS).
-#ifndef SQ_MAPBLK
-#define SQ_MAPBLK 4096
-#endif
-// 1: multi-PSK kernels load each lane's keyring entry (chaining value and
+constexpr uint32_t kMapBlk = 4096;
+// Multi-PSK kernels load each lane's keyring entry (chaining value and
 // first message block) right after the descriptor, so the gather overlaps
 // the plan step (192 VGPRs: 2 waves per SIMD, still 2-3 % faster on the
-// 256-PSK batch in-process, profiles/r03/ab); 0: loaded by the hash itself
-// (round 2)
-#ifndef SQ_PSKPRE
-#define SQ_PSKPRE 1
-#endif
+// 256-PSK batch in-process, profiles/r03/ab); round 2 loaded it in the hash
+// itself.
+constexpr bool kPskPre = true;
+// (Round 6: the compile-time switches of these constants were folded into
+// them; their variants are in git history and DESIGN.md section 5.)
 // Timeline builds (scripts/dev/timeline.py, never shipped): lane 0 of every
 // wave records the constant-rate clock at its phase boundaries.
 #ifndef SQ_TIMELINE
@@ -110,21 +98,15 @@ namespace sq {
 // size).  So launches of at least kXcdMinUnits units (~5.7 GB of payload at
 // the byte-sized units) remap (KParams.xcd).  Runs of 32-768 blocks per XCD
 // inside 8-run windows instead of eighths gained less at 16M and nothing at
-// 1M.  SQ_XCD (timing builds): -1 that rule, 0 never, 1 always.
-#ifndef SQ_XCD
-#define SQ_XCD -1
-#endif
-
+// 1M.
 constexpr uint64_t kXcdMinUnits = 1u << 18;
 
-#define SQ_STR2(x) #x
-#define SQ_STR(x) SQ_STR2(x)
+static_assert(kU == 4 && kDefaultUnitPackets == 26 && kNt == 3 && kWpb == 2 && kDonate &&
+                  kAlign == 3 && kMapBlk == 4096,
+              "sqobfs_build_info states these");
 extern "C" const char *sqobfs_build_info(void) {
-  return "gfx950 obfs_kernel U=" SQ_STR(SQ_U) " default_ppw=" SQ_STR(SQ_PPW) " NT=" SQ_STR(SQ_NT)
-         " wpb=" SQ_STR(SQ_WPB)
-         " donate=" SQ_STR(SQ_DONATE) " align=" SQ_STR(SQ_ALIGN)
-         " map=" SQ_STR(SQ_MAPBLK)
-         " windows=buffer earlysalt=1 dppred=1 xcd=" SQ_STR(SQ_XCD);
+  return "gfx950 obfs_kernel U=4 default_ppw=26 NT=3 wpb=2 donate=1 align=3 map=4096"
+         " windows=buffer earlysalt=1 dppred=1 xcd=rule";
 }
 
 // default unit size (KParams.ppw == 0); any 1 .. kMaxUnitPackets works
@@ -442,7 +424,7 @@ __device__ __forceinline__ void finalize_desc(const KParams &P, uint32_t p, bool
   }
 }
 
-// The words of a keyring entry one compression needs (SQ_PSKPRE): loaded
+// The words of a keyring entry one compression needs (kPskPre): loaded
 // early, consumed by the hash.
 struct PskHot {
   uint64_t h[8];   // BLAKE2b chaining value | SHA-256 state (first 32 bytes)
@@ -453,15 +435,13 @@ struct PskHot {
 
 // message words of the first block loaded early (timing builds vary it; the
 // rest are read by the hash)
-#ifndef SQ_PSKPRE_M
-#define SQ_PSKPRE_M 16
-#endif
+constexpr uint32_t kPskPreM = 16;
 template <int KIND>
 __device__ __forceinline__ void load_hot(const KParams &P, const PskEntry *E, PskHot &H) {
   // the keyring's uniform bounds (sq_api.hip keyring_hot_words): words no
   // entry needs are zero and not loaded, the chaining value of a keyring of
   // short PSKs is the initial state
-  const uint32_t mw = P.psk_hot_m < SQ_PSKPRE_M ? P.psk_hot_m : SQ_PSKPRE_M;
+  const uint32_t mw = P.psk_hot_m < kPskPreM ? P.psk_hot_m : kPskPreM;
   if (P.psk_hot_iv) {
     if (KIND == 0) {
       b2_init256(H.h);
@@ -501,7 +481,7 @@ __device__ __forceinline__ void salamander_key_hot(const PskHot &H, const PskEnt
 #pragma unroll
     for (int j = 0; j < 16; j++) {
       const uint32_t idx = 16 * blk + j;
-      uint64_t x = blk == 0 && j < SQ_PSKPRE_M ? H.m[j] : E->m[idx];  // (H.m: zero past mw)
+      uint64_t x = blk == 0 && j < kPskPreM ? H.m[j] : E->m[idx];  // (H.m: zero past mw)
       x |= (idx == w) ? lo : 0ull;
       x |= (idx == w + 1) ? hi : 0ull;
       m[j] = x;
@@ -541,7 +521,7 @@ __device__ __forceinline__ void xplus_key_hot(const PskHot &H, const PskEntry *E
     for (int j = 0; j < 16; j++) {
       const uint32_t idx = 16 * blk + j;
       const uint64_t hv = H.m[j >> 1];
-      uint32_t x = blk == 0 && (j >> 1) < SQ_PSKPRE_M ? (uint32_t)(j & 1 ? hv >> 32 : hv)
+      uint32_t x = blk == 0 && (j >> 1) < kPskPreM ? (uint32_t)(j & 1 ? hv >> 32 : hv)
                                                      : m32[idx];
 #pragma unroll
       for (int k = 0; k < 5; k++) x |= (idx == w + k) ? c[k] : 0u;
@@ -724,10 +704,10 @@ static_assert(sizeof(ChunkRec) == 96, "ChunkRec layout");
 // per flat block, the owning packet's record index (bits 0-5) and the
 // block's role (bit 6: special first block, bit 7: special last block).
 // The stream reads one byte per block: no search, no cross-lane work.
-constexpr uint32_t kMapBlocks = SQ_MAPBLK;  // 64 KiB of output per unit (4096)
+constexpr uint32_t kMapBlocks = kMapBlk;  // 64 KiB of output per unit (4096)
 constexpr uint32_t kRoleFirst = 64, kRoleLast = 128;
 // slack for the steps the double-buffered loop issues past the end
-constexpr uint32_t kMapSlack = 2 * kWave * SQ_U + 64;
+constexpr uint32_t kMapSlack = 2 * kWave * kU + 64;
 // record index of the phase slots (below): no packet (ranks are <= 62)
 constexpr uint32_t kRankNone = kWave - 1;
 constexpr uint32_t kOffPhase = 0xFFFFF000u;  // + 16 c (c < 64) stays past any span
@@ -819,7 +799,7 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
   // not in place, and its leading bytes are a whole junction block or none.
   const bool ahead = lane == ppw, head = lane == 0 && has_prev;
   const uint64_t LE = (rs + 63) & ~63ull;
-  const bool donate = SQ_DONATE && (ahead || head) && G.ne && !ovl && LE > B0r &&
+  const bool donate = kDonate && (ahead || head) && G.ne && !ovl && LE > B0r &&
                       B0r + 16ull * nraw > LE && (G.obh || (rs & 15) == 0 || G.pfull);
   const uint32_t don = donate ? (uint32_t)((LE - B0r) >> 4) : 0u;
   const uint64_t B0 = donate && head ? LE : B0r;
@@ -852,7 +832,7 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
                                      __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
   const uint32_t K = (uint32_t)__popcll(fm);
   const uint32_t T0 = __builtin_amdgcn_readfirstlane(__shfl(incl, kWave - 1, kWave));
-  U.map = T0 + (1u << SQ_ALIGN) <= kMapBlocks;
+  U.map = T0 + (1u << kAlign) <= kMapBlocks;
   // interior blocks [i_lo, i_hi): the only ones loaded
   const uint32_t i_lo = G.hf ? 1u : 0u, i_hi = G.hl ? nblk - 1 : nblk;
   const bool has_int = i_hi > i_lo;
@@ -868,8 +848,8 @@ __device__ __forceinline__ UnitStream plan_unit(const PacketJob &J, bool owner, 
   U.fast = T0 != 0 && __ballot(mis) == 0 && d_hi - d_lo <= kMaxSpan && sok;
   // map path (buffer streaming only: the generic path walks [0, T) by
   // `locate`): shift the flat space so that slot c sits at d_lo's line phase
-  const uint32_t phase = U.map && U.fast && SQ_ALIGN
-                             ? (uint32_t)(d_lo >> 4) & ((1u << SQ_ALIGN) - 1u)
+  const uint32_t phase = U.map && U.fast && kAlign
+                             ? (uint32_t)(d_lo >> 4) & ((1u << kAlign) - 1u)
                              : 0u;
   const uint32_t start = start0 + phase;
   G.start = start;
@@ -947,7 +927,7 @@ __device__ __forceinline__ void fill_unit(const KParams &P, const PacketJob &J,
     win16(w, (uint32_t)(J.src_pay & 15) + 16 - S, sl);
   }
   // single PSK: the kernarg copy (scalar loads); several: the device table
-  derive_key<KIND, MULTI && SQ_PSKPRE>(do_hash, MULTI ? P.psk_table + pid : &P.psk0, hot, sl,
+  derive_key<KIND, MULTI && kPskPre>(do_hash, MULTI ? P.psk_table + pid : &P.psk0, hot, sl,
                                         key);
   const uint64_t rs = G.rs, re = G.re;
   // head image: output bytes [rs, rs + 32) = salt || payload ^ key
@@ -1069,8 +1049,8 @@ __device__ __forceinline__ uint32_t locate(uint32_t cst, uint32_t b0, uint32_t c
 constexpr uint32_t kOffNone = 0xFFFFFFF0u;
 // cache-policy bits of the stream's buffer ops (gfx950: sc0 = 1, nt = 2,
 // sc1 = 16)
-constexpr int kAuxLd = (SQ_NT & 1) ? 2 : 0;  // nt
-constexpr int kAuxSt = (SQ_NT & 2) ? 2 : 0;
+constexpr int kAuxLd = (kNt & 1) ? 2 : 0;  // nt
+constexpr int kAuxSt = (kNt & 2) ? 2 : 0;
 
 // One stream step in flight: U blocks per lane with their keystreams (or
 // special values) and output offsets.
@@ -1216,7 +1196,7 @@ __global__ __launch_bounds__(WPB * kWave) void obfs_kernel(const KParams P) {
   uint32_t olen;
   finalize_desc<KIND, DIR, MULTI>(P, p, valid, d, J, salt, do_hash, E, olen);
   PskHot hot;
-  if constexpr (MULTI && SQ_PSKPRE) {
+  if constexpr (MULTI && kPskPre) {
     load_hot<KIND>(P, E, hot);  // in flight during the plan
   }
   SQ_STAMP(1);
@@ -1334,7 +1314,7 @@ __global__ void psk_prepare_kernel(int kind, const uint8_t *blob, const uint64_t
 // 1.5 % of it for every kernel and direction (Salamander obfuscate 2.6 %
 // faster than 4-wave groups, XPlus obfuscate 3.4 % faster than 1-wave ones).
 template <int KIND, int DIR>
-constexpr int kWavesPerGroup = SQ_WPB;
+constexpr int kWavesPerGroup = kWpb;
 
 // sqobfs_debug_time_next_launch: events the calling thread's next launch
 // records with its own dispatch (no marker packets between kernels)
@@ -1362,7 +1342,7 @@ static int launch_k(const KParams &P, hipStream_t s) {
 
 template <int KIND, int DIR, bool MULTI>
 static int launch_one(const KParams *kp, hipStream_t s) {
-  constexpr int U = SQ_U;
+  constexpr int U = kU;
   KParams P = *kp;
   if (P.ppw == 0) P.ppw = kPktPerWave;
   if (P.ppw > kMaxUnitPackets) {
@@ -1370,7 +1350,7 @@ static int launch_one(const KParams *kp, hipStream_t s) {
     return -1;
   }
   const uint64_t units = ((uint64_t)P.n + P.ppw - 1) / P.ppw;
-  P.xcd = SQ_XCD < 0 ? (units >= kXcdMinUnits ? 1u : 0u) : (uint32_t)SQ_XCD;
+  P.xcd = units >= kXcdMinUnits ? 1u : 0u;
   return launch_k<KIND, DIR, MULTI, U, kWavesPerGroup<KIND, DIR>>(P, s);
 }
 

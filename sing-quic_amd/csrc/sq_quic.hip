@@ -38,10 +38,7 @@ namespace sq {
 // Threads per workgroup.  Its waves share nothing, and a workgroup's slots
 // free only when all of its waves have ended: 1-wave groups measured 1.3 %
 // (seal) and 1.0 % (open) faster than 4-wave ones, 3 interleaved passes.
-#ifndef SQ_QBLOCK
-#define SQ_QBLOCK 64
-#endif
-constexpr uint32_t kQBlock = SQ_QBLOCK;
+constexpr uint32_t kQBlock = 64;
 constexpr uint32_t kQWaves = kQBlock / kWave;
 // Packets per wave (owner lanes of phases 1 and 3).  32 with a 1,536-byte
 // cooperative range (MTU-sized packets; longer ones take the owner lane's
@@ -49,21 +46,13 @@ constexpr uint32_t kQWaves = kQBlock / kWave;
 // SIMD; the 2,048-byte range needed 25 KB, 6 per CU) and halves the idle
 // lanes of the owner phases: seal 1,570 -> 1,406 us against 16 packets and
 // 2,048 B (24: 1,545; 40: 1,677).
-#ifndef SQ_QPPW
-#define SQ_QPPW 32
-#endif
-constexpr uint32_t kQPpw = SQ_QPPW;
-#ifndef SQ_QCOOPMAX
-#define SQ_QCOOPMAX 1536
-#endif
+constexpr uint32_t kQPpw = 32;
 // Waves per SIMD the register allocation must allow.  With pairs the LDS
 // admits 3; the fused seal needs 177 VGPRs uncapped (2 waves) and 168 with
 // 40 bytes of spills at 3: 1,548 -> 1,467 us, every other kernel unchanged
 // (two interleaved passes).
-#ifndef SQ_QMINW
-#define SQ_QMINW 3
-#endif
-constexpr uint32_t kQCoopMax = SQ_QCOOPMAX;  // payloads up to this size take the cooperative pass
+constexpr uint32_t kQMinWaves = 3;
+constexpr uint32_t kQCoopMax = 1536;  // payloads up to this size take the cooperative pass
 constexpr uint32_t kQMaxBlk = kQPpw * (kQCoopMax / 64);
 // Pairs: every packet's flat blocks start at an even index, and the even
 // lane of each pair of lanes folds its neighbour's partial MAC into its own
@@ -507,12 +496,7 @@ __device__ __forceinline__ void coop_block(const QuicKeyDev &K, QRec &R, uint32_
 // Payloads above kQCoopMax bytes are walked by their owner lane in phase 3
 // (the sequential payload_pass), so any length works.
 template <bool OPEN, bool MULTI, bool OB>
-#if SQ_QMINW
-__global__ __launch_bounds__(kQBlock, SQ_QMINW) void quic_kernel
-#else
-__global__ __launch_bounds__(kQBlock) void quic_kernel
-#endif
-(const QParams Q) {
+__global__ __launch_bounds__(kQBlock, kQMinWaves) void quic_kernel(const QParams Q) {
   __shared__ QRec recs[kQWaves][kQPpw];
   __shared__ uint32_t parts[kQWaves][kQParts][5];
   const uint32_t lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;

@@ -59,19 +59,13 @@
 
 namespace sq {
 
-#ifndef SQ_GBLOCK
-#define SQ_GBLOCK 768
-#endif
-constexpr uint32_t kGBlock = SQ_GBLOCK;  // 12 waves: one block per CU (156 KB of LDS)
+constexpr uint32_t kGBlock = 768;  // 12 waves: one block per CU (156 KB of LDS)
 constexpr uint32_t kGWaves = kGBlock / kWave;
 // Packets per wave (owner lanes).  32 with 12-wave workgroups (the LDS
 // tables plus 32 records per wave fill 156 KB, 3 waves per SIMD) measured
 // seal 3,246 -> 3,146 us and open 3,252 -> 3,056 us against 16 packets in
 // 16-wave groups (4 waves per SIMD), three interleaved passes.
-#ifndef SQ_GPPW
-#define SQ_GPPW 32
-#endif
-constexpr uint32_t kGPpw = SQ_GPPW;
+constexpr uint32_t kGPpw = 32;
 constexpr uint32_t kGCoopMax = 16 * kGcmPow;   // 2048 B
 
 // ---------------------------------------------------------------- AES-128

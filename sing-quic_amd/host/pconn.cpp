@@ -298,6 +298,8 @@ struct Engine {
   std::vector<Job> pending;  // routed to the GPU while flight_cap launches fly
   uint32_t pending_dgrams = 0;
   uint32_t pend_max = kDefPendMax;  // past it, bulk batches overflow to the CPU path
+  // (round 6 swept both in lat_bench hops: flight caps 1 / 2 / 4 and
+  // overflow at 0 / 2,048 / 4,096 / 8,192 datagrams)
   uint32_t nflight = 0;     // non-polling launches started and not yet landed
   uint32_t flight_cap = kDefFlightCap;
   bool cstop = false;
@@ -419,10 +421,6 @@ Engine *engine_get(sqobfs_ctx *ctx, int *status) {
   if (aff == SQOBFS_ENGINE_AFFINITY_L3) E->ncpus = l3_cpus(&E->cpus);
   auto gc = g_group_cfg.find(ctx);
   if (gc != g_group_cfg.end()) E->group_max = gc->second;
-  if (const char *fc = getenv("SQ_ENGINE_FLIGHTS"))  // (dev: the cap sweep)
-    E->flight_cap = std::max(1, std::min(atoi(fc), (int)kMaxFlights));
-  if (const char *pm = getenv("SQ_ENGINE_PENDMAX"))  // (dev: the overflow sweep; 0 = none)
-    E->pend_max = (uint32_t)atoi(pm);
   E->wake = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
   E->epfd = epoll_create1(EPOLL_CLOEXEC);
   epoll_event ev{};
