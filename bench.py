@@ -482,6 +482,24 @@ def load_traffic(config: str, kernel_bytes: float):
     return d.get("hbm_bytes_per_launch"), d
 
 
+def copy_at_footprint(config: str):
+    """The best plain copy's fraction of 8 TB/s at this config's footprint,
+    measured in a process of its own (profiles/r06/ragged/copy_at_footprint.json,
+    scripts/dev/footprint.sh), or None: the ceiling a streaming kernel of that
+    size reaches on this hardware ("The copy control")."""
+    path = os.path.join(REPO, "profiles", "r06", "ragged", "copy_at_footprint.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    c = d.get("configs", {}).get(config)
+    if not c:
+        return None
+    return {"copy_frac": c["copy_best_frac"], "case": c["case"],
+            "kernel_frac_isolated": c["kernel_frac_isolated"],
+            "source": "profiles/r06/ragged/copy_at_footprint.json (" + c["box"] + ")"}
+
+
 def inproc_bench(args):
     """K contexts in one process (the Go service's multi-GPU path), steps of
     sqobfs_shard_launch kept --inflight deep (each waited through its ticket;
@@ -906,6 +924,10 @@ def main():
     }
     if pmc:
         out["roofline"]["traffic_source"] = pmc.get("source")
+    cf = copy_at_footprint(args.config) if args.layout == "dense" and not args.packets else None
+    if cf:
+        out["roofline"]["copy_at_footprint"] = cf
+        out["roofline"]["frac_of_copy_at_footprint"] = round(achieved / PEAK_HBM_GBS / cf["copy_frac"], 4)
     if args.latency and rank == 0:
         out["latency"] = latency_bench()
     if not args.no_e2e:
