@@ -60,8 +60,96 @@ __global__ void __launch_bounds__(256) writeonly(uint4 *p, size_t n16) {
     p[i] = make_uint4((uint32_t)i, 1u, 2u, 3u);
 }
 
+// device in, mapped host out (the inbound bytes came by DMA)
+__global__ void __launch_bounds__(256) dev2host(const uint4 *src, uint4 *dst, size_t n16) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x * kU;
+  for (size_t b = ((size_t)blockIdx.x * blockDim.x) * kU + threadIdx.x; b < n16; b += stride) {
+    uint4 v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const size_t i = b + (size_t)u * blockDim.x;
+      if (i < n16) v[u] = src[i];
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const size_t i = b + (size_t)u * blockDim.x;
+      if (i < n16) dst[i] = make_uint4(v[u].x ^ 0x5a5a5a5au, v[u].y ^ 1u, v[u].z, v[u].w ^ 7u);
+    }
+  }
+}
+
+// Staged variants over one page-locked buffer of `bytes`, split into
+// `chunks` pieces on `ns` streams (piece i on stream i % ns):
+//   hybrid: H2D copy of the piece, then a kernel reading it from HBM and
+//           writing the result to the host buffer directly;
+//   staged: H2D copy, kernel in place in HBM, D2H copy.
+int staged(int reps) {
+  const size_t sizes[] = {1u << 20, 5530000, 22118400};
+  const int chunk_opts[] = {1, 2, 4, 8};
+  const size_t cap = sizes[2];
+  void *h;
+  CK(hipHostMalloc(&h, cap, hipHostMallocDefault));
+  memset(h, 1, cap);
+  void *hd;
+  CK(hipHostGetDevicePointer(&hd, h, 0));
+  void *d;
+  CK(hipMalloc(&d, cap));
+  hipStream_t st[2];
+  for (auto &x : st) CK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+  hipEvent_t e0, e1, j[2];
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (auto &x : j) CK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+  for (int mode = 0; mode < 2; mode++)
+    for (size_t bytes : sizes)
+      for (int chunks : chunk_opts)
+        for (int ns = 1; ns <= 2; ns++) {
+          if (ns == 2 && chunks == 1) continue;
+          const size_t piece = (bytes / chunks + 15) & ~(size_t)15;
+          auto run = [&] {
+            // both streams start after the previous repetition's end
+            CK(hipEventRecord(j[0], st[0]));
+            CK(hipStreamWaitEvent(st[1], j[0], 0));
+            for (int c = 0; c < chunks; c++) {
+              const size_t off = c * piece;
+              if (off >= bytes) break;
+              const size_t len = bytes - off < piece ? bytes - off : piece;
+              hipStream_t s = st[c % ns];
+              uint8_t *hp = (uint8_t *)h + off, *hdp = (uint8_t *)hd + off, *dp = (uint8_t *)d + off;
+              CK(hipMemcpyAsync(dp, hp, len, hipMemcpyHostToDevice, s));
+              const int g = (int)((len / 16 + 256 * kU - 1) / (256 * kU));
+              if (mode == 0) {
+                dev2host<<<g, 256, 0, s>>>((const uint4 *)dp, (uint4 *)hdp, len / 16);
+              } else {
+                inplace<<<g, 256, 0, s>>>((uint4 *)dp, len / 16);
+                CK(hipMemcpyAsync(hp, dp, len, hipMemcpyDeviceToHost, s));
+              }
+            }
+            CK(hipEventRecord(j[1], st[1]));
+            CK(hipStreamWaitEvent(st[0], j[1], 0));
+          };
+          for (int w = 0; w < 3; w++) run();
+          CK(hipStreamSynchronize(st[0]));
+          CK(hipEventRecord(e0, st[0]));
+          for (int r = 0; r < reps; r++) run();
+          CK(hipEventRecord(e1, st[0]));
+          CK(hipEventSynchronize(e1));
+          float ms = 0;
+          CK(hipEventElapsedTime(&ms, e0, e1));
+          const double us = ms * 1e3 / reps;
+          printf("{\"alloc\": \"default\", \"bytes\": %zu, \"chunks\": %d, \"streams\": %d, "
+                 "\"kernel\": \"%s\", \"us\": %.1f, \"GBps\": %.2f}\n",
+                 bytes, chunks, ns, mode == 0 ? "hybrid" : "staged", us, bytes / us / 1e3);
+          fflush(stdout);
+        }
+  CK(hipFree(d));
+  CK(hipHostFree(h));
+  return 0;
+}
+
 int main(int argc, char **argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 20;
+  if (argc > 2 && !strcmp(argv[2], "staged")) return staged(reps);
   struct Alloc {
     const char *name;
     unsigned flags;

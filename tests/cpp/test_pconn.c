@@ -880,7 +880,7 @@ static void t_routing(void) {
 /* ------------------------------------------------------------ load */
 typedef struct {
   int fd;
-  volatile int stop;
+  int stop; /* (atomic accesses) */
   long got, checked, bad;
 } LoadPeer;
 
@@ -906,7 +906,7 @@ static void *load_peer(void *arg) {
     }
     struct pollfd p = {r->fd, POLLIN, 0};
     if (poll(&p, 1, 20) <= 0) {
-      if (r->stop) break;
+      if (__atomic_load_n(&r->stop, __ATOMIC_ACQUIRE)) break;
       continue;
     }
     const int m = recvmmsg(r->fd, h, M, MSG_DONTWAIT, NULL);
@@ -1021,7 +1021,7 @@ static void t_load(void) {
            (unsigned long long)(s3.cpu_batches - s2.cpu_batches),
            (unsigned long long)(s3.tx_batches - s2.tx_batches));
   sleep_ms(100);
-  r.stop = 1;
+  __atomic_store_n(&r.stop, 1, __ATOMIC_RELEASE);
   pthread_join(th, NULL);
   EXPECT(r.bad == 0 && r.checked > 100, "load: %ld of %ld decoded datagrams differ", r.bad,
          r.checked);
@@ -1222,6 +1222,95 @@ static void t_group(int kind, int short_psks) {
     if (k != 1 && k != 2) sqobfs_keyring_destroy(kr[k]);
   sqobfs_engine_trim(ctx);
   EXPECT(sqobfs_debug_host_allocs() == a0, "group: host allocs");
+  sqobfs_close(ctx);
+}
+
+/* More PSKs than one merged keyring holds: 300 pump pconns, a
+ * keyring of its own PSK each, queue two transmit and two receive datagrams
+ * while the engine's one worker is held; released, the coalesced launches
+ * (32 batches each) fill the merged keyring past its 256 entries, so the
+ * engine starts a new one mid-traffic.  Every datagram is the reference's
+ * under its own conn's PSK. */
+static void t_many_psks(int kind) {
+  enum { K = 300, N = 2 };
+  const int S = salt_len(kind);
+  sqobfs_ctx *ctx = NULL;
+  CHECK(sqobfs_open(0, &ctx));
+  CHECK(sqobfs_engine_set_workers(ctx, 1));
+  const int64_t a0 = sqobfs_debug_host_allocs();
+  static uint8_t psk[K][12];
+  static sqobfs_keyring *kr[K];
+  static sqobfs_pconn *pc[K];
+  sqobfs_pconn_opts o;
+  memset(&o, 0, sizeof o);
+  o.cpu_max = SQOBFS_PCONN_NEVER; /* every batch launches */
+  o.batch = 4;
+  for (int k = 0; k < K; k++) {
+    for (int b = 0; b < 12; b++) psk[k][b] = (uint8_t)(k * 7 + b * 131 + (k >> 8));
+    uint64_t off = 0;
+    uint32_t len = 12;
+    CHECK(sqobfs_keyring_create(ctx, kind, 1, psk[k], &off, &len, &kr[k]));
+    CHECK(sqobfs_pconn_open(ctx, kr[k], -1, &o, &pc[k]));
+  }
+  static uint8_t pay[K][N][1400], wire[K][N][1500];
+  static uint32_t plen[K][N], wlen[K][N];
+  sqobfs_engine_info i0, i1;
+  CHECK(sqobfs_engine_info_get(ctx, &i0));
+  sqobfs_debug_engine_hold(1);
+  for (int k = 0; k < K; k++)
+    for (int i = 0; i < N; i++) {
+      plen[k][i] = (uint32_t)(rnd() % 1385);
+      for (uint32_t j = 0; j < plen[k][i]; j++) pay[k][i][j] = (uint8_t)rnd();
+      CHECK(sqobfs_pconn_write(pc[k], pay[k][i], plen[k][i], NULL, (uint64_t)i));
+      uint8_t salt[16];
+      for (int b = 0; b < 16; b++) salt[b] = (uint8_t)rnd();
+      ref_write_psk(kind, psk[k], 12, salt, pay[k][i], plen[k][i], wire[k][i]);
+      wlen[k][i] = plen[k][i] + (uint32_t)S;
+      CHECK(sqobfs_pconn_rx_push(pc[k], wire[k][i], wlen[k][i], NULL, (uint64_t)i));
+    }
+  sqobfs_debug_engine_hold(0);
+  for (int k = 0; k < K; k++) {
+    int got = 0;
+    while (got < N) {
+      sqobfs_pconn_tx v;
+      CHECK(sqobfs_pconn_tx_take(pc[k], 5000, &v));
+      for (uint32_t i = 0; i < v.count; i++, got++) {
+        const uint8_t *w = v.base + v.off[i];
+        const uint64_t id = v.tag[i];
+        uint8_t ref[MAXW];
+        EXPECT(id == (uint64_t)got && v.len[i] == plen[k][id] + (uint32_t)S,
+               "many PSKs kind %d conn %d: datagram %d len %u", kind, k, got, v.len[i]);
+        ref_write_psk(kind, psk[k], 12, w, pay[k][id], plen[k][id], ref);
+        EXPECT(!memcmp(ref, w, v.len[i]), "many PSKs kind %d conn %d: wire %d differs", kind, k,
+               got);
+      }
+      CHECK(sqobfs_pconn_tx_done(pc[k]));
+    }
+    for (int i = 0; i < N; i++) {
+      uint8_t got_p[MAXW], ref[MAXW];
+      uint32_t n;
+      uint64_t tag;
+      CHECK(sqobfs_pconn_read(pc[k], got_p, MAXW, &n, NULL, &tag));
+      const long want = ref_read_psk(kind, psk[k], 12, wire[k][i], wlen[k][i], ref);
+      EXPECT(tag == (uint64_t)i && (long)n == want && (!n || !memcmp(got_p, ref, n)),
+             "many PSKs kind %d conn %d: read %d", kind, k, i);
+    }
+    sqobfs_pconn_stats st;
+    CHECK(sqobfs_pconn_stats_get(pc[k], &st));
+    EXPECT(st.cpu_batches == 0 && st.gpu_failures == 0, "many PSKs conn %d: %llu CPU batches", k,
+           (unsigned long long)st.cpu_batches);
+  }
+  CHECK(sqobfs_engine_info_get(ctx, &i1));
+  const uint64_t gl = i1.group_launches - i0.group_launches;
+  const uint64_t gb = i1.group_batches - i0.group_batches;
+  EXPECT(gb >= K && gl * 32 >= gb && gl >= 2 * K / 32, "many PSKs kind %d: %llu coalesced "
+         "launches carrying %llu batches", kind, (unsigned long long)gl, (unsigned long long)gb);
+  printf("  many PSKs kind %d: %d conns of distinct PSKs, %llu coalesced launches carrying %llu "
+         "batches, wire == reference\n", kind, K, (unsigned long long)gl, (unsigned long long)gb);
+  for (int k = 0; k < K; k++) sqobfs_pconn_close(pc[k]);
+  for (int k = 0; k < K; k++) sqobfs_keyring_destroy(kr[k]);
+  sqobfs_engine_trim(ctx);
+  EXPECT(sqobfs_debug_host_allocs() == a0, "many PSKs: host allocs");
   sqobfs_close(ctx);
 }
 
@@ -1467,6 +1556,8 @@ int main(int argc, char **argv) {
     t_group(SQOBFS_XPLUS, 0);
     t_group(SQOBFS_SALAMANDER, 1);
     t_group(SQOBFS_XPLUS, 1);
+    t_many_psks(SQOBFS_SALAMANDER);
+    t_many_psks(SQOBFS_XPLUS);
     t_group_stress(SQOBFS_SALAMANDER, 0);
     t_group_stress(SQOBFS_XPLUS, 0);
     t_group_stress(SQOBFS_SALAMANDER, 1);
