@@ -5,9 +5,12 @@ kernel's time: the Shoup multiply by H^m per chunk, the GHASH multiply per
 block, the AES keystream per block pair.  Builds
 build/ablate/<name>/libsqobfs.so from the in-tree objects plus a modified
 copy of sq_quic_gcm.hip (nothing here ships; SQOBFS_LIB selects a build).
-usage: python3 scripts/dev/gcm_ablate.py"""
+usage: python3 scripts/dev/gcm_ablate.py [set]   (set: ablate, the default;
+occupancy: workgroup size / packets per wave variants, correct output)"""
 import os
+import shutil
 import subprocess
+import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
@@ -19,6 +22,16 @@ VARIANTS = {
     "no_ghash": [("      ghash_absorb(y, g);\n      gmul_pos<KM == 1>(y, K.hpos);", "      ghash_absorb(y, g);")],
     "no_aes": [("    aes_encrypt_n<KM, 2>(K.rk, tT, tcol, s2);", "")],
 }
+SETS = {
+    "ablate": VARIANTS,
+    "occupancy": {
+        "base": [],
+        "w16p16": [("constexpr uint32_t kGBlock = 768;", "constexpr uint32_t kGBlock = 1024;"),
+                   ("constexpr uint32_t kGPpw = 32;", "constexpr uint32_t kGPpw = 16;")],
+    },
+}
+VARIANTS = SETS[sys.argv[1] if len(sys.argv) > 1 else "ablate"]
+shutil.rmtree(os.path.join(REPO, "build", "ablate"), ignore_errors=True)
 objs = [os.path.join(PKG, "build", "obj", f + ".o")
         for f in ("sq_kernels", "sq_quic", "sq_api", "packet_conn", "udp_batch", "pconn", "sq_cpu")]
 src = open(SRC).read()

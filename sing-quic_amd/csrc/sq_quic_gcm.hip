@@ -438,6 +438,77 @@ __device__ __forceinline__ void gcm_run(const GKey<KM> &K, const uint32_t *tT, u
   }
 }
 
+// The cooperative pass's share of a packet: nfull (1..4) FULL payload
+// blocks, blocks blk0 .. blk0 + nfull - 1 at src / dst (the chunk's start).
+// No partial block ever reaches it (a payload's last, partial block is its
+// owner lane's, in phase 3), so the body is straight-line code: no masks,
+// no byte-exact helpers, no divergent branches but the predicated loads and
+// stores of a short chunk.  The blocks sit right-aligned in 4 slots (slot s
+// holds block s - z, z = 4 - nfull; slots below z are zero and absorb
+// nothing, so Horner over the 4 slots equals Horner over the nfull blocks).
+// All four loads are issued before the first store (in place, and the fused
+// open's output 8 bytes before its input, never overwrite unread input).
+// y = the chunk's GHASH partial (Horner with H from 0).  ct32 (seal, the
+// packet's first chunk): LDS words that receive ciphertext blocks 0 and 1.
+// OB: as gcm_run (okr = the key rotated to the payload start).
+template <bool OPEN, int KM, bool OB>
+__device__ __forceinline__ void gcm_chunk(const GKey<KM> &K, const uint32_t *tT, uint32_t tcol,
+                                          const uint32_t (&nonce)[3], uint32_t blk0,
+                                          uint32_t nfull, uint64_t src, uint64_t dst,
+                                          uint32_t (&y)[4], uint32_t *ct32,
+                                          const uint32_t (&okr)[8]) {
+  const uint32_t z = 4u - nfull;
+  const uint64_t sz = src - 16ull * z, dz = dst - 16ull * z;  // slot s at sz + 16 s
+  uint32_t in[4][4];
+#pragma unroll
+  for (int s = 0; s < 4; s++) {
+    if (s == 3 || (uint32_t)s >= z) {
+      const u32x4 v = gld<u32x4_a1>(sz + 16ull * s);
+      in[s][0] = v.x; in[s][1] = v.y; in[s][2] = v.z; in[s][3] = v.w;
+    } else {
+#pragma unroll
+      for (int w = 0; w < 4; w++) in[s][w] = 0u;
+    }
+  }
+#pragma unroll
+  for (int w = 0; w < 4; w++) y[w] = 0u;
+  const uint32_t ctr = 2u + blk0 - z;  // slot 0's counter
+#pragma unroll
+  for (int h = 0; h < 4; h += 2) {
+    uint32_t s2[2][4] = {{nonce[0], nonce[1], nonce[2], __builtin_bswap32(ctr + h)},
+                         {nonce[0], nonce[1], nonce[2], __builtin_bswap32(ctr + h + 1)}};
+    aes_encrypt_n<KM, 2>(K.rk, tT, tcol, s2);
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      const int s = h + q;
+      const uint32_t live = s == 3 || (uint32_t)s >= z ? 0xFFFFFFFFu : 0u;
+      uint32_t x[4], c[4], kw[4];
+#pragma unroll
+      for (int w = 0; w < 4; w++) {
+        // block s - z's half of the key: (s - z) & 1 == (s + z) & 1
+        kw[w] = OB ? bsel((s + z) & 1u, okr[4 + w], okr[w]) : 0u;
+        x[w] = (OB && OPEN) ? in[s][w] ^ kw[w] : in[s][w];
+        c[w] = (x[w] ^ s2[q][w]) & live;
+      }
+      if (OPEN) {
+#pragma unroll
+        for (int w = 0; w < 4; w++) x[w] &= live;
+      }
+      const uint32_t(&g)[4] = OPEN ? x : c;
+      ghash_absorb(y, g);
+      gmul_pos<KM == 1>(y, K.hpos);
+      if (s == 3 || (uint32_t)s >= z) {
+        uint32_t o[4];
+#pragma unroll
+        for (int w = 0; w < 4; w++) o[w] = (OB && !OPEN) ? c[w] ^ kw[w] : c[w];
+        gst<u32x4_a1>(dz + 16ull * s, u32x4_a1{o[0], o[1], o[2], o[3]});
+        if (!OPEN && ct32 && blk0 == 0 && (uint32_t)s - z < 2u)
+          *(u32x4 *)(ct32 + 4 * ((uint32_t)s - z)) = u32x4{c[0], c[1], c[2], c[3]};
+      }
+    }
+  }
+}
+
 // 5 header-protection mask bytes (RFC 9001 5.4.3): AES-ECB(hp, sample)
 template <int KM>
 __device__ __forceinline__ void gcm_hp_mask(const GKey<KM> &K, const uint32_t *tT, uint32_t tcol,
@@ -651,7 +722,9 @@ __device__ __forceinline__ void gcm_unit(const QGParams &Q, uint64_t base, uint3
   const uint32_t np = (pl + 15) / 16;
   // the header's GHASH, placed ahead of the payload blocks
   if (coop && np) K.mul_pow(y, np);
-  const uint32_t nblk = coop ? (pl + 63) / 64 : 0u;
+  // chunks of the cooperative pass: the full blocks, 4 per chunk (the last,
+  // partial block is the owner's, phase 3)
+  const uint32_t nblk = coop ? (pl / 16 + 3) / 4 : 0u;
   uint32_t incl = nblk;
 #pragma unroll
   for (int d = 1; d < kWave; d <<= 1) {
@@ -692,23 +765,18 @@ __device__ __forceinline__ void gcm_unit(const QGParams &Q, uint64_t base, uint3
     if (f < T) {
       GRec &R = recs[pp];
       const GKey<KM> KB = key_of<MULTI, STAGED>(Q, R.kid, tP, tH, tK);
-      const uint32_t b = f - R.start, off0 = 64 * b;
-      const uint32_t nv = R.pl - off0 < 64 ? R.pl - off0 : 64u;
+      const uint32_t b = f - R.start, left = R.pl / 16 - 4 * b;  // full blocks from here
+      const uint32_t nfull = left < 4 ? left : 4u;
       const uint32_t rn[3] = {R.nonce[0], R.nonce[1], R.nonce[2]};
-      uint32_t yb[4] = {0u, 0u, 0u, 0u}, f32[8];
-      uint32_t rokr[8];
+      uint32_t yb[4], rokr[8];
 #pragma unroll
       for (int i = 0; i < 8; i++) rokr[i] = OB ? R.okr[i] : 0u;
-      gcm_run<OPEN, KM, OB>(KB, tT, tcol, rn, 2 + 4 * b, R.src + off0, R.dst + off0, nv, yb,
-                               f32, rokr);
-      const uint32_t m = R.np - 4 * b - (nv + 15) / 16;  // payload blocks after this chunk
+      gcm_chunk<OPEN, KM, OB>(KB, tT, tcol, rn, 4 * b, nfull, R.src + 64ull * b,
+                              R.dst + 64ull * b, yb, R.ct32, rokr);
+      const uint32_t m = R.np - 4 * b - nfull;  // payload blocks after this chunk
       if (m) KB.mul_pow(yb, m);
 #pragma unroll
       for (int i = 0; i < 4; i++) atomicXor(&R.x[i], yb[i]);
-      if (!OPEN && b == 0) {
-#pragma unroll
-        for (int i = 0; i < 8; i++) R.ct32[i] = f32[i];
-      }
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -725,6 +793,38 @@ __device__ __forceinline__ void gcm_unit(const QGParams &Q, uint64_t base, uint3
     for (int i = 0; i < 4; i++) y[i] = recs[lane].x[i];
 #pragma unroll
     for (int i = 0; i < 8; i++) ct32[i] = recs[lane].ct32[i];
+    const uint32_t nb = pl & 15u;
+    if (nb) {  // the payload's last, partial block: C * H joins the chunks' sum
+      const uint32_t k = pl / 16;
+      const uint64_t ps = src + hdr + 16ull * k;
+      uint32_t x[4], c[4], ks[4] = {nonce[0], nonce[1], nonce[2], __builtin_bswap32(2u + k)};
+      load16(ps, src + hdr + pl, x);
+      aes_encrypt<KM>(K.rk, tT, tcol, ks);
+      uint32_t kw[4];
+#pragma unroll
+      for (int w = 0; w < 4; w++) {
+        const uint32_t m = range_mask(0, (int)nb, w);
+        kw[w] = OB ? recs[lane].okr[4 * (k & 1) + w] & m : 0u;
+        if (OB && OPEN) x[w] ^= kw[w];
+        c[w] = (x[w] ^ ks[w]) & m;
+      }
+      uint32_t t[4] = {0u, 0u, 0u, 0u};
+      ghash_absorb(t, OPEN ? x : c);
+      gmul_pos<MULTI>(t, K.hpos);
+#pragma unroll
+      for (int w = 0; w < 4; w++) y[w] ^= t[w];
+      uint32_t o[4];
+#pragma unroll
+      for (int w = 0; w < 4; w++) o[w] = (OB && !OPEN) ? c[w] ^ kw[w] : c[w];
+      store16(dst + hdr + 16ull * k, o, nb);
+      if (!OPEN && k < 2) {
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+          if (k == 0) ct32[w] = c[w];
+          else ct32[4 + w] = c[w];
+        }
+      }
+    }
   } else {
     uint32_t rokr[8];
 #pragma unroll
