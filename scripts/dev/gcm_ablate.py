@@ -28,6 +28,7 @@ SETS = {
         "base": [],
         "w16p16": [("constexpr uint32_t kGBlock = 768;", "constexpr uint32_t kGBlock = 1024;"),
                    ("constexpr uint32_t kGPpw = 32;", "constexpr uint32_t kGPpw = 16;")],
+        "w16p32": [("constexpr uint32_t kGBlock = 768;", "constexpr uint32_t kGBlock = 1024;")],
     },
 }
 VARIANTS = SETS[sys.argv[1] if len(sys.argv) > 1 else "ablate"]

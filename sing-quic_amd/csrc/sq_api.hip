@@ -1113,9 +1113,29 @@ void gcm_key(const sqobfs_quic_key &k, sq::QuicGcmKeyDev &d) {
     d.hrk[i] = (d.hrk[i] >> 16) | (d.hrk[i] << 16);
   }
   const G128 h = g_load(hb);
-  G128 p = h;
-  for (uint32_t pw = 0; pw < sq::kGcmPow; pw++) {
-    if (pw) p = g_mul(p, h);
+  const G128 h4 = g_mul(g_mul(h, h), g_mul(h, h));
+  // position tables of H: nibble j enters Shoup's Horner loop j-th and is
+  // multiplied by x^4 (31 - j) more times
+  for (int n = 0; n < 16; n++) {
+    G128 v{0, 0};
+    for (int b = 0; b < 4; b++) {  // n H: bit 8 >> b of n is x^b
+      if (!(n & (8 >> b))) continue;
+      G128 t = h;
+      for (int i = 0; i < b; i++) t = g_mulx(t);
+      v.hi ^= t.hi;
+      v.lo ^= t.lo;
+    }
+    for (int j = 31; j >= 0; j--) {
+      d.hpos[j][n][0] = (uint32_t)(v.hi >> 32);
+      d.hpos[j][n][1] = (uint32_t)v.hi;
+      d.hpos[j][n][2] = (uint32_t)(v.lo >> 32);
+      d.hpos[j][n][3] = (uint32_t)v.lo;
+      for (int k = 0; k < 4; k++) v = g_mulx(v);
+    }
+  }
+  G128 p = h4;
+  for (uint32_t pw = 0; pw < sq::kGcmPow4; pw++) {  // table pw: H^(4 (pw + 1))
+    if (pw) p = g_mul(p, h4);
     G128 e[16] = {};
     e[8] = p;  // Shoup: entry 8 = H^k, 4 = H^k x, 2 = H^k x^2, 1 = H^k x^3
     e[4] = g_mulx(e[8]);
@@ -1137,19 +1157,6 @@ void gcm_key(const sqobfs_quic_key &k, sq::QuicGcmKeyDev &d) {
       d.htab[pw][sl][1] = (uint32_t)e[n].hi;
       d.htab[pw][sl][2] = (uint32_t)(e[n].lo >> 32);
       d.htab[pw][sl][3] = (uint32_t)e[n].lo;
-    }
-    if (pw == 0) {  // position tables of H: nibble j enters Shoup's Horner
-                    // loop j-th and is multiplied by x^4 (31 - j) more times
-      for (int n = 0; n < 16; n++) {
-        G128 v = e[n];
-        for (int j = 31; j >= 0; j--) {
-          d.hpos[j][n][0] = (uint32_t)(v.hi >> 32);
-          d.hpos[j][n][1] = (uint32_t)v.hi;
-          d.hpos[j][n][2] = (uint32_t)(v.lo >> 32);
-          d.hpos[j][n][3] = (uint32_t)v.lo;
-          for (int k = 0; k < 4; k++) v = g_mulx(v);
-        }
-      }
     }
   }
 }

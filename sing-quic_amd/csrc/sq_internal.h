@@ -120,19 +120,22 @@ struct QParams {
 // AES-128-GCM (TLS_AES_128_GCM_SHA256) connection keys on the device:
 // AES-128 key schedules of the payload key and the header-protection key as
 // little-endian column words (word 4r + c = bytes 4c..4c+3 of round key r),
-// the IV, per-position tables of H (hpos[j][n] = htab[0][n] x^(4 (31 - j)):
-// X * H is the XOR of hpos[j][nibble j of X], 32 independent lookups, no
-// shifts), and 4-bit GHASH tables of H^1 .. H^kGcmPow (Shoup's method; slot
-// n ^ ((k-1) & 15) of table k-1 = the nibble polynomial n times H^k, as
-// big-endian words).
-constexpr uint32_t kGcmPow = 128;
+// the IV, per-position tables of H (hpos[j][n] = n x^(4 (31 - j)) H: X * H is
+// the XOR of hpos[j][nibble j of X], 32 independent lookups, no shifts), and
+// 4-bit GHASH tables of H^4, H^8, .. H^(4 kGcmPow4) (Shoup's method; slot
+// n ^ (j & 15) of table j = the nibble polynomial n times H^(4 (j + 1)), as
+// big-endian words): the cooperative pass cuts a payload into 4-block chunks
+// aligned to its last full block, so a chunk's partial GHASH is placed by a
+// power of H^4.
+constexpr uint32_t kGcmPow = 128;  // payload blocks of the cooperative pass (2,048 B)
+constexpr uint32_t kGcmPow4 = kGcmPow / 4;
 struct QuicGcmKeyDev {
   uint32_t rk[44];   // AES-128 key schedule, words 4..39 (rounds 1-9) rotated
   uint32_t hrk[44];  // by 16 bits (sq_quic_gcm.hip aes_encrypt_n); hrk: the HP key's
   uint32_t iv[3];
   uint32_t pad;
   uint32_t hpos[32][16][4];
-  uint32_t htab[kGcmPow][16][4];
+  uint32_t htab[kGcmPow4][16][4];
 };
 
 // AES-128-GCM launch; rk0 / hrk0 / iv0 = keyring entry 0 (kernarg); t0 = the

@@ -66,6 +66,7 @@ constexpr uint32_t kGWaves = kGBlock / kWave;
 // seal 3,246 -> 3,146 us and open 3,252 -> 3,056 us against 16 packets in
 // 16-wave groups (4 waves per SIMD), three interleaved passes.
 constexpr uint32_t kGPpw = 32;
+static_assert(kGPpw <= 32, "chunk-list entries hold the packet in 5 bits (gcm_unit)");
 constexpr uint32_t kGCoopMax = 16 * kGcmPow;   // 2048 B
 
 // ---------------------------------------------------------------- AES-128
@@ -347,10 +348,9 @@ __device__ __forceinline__ void ghash_absorb(uint32_t (&y)[4], const uint32_t (&
 template <int KM>
 struct GKey {
   const uint32_t *rk, *hrk, *iv, *hpos, *htab;
-  __device__ __forceinline__ const uint32_t *pow(uint32_t k) const { return htab + 64 * (k - 1); }
-  // x <- x * H^k (k = 1 .. kGcmPow)
-  __device__ __forceinline__ void mul_pow(uint32_t (&x)[4], uint32_t k) const {
-    gmul<KM == 1>(x, pow(k), (k - 1) & 15u);
+  // x <- x * H^(4 k) (k = 1 .. kGcmPow4)
+  __device__ __forceinline__ void mul_pow4(uint32_t (&x)[4], uint32_t k) const {
+    gmul<KM == 1>(x, htab + 64 * (k - 1), (k - 1) & 15u);
   }
 };
 
@@ -448,15 +448,17 @@ __device__ __forceinline__ void gcm_run(const GKey<KM> &K, const uint32_t *tT, u
 // nothing, so Horner over the 4 slots equals Horner over the nfull blocks).
 // All four loads are issued before the first store (in place, and the fused
 // open's output 8 bytes before its input, never overwrite unread input).
-// y = the chunk's GHASH partial (Horner with H from 0).  ct32 (seal, the
-// packet's first chunk): LDS words that receive ciphertext blocks 0 and 1.
+// y = the chunk's GHASH partial: Horner with H from y0 entering before its
+// first block (the header's GHASH for a payload's first chunk, else zero).
+// ct32 (seal): the packet's LDS words that receive ciphertext blocks 0 and 1
+// (the first chunk may be short: block 1 can be the second chunk's).
 // OB: as gcm_run (okr = the key rotated to the payload start).
 template <bool OPEN, int KM, bool OB>
 __device__ __forceinline__ void gcm_chunk(const GKey<KM> &K, const uint32_t *tT, uint32_t tcol,
                                           const uint32_t (&nonce)[3], uint32_t blk0,
                                           uint32_t nfull, uint64_t src, uint64_t dst,
-                                          uint32_t (&y)[4], uint32_t *ct32,
-                                          const uint32_t (&okr)[8]) {
+                                          const uint32_t (&y0)[4], uint32_t (&y)[4],
+                                          uint32_t *ct32, const uint32_t (&okr)[8]) {
   const uint32_t z = 4u - nfull;
   const uint64_t sz = src - 16ull * z, dz = dst - 16ull * z;  // slot s at sz + 16 s
   uint32_t in[4][4];
@@ -485,8 +487,8 @@ __device__ __forceinline__ void gcm_chunk(const GKey<KM> &K, const uint32_t *tT,
       uint32_t x[4], c[4], kw[4];
 #pragma unroll
       for (int w = 0; w < 4; w++) {
-        // block s - z's half of the key: (s - z) & 1 == (s + z) & 1
-        kw[w] = OB ? bsel((s + z) & 1u, okr[4 + w], okr[w]) : 0u;
+        // the half of the key of block blk0 + s - z: parity (blk0 + s + z) & 1
+        kw[w] = OB ? bsel((blk0 + s + z) & 1u, okr[4 + w], okr[w]) : 0u;
         x[w] = (OB && OPEN) ? in[s][w] ^ kw[w] : in[s][w];
         c[w] = (x[w] ^ s2[q][w]) & live;
       }
@@ -495,15 +497,17 @@ __device__ __forceinline__ void gcm_chunk(const GKey<KM> &K, const uint32_t *tT,
         for (int w = 0; w < 4; w++) x[w] &= live;
       }
       const uint32_t(&g)[4] = OPEN ? x : c;
-      ghash_absorb(y, g);
+#pragma unroll
+      for (int w = 0; w < 4; w++)  // (the Horner state entering block 0)
+        y[w] = xor3(y[w], __builtin_bswap32(g[w]), (uint32_t)s == z ? y0[w] : 0u);
       gmul_pos<KM == 1>(y, K.hpos);
       if (s == 3 || (uint32_t)s >= z) {
         uint32_t o[4];
 #pragma unroll
         for (int w = 0; w < 4; w++) o[w] = (OB && !OPEN) ? c[w] ^ kw[w] : c[w];
         gst<u32x4_a1>(dz + 16ull * s, u32x4_a1{o[0], o[1], o[2], o[3]});
-        if (!OPEN && ct32 && blk0 == 0 && (uint32_t)s - z < 2u)
-          *(u32x4 *)(ct32 + 4 * ((uint32_t)s - z)) = u32x4{c[0], c[1], c[2], c[3]};
+        const uint32_t bi = blk0 + (uint32_t)s - z;  // the payload's block index
+        if (!OPEN && ct32 && bi < 2u) *(u32x4 *)(ct32 + 4 * bi) = u32x4{c[0], c[1], c[2], c[3]};
       }
     }
   }
@@ -524,10 +528,11 @@ __device__ __forceinline__ void gcm_hp_mask(const GKey<KM> &K, const uint32_t *t
 
 struct alignas(16) GRec {
   uint64_t src, dst;   // payload start in the input / output
-  uint32_t pl, start;  // payload bytes; first flat chunk
+  uint32_t pl, pad0;   // payload bytes
   uint32_t np, kid;    // payload blocks (16 B); keyring index
   uint32_t nonce[3], pad;
   uint32_t x[4];       // GHASH accumulator (big-endian words), ds_xor target
+  uint32_t yh[4];      // the header's GHASH (joins the first chunk's Horner)
   uint32_t ct32[8];    // ciphertext bytes 0..31 (the header-protection sample)
   uint32_t okr[8];     // fused Salamander layer: key rotated to the payload start
 };
@@ -559,7 +564,7 @@ __device__ __forceinline__ void stage_key(const QuicGcmKeyDev *E, uint32_t *tP, 
                                           uint32_t *tK) {
   if (threadIdx.x < 3) tK[88 + threadIdx.x] = E->iv[threadIdx.x];  // (round keys: scalar loads)
   const uint32_t *src = &E->hpos[0][0][0];  // hpos then htab, contiguous
-  for (uint32_t i = threadIdx.x; i < (32 + kGcmPow) * 16; i += kGBlock) {
+  for (uint32_t i = threadIdx.x; i < (32 + kGcmPow4) * 16; i += kGBlock) {
     const u32x4 v = gld<u32x4>((uint64_t)(src + 4 * i));
     if (i < 32 * 16) *(u32x4 *)(tP + 4 * i) = v;
     else *(u32x4 *)(tH + 4 * (i - 32 * 16)) = v;
@@ -573,7 +578,8 @@ template <bool OPEN, bool MULTI, bool OB, bool STAGED>
 __device__ __forceinline__ void gcm_unit(const QGParams &Q, uint64_t base, uint32_t cnt,
                                          uint32_t skid, uint32_t lane,
                                          const uint32_t *tT, uint32_t tcol, const uint32_t *tP,
-                                         const uint32_t *tH, const uint32_t *tK, GRec *recs) {
+                                         const uint32_t *tH, const uint32_t *tK, GRec *recs,
+                                         uint16_t *clist) {
   constexpr int KM = MULTI ? 1 : (STAGED ? 2 : 0);
   // the unit's packets: positions [base, base + cnt) (grouped batches: of
   // the key order)
@@ -720,30 +726,40 @@ __device__ __forceinline__ void gcm_unit(const QGParams &Q, uint64_t base, uint3
   }
   const bool coop = live && pl <= kGCoopMax;
   const uint32_t np = (pl + 15) / 16;
-  // the header's GHASH, placed ahead of the payload blocks
-  if (coop && np) K.mul_pow(y, np);
-  // chunks of the cooperative pass: the full blocks, 4 per chunk (the last,
-  // partial block is the owner's, phase 3)
+  // chunks of the cooperative pass: the full blocks, 4 per chunk, aligned to
+  // the last full one (the first chunk may be short; the last, partial block
+  // is the owner's, phase 3).  The header's GHASH enters the first chunk's
+  // Horner, so every chunk's partial is placed by a power of H^4.
   const uint32_t nblk = coop ? (pl / 16 + 3) / 4 : 0u;
-  uint32_t incl = nblk;
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    const uint32_t t = __shfl_up(incl, d, kWave);
-    if (lane >= (uint32_t)d) incl += t;
+  // The unit's chunks in k-major order (k = chunks from the payload's end):
+  // entry f of clist = packet | k << 5 -- every packet's last chunk, then
+  // every packet's second last, ... (phase 2 walks the list from its end).
+  // The lanes of a step then mostly
+  // share k, so their multiplies by H^4k read ONE Shoup table (a lane group
+  // reading different tables met in the same banks: ~15 % of the LDS's
+  // cycles were conflicts), and their accumulations go to different packets.
+  uint32_t T = 0;  // (wave-uniform)
+  for (uint32_t k = 0;; k++) {
+    const uint64_t M = __ballot(nblk > k);  // (owner lanes only: bits 0..31)
+    if (!M) break;
+    if (nblk > k)
+      clist[T + __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u)] = (uint16_t)(lane | (k << 5));
+    T += (uint32_t)__popcll(M);
   }
-  const uint32_t start = incl - nblk, T = __shfl(incl, kWave - 1, kWave);
   if (lane < kGPpw) {
     GRec &R = recs[lane];
     R.src = src + hdr;
     R.dst = dst + hdr;
     R.pl = pl;
-    R.start = start;
     R.np = np;
     R.kid = kid;
 #pragma unroll
     for (int i = 0; i < 3; i++) R.nonce[i] = nonce[i];
 #pragma unroll
-    for (int i = 0; i < 4; i++) R.x[i] = coop ? y[i] : 0u;
+    for (int i = 0; i < 4; i++) {
+      R.x[i] = coop && nblk == 0 ? y[i] : 0u;
+      R.yh[i] = y[i];
+    }
 #pragma unroll
     for (int i = 0; i < 8; i++) R.ct32[i] = 0u;
     if (OB) {
@@ -758,23 +774,29 @@ __device__ __forceinline__ void gcm_unit(const QGParams &Q, uint64_t base, uint3
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
-  // ---- 2. cooperative payload pass over the flat chunk space
+  // ---- 2. cooperative payload pass over the chunk list
   for (uint32_t base = 0; base < T; base += kWave) {
     const uint32_t f = base + lane;
-    const uint32_t pp = q_locate(start, base, f < T ? f : T - 1);
     if (f < T) {
-      GRec &R = recs[pp];
+      // (read from the end: a packet's chunks run in address order -- the
+      // fused open writes its output 8 bytes before its input, so a chunk
+      // must never run after the one behind it)
+      const uint32_t e = clist[T - 1 - f], k = e >> 5;
+      GRec &R = recs[e & 31u];
       const GKey<KM> KB = key_of<MULTI, STAGED>(Q, R.kid, tP, tH, tK);
-      const uint32_t b = f - R.start, left = R.pl / 16 - 4 * b;  // full blocks from here
-      const uint32_t nfull = left < 4 ? left : 4u;
+      // chunk k from the end: full blocks [end - nfull, end), end = npf - 4 k
+      const uint32_t npf = R.pl / 16, b = (npf + 3) / 4 - 1 - k;
+      const uint32_t end = npf - 4 * k, nfull = end < 4 ? end : 4u;
       const uint32_t rn[3] = {R.nonce[0], R.nonce[1], R.nonce[2]};
-      uint32_t yb[4], rokr[8];
+      uint32_t yb[4], rokr[8], y0[4];
 #pragma unroll
       for (int i = 0; i < 8; i++) rokr[i] = OB ? R.okr[i] : 0u;
-      gcm_chunk<OPEN, KM, OB>(KB, tT, tcol, rn, 4 * b, nfull, R.src + 64ull * b,
-                              R.dst + 64ull * b, yb, R.ct32, rokr);
-      const uint32_t m = R.np - 4 * b - nfull;  // payload blocks after this chunk
-      if (m) KB.mul_pow(yb, m);
+#pragma unroll
+      for (int i = 0; i < 4; i++) y0[i] = b == 0 ? R.yh[i] : 0u;
+      gcm_chunk<OPEN, KM, OB>(KB, tT, tcol, rn, end - nfull, nfull,
+                              R.src + 16ull * (end - nfull), R.dst + 16ull * (end - nfull), y0,
+                              yb, R.ct32, rokr);
+      if (k) KB.mul_pow4(yb, k);  // 4 k full blocks follow
 #pragma unroll
       for (int i = 0; i < 4; i++) atomicXor(&R.x[i], yb[i]);
     }
@@ -794,7 +816,7 @@ __device__ __forceinline__ void gcm_unit(const QGParams &Q, uint64_t base, uint3
 #pragma unroll
     for (int i = 0; i < 8; i++) ct32[i] = recs[lane].ct32[i];
     const uint32_t nb = pl & 15u;
-    if (nb) {  // the payload's last, partial block: C * H joins the chunks' sum
+    if (nb) {  // the payload's last, partial block
       const uint32_t k = pl / 16;
       const uint64_t ps = src + hdr + 16ull * k;
       uint32_t x[4], c[4], ks[4] = {nonce[0], nonce[1], nonce[2], __builtin_bswap32(2u + k)};
@@ -808,11 +830,8 @@ __device__ __forceinline__ void gcm_unit(const QGParams &Q, uint64_t base, uint3
         if (OB && OPEN) x[w] ^= kw[w];
         c[w] = (x[w] ^ ks[w]) & m;
       }
-      uint32_t t[4] = {0u, 0u, 0u, 0u};
-      ghash_absorb(t, OPEN ? x : c);
-      gmul_pos<MULTI>(t, K.hpos);
-#pragma unroll
-      for (int w = 0; w < 4; w++) y[w] ^= t[w];
+      ghash_absorb(y, OPEN ? x : c);  // (the chunks' sum is placed up to the
+      gmul_pos<MULTI>(y, K.hpos);      // last full block: times H once more)
       uint32_t o[4];
 #pragma unroll
       for (int w = 0; w < 4; w++) o[w] = (OB && !OPEN) ? c[w] ^ kw[w] : c[w];
@@ -891,17 +910,21 @@ __device__ __forceinline__ void gcm_unit(const QGParams &Q, uint64_t base, uint3
 // from one v_perm, the image's base is the immediate), the power tables
 // (32 KiB), the staged key words (TK), then the waves' records.  TABLES
 // false (per-packet keys from global memory): no position or power tables.
+constexpr uint32_t kGList = kGPpw * kGcmPow4;  // chunk-list entries per wave
 template <bool TABLES, uint32_t TK>
-constexpr uint32_t kLdsWords = (TABLES ? 32 * 64 + kGcmPow * 64 : 0u) + 256 * 64 +
-                               (TK + 3) / 4 * 4 + (uint32_t)sizeof(GRec) * kGWaves * kGPpw / 4;
+constexpr uint32_t kLdsWords = (TABLES ? 32 * 64 + kGcmPow4 * 64 : 0u) + 256 * 64 +
+                               (TK + 3) / 4 * 4 + (uint32_t)sizeof(GRec) * kGWaves * kGPpw / 4 +
+                               kGWaves * kGList / 2;
 template <bool TABLES, uint32_t TK>
 __device__ __forceinline__ void gcm_lds(uint32_t *lds, uint32_t *&tP, uint32_t *&tT, uint32_t *&tH,
-                                        uint32_t *&tK, GRec (*&recs)[kGPpw]) {
+                                        uint32_t *&tK, GRec (*&recs)[kGPpw],
+                                        uint16_t (*&clists)[kGList]) {
   tP = lds;
   tT = lds + (TABLES ? 32 * 64 : 0);
   tH = tT + 256 * 64;
-  tK = tH + (TABLES ? kGcmPow * 64 : 0);
+  tK = tH + (TABLES ? kGcmPow4 * 64 : 0);
   recs = reinterpret_cast<GRec(*)[kGPpw]>(tK + (TK + 3) / 4 * 4);
+  clists = reinterpret_cast<uint16_t(*)[kGList]>(recs + kGWaves);
 }
 
 // The T-table image (every launch) and, single key, the key's GHASH tables,
@@ -916,7 +939,7 @@ __device__ __forceinline__ void stage_common(const QGParams &Q, uint32_t *tT, ui
   }
   if (!MULTI) {
     const uint32_t *src = &Q.keys[0].hpos[0][0][0];  // hpos then htab, contiguous
-    for (uint32_t i = threadIdx.x; i < (32 + kGcmPow) * 16; i += kGBlock) {
+    for (uint32_t i = threadIdx.x; i < (32 + kGcmPow4) * 16; i += kGBlock) {
       const u32x4 v = gld<u32x4>((uint64_t)(src + 4 * i));
       if (i < 32 * 16) *(u32x4 *)(tP + 4 * i) = v;
       else *(u32x4 *)(tH + 4 * (i - 32 * 16)) = v;
@@ -933,7 +956,8 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords<!MULTI, 4>];
   uint32_t *tP, *tT, *tH, *tK;
   GRec(*recs)[kGPpw];
-  gcm_lds<!MULTI, 4>(lds, tP, tT, tH, tK, recs);
+  uint16_t(*clists)[kGList];
+  gcm_lds<!MULTI, 4>(lds, tP, tT, tH, tK, recs, clists);
   const uint64_t units = ((uint64_t)Q.n + kGPpw - 1) / kGPpw;
   stage_common<MULTI>(Q, tT, tP, tH, tK);
   __syncthreads();
@@ -943,7 +967,8 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_kernel(const QGParams Q) {
   for (uint64_t u = (uint64_t)blockIdx.x * kGWaves + wv; u < units; u += stride) {
     const uint64_t base = u * kGPpw;
     const uint32_t cnt = Q.n - base < kGPpw ? (uint32_t)(Q.n - base) : kGPpw;
-    gcm_unit<OPEN, MULTI, OB, false>(Q, base, cnt, 0u, lane, tT, tcol, tP, tH, tK, recs[wv]);
+    gcm_unit<OPEN, MULTI, OB, false>(Q, base, cnt, 0u, lane, tT, tcol, tP, tH, tK, recs[wv],
+                                     clists[wv]);
   }
 }
 
@@ -963,7 +988,8 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_staged_kernel(const QGParams
   __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords<true, 92>];
   uint32_t *tP, *tT, *tH, *tK;  // tK[88..90]: the staged key's IV
   GRec(*recs)[kGPpw];
-  gcm_lds<true, 92>(lds, tP, tT, tH, tK, recs);
+  uint16_t(*clists)[kGList];
+  gcm_lds<true, 92>(lds, tP, tT, tH, tK, recs, clists);
   stage_common<true>(Q, tT, tP, tH, tK);
   __syncthreads();
   const uint32_t lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
@@ -996,7 +1022,7 @@ __global__ __launch_bounds__(kGBlock) void quic_gcm_staged_kernel(const QGParams
     if (first >= cnt_k) continue;
     const uint32_t cnt = cnt_k - first < kGPpw ? (uint32_t)(cnt_k - first) : kGPpw;
     gcm_unit<OPEN, false, OB, true>(Q, (uint64_t)rfl32(kstart[k]) + first, cnt, k,
-                                    lane, tT, tcol, tP, tH, tK, recs[wv]);
+                                    lane, tT, tcol, tP, tH, tK, recs[wv], clists[wv]);
   }
 }
 
