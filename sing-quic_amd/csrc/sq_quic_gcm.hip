@@ -135,17 +135,20 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 // -- 3 VALU ops per column besides the 4 v_perm addresses; the key schedule
 // holds rounds 1-9 already rotated (sq_api.hip gcm_key).  The last round
 // takes the S-box byte (T0 byte 1, T1 bytes 2 and 3) instead.
-template <int KM, int NB>
+// R0 > 1: s holds the state entering round R0 (aes_ctr_n).
+template <int KM, int NB, int R0 = 1>
 __device__ __forceinline__ void aes_encrypt_n(const uint32_t *rk, const uint32_t *tT, uint32_t lo,
                                               uint32_t (&s)[NB][4]) {
   uint32_t k[4];
-  round_key<KM>(rk, 0, k);
+  if (R0 == 1) {
+    round_key<KM>(rk, 0, k);
 #pragma unroll
-  for (int q = 0; q < NB; q++)
+    for (int q = 0; q < NB; q++)
 #pragma unroll
-    for (int c = 0; c < 4; c++) s[q][c] ^= k[c];
+      for (int c = 0; c < 4; c++) s[q][c] ^= k[c];
+  }
 #pragma unroll
-  for (int r = 1; r < 10; r++) {
+  for (int r = R0; r < 10; r++) {
     uint32_t kr[4];  // (rotated by 16 in the key schedule)
     round_key<KM>(rk, r, kr);
     uint32_t t[NB][4];
@@ -181,6 +184,68 @@ __device__ __forceinline__ void aes_encrypt_n(const uint32_t *rk, const uint32_t
   for (int q = 0; q < NB; q++)
 #pragma unroll
     for (int c = 0; c < 4; c++) s[q][c] = t[q][c];
+}
+
+// Counter blocks nonce || be32(c) with c < 256 (a cooperative chunk's
+// blocks: c = 2 + block index <= 129) differ only in byte 15.  Round 1 then
+// varies in one lookup (that byte, into column 0), round 2 in four (column
+// 0's bytes, one into each column): the rest of both rounds is the same for
+// every block of a packet.  aes_ctr_pre computes those parts once per chunk
+// (27 lookups); aes_ctr_n then runs a block's rounds 1 and 2 in 5 lookups and
+// 12 VALU instead of 32 and ~60, and rounds 3-10 as aes_encrypt_n.
+struct CtrPre {
+  uint32_t c0;     // round-1 column 0 without the counter byte's term
+  uint32_t f[4];   // round-2 columns without column 0's terms
+  uint32_t k15;    // round key 0, byte 15 (the counter byte's key byte)
+};
+template <int KM>
+__device__ __forceinline__ void aes_ctr_pre(const uint32_t *rk, const uint32_t *tT, uint32_t lo,
+                                            const uint32_t (&nonce)[3], CtrPre &P) {
+  uint32_t k[4], kr[4];
+  round_key<KM>(rk, 0, k);
+  // round 0; word 3 = the counter's zero bytes 0..2 under the key (byte 3
+  // varies: unused here)
+  const uint32_t s[4] = {nonce[0] ^ k[0], nonce[1] ^ k[1], nonce[2] ^ k[2], k[3]};
+  P.k15 = k[3] >> 24;
+  round_key<KM>(rk, 1, kr);  // (rotated by 16)
+  uint32_t c[4];
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint32_t a0 = t0at(tT, trow(s[q], lo, 0));
+    const uint32_t a1 = t1at(tT, trow(s[(q + 1) & 3], lo, 1));
+    const uint32_t a2 = t0at(tT, trow(s[(q + 2) & 3], lo, 2));
+    const uint32_t a3 = q == 0 ? 0u : t1at(tT, trow(s[(q + 3) & 3], lo, 3));
+    c[q] = xor3(a0, a1, rotl(xor3(a2, a3, kr[q]), 16));
+  }
+  P.c0 = c[0];
+  round_key<KM>(rk, 2, kr);
+  // round 2 over {col0, c1, c2, c3}: column q reads col0's byte (4 - q) & 3
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint32_t a0 = q == 0 ? 0u : t0at(tT, trow(c[q], lo, 0));
+    const uint32_t a1 = q == 3 ? 0u : t1at(tT, trow(c[(q + 1) & 3], lo, 1));
+    const uint32_t a2 = q == 2 ? 0u : t0at(tT, trow(c[(q + 2) & 3], lo, 2));
+    const uint32_t a3 = q == 1 ? 0u : t1at(tT, trow(c[(q + 3) & 3], lo, 3));
+    P.f[q] = xor3(a0, a1, rotl(xor3(a2, a3, kr[q]), 16));
+  }
+}
+// keystream blocks for counters ctr[q] (< 256) under P's nonce and key
+template <int KM, int NB>
+__device__ __forceinline__ void aes_ctr_n(const uint32_t *rk, const uint32_t *tT, uint32_t lo,
+                                          const CtrPre &P, const uint32_t (&ctr)[NB],
+                                          uint32_t (&s)[NB][4]) {
+#pragma unroll
+  for (int q = 0; q < NB; q++) {
+    // round 1: column 0 = c0 ^ T3[counter byte ^ key byte]
+    const uint32_t x = (ctr[q] ^ P.k15) & 0xFFu;
+    const uint32_t col0 = P.c0 ^ rotl(t1at(tT, __builtin_amdgcn_perm(lo, x, 0x0C0C0004u)), 16);
+    // round 2: each column's one term from col0
+    s[q][0] = P.f[0] ^ t0at(tT, trow(col0, lo, 0));
+    s[q][1] = P.f[1] ^ rotl(t1at(tT, trow(col0, lo, 3)), 16);
+    s[q][2] = P.f[2] ^ rotl(t0at(tT, trow(col0, lo, 2)), 16);
+    s[q][3] = P.f[3] ^ t1at(tT, trow(col0, lo, 1));
+  }
+  aes_encrypt_n<KM, NB, 3>(rk, tT, lo, s);
 }
 
 template <int KM>
@@ -474,12 +539,14 @@ __device__ __forceinline__ void gcm_chunk(const GKey<KM> &K, const uint32_t *tT,
   }
 #pragma unroll
   for (int w = 0; w < 4; w++) y[w] = 0u;
-  const uint32_t ctr = 2u + blk0 - z;  // slot 0's counter
+  const uint32_t ctr = 2u + blk0 - z;  // slot 0's counter (live slots: <= 129)
+  CtrPre P;
+  aes_ctr_pre<KM>(K.rk, tT, tcol, nonce, P);
 #pragma unroll
   for (int h = 0; h < 4; h += 2) {
-    uint32_t s2[2][4] = {{nonce[0], nonce[1], nonce[2], __builtin_bswap32(ctr + h)},
-                         {nonce[0], nonce[1], nonce[2], __builtin_bswap32(ctr + h + 1)}};
-    aes_encrypt_n<KM, 2>(K.rk, tT, tcol, s2);
+    uint32_t s2[2][4];
+    const uint32_t cq[2] = {ctr + h, ctr + h + 1};
+    aes_ctr_n<KM, 2>(K.rk, tT, tcol, P, cq, s2);
 #pragma unroll
     for (int q = 0; q < 2; q++) {
       const int s = h + q;
