@@ -31,8 +31,17 @@ SETS = {
         "w16p32": [("constexpr uint32_t kGBlock = 768;", "constexpr uint32_t kGBlock = 1024;")],
     },
 }
+SETS["shoup"] = {"e_sunroll": [("""#pragma unroll 1
+  for (int i = 0; i < 4; i++) {
+    const uint32_t w4 = w << 4;
+    uint32_t z4 = 0;""", """#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    asm volatile("" : "+v"(w), "+v"(z0), "+v"(z1), "+v"(z2), "+v"(z3));
+    const uint32_t w4 = w << 4;
+    uint32_t z4 = 0;""")]}
 VARIANTS = SETS[sys.argv[1] if len(sys.argv) > 1 else "ablate"]
-shutil.rmtree(os.path.join(REPO, "build", "ablate"), ignore_errors=True)
+if not os.environ.get("KEEP"):  # (KEEP=1: add to scripts/dev/ab_head.sh's builds)
+    shutil.rmtree(os.path.join(REPO, "build", "ablate"), ignore_errors=True)
 objs = [os.path.join(PKG, "build", "obj", f + ".o")
         for f in ("sq_kernels", "sq_quic", "sq_api", "packet_conn", "udp_batch", "pconn", "sq_cpu")]
 src = open(SRC).read()

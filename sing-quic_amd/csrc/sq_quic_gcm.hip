@@ -177,8 +177,10 @@ __device__ __forceinline__ void aes_encrypt_n(const uint32_t *rk, const uint32_t
       const uint32_t a1 = t0at(tT, trow(s[q][(c + 1) & 3], lo, 1));
       const uint32_t a2 = t1at(tT, trow(s[q][(c + 2) & 3], lo, 2));
       const uint32_t a3 = t1at(tT, trow(s[q][(c + 3) & 3], lo, 3));
-      t[q][c] = (((a0 >> 8) & 0xFFu) | (a1 & 0xFF00u) | (a2 & 0xFF0000u) | (a3 & 0xFF000000u)) ^
-                k[c];
+      // S-box bytes: T0 byte 1 (a0, a1), T1 bytes 2 and 3 (a2, a3), two v_perm
+      // into complementary bytes, then one three-input XOR with the key
+      t[q][c] = xor3(__builtin_amdgcn_perm(a1, a0, 0x0C0C0501u),
+                     __builtin_amdgcn_perm(a3, a2, 0x07020C0Cu), k[c]);
     }
 #pragma unroll
   for (int q = 0; q < NB; q++)
