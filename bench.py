@@ -591,7 +591,7 @@ def quic_valu_roofline(suite_name: str, op: str, kernel_us: float):
     against 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction
     (`frac`) and against the measured integer issue rate
     (`frac_of_measured_int_rate`)."""
-    for rnd in ("r05", "r04", "r03", "r02"):  # the newest committed pass
+    for rnd in ("r06", "r05", "r04", "r03", "r02"):  # the newest committed pass
         f = os.path.join(REPO, "profiles", rnd, "quic", "quic_pmc_summary.json")
         if os.path.exists(f):
             break
