@@ -352,7 +352,7 @@ typedef struct sqobfs_quic_batch {
 /* A keyring holds connections of ONE suite (a batch is sealed / opened
  * with the keyring's suite).  sqobfs_quic_keyring_create is the
  * ChaCha20-Poly1305 form.  For AES-128-GCM the key schedules and the GHASH
- * tables (about 33 KiB per connection) are prepared here, once. */
+ * tables (about 16.5 KiB per connection) are prepared here, once. */
 int sqobfs_quic_keyring_create_suite(sqobfs_ctx *ctx, uint32_t suite, uint32_t count,
                                      const sqobfs_quic_key *keys, sqobfs_quic_keyring **out);
 int sqobfs_quic_keyring_create(sqobfs_ctx *ctx, uint32_t count, const sqobfs_quic_key *keys,
