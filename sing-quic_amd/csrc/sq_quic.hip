@@ -14,13 +14,16 @@
 // Decomposition (quic_kernel below): 32 packets per wave, three phases.
 //   1. owner lane per packet: descriptor, header protection off (open), the
 //      Poly1305 key block and the MAC over the header;
-//   2. all 64 lanes: the packets' 64-byte ChaCha20 keystream blocks
-//      (counter 1..) as one flat space, one block per lane per step, so
-//      consecutive lanes read and write consecutive bytes; each lane's four
+//   2. all 64 lanes: the packets' FULL 64-byte blocks (keystream counter
+//      1..) as one flat space, one block per lane per step, so consecutive
+//      lanes read and write consecutive bytes (unaligned 16-byte loads and
+//      stores: no realignment, no partial stores); each lane's four
 //      ciphertext chunks are Horner-ed into a partial MAC (26-bit limbs,
 //      v_mad_u64_u32 products) and lane pairs fold theirs;
-//   3. owner lane: the partials combined with powers of r, the tag, and
-//      (seal) the header-protection mask from the ciphertext sample.
+//   3. owner lane: the partials combined with powers of r, the payload's
+//      tail (its last pl % 64 bytes: keystream block from the lane pairs,
+//      byte-exact stores), the tag, and (seal) the header-protection mask
+//      from the ciphertext sample.
 // The owner phases' ChaCha20 blocks are shared by lanes l and l + 32
 // (lane pairs).  Payloads past the cooperative range are walked by their
 // owner lane with a streaming realigner (payload_pass): aligned 16-byte
@@ -381,104 +384,81 @@ struct alignas(16) QRec {
   uint32_t kid, nblk;     // key index; keystream blocks (64 bytes each)
   uint32_t nonce[3];
   uint32_t r[5];          // Poly1305 r (26-bit limbs; the 5 r terms are formed on use)
-  uint32_t r4[5], rl[5];  // pairs: r^4 and r^klast (chunks of the last block)
-  uint32_t pad[2];
+  uint32_t r4[5];         // pairs: r^4
+  uint32_t pad[7];
   uint32_t ct32[8];       // ciphertext bytes 0..31 (the header-protection sample)
   uint32_t okr[8];        // fused Salamander layer: key rotated to the payload start
 };
 static_assert(sizeof(QRec) == 176, "QRec layout");
 
-// One 64-byte keystream block of one packet (cooperative pass, any lane):
-// XOR up to 64 payload bytes, Horner their <= 4 MAC blocks from h = 0 with
-// the packet's r, realign into aligned 16-byte output stores.
-// Input of one 64-byte block: the aligned 16-byte blocks covering
-// [S, S + 64), S = payload + 64 b, clamped to the ones holding valid bytes
-// (zero past the end).
-__device__ __forceinline__ void coop_load(const QRec &R, uint32_t b, uint32_t (&blk)[5][4]) {
-  const uint32_t off0 = 64 * b;
-  const uint64_t S = R.src + off0, last = (R.src + R.pl - 1) & ~15ull;
-  const uint32_t ib = (uint32_t)(S & 15);
-#pragma unroll
-  for (int i = 0; i < 5; i++) {
-    const uint64_t A = S - ib + 16ull * i;
-    const u32x4 x = gld<u32x4>(A < last ? A : last);
-    const bool ok = A <= last;
-    blk[i][0] = ok ? x.x : 0u; blk[i][1] = ok ? x.y : 0u;
-    blk[i][2] = ok ? x.z : 0u; blk[i][3] = ok ? x.w : 0u;
-  }
-}
-
-// Junctions: the aligned output block a lane shares with the lane
-// holding the packet's next keystream block is written whole, once, by the
-// later lane (its head bytes OR the earlier lane's tail bytes, over a lane
-// shuffle) instead of as two byte-exact partial stores.  merge_head: this
-// lane's first output block is such a junction (skip it here; `head` = its
-// bytes [oa, 16), zero below); give_tail: its last one is (skip it; `tail` =
-// its bytes [0, oa), zero above).
+// One full 64-byte block b of one packet (cooperative pass, any lane): four
+// unaligned 16-byte loads (issued before the keystream block), XOR, the
+// chunks' Horner from h = 0 with the packet's r (partial MAC), four
+// unaligned 16-byte stores.  gfx950 under the HSA runtime's unaligned mode
+// moves a 16-byte access at any byte address in one instruction, so the
+// round-5 realignment (five aligned loads and funnel shifts in, funnels and
+// a shared "junction" block between neighbouring lanes out, byte-exact
+// partial stores at a packet's ends) is gone; only full blocks come here
+// (a payload's tail is its owner's, phase 3).  All loads precede the
+// stores: in place, and the fused open's output 8 bytes before its input,
+// never overwrite unread input (a block's stores reach 8 bytes into the
+// previous block, read by an earlier lane or step).
 template <bool OPEN, bool OB>
-__device__ __forceinline__ void coop_block(const QuicKeyDev &K, QRec &R, uint32_t b,
-                                           const uint32_t (&blk)[5][4], uint32_t (&contrib)[5],
-                                           bool merge_head, bool give_tail, uint32_t (&head)[4],
-                                           uint32_t (&tail)[4]) {
+__device__ __forceinline__ void coop_full(const QuicKeyDev &K, QRec &R, uint32_t b,
+                                          uint32_t (&contrib)[5]) {
+  const uint64_t S = R.src + 64ull * b, D = R.dst + 64ull * b;
+  uint32_t in[4][4];
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const u32x4 v = gld<u32x4_a1>(S + 16ull * q);
+    in[q][0] = v.x; in[q][1] = v.y; in[q][2] = v.z; in[q][3] = v.w;
+  }
   uint32_t ks[16];
   chacha20_block(K.key, 1 + b, R.nonce, ks);
-  const uint32_t off0 = 64 * b, nv = R.pl - off0 < 64 ? R.pl - off0 : 64;
-  const uint32_t ib = (uint32_t)((R.src + off0) & 15);
   Poly L;
   L.r0 = R.r[0]; L.r1 = R.r[1]; L.r2 = R.r[2]; L.r3 = R.r[3]; L.r4 = R.r[4];
   L.s1 = L.r1 * 5; L.s2 = L.r2 * 5; L.s3 = L.r3 * 5; L.s4 = L.r4 * 5;
   L.h0 = L.h1 = L.h2 = L.h3 = L.h4 = 0;
-  uint32_t o[4][4];
 #pragma unroll
-  for (uint32_t q = 0; q < 4; q++) {
-    const int nb = (int)nv - 16 * (int)q;  // valid bytes of this chunk (may be <= 0)
-    uint32_t in[4];
-    funnel(blk[q], blk[q + 1], ib, in);
+  for (int q = 0; q < 4; q++) {
+    uint32_t x[4], c[4];
 #pragma unroll
     for (int w = 0; w < 4; w++) {
-      in[w] &= range_mask(0, nb, w);
-      if (OB && OPEN) in[w] ^= R.okr[(4 * q + w) & 7] & range_mask(0, nb, w);
-      o[q][w] = (in[w] ^ ks[4 * q + w]) & range_mask(0, nb, w);
+      // (the key's half of chunk q: byte offset 64 b + 16 q, mod 32)
+      x[w] = (OB && OPEN) ? in[q][w] ^ R.okr[4 * (q & 1) + w] : in[q][w];
+      c[w] = x[w] ^ ks[4 * q + w];
     }
-    if (nb > 0) {
-      if (OPEN) poly_block(L, in);
-      else poly_block(L, o[q]);
-    }
+    if (OPEN) poly_block(L, x);
+    else poly_block(L, c);
     if (!OPEN && b == 0 && q < 2) {
 #pragma unroll
-      for (int w = 0; w < 4; w++) R.ct32[4 * q + w] = o[q][w];
+      for (int w = 0; w < 4; w++) R.ct32[4 * q + w] = c[w];
     }
     if (OB && !OPEN) {
 #pragma unroll
-      for (int w = 0; w < 4; w++) o[q][w] ^= R.okr[(4 * q + w) & 7] & range_mask(0, nb, w);
+      for (int w = 0; w < 4; w++) c[w] ^= R.okr[4 * (q & 1) + w];
     }
+    gst<u32x4_a1>(D + 16ull * q, u32x4_a1{c[0], c[1], c[2], c[3]});
   }
   contrib[0] = L.h0; contrib[1] = L.h1; contrib[2] = L.h2; contrib[3] = L.h3; contrib[4] = L.h4;
-  // output: realign the 64 bytes at D into aligned 16-byte blocks; the first
-  // and last are shared with the neighbouring blocks' lanes (partial stores)
-  const uint64_t D = R.dst + off0;
-  const uint32_t oa = (uint32_t)(D & 15);
-  const uint32_t zero[4] = {0u, 0u, 0u, 0u};
+}
+
+// ChaCha20 block `counter` under each owner lane's key and nonce, all 16
+// words in the owner (low) lane (lane pairs: every lane must call it).
+template <bool MULTI>
+__device__ __forceinline__ void ks_lanes(const QuicKeyDev *K, uint32_t counter,
+                                         const uint32_t (&nonce)[3], uint32_t lane,
+                                         uint32_t (&ks)[16]) {
+  const bool hi = lane >= kWave / 2;
+  const QuicKeyDev *KP = MULTI ? xlow_ptr(K, hi) : K;
+  uint32_t o[8];
+  chacha20_pair(KP->key, counter, nonce[0], nonce[1], nonce[2], hi, o);
 #pragma unroll
-  for (uint32_t j = 0; j < 5; j++) {
-    uint32_t ob[4];
-    funnel(j == 0 ? zero : o[j - 1], j == 4 ? zero : o[j], 16 - oa, ob);
-    const uint32_t lo = j == 0 ? oa : 0u;
-    const int hi_i = (int)(oa + nv) - 16 * (int)j;
-    const uint32_t hi = hi_i < 16 ? (uint32_t)(hi_i > 0 ? hi_i : 0) : 16u;
-    if (j == 0) {
-#pragma unroll
-      for (int w = 0; w < 4; w++) head[w] = ob[w];
-    }
-    if (j == 4) {
-#pragma unroll
-      for (int w = 0; w < 4; w++) tail[w] = ob[w];
-    }
-    const bool skip = (j == 0 && merge_head) || (j == 4 && give_tail);
-    if (hi > lo && !skip) {
-      if (lo == 0 && hi == 16) gst<u32x4>(D - oa + 16ull * j, u32x4{ob[0], ob[1], ob[2], ob[3]});
-      else store_partial(D - oa + 16ull * j, ob, lo, hi);
-    }
+  for (int i = 0; i < 4; i++) {  // low lane: words 4i, 4i+1; high lane: 4i+2, 4i+3
+    ks[4 * i] = o[2 * i];
+    ks[4 * i + 1] = o[2 * i + 1];
+    ks[4 * i + 2] = xhalf(o[2 * i], hi);
+    ks[4 * i + 3] = xhalf(o[2 * i + 1], hi);
   }
 }
 
@@ -650,9 +630,7 @@ __global__ __launch_bounds__(kQBlock, kQMinWaves) void quic_kernel(const QParams
     }
   }
   const bool coop = live && pl <= kQCoopMax;
-  const uint32_t nblk = coop ? (pl + 63) / 64 : 0u;
-  // chunks of the last block (1..4) and, for pairs, r^2..r^4
-  const uint32_t klast = nblk ? ((pl - 64 * (nblk - 1)) + 15) / 16 : 1u;
+  const uint32_t nblk = coop ? pl / 64 : 0u;  // full blocks (the tail is phase 3's)
   const uint32_t nflat = (nblk + 1) & ~1u;
   uint32_t incl = nflat;
 #pragma unroll
@@ -673,17 +651,12 @@ __global__ __launch_bounds__(kQBlock, kQMinWaves) void quic_kernel(const QParams
     for (int i = 0; i < 3; i++) R.nonce[i] = nonce[i];
     R.r[0] = P.r0; R.r[1] = P.r1; R.r[2] = P.r2; R.r[3] = P.r3; R.r[4] = P.r4;
     if (nblk) {
-      // X.h = r^k for k = 2, 3, 4 (X.r = r)
+      // X.h = r^4 (X.r = r)
       Poly X = P;
       X.h0 = P.r0; X.h1 = P.r1; X.h2 = P.r2; X.h3 = P.r3; X.h4 = P.r4;
-      uint32_t l0 = X.h0, l1 = X.h1, l2 = X.h2, l3 = X.h3, l4 = X.h4;  // r^klast
 #pragma unroll
-      for (uint32_t k = 2; k <= 4; k++) {
-        poly_mul(X);
-        if (klast == k) { l0 = X.h0; l1 = X.h1; l2 = X.h2; l3 = X.h3; l4 = X.h4; }
-      }
+      for (uint32_t k = 2; k <= 4; k++) poly_mul(X);
       R.r4[0] = X.h0; R.r4[1] = X.h1; R.r4[2] = X.h2; R.r4[3] = X.h3; R.r4[4] = X.h4;
-      R.rl[0] = l0; R.rl[1] = l1; R.rl[2] = l2; R.rl[3] = l3; R.rl[4] = l4;
     }
 #pragma unroll
     for (int i = 0; i < 8; i++) R.ct32[i] = 0u;
@@ -706,29 +679,9 @@ __global__ __launch_bounds__(kQBlock, kQMinWaves) void quic_kernel(const QParams
     QRec &R = recs[wv][pp];
     const uint32_t b = f - R.start;
     uint32_t c5[5] = {0u, 0u, 0u, 0u, 0u};
-    uint32_t h4[4] = {0u, 0u, 0u, 0u}, t4[4] = {0u, 0u, 0u, 0u};
-    bool mh = false;
-    uint64_t jaddr = 0;
     if (f < T && b < R.nblk) {  // (b == nblk: an odd packet's padding block)
       const QuicKeyDev &KB = MULTI ? Q.keys[R.kid] : Q.key0;
-      // junctions: both neighbours in this step and in this packet, and the
-      // block whole inside the packet's output (a packet's last block may
-      // end inside it: the tag or another packet's bytes follow)
-      const uint32_t oa = (uint32_t)(R.dst & 15);
-      const uint32_t rem = R.pl - 64 * b, rem1 = rem > 64 ? rem - 64 : 0u;
-      mh = b > 0 && lane > 0 && oa + (rem < 64 ? rem : 64u) >= 16;
-      const bool gt = b + 1 < R.nblk && lane + 1 < kWave &&
-                      oa + (rem1 < 64 ? rem1 : 64u) >= 16;
-      jaddr = R.dst + 64ull * b - oa;
-      uint32_t blk[5][4];
-      coop_load(R, b, blk);
-      coop_block<OPEN, OB>(KB, R, b, blk, c5, mh, gt, h4, t4);
-    }
-    {  // the junction: this lane's head bytes | the previous lane's tail bytes
-      uint32_t pt[4];
-#pragma unroll
-      for (int w = 0; w < 4; w++) pt[w] = __shfl_up(t4[w], 1, kWave);
-      if (mh) gst<u32x4>(jaddr, u32x4{h4[0] | pt[0], h4[1] | pt[1], h4[2] | pt[2], h4[3] | pt[3]});
+      coop_full<OPEN, OB>(KB, R, b, c5);
     }
     // the odd neighbour's partial (the same packet: pairs start even)
     uint32_t n5[5];
@@ -736,8 +689,8 @@ __global__ __launch_bounds__(kQBlock, kQMinWaves) void quic_kernel(const QParams
     for (int i = 0; i < 5; i++) n5[i] = __shfl_down(c5[i], 1, kWave);
     if (!(lane & 1) && f < T) {
       if (b + 1 < R.nblk) {
-        // P_b r^k + P_b+1, k = 4, or klast for the packet's last block
-        const uint32_t *m = b + 2 == R.nblk ? R.rl : R.r4;
+        // P_b r^4 + P_b+1
+        const uint32_t *m = R.r4;
         Poly X;
         X.r0 = m[0]; X.r1 = m[1]; X.r2 = m[2]; X.r3 = m[3]; X.r4 = m[4];
         X.s1 = X.r1 * 5; X.s2 = X.r2 * 5; X.s3 = X.r3 * 5; X.s4 = X.r4 * 5;
@@ -756,13 +709,16 @@ __global__ __launch_bounds__(kQBlock, kQMinWaves) void quic_kernel(const QParams
   // pairs: every lane stays for the mask block)
   const bool fin = owner && live;
   if (owner && !live) Q.out_len[p] = status;
+  // the payload's tail keystream (block nblk + 1; every lane: lane pairs)
+  uint32_t tks[16];
+  ks_lanes<MULTI>(K, 1 + nblk, nonce, lane, tks);
   if (OPEN && !fin) return;
   uint32_t ct32[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
   uint32_t tag[4] = {0u, 0u, 0u, 0u}, sample[4] = {0u, 0u, 0u, 0u};
   if (fin) {
     if (coop) {
-      // pairs: h = h r^c + E_j, c = 8 chunks for a whole pair, r^klast for a
-      // last pair of one block, r^(4 + klast) for one of two
+      // pairs: h = h r^c + E_j, c = 8 chunks for a whole pair, 4 for a
+      // last pair of one block
       const QRec &Rq = recs[wv][lane];
       Poly R1;
       R1.r0 = P.r0; R1.r1 = P.r1; R1.r2 = P.r2; R1.r3 = P.r3; R1.r4 = P.r4;
@@ -770,15 +726,12 @@ __global__ __launch_bounds__(kQBlock, kQMinWaves) void quic_kernel(const QParams
       Poly X;
       X.r0 = Rq.r4[0]; X.r1 = Rq.r4[1]; X.r2 = Rq.r4[2]; X.r3 = Rq.r4[3]; X.r4 = Rq.r4[4];
       X.s1 = X.r1 * 5; X.s2 = X.r2 * 5; X.s3 = X.r3 * 5; X.s4 = X.r4 * 5;
-      Poly Y = X;
       X.h0 = X.r0; X.h1 = X.r1; X.h2 = X.r2; X.h3 = X.r3; X.h4 = X.r4;
       poly_mul(X);  // r^8
-      Y.h0 = Rq.rl[0]; Y.h1 = Rq.rl[1]; Y.h2 = Rq.rl[2]; Y.h3 = Rq.rl[3]; Y.h4 = Rq.rl[4];
-      poly_mul(Y);  // r^(4 + klast)
       const bool one = nblk & 1;  // the last pair holds one block
-      const uint32_t M0 = one ? Rq.rl[0] : Y.h0, M1 = one ? Rq.rl[1] : Y.h1,
-                     M2 = one ? Rq.rl[2] : Y.h2, M3 = one ? Rq.rl[3] : Y.h3,
-                     M4 = one ? Rq.rl[4] : Y.h4;
+      const uint32_t M0 = one ? Rq.r4[0] : X.h0, M1 = one ? Rq.r4[1] : X.h1,
+                     M2 = one ? Rq.r4[2] : X.h2, M3 = one ? Rq.r4[3] : X.h3,
+                     M4 = one ? Rq.r4[4] : X.h4;
       const uint32_t npair = nflat / 2;
       for (uint32_t j = 0; j < npair; j++) {
         const bool lastp = j + 1 == npair;
@@ -792,11 +745,40 @@ __global__ __launch_bounds__(kQBlock, kQMinWaves) void quic_kernel(const QParams
         const uint32_t *c5 = parts[wv][start / 2 + j];
         P.h0 += c5[0]; P.h1 += c5[1]; P.h2 += c5[2]; P.h3 += c5[3]; P.h4 += c5[4];
       }
-      // restore r for the lengths block
+      // restore r for the tail and the lengths block
       P.r0 = R1.r0; P.r1 = R1.r1; P.r2 = R1.r2; P.r3 = R1.r3; P.r4 = R1.r4;
       P.s1 = R1.s1; P.s2 = R1.s2; P.s3 = R1.s3; P.s4 = R1.s4;
 #pragma unroll
       for (int i = 0; i < 8; i++) ct32[i] = Rq.ct32[i];
+      // the tail: pl % 64 bytes after the full blocks, byte-exact, chunk by
+      // chunk (the MAC pads the last chunk with zeros, RFC 8439 2.8)
+      const uint32_t tail = pl - 64 * nblk;
+      const uint64_t ts = src + hdr + 64ull * nblk, td = dst + hdr + 64ull * nblk;
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {
+        if (16 * q < tail) {
+          const uint32_t nb = tail - 16 * q < 16 ? tail - 16 * q : 16u;
+          uint32_t x[4], c[4], kw[4];
+          load16(ts + 16 * q, ts + tail, x);
+#pragma unroll
+          for (int w = 0; w < 4; w++) {
+            const uint32_t m = range_mask(0, (int)nb, w);
+            kw[w] = OB ? Rq.okr[4 * (q & 1) + w] & m : 0u;
+            if (OB && OPEN) x[w] ^= kw[w];
+            c[w] = (x[w] ^ tks[4 * q + w]) & m;
+          }
+          if (OPEN) poly_block(P, x);
+          else poly_block(P, c);
+          if (!OPEN && nblk == 0 && q < 2) {
+#pragma unroll
+            for (int w = 0; w < 4; w++) ct32[4 * q + w] = c[w];
+          }
+          uint32_t o[4];
+#pragma unroll
+          for (int w = 0; w < 4; w++) o[w] = (OB && !OPEN) ? c[w] ^ kw[w] : c[w];
+          store16(td + 16 * q, o, nb);
+        }
+      }
     } else {
       uint32_t okr[8];
 #pragma unroll
