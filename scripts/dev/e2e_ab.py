@@ -20,7 +20,7 @@ for path in sys.argv[3:]:
     sqobfs._lib = sqobfs.load(path)
     ctx = sqobfs.Context(0)
     kr = sqobfs.Keyring(ctx, sqobfs.SALAMANDER, [bench.PSK])
-    libs.append((os.path.basename(path), sqobfs._lib, ctx, kr))
+    libs.append((os.path.basename(os.path.dirname(path)) or os.path.basename(path), sqobfs._lib, ctx, kr))
 res = {}
 for r in range(rounds):
     for name, lib, ctx, kr in libs:

@@ -40,7 +40,7 @@ struct sqobfs_ctx {
   size_t pinned_cap = 0;
   uint8_t *dev = nullptr;
   size_t dev_cap = 0;
-  hipEvent_t ev[32] = {};  // pipeline events of sqobfs_run_host (kEvents)
+  hipEvent_t ev[64] = {};  // pipeline events of sqobfs_run_host (kEvents)
   // SQOBFS_FLAG_DEVICE_SALT: ChaCha20 key and the next launch sequence number
   uint32_t salt_key[8] = {};
   std::atomic<uint64_t> salt_seq{0};
@@ -100,8 +100,11 @@ void tab_free(void *p) {
 }
 // live sqobfs_host_alloc blocks (sqobfs_debug_host_allocs: leak checks)
 std::atomic<int64_t> g_host_allocs{0};
-constexpr uint32_t kEvents = 32;
+constexpr uint32_t kEvents = 64;
 static_assert(sizeof(((sqobfs_ctx *)nullptr)->ev) / sizeof(hipEvent_t) == kEvents, "event ring");
+// three events per pipeline piece (copy-in, kernel, copy-out), none reused
+// within a call: at most 2 kHostChunks - 1 + 3 pieces
+static_assert(3 * (2 * kHostChunks + 2) <= kEvents, "run_host pieces");
 }
 
 // The streams a keyring's table was read on.  Destroying the keyring records
@@ -495,13 +498,28 @@ struct Range {
   uint32_t p0, p1;   // packets of the chunk
 };
 
+// What run_host's slot packing (slot_pack) needs to know of a batch,
+// gathered in packet_spans' pass: whether packet i sits at in_off[0] + i si
+// and out_off[0] + i so, and the widest input and output.
+struct SlotScan {
+  bool strided = false;   // (set by the caller when the layout may be strided)
+  size_t si = 0, so = 0;  // candidate strides
+  size_t wi = 0, wo = 0;  // widest input (with XPlus in_cap) and output
+};
+
 // The input and output byte ranges packets [p0, p1) of hb touch (empty
-// ranges are {0, 0}), per the output-length rules of include/sqobfs.h.
+// ranges are {0, 0}), per the output-length rules of include/sqobfs.h; with
+// a scan, its stride check and widths over the same packets (one pass: at
+// 256K packets each pass over the descriptors costs ~0.1 ms before the
+// pipeline's first copy).
 void packet_spans(const sqobfs_batch *hb, int kind, int dir, uint32_t p0, uint32_t p1,
-                  Range &ri, Range &ro) {
+                  Range &ri, Range &ro, SlotScan *scan = nullptr) {
   const size_t S = salt_len(kind);
   ri = Range{SIZE_MAX, 0, p0, p1};
   ro = Range{SIZE_MAX, 0, p0, p1};
+  bool strided = scan && scan->strided;
+  size_t wi = 0, wo = 0;
+  const uint64_t i0 = scan ? hb->in_off[0] : 0, o0 = scan ? hb->out_off[0] : 0;
   for (uint32_t i = p0; i < p1; i++) {
     const size_t len = hb->in_len[i];
     size_t cap = len;
@@ -519,9 +537,19 @@ void packet_spans(const sqobfs_batch *hb, int kind, int dir, uint32_t p0, uint32
       ro.lo = std::min<size_t>(ro.lo, hb->out_off[i]);
       ro.hi = std::max<size_t>(ro.hi, hb->out_off[i] + osz);
     }
+    if (strided) {
+      strided = hb->in_off[i] == i0 + scan->si * i && hb->out_off[i] == o0 + scan->so * i;
+      wi = std::max(wi, cap);
+      wo = std::max(wo, osz);
+    }
   }
   if (ri.lo > ri.hi) ri.lo = ri.hi = 0;
   if (ro.lo > ro.hi) ro.lo = ro.hi = 0;
+  if (scan) {
+    scan->strided = strided;
+    scan->wi = std::max(scan->wi, wi);
+    scan->wo = std::max(scan->wo, wo);
+  }
 }
 
 // byte range ra of buffer a and rb of buffer b overlap
@@ -563,7 +591,12 @@ void par_memcpy(void *dst, const void *src, size_t n) {
   std::vector<std::thread> th;
   for (unsigned t = 0; t < nt; t++) {
     const size_t lo = n * t / nt, hi = n * (t + 1) / nt;
-    th.emplace_back([=] { memcpy((uint8_t *)dst + lo, (const uint8_t *)src + lo, hi - lo); });
+    auto part = [=] { memcpy((uint8_t *)dst + lo, (const uint8_t *)src + lo, hi - lo); };
+    try {
+      th.emplace_back(part);
+    } catch (...) {  // (no thread: that part on this one)
+      part();
+    }
   }
   for (auto &x : th) x.join();
 }
@@ -586,29 +619,26 @@ struct SlotPack {
   size_t pi = 0, po = 0;    // staged pitches
 };
 
-SlotPack slot_pack(const sqobfs_batch *hb, int kind, int dir, size_t in_lo, size_t in_hi,
-                   size_t out_lo, size_t out_hi, bool pinned) {
+// A scan candidate: a batch run_host may pack (page-locked buffers, at
+// least 64 packets, host salts, increasing first offsets).
+SlotScan slot_scan_start(const sqobfs_batch *hb, bool pinned) {
+  SlotScan sc;
+  if (!pinned || hb->n < 64 || (hb->flags & SQOBFS_FLAG_DEVICE_SALT)) return sc;
+  if (hb->in_off[1] <= hb->in_off[0] || hb->out_off[1] <= hb->out_off[0]) return sc;
+  sc.strided = true;
+  sc.si = hb->in_off[1] - hb->in_off[0];
+  sc.so = hb->out_off[1] - hb->out_off[0];
+  return sc;
+}
+
+SlotPack slot_pack(const sqobfs_batch *hb, const SlotScan &sc, size_t in_lo, size_t in_hi,
+                   size_t out_lo, size_t out_hi) {
   SlotPack sp;
-  const uint32_t n = hb->n;
-  if (!pinned || n < 64 || (hb->flags & SQOBFS_FLAG_DEVICE_SALT)) return sp;
-  if (hb->in_off[1] <= hb->in_off[0] || hb->out_off[1] <= hb->out_off[0]) return sp;
-  sp.si = hb->in_off[1] - hb->in_off[0];
-  sp.so = hb->out_off[1] - hb->out_off[0];
-  const size_t S = salt_len(kind);
-  for (uint32_t i = 0; i < n; i++) {
-    if (hb->in_off[i] != hb->in_off[0] + sp.si * i || hb->out_off[i] != hb->out_off[0] + sp.so * i)
-      return sp;
-    const size_t len = hb->in_len[i];
-    size_t cap = len;
-    if (kind == SQOBFS_XPLUS && dir == SQOBFS_DEOBFUSCATE && hb->in_cap)
-      cap = std::max<size_t>(len, hb->in_cap[i]);
-    size_t osz;
-    if (dir == SQOBFS_OBFUSCATE) osz = S + len;
-    else if (kind == SQOBFS_SALAMANDER) osz = len <= S ? len : len - S;
-    else osz = len < S ? 0 : cap - S;
-    sp.wi = std::max(sp.wi, cap);
-    sp.wo = std::max(sp.wo, osz);
-  }
+  if (!sc.strided) return sp;
+  sp.si = sc.si;
+  sp.so = sc.so;
+  sp.wi = sc.wi;
+  sp.wo = sc.wo;
   const bool lines = hb->flags & SQOBFS_FLAG_OUT_LINES;
   const bool blocks = lines || (hb->flags & SQOBFS_FLAG_OUT_BLOCKS);
   const size_t oa = lines ? 128 : 16;
@@ -1424,8 +1454,6 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
   const uint32_t n = hb->n;
   const int kind = kr->kind;
   const size_t S = salt_len(kind);
-  // ---- pass over the descriptors: psk ids, and per chunk of packets the
-  // input / output byte ranges it touches
   if (hb->psk_id)
     for (uint32_t i = 0; i < n; i++)
       if (hb->psk_id[i] >= kr->count) return SQ_EPSK;
@@ -1437,18 +1465,34 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
   const bool in_pinned = is_pinned(hb->in), out_pinned = is_pinned(hb->out);
   const uint32_t maxc = in_pinned && out_pinned ? 2 * kHostChunks : kHostChunks;
   const uint32_t nchunk = n < 4096 ? 1u : std::min<uint32_t>(maxc, (n + 4095) / 4096);
-  std::vector<Range> rin(nchunk), rout(nchunk);
-  for (uint32_t c = 0; c < nchunk; c++) {
-    const uint32_t p0 = (uint32_t)((uint64_t)n * c / nchunk);
-    const uint32_t p1 = (uint32_t)((uint64_t)n * (c + 1) / nchunk);
-    packet_spans(hb, kind, dir, p0, p1, rin[c], rout[c]);
+  // Pieces of the pipeline: nchunk equal chunks; from 4 chunks on, the last
+  // one is cut into 1/2, 1/4 and 1/4, so the drain -- the last piece's kernel
+  // and copy-out, with nothing left to copy in -- moves a quarter chunk
+  // ("Where the e2e time goes")
+  std::vector<uint32_t> cut{0};
+  if (nchunk < 4) {
+    for (uint32_t c = 1; c <= nchunk; c++) cut.push_back((uint32_t)((uint64_t)n * c / nchunk));
+  } else {
+    const uint64_t W = 4ull * nchunk;
+    uint64_t acc = 0;
+    for (uint32_t c = 0; c + 1 < nchunk; c++) cut.push_back((uint32_t)(n * (acc += 4) / W));
+    for (const uint32_t w : {2u, 1u, 1u}) cut.push_back((uint32_t)(n * (acc += w) / W));
   }
-  // Chunks run concurrently: if one chunk's output bytes overlap another
-  // chunk's input or output bytes (in-place or interleaved layouts), run
-  // the batch as a single chunk instead.
+  const uint32_t npiece = (uint32_t)cut.size() - 1;
+  // ---- one pass over the descriptors: per piece the input / output byte
+  // ranges it touches, and what slot packing needs to know
+  std::vector<Range> rin(npiece), rout(npiece);
+  // (one thread: spreading the pass over 8 threads measured 1-4 % slower
+  // end to end at 256K packets)
+  SlotScan scan = slot_scan_start(hb, in_pinned && out_pinned);
+  for (uint32_t c = 0; c < npiece; c++)
+    packet_spans(hb, kind, dir, cut[c], cut[c + 1], rin[c], rout[c], &scan);
+  // Pieces run concurrently: if one piece's output bytes overlap another
+  // piece's input or output bytes (in-place or interleaved layouts), run
+  // the batch as a single piece instead.
   if (parts_clash(hb, rin, rout)) {
     Range ri{SIZE_MAX, 0, 0, n}, ro{SIZE_MAX, 0, 0, n};
-    for (uint32_t c = 0; c < nchunk; c++) {
+    for (uint32_t c = 0; c < npiece; c++) {
       if (rin[c].hi > rin[c].lo) ri.lo = std::min(ri.lo, rin[c].lo), ri.hi = std::max(ri.hi, rin[c].hi);
       if (rout[c].hi > rout[c].lo) ro.lo = std::min(ro.lo, rout[c].lo), ro.hi = std::max(ro.hi, rout[c].hi);
     }
@@ -1468,6 +1512,8 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
   if (in_lo > in_hi) in_lo = in_hi = 0;
   if (out_lo > out_hi) out_lo = out_hi = 0;
   const bool preserve = !(hb->flags & SQOBFS_FLAG_OUT_UNINIT);
+  const bool dev_salt = hb->flags & SQOBFS_FLAG_DEVICE_SALT;
+  const bool host_salt = dir == SQOBFS_OBFUSCATE && !dev_salt;
 
   // staging layout (device mirror of the host ranges; pinned copies only
   // for what is pageable)
@@ -1479,24 +1525,49 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
   const size_t A = 256;
   const bool lines = hb->flags & SQOBFS_FLAG_OUT_LINES;
   // fixed-stride slots: packed rows instead of the spans (slot_pack)
-  const SlotPack sp = nrun == nchunk ? slot_pack(hb, kind, dir, in_lo, in_hi, out_lo, out_hi,
-                                                 in_pinned && out_pinned)
+  const SlotPack sp = nrun == npiece ? slot_pack(hb, scan, in_lo, in_hi, out_lo, out_hi)
                                      : SlotPack{};
   size_t o = 0;
   const size_t o_in = sp.on ? 0 : o + (((uintptr_t)hb->in + in_lo) & 15);
   o = align_up(sp.on ? sp.pi * n : o_in + (in_hi - in_lo), A);
   const size_t o_out = sp.on ? o : o + (((uintptr_t)hb->out + out_lo) & (lines ? 127 : 15));
   o = align_up(sp.on ? o_out + sp.po * n : o_out + (out_hi - out_lo) + (lines ? 128 : 0), A);
-  const size_t o_inoff = o;    o = align_up(o + 8ull * n, A);
-  const size_t o_inlen = o;    o = align_up(o + 4ull * n, A);
-  const size_t o_outoff = o;   o = align_up(o + 8ull * n, A);
+  // The descriptors the kernels read, in two groups, each one block of
+  // arrays and one copy: the first piece's (staged and copied before any
+  // payload moves) and the rest's (staged while the first piece's payload
+  // is on the link).  Staging all of them first held the pipeline's first
+  // copy back by ~0.4 ms at 256K packets.
+  struct DescGroup {
+    uint32_t p0, p1;
+    size_t base, inlen, outoff, salt, pid, cap, end;  // in_off at base
+  };
+  auto group_at = [&](uint32_t p0, uint32_t p1, size_t at) {
+    DescGroup g;
+    const size_t m = p1 - p0;
+    g.p0 = p0;
+    g.p1 = p1;
+    g.base = at;
+    size_t x = at + 8 * m;
+    g.inlen = x = align_up(x, 16);
+    x += 4 * m;
+    g.outoff = x = align_up(x, 16);
+    x += 8 * m;
+    g.salt = x = align_up(x, 16);
+    x += host_salt ? S * m : 0;
+    g.pid = x = align_up(x, 16);
+    x += hb->psk_id ? 2 * m : 0;
+    g.cap = x = align_up(x, 16);
+    x += hb->in_cap ? 4 * m : 0;
+    g.end = x;
+    return g;
+  };
+  DescGroup grp[2];
+  grp[0] = group_at(rin[0].p0, rin[0].p1, o);
+  o = align_up(grp[0].end, A);
+  grp[1] = group_at(nrun > 1 ? rin[1].p0 : n, n, o);
+  o = align_up(grp[1].end, A);
   const size_t o_outlen = o;   o = align_up(o + 4ull * n, A);
-  const bool dev_salt = hb->flags & SQOBFS_FLAG_DEVICE_SALT;
   const size_t o_saltout = o;  o = align_up(o + (dev_salt && hb->salt_out ? S * n : 0), A);
-  const size_t o_salt = o;
-  o = align_up(o + (dir == SQOBFS_OBFUSCATE && !dev_salt ? S * n : 0), A);
-  const size_t o_pid = o;      o = align_up(o + (hb->psk_id ? 2ull * n : 0), A);
-  const size_t o_cap = o;      o = align_up(o + (hb->in_cap ? 4ull * n : 0), A);
   const size_t total = o;
 
   std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1539,32 +1610,50 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
     if (st_ != SQ_OK) return drain(st_);                   \
   } while (0)
 
-  // descriptors: small, copied once up front
-  if (sp.on) {  // packed rows: packet i's bytes at row i, phase kept
-    uint64_t *io = (uint64_t *)(H + o_inoff), *oo = (uint64_t *)(H + o_outoff);
-    for (uint32_t i = 0; i < n; i++) {
-      io[i] = sp.pi * i + sp.phi;
-      oo[i] = sp.po * i + sp.pho;
+  // a descriptor group: staged, then one copy on the copy-in stream
+  auto stage_group = [&](const DescGroup &g) {
+    const size_t m = g.p1 - g.p0;
+    if (m == 0) return hipSuccess;
+    if (sp.on) {  // packed rows: packet i's bytes at row i, phase kept
+      uint64_t *io = (uint64_t *)(H + g.base), *oo = (uint64_t *)(H + g.outoff);
+      for (uint32_t i = g.p0; i < g.p1; i++) {
+        io[i - g.p0] = sp.pi * i + sp.phi;
+        oo[i - g.p0] = sp.po * i + sp.pho;
+      }
+    } else {
+      memcpy(H + g.base, hb->in_off + g.p0, 8 * m);
+      memcpy(H + g.outoff, hb->out_off + g.p0, 8 * m);
     }
-  } else {
-    memcpy(H + o_inoff, hb->in_off, 8ull * n);
-    memcpy(H + o_outoff, hb->out_off, 8ull * n);
-  }
-  memcpy(H + o_inlen, hb->in_len, 4ull * n);
-  if (dir == SQOBFS_OBFUSCATE && !dev_salt) memcpy(H + o_salt, hb->salt, S * n);
-  if (hb->psk_id) memcpy(H + o_pid, hb->psk_id, 2ull * n);
-  if (hb->in_cap) memcpy(H + o_cap, hb->in_cap, 4ull * n);
-  SQ_TRY_DRAIN(hipMemcpyAsync(D + o_inoff, H + o_inoff, o_outlen - o_inoff, hipMemcpyHostToDevice,
-                        ctx->h2d));
-  SQ_TRY_DRAIN(hipMemcpyAsync(D + o_salt, H + o_salt, total - o_salt, hipMemcpyHostToDevice,
-                        ctx->h2d));
+    memcpy(H + g.inlen, hb->in_len + g.p0, 4 * m);
+    if (host_salt) memcpy(H + g.salt, hb->salt + S * g.p0, S * m);
+    if (hb->psk_id) memcpy(H + g.pid, hb->psk_id + g.p0, 2 * m);
+    if (hb->in_cap) memcpy(H + g.cap, hb->in_cap + g.p0, 4 * m);
+    return hipMemcpyAsync(D + g.base, H + g.base, g.end - g.base, hipMemcpyHostToDevice, ctx->h2d);
+  };
+  // a landed piece's results to the caller: out_len (and salt_out) from
+  // staging, and pageable output bytes; run while later pieces still move
+  auto finish = [&](uint32_t c) {
+    const uint32_t p0 = rin[c].p0, m = rin[c].p1 - rin[c].p0;
+    memcpy(hb->out_len + p0, H + o_outlen + 4ull * p0, 4ull * m);
+    if (dev_salt && hb->salt_out) memcpy(hb->salt_out + S * p0, H + o_saltout + S * p0, S * m);
+    if (!out_pinned && rout[c].hi > rout[c].lo)
+      par_memcpy(hb->out + rout[c].lo, hout(rout[c].lo), rout[c].hi - rout[c].lo);
+  };
 
+  // pageable output is copied out piece by piece while later pieces move;
+  // with page-locked output only out_len (and salt_out) remain, one copy at
+  // the end (per-piece copies and waits cost more than they overlap)
+  const bool per_piece = !out_pinned && nrun > 1;
   // ---- pipeline: H2D(c) on h2d | kernel(c) on the compute stream | D2H(c)
-  // on d2h, chained by events; chunk c+1's copy-in overlaps chunk c's
-  // kernel and chunk c-1's copy-out.
+  // on d2h, chained by events; piece c+1's copy-in overlaps piece c's
+  // kernel and piece c-1's copy-out, and the host finishes each landed
+  // piece while the later ones move.
+  SQ_TRY_DRAIN(stage_group(grp[0]));
+  uint32_t fin = 0;  // pieces finished on the host
   for (uint32_t c = 0; c < nrun; c++) {
     const Range &ri = rin[c], &ro = rout[c];
     const uint32_t rows = ri.p1 - ri.p0;
+    if (c == 1) SQ_TRY_DRAIN(stage_group(grp[1]));
     if (sp.on) {  // rows [p0, p1): the first wi / wo bytes of each slot
       if (sp.wi && rows)
         SQ_TRY_DRAIN(hipMemcpy2DAsync(D + o_in + sp.pi * ri.p0 + sp.phi, sp.pi,
@@ -1592,21 +1681,23 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
       SQ_TRY_DRAIN(hipMemcpyAsync(dout(ro.lo), src, ro.hi - ro.lo, hipMemcpyHostToDevice,
                                   ctx->h2d));
     }
-    hipEvent_t ev_in = ctx->ev[(2 * c) % kEvents], ev_k = ctx->ev[(2 * c + 1) % kEvents];
+    hipEvent_t ev_in = ctx->ev[3 * c], ev_k = ctx->ev[3 * c + 1], ev_out = ctx->ev[3 * c + 2];
     SQ_TRY_DRAIN(hipEventRecord(ev_in, ctx->h2d));
     SQ_TRY_DRAIN(hipStreamWaitEvent(ctx->stream, ev_in, 0));
+    const DescGroup &g = grp[c == 0 ? 0 : 1];
+    const size_t k = ri.p0 - g.p0;  // the piece's first packet within its group
     sqobfs_batch db = *hb;
-    db.n = ri.p1 - ri.p0;
+    db.n = rows;
     db.in = sp.on ? D + o_in : din(0);  // in_off[i] >= in_lo for every packet of the batch
-    db.in_off = (const uint64_t *)(D + o_inoff) + ri.p0;
-    db.in_len = (const uint32_t *)(D + o_inlen) + ri.p0;
+    db.in_off = (const uint64_t *)(D + g.base) + k;
+    db.in_len = (const uint32_t *)(D + g.inlen) + k;
     db.out = sp.on ? D + o_out : dout(0);
-    db.out_off = (const uint64_t *)(D + o_outoff) + ri.p0;
+    db.out_off = (const uint64_t *)(D + g.outoff) + k;
     db.out_len = (uint32_t *)(D + o_outlen) + ri.p0;
-    db.salt = dir == SQOBFS_OBFUSCATE && !dev_salt ? D + o_salt + S * ri.p0 : nullptr;
+    db.salt = host_salt ? D + g.salt + S * k : nullptr;
     db.salt_out = dev_salt && hb->salt_out ? D + o_saltout + S * ri.p0 : nullptr;
-    db.psk_id = hb->psk_id ? (const uint16_t *)(D + o_pid) + ri.p0 : nullptr;
-    db.in_cap = hb->in_cap ? (const uint32_t *)(D + o_cap) + ri.p0 : nullptr;
+    db.psk_id = hb->psk_id ? (const uint16_t *)(D + g.pid) + k : nullptr;
+    db.in_cap = hb->in_cap ? (const uint32_t *)(D + g.cap) + k : nullptr;
     if (db.n) {
       sq::KParams kp = make_params(ctx, kr, &db);
       if (kp.ppw == 0) {  // lengths are on the host: size the units by bytes
@@ -1632,14 +1723,39 @@ int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
       SQ_TRY_DRAIN(hipMemcpyAsync(dst, dout(ro.lo), ro.hi - ro.lo, hipMemcpyDeviceToHost,
                                   ctx->d2h));
     }
+    if (!per_piece) continue;
+    if (rows) {
+      SQ_TRY_DRAIN(hipMemcpyAsync(H + o_outlen + 4ull * ri.p0, D + o_outlen + 4ull * ri.p0,
+                                  4ull * rows, hipMemcpyDeviceToHost, ctx->d2h));
+      if (dev_salt && hb->salt_out)
+        SQ_TRY_DRAIN(hipMemcpyAsync(H + o_saltout + S * ri.p0, D + o_saltout + S * ri.p0,
+                                    S * rows, hipMemcpyDeviceToHost, ctx->d2h));
+    }
+    SQ_TRY_DRAIN(hipEventRecord(ev_out, ctx->d2h));
+    // finish the pieces that have landed meanwhile, in order
+    while (fin < c) {
+      const hipError_t q = hipEventQuery(ctx->ev[3 * fin + 2]);
+      if (q == hipErrorNotReady) {
+        (void)hipGetLastError();
+        break;
+      }
+      SQ_TRY_DRAIN(q);
+      finish(fin++);
+    }
+  }
+  if (per_piece) {
+    for (; fin < nrun; fin++) {
+      SQ_TRY_DRAIN(hipEventSynchronize(ctx->ev[3 * fin + 2]));
+      finish(fin);
+    }
+    SQ_TRY_DRAIN(hipStreamSynchronize(ctx->d2h));
+    return SQ_OK;
   }
   SQ_TRY_DRAIN(hipMemcpyAsync(H + o_outlen, D + o_outlen, 4ull * n, hipMemcpyDeviceToHost, ctx->d2h));
   if (dev_salt && hb->salt_out)
     SQ_TRY_DRAIN(hipMemcpyAsync(H + o_saltout, D + o_saltout, S * n, hipMemcpyDeviceToHost, ctx->d2h));
   SQ_TRY_DRAIN(hipStreamSynchronize(ctx->d2h));
-  // pageable output: copy back in chunk order (later chunks win where
-  // ranges interleave, matching the device order)
-  if (!out_pinned)
+  if (!out_pinned)  // (one piece)
     for (uint32_t c = 0; c < nrun; c++)
       if (rout[c].hi > rout[c].lo)
         par_memcpy(hb->out + rout[c].lo, hout(rout[c].lo), rout[c].hi - rout[c].lo);
