@@ -570,3 +570,63 @@ def test_host_failure_drains_pipeline(ctx, kind):
         sqobfs.debug_fail_chunk(-1)
         for k in keep:
             k.free()
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_pipeline_device_salts(ctx, kind, pinned):
+    """SQOBFS_FLAG_DEVICE_SALT through run_host's multi-piece pipeline (20,000
+    packets: 5 chunks, the last cut in three): every piece is a launch with
+    its own sequence number, salt_out comes back piece by piece (per landed
+    piece with pageable output, in one copy with page-locked output), and the
+    wire is the oracle's obfuscation with exactly those salts."""
+    S = sqobfs.SALT_LEN[kind]
+    rng = np.random.Generator(np.random.PCG64(610 + kind + 2 * pinned))
+    n = 20000
+    lens = rng.integers(0, 1500, n)
+    psks = [PSK, b"r" * 33]
+    ids = rng.integers(0, 2, n)
+    hb = gh.make_case(rng, kind, OBFUSCATE, lens, psks, psk_ids=ids, in_align=1, out_align=1)
+    hb.flags = sqobfs.FLAG_DEVICE_SALT
+    hb.salt_out = np.zeros(n * S, np.uint8)
+    keep = []
+    try:
+        if pinned:
+            _pin(ctx, hb, keep)
+        seq0 = ctx.salt_seq
+        with sqobfs.Keyring(ctx, kind, psks) as kr:
+            gh.run_host(ctx, kr, OBFUSCATE, hb)
+        assert ctx.salt_seq - seq0 == 7, "one sequence number per piece (5 chunks, last cut in 3)"
+        salts = hb.salt_out.reshape(n, S)
+        assert len({bytes(r) for r in salts}) == n, "salts repeat across pieces"
+        ref_in = gh.clone(hb)
+        ref_in.flags = 0
+        ref_in.salt = hb.salt_out.copy()
+        ref = gh.run_oracle(kind, OBFUSCATE, psks, ref_in)
+        gh.assert_same(hb, ref, f"run_host device salts pinned={pinned}")
+    finally:
+        for k in keep:
+            k.free()
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_host_failure_pageable_pieces(ctx, kind):
+    """A failure injected at piece 4 of a pageable batch (its landed pieces
+    are copied out while later ones move): the error comes back, out_len of
+    the failed batch is not trusted, and the context reruns the batch
+    correctly."""
+    rng = np.random.Generator(np.random.PCG64(620 + kind))
+    n = 20000
+    lens = rng.integers(0, 1500, n)
+    hb = gh.make_case(rng, kind, OBFUSCATE, lens, [PSK])
+    ref = gh.run_oracle(kind, OBFUSCATE, [PSK], hb)
+    try:
+        with sqobfs.Keyring(ctx, kind, [PSK]) as kr:
+            sqobfs.debug_fail_chunk(4)
+            with pytest.raises(sqobfs.SqError) as ei:
+                gh.run_host(ctx, kr, OBFUSCATE, hb)
+            assert ei.value.status == sqobfs.SQ_EDEVICE
+            gh.run_host(ctx, kr, OBFUSCATE, hb)
+        gh.assert_same(hb, ref, "after an injected failure (pageable pieces)")
+    finally:
+        sqobfs.debug_fail_chunk(-1)
