@@ -470,7 +470,7 @@ def load_traffic(config: str, kernel_bytes: float):
     """HBM bytes per launch from the committed PMC pass (the latest round's
     profiles/rNN/pmc_<config>.json)."""
     path = None
-    for rnd in ("r05", "r04", "r03", "r02"):
+    for rnd in ("r06", "r05", "r04", "r03", "r02"):
         p = os.path.join(REPO, "profiles", rnd, f"pmc_{config}.json")
         if os.path.exists(p):
             path = p

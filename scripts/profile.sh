@@ -6,7 +6,7 @@ cd $GRAFT_REPO_ROOT
 O=gpurun_out/$1; shift
 mkdir -p $O
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o kt -- \
-  python bench.py --steps 10 --warmup 2 --no-cpu-baseline "$@" > $O/kt.json 2> $O/kt.log \
+  python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e "$@" > $O/kt.json 2> $O/kt.log \
   || { echo "kernel trace failed"; tail -5 $O/kt.log; exit 1; }
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" \
@@ -15,7 +15,7 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
            "GRBM_GUI_ACTIVE GRBM_COUNT"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $O/p$i -o p -- \
-    python bench.py --steps 5 --warmup 1 --warmup-s 0 --no-cpu-baseline "$@" > $O/p$i.log 2>&1 \
+    python bench.py --steps 5 --warmup 1 --warmup-s 0 --no-cpu-baseline --no-e2e "$@" > $O/p$i.log 2>&1 \
     || { echo "pass $i ($grp) failed"; tail -5 $O/p$i.log; exit 1; }
 done
 python scripts/pmc_summary.py $O
