@@ -39,6 +39,45 @@ SETS["shoup"] = {"e_sunroll": [("""#pragma unroll 1
     asm volatile("" : "+v"(w), "+v"(z0), "+v"(z1), "+v"(z2), "+v"(z3));
     const uint32_t w4 = w << 4;
     uint32_t z4 = 0;""")]}
+# round 6, late: more LDS lookups in flight at 3 waves per SIMD (the kernels
+# hold 140-167 VGPRs of the 170 that occupancy allows): the multiply by H
+# with its 8 lookups of a word issued together (4 groups, not 8), the Shoup
+# multiply by H^m likewise, and both (correct output)
+_POS4 = """    for (int h = 0; h < 8; h += 4) {
+      // (an empty asm the next reads' addresses depend on, after the last
+      // XORs: keeps the unrolled reads from being hoisted into 128 VGPRs)
+      asm volatile("" : "+v"(w), "+v"(z0), "+v"(z1), "+v"(z2), "+v"(z3));
+      const uint32_t w4 = w << 4;
+      u32x4 e[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int jj = h + j;
+        const uint32_t off = (((jj & 1) ? w : w4) >> (8 * (jj >> 1))) & 0xF0u;
+        const char *p = base + 256 * (8 * i + jj) + off;
+        e[j] = *(const u32x4 *)p;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j += 2) {"""
+_POS8 = _POS4.replace("h += 4", "h += 8").replace("u32x4 e[4];", "u32x4 e[8];").replace(
+    "j < 4; j++", "j < 8; j++").replace("j < 4; j += 2", "j < 8; j += 2")
+_SH4 = """    for (int h = 0; h < 8; h += 4) {  // (4 reads in flight: 8 made the kernels spill)
+      u32x4 e[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int jj = h + j;
+        const uint32_t off = ((((jj & 1) ? w : w4) >> (8 * (jj >> 1))) & 0xF0u) ^ sw16;
+        if (GLOBAL) e[j] = gld<u32x4>((uint64_t)(t + off));
+        else e[j] = *(const u32x4 *)(t + off);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) {"""
+_SH8 = _SH4.replace("h += 4", "h += 8").replace("u32x4 e[4];", "u32x4 e[8];").replace(
+    "j < 4; j++) {\n        const int jj", "j < 8; j++) {\n        const int jj").replace(
+    "#pragma unroll\n      for (int j = 0; j < 4; j++) {\n        if", "#pragma unroll\n      for (int j = 0; j < 8; j++) {\n        if")
+_SH8 = _SH8.replace("      for (int j = 0; j < 4; j++) {\n        const int jj", "      for (int j = 0; j < 8; j++) {\n        const int jj")
+_SH8 = _SH8[:_SH8.rindex("j < 4; j++) {")] + "j < 8; j++) {"
+SETS["ilp"] = {"base": [], "pos8": [(_POS4, _POS8)], "shoup8": [(_SH4, _SH8)],
+               "both8": [(_POS4, _POS8), (_SH4, _SH8)]}
 VARIANTS = SETS[sys.argv[1] if len(sys.argv) > 1 else "ablate"]
 if not os.environ.get("KEEP"):  # (KEEP=1: add to scripts/dev/ab_head.sh's builds)
     shutil.rmtree(os.path.join(REPO, "build", "ablate"), ignore_errors=True)
