@@ -265,14 +265,17 @@ int sqobfs_xplus_deobfuscate(sqobfs_ctx *ctx, const sqobfs_keyring *kr,
 int sqobfs_launch(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
                   const sqobfs_batch *b, void *stream);
 
-/* Host-memory batch, synchronous.  The batch is cut into up to 8 chunks of
- * packets whose copy-in (H2D), kernel and copy-out (D2H) run on three
- * streams and overlap.  Pinned caller buffers (sqobfs_host_alloc) are
- * copied by DMA directly; pageable ones go through pinned staging.  Output
+/* Host-memory batch, synchronous.  The batch is cut into pieces of
+ * consecutive packets (up to 8 chunks of >= 4,096 packets, 16 when both
+ * buffers are pinned; from 4 chunks on, the last chunk is cut in three)
+ * whose copy-in (H2D), kernel and copy-out (D2H) run on three streams and
+ * overlap.  Pinned caller buffers (sqobfs_host_alloc) are copied by DMA
+ * directly; pageable ones go through pinned staging, and a pageable
+ * output is copied out piece by piece while later pieces move.  Output
  * bytes outside the packets' output regions are preserved unless
  * flags has SQOBFS_FLAG_OUT_UNINIT.  With SQOBFS_FLAG_DEVICE_SALT every
- * chunk is one launch with its own sequence number (salts of chunk c =
- * keystream(seq_c) over the chunk's packets, in packet order). */
+ * piece is one launch with its own sequence number (salts of piece c =
+ * keystream(seq_c) over the piece's packets, in packet order). */
 int sqobfs_run_host(sqobfs_ctx *ctx, const sqobfs_keyring *kr, int dir,
                     const sqobfs_batch *host_batch);
 
