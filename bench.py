@@ -985,13 +985,20 @@ def e2e_all_ranks(torch, sqobfs, ctx, kr, kind, dist, tdev, world, n=1 << 18, L=
     aggregate_gib_s = the payload of every rank / the max-over-ranks wall
     time; per_rank = each rank's own rate.  Bounded (~0.4 GB per rank).
     One packet per rank is checked against the device path's contract (its
-    out_len); the bytes' parity is tests/test_gpu_*'s."""
+    out_len); the bytes' parity is tests/test_gpu_*'s.  A rank whose part
+    fails (e.g. page-locked memory refused) still joins every collective, so
+    no rank waits forever; the result then names the failed ranks instead of
+    an aggregate, and the bench line is printed as usual."""
     import numpy as np
     S = 8 if kind == 0 else 16
     rng = np.random.Generator(np.random.PCG64(11 + (dist.get_rank() if dist else 0)))
     nin, nout = n * slot(L), n * slot(L + S)
-    pd, po = sqobfs.PinnedArray(ctx, nin), sqobfs.PinnedArray(ctx, nout)
+    pins, err, ok, dt = [], None, False, 0.0
     try:
+        pd = sqobfs.PinnedArray(ctx, nin)
+        pins.append(pd)
+        po = sqobfs.PinnedArray(ctx, nout)
+        pins.append(po)
         pd.array[:] = np.frombuffer(rng.bytes(nin), np.uint8)
         in_off = np.arange(n, dtype=np.uint64) * slot(L)
         out_off = np.arange(n, dtype=np.uint64) * slot(L + S)
@@ -1002,33 +1009,44 @@ def e2e_all_ranks(torch, sqobfs, ctx, kr, kind, dist, tdev, world, n=1 << 18, L=
         b = hb.as_batch()
         sqobfs.run_host(ctx, kr, sqobfs.OBFUSCATE, b)  # (warm: staging buffers, clocks)
         ok = bool(hb.out_len[0] == L + S and hb.out_len[-1] == L + S)
-        if dist:
-            dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            sqobfs.run_host(ctx, kr, sqobfs.OBFUSCATE, b)
-        dt = time.perf_counter() - t0
-    finally:
-        pd.free()
-        po.free()
-    own = n * L * reps / dt / 2**30
+    except Exception as e:  # (reported below; this rank still joins the collectives)
+        err = f"{type(e).__name__}: {e}"
     if dist:
-        t = torch.tensor([own, dt, 1.0 if ok else 0.0], dtype=torch.float64, device=tdev)
+        dist.barrier()
+    if err is None:
+        try:
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                sqobfs.run_host(ctx, kr, sqobfs.OBFUSCATE, b)
+            dt = time.perf_counter() - t0
+        except Exception as e:
+            err = f"{type(e).__name__}: {e}"
+    for p in pins:
+        p.free()
+    own = n * L * reps / dt / 2**30 if err is None else 0.0
+    if dist:
+        t = torch.tensor([own, dt, 1.0 if ok else 0.0, 0.0 if err is None else 1.0],
+                         dtype=torch.float64, device=tdev)
         g = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(g, t)
         rates = [float(x[0]) for x in g]
         wall = max(float(x[1]) for x in g)
         ok = all(float(x[2]) > 0 for x in g)
+        failed = [r for r, x in enumerate(g) if float(x[3]) > 0]
     else:
-        rates, wall = [own], dt
-    return {"aggregate_gib_s": round(n * L * reps * world / wall / 2**30, 3),
-            "per_rank": [round(r, 3) for r in rates],
-            "wall_s": round(wall, 5), "packets_per_rank": n, "payload_bytes": L, "reps": reps,
-            "out_len_ok": ok,
-            "rule": "sum over ranks of n x L x reps / max-over-ranks wall; all ranks released "
-                    "by one barrier after the timed region (not part of `value`)",
-            "path": "sqobfs_run_host, page-locked caller slots, SQOBFS_FLAG_OUT_UNINIT, "
-                    "host salts"}
+        rates, wall, failed = [own], dt, ([0] if err else [])
+    res = {} if failed else {"aggregate_gib_s": round(n * L * reps * world / wall / 2**30, 3)}
+    res.update({"per_rank": [round(r, 3) for r in rates], "wall_s": round(wall, 5),
+           "packets_per_rank": n, "payload_bytes": L, "reps": reps, "out_len_ok": ok,
+           "rule": "sum over ranks of n x L x reps / max-over-ranks wall; all ranks released "
+                   "by one barrier after the timed region (not part of `value`)",
+           "path": "sqobfs_run_host, page-locked caller slots, SQOBFS_FLAG_OUT_UNINIT, "
+                   "host salts"})
+    if failed:
+        res["failed_ranks"] = failed
+        if err:
+            res["error"] = err  # (this rank's; rank 0 prints the line)
+    return res
 
 
 def e2e_rate(torch, sqobfs, ctx, kr, kind, n, L):

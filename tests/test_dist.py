@@ -95,3 +95,76 @@ def test_bench_bare_launch_refuses_more_ranks_than_gpus():
     assert r.returncode == 2, r.stderr[-2000:]
     assert "GPU(s) visible" in r.stderr
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+class _StubSqobfs:
+    """Just enough of the sqobfs binding for bench.e2e_all_ranks on the CPU:
+    page-locked arrays are numpy arrays (refused on `fail_rank`), run_host
+    writes the out_len the contract gives."""
+    OBFUSCATE = 0
+    FLAG_OUT_UNINIT = 1
+
+    def __init__(self, rank, fail_rank):
+        self.rank, self.fail_rank = rank, fail_rank
+
+    def PinnedArray(self, ctx, nbytes):  # noqa: N802 (the binding's name)
+        if self.rank == self.fail_rank:
+            raise MemoryError("page-locked allocation refused (stub)")
+
+        class _P:
+            array = np.zeros(nbytes, np.uint8)
+
+            def free(self):
+                pass
+        return _P()
+
+    def HostBatch(self, data, in_off, in_len, out, out_off, out_len, salt, flags=0):  # noqa: N802
+        class _H:
+            pass
+        h = _H()
+        h.in_len, h.out_len = in_len, out_len
+        h.as_batch = lambda: h
+        return h
+
+    def run_host(self, ctx, kr, direction, b):
+        import time
+        time.sleep(0.005)  # (a wall time the 5-decimal rounding of wall_s keeps)
+        b.out_len[:] = b.in_len + 8
+
+
+def _e2e_worker(rank, world, port, fail_rank, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    res = bench.e2e_all_ranks(torch, _StubSqobfs(rank, fail_rank), None, None, 0, dist,
+                              torch.device("cpu"), world, n=4096, reps=2)
+    if rank == 0:
+        q.put(res)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_rank", [-1, 1])
+def test_bench_e2e_leg_survives_a_failed_rank(fail_rank):
+    """bench.py's host-staged leg on 2 gloo ranks: when one rank's part fails
+    (its page-locked buffers refused), every rank still joins the barrier and
+    the gather -- nothing hangs -- and rank 0 reports the failed rank instead
+    of an aggregate; with no failure, the aggregate is both ranks' payload
+    over the max-over-ranks wall."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29621 + (fail_rank + 1)
+    procs = [ctx.Process(target=_e2e_worker, args=(r, 2, port, fail_rank, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert len(res["per_rank"]) == 2
+    if fail_rank < 0:
+        assert "failed_ranks" not in res and res["out_len_ok"]
+        payload = 2 * 4096 * 1350 * 2
+        assert abs(res["aggregate_gib_s"] - payload / res["wall_s"] / 2**30) <= 0.01 * res["aggregate_gib_s"]
+    else:
+        assert res["failed_ranks"] == [1] and "aggregate_gib_s" not in res
+        assert res["per_rank"][1] == 0.0 and not res["out_len_ok"]
