@@ -948,17 +948,25 @@ static void t_load(void) {
   /* 1. bursts of 64 with gaps: the CPU path */
   sqobfs_pconn_stats s0, s1, s2, s3;
   CHECK(sqobfs_pconn_stats_get(pc, &s0));
+  /* the break-even route moves with the measured CPU rate (a sanitizer
+   * build's CPU path is ~10x slower and jittery): the expectation below
+   * holds for the lowest route the phase saw */
+  uint64_t route = UINT64_MAX;
   for (int b = 0; b < 20; b++) {
+    CHECK(sqobfs_engine_info_get(g_ctx, &ei));
+    if (ei.route_bytes < route) route = ei.route_bytes;
     for (int j = 0; j < 64; j++, seq++) {
       load_payload(seq, pay);
       CHECK(sqobfs_pconn_write(pc, pay, 1350, &to, 0));
     }
+    CHECK(sqobfs_engine_info_get(g_ctx, &ei));
+    if (ei.route_bytes < route) route = ei.route_bytes;
     sleep_ms(3);
   }
   sleep_ms(20);
   CHECK(sqobfs_pconn_stats_get(pc, &s1));
   CHECK(sqobfs_engine_info_get(g_ctx, &ei));
-  const uint64_t route = ei.route_bytes;
+  if (ei.route_bytes < route) route = ei.route_bytes;
   EXPECT(s1.tx_datagrams - s0.tx_datagrams == 1280, "bursts: %llu of 1280 sent",
          (unsigned long long)(s1.tx_datagrams - s0.tx_datagrams));
   if (route >= 64ull * (1350 + 1024) && s1.tx_max_batch <= 64)  /* (no bursts merged) */
