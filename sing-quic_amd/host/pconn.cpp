@@ -124,8 +124,11 @@ constexpr uint32_t kMaxFlights = 32;
 // them together -- the natural batching of the GPU route
 constexpr uint32_t kDefFlightCap = 1;
 // datagrams waiting for the launch slot past which a bulk batch overflows to
-// the CPU path (gpu_saturated)
-constexpr uint32_t kDefPendMax = 2048;
+// the CPU path (gpu_saturated).  lat_bench hops 8 unpaced, in-process
+// against the CPU path: 8,192 / 4,096 / 2,048 waiting datagrams 0.7-1.2x its
+// rate, 256 1.09-1.20x in four runs on three boxes at less host CPU per GiB,
+// 128 0.9-1.27x
+constexpr uint32_t kDefPendMax = 256;
 
 // sqobfs_debug_engine_fail, sqobfs_debug_pool_fail, sqobfs_debug_engine_hold
 std::atomic<int> g_fail_count{0};
