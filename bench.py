@@ -1109,7 +1109,8 @@ def e2e_rate(torch, sqobfs, ctx, kr, kind, n, L):
                      "ms_per_batch": round(dt * 1e3, 3)}
     for p in pins:
         p.free()
-    res["path"] = ("sqobfs_run_host: 8-chunk H2D | kernel | D2H pipeline on 3 HIP streams; "
+    res["path"] = ("sqobfs_run_host: H2D | kernel | D2H pipeline on 3 HIP streams (8 chunks, 16 "
+                   "with page-locked buffers, the last cut in three); "
                    "fixed-stride page-locked slots staged as packed rows (2-D copies)")
     return res
 
